@@ -1,0 +1,214 @@
+"""bench.py -- committed entries/sec of the batched multi-group Raft step
+round on MI355X (BASELINE.json metric), plus %HBM roofline and the CPU
+oracle timed on the host cores.
+
+One step = one step round (drb_step_round) over every group on the GPU:
+proposals in, replication, quorum commit, ReadIndex, KV apply, messages
+out -- the dragonboat step loop for all replicas at once.
+
+Default workload = BASELINE.json configs[2]:
+1,048,576 active groups x 3 replicas per GPU, 16 B PBKV writes (k=1 per
+group per round) and a 9:1 ReadIndex:write mix batched into one ReadIndex
+ctx per group per round, one LocalTick per round.  Multi-GPU: groups are
+sharded over ranks (weak scaling, no data-path collective).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def alg_bytes_per_group_round(R=3, k=1, P=16, reads=True):
+    """SURVEY.md 8(d) algorithmic bytes for one group-round (co-resident)."""
+    e = 56 + ((P + 1 + 15) // 16) * 16          # entry record
+    b_round = 96 + 48 * R + 96 * (R - 1)        # leader core, remotes, flw
+    b_entries = k * e * (1 + 2 * (R - 1))       # leader write, flw r+w
+    b_apply = k * R * ((P + 1) + 2 * 16)        # Cmd read + slot r/w
+    b_read = (64 + 9 * 16) if reads else 0      # ctx push/confirm + lookups
+    return b_round + b_entries + b_apply + b_read
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--groups", type=int, default=1 << 20,
+                    help="groups per GPU")
+    ap.add_argument("--replicas", type=int, default=3)
+    ap.add_argument("--k", type=int, default=1, help="writes/group/round")
+    ap.add_argument("--no-read-index", action="store_true")
+    ap.add_argument("--tick-every", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, seconds):
+    """The CPU oracle (C restatement of the reference path) on the host:
+    a bounded sample of the same workload, groups split over threads."""
+    from dragonboat_amd import workload
+    from oracle import pyoracle as po
+    import ctypes as C
+    from dragonboat_amd.abi import RoundOut
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    G = 1000 * cores  # C1 scale per core
+    c = po.Cluster(G, args.replicas, logdb_keep=64)
+    c.setup_steady(0)
+    L = po.lib()
+    seed = 0x5EEDD8B0
+    parts = [(i * G // cores, (i + 1) * G // cores) for i in range(cores)]
+    committed = 0
+    rounds = 0
+    t_start = time.perf_counter()
+    t_run = 0.0
+    while time.perf_counter() - t_start < seconds:
+        counts, ents, pool = workload.build_batch(G, args.k, seed, rounds)
+        c.stage_proposals(counts, args.k, ents, pool)
+        if not args.no_read_index:
+            lo, hi = workload.build_read_index(G, seed, rounds, rounds + 30)
+            c.stage_read_index(lo, hi)
+        outs = [RoundOut() for _ in parts]
+        tick = int(args.tick_every > 0 and rounds % args.tick_every == 0)
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=L.orc_cluster_round_range,
+                               args=(c.p, tick, a, b, C.byref(o)))
+              for (a, b), o in zip(parts, outs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        L.orc_cluster_end_round(c.p)
+        t_run += time.perf_counter() - t0
+        committed += sum(o.committed_entries for o in outs)
+        rounds += 1
+    return dict(value=committed / t_run if t_run else 0.0,
+                unit="committed entries/s", cores=cores, kind="port",
+                sample="%d groups x %d replicas, %d rounds of the same "
+                       "workload (k=%d, %s, tick every %d), CPU "
+                       "restatement (oracle/), not dragonboat" % (
+                           G, args.replicas, rounds, args.k,
+                           "9:1 ReadIndex" if not args.no_read_index
+                           else "writes only", args.tick_every))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    from dragonboat_amd.engine import Engine
+    G, R, k = args.groups, args.replicas, args.k
+    reads = not args.no_read_index
+    NP = 8  # staged input batches (resident in HBM before timing)
+    eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                 max_props=max(1, k), prop_slots=NP, ri_slots=NP,
+                 mailbox=15, kv_slots=512, kv_val_cap=4,
+                 first_shard_id=1 + rank * G, device=local)
+    seed = 0x5EEDD8B0 ^ rank
+    eng.init_steady(term=2, leader_slot=0, seed=seed)
+    for b in range(NP):
+        eng.gen_kv_proposals(b, k, 256, 4, seed, b)
+        eng.gen_read_index(b, seed, b + 30)
+    stream = torch.cuda.ExternalStream(eng.stream)
+
+    def step(i):
+        tick = args.tick_every > 0 and i % args.tick_every == 0
+        eng.step_async(tick=tick, prop_slot=i % NP,
+                       ri_slot=(i % NP) if reads else 0xFFFFFFFF)
+
+    for i in range(args.warmup):
+        step(i)
+    eng.sync()
+    eng.read_counters(reset=True)
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.sync()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        step(args.warmup + i)
+        ev[i][1].record(stream)
+    eng.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    out = eng.read_counters(reset=True)
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
+    elapsed = t1 - t0
+    committed = out.committed_entries
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        c = torch.tensor([committed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(c)
+        committed = int(c.item())
+    value = committed / elapsed
+    alg = alg_bytes_per_group_round(R, k, 16, reads) * G
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    if out.fallbacks or out.errors:
+        print("WARNING: fallbacks=%d errors=%d" % (out.fallbacks, out.errors),
+              file=sys.stderr)
+    if rank == 0:
+        res = {
+            "metric": "committed entries/sec (node) at 1M active 3-replica "
+                      "groups, 16B payload; %HBM BW",
+            "value": value,
+            "unit": "committed entries/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (SURVEY 8d seeded PBKV writes + ReadIndex)",
+            "config": {
+                "workload": "C3: %d active groups x %d replicas per GPU, "
+                            "16B PBKV writes k=%d/group/round%s, tick every "
+                            "%d round(s)" % (
+                                G, R, k, ", 9:1 ReadIndex:write" if reads
+                                else "", args.tick_every),
+                "groups_per_gpu": G, "replicas": R,
+                "parallelism": "groups sharded, replicas co-resident"},
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "alg_bytes_per_launch": alg,
+                "kernel_ms": kern_ms},
+            "counters": {"committed_per_round": committed / K / world,
+                         "messages": out.messages,
+                         "ready_to_reads": out.ready_to_reads,
+                         "fallbacks": out.fallbacks, "errors": out.errors},
+        }
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+"""ctypes mirror of include/drb_engine.h (the C-ABI boundary).
+
+Plain data only: these Structures describe the records that cross the
+boundary (pb.Entry, pb.Message, per-replica raft state, round I/O).
+"""
+import ctypes as C
+
+DRB_MAX_REPLICAS = 8
+DRB_RI_DEPTH = 4
+DRB_NONE = 0xFFFFFFFF
+
+# status codes
+DRB_OK = 0
+DRB_EINVAL = -1
+DRB_EDEVICE = -2
+DRB_ENOMEM = -3
+DRB_ENOSYS = -4
+DRB_ERANGE = -5
+
+# raftpb.MessageType (raftpb/types.go:8-37)
+MSG = dict(
+    LocalTick=0, Election=1, LeaderHeartbeat=2, ConfigChangeEvent=3, NoOP=4,
+    Ping=5, Pong=6, Propose=7, SnapshotStatus=8, Unreachable=9,
+    CheckQuorum=10, BatchedReadIndex=11, Replicate=12, ReplicateResp=13,
+    RequestVote=14, RequestVoteResp=15, InstallSnapshot=16, Heartbeat=17,
+    HeartbeatResp=18, ReadIndex=19, ReadIndexResp=20, Quiesce=21,
+    SnapshotReceived=22, LeaderTransfer=23, TimeoutNow=24, RateLimit=25,
+    RequestPreVote=26, RequestPreVoteResp=27, LogQuery=28)
+MSG_NAME = {v: k for k, v in MSG.items()}
+
+# raftpb.EntryType
+ENTRY_APPLICATION = 0
+ENTRY_CONFIG_CHANGE = 1
+ENTRY_ENCODED = 2
+ENTRY_METADATA = 3
+
+# raft.State (internal/raft/raft.go:63-71)
+FOLLOWER, CANDIDATE, PREVOTE_CANDIDATE, LEADER, NONVOTING, WITNESS = range(6)
+
+# remoteStateType (internal/raft/remote.go:54-59)
+REMOTE_RETRY, REMOTE_WAIT, REMOTE_REPLICATE, REMOTE_SNAPSHOT = range(4)
+
+F_HOSTED = 1
+F_FALLBACK = 2
+F_ERROR = 4
+
+FB = dict(NONE=0, TERM_MISMATCH=1, MESSAGE_TYPE=2, ELECTION=3,
+          CHECK_QUORUM=4, ENTRY_TYPE=5, CAPACITY=6, ROLE=7, PROPOSAL=8,
+          ERR_LOG_RANGE=100, ERR_COMMIT=101, ERR_CONFLICT=102,
+          ERR_APPEND=103, ERR_APPLY=104, ERR_READINDEX=105)
+
+
+class RemoteState(C.Structure):
+    _fields_ = [("match", C.c_uint64), ("next", C.c_uint64),
+                ("state", C.c_uint32), ("active", C.c_uint32)]
+
+
+class ReadStatus(C.Structure):
+    _fields_ = [("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64),
+                ("index", C.c_uint64), ("from_", C.c_uint64),
+                ("confirmed", C.c_uint32), ("pad", C.c_uint32)]
+
+
+_REPLICA_U64 = [
+    "shard_id", "replica_id", "term", "vote", "leader_id", "applied",
+    "election_tick", "heartbeat_tick", "randomized_election_timeout",
+    "tick_count", "committed", "processed", "last_index", "marker_index",
+    "saved_to", "applied_to_index", "applied_to_term", "applied_index",
+    "confirmed_index", "pushed_index", "prev_term", "prev_vote",
+    "prev_commit", "sm_index", "sm_term", "kv_count"]
+
+
+class ReplicaState(C.Structure):
+    _fields_ = ([(n, C.c_uint64) for n in _REPLICA_U64] +
+                [("role", C.c_uint32), ("flags", C.c_uint32),
+                 ("fallback_reason", C.c_uint32), ("ri_count", C.c_uint32),
+                 ("remotes", RemoteState * DRB_MAX_REPLICAS),
+                 ("ri", ReadStatus * DRB_RI_DEPTH)])
+
+    def to_dict(self, num_replicas=None):
+        d = {n: getattr(self, n) for n in _REPLICA_U64}
+        for n in ("role", "flags", "fallback_reason", "ri_count"):
+            d[n] = getattr(self, n)
+        nr = num_replicas or DRB_MAX_REPLICAS
+        d["remotes"] = [(r.match, r.next, r.state, r.active)
+                        for r in list(self.remotes)[:nr]]
+        d["ri"] = [(x.ctx_low, x.ctx_high, x.index, x.from_, x.confirmed)
+                   for x in list(self.ri)[:self.ri_count]]
+        return d
+
+
+class Entry(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("index", C.c_uint64),
+                ("key", C.c_uint64), ("client_id", C.c_uint64),
+                ("series_id", C.c_uint64), ("responded_to", C.c_uint64),
+                ("type", C.c_uint32), ("cmd_len", C.c_uint32),
+                ("cmd_off", C.c_uint64)]
+
+
+class Message(C.Structure):
+    _fields_ = [("shard_id", C.c_uint64), ("from_", C.c_uint64),
+                ("to", C.c_uint64), ("term", C.c_uint64),
+                ("log_term", C.c_uint64), ("log_index", C.c_uint64),
+                ("commit", C.c_uint64), ("hint", C.c_uint64),
+                ("hint_high", C.c_uint64), ("type", C.c_uint32),
+                ("reject", C.c_uint32), ("n_entries", C.c_uint64),
+                ("entries_off", C.c_uint64)]
+
+
+class ReadyToRead(C.Structure):
+    _fields_ = [("shard_id", C.c_uint64), ("replica_id", C.c_uint64),
+                ("index", C.c_uint64), ("ctx_low", C.c_uint64),
+                ("ctx_high", C.c_uint64)]
+
+
+class Config(C.Structure):
+    _fields_ = [("num_groups", C.c_uint64), ("first_shard_id", C.c_uint64),
+                ("num_replicas", C.c_uint32), ("window", C.c_uint32),
+                ("cmd_cap", C.c_uint32), ("max_props", C.c_uint32),
+                ("prop_slots", C.c_uint32), ("ri_slots", C.c_uint32),
+                ("mailbox", C.c_uint32), ("kv_slots", C.c_uint32),
+                ("kv_val_cap", C.c_uint32), ("election_rtt", C.c_uint32),
+                ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
+                ("device", C.c_int32), ("reserved", C.c_uint32)]
+
+
+class RoundIn(C.Structure):
+    _fields_ = [("tick", C.c_uint32), ("prop_slot", C.c_uint32),
+                ("ri_slot", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class RoundOut(C.Structure):
+    _fields_ = [("round", C.c_uint64), ("committed_entries", C.c_uint64),
+                ("applied_entries", C.c_uint64), ("messages", C.c_uint64),
+                ("ready_to_reads", C.c_uint64),
+                ("dropped_read_indexes", C.c_uint64),
+                ("fallbacks", C.c_uint64), ("errors", C.c_uint64)]
+
+    def to_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+def message_to_tuple(m, ents, pool):
+    """Canonical comparable form of a pb.Message (+ its entries)."""
+    es = []
+    for i in range(m.n_entries):
+        e = ents[m.entries_off + i]
+        es.append(entry_to_tuple(e, pool))
+    return (m.shard_id, m.from_, m.to, m.type, m.term, m.log_term,
+            m.log_index, m.commit, m.reject, m.hint, m.hint_high, tuple(es))
+
+
+def entry_to_tuple(e, pool):
+    cmd = bytes(pool[e.cmd_off:e.cmd_off + e.cmd_len]) if e.cmd_len else b""
+    return (e.term, e.index, e.type, e.key, e.client_id, e.series_id,
+            e.responded_to, cmd)

@@ -1,0 +1,1152 @@
+// drb_engine.hip -- host side of the C ABI (include/drb_engine.h) and the
+// auxiliary device kernels (initialisation, input generation, state
+// movement, CRC32).  The step round itself is drb_step.hpp.
+//
+// Written for gfx950 (MI355X) only.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/drb_engine.h"
+#include "drb_layout.hpp"
+#include "drb_step.hpp"
+
+using namespace drb;
+
+#define HIPCHK(x)                                                        \
+  do {                                                                   \
+    hipError_t e_ = (x);                                                 \
+    if (e_ != hipSuccess) {                                              \
+      fprintf(stderr, "drb_engine: %s failed: %s (%s:%d)\n", #x,          \
+              hipGetErrorString(e_), __FILE__, __LINE__);                \
+      return DRB_EDEVICE;                                                \
+    }                                                                    \
+  } while (0)
+
+struct drb_engine {
+  drb_config cfg;
+  View v;
+  View *dview;  // device copy of v (kernels read it with scalar loads)
+  hipStream_t stream;
+  uint64_t round;
+  uint64_t bytes;
+  std::vector<void *> allocs;
+  void *scratch;
+  size_t scratch_bytes;
+};
+
+static __host__ __device__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+template <typename T>
+static int dalloc(drb_engine *e, T **p, uint64_t count) {
+  uint64_t b = count * sizeof(T);
+  if (b == 0) b = 16;
+  void *q = nullptr;
+  HIPCHK(hipMalloc(&q, b));
+  HIPCHK(hipMemsetAsync(q, 0, b, e->stream));
+  e->allocs.push_back(q);
+  e->bytes += b;
+  *p = (T *)q;
+  return DRB_OK;
+}
+
+static int scratch(drb_engine *e, size_t bytes, void **out) {
+  if (bytes > e->scratch_bytes) {
+    if (e->scratch) HIPCHK(hipFree(e->scratch));
+    e->scratch = nullptr;
+    size_t b = std::max(bytes, (size_t)1 << 20);
+    HIPCHK(hipMalloc(&e->scratch, b));
+    e->scratch_bytes = b;
+  }
+  *out = e->scratch;
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- gather
+template <typename T>
+__global__ void k_gather(const T *base, const uint64_t *idx, T *out,
+                         uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = base[idx[i]];
+}
+
+template <typename T>
+__global__ void k_scatter(T *base, const uint64_t *idx, const T *in,
+                          uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) base[idx[i]] = in[i];
+}
+
+template <typename T>
+static int gather(drb_engine *e, const T *base,
+                  const std::vector<uint64_t> &idx, std::vector<T> &out) {
+  uint64_t n = idx.size();
+  out.resize(n);
+  if (!n) return DRB_OK;
+  void *s;
+  if (scratch(e, n * (8 + sizeof(T)) + 64, &s)) return DRB_EDEVICE;
+  uint64_t *didx = (uint64_t *)s;
+  T *dout = (T *)((char *)s + ((n * 8 + 15) & ~15ull));
+  HIPCHK(hipMemcpyAsync(didx, idx.data(), n * 8, hipMemcpyHostToDevice,
+                        e->stream));
+  k_gather<T><<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(base, didx,
+                                                                   dout, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out.data(), dout, n * sizeof(T), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+template <typename T>
+static int scatter(drb_engine *e, T *base, const std::vector<uint64_t> &idx,
+                   const std::vector<T> &in) {
+  uint64_t n = idx.size();
+  if (!n) return DRB_OK;
+  void *s;
+  if (scratch(e, n * (8 + sizeof(T)) + 64, &s)) return DRB_EDEVICE;
+  uint64_t *didx = (uint64_t *)s;
+  T *din = (T *)((char *)s + ((n * 8 + 15) & ~15ull));
+  HIPCHK(hipMemcpyAsync(didx, idx.data(), n * 8, hipMemcpyHostToDevice,
+                        e->stream));
+  HIPCHK(hipMemcpyAsync(din, in.data(), n * sizeof(T), hipMemcpyHostToDevice,
+                        e->stream));
+  k_scatter<T><<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(base, didx,
+                                                                    din, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+static uint4 mk4h(uint64_t a, uint64_t b) {
+  uint4 q;
+  q.x = (uint32_t)a;
+  q.y = (uint32_t)(a >> 32);
+  q.z = (uint32_t)b;
+  q.w = (uint32_t)(b >> 32);
+  return q;
+}
+static uint64_t lo64h(uint4 q) { return (uint64_t)q.x | ((uint64_t)q.y << 32); }
+static uint64_t hi64h(uint4 q) { return (uint64_t)q.z | ((uint64_t)q.w << 32); }
+
+__global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t val) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = val;
+}
+
+// ---------------------------------------------------------------- create
+extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
+  if (!cfg || !out) return DRB_EINVAL;
+  *out = nullptr;
+  if (cfg->num_groups == 0 || cfg->num_replicas < 1 ||
+      cfg->num_replicas > DRB_MAX_REPLICAS)
+    return DRB_EINVAL;
+  if (!is_pow2(cfg->window) || cfg->window < 4 || cfg->window > 65535)
+    return DRB_EINVAL;
+  if (cfg->cmd_cap == 0 || cfg->cmd_cap % 16 || cfg->cmd_cap > 64)
+    return DRB_ENOSYS;  // longer inline Cmds are a later round (C5)
+  if (cfg->mailbox < 4 || cfg->mailbox > 15) return DRB_EINVAL;
+  if (!is_pow2(cfg->kv_slots) || cfg->kv_val_cap == 0 ||
+      cfg->kv_val_cap > 124)
+    return DRB_EINVAL;
+  if (cfg->max_props == 0 || cfg->prop_slots == 0 || cfg->ri_slots == 0)
+    return DRB_EINVAL;
+  if (cfg->election_rtt == 0 || cfg->heartbeat_rtt == 0) return DRB_EINVAL;
+  // limitSize never binds inside the window (entryutils.go:50-63)
+  if ((uint64_t)cfg->window * (128 + cfg->cmd_cap) > MAX_ENTRY_SIZE)
+    return DRB_EINVAL;
+  drb_engine *e = new drb_engine();
+  e->cfg = *cfg;
+  e->round = 0;
+  e->bytes = 0;
+  e->scratch = nullptr;
+  e->scratch_bytes = 0;
+  if (hipSetDevice(cfg->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
+          hipSuccess) {
+    delete e;
+    return DRB_EDEVICE;
+  }
+  View &v = e->v;
+  memset(&v, 0, sizeof(v));
+  const uint64_t G = cfg->num_groups, R = cfg->num_replicas;
+  v.G = G;
+  v.R = (uint32_t)R;
+  v.W = cfg->window;
+  v.C16 = cfg->cmd_cap / 16;
+  v.MB = cfg->mailbox;
+  v.KS = cfg->kv_slots;
+  v.kv_val_cap = cfg->kv_val_cap;
+  v.KVW = 1 + (cfg->kv_val_cap > 4 ? (cfg->kv_val_cap - 4 + 15) / 16 : 0);
+  v.max_props = cfg->max_props;
+  v.election_rtt = cfg->election_rtt;
+  v.heartbeat_rtt = cfg->heartbeat_rtt;
+  v.check_quorum = cfg->check_quorum;
+  v.first_shard_id = cfg->first_shard_id;
+  int rc = 0;
+  rc |= dalloc(e, &v.u64, (uint64_t)NUM_U64 * R * G);
+  rc |= dalloc(e, &v.u32, (uint64_t)NUM_U32 * R * G);
+  rc |= dalloc(e, &v.rem_match, R * R * G);
+  rc |= dalloc(e, &v.rem_next, R * R * G);
+  rc |= dalloc(e, &v.rem_state, R * R * G);
+  rc |= dalloc(e, &v.rem_active, R * R * G);
+  rc |= dalloc(e, &v.ri_ctx, R * DRB_RI_DEPTH * G);
+  rc |= dalloc(e, &v.ri_idx, R * DRB_RI_DEPTH * G);
+  rc |= dalloc(e, &v.ri_conf, R * DRB_RI_DEPTH * G);
+  rc |= dalloc(e, &v.ring, R * v.W * (ENT_META + v.C16) * G);
+  rc |= dalloc(e, &v.mbox, 2 * R * R * v.MB * MSG_CHUNKS * G);
+  rc |= dalloc(e, &v.mbox_meta, 2 * R * G);
+  rc |= dalloc(e, &v.kv, R * G * v.KS * v.KVW);
+  rc |= dalloc(e, &v.props,
+               (uint64_t)cfg->prop_slots * v.max_props * (PROP_META + v.C16) *
+                   G);
+  rc |= dalloc(e, &v.prop_count, (uint64_t)cfg->prop_slots * G);
+  rc |= dalloc(e, &v.ri_in, (uint64_t)cfg->ri_slots * G);
+  rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
+  rc |= dalloc(e, &v.rtr_count, R * G);
+  rc |= dalloc(e, &v.counters, NUM_COUNTERS);
+  rc |= dalloc(e, &e->dview, 1);
+  if (!rc) {  // no Replicate in flight: ring_guard = +inf
+    k_fill_u64<<<(unsigned)((R * G + 255) / 256), 256, 0, e->stream>>>(
+        v.u64 + u64_ix(v, F_RING_GUARD, 0, 0), R * G, ~0ull);
+    if (hipGetLastError() != hipSuccess) rc = 1;
+  }
+  if (!rc && hipMemcpyAsync(e->dview, &e->v, sizeof(View),
+                            hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    rc = 1;
+  if (rc || hipStreamSynchronize(e->stream) != hipSuccess) {
+    drb_engine_destroy(e);
+    return DRB_ENOMEM;
+  }
+  *out = e;
+  return DRB_OK;
+}
+
+extern "C" int drb_engine_destroy(drb_engine *e) {
+  if (!e) return DRB_EINVAL;
+  (void)hipStreamSynchronize(e->stream);
+  for (void *p : e->allocs) (void)hipFree(p);
+  if (e->scratch) (void)hipFree(e->scratch);
+  (void)hipStreamDestroy(e->stream);
+  delete e;
+  return DRB_OK;
+}
+
+extern "C" uint64_t drb_engine_device_bytes(const drb_engine *e) {
+  return e ? e->bytes : 0;
+}
+
+extern "C" void *drb_engine_stream(drb_engine *e) {
+  return e ? (void *)e->stream : nullptr;
+}
+
+extern "C" int drb_engine_sync(drb_engine *e) {
+  if (!e) return DRB_EINVAL;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+extern "C" uint64_t drb_engine_round(const drb_engine *e) {
+  return e ? e->round : 0;
+}
+
+// ---------------------------------------------------------------- state
+static const int kU64Order[NUM_U64 - 2] = {
+    F_TERM,           F_VOTE,          F_LEADER_ID,       F_APPLIED,
+    F_ELECTION_TICK,  F_HEARTBEAT_TICK, F_RAND_TIMEOUT,   F_TICK_COUNT,
+    F_COMMITTED,      F_PROCESSED,     F_LAST_INDEX,      F_MARKER_INDEX,
+    F_SAVED_TO,       F_APPLIED_TO_INDEX, F_APPLIED_TO_TERM, F_APPLIED_INDEX,
+    F_CONFIRMED_INDEX, F_PUSHED_INDEX, F_PREV_TERM,       F_PREV_VOTE,
+    F_PREV_COMMIT,    F_SM_INDEX,      F_SM_TERM,         F_KV_COUNT};
+
+// drb_replica_state fields 2.. in kU64Order order (after shard/replica id)
+static uint64_t *st_u64(drb_replica_state *s, int k) {
+  uint64_t *base = &s->term;
+  return base + k;
+}
+
+static int check_range(drb_engine *e, uint64_t first, uint64_t n) {
+  if (!e || first >= e->cfg.num_groups || n > e->cfg.num_groups - first)
+    return DRB_ERANGE;
+  return DRB_OK;
+}
+
+extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
+                                   uint64_t n_groups,
+                                   const drb_replica_state *st) {
+  if (check_range(e, first_group, n_groups)) return DRB_ERANGE;
+  const View &v = e->v;
+  const uint32_t R = v.R;
+  std::vector<uint64_t> i64, i32, irm;
+  std::vector<uint64_t> d64;
+  std::vector<uint32_t> d32, drs, dra;
+  std::vector<uint64_t> drm, drn;
+  std::vector<uint64_t> iri;
+  std::vector<uint4> dric, drii;
+  std::vector<uint32_t> dricf;
+  for (uint64_t gi = 0; gi < n_groups; ++gi) {
+    uint64_t g = first_group + gi;
+    for (uint32_t s = 0; s < R; ++s) {
+      drb_replica_state c = st[gi * R + s];
+      for (int k = 0; k < NUM_U64 - 2; ++k) {
+        i64.push_back(u64_ix(v, kU64Order[k], s, g));
+        d64.push_back(*st_u64(&c, k));
+      }
+      uint32_t w[NUM_U32] = {c.role, c.flags, c.fallback_reason, c.ri_count};
+      for (int k = 0; k < NUM_U32; ++k) {
+        i32.push_back(u32_ix(v, k, s, g));
+        d32.push_back(w[k]);
+      }
+      for (uint32_t p = 0; p < R; ++p) {
+        irm.push_back(rem_ix(v, s, p, g));
+        drm.push_back(c.remotes[p].match);
+        drn.push_back(c.remotes[p].next);
+        drs.push_back(c.remotes[p].state);
+        dra.push_back(c.remotes[p].active);
+      }
+      for (uint32_t d = 0; d < DRB_RI_DEPTH; ++d) {
+        iri.push_back(ri_ix(v, s, d, g));
+        dric.push_back(mk4h(c.ri[d].ctx_low, c.ri[d].ctx_high));
+        drii.push_back(mk4h(c.ri[d].index, c.ri[d].from));
+        dricf.push_back(c.ri[d].confirmed);
+      }
+    }
+  }
+  int rc = 0;
+  rc |= scatter(e, v.u64, i64, d64);
+  rc |= scatter(e, v.u32, i32, d32);
+  rc |= scatter(e, v.rem_match, irm, drm);
+  rc |= scatter(e, v.rem_next, irm, drn);
+  rc |= scatter(e, v.rem_state, irm, drs);
+  rc |= scatter(e, v.rem_active, irm, dra);
+  rc |= scatter(e, v.ri_ctx, iri, dric);
+  rc |= scatter(e, v.ri_idx, iri, drii);
+  rc |= scatter(e, v.ri_conf, iri, dricf);
+  return rc ? DRB_EDEVICE : DRB_OK;
+}
+
+extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
+                                   uint64_t n_groups, drb_replica_state *st) {
+  if (check_range(e, first_group, n_groups)) return DRB_ERANGE;
+  const View &v = e->v;
+  const uint32_t R = v.R;
+  std::vector<uint64_t> i64, i32, irm, iri;
+  for (uint64_t gi = 0; gi < n_groups; ++gi) {
+    uint64_t g = first_group + gi;
+    for (uint32_t s = 0; s < R; ++s) {
+      for (int k = 0; k < NUM_U64 - 2; ++k)
+        i64.push_back(u64_ix(v, kU64Order[k], s, g));
+      for (int k = 0; k < NUM_U32; ++k) i32.push_back(u32_ix(v, k, s, g));
+      for (uint32_t p = 0; p < R; ++p) irm.push_back(rem_ix(v, s, p, g));
+      for (uint32_t d = 0; d < DRB_RI_DEPTH; ++d)
+        iri.push_back(ri_ix(v, s, d, g));
+    }
+  }
+  std::vector<uint64_t> d64, drm, drn;
+  std::vector<uint32_t> d32, drs, dra, dricf;
+  std::vector<uint4> dric, drii;
+  int rc = 0;
+  rc |= gather(e, v.u64, i64, d64);
+  rc |= gather(e, v.u32, i32, d32);
+  rc |= gather(e, v.rem_match, irm, drm);
+  rc |= gather(e, v.rem_next, irm, drn);
+  rc |= gather(e, v.rem_state, irm, drs);
+  rc |= gather(e, v.rem_active, irm, dra);
+  rc |= gather(e, v.ri_ctx, iri, dric);
+  rc |= gather(e, v.ri_idx, iri, drii);
+  rc |= gather(e, v.ri_conf, iri, dricf);
+  if (rc) return DRB_EDEVICE;
+  size_t a = 0, b = 0, c2 = 0, d = 0;
+  for (uint64_t gi = 0; gi < n_groups; ++gi) {
+    uint64_t g = first_group + gi;
+    for (uint32_t s = 0; s < R; ++s) {
+      drb_replica_state &o = st[gi * R + s];
+      memset(&o, 0, sizeof(o));
+      o.shard_id = v.first_shard_id + g;
+      o.replica_id = s + 1;
+      for (int k = 0; k < NUM_U64 - 2; ++k) *st_u64(&o, k) = d64[a++];
+      o.role = d32[b++];
+      o.flags = d32[b++];
+      o.fallback_reason = d32[b++];
+      o.ri_count = d32[b++];
+      for (uint32_t p = 0; p < R; ++p, ++c2) {
+        o.remotes[p].match = drm[c2];
+        o.remotes[p].next = drn[c2];
+        o.remotes[p].state = drs[c2];
+        o.remotes[p].active = dra[c2];
+      }
+      for (uint32_t q = 0; q < DRB_RI_DEPTH; ++q, ++d) {
+        if (q >= o.ri_count) continue;
+        o.ri[q].ctx_low = lo64h(dric[d]);
+        o.ri[q].ctx_high = hi64h(dric[d]);
+        o.ri[q].index = lo64h(drii[d]);
+        o.ri[q].from = hi64h(drii[d]);
+        o.ri[q].confirmed = dricf[d];
+      }
+    }
+  }
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- log
+static void entry_to_chunks(const View &v, const drb_entry &en,
+                            const uint8_t *pool, uint4 *out /*3 + C16*/) {
+  out[0] = mk4h(en.term, en.key);
+  out[1] = mk4h(en.client_id, en.series_id);
+  out[2] = mk4h(en.responded_to, 0);
+  out[2].z = en.type;
+  out[2].w = en.cmd_len;
+  for (uint32_t c = 0; c < v.C16; ++c) {
+    uint8_t b[16] = {0};
+    for (uint32_t k = 0; k < 16; ++k) {
+      uint32_t o = c * 16 + k;
+      if (o < en.cmd_len) b[k] = pool[en.cmd_off + o];
+    }
+    memcpy(&out[ENT_META + c], b, 16);
+  }
+}
+
+extern "C" int drb_import_log(drb_engine *e, uint64_t group, uint32_t slot,
+                              const drb_entry *ents, size_t n,
+                              const uint8_t *pool) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  const View &v = e->v;
+  if (n > v.W) return DRB_ERANGE;
+  std::vector<uint64_t> idx;
+  std::vector<uint4> val;
+  std::vector<uint4> ch(ENT_META + v.C16);
+  for (size_t i = 0; i < n; ++i) {
+    if (ents[i].cmd_len > v.C16 * 16) return DRB_ERANGE;
+    if (i && ents[i].index != ents[i - 1].index + 1) return DRB_EINVAL;
+    entry_to_chunks(v, ents[i], pool, ch.data());
+    for (uint32_t c = 0; c < ENT_META + v.C16; ++c) {
+      idx.push_back(ring_ix(v, slot, ents[i].index, c, group));
+      val.push_back(ch[c]);
+    }
+  }
+  if (scatter(e, v.ring, idx, val)) return DRB_EDEVICE;
+  if (n) {
+    std::vector<uint64_t> ri = {u64_ix(v, F_RING_LO, slot, group)};
+    std::vector<uint64_t> rv = {ents[0].index};
+    if (scatter(e, v.u64, ri, rv)) return DRB_EDEVICE;
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_export_log(drb_engine *e, uint64_t group, uint32_t slot,
+                              uint64_t lo, uint64_t hi, drb_entry *out,
+                              uint8_t *pool, size_t pool_cap) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  if (hi < lo) return DRB_OK;
+  const View &v = e->v;
+  if (hi - lo + 1 > v.W) return DRB_ERANGE;
+  std::vector<uint64_t> idx;
+  for (uint64_t i = lo; i <= hi; ++i)
+    for (uint32_t c = 0; c < ENT_META + v.C16; ++c)
+      idx.push_back(ring_ix(v, slot, i, c, group));
+  std::vector<uint4> val;
+  if (gather(e, v.ring, idx, val)) return DRB_EDEVICE;
+  size_t used = 0, k = 0;
+  for (uint64_t i = lo; i <= hi; ++i, ++k) {
+    const uint4 *c = &val[k * (ENT_META + v.C16)];
+    drb_entry &o = out[k];
+    o.term = lo64h(c[0]);
+    o.key = hi64h(c[0]);
+    o.client_id = lo64h(c[1]);
+    o.series_id = hi64h(c[1]);
+    o.responded_to = lo64h(c[2]);
+    o.type = c[2].z;
+    o.cmd_len = c[2].w;
+    o.index = i;
+    o.cmd_off = used;
+    if (o.cmd_len > v.C16 * 16 || used + o.cmd_len > pool_cap)
+      return DRB_ERANGE;
+    memcpy(pool + used, &c[ENT_META], o.cmd_len);
+    used += o.cmd_len;
+  }
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- init
+// ConfigChange{AddNode, ReplicaID id, "localhost:<26000+id-1>", Initialize}
+// (configchange.go:28-56, bootstrap peer.go:404-428)
+__host__ __device__ static uint32_t cc_bytes(uint32_t id, uint8_t *b) {
+  uint32_t i = 0;
+  b[i++] = 0x08;
+  b[i++] = 0;
+  b[i++] = 0x10;
+  b[i++] = 0;
+  b[i++] = 0x18;
+  b[i++] = (uint8_t)id;  // id < 128
+  b[i++] = 0x22;
+  b[i++] = 15;
+  const char *h = "localhost:";
+  for (int k = 0; k < 10; ++k) b[i++] = (uint8_t)h[k];
+  uint32_t port = 26000 + id - 1;
+  char d[5];
+  for (int k = 4; k >= 0; --k) {
+    d[k] = (char)('0' + port % 10);
+    port /= 10;
+  }
+  for (int k = 0; k < 5; ++k) b[i++] = (uint8_t)d[k];
+  b[i++] = 0x28;
+  b[i++] = 1;
+  return i;  // 25
+}
+
+__global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
+                              uint64_t seed) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t s = blockIdx.y;
+  if (g >= v.G) return;
+  const uint64_t R = v.R, L1 = R + 1;  // last index: R config + 1 no-op
+  const bool is_leader = s == leader;
+  uint64_t *u = v.u64;
+#define SET(F, x) u[u64_ix(v, F, s, g)] = (x)
+  SET(F_TERM, term);
+  SET(F_VOTE, leader + 1);
+  SET(F_LEADER_ID, leader + 1);
+  SET(F_APPLIED, L1);
+  SET(F_ELECTION_TICK, 0);
+  SET(F_HEARTBEAT_TICK, 0);
+  SET(F_RAND_TIMEOUT,
+      v.election_rtt +
+          mix64(seed ^ (0xE1ull << 56) ^ (g * R + s)) % v.election_rtt);
+  SET(F_TICK_COUNT, 1);
+  SET(F_COMMITTED, L1);
+  SET(F_PROCESSED, L1);
+  SET(F_LAST_INDEX, L1);
+  SET(F_MARKER_INDEX, L1 + 1);
+  SET(F_SAVED_TO, L1);
+  SET(F_APPLIED_TO_INDEX, L1);
+  SET(F_APPLIED_TO_TERM, term);
+  SET(F_APPLIED_INDEX, L1);
+  SET(F_CONFIRMED_INDEX, L1);
+  SET(F_PUSHED_INDEX, L1);
+  SET(F_PREV_TERM, term);
+  SET(F_PREV_VOTE, leader + 1);
+  SET(F_PREV_COMMIT, L1);
+  SET(F_SM_INDEX, L1);
+  SET(F_SM_TERM, term);
+  SET(F_KV_COUNT, 0);
+  SET(F_RING_LO, 1);
+  SET(F_RING_GUARD, ~0ull);
+#undef SET
+  v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
+  v.u32[u32_ix(v, W_FLAGS, s, g)] = DRB_F_HOSTED;
+  v.u32[u32_ix(v, W_FB_REASON, s, g)] = 0;
+  v.u32[u32_ix(v, W_RI_COUNT, s, g)] = 0;
+  for (uint32_t p = 0; p < v.R; ++p) {
+    uint64_t m, n;
+    uint32_t st, act;
+    if (is_leader) {  // after the no-op round trip (raft.go:1878-1908)
+      m = L1;
+      n = L1 + 1;
+      st = p == s ? DRB_REMOTE_RETRY : DRB_REMOTE_REPLICATE;
+      act = p == s ? 0 : 1;
+    } else {  // becomeFollowerKE at the vote (raft.go:1088-1097)
+      m = p == s ? R : 0;
+      n = R + 1;
+      st = DRB_REMOTE_RETRY;
+      act = 0;
+    }
+    v.rem_match[rem_ix(v, s, p, g)] = m;
+    v.rem_next[rem_ix(v, s, p, g)] = n;
+    v.rem_state[rem_ix(v, s, p, g)] = st;
+    v.rem_active[rem_ix(v, s, p, g)] = act;
+  }
+  // resident window: R config-change entries (term 1) + the no-op (term)
+  for (uint64_t i = 1; i <= L1; ++i) {
+    bool cc = i <= R;
+    v.ring[ring_ix(v, s, i, 0, g)] = make_uint4(
+        (uint32_t)(cc ? 1 : term), (uint32_t)((cc ? 1 : term) >> 32), 0, 0);
+    v.ring[ring_ix(v, s, i, 1, g)] = make_uint4(0, 0, 0, 0);
+    uint8_t b[32] = {0};
+    uint32_t len = cc ? cc_bytes((uint32_t)i, b) : 0;
+    v.ring[ring_ix(v, s, i, 2, g)] =
+        make_uint4(0, 0, cc ? DRB_ENTRY_CONFIG_CHANGE : DRB_ENTRY_APPLICATION,
+                   len);
+    for (uint32_t c = 0; c < v.C16; ++c) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t k = 0; k < 16; ++k) {
+        uint32_t o = c * 16 + k;
+        if (o < 32) w[k >> 2] |= (uint32_t)b[o] << (8 * (k & 3));
+      }
+      v.ring[ring_ix(v, s, i, ENT_META + c, g)] =
+          make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+extern "C" int drb_init_steady(drb_engine *e, uint64_t term,
+                               uint32_t leader_slot, uint64_t seed) {
+  if (!e || leader_slot >= e->cfg.num_replicas || term < 2) return DRB_EINVAL;
+  if (e->cfg.cmd_cap < 32 || e->v.W < e->cfg.num_replicas + 2)
+    return DRB_EINVAL;
+  dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
+  k_init_steady<<<grid, 256, 0, e->stream>>>(e->v, term, leader_slot, seed);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- inputs
+extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
+                                   const uint32_t *counts,
+                                   const drb_entry *ents,
+                                   const uint8_t *pool) {
+  if (!e || slot >= e->cfg.prop_slots) return DRB_ERANGE;
+  const View &v = e->v;
+  const uint64_t G = v.G;
+  const uint32_t chunks = PROP_META + v.C16;
+  std::vector<uint4> host((uint64_t)v.max_props * chunks * G);
+  memset(host.data(), 0, host.size() * sizeof(uint4));
+  for (uint64_t g = 0; g < G; ++g) {
+    if (counts[g] > v.max_props) return DRB_ERANGE;
+    for (uint32_t j = 0; j < counts[g]; ++j) {
+      const drb_entry &en = ents[g * v.max_props + j];
+      if (en.cmd_len > v.C16 * 16) return DRB_ERANGE;
+      uint64_t b = (uint64_t)j * chunks * G + g;
+      host[b + 0 * G] = mk4h(en.key, en.client_id);
+      host[b + 1 * G] = mk4h(en.series_id, en.responded_to);
+      uint4 p2 = {en.type, en.cmd_len, 0, 0};
+      host[b + 2 * G] = p2;
+      for (uint32_t c = 0; c < v.C16; ++c) {
+        uint8_t by[16] = {0};
+        for (uint32_t k = 0; k < 16; ++k)
+          if (c * 16 + k < en.cmd_len) by[k] = pool[en.cmd_off + c * 16 + k];
+        memcpy(&host[b + (PROP_META + c) * G], by, 16);
+      }
+    }
+  }
+  uint4 *dst = v.props + prop_ix(v, slot, 0, 0, 0);
+  HIPCHK(hipMemcpyAsync(dst, host.data(), host.size() * sizeof(uint4),
+                        hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(v.prop_count + (uint64_t)slot * G, counts, G * 4,
+                        hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+// SURVEY 8(d) synthetic writes; bit-identical to dragonboat_amd/workload.py
+__global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
+                         uint32_t val_len, uint64_t seed, uint64_t salt) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  const uint64_t cid = mix64(seed ^ 0xC11E47C11E47C11Eull ^ g) | 1;
+  for (uint32_t j = 0; j < k; ++j) {
+    uint64_t r0 = mix64(seed ^ (g * 0x9E3779B97F4A7C15ull) ^ (salt << 32) ^
+                        ((uint64_t)j << 16));
+    uint64_t r1 = mix64(r0), r2 = mix64(r1);
+    uint64_t kv_key = r1 % key_space;
+    // Cmd = 00 | 0a 08 <key8 LE> 12 <vlen> <val>
+    uint8_t b[64];
+    for (int q = 0; q < 64; ++q) b[q] = 0;
+    b[0] = 0x00;
+    b[1] = 0x0a;
+    b[2] = 8;
+    for (int q = 0; q < 8; ++q) b[3 + q] = (uint8_t)(kv_key >> (8 * q));
+    b[11] = 0x12;
+    b[12] = (uint8_t)val_len;
+    uint64_t x = r2;
+    for (uint32_t q = 0; q < val_len; ++q) {
+      if (q && (q % 8) == 0) x = mix64(x);
+      b[13 + q] = (uint8_t)(x >> (8 * (q % 8)));
+    }
+    uint32_t clen = 13 + val_len;
+    v.props[prop_ix(v, ps, j, 0, g)] = mk4(r0 | 1, cid);
+    v.props[prop_ix(v, ps, j, 1, g)] = mk4(0, 0);
+    v.props[prop_ix(v, ps, j, 2, g)] =
+        make_uint4(DRB_ENTRY_ENCODED, clen, 0, 0);
+    for (uint32_t c = 0; c < v.C16; ++c) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t q = 0; q < 16; ++q)
+        w[q >> 2] |= (uint32_t)b[c * 16 + q] << (8 * (q & 3));
+      v.props[prop_ix(v, ps, j, PROP_META + c, g)] =
+          make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  v.prop_count[(uint64_t)ps * v.G + g] = k;
+}
+
+extern "C" int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
+                                    uint32_t key_space, uint32_t val_len,
+                                    uint64_t seed, uint64_t salt) {
+  if (!e || slot >= e->cfg.prop_slots || k > e->cfg.max_props || !key_space)
+    return DRB_EINVAL;
+  if (13 + val_len > e->cfg.cmd_cap || val_len > 50) return DRB_EINVAL;
+  k_gen_kv<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
+      e->v, slot, k, key_space, val_len, seed, salt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+extern "C" int drb_stage_read_index(drb_engine *e, uint32_t slot,
+                                    const uint64_t *ctx_low,
+                                    const uint64_t *ctx_high) {
+  if (!e || slot >= e->cfg.ri_slots) return DRB_ERANGE;
+  const uint64_t G = e->v.G;
+  std::vector<uint4> host(G);
+  for (uint64_t g = 0; g < G; ++g) host[g] = mk4h(ctx_low[g], ctx_high[g]);
+  HIPCHK(hipMemcpyAsync(e->v.ri_in + (uint64_t)slot * G, host.data(),
+                        G * sizeof(uint4), hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+__global__ void k_gen_ri(View v, uint32_t rs, uint64_t seed, uint64_t salt,
+                         uint64_t high) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  uint64_t low = mix64(seed ^ 0x5EAD1DE85EAD1DE8ull ^
+                       (g * 0x9E3779B97F4A7C15ull) ^ (salt << 40)) |
+                 1;
+  v.ri_in[(uint64_t)rs * v.G + g] = mk4(low, high);
+}
+
+extern "C" int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
+                                  uint64_t high) {
+  if (!e || slot >= e->cfg.ri_slots) return DRB_ERANGE;
+  k_gen_ri<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
+      e->v, slot, seed, e->round + 1, high);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- ingest
+static bool slot_hosted(drb_engine *e, uint64_t g, uint32_t s, bool *ok) {
+  std::vector<uint64_t> idx = {u32_ix(e->v, W_FLAGS, s, g)};
+  std::vector<uint32_t> f;
+  *ok = gather(e, e->v.u32, idx, f) == DRB_OK;
+  return *ok && (f[0] & DRB_F_HOSTED) &&
+         !(f[0] & (DRB_F_FALLBACK | DRB_F_ERROR));
+}
+
+extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
+                          const drb_entry *ents, const uint8_t *pool,
+                          uint64_t *accepted, uint64_t *dropped) {
+  if (!e) return DRB_EINVAL;
+  const View &v = e->v;
+  const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
+  const uint32_t tag = (uint32_t)e->round;
+  uint64_t acc = 0, drop = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const drb_message &m = msgs[i];
+    uint64_t g = m.shard_id - v.first_shard_id;
+    bool ok = g < v.G && m.to >= 1 && m.to <= v.R && m.from >= 1 &&
+              m.from <= v.R && m.from != m.to && m.n_entries <= 0xffff;
+    bool okd = true;
+    if (ok) ok = slot_hosted(e, g, (uint32_t)(m.to - 1), &okd);
+    bool from_hosted = ok ? slot_hosted(e, g, (uint32_t)(m.from - 1), &okd)
+                          : false;
+    if (!okd) return DRB_EDEVICE;
+    if (!ok || from_hosted) {  // transport delivers only remote senders
+      drop++;
+      continue;
+    }
+    uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
+    std::vector<uint64_t> mi = {mmeta_ix(v, buf, from, g)};
+    std::vector<uint64_t> meta;
+    if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
+    uint64_t cur = meta[0];
+    if ((uint32_t)(cur >> 32) != tag) cur = (uint64_t)tag << 32;
+    uint32_t k = (uint32_t)(cur >> (4 * to)) & 15u;
+    if (k >= v.MB) {  // MessageQueue full (message.go:105-123)
+      drop++;
+      continue;
+    }
+    // entries travel in the sender's (unhosted) window slot
+    if (m.type == DRB_MSG_REPLICATE && m.n_entries) {
+      if (m.n_entries > v.W) {
+        drop++;
+        continue;
+      }
+      std::vector<drb_entry> es(ents + m.entries_off,
+                                ents + m.entries_off + m.n_entries);
+      for (size_t q = 0; q < es.size(); ++q) es[q].index = m.log_index + 1 + q;
+      int rc = drb_import_log(e, g, from, es.data(), es.size(), pool);
+      if (rc) return rc;
+    }
+    std::vector<uint64_t> idx;
+    std::vector<uint4> val;
+    uint4 c0;
+    c0.x = msg_meta(m.type, m.reject ? 1 : 0, (uint32_t)m.n_entries);
+    c0.y = 0;
+    c0.z = (uint32_t)m.term;
+    c0.w = (uint32_t)(m.term >> 32);
+    uint4 c[4] = {c0, mk4h(m.log_index, m.log_term), mk4h(m.commit, m.hint),
+                  mk4h(m.hint_high, 0)};
+    for (uint32_t q = 0; q < MSG_CHUNKS; ++q) {
+      idx.push_back(mbox_ix(v, buf, from, to, k, q, g));
+      val.push_back(c[q]);
+    }
+    if (scatter(e, v.mbox, idx, val)) return DRB_EDEVICE;
+    cur += 1ull << (4 * to);
+    std::vector<uint64_t> mv = {cur};
+    if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
+    acc++;
+  }
+  if (accepted) *accepted = acc;
+  if (dropped) *dropped = drop;
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- step
+template <int R>
+static void launch_step(drb_engine *e, const RoundParams &p) {
+  dim3 grid((unsigned)((e->v.G + 255) / 256), R);
+  step_kernel<R><<<grid, 256, 0, e->stream>>>(e->dview, p);
+}
+
+extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
+  if (!e || !in) return DRB_EINVAL;
+  if (in->prop_slot != DRB_NONE && in->prop_slot >= e->cfg.prop_slots)
+    return DRB_ERANGE;
+  if (in->ri_slot != DRB_NONE && in->ri_slot >= e->cfg.ri_slots)
+    return DRB_ERANGE;
+  RoundParams p;
+  p.round = e->round + 1;
+  p.tick = in->tick ? 1 : 0;
+  p.prop_slot = in->prop_slot;
+  p.ri_slot = in->ri_slot;
+  p.pad = 0;
+  switch (e->v.R) {
+    case 1: launch_step<1>(e, p); break;
+    case 2: launch_step<2>(e, p); break;
+    case 3: launch_step<3>(e, p); break;
+    case 4: launch_step<4>(e, p); break;
+    case 5: launch_step<5>(e, p); break;
+    case 6: launch_step<6>(e, p); break;
+    case 7: launch_step<7>(e, p); break;
+    case 8: launch_step<8>(e, p); break;
+    default: return DRB_EINVAL;
+  }
+  HIPCHK(hipGetLastError());
+  e->round++;
+  return DRB_OK;
+}
+
+extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
+                                 int reset) {
+  if (!e || !out) return DRB_EINVAL;
+  unsigned long long c[NUM_COUNTERS];
+  HIPCHK(hipMemcpyAsync(c, e->v.counters, sizeof(c), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  out->round = e->round;
+  out->committed_entries = c[C_COMMITTED];
+  out->applied_entries = c[C_APPLIED];
+  out->messages = c[C_MESSAGES];
+  out->ready_to_reads = c[C_RTR];
+  out->dropped_read_indexes = c[C_DROPPED_RI];
+  out->fallbacks = c[C_FALLBACKS];
+  out->errors = c[C_ERRORS];
+  if (reset) {
+    HIPCHK(hipMemsetAsync(e->v.counters, 0, sizeof(c), e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_step_round(drb_engine *e, const drb_round_in *in,
+                              drb_round_out *out) {
+  if (!e || !in) return DRB_EINVAL;
+  HIPCHK(hipMemsetAsync(e->v.counters, 0,
+                        NUM_COUNTERS * sizeof(unsigned long long), e->stream));
+  int rc = drb_step_round_async(e, in);
+  if (rc) return rc;
+  if (out) return drb_read_counters(e, out, 1);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- outputs
+static int export_pair(drb_engine *e, uint32_t buf, uint32_t tag, uint64_t g,
+                       uint32_t from, uint32_t to, drb_message *out,
+                       size_t cap, size_t *nm, drb_entry *ents, size_t ecap,
+                       size_t *ne, uint8_t *pool, size_t pcap, size_t *np,
+                       uint64_t cnt) {
+  const View &v = *&e->v;
+  uint32_t k = (uint32_t)(cnt >> (4 * to)) & 15u;
+  if (!k) return DRB_OK;
+  std::vector<uint64_t> idx;
+  for (uint32_t q = 0; q < k; ++q)
+    for (uint32_t c = 0; c < MSG_CHUNKS; ++c)
+      idx.push_back(mbox_ix(v, buf, from, to, q, c, g));
+  std::vector<uint4> val;
+  if (gather(e, v.mbox, idx, val)) return DRB_EDEVICE;
+  (void)tag;
+  for (uint32_t q = 0; q < k; ++q) {
+    if (*nm >= cap) return DRB_ERANGE;
+    const uint4 *c = &val[q * MSG_CHUNKS];
+    drb_message &m = out[(*nm)++];
+    memset(&m, 0, sizeof(m));
+    m.shard_id = v.first_shard_id + g;
+    m.from = from + 1;
+    m.to = to + 1;
+    m.type = c[0].x & 0xffu;
+    m.reject = (c[0].x >> 8) & 1u;
+    m.term = hi64h(c[0]);
+    uint64_t ne_ = c[0].x >> 16;
+    switch (m.type) {
+      case DRB_MSG_REPLICATE:
+        m.log_index = lo64h(c[1]);
+        m.log_term = hi64h(c[1]);
+        m.commit = lo64h(c[2]);
+        break;
+      case DRB_MSG_REPLICATE_RESP:
+        m.log_index = lo64h(c[1]);
+        m.hint = hi64h(c[2]);
+        break;
+      case DRB_MSG_HEARTBEAT:
+      case DRB_MSG_HEARTBEAT_RESP:
+        m.commit = lo64h(c[2]);
+        m.hint = hi64h(c[2]);
+        m.hint_high = lo64h(c[3]);
+        break;
+      default:
+        m.log_index = lo64h(c[1]);
+        m.log_term = hi64h(c[1]);
+        m.commit = lo64h(c[2]);
+        m.hint = hi64h(c[2]);
+        m.hint_high = lo64h(c[3]);
+        break;
+    }
+    m.n_entries = ne_;
+    m.entries_off = *ne;
+    if (m.type == DRB_MSG_REPLICATE && ne_) {
+      if (*ne + ne_ > ecap) return DRB_ERANGE;
+      size_t used = 0;
+      int rc = drb_export_log(e, g, from, m.log_index + 1, m.log_index + ne_,
+                              ents + *ne, pool + *np, pcap - *np);
+      if (rc) return rc;
+      for (uint64_t q2 = 0; q2 < ne_; ++q2) {
+        ents[*ne + q2].cmd_off += *np;
+        used += ents[*ne + q2].cmd_len;
+      }
+      *ne += ne_;
+      *np += used;
+    }
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_export_outbox(drb_engine *e, uint64_t group,
+                                 uint32_t from_slot, drb_message *out,
+                                 size_t cap, drb_entry *ents, size_t ent_cap,
+                                 uint8_t *pool, size_t pool_cap,
+                                 size_t *n_msgs) {
+  if (!e || group >= e->cfg.num_groups || from_slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  const View &v = e->v;
+  const uint32_t buf = (uint32_t)(e->round & 1);
+  std::vector<uint64_t> mi = {mmeta_ix(v, buf, from_slot, group)};
+  std::vector<uint64_t> meta;
+  if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
+  size_t nm = 0, ne = 0, np = 0;
+  if ((uint32_t)(meta[0] >> 32) == (uint32_t)e->round && e->round > 0) {
+    // send order across destinations is not recorded per message; the
+    // per-destination order is (messages are compared per destination)
+    for (uint32_t to = 0; to < v.R; ++to) {
+      int rc = export_pair(e, buf, (uint32_t)e->round, group, from_slot, to,
+                           out, cap, &nm, ents, ent_cap, &ne, pool, pool_cap,
+                           &np, meta[0]);
+      if (rc) return rc;
+    }
+  }
+  if (n_msgs) *n_msgs = nm;
+  return DRB_OK;
+}
+
+extern "C" int drb_export_ready_to_reads(drb_engine *e, uint64_t group,
+                                         uint32_t slot, drb_ready_to_read *out,
+                                         size_t cap, size_t *n_out) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  const View &v = e->v;
+  std::vector<uint64_t> ci = {ix(v, slot, group)};
+  std::vector<uint32_t> cnt;
+  if (gather(e, v.rtr_count, ci, cnt)) return DRB_EDEVICE;
+  uint32_t n = std::min<uint32_t>(cnt[0], RTR_CAP);
+  std::vector<uint64_t> idx;
+  for (uint32_t k = 0; k < n; ++k)
+    for (uint32_t c = 0; c < 2; ++c) idx.push_back(rtr_ix(v, slot, k, c, group));
+  std::vector<uint4> val;
+  if (gather(e, v.rtr, idx, val)) return DRB_EDEVICE;
+  for (uint32_t k = 0; k < n && k < cap; ++k) {
+    out[k].shard_id = v.first_shard_id + group;
+    out[k].replica_id = slot + 1;
+    out[k].index = lo64h(val[2 * k]);
+    out[k].ctx_low = hi64h(val[2 * k]);
+    out[k].ctx_high = lo64h(val[2 * k + 1]);
+  }
+  if (n_out) *n_out = n;
+  return DRB_OK;
+}
+
+static int read_kv_table(drb_engine *e, uint64_t group, uint32_t slot,
+                         std::vector<uint4> &tbl) {
+  const View &v = e->v;
+  tbl.resize((uint64_t)v.KS * v.KVW);
+  HIPCHK(hipMemcpyAsync(tbl.data(), v.kv + kv_ix(v, slot, group, 0),
+                        tbl.size() * sizeof(uint4), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+static void slot_value(const View &v, const uint4 *sl, uint8_t *val,
+                       uint32_t vlen) {
+  uint8_t tmp[16 * 9];
+  memcpy(tmp, &sl[0].w, 4);
+  for (uint32_t c = 1; c < v.KVW; ++c) memcpy(tmp + 4 + (c - 1) * 16, &sl[c], 16);
+  memcpy(val, tmp, vlen);
+}
+
+extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
+                             const uint8_t *key, uint32_t key_len,
+                             uint8_t *val, uint32_t val_cap,
+                             uint32_t *val_len) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  if (key_len > 8) return 1;
+  const View &v = e->v;
+  uint64_t k8 = 0;
+  for (uint32_t i = 0; i < key_len; ++i) k8 |= (uint64_t)key[i] << (8 * i);
+  std::vector<uint4> tbl;
+  if (read_kv_table(e, group, slot, tbl)) return DRB_EDEVICE;
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint32_t i = 0; i < key_len; ++i)
+    h = (h ^ ((k8 >> (8 * i)) & 0xff)) * 0x100000001b3ull;
+  h ^= h >> 29;
+  uint32_t ks = (uint32_t)h & (v.KS - 1);
+  for (uint32_t p = 0; p < v.KS; ++p) {
+    const uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
+    bool used = (sl[0].z >> 31) & 1u;
+    if (!used) return 1;
+    uint32_t klen = sl[0].z & 0xffu, vlen = (sl[0].z >> 8) & 0xfffu;
+    if (klen == key_len && lo64h(sl[0]) == k8) {
+      if (val_len) *val_len = vlen;
+      if (vlen > val_cap) return DRB_ERANGE;
+      slot_value(v, sl, val, vlen);
+      return DRB_OK;
+    }
+    ks = (ks + 1) & (v.KS - 1);
+  }
+  return 1;
+}
+
+extern "C" int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot,
+                             uint8_t *keys, uint32_t *key_lens, uint8_t *vals,
+                             uint32_t *val_lens, size_t cap, size_t *n_out) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  const View &v = e->v;
+  std::vector<uint4> tbl;
+  if (read_kv_table(e, group, slot, tbl)) return DRB_EDEVICE;
+  size_t n = 0;
+  for (uint32_t ks = 0; ks < v.KS; ++ks) {
+    const uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
+    if (!((sl[0].z >> 31) & 1u)) continue;
+    if (n < cap) {
+      uint32_t klen = sl[0].z & 0xffu, vlen = (sl[0].z >> 8) & 0xfffu;
+      uint64_t k8 = lo64h(sl[0]);
+      for (uint32_t i = 0; i < 8; ++i) keys[n * 8 + i] = (uint8_t)(k8 >> (8 * i));
+      key_lens[n] = klen;
+      slot_value(v, sl, vals + n * v.kv_val_cap, vlen);
+      val_lens[n] = vlen;
+    }
+    n++;
+  }
+  if (n_out) *n_out = n;
+  return n > cap ? DRB_ERANGE : DRB_OK;
+}
+
+// ---------------------------------------------------------------- CRC32
+// Slicing-by-8 CRC32-IEEE, one lane per buffer; the 8 x 256 table is
+// staged in LDS once per workgroup.
+__constant__ uint32_t c_crc_tab[8][256];
+
+__global__ void k_crc32(const uint8_t *data, const uint64_t *off,
+                        const uint32_t *len, uint32_t *crc, uint64_t n) {
+  __shared__ uint32_t t[8][256];
+  for (uint32_t i = threadIdx.x; i < 8 * 256; i += blockDim.x)
+    t[i >> 8][i & 255] = c_crc_tab[i >> 8][i & 255];
+  __syncthreads();
+  uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const uint8_t *p = data + off[b];
+  uint32_t l = len[b];
+  uint32_t c = 0xffffffffu;
+  while (l && ((uintptr_t)p & 7)) {
+    c = t[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+    l--;
+  }
+  while (l >= 8) {
+    uint64_t w = *(const uint64_t *)p;
+    uint32_t lo = (uint32_t)w ^ c, hi = (uint32_t)(w >> 32);
+    c = t[7][lo & 0xff] ^ t[6][(lo >> 8) & 0xff] ^ t[5][(lo >> 16) & 0xff] ^
+        t[4][lo >> 24] ^ t[3][hi & 0xff] ^ t[2][(hi >> 8) & 0xff] ^
+        t[1][(hi >> 16) & 0xff] ^ t[0][hi >> 24];
+    p += 8;
+    l -= 8;
+  }
+  while (l--) c = t[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+  crc[b] = c ^ 0xffffffffu;
+}
+
+static int crc_tab_ready = 0;
+
+extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
+                                    size_t data_len, const uint64_t *off,
+                                    const uint32_t *len, size_t n,
+                                    uint32_t *crc) {
+  if (!e) return DRB_EINVAL;
+  if (!n) return DRB_OK;
+  for (size_t i = 0; i < n; ++i)
+    if (off[i] + len[i] > data_len) return DRB_ERANGE;
+  if (!crc_tab_ready) {
+    uint32_t tab[8][256];
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tab[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s)
+        tab[s][i] = tab[0][tab[s - 1][i] & 0xff] ^ (tab[s - 1][i] >> 8);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
+    crc_tab_ready = 1;
+  }
+  size_t bytes = ((data_len + 15) & ~15ull) + n * 8 + ((n * 4 + 15) & ~15ull) * 2;
+  void *s;
+  if (scratch(e, bytes + 64, &s)) return DRB_EDEVICE;
+  uint8_t *dd = (uint8_t *)s;
+  uint64_t *doff = (uint64_t *)(dd + ((data_len + 15) & ~15ull));
+  uint32_t *dlen = (uint32_t *)(doff + n);
+  uint32_t *dcrc = dlen + ((n + 3) & ~3ull);
+  HIPCHK(hipMemcpyAsync(dd, data, data_len, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(doff, off, n * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(dlen, len, n * 4, hipMemcpyHostToDevice, e->stream));
+  k_crc32<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(dd, doff, dlen,
+                                                               dcrc, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(crc, dcrc, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}

@@ -1,0 +1,154 @@
+// drb_layout.hpp -- HBM layout of the engine (structure-of-arrays).
+//
+// Every per-replica array is indexed [slot][group]: lanes of a wavefront
+// step 64 consecutive groups of the SAME replica slot, so each field load
+// is one coalesced 512 B (u64) or 1 KiB (uint4) access and every wave is
+// role-homogeneous (all leaders or all followers) -- no divergence on the
+// steady-state path.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace drb {
+
+// per-replica u64 fields (drb_replica_state order), array [F][slot][g]
+enum U64Field : int {
+  F_TERM = 0,
+  F_VOTE,
+  F_LEADER_ID,
+  F_APPLIED,
+  F_ELECTION_TICK,
+  F_HEARTBEAT_TICK,
+  F_RAND_TIMEOUT,
+  F_TICK_COUNT,
+  F_COMMITTED,
+  F_PROCESSED,
+  F_LAST_INDEX,
+  F_MARKER_INDEX,
+  F_SAVED_TO,
+  F_APPLIED_TO_INDEX,
+  F_APPLIED_TO_TERM,
+  F_APPLIED_INDEX,
+  F_CONFIRMED_INDEX,
+  F_PUSHED_INDEX,
+  F_PREV_TERM,
+  F_PREV_VOTE,
+  F_PREV_COMMIT,
+  F_SM_INDEX,
+  F_SM_TERM,
+  F_KV_COUNT,
+  F_RING_LO,     // lowest index still resident in the window (internal)
+  F_RING_GUARD,  // lowest index referenced by last round's Replicates
+  NUM_U64
+};
+
+// per-replica u32 fields, array [F][slot][g]
+enum U32Field : int { W_ROLE = 0, W_FLAGS, W_FB_REASON, W_RI_COUNT, NUM_U32 };
+
+// message record: 4 x uint4 = 64 B, chunks written only as the type needs
+//   c0 = {meta u32 (type | reject<<8 | n_entries<<16), 0, term u64}
+//   c1 = {log_index, log_term}
+//   c2 = {commit, hint}
+//   c3 = {hint_high, 0}
+constexpr int MSG_CHUNKS = 4;
+// entry meta in the ring: 3 x uint4 = 48 B (+ cmd_cap bytes of Cmd)
+//   m0 = {term, key}  m1 = {client_id, series_id}
+//   m2 = {responded_to, type u32 | cmd_len u32 << 32}
+constexpr int ENT_META = 3;
+// staged proposal: 3 x uint4 + cmd chunks
+//   p0 = {key, client_id} p1 = {series_id, responded_to}
+//   p2 = {type | cmd_len << 32, 0}
+constexpr int PROP_META = 3;
+constexpr int RTR_CAP = 8;  // ReadyToRead records per replica per round
+
+struct View {
+  uint64_t G;      // groups
+  uint32_t R;      // replicas
+  uint32_t W;      // window entries (pow2)
+  uint32_t C16;    // cmd chunks of 16 B
+  uint32_t MB;     // mailbox messages per (sender, receiver)
+  uint32_t KS;     // kv slots per replica (pow2)
+  uint32_t KVW;    // kv slot stride in uint4 units
+  uint32_t kv_val_cap;
+  uint32_t max_props;
+  uint32_t election_rtt, heartbeat_rtt, check_quorum;
+  uint32_t pad0;
+  uint64_t first_shard_id;
+
+  uint64_t *u64;          // [NUM_U64][R][G]
+  uint32_t *u32;          // [NUM_U32][R][G]
+  uint64_t *rem_match;    // [R(self)][R(peer)][G]
+  uint64_t *rem_next;     // [R][R][G]
+  uint32_t *rem_state;    // [R][R][G]
+  uint32_t *rem_active;   // [R][R][G]
+  uint4 *ri_ctx;          // [R][D][G] {low, high}
+  uint4 *ri_idx;          // [R][D][G] {index, from}
+  uint32_t *ri_conf;      // [R][D][G]
+  uint4 *ring;            // [R][W][ENT_META + C16][G]
+  uint4 *mbox;            // [2][R*R][MB][MSG_CHUNKS][G]
+  uint64_t *mbox_meta;    // [2][R][G] (tag << 32 | 4-bit counts per dest)
+  uint4 *kv;              // [R][G][KS][KVW]
+  uint4 *props;           // [P][max_props][PROP_META + C16][G]
+  uint32_t *prop_count;   // [P][G]
+  uint4 *ri_in;           // [RS][G] {low, high}
+  uint4 *rtr;             // [R][RTR_CAP][G] x 2 chunks {index, low},{high,0}
+  uint32_t *rtr_count;    // [R][G]
+  unsigned long long *counters;  // [8] (drb_round_out order from index 1)
+};
+
+__host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,
+                                       uint64_t g) {
+  return (uint64_t)slot * v.G + g;
+}
+__host__ __device__ inline uint64_t u64_ix(const View &v, int f,
+                                           uint32_t slot, uint64_t g) {
+  return ((uint64_t)f * v.R + slot) * v.G + g;
+}
+__host__ __device__ inline uint64_t u32_ix(const View &v, int f,
+                                           uint32_t slot, uint64_t g) {
+  return ((uint64_t)f * v.R + slot) * v.G + g;
+}
+__host__ __device__ inline uint64_t rem_ix(const View &v, uint32_t self,
+                                           uint32_t peer, uint64_t g) {
+  return ((uint64_t)self * v.R + peer) * v.G + g;
+}
+__host__ __device__ inline uint64_t ri_ix(const View &v, uint32_t slot,
+                                          uint32_t d, uint64_t g) {
+  return ((uint64_t)slot * 4 /*DRB_RI_DEPTH*/ + d) * v.G + g;
+}
+__host__ __device__ inline uint64_t ring_ix(const View &v, uint32_t slot,
+                                            uint64_t index, uint32_t chunk,
+                                            uint64_t g) {
+  uint64_t rs = index & (v.W - 1);
+  return (((uint64_t)slot * v.W + rs) * (ENT_META + v.C16) + chunk) * v.G + g;
+}
+__host__ __device__ inline uint64_t mbox_ix(const View &v, uint32_t buf,
+                                            uint32_t from, uint32_t to,
+                                            uint32_t k, uint32_t chunk,
+                                            uint64_t g) {
+  uint64_t pair = (uint64_t)from * v.R + to;
+  return ((((uint64_t)buf * v.R * v.R + pair) * v.MB + k) * MSG_CHUNKS +
+          chunk) * v.G + g;
+}
+__host__ __device__ inline uint64_t mmeta_ix(const View &v, uint32_t buf,
+                                             uint32_t from, uint64_t g) {
+  return ((uint64_t)buf * v.R + from) * v.G + g;
+}
+__host__ __device__ inline uint64_t kv_ix(const View &v, uint32_t slot,
+                                          uint64_t g, uint32_t ks) {
+  return (((uint64_t)slot * v.G + g) * v.KS + ks) * v.KVW;
+}
+__host__ __device__ inline uint64_t prop_ix(const View &v, uint32_t ps,
+                                            uint32_t j, uint32_t chunk,
+                                            uint64_t g) {
+  return (((uint64_t)ps * v.max_props + j) * (PROP_META + v.C16) + chunk) *
+             v.G + g;
+}
+__host__ __device__ inline uint64_t rtr_ix(const View &v, uint32_t slot,
+                                           uint32_t k, uint32_t chunk,
+                                           uint64_t g) {
+  return (((uint64_t)slot * RTR_CAP + k) * 2 + chunk) * v.G + g;
+}
+
+}  // namespace drb

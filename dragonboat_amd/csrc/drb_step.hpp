@@ -1,0 +1,1279 @@
+// drb_step.hpp -- the fused step-round kernel.
+//
+// One lane = one replica (slot, group).  A round is one iteration of
+// dragonboat's step loop (node_test.go:274-353, engine.go:1304-1364) for
+// that replica: handleEvents (node.go:1161-1223) -> getUpdate
+// (node.go:1025) -> apply (rsm StateMachine.Handle) -> Peer.Commit
+// (peer.go:292).  Messages emitted in round t land in the mailbox buffer
+// t&1 and are consumed in round t+1 -- exactly the delivery of the
+// reference step loop, where all sends happen after every node has handled
+// its events.  Inbox order = Replicate messages by sender slot, then all
+// other messages by sender slot (node_test.go:311-339), then the LocalTick.
+//
+// The lane first runs a read-only pre-pass over its inbox and inputs; if
+// the round would leave the fast path (term change, election, lost quorum,
+// unsupported message/entry, capacity) it marks the replica
+// DRB_F_FALLBACK and returns WITHOUT mutating anything.
+#pragma once
+#include "../../include/drb_engine.h"
+#include "drb_layout.hpp"
+
+namespace drb {
+
+#define DRB_DEV __device__ __forceinline__
+
+constexpr uint64_t MAX_ENTRY_SIZE = 64ull * 1024 * 1024;  // soft.go:186
+
+// counters[] slots
+enum : int {
+  C_COMMITTED = 0,
+  C_APPLIED,
+  C_MESSAGES,
+  C_RTR,
+  C_DROPPED_RI,
+  C_FALLBACKS,
+  C_ERRORS,
+  C_ROUNDS,
+  NUM_COUNTERS
+};
+
+template <int R>
+struct Rep {
+  // raft / entryLog / inMemory / node / rsm state
+  uint64_t term, vote, leader_id, applied, election_tick, heartbeat_tick;
+  uint64_t rand_timeout, tick_count, committed, processed, last, marker;
+  uint64_t saved_to, applied_to_index, applied_to_term, applied_index;
+  uint64_t confirmed_index, pushed_index, prev_term, prev_vote, prev_commit;
+  uint64_t sm_index, sm_term, kv_count, ring_lo, ring_guard;
+  uint32_t role, flags, fb, ri_count;
+  // leader remotes live in LDS (RemLds), see rem_get/rem_put
+  // leader: readIndex queue
+  uint64_t ri_lo[DRB_RI_DEPTH], ri_hi[DRB_RI_DEPTH], ri_ix[DRB_RI_DEPTH],
+      ri_fr[DRB_RI_DEPTH];
+  uint32_t ri_cf[DRB_RI_DEPTH];
+  // round-local
+  uint32_t out_cnt;   // 4-bit message count per destination slot
+  uint32_t nmsgs;
+  uint32_t nrtr;
+  uint32_t ndropped_ri;
+  uint64_t guard_new;
+  bool leader_update;
+  bool err;
+};
+
+// Per-lane remote progress table in LDS, [peer][lane]: dynamically
+// indexed by the sender slot without spilling to scratch, and conflict-free
+// (consecutive lanes hit consecutive banks).
+template <int R>
+struct RemLds {
+  uint64_t m[R][256];
+  uint64_t n[R][256];
+  uint32_t st[R][256];
+  uint32_t a[R][256];
+};
+
+struct Lane {
+  void *rl;       // RemLds<R> of this workgroup
+  uint32_t tid;   // lane within the workgroup
+  const View *v;
+  uint32_t slot;
+  uint64_t g;
+  uint32_t rbuf, wbuf;
+  uint64_t round;
+};
+
+// ------------------------------------------------------------ helpers
+DRB_DEV uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+DRB_DEV uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+DRB_DEV uint64_t lo64(uint4 q) { return (uint64_t)q.x | ((uint64_t)q.y << 32); }
+DRB_DEV uint64_t hi64(uint4 q) { return (uint64_t)q.z | ((uint64_t)q.w << 32); }
+
+template <int R>
+DRB_DEV void set_error(Rep<R> &r, uint32_t reason) {
+  if (!r.err) {
+    r.err = true;
+    r.fb = reason;
+  }
+}
+
+// entry term at index (entryLog.term, logentry.go:142-155) from the
+// resident window
+template <int R>
+DRB_DEV uint64_t log_term(const Lane &L, Rep<R> &r, uint64_t index) {
+  if (index == 0 || index > r.last) return 0;  // first-1 == 0 on this path
+  if (index < r.ring_lo) {
+    set_error(r, DRB_ERR_LOG_RANGE);
+    return 0;
+  }
+  uint4 q = L.v->ring[ring_ix(*L.v, L.slot, index, 0, L.g)];
+  return (uint64_t)q.x | ((uint64_t)q.y << 32);
+}
+DRB_DEV uint4 mk4(uint64_t a, uint64_t b) {
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b,
+                    (uint32_t)(b >> 32));
+}
+
+template <int R>
+DRB_DEV uint64_t ring_term(const Lane &L, uint32_t slot, uint64_t index) {
+  return lo64(L.v->ring[ring_ix(*L.v, slot, index, 0, L.g)]);
+}
+
+// ------------------------------------------------------------ messages
+struct Msg {
+  uint32_t type, reject, n;
+  uint64_t term, log_index, log_term, commit, hint, hint_high;
+};
+
+__host__ __device__ inline uint32_t msg_meta(uint32_t type, uint32_t reject,
+                                             uint32_t n) {
+  return type | (reject << 8) | (n << 16);
+}
+
+// send (raft.go:683-687): From = self, Term = r.term for non-request types
+template <int R>
+DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
+  const View &v = *L.v;
+  uint32_t k = (r.out_cnt >> (4 * to_slot)) & 15u;
+  if (k >= v.MB) {  // bounded by the pre-pass; never expected
+    set_error(r, DRB_FB_CAPACITY);
+    return;
+  }
+  r.out_cnt += 1u << (4 * to_slot);
+  r.nmsgs++;
+  uint64_t term = (m.type == DRB_MSG_READ_INDEX) ? 0 : r.term;
+  v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] =
+      make_uint4(msg_meta(m.type, m.reject, m.n), 0, (uint32_t)term,
+                 (uint32_t)(term >> 32));
+  switch (m.type) {
+    case DRB_MSG_REPLICATE:
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] =
+          mk4(m.log_index, m.log_term);
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] =
+          mk4(m.commit, 0);
+      break;
+    case DRB_MSG_REPLICATE_RESP:
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] =
+          mk4(m.log_index, 0);
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] = mk4(0, m.hint);
+      break;
+    case DRB_MSG_HEARTBEAT:
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] =
+          mk4(m.commit, m.hint);
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 3, L.g)] =
+          mk4(m.hint_high, 0);
+      break;
+    case DRB_MSG_HEARTBEAT_RESP:
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] = mk4(0, m.hint);
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 3, L.g)] =
+          mk4(m.hint_high, 0);
+      break;
+    default:  // ReadIndexResp / ReadIndex: every field
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] =
+          mk4(m.log_index, m.log_term);
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] =
+          mk4(m.commit, m.hint);
+      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 3, L.g)] =
+          mk4(m.hint_high, 0);
+      break;
+  }
+}
+
+DRB_DEV Msg read_msg(const Lane &L, uint32_t from, uint32_t k) {
+  const View &v = *L.v;
+  Msg m;
+  uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 0, L.g)];
+  m.type = c0.x & 0xffu;
+  m.reject = (c0.x >> 8) & 1u;
+  m.n = c0.x >> 16;
+  m.term = hi64(c0);
+  m.log_index = m.log_term = m.commit = m.hint = m.hint_high = 0;
+  switch (m.type) {
+    case DRB_MSG_REPLICATE: {
+      uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
+      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
+      m.log_index = lo64(c1);
+      m.log_term = hi64(c1);
+      m.commit = lo64(c2);
+      break;
+    }
+    case DRB_MSG_REPLICATE_RESP: {
+      uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
+      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
+      m.log_index = lo64(c1);
+      m.hint = hi64(c2);
+      break;
+    }
+    case DRB_MSG_HEARTBEAT:
+    case DRB_MSG_HEARTBEAT_RESP: {
+      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
+      uint4 c3 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 3, L.g)];
+      m.commit = lo64(c2);
+      m.hint = hi64(c2);
+      m.hint_high = lo64(c3);
+      break;
+    }
+    default: {
+      uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
+      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
+      uint4 c3 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 3, L.g)];
+      m.log_index = lo64(c1);
+      m.log_term = hi64(c1);
+      m.commit = lo64(c2);
+      m.hint = hi64(c2);
+      m.hint_high = lo64(c3);
+      break;
+    }
+  }
+  return m;
+}
+
+// ------------------------------------------------------------ remote FSM
+// The remotes live in registers; a runtime slot index selects through a
+// short chain of v_cndmask instead of indexing an array (which would put
+// the whole array in scratch memory).
+struct RemoteV {
+  uint64_t m, n;
+  uint32_t st, a;
+};
+
+template <int R>
+DRB_DEV RemLds<R> &rl_of(const Lane &L) {
+  return *(RemLds<R> *)L.rl;
+}
+
+template <int R>
+DRB_DEV RemoteV rem_get(const Lane &L, int s) {
+  RemLds<R> &t = rl_of<R>(L);
+  return RemoteV{t.m[s][L.tid], t.n[s][L.tid], t.st[s][L.tid],
+                 t.a[s][L.tid]};
+}
+
+template <int R>
+DRB_DEV void rem_put(const Lane &L, int s, const RemoteV &x) {
+  RemLds<R> &t = rl_of<R>(L);
+  t.m[s][L.tid] = x.m;
+  t.n[s][L.tid] = x.n;
+  t.st[s][L.tid] = x.st;
+  t.a[s][L.tid] = x.a;
+}
+
+// remote.go:103-213 on a local copy
+DRB_DEV void rv_wait_to_retry(RemoteV &x) {
+  if (x.st == DRB_REMOTE_WAIT) x.st = DRB_REMOTE_RETRY;
+}
+DRB_DEV bool rv_is_paused(const RemoteV &x) {
+  return x.st == DRB_REMOTE_WAIT || x.st == DRB_REMOTE_SNAPSHOT;
+}
+DRB_DEV bool rv_try_update(RemoteV &x, uint64_t index) {
+  if (x.n < index + 1) x.n = index + 1;
+  if (x.m < index) {
+    rv_wait_to_retry(x);
+    x.m = index;
+    return true;
+  }
+  return false;
+}
+
+template <int R>
+DRB_DEV bool rem_try_update(const Lane &L, int s, uint64_t index) {
+  RemoteV x = rem_get<R>(L, s);
+  bool u = rv_try_update(x, index);
+  rem_put<R>(L, s, x);
+  return u;
+}
+
+// ------------------------------------------------------------ log
+// commitTo (logentry.go:336-349)
+template <int R>
+DRB_DEV void commit_to(Rep<R> &r, uint64_t index) {
+  if (index <= r.committed) return;
+  if (index > r.last) {
+    set_error(r, DRB_ERR_COMMIT);
+    return;
+  }
+  r.committed = index;
+}
+
+// sendReplicateMessage (raft.go:787-819) + makeReplicateMessage (738-769)
+template <int R>
+DRB_DEV void send_replicate(const Lane &L, Rep<R> &r, int to) {
+  RemoteV x = rem_get<R>(L, to);
+  if (rv_is_paused(x)) return;
+  const uint64_t next = x.n;
+  Msg m = {};
+  m.type = DRB_MSG_REPLICATE;
+  m.log_index = next - 1;
+  m.log_term = log_term(L, r, next - 1);
+  m.commit = r.committed;
+  // entries(next, maxEntrySize): [next, last]; limitSize never binds in the
+  // resident window (W * (128 + cmd_cap) < 64 MiB, checked at create)
+  uint64_t n = next <= r.last ? r.last - next + 1 : 0;
+  if (n > 0) {
+    if (next < r.ring_lo) {  // would come from LogDB (logentry.go:180-195)
+      set_error(r, DRB_ERR_LOG_RANGE);
+      return;
+    }
+    m.n = (uint32_t)n;
+    r.guard_new = umin64(r.guard_new, next);
+    // remote.progress (remote.go:159-168)
+    if (x.st == DRB_REMOTE_REPLICATE)
+      x.n = r.last + 1;
+    else if (x.st == DRB_REMOTE_RETRY)
+      x.st = DRB_REMOTE_WAIT;
+    rem_put<R>(L, to, x);
+  }
+  emit(L, r, to, m);
+}
+
+// broadcastReplicateMessage (raft.go:821-833)
+template <int R>
+DRB_DEV void broadcast_replicate(const Lane &L, Rep<R> &r) {
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if ((uint32_t)s != L.slot) send_replicate(L, r, s);
+}
+
+// broadcastHeartbeatMessageWithHint (raft.go:859-871) + sendHeartbeat
+template <int R>
+DRB_DEV void broadcast_heartbeat_hint(const Lane &L, Rep<R> &r, uint64_t lo,
+                                      uint64_t hi) {
+#pragma unroll
+  for (int s = 0; s < R; ++s) {
+    if ((uint32_t)s == L.slot) continue;
+    Msg m = {};
+    m.type = DRB_MSG_HEARTBEAT;
+    m.commit = umin64(rem_get<R>(L, s).m, r.committed);
+    m.hint = lo;
+    m.hint_high = hi;
+    emit(L, r, s, m);
+  }
+}
+
+// broadcastHeartbeatMessage (raft.go:849-857)
+template <int R>
+DRB_DEV void broadcast_heartbeat(const Lane &L, Rep<R> &r) {
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if ((uint32_t)d + 1 == r.ri_count) {  // peepCtx: last queued
+      lo = r.ri_lo[d];
+      hi = r.ri_hi[d];
+    }
+  broadcast_heartbeat_hint(L, r, lo, hi);
+}
+
+// sortMatchValues + tryCommit (raft.go:884-942): quorum-th largest match
+template <int R>
+DRB_DEV bool try_commit(const Lane &L, Rep<R> &r) {
+  uint64_t m[R];
+#pragma unroll
+  for (int s = 0; s < R; ++s) m[s] = rl_of<R>(L).m[s][L.tid];
+  // sorting network (odd-even transposition), ascending
+#pragma unroll
+  for (int p = 0; p < R; ++p)
+#pragma unroll
+    for (int i = (p & 1); i + 1 < R; i += 2) {
+      uint64_t a = m[i], b = m[i + 1];
+      m[i] = umin64(a, b);
+      m[i + 1] = umax64(a, b);
+    }
+  constexpr int quorum = R / 2 + 1;
+  uint64_t q = m[R - quorum];
+  // entryLog.tryCommit (logentry.go:395-410)
+  if (q <= r.committed) return false;
+  uint64_t lterm = log_term(L, r, q);
+  if (lterm == r.term) {
+    commit_to(r, q);
+    return true;
+  }
+  return false;
+}
+
+// addReadyToRead (raft.go:1833-1839): written straight to the round output
+template <int R>
+DRB_DEV void add_ready(const Lane &L, Rep<R> &r, uint64_t index, uint64_t lo,
+                       uint64_t hi) {
+  const View &v = *L.v;
+  if (r.nrtr >= RTR_CAP) {
+    set_error(r, DRB_FB_CAPACITY);
+    return;
+  }
+  v.rtr[rtr_ix(v, L.slot, r.nrtr, 0, L.g)] = mk4(index, lo);
+  v.rtr[rtr_ix(v, L.slot, r.nrtr, 1, L.g)] = mk4(hi, 0);
+  r.nrtr++;
+}
+
+// readIndex.addRequest (readindex.go:43-66)
+template <int R>
+DRB_DEV void ri_add_request(Rep<R> &r, uint64_t index, uint64_t lo,
+                            uint64_t hi, uint64_t from) {
+  bool found = false;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if ((uint32_t)d < r.ri_count && r.ri_lo[d] == lo && r.ri_hi[d] == hi)
+      found = true;
+  if (found) return;
+  uint64_t tail_index = 0;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if ((uint32_t)d + 1 == r.ri_count) tail_index = r.ri_ix[d];
+  if (r.ri_count > 0 && index < tail_index) {
+    set_error(r, DRB_ERR_READINDEX);
+    return;
+  }
+  if (r.ri_count >= DRB_RI_DEPTH) {  // excluded by the pre-pass
+    set_error(r, DRB_FB_CAPACITY);
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if ((uint32_t)d == r.ri_count) {
+      r.ri_lo[d] = lo;
+      r.ri_hi[d] = hi;
+      r.ri_ix[d] = index;
+      r.ri_fr[d] = from;
+      r.ri_cf[d] = 0;
+    }
+  r.ri_count++;
+}
+
+// handleReadIndexLeaderConfirmation (raft.go:1955-1974) +
+// readIndex.confirm (readindex.go:77-115)
+template <int R>
+DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
+                        uint32_t from_slot) {
+  int pos = -1;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if (pos < 0 && (uint32_t)d < r.ri_count && r.ri_lo[d] == lo &&
+        r.ri_hi[d] == hi)
+      pos = d;
+  if (pos < 0) return;
+  uint32_t cf = 0;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if (d == pos) {
+      r.ri_cf[d] |= 1u << from_slot;
+      cf = r.ri_cf[d];
+    }
+  constexpr int quorum = R / 2 + 1;
+  if ((int)__builtin_popcount(cf) + 1 < quorum) return;
+  uint64_t sidx = 0;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d)
+    if (d == pos) sidx = r.ri_ix[d];
+  // release queue[0..pos], each with index rewritten to sidx
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d) {
+    if (d > pos) continue;
+    if (r.ri_ix[d] > sidx) set_error(r, DRB_ERR_READINDEX);
+    uint64_t fr = r.ri_fr[d];
+    if (fr == 0 || fr == (uint64_t)L.slot + 1) {
+      add_ready(L, r, sidx, r.ri_lo[d], r.ri_hi[d]);
+    } else {
+      Msg m = {};
+      m.type = DRB_MSG_READ_INDEX_RESP;
+      m.log_index = sidx;
+      m.hint = lo;  // the confirming ctx (raft.go:1966-1970)
+      m.hint_high = hi;
+      emit(L, r, (uint32_t)(fr - 1), m);
+    }
+  }
+  // shift the remaining queue down by pos+1
+  uint32_t done = (uint32_t)pos + 1;
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d) {
+    uint64_t nl = 0, nh = 0, ni = 0, nf = 0;
+    uint32_t nc = 0;
+#pragma unroll
+    for (int e = 0; e < DRB_RI_DEPTH; ++e)
+      if ((uint32_t)e == (uint32_t)d + done) {
+        nl = r.ri_lo[e];
+        nh = r.ri_hi[e];
+        ni = r.ri_ix[e];
+        nf = r.ri_fr[e];
+        nc = r.ri_cf[e];
+      }
+    r.ri_lo[d] = nl;
+    r.ri_hi[d] = nh;
+    r.ri_ix[d] = ni;
+    r.ri_fr[d] = nf;
+    r.ri_cf[d] = nc;
+  }
+  r.ri_count -= done;
+}
+
+// ------------------------------------------------------------ handlers
+// handleLeaderReplicateResp (raft.go:1878-1908), via lw (2309-2323)
+template <int R>
+DRB_DEV void leader_replicate_resp(const Lane &L, Rep<R> &r, int s,
+                                   const Msg &m) {
+  RemoteV x = rem_get<R>(L, s);
+  x.a = 1;  // setActive
+  if (!m.reject) {
+    bool paused = rv_is_paused(x);
+    bool upd = rv_try_update(x, m.log_index);
+    if (upd && x.st == DRB_REMOTE_RETRY) {  // respondedTo (remote.go:170)
+      x.n = x.m + 1;                        // becomeReplicate
+      x.st = DRB_REMOTE_REPLICATE;
+    }
+    rem_put<R>(L, s, x);
+    if (upd) {
+      if (try_commit(L, r))
+        broadcast_replicate(L, r);
+      else if (paused)
+        send_replicate(L, r, s);
+    }
+  } else {
+    // decreaseTo (remote.go:182-198)
+    bool dec = false;
+    if (x.st == DRB_REMOTE_REPLICATE) {
+      if (m.log_index > x.m) {
+        x.n = x.m + 1;
+        dec = true;
+      }
+    } else if (x.n - 1 == m.log_index) {
+      rv_wait_to_retry(x);
+      x.n = umax64(1, umin64(m.log_index, m.hint + 1));
+      dec = true;
+    }
+    if (dec && x.st == DRB_REMOTE_REPLICATE) {
+      // enterRetryState (raft.go:2013-2017): becomeRetry
+      x.n = x.m + 1;
+      x.st = DRB_REMOTE_RETRY;
+    }
+    rem_put<R>(L, s, x);
+    if (dec) send_replicate(L, r, s);
+  }
+}
+
+// handleLeaderHeartbeatResp (raft.go:1910-1923)
+template <int R>
+DRB_DEV void leader_heartbeat_resp(const Lane &L, Rep<R> &r, int s,
+                                   const Msg &m) {
+  RemoteV x = rem_get<R>(L, s);
+  x.a = 1;
+  rv_wait_to_retry(x);
+  rem_put<R>(L, s, x);
+  if (x.m < r.last) send_replicate(L, r, s);
+  if (m.hint != 0) ri_confirm(L, r, m.hint, m.hint_high, (uint32_t)s);
+}
+
+// hasCommittedEntryAtCurrentTerm (raft.go:1818-1827)
+template <int R>
+DRB_DEV bool committed_at_term(const Lane &L, Rep<R> &r) {
+  return log_term(L, r, r.committed) == r.term;
+}
+
+// handleLeaderReadIndex (raft.go:1842-1876)
+template <int R>
+DRB_DEV void leader_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
+                               uint64_t hi, uint64_t from) {
+  if (R > 1) {
+    if (!committed_at_term(L, r)) {
+      r.ndropped_ri++;  // reportDroppedReadIndex
+      return;
+    }
+    ri_add_request(r, r.committed, lo, hi, from);
+    broadcast_heartbeat_hint(L, r, lo, hi);
+  } else {
+    add_ready(L, r, r.committed, lo, hi);
+  }
+}
+
+// handleFollowerReplicate (raft.go:2122) -> handleReplicateMessage
+// (raft.go:1444-1484) -> tryAppend (logentry.go:296-310) -> merge
+// (inmemory.go:199-230)
+template <int R>
+DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
+                                const Msg &m) {
+  const View &v = *L.v;
+  r.election_tick = 0;  // leaderIsAvailable
+  r.leader_id = (uint64_t)s + 1;
+  r.leader_update = true;
+  Msg resp = {};
+  resp.type = DRB_MSG_REPLICATE_RESP;
+  if (m.log_index < r.committed) {
+    resp.log_index = r.committed;
+    emit(L, r, s, resp);
+    return;
+  }
+  if (log_term(L, r, m.log_index) == m.log_term) {
+    // getConflictIndex: first entry whose term differs
+    uint64_t ci = 0;
+    for (uint32_t i = 0; i < m.n; ++i) {
+      uint64_t idx = m.log_index + 1 + i;
+      uint64_t et = ring_term<R>(L, (uint32_t)s, idx);
+      if (log_term(L, r, idx) != et) {
+        ci = idx;
+        break;
+      }
+    }
+    if (ci != 0) {
+      if (ci <= r.committed) {
+        set_error(r, DRB_ERR_CONFLICT);
+        return;
+      }
+      uint64_t new_last = m.log_index + m.n;
+      uint64_t first_term = ring_term<R>(L, (uint32_t)s, ci);
+      bool inmem_nonempty = r.last >= r.marker;
+      if (ci == r.marker + (inmem_nonempty ? r.last - r.marker + 1 : 0)) {
+        // append at the end: checkEntriesToAppend(existing, ents)
+        if (inmem_nonempty && log_term(L, r, r.last) > first_term)
+          set_error(r, DRB_ERR_APPEND);
+      } else if (ci <= r.marker) {
+        r.marker = ci;
+        r.saved_to = ci - 1;
+      } else {
+        // keep [marker, ci) then append
+        if (ci - 1 > r.last) {
+          set_error(r, DRB_ERR_APPEND);
+          return;
+        }
+        if (log_term(L, r, ci - 1) > first_term)
+          set_error(r, DRB_ERR_APPEND);
+        r.saved_to = umin64(r.saved_to, ci - 1);
+      }
+      // copy entries [ci, new_last] from the leader's window
+      const uint32_t chunks = ENT_META + v.C16;
+      for (uint64_t idx = ci; idx <= new_last; ++idx) {
+        for (uint32_t c = 0; c < chunks; ++c)
+          v.ring[ring_ix(v, L.slot, idx, c, L.g)] =
+              v.ring[ring_ix(v, (uint32_t)s, idx, c, L.g)];
+      }
+      r.last = new_last;
+      if (new_last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, new_last + 1 - v.W);
+    }
+    uint64_t last_idx = m.log_index + m.n;
+    commit_to(r, umin64(last_idx, m.commit));
+    resp.log_index = last_idx;
+  } else {
+    resp.reject = 1;
+    resp.log_index = m.log_index;
+    resp.hint = r.last;
+  }
+  emit(L, r, s, resp);
+}
+
+// handleFollowerHeartbeat (raft.go:2128) -> handleHeartbeatMessage (1400)
+template <int R>
+DRB_DEV void follower_heartbeat(const Lane &L, Rep<R> &r, int s,
+                                const Msg &m) {
+  r.election_tick = 0;
+  r.leader_id = (uint64_t)s + 1;
+  r.leader_update = true;
+  commit_to(r, m.commit);
+  Msg resp = {};
+  resp.type = DRB_MSG_HEARTBEAT_RESP;
+  resp.hint = m.hint;
+  resp.hint_high = m.hint_high;
+  emit(L, r, s, resp);
+}
+
+// handleFollowerReadIndexResp (raft.go:2155-2164)
+template <int R>
+DRB_DEV void follower_read_index_resp(const Lane &L, Rep<R> &r, int s,
+                                      const Msg &m) {
+  r.election_tick = 0;
+  r.leader_id = (uint64_t)s + 1;
+  r.leader_update = true;
+  add_ready(L, r, m.log_index, m.hint, m.hint_high);
+}
+
+template <int R>
+DRB_DEV void dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m) {
+  if (r.role == DRB_LEADER) {
+    if (m.type == DRB_MSG_REPLICATE_RESP)
+      leader_replicate_resp(L, r, s, m);
+    else if (m.type == DRB_MSG_HEARTBEAT_RESP)
+      leader_heartbeat_resp(L, r, s, m);
+    else if (m.type == DRB_MSG_READ_INDEX)
+      leader_read_index(L, r, m.hint, m.hint_high, (uint64_t)s + 1);
+  } else {
+    if (m.type == DRB_MSG_REPLICATE)
+      follower_replicate(L, r, s, m);
+    else if (m.type == DRB_MSG_HEARTBEAT)
+      follower_heartbeat(L, r, s, m);
+    else if (m.type == DRB_MSG_READ_INDEX_RESP)
+      follower_read_index_resp(L, r, s, m);
+  }
+}
+
+// ------------------------------------------------------------ apply
+// FNV-1a over the key bytes, for the open-addressing slot
+DRB_DEV uint64_t kv_hash(uint64_t key8, uint32_t klen) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint32_t i = 0; i < klen; ++i)
+    h = (h ^ ((key8 >> (8 * i)) & 0xff)) * 0x100000001b3ull;
+  return h ^ (h >> 29);
+}
+
+// the Cmd staged in four registers-quads (no dynamically indexed arrays:
+// those would be placed in scratch memory)
+struct Cmd4 {
+  uint4 c0, c1, c2, c3;
+};
+
+DRB_DEV uint8_t chunk_byte(const Cmd4 &c, uint32_t i) {
+  const uint32_t qi = i >> 4;
+  const uint4 q = qi == 0 ? c.c0 : qi == 1 ? c.c1 : qi == 2 ? c.c2 : c.c3;
+  uint32_t w = (i >> 2) & 3;
+  uint32_t word = w == 0 ? q.x : w == 1 ? q.y : w == 2 ? q.z : q.w;
+  return (uint8_t)(word >> (8 * (i & 3)));
+}
+
+// handleEntry (statemachine.go:935-969) -> update (1057-1103) ->
+// GetPayload (encoded.go:55-65) -> KVTest.Update (kvtest.go:145-162).
+// Returns: 0 noop applied, 1 KV updated, -1 not on the fast path.
+template <int R>
+DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
+  const View &v = *L.v;
+  uint4 m0 = v.ring[ring_ix(v, L.slot, index, 0, L.g)];
+  uint4 m1 = v.ring[ring_ix(v, L.slot, index, 1, L.g)];
+  uint4 m2 = v.ring[ring_ix(v, L.slot, index, 2, L.g)];
+  uint64_t term = lo64(m0);
+  uint64_t client_id = lo64(m1), series_id = hi64(m1);
+  uint32_t type = m2.z, clen = m2.w;
+  if (type == DRB_ENTRY_CONFIG_CHANGE) return -1;
+  if (client_id == 0) {  // not session managed
+    if (clen != 0) return -1;  // reference panics
+    r.sm_index = index;
+    r.sm_term = term;
+    return 0;
+  }
+  if (series_id != 0) return -1;  // sessions stay on the CPU path
+  // the Cmd, staged in registers (cmd_cap <= 64 B on this path: C16 <= 4)
+  Cmd4 cmd;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  cmd.c0 = v.ring[ring_ix(v, L.slot, index, ENT_META, L.g)];
+  cmd.c1 = v.C16 > 1 ? v.ring[ring_ix(v, L.slot, index, ENT_META + 1, L.g)]
+                     : z4;
+  cmd.c2 = v.C16 > 2 ? v.ring[ring_ix(v, L.slot, index, ENT_META + 2, L.g)]
+                     : z4;
+  cmd.c3 = v.C16 > 3 ? v.ring[ring_ix(v, L.slot, index, ENT_META + 3, L.g)]
+                     : z4;
+  uint32_t off = 0, plen = clen;
+  if (type == DRB_ENTRY_ENCODED) {
+    if (clen == 0) return -1;
+    uint8_t h = chunk_byte(cmd, 0);
+    if ((h & 0xf0) != 0 || (h & 0x0e) != 0 || (h & 1)) return -1;
+    off = 1;
+    plen = clen - 1;
+  } else if (type != DRB_ENTRY_APPLICATION) {
+    return -1;
+  }
+  // PBKV.Unmarshal (kvpb/kv.go:76-283) restricted to single-byte varints
+  uint64_t key8 = 0;
+  uint32_t klen = 0, voff = 0, vlen = 0;
+  bool have_k = false, have_v = false;
+  uint32_t i = 0;
+  while (i < plen) {
+    uint8_t tag = chunk_byte(cmd, off + i);
+    if (i + 1 >= plen) return -1;
+    uint8_t l = chunk_byte(cmd, off + i + 1);
+    if (l >= 0x80) return -1;
+    if (i + 2 + l > plen) return -1;
+    if (tag == 0x0a) {
+      if (l > 8) return -1;
+      key8 = 0;
+      for (uint32_t b = 0; b < l; ++b)
+        key8 |= (uint64_t)chunk_byte(cmd, off + i + 2 + b) << (8 * b);
+      klen = l;
+      have_k = true;
+    } else if (tag == 0x12) {
+      if (l > v.kv_val_cap) return -1;
+      voff = off + i + 2;
+      vlen = l;
+      have_v = true;
+    } else {
+      return -1;
+    }
+    i += 2 + l;
+  }
+  if (!have_k || !have_v) return -1;
+  // open-addressing upsert into this replica's table
+  uint32_t mask = v.KS - 1;
+  uint32_t ks = (uint32_t)kv_hash(key8, klen) & mask;
+  uint4 *tbl = v.kv + kv_ix(v, L.slot, L.g, 0);
+  for (uint32_t probe = 0; probe < v.KS; ++probe) {
+    uint4 *sl = tbl + (uint64_t)ks * v.KVW;
+    uint4 h = sl[0];
+    bool used = (h.z >> 31) & 1u;
+    uint32_t sklen = h.z & 0xffu;
+    bool hit = used && sklen == klen && lo64(h) == key8;
+    if (!used || hit) {
+      // value bytes: first 4 in h.w, the rest in the following chunks
+      uint32_t w0 = 0;
+      for (uint32_t b = 0; b < vlen && b < 4; ++b)
+        w0 |= (uint32_t)chunk_byte(cmd, voff + b) << (8 * b);
+      sl[0] = make_uint4((uint32_t)key8, (uint32_t)(key8 >> 32),
+                         (1u << 31) | (vlen << 8) | klen, w0);
+      for (uint32_t c = 1; c < v.KVW; ++c) {
+        uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b) {
+          uint32_t src = 4 + (c - 1) * 16 + b;
+          if (src < vlen)
+            wv[b >> 2] |= (uint32_t)chunk_byte(cmd, voff + src)
+                          << (8 * (b & 3));
+        }
+        sl[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+      r.kv_count++;
+      r.sm_index = index;
+      r.sm_term = term;
+      return 1;
+    }
+    ks = (ks + 1) & mask;
+  }
+  return -1;  // table full
+}
+
+// ------------------------------------------------------------ load/store
+template <int R>
+DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
+  const View &v = *L.v;
+#define LD(F, x) r.x = v.u64[u64_ix(v, F, L.slot, L.g)]
+  LD(F_TERM, term);
+  LD(F_VOTE, vote);
+  LD(F_LEADER_ID, leader_id);
+  LD(F_APPLIED, applied);
+  LD(F_ELECTION_TICK, election_tick);
+  LD(F_HEARTBEAT_TICK, heartbeat_tick);
+  LD(F_RAND_TIMEOUT, rand_timeout);
+  LD(F_TICK_COUNT, tick_count);
+  LD(F_COMMITTED, committed);
+  LD(F_PROCESSED, processed);
+  LD(F_LAST_INDEX, last);
+  LD(F_MARKER_INDEX, marker);
+  LD(F_SAVED_TO, saved_to);
+  LD(F_APPLIED_TO_INDEX, applied_to_index);
+  LD(F_APPLIED_TO_TERM, applied_to_term);
+  LD(F_APPLIED_INDEX, applied_index);
+  LD(F_CONFIRMED_INDEX, confirmed_index);
+  LD(F_PUSHED_INDEX, pushed_index);
+  LD(F_PREV_TERM, prev_term);
+  LD(F_PREV_VOTE, prev_vote);
+  LD(F_PREV_COMMIT, prev_commit);
+  LD(F_SM_INDEX, sm_index);
+  LD(F_SM_TERM, sm_term);
+  LD(F_KV_COUNT, kv_count);
+  LD(F_RING_LO, ring_lo);
+  LD(F_RING_GUARD, ring_guard);
+#undef LD
+  r.role = v.u32[u32_ix(v, W_ROLE, L.slot, L.g)];
+  r.flags = v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)];
+  r.fb = v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)];
+  r.ri_count = v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)];
+  if (r.role == DRB_LEADER) {
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+      rem_put<R>(L, s,
+                 RemoteV{v.rem_match[rem_ix(v, L.slot, s, L.g)],
+                         v.rem_next[rem_ix(v, L.slot, s, L.g)],
+                         v.rem_state[rem_ix(v, L.slot, s, L.g)],
+                         v.rem_active[rem_ix(v, L.slot, s, L.g)]});
+  }
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d) {
+    if ((uint32_t)d < r.ri_count) {
+      uint4 c = v.ri_ctx[ri_ix(v, L.slot, d, L.g)];
+      uint4 i = v.ri_idx[ri_ix(v, L.slot, d, L.g)];
+      r.ri_lo[d] = lo64(c);
+      r.ri_hi[d] = hi64(c);
+      r.ri_ix[d] = lo64(i);
+      r.ri_fr[d] = hi64(i);
+      r.ri_cf[d] = v.ri_conf[ri_ix(v, L.slot, d, L.g)];
+    } else {
+      r.ri_lo[d] = r.ri_hi[d] = r.ri_ix[d] = r.ri_fr[d] = 0;
+      r.ri_cf[d] = 0;
+    }
+  }
+}
+
+// fields that stay constant on the steady-state path: stored only when
+// they changed (keeps their HBM writes, and the registers of a full copy of
+// the pre-round state, off the hot path)
+struct Cold {
+  uint64_t term, vote, leader_id, rand_timeout, prev_term, prev_vote;
+  uint64_t sm_term, applied_to_term;
+  uint32_t flags, fb;
+};
+
+template <int R>
+DRB_DEV Cold cold_of(const Rep<R> &r) {
+  return Cold{r.term,      r.vote,      r.leader_id, r.rand_timeout,
+              r.prev_term, r.prev_vote, r.sm_term,   r.applied_to_term,
+              r.flags,     r.fb};
+}
+
+template <int R>
+DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, const Cold &o) {
+  const View &v = *L.v;
+#define STC(F, x) \
+  if (r.x != o.x) v.u64[u64_ix(v, F, L.slot, L.g)] = r.x
+#define ST(F, x) v.u64[u64_ix(v, F, L.slot, L.g)] = r.x
+  STC(F_TERM, term);
+  STC(F_VOTE, vote);
+  STC(F_LEADER_ID, leader_id);
+  STC(F_RAND_TIMEOUT, rand_timeout);
+  STC(F_PREV_TERM, prev_term);
+  STC(F_PREV_VOTE, prev_vote);
+  STC(F_SM_TERM, sm_term);
+  STC(F_APPLIED_TO_TERM, applied_to_term);
+  ST(F_APPLIED, applied);
+  ST(F_ELECTION_TICK, election_tick);
+  ST(F_HEARTBEAT_TICK, heartbeat_tick);
+  ST(F_TICK_COUNT, tick_count);
+  ST(F_COMMITTED, committed);
+  ST(F_PROCESSED, processed);
+  ST(F_LAST_INDEX, last);
+  ST(F_MARKER_INDEX, marker);
+  ST(F_SAVED_TO, saved_to);
+  ST(F_APPLIED_TO_INDEX, applied_to_index);
+  ST(F_APPLIED_INDEX, applied_index);
+  ST(F_CONFIRMED_INDEX, confirmed_index);
+  ST(F_PUSHED_INDEX, pushed_index);
+  ST(F_PREV_COMMIT, prev_commit);
+  ST(F_SM_INDEX, sm_index);
+  ST(F_KV_COUNT, kv_count);
+  ST(F_RING_LO, ring_lo);
+  ST(F_RING_GUARD, ring_guard);
+#undef ST
+#undef STC
+  if (r.flags != o.flags) v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)] = r.flags;
+  if (r.fb != o.fb) v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)] = r.fb;
+  v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)] = r.ri_count;
+  if (r.role == DRB_LEADER) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      RemoteV x = rem_get<R>(L, s);
+      v.rem_match[rem_ix(v, L.slot, s, L.g)] = x.m;
+      v.rem_next[rem_ix(v, L.slot, s, L.g)] = x.n;
+      v.rem_state[rem_ix(v, L.slot, s, L.g)] = x.st;
+      v.rem_active[rem_ix(v, L.slot, s, L.g)] = x.a;
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < DRB_RI_DEPTH; ++d) {
+    if ((uint32_t)d >= r.ri_count) continue;
+    v.ri_ctx[ri_ix(v, L.slot, d, L.g)] = mk4(r.ri_lo[d], r.ri_hi[d]);
+    v.ri_idx[ri_ix(v, L.slot, d, L.g)] = mk4(r.ri_ix[d], r.ri_fr[d]);
+    v.ri_conf[ri_ix(v, L.slot, d, L.g)] = r.ri_cf[d];
+  }
+}
+
+// ------------------------------------------------------------ the kernel
+struct RoundParams {
+  uint64_t round;      // t (>= 1)
+  uint32_t tick;
+  uint32_t prop_slot;  // DRB_NONE: none
+  uint32_t ri_slot;    // DRB_NONE: none
+  uint32_t pad;
+};
+
+DRB_DEV void wave_add(unsigned long long *ctr, uint64_t val) {
+  // one atomic per wavefront: reduce over the 64 lanes first
+  uint64_t s = val;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(ctr, (unsigned long long)s);
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
+                                                   RoundParams p) {
+  // the View lives in HBM: every field load is wave-uniform (s_load)
+  const View &v = *vp;
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t slot = blockIdx.y;
+  __shared__ RemLds<R> rl;
+  Lane L;
+  L.rl = &rl;
+  L.tid = threadIdx.x;
+  L.v = vp;
+  L.slot = slot;
+  L.g = g;
+  L.round = p.round;
+  L.rbuf = (uint32_t)((p.round - 1) & 1);
+  L.wbuf = (uint32_t)(p.round & 1);
+  uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
+  uint64_t c_rtr = 0, c_drop = 0;
+  bool active = g < v.G;
+  uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
+  if (!(flags & DRB_F_HOSTED) || (flags & (DRB_F_FALLBACK | DRB_F_ERROR)))
+    active = false;
+  if (active) {
+    Rep<R> r;
+    load_rep(L, r);
+    r.out_cnt = 0;
+    r.nmsgs = 0;
+    r.nrtr = 0;
+    r.ndropped_ri = 0;
+    r.guard_new = ~0ull;
+    r.leader_update = false;
+    r.err = false;
+    const Cold orig = cold_of(r);
+    const uint32_t tag_prev = (uint32_t)(p.round - 1);
+
+    // ---------------------------------------------- pre-pass (read only)
+    uint32_t fb = DRB_FB_NONE;
+    const bool is_leader = r.role == DRB_LEADER;
+    if (!is_leader && r.role != DRB_FOLLOWER) fb = DRB_FB_ROLE;
+    uint32_t nin_packed = 0;  // 4-bit inbox count per sender slot
+    uint32_t total_in = 0, n_ri_msgs = 0, resp_from = 0;
+    uint64_t max_app = 0;
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if ((uint32_t)s == slot) continue;
+      uint64_t meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, g)];
+      uint32_t ns = 0;
+      if ((uint32_t)(meta >> 32) == tag_prev)
+        ns = (uint32_t)(meta >> (4 * slot)) & 15u;
+      nin_packed |= ns << (4 * s);
+      for (uint32_t k = 0; k < ns; ++k) {
+        uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
+        uint32_t type = c0.x & 0xffu;
+        uint64_t mterm = hi64(c0);
+        bool ok;
+        if (is_leader)
+          ok = type == DRB_MSG_REPLICATE_RESP ||
+               type == DRB_MSG_HEARTBEAT_RESP || type == DRB_MSG_READ_INDEX;
+        else
+          ok = type == DRB_MSG_REPLICATE || type == DRB_MSG_HEARTBEAT ||
+               type == DRB_MSG_READ_INDEX_RESP;
+        if (!ok && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
+        if (mterm != 0 && mterm != r.term && fb == DRB_FB_NONE)
+          fb = DRB_FB_TERM_MISMATCH;
+        if (type == DRB_MSG_READ_INDEX) n_ri_msgs++;
+        if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)
+          resp_from |= 1u << s;
+        if (type == DRB_MSG_REPLICATE) {
+          uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
+          max_app = umax64(max_app, lo64(c1) + (c0.x >> 16));
+        }
+      }
+      total_in += ns;
+    }
+    // messages per destination <= inbox + readIndex + tick + proposal
+    if (total_in + 3 > v.MB && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
+    uint32_t nprops = 0;
+    uint64_t in_lo = 0, in_hi = 0;
+    // lowest index the round may still read: apply cursor, commit term,
+    // applied-to term
+    const uint64_t keep_common =
+        umin64(umin64(r.processed + 1, r.committed), r.sm_index);
+    if (is_leader) {
+      if (p.prop_slot != DRB_NONE)
+        nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
+      if (p.ri_slot != DRB_NONE) {
+        uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
+        in_lo = lo64(c);
+        in_hi = hi64(c);
+      }
+      if (r.ri_count + (in_lo != 0) + n_ri_msgs > DRB_RI_DEPTH &&
+          fb == DRB_FB_NONE)
+        fb = DRB_FB_CAPACITY;
+      for (uint32_t j = 0; j < nprops; ++j) {
+        uint4 p2 = v.props[prop_ix(v, p.prop_slot, j, 2, g)];
+        uint32_t type = p2.x, clen = p2.y;
+        if ((type != DRB_ENTRY_APPLICATION && type != DRB_ENTRY_ENCODED) &&
+            fb == DRB_FB_NONE)
+          fb = DRB_FB_ENTRY_TYPE;
+        if (clen > v.C16 * 16 && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
+      }
+      // window: appended entries must not evict what is still needed
+      uint64_t keep = umin64(r.ring_guard, keep_common);
+#pragma unroll
+      for (int s = 0; s < R; ++s)
+        if ((uint32_t)s != slot) keep = umin64(keep, rem_get<R>(L, s).n - 1);
+      if (nprops && r.last + nprops >= keep + v.W && fb == DRB_FB_NONE)
+        fb = DRB_FB_CAPACITY;
+      // tick: CheckQuorum (raft.go:623-633)
+      if (p.tick && v.check_quorum &&
+          r.election_tick + 1 >= v.election_rtt) {
+        int c = 1;
+#pragma unroll
+        for (int s = 0; s < R; ++s)
+          if ((uint32_t)s != slot &&
+              (rem_get<R>(L, s).a || ((resp_from >> s) & 1)))
+            c++;
+        if (c < R / 2 + 1 && fb == DRB_FB_NONE) fb = DRB_FB_CHECK_QUORUM;
+      }
+    } else {
+      if (max_app && max_app >= keep_common + v.W &&
+          fb == DRB_FB_NONE)
+        fb = DRB_FB_CAPACITY;
+      if (p.tick) {
+        uint64_t et = (total_in ? 0 : r.election_tick) + 1;
+        if (et >= r.rand_timeout && fb == DRB_FB_NONE) fb = DRB_FB_ELECTION;
+      }
+    }
+    if (fb != DRB_FB_NONE) {
+      r.flags |= DRB_F_FALLBACK;
+      r.fb = fb;
+      v.u32[u32_ix(v, W_FLAGS, slot, g)] = r.flags;
+      v.u32[u32_ix(v, W_FB_REASON, slot, g)] = r.fb;
+      c_fb = 1;
+    } else {
+      // ---------------------------------------- handleEvents (node.go)
+      // updateAppliedIndex (node.go:1133-1137)
+      r.applied_index = r.sm_index;
+      r.applied = r.applied_index;
+      // handleReadIndex (node.go:1296) -> Peer.ReadIndex (peer.go:309)
+      if (is_leader && in_lo != 0) leader_read_index(L, r, in_lo, in_hi, 0);
+      // handleReceivedMessages: Replicates by sender, then the rest
+#pragma unroll 1
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll 1
+        for (int s = 0; s < R; ++s) {
+          if ((uint32_t)s == slot) continue;
+          const uint32_t ns = (nin_packed >> (4 * s)) & 15u;
+          for (uint32_t k = 0; k < ns; ++k) {
+            uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
+            bool isrep = (c0.x & 0xffu) == DRB_MSG_REPLICATE;
+            if (isrep != (pass == 0)) continue;
+            Msg m = read_msg(L, s, k);
+            dispatch(L, r, s, m);
+          }
+        }
+      }
+      // LocalTick (node.tick node.go:1562 -> raft.tick raft.go:571-648)
+      if (p.tick) {
+        r.tick_count++;
+        if (is_leader) {
+          r.election_tick++;
+          if (r.election_tick >= v.election_rtt) {
+            r.election_tick = 0;
+            if (v.check_quorum) {
+              // leaderHasQuorum (raft.go:395-405): quorum held (pre-pass)
+#pragma unroll
+              for (int s = 0; s < R; ++s) rl_of<R>(L).a[s][L.tid] = 0;
+            }
+          }
+          r.heartbeat_tick++;
+          if (r.heartbeat_tick >= v.heartbeat_rtt) {
+            r.heartbeat_tick = 0;
+            broadcast_heartbeat(L, r);
+          }
+        } else {
+          r.election_tick++;
+        }
+      }
+      // handleProposals (node.go:1275) -> handleLeaderPropose
+      // (raft.go:1794-1815) -> appendEntries (raft.go:944-955)
+      if (nprops) {
+        const uint32_t chunks = PROP_META + v.C16;
+        for (uint32_t j = 0; j < nprops; ++j) {
+          uint64_t idx = r.last + 1 + j;
+          uint4 p0 = v.props[prop_ix(v, p.prop_slot, j, 0, g)];
+          uint4 p1 = v.props[prop_ix(v, p.prop_slot, j, 1, g)];
+          uint4 p2 = v.props[prop_ix(v, p.prop_slot, j, 2, g)];
+          v.ring[ring_ix(v, slot, idx, 0, g)] = mk4(r.term, lo64(p0));
+          v.ring[ring_ix(v, slot, idx, 1, g)] = mk4(hi64(p0), lo64(p1));
+          v.ring[ring_ix(v, slot, idx, 2, g)] =
+              make_uint4(p1.z, p1.w, p2.x, p2.y);
+          for (uint32_t c = PROP_META; c < chunks; ++c)
+            v.ring[ring_ix(v, slot, idx, c, g)] =
+                v.props[prop_ix(v, p.prop_slot, j, c, g)];
+        }
+        r.last += nprops;
+        if (r.last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, r.last + 1 - v.W);
+        rem_try_update<R>(L, (int)slot, r.last);  // self remote
+        if (R == 1) try_commit(L, r);
+        broadcast_replicate(L, r);
+      }
+
+      // ---------------------------------------- getUpdate (node.go:1025)
+      bool inmem_nonempty = r.last >= r.marker;
+      uint64_t save_lo = r.saved_to + 1;
+      bool has_save = inmem_nonempty && save_lo >= r.marker && save_lo <= r.last;
+      bool has_apply = r.committed > r.processed;
+      bool state_changed = !(r.term == r.prev_term && r.vote == r.prev_vote &&
+                             r.committed == r.prev_commit);
+      bool state_empty = r.term == 0 && r.vote == 0 && r.committed == 0;
+      bool has_update = has_save || r.leader_update || r.nmsgs > 0 ||
+                        has_apply || (!state_empty && state_changed) ||
+                        r.nrtr > 0 || r.ndropped_ri > 0;
+      uint64_t apply_lo = 0, apply_hi = 0;
+      if (has_update || r.confirmed_index != r.applied_index) {
+        // validateUpdate / pushEntries (node.go:1100) / Peer.Commit
+        if (has_apply) {
+          // pb.EntriesToApply(CommittedEntries, pushedIndex, strict)
+          // (raftpb/entry.go:27-47) then node.pushEntries (node.go:625)
+          apply_lo = r.processed + 1;
+          apply_hi = r.committed;
+          if (apply_hi <= r.pushed_index || apply_lo > r.pushed_index + 1) {
+            set_error(r, DRB_ERR_APPLY);
+            apply_lo = 0;
+          } else {
+            apply_lo = r.pushed_index + 1;
+            r.pushed_index = apply_hi;
+          }
+        }
+        if (state_changed && !state_empty) {
+          r.prev_term = r.term;
+          r.prev_vote = r.vote;
+          r.prev_commit = r.committed;
+        }
+        r.confirmed_index = r.applied_index;
+        // Peer.Commit -> entryLog.commitUpdate (logentry.go:351-371)
+        if (has_save) r.saved_to = r.last;  // savedLogTo(last, term(last))
+        if (has_apply) r.processed = apply_hi;
+        uint64_t la = r.applied_index;
+        if (la > 0) {
+          if (la > r.committed || la > r.processed)
+            set_error(r, DRB_ERR_COMMIT);
+          // inMemory.appliedLogTo (inmemory.go:138-164)
+          if (la >= r.marker && r.last >= r.marker && la <= r.last) {
+            r.applied_to_index = la;
+            r.applied_to_term = log_term(L, r, la);
+            r.marker = la + 1;
+          }
+        }
+        // clearReadyToRead: records stay in the round output buffer
+      }
+      // ---------------------------------------- StateMachine.Handle
+      if (apply_hi >= apply_lo && apply_lo != 0) {
+        uint64_t from = umax64(apply_lo, r.sm_index + 1);
+        for (uint64_t idx = from; idx <= apply_hi; ++idx) {
+          int rc = apply_entry(L, r, idx);
+          if (rc < 0) {
+            // the rsm apply of this replica leaves the fast path at idx;
+            // the raft round itself completed
+            r.flags |= DRB_F_FALLBACK;
+            r.fb = DRB_FB_ENTRY_TYPE;
+            c_fb = 1;
+            break;
+          }
+          c_applied++;
+          if (rc == 1 && is_leader) c_commit++;
+        }
+      }
+      // ring guard for the next round's appends
+      r.ring_guard = r.guard_new;
+      if (r.err) {
+        r.flags |= DRB_F_ERROR;
+        c_err = 1;
+      }
+      store_rep(L, r, orig);
+      c_msgs = r.nmsgs;
+      c_rtr = r.nrtr;
+      c_drop = r.ndropped_ri;
+    }
+    // outbox meta for this round (tag = round): written even when empty
+    v.mbox_meta[mmeta_ix(v, L.wbuf, slot, g)] =
+        ((uint64_t)(uint32_t)p.round << 32) | r.out_cnt;
+    v.rtr_count[ix(v, slot, g)] = r.nrtr;
+  }
+  wave_add(&v.counters[C_COMMITTED], c_commit);
+  wave_add(&v.counters[C_APPLIED], c_applied);
+  wave_add(&v.counters[C_MESSAGES], c_msgs);
+  wave_add(&v.counters[C_RTR], c_rtr);
+  wave_add(&v.counters[C_DROPPED_RI], c_drop);
+  wave_add(&v.counters[C_FALLBACKS], c_fb);
+  wave_add(&v.counters[C_ERRORS], c_err);
+}
+
+}  // namespace drb

@@ -1,0 +1,282 @@
+"""Python binding of the C ABI (include/drb_engine.h).
+
+This is plumbing for tests and bench.py: every call goes straight to the
+HIP engine in dragonboat_amd/_lib/libdrb_engine.so.  There is no CPU
+fallback -- if the library or the GPU is missing, Engine() raises.
+"""
+import ctypes as C
+import os
+
+from . import abi
+from .abi import (Config, Entry, Message, ReadyToRead, ReplicaState, RoundIn,
+                  RoundOut, entry_to_tuple, message_to_tuple)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libdrb_engine.so")
+
+_lib = None
+
+P = C.c_void_p
+U64 = C.c_uint64
+U32 = C.c_uint32
+PU64 = C.POINTER(C.c_uint64)
+PU32 = C.POINTER(C.c_uint32)
+PU8 = C.POINTER(C.c_uint8)
+SZ = C.c_size_t
+
+# every symbol include/drb_engine.h declares, with its signature
+SIGNATURES = {
+    "drb_engine_create": (C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+    "drb_engine_destroy": (C.c_int, [P]),
+    "drb_engine_device_bytes": (U64, [P]),
+    "drb_engine_stream": (P, [P]),
+    "drb_engine_sync": (C.c_int, [P]),
+    "drb_engine_round": (U64, [P]),
+    "drb_import_replicas": (C.c_int, [P, U64, U64,
+                                      C.POINTER(ReplicaState)]),
+    "drb_export_replicas": (C.c_int, [P, U64, U64,
+                                      C.POINTER(ReplicaState)]),
+    "drb_import_log": (C.c_int, [P, U64, U32, C.POINTER(Entry), SZ, PU8]),
+    "drb_export_log": (C.c_int, [P, U64, U32, U64, U64, C.POINTER(Entry),
+                                 PU8, SZ]),
+    "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
+    "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8]),
+    "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
+    "drb_stage_read_index": (C.c_int, [P, U32, PU64, PU64]),
+    "drb_gen_read_index": (C.c_int, [P, U32, U64, U64]),
+    "drb_ingest": (C.c_int, [P, C.POINTER(Message), SZ, C.POINTER(Entry),
+                             PU8, PU64, PU64]),
+    "drb_step_round": (C.c_int, [P, C.POINTER(RoundIn),
+                                 C.POINTER(RoundOut)]),
+    "drb_step_round_async": (C.c_int, [P, C.POINTER(RoundIn)]),
+    "drb_read_counters": (C.c_int, [P, C.POINTER(RoundOut), C.c_int]),
+    "drb_export_outbox": (C.c_int, [P, U64, U32, C.POINTER(Message), SZ,
+                                    C.POINTER(Entry), SZ, PU8, SZ,
+                                    C.POINTER(SZ)]),
+    "drb_export_ready_to_reads": (C.c_int, [P, U64, U32,
+                                            C.POINTER(ReadyToRead), SZ,
+                                            C.POINTER(SZ)]),
+    "drb_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32, PU32]),
+    "drb_kv_export": (C.c_int, [P, U64, U32, PU8, PU32, PU8, PU32, SZ,
+                                C.POINTER(SZ)]),
+    "drb_crc32_ieee_batch": (C.c_int, [P, PU8, SZ, PU64, PU32, SZ, PU32]),
+}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "dragonboat_amd: %s is missing; run "
+                "python -c 'import __graft_entry__; __graft_entry__.build()'"
+                % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class DrbError(RuntimeError):
+    pass
+
+
+def _ck(rc, what):
+    if rc < 0:
+        raise DrbError("%s failed with status %d" % (what, rc))
+    return rc
+
+
+def _u8(b):
+    return (C.c_uint8 * max(1, len(b))).from_buffer_copy(bytes(b) or b"\0")
+
+
+DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
+                cmd_cap=32, max_props=4, prop_slots=2, ri_slots=2,
+                mailbox=15, kv_slots=512, kv_val_cap=4, election_rtt=10,
+                heartbeat_rtt=1, check_quorum=1, device=0)
+
+
+class Engine:
+    """One MI355X-resident set of G groups x R replica slots."""
+
+    def __init__(self, **kw):
+        cfg = dict(DEFAULTS)
+        cfg.update(kw)
+        self.cfg = cfg
+        c = Config(cfg["num_groups"], cfg["first_shard_id"],
+                   cfg["num_replicas"], cfg["window"], cfg["cmd_cap"],
+                   cfg["max_props"], cfg["prop_slots"], cfg["ri_slots"],
+                   cfg["mailbox"], cfg["kv_slots"], cfg["kv_val_cap"],
+                   cfg["election_rtt"], cfg["heartbeat_rtt"],
+                   cfg["check_quorum"], cfg["device"], 0)
+        h = P()
+        _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
+            "drb_engine_create")
+        self.h = h
+        self.G = cfg["num_groups"]
+        self.R = cfg["num_replicas"]
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().drb_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---------------------------------------------------------- state
+    @property
+    def device_bytes(self):
+        return lib().drb_engine_device_bytes(self.h)
+
+    @property
+    def round(self):
+        return lib().drb_engine_round(self.h)
+
+    @property
+    def stream(self):
+        return lib().drb_engine_stream(self.h)
+
+    def sync(self):
+        _ck(lib().drb_engine_sync(self.h), "drb_engine_sync")
+
+    def import_replicas(self, first_group, states):
+        n = len(states) // self.R
+        arr = (ReplicaState * len(states))(*states)
+        _ck(lib().drb_import_replicas(self.h, first_group, n, arr),
+            "drb_import_replicas")
+
+    def export_replicas(self, first_group, n_groups):
+        arr = (ReplicaState * (n_groups * self.R))()
+        _ck(lib().drb_export_replicas(self.h, first_group, n_groups, arr),
+            "drb_export_replicas")
+        return list(arr)
+
+    def export(self, g, slot):
+        return self.export_replicas(g, 1)[slot]
+
+    def import_log(self, g, slot, entries, pool):
+        """entries: Entry array (indices set), pool: uint8 array."""
+        _ck(lib().drb_import_log(self.h, g, slot, entries, len(entries), pool),
+            "drb_import_log")
+
+    def export_log(self, g, slot, lo, hi):
+        n = hi - lo + 1
+        if n <= 0:
+            return []
+        arr = (Entry * n)()
+        pcap = n * self.cfg["cmd_cap"] + 16
+        pool = (C.c_uint8 * pcap)()
+        _ck(lib().drb_export_log(self.h, g, slot, lo, hi, arr, pool, pcap),
+            "drb_export_log")
+        return [entry_to_tuple(arr[i], pool) for i in range(n)]
+
+    def init_steady(self, term=2, leader_slot=0, seed=0x5EEDD8B0):
+        _ck(lib().drb_init_steady(self.h, term, leader_slot, seed),
+            "drb_init_steady")
+
+    # ---------------------------------------------------------- inputs
+    def stage_proposals(self, slot, counts, ents, pool):
+        _ck(lib().drb_stage_proposals(self.h, slot, counts, ents, pool),
+            "drb_stage_proposals")
+
+    def gen_kv_proposals(self, slot, k, key_space, val_len, seed, salt):
+        _ck(lib().drb_gen_kv_proposals(self.h, slot, k, key_space, val_len,
+                                       seed, salt), "drb_gen_kv_proposals")
+
+    def stage_read_index(self, slot, low, high):
+        _ck(lib().drb_stage_read_index(self.h, slot, low, high),
+            "drb_stage_read_index")
+
+    def gen_read_index(self, slot, seed, high):
+        _ck(lib().drb_gen_read_index(self.h, slot, seed, high),
+            "drb_gen_read_index")
+
+    def ingest(self, marr, n, earr, pool):
+        acc, drop = U64(), U64()
+        _ck(lib().drb_ingest(self.h, marr, n, earr, pool, C.byref(acc),
+                             C.byref(drop)), "drb_ingest")
+        return acc.value, drop.value
+
+    # ---------------------------------------------------------- round
+    def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE):
+        rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, 0)
+        out = RoundOut()
+        _ck(lib().drb_step_round(self.h, C.byref(rin), C.byref(out)),
+            "drb_step_round")
+        return out
+
+    def step_async(self, tick=False, prop_slot=abi.DRB_NONE,
+                   ri_slot=abi.DRB_NONE):
+        rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, 0)
+        _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
+            "drb_step_round_async")
+
+    def read_counters(self, reset=True):
+        out = RoundOut()
+        _ck(lib().drb_read_counters(self.h, C.byref(out), int(reset)),
+            "drb_read_counters")
+        return out
+
+    # ---------------------------------------------------------- outputs
+    def export_outbox(self, g, slot):
+        cap, ecap = 16 * self.R, 16 * self.R * self.cfg["window"]
+        pcap = ecap * self.cfg["cmd_cap"] + 16
+        marr = (Message * cap)()
+        earr = (Entry * ecap)()
+        pool = (C.c_uint8 * pcap)()
+        n = SZ()
+        _ck(lib().drb_export_outbox(self.h, g, slot, marr, cap, earr, ecap,
+                                    pool, pcap, C.byref(n)),
+            "drb_export_outbox")
+        return [message_to_tuple(marr[i], earr, pool) for i in range(n.value)]
+
+    def export_ready(self, g, slot):
+        cap = 16
+        arr = (ReadyToRead * cap)()
+        n = SZ()
+        _ck(lib().drb_export_ready_to_reads(self.h, g, slot, arr, cap,
+                                            C.byref(n)),
+            "drb_export_ready_to_reads")
+        return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high)
+                for i in range(min(n.value, cap))]
+
+    def kv_export(self, g, slot):
+        cap = self.cfg["kv_slots"]
+        vcap = self.cfg["kv_val_cap"]
+        keys = (C.c_uint8 * (8 * cap))()
+        vals = (C.c_uint8 * (vcap * cap))()
+        kl, vl = (U32 * cap)(), (U32 * cap)()
+        n = SZ()
+        _ck(lib().drb_kv_export(self.h, g, slot, keys, kl, vals, vl, cap,
+                                C.byref(n)), "drb_kv_export")
+        kb, vb = bytes(keys), bytes(vals)
+        return {kb[i * 8:i * 8 + kl[i]]: vb[i * vcap:i * vcap + vl[i]]
+                for i in range(n.value)}
+
+    def kv_lookup(self, g, slot, key):
+        vcap = self.cfg["kv_val_cap"]
+        val = (C.c_uint8 * vcap)()
+        vl = U32()
+        rc = _ck(lib().drb_kv_lookup(self.h, g, slot, _u8(key), len(key),
+                                     val, vcap, C.byref(vl)), "drb_kv_lookup")
+        return None if rc == 1 else bytes(val[:vl.value])
+
+    def crc32_batch(self, buffers):
+        data = b"".join(buffers)
+        offs, lens, o = [], [], 0
+        for b in buffers:
+            offs.append(o)
+            lens.append(len(b))
+            o += len(b)
+        n = len(buffers)
+        crc = (U32 * max(1, n))()
+        _ck(lib().drb_crc32_ieee_batch(self.h, _u8(data), len(data),
+                                       (U64 * max(1, n))(*offs),
+                                       (U32 * max(1, n))(*lens), n, crc),
+            "drb_crc32_ieee_batch")
+        return list(crc[:n])

@@ -1,0 +1,90 @@
+"""Synthetic inputs of SURVEY.md 8(d), defined bit-exactly.
+
+The same definition is implemented on the device by drb_gen_kv_proposals /
+drb_gen_read_index (dragonboat_amd/csrc/drb_engine.hip); this module builds
+the identical records on the host so tests can stage them through
+drb_stage_proposals and compare.
+
+Per group g, batch salt s, proposal j (k per group per round):
+  r0 = mix64(seed ^ (g * GOLDEN) ^ (s << 32) ^ (j << 16))
+  r1 = mix64(r0); r2 = mix64(r1)
+  Entry.Key      = r0 | 1                   (request.go:1047, non-zero)
+  Entry.ClientID = mix64(seed ^ CLIENT ^ g) | 1   NoOP session
+  SeriesID = RespondedTo = 0, Type = EncodedEntry (encoded.go:83-93)
+  Cmd = 0x00 || PBKV{key = LE64(r1 % key_space), val = bytes of r2 chain}
+"""
+import struct
+
+import ctypes as C
+
+from .abi import ENTRY_ENCODED, Entry
+
+MASK = (1 << 64) - 1
+GOLDEN = 0x9E3779B97F4A7C15
+CLIENT = 0xC11E47C11E47C11E
+RI_SALT = 0x5EAD1DE85EAD1DE8
+
+
+def mix64(z):
+    z = (z + GOLDEN) & MASK
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK
+    return z ^ (z >> 31)
+
+
+def client_id(seed, g):
+    return mix64(seed ^ CLIENT ^ g) | 1
+
+
+def pbkv16(key8, val):
+    return b"\x0a" + bytes([len(key8)]) + key8 + b"\x12" + bytes([len(val)]) \
+        + val
+
+
+def proposal(seed, g, s, j, key_space, val_len):
+    r0 = mix64(seed ^ ((g * GOLDEN) & MASK) ^ ((s << 32) & MASK) ^ (j << 16))
+    r1 = mix64(r0)
+    r2 = mix64(r1)
+    key8 = struct.pack("<Q", r1 % key_space)
+    vb = b""
+    x = r2
+    while len(vb) < val_len:
+        vb += struct.pack("<Q", x)
+        x = mix64(x)
+    cmd = b"\x00" + pbkv16(key8, vb[:val_len])
+    return dict(key=r0 | 1, client_id=client_id(seed, g), series_id=0,
+                responded_to=0, type=ENTRY_ENCODED, cmd=cmd)
+
+
+def build_batch(num_groups, k, seed, salt, key_space=256, val_len=4,
+                groups=None):
+    """Returns (counts[u32 G], ents[Entry G*k], pool, python list)."""
+    counts = (C.c_uint32 * num_groups)()
+    ents = (Entry * max(1, num_groups * k))()
+    pool = bytearray()
+    gs = range(num_groups) if groups is None else groups
+    for g in gs:
+        counts[g] = k
+        for j in range(k):
+            p = proposal(seed, g, salt, j, key_space, val_len)
+            ents[g * k + j] = Entry(0, 0, p["key"], p["client_id"], 0, 0,
+                                    p["type"], len(p["cmd"]), len(pool))
+            pool += p["cmd"]
+    pbuf = (C.c_uint8 * max(1, len(pool))).from_buffer_copy(bytes(pool) or
+                                                           b"\0")
+    return counts, ents, pbuf
+
+
+def read_index_ctx(seed, g, salt, high):
+    """pendingReadIndex.genCtx (request.go:864-875): Low random non-zero."""
+    low = mix64(seed ^ RI_SALT ^ ((g * GOLDEN) & MASK) ^ (salt << 40)) | 1
+    return low, high
+
+
+def build_read_index(num_groups, seed, salt, high, groups=None):
+    lo = (C.c_uint64 * num_groups)()
+    hi = (C.c_uint64 * num_groups)()
+    gs = range(num_groups) if groups is None else groups
+    for g in gs:
+        lo[g], hi[g] = read_index_ctx(seed, g, salt, high)
+    return lo, hi

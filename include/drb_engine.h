@@ -1,0 +1,404 @@
+/*
+ * drb_engine.h -- C ABI of the MI355X-native batched multi-group Raft
+ * replication engine (dragonboat_amd).
+ *
+ * This header is the drop-in boundary.  Every entry point replaces one
+ * interface on dragonboat's replication fast path; the reference interface
+ * it stands in for is cited next to it (paths relative to the dragonboat
+ * v4 source tree).  All types are plain C: fixed-width integers, plain
+ * pointers and sizes.  No torch / HIP types cross this boundary.
+ *
+ * Execution model:
+ *   One engine owns G Raft groups x R replica slots resident in HBM as
+ *   structure-of-arrays.  Replica slot s of every group has replica ID s+1.
+ *   drb_step_round() executes ONE step round for every hosted replica, with
+ *   exactly the semantics of one iteration of dragonboat's step loop
+ *   (node_test.go:274-353 / engine.go:1304-1364): each replica drains its
+ *   inbox (messages sent in the previous round), handles its tick, ReadIndex
+ *   batch and proposals, builds its Update, applies committed entries to
+ *   its in-memory KV state machine and commits the Update; messages it
+ *   sends are delivered at the end of the round.
+ *
+ * Threading: an engine is not re-entrant; one host thread drives it (the
+ * reference holds node.raftMu across stepNode, node.go:1140).
+ *
+ * Error behaviour: functions return DRB_OK (0) or a negative DRB_E* code.
+ * Conditions the reference reports with plog.Panicf mark the replica
+ * DRB_F_ERROR; paths that stay on the reference CPU code (election,
+ * membership change, snapshot, session management, higher/lower term
+ * messages) mark it DRB_F_FALLBACK *before* it mutates any state, so the
+ * pre-round state can be exported to the CPU raft.Peer.
+ */
+#ifndef DRB_ENGINE_H
+#define DRB_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRB_MAX_REPLICAS 8
+#define DRB_RI_DEPTH 4        /* device readIndex queue depth (readindex.go:30-33) */
+
+/* status codes */
+#define DRB_OK 0
+#define DRB_EINVAL (-1)
+#define DRB_EDEVICE (-2)
+#define DRB_ENOMEM (-3)
+#define DRB_ENOSYS (-4)
+#define DRB_ERANGE (-5)
+
+/* raftpb.MessageType (raftpb/types.go:8-37) */
+enum drb_message_type {
+  DRB_MSG_LOCAL_TICK = 0,
+  DRB_MSG_ELECTION = 1,
+  DRB_MSG_LEADER_HEARTBEAT = 2,
+  DRB_MSG_CONFIG_CHANGE_EVENT = 3,
+  DRB_MSG_NOOP = 4,
+  DRB_MSG_PING = 5,
+  DRB_MSG_PONG = 6,
+  DRB_MSG_PROPOSE = 7,
+  DRB_MSG_SNAPSHOT_STATUS = 8,
+  DRB_MSG_UNREACHABLE = 9,
+  DRB_MSG_CHECK_QUORUM = 10,
+  DRB_MSG_BATCHED_READ_INDEX = 11,
+  DRB_MSG_REPLICATE = 12,
+  DRB_MSG_REPLICATE_RESP = 13,
+  DRB_MSG_REQUEST_VOTE = 14,
+  DRB_MSG_REQUEST_VOTE_RESP = 15,
+  DRB_MSG_INSTALL_SNAPSHOT = 16,
+  DRB_MSG_HEARTBEAT = 17,
+  DRB_MSG_HEARTBEAT_RESP = 18,
+  DRB_MSG_READ_INDEX = 19,
+  DRB_MSG_READ_INDEX_RESP = 20,
+  DRB_MSG_QUIESCE = 21,
+  DRB_MSG_SNAPSHOT_RECEIVED = 22,
+  DRB_MSG_LEADER_TRANSFER = 23,
+  DRB_MSG_TIMEOUT_NOW = 24,
+  DRB_MSG_RATE_LIMIT = 25,
+  DRB_MSG_REQUEST_PREVOTE = 26,
+  DRB_MSG_REQUEST_PREVOTE_RESP = 27,
+  DRB_MSG_LOG_QUERY = 28
+};
+
+/* raftpb.EntryType (raftpb/types.go) */
+enum drb_entry_type {
+  DRB_ENTRY_APPLICATION = 0,
+  DRB_ENTRY_CONFIG_CHANGE = 1,
+  DRB_ENTRY_ENCODED = 2,
+  DRB_ENTRY_METADATA = 3
+};
+
+/* raft.State (internal/raft/raft.go:63-71) */
+enum drb_role {
+  DRB_FOLLOWER = 0,
+  DRB_CANDIDATE = 1,
+  DRB_PREVOTE_CANDIDATE = 2,
+  DRB_LEADER = 3,
+  DRB_NONVOTING = 4,
+  DRB_WITNESS = 5
+};
+
+/* remoteStateType (internal/raft/remote.go:54-59) */
+enum drb_remote_fsm {
+  DRB_REMOTE_RETRY = 0,
+  DRB_REMOTE_WAIT = 1,
+  DRB_REMOTE_REPLICATE = 2,
+  DRB_REMOTE_SNAPSHOT = 3
+};
+
+/* drb_replica_state.flags */
+#define DRB_F_HOSTED 1u    /* stepped by this engine */
+#define DRB_F_FALLBACK 2u  /* handed back to the CPU raft.Peer, frozen here */
+#define DRB_F_ERROR 4u     /* invariant violation (reference: plog.Panicf) */
+
+/* drb_replica_state.fallback_reason */
+enum drb_fallback_reason {
+  DRB_FB_NONE = 0,
+  DRB_FB_TERM_MISMATCH = 1,     /* raft.go:1540-1590 term gate not on fast path */
+  DRB_FB_MESSAGE_TYPE = 2,      /* message type handled only on the CPU path */
+  DRB_FB_ELECTION = 3,          /* raft.go:602 election timeout */
+  DRB_FB_CHECK_QUORUM = 4,      /* raft.go:1785 leader lost quorum */
+  DRB_FB_ENTRY_TYPE = 5,        /* config change / session / compressed entry */
+  DRB_FB_CAPACITY = 6,          /* window / mailbox / readIndex capacity */
+  DRB_FB_ROLE = 7,              /* candidate / non-voting / witness */
+  DRB_FB_PROPOSAL = 8,          /* proposal at a non-leader replica */
+  DRB_ERR_LOG_RANGE = 100,      /* entry outside the resident window */
+  DRB_ERR_COMMIT = 101,         /* logentry.go:336-349 commitTo panic */
+  DRB_ERR_CONFLICT = 102,       /* logentry.go:296-310 conflict <= committed */
+  DRB_ERR_APPEND = 103,         /* entryutils.go:36-48 hole / term regress */
+  DRB_ERR_APPLY = 104,          /* statemachine.go:935-969 malformed entry */
+  DRB_ERR_READINDEX = 105       /* readindex.go:43-115 invariant */
+};
+
+/* remote (internal/raft/remote.go:72-80); remotes[] is indexed by slot. */
+typedef struct drb_remote_state {
+  uint64_t match;
+  uint64_t next;
+  uint32_t state;   /* drb_remote_fsm */
+  uint32_t active;  /* remote.active (remote.go:215-225) */
+} drb_remote_state;
+
+/* readStatus (internal/raft/readindex.go:21-26), kept in queue order. */
+typedef struct drb_read_status {
+  uint64_t ctx_low;    /* pb.SystemCtx.Low */
+  uint64_t ctx_high;   /* pb.SystemCtx.High */
+  uint64_t index;
+  uint64_t from;
+  uint32_t confirmed;  /* bit s set: replica slot s confirmed */
+  uint32_t pad;
+} drb_read_status;
+
+/*
+ * Per-replica state: the fields of raft (raft.go:199-239), entryLog
+ * (logentry.go:78-84), inMemory (inmemory.go:30-39), Peer.prevState
+ * (peer.go:59), node (node.go appliedIndex/confirmedIndex/pushedIndex) and
+ * the rsm/KV apply cursor that the fast path reads or writes.  This is
+ * the record drb_export_replicas()/drb_import_replicas() move between the
+ * device SoA and a CPU raft.Peer on fallback.
+ */
+typedef struct drb_replica_state {
+  uint64_t shard_id;
+  uint64_t replica_id;
+  uint64_t term;
+  uint64_t vote;
+  uint64_t leader_id;
+  uint64_t applied;                    /* raft.applied */
+  uint64_t election_tick;
+  uint64_t heartbeat_tick;
+  uint64_t randomized_election_timeout;
+  uint64_t tick_count;
+  uint64_t committed;                  /* entryLog.committed */
+  uint64_t processed;                  /* entryLog.processed */
+  uint64_t last_index;                 /* entryLog.lastIndex() */
+  uint64_t marker_index;               /* inMemory.markerIndex */
+  uint64_t saved_to;                   /* inMemory.savedTo */
+  uint64_t applied_to_index;           /* inMemory.appliedToIndex */
+  uint64_t applied_to_term;            /* inMemory.appliedToTerm */
+  uint64_t applied_index;              /* node.appliedIndex */
+  uint64_t confirmed_index;            /* node.confirmedIndex */
+  uint64_t pushed_index;               /* node.pushedIndex */
+  uint64_t prev_term;                  /* Peer.prevState.Term */
+  uint64_t prev_vote;                  /* Peer.prevState.Vote */
+  uint64_t prev_commit;                /* Peer.prevState.Commit */
+  uint64_t sm_index;                   /* StateMachine.index (statemachine.go:716) */
+  uint64_t sm_term;                    /* StateMachine.term */
+  uint64_t kv_count;                   /* KVTest.Count (kvtest.go:146) */
+  uint32_t role;                       /* drb_role */
+  uint32_t flags;                      /* DRB_F_* */
+  uint32_t fallback_reason;            /* drb_fallback_reason */
+  uint32_t ri_count;                   /* valid entries in ri[] */
+  drb_remote_state remotes[DRB_MAX_REPLICAS];
+  drb_read_status ri[DRB_RI_DEPTH];
+} drb_replica_state;
+
+/* pb.Entry (raftpb/entry.go:6-16); Cmd bytes live in a caller pool. */
+typedef struct drb_entry {
+  uint64_t term;
+  uint64_t index;
+  uint64_t key;
+  uint64_t client_id;
+  uint64_t series_id;
+  uint64_t responded_to;
+  uint32_t type;      /* drb_entry_type */
+  uint32_t cmd_len;
+  uint64_t cmd_off;   /* byte offset of Cmd in the pool */
+} drb_entry;
+
+/*
+ * pb.Message (raftpb/message.go:6-20) for the fields this path uses; the
+ * embedded Snapshot is always empty here.  Entries are
+ * ents[entries_off .. entries_off + n_entries).
+ */
+typedef struct drb_message {
+  uint64_t shard_id;
+  uint64_t from;
+  uint64_t to;
+  uint64_t term;
+  uint64_t log_term;
+  uint64_t log_index;
+  uint64_t commit;
+  uint64_t hint;
+  uint64_t hint_high;
+  uint32_t type;      /* drb_message_type */
+  uint32_t reject;
+  uint64_t n_entries;
+  uint64_t entries_off;
+} drb_message;
+
+/* pb.ReadyToRead (raftpb/update.go) */
+typedef struct drb_ready_to_read {
+  uint64_t shard_id;
+  uint64_t replica_id;
+  uint64_t index;
+  uint64_t ctx_low;
+  uint64_t ctx_high;
+} drb_ready_to_read;
+
+/* Engine sizing.  Raft knobs mirror config.Config (config/config.go:65-200). */
+typedef struct drb_config {
+  uint64_t num_groups;       /* G groups on this device */
+  uint64_t first_shard_id;   /* ShardID of group g = first_shard_id + g */
+  uint32_t num_replicas;     /* R, 1..DRB_MAX_REPLICAS; replica IDs 1..R */
+  uint32_t window;           /* W resident entries per replica (power of 2) */
+  uint32_t cmd_cap;          /* max Cmd bytes per resident entry (mult. of 16) */
+  uint32_t max_props;        /* max proposals per group per round */
+  uint32_t prop_slots;       /* staged proposal batches */
+  uint32_t ri_slots;         /* staged ReadIndex batches */
+  uint32_t mailbox;          /* messages per (sender, receiver) per round */
+  uint32_t kv_slots;         /* KV open-addressing slots per replica (pow2) */
+  uint32_t kv_val_cap;       /* max value bytes stored inline per KV slot */
+  uint32_t election_rtt;     /* Config.ElectionRTT */
+  uint32_t heartbeat_rtt;    /* Config.HeartbeatRTT */
+  uint32_t check_quorum;     /* Config.CheckQuorum */
+  int32_t device;            /* HIP device ordinal */
+  uint32_t reserved;
+} drb_config;
+
+/* One step round (engine.processSteps, engine.go:1304). */
+typedef struct drb_round_in {
+  uint32_t tick;       /* 1: one LocalTick per hosted replica (nodehost.go:1903) */
+  uint32_t prop_slot;  /* staged proposal batch to consume, DRB_NONE for none */
+  uint32_t ri_slot;    /* staged ReadIndex batch, DRB_NONE for none */
+  uint32_t reserved;
+} drb_round_in;
+
+#define DRB_NONE 0xffffffffu
+
+typedef struct drb_round_out {
+  uint64_t round;                 /* index of the round just executed */
+  uint64_t committed_entries;     /* sum of leader commit advance, app entries */
+  uint64_t applied_entries;       /* entries applied over all replicas */
+  uint64_t messages;              /* messages sent in this round */
+  uint64_t ready_to_reads;        /* ReadyToRead records produced */
+  uint64_t dropped_read_indexes;  /* raft.droppedReadIndexes */
+  uint64_t fallbacks;             /* replicas newly marked DRB_F_FALLBACK */
+  uint64_t errors;                /* replicas newly marked DRB_F_ERROR */
+} drb_round_out;
+
+typedef struct drb_engine drb_engine;
+
+/* --- lifecycle --------------------------------------------------------- */
+
+/* Allocates the SoA state in HBM.  Replaces newExecEngine (engine.go:1009)
+ * plus per-shard node/raft construction (node.go:136, raft.go:241) for the
+ * groups this device hosts. */
+int drb_engine_create(const drb_config *cfg, drb_engine **out);
+int drb_engine_destroy(drb_engine *e);
+/* Bytes of HBM the engine holds. */
+uint64_t drb_engine_device_bytes(const drb_engine *e);
+/* The hipStream_t every kernel of this engine is launched on. */
+void *drb_engine_stream(drb_engine *e);
+int drb_engine_sync(drb_engine *e);
+uint64_t drb_engine_round(const drb_engine *e);
+
+/* --- state movement (fallback boundary, SURVEY 8b "Fallback") ---------- */
+
+/* st[(g - first_group) * R + slot]. */
+int drb_import_replicas(drb_engine *e, uint64_t first_group, uint64_t n_groups,
+                        const drb_replica_state *st);
+int drb_export_replicas(drb_engine *e, uint64_t first_group, uint64_t n_groups,
+                        drb_replica_state *st);
+/* Writes entries (contiguous indices) into the resident window of one
+ * replica: the inMemory.entries / LogDB content the fast path reads. */
+int drb_import_log(drb_engine *e, uint64_t group, uint32_t slot,
+                   const drb_entry *ents, size_t n, const uint8_t *pool);
+/* Reads indices [lo, hi] of one replica's window.  pool receives Cmd bytes
+ * (pool_cap bytes available). */
+int drb_export_log(drb_engine *e, uint64_t group, uint32_t slot, uint64_t lo,
+                   uint64_t hi, drb_entry *out, uint8_t *pool,
+                   size_t pool_cap);
+
+/* Device-side initialisation of every group to the post-election steady
+ * state: bootstrap (peer.go:404-428) with R config-change entries at term
+ * 1, replica `leader_slot` elected at `term` (raft.go:1176, 1038) and its
+ * no-op entry committed and applied everywhere.  Equivalent to running
+ * the CPU election path per group; `seed` feeds the randomized election
+ * timeout (raft.go:658-661). */
+int drb_init_steady(drb_engine *e, uint64_t term, uint32_t leader_slot,
+                    uint64_t seed);
+
+/* --- inputs ------------------------------------------------------------- */
+
+/* Stage proposals for one round: counts[g] entries for group g taken from
+ * ents[g * max_props ...].  Replaces entryQueue.add (queue.go:60) feeding
+ * node.handleProposals (node.go:1275).  Consumed by the group's leader. */
+int drb_stage_proposals(drb_engine *e, uint32_t slot, const uint32_t *counts,
+                        const drb_entry *ents, const uint8_t *pool);
+/* Device-side synthetic proposal generator (bench / SURVEY 8d inputs):
+ * k KVTest PBKV writes per group, NoOP session, EncodedEntry v0. */
+int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
+                         uint32_t key_space, uint32_t val_len, uint64_t seed,
+                         uint64_t salt);
+/* Stage one ReadIndex ctx per group (ctx_low[g] == 0: none).  Replaces
+ * pendingReadIndex.read + node.handleReadIndex (request.go:845,
+ * node.go:1296). */
+int drb_stage_read_index(drb_engine *e, uint32_t slot, const uint64_t *ctx_low,
+                         const uint64_t *ctx_high);
+int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
+                       uint64_t high);
+
+/* Inbound boundary: IMessageHandler.HandleMessageBatch
+ * (internal/transport/transport.go:86-91, nodehost.go:2072-2122).  Places
+ * messages from replicas NOT hosted by this engine into the inbox of the
+ * next round.  Messages for unknown shards / unhosted targets, or beyond
+ * the mailbox capacity, are dropped (nodehost.go:2112-2114). */
+int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
+               const drb_entry *ents, const uint8_t *pool, uint64_t *accepted,
+               uint64_t *dropped);
+
+/* --- the step round ---------------------------------------------------- */
+
+/* Replaces engine.processSteps (engine.go:1304) -> node.stepNode
+ * (node.go:1139) -> Peer.Handle/GetUpdate/Commit (peer.go:184,198,292)
+ * -> StateMachine.Handle (internal/rsm/statemachine.go:599) for every
+ * hosted replica, with an in-memory ILogDB.  Stream-ordered; `out` is
+ * filled after the round completes (this call synchronises). */
+int drb_step_round(drb_engine *e, const drb_round_in *in, drb_round_out *out);
+/* Same, without the host synchronisation; counters accumulate on device
+ * and are read by drb_read_counters(). */
+int drb_step_round_async(drb_engine *e, const drb_round_in *in);
+int drb_read_counters(drb_engine *e, drb_round_out *out, int reset);
+
+/* --- outputs ----------------------------------------------------------- */
+
+/* Outbound boundary: the messages one replica sent in the last round
+ * (node.sendReplicateMessages / sendMessages, node.go:1007-1022 ->
+ * Transport.Send, transport.go:346), in send order.  Entries of Replicate
+ * messages are copied out with Cmd bytes into pool. */
+int drb_export_outbox(drb_engine *e, uint64_t group, uint32_t from_slot,
+                      drb_message *out, size_t cap, drb_entry *ents,
+                      size_t ent_cap, uint8_t *pool, size_t pool_cap,
+                      size_t *n_msgs);
+/* pb.Update.ReadyToReads of the last round for one replica. */
+int drb_export_ready_to_reads(drb_engine *e, uint64_t group, uint32_t slot,
+                              drb_ready_to_read *out, size_t cap,
+                              size_t *n_out);
+
+/* IStateMachine.Lookup used by NodeHost.ReadLocalNode (nodehost.go:849). */
+int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
+                  const uint8_t *key, uint32_t key_len, uint8_t *val,
+                  uint32_t val_cap, uint32_t *val_len);
+/* Dumps every KV pair of one replica: keys[i*8..], key_lens[i],
+ * vals[i*kv_val_cap..], val_lens[i]; returns the count in *n_out. */
+int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot, uint8_t *keys,
+                  uint32_t *key_lens, uint8_t *vals, uint32_t *val_lens,
+                  size_t cap, size_t *n_out);
+
+/* --- codecs (raftpb EntryBatch encode / CRC path) ---------------------- */
+
+/* crc32.ChecksumIEEE (Go hash/crc32) over n independent buffers on the
+ * device: crc[i] = CRC32-IEEE(data[off[i] .. off[i]+len[i])).  The framing
+ * CRC of internal/transport/tcp.go:146,232.  Host pointers; the engine
+ * stages them through HBM. */
+int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data, size_t data_len,
+                         const uint64_t *off, const uint32_t *len, size_t n,
+                         uint32_t *crc);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DRB_ENGINE_H */

@@ -1,0 +1,851 @@
+/*
+ * node_oracle.c -- CPU restatement of the node-level step round, the rsm
+ * apply path and the KVTest state machine.  TEST INFRASTRUCTURE ONLY.
+ *
+ *   node.handleEvents            node.go:1161-1223
+ *   node.handleReadIndex         node.go:1296-1307
+ *   node.handleReceivedMessages  node.go:1347-1377 (+ handleMessage 1379)
+ *   node.handleProposals         node.go:1275-1294
+ *   node.tick                    node.go:1562-1579
+ *   node.getUpdate               node.go:1025-1042
+ *   Peer.HasUpdate/GetUpdate     peer.go:198-289, getUpdate 333-379,
+ *                                getUpdateCommit 432-449
+ *   Peer.Commit                  peer.go:292-305
+ *   step() loop                  node_test.go:274-353
+ *   StateMachine.Handle/handle   internal/rsm/statemachine.go:599-906
+ *   handleEntry/update/noop      statemachine.go:935-1103
+ *   setApplied/setLastApplied    statemachine.go:716-760
+ *   GetPayload/getDecodedPayload internal/rsm/encoded.go:55-170
+ *   KVTest.Update                internal/tests/kvtest.go:145-162,311
+ *   pb.EntriesToApply            raftpb/entry.go:27-47
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle_internal.h"
+
+/* ------------------------------------------------------------------ */
+/* KVTest: map[string]string + Count                                    */
+/* ------------------------------------------------------------------ */
+typedef struct kv_item {
+  uint8_t *key;
+  uint8_t *val;
+  uint32_t klen, vlen;
+  int used;
+} kv_item;
+
+typedef struct orc_kv {
+  kv_item *t;
+  size_t cap, n;
+  uint64_t count;
+} orc_kv;
+
+static uint64_t fnv1a(const uint8_t *p, size_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+  return h;
+}
+
+static void kv_insert_raw(orc_kv *kv, uint8_t *key, uint32_t klen, uint8_t *val,
+                          uint32_t vlen) {
+  size_t m = kv->cap - 1;
+  size_t i = (size_t)fnv1a(key, klen) & m;
+  while (kv->t[i].used) {
+    if (kv->t[i].klen == klen && memcmp(kv->t[i].key, key, klen) == 0) {
+      free(kv->t[i].val);
+      free(key);
+      kv->t[i].val = val;
+      kv->t[i].vlen = vlen;
+      return;
+    }
+    i = (i + 1) & m;
+  }
+  kv->t[i].used = 1;
+  kv->t[i].key = key;
+  kv->t[i].klen = klen;
+  kv->t[i].val = val;
+  kv->t[i].vlen = vlen;
+  kv->n++;
+}
+
+static void kv_grow(orc_kv *kv) {
+  size_t oc = kv->cap;
+  kv_item *ot = kv->t;
+  kv->cap = oc ? oc * 2 : 16;
+  kv->t = (kv_item *)calloc(kv->cap, sizeof(kv_item));
+  kv->n = 0;
+  for (size_t i = 0; i < oc; i++)
+    if (ot[i].used)
+      kv_insert_raw(kv, ot[i].key, ot[i].klen, ot[i].val, ot[i].vlen);
+  free(ot);
+}
+
+static uint8_t *dupbytes(const uint8_t *p, uint32_t n) {
+  uint8_t *d = (uint8_t *)malloc(n ? n : 1);
+  if (n) memcpy(d, p, n);
+  return d;
+}
+
+/* updateStore (kvtest.go:311-313): s.KVStore[key] = value */
+static void kv_update_store(orc_kv *kv, const uint8_t *key, uint32_t klen,
+                            const uint8_t *val, uint32_t vlen) {
+  if ((kv->n + 1) * 2 > kv->cap) kv_grow(kv);
+  kv_insert_raw(kv, dupbytes(key, klen), klen, dupbytes(val, vlen), vlen);
+}
+
+static const kv_item *kv_find(const orc_kv *kv, const uint8_t *key,
+                              uint32_t klen) {
+  if (!kv->cap) return NULL;
+  size_t m = kv->cap - 1;
+  size_t i = (size_t)fnv1a(key, klen) & m;
+  while (kv->t[i].used) {
+    if (kv->t[i].klen == klen && memcmp(kv->t[i].key, key, klen) == 0)
+      return &kv->t[i];
+    i = (i + 1) & m;
+  }
+  return NULL;
+}
+
+static void kv_free(orc_kv *kv) {
+  for (size_t i = 0; i < kv->cap; i++)
+    if (kv->t[i].used) {
+      free(kv->t[i].key);
+      free(kv->t[i].val);
+    }
+  free(kv->t);
+  memset(kv, 0, sizeof(*kv));
+}
+
+/* ------------------------------------------------------------------ */
+/* node                                                                 */
+/* ------------------------------------------------------------------ */
+typedef struct orc_node {
+  orc_raft *r;
+  orc_logdb *db;
+  orc_kv kv;
+  uint64_t sm_index, sm_term; /* StateMachine.index/term */
+  uint64_t la_index, la_term; /* StateMachine.lastApplied */
+  uint64_t applied_index, confirmed_index, pushed_index;
+  uint64_t prev_term, prev_vote, prev_commit; /* Peer.prevState */
+  uint64_t current_tick;
+  orc_mvec inbox;  /* MessageQueue contents */
+  uint32_t *inbox_from_slot;
+  size_t inbox_from_cap;
+  orc_evec props; /* incomingProposals */
+  int has_ri;
+  orc_ctx ri;
+  int hosted;
+  orc_mvec out;   /* ud.Messages of the last round */
+  orc_rtr *rtr;   /* ud.ReadyToReads of the last round */
+  size_t nrtr, caprtr;
+  orc_evec applyq; /* tasks pushed for the apply worker */
+} orc_node;
+
+struct orc_cluster {
+  orc_cluster_cfg cfg;
+  orc_node *nodes; /* [g * R + slot] */
+  uint64_t round;
+};
+
+static orc_node *node_at(orc_cluster *c, uint64_t g, uint32_t s) {
+  return &c->nodes[g * c->cfg.num_replicas + s];
+}
+
+static void msg_clone(orc_msg *dst, const orc_msg *src) {
+  *dst = *src;
+  memset(&dst->ents, 0, sizeof(dst->ents));
+  ev_copy_range(&dst->ents, src->ents.v, src->ents.n);
+}
+
+/* MessageQueue.Add (internal/server/message.go:105-123) */
+static void node_enqueue(orc_node *n, const orc_msg *m, uint32_t from_slot) {
+  orc_msg cp;
+  msg_clone(&cp, m);
+  if (n->inbox.n == n->inbox_from_cap) {
+    n->inbox_from_cap = n->inbox_from_cap ? n->inbox_from_cap * 2 : 8;
+    n->inbox_from_slot = (uint32_t *)realloc(
+        n->inbox_from_slot, n->inbox_from_cap * sizeof(uint32_t));
+  }
+  n->inbox_from_slot[n->inbox.n] = from_slot;
+  mv_push(&n->inbox, &cp);
+}
+
+/* ---- rsm apply (statemachine.go) ------------------------------------ */
+/* setApplied (statemachine.go:716-725) */
+static void sm_set_applied(orc_node *n, uint64_t index, uint64_t term) {
+  if (n->sm_index + 1 != index)
+    orc_panic("applied index %llu, new index %llu",
+              (unsigned long long)n->sm_index, (unsigned long long)index);
+  if (n->sm_term > term)
+    orc_panic("applied term %llu, new term %llu",
+              (unsigned long long)n->sm_term, (unsigned long long)term);
+  n->sm_index = index;
+  n->sm_term = term;
+}
+
+static int entry_is_session_managed(const orc_entry *e) {
+  /* IsSessionManaged (raftpb/raft.go:90-99) */
+  if (e->type == DRB_ENTRY_CONFIG_CHANGE) return 0;
+  return e->client_id != 0;
+}
+
+/* handleEntry (statemachine.go:935-969) -> update (1057-1103) ->
+ * KVTest.Update (kvtest.go:145-162).  Returns 1 if the KV was updated. */
+static int sm_handle_entry(orc_node *n, const orc_entry *e) {
+  uint32_t clen = e->cmd ? e->cmd->len : 0;
+  if (e->type == DRB_ENTRY_CONFIG_CHANGE) {
+    /* configChange (statemachine.go:1006-1019): membership is not on the
+     * fast path; the bootstrap AddNode entries name existing members so
+     * node.ApplyConfigChange only clears pendingConfigChange. */
+    sm_set_applied(n, e->index, e->term);
+    n->r->pending_config_change = 0;
+    return 0;
+  }
+  if (!entry_is_session_managed(e)) {
+    if (clen == 0) { /* noop (statemachine.go:1047-1054) */
+      sm_set_applied(n, e->index, e->term);
+      return 0;
+    }
+    orc_panic("not session managed, not empty");
+  }
+  /* IsNewSessionRequest / IsEndOfSessionRequest (raftpb/raft.go:108-126) */
+  if (clen == 0 && (e->series_id == UINT64_MAX - 1 ||
+                    e->series_id == UINT64_MAX))
+    orc_panic("session management is not on the fast path");
+  if (e->series_id != 0)
+    orc_panic("regular client sessions are not on the fast path");
+  /* update(): NoOP session -> GetPayload -> sm.Update; setApplied deferred */
+  const uint8_t *payload;
+  uint32_t plen;
+  switch (e->type) {
+    case DRB_ENTRY_APPLICATION:
+      payload = clen ? e->cmd->data : NULL;
+      plen = clen;
+      break;
+    case DRB_ENTRY_ENCODED: {
+      if (clen == 0) orc_panic("index out of range [0] with length 0");
+      uint8_t h = e->cmd->data[0];
+      uint8_t ver = h & 0xf0, ct = h & 0x0e;
+      int has_session = (h & 1) == 1;
+      if (ver != 0) orc_panic("unknown cmd encoding version");
+      if (has_session) orc_panic("v0 cmd has session info");
+      if (ct != 0) orc_panic("compressed payload is not on the fast path");
+      payload = e->cmd->data + 1;
+      plen = clen - 1;
+      break;
+    }
+    default:
+      orc_panic("unknown entry type");
+  }
+  /* KVTest.Update */
+  n->kv.count++;
+  const uint8_t *k, *v;
+  uint32_t kl, vl;
+  if (orc_pbkv_unmarshal(payload, plen, &k, &kl, &v, &vl))
+    orc_panic("PBKV unmarshal failed");
+  kv_update_store(&n->kv, k, kl, v, vl);
+  sm_set_applied(n, e->index, e->term);
+  return 1;
+}
+
+/* pb.EntriesToApply (raftpb/entry.go:27-47): index of the first entry to
+ * keep, or n when none */
+static size_t entries_to_apply_off(const orc_entry *ents, size_t n,
+                                   uint64_t applied, int strict) {
+  if (n == 0) return 0;
+  uint64_t last = ents[n - 1].index, first = ents[0].index;
+  if (last <= applied) {
+    if (strict)
+      orc_panic("got entries [%llu-%llu] older than current state %llu",
+                (unsigned long long)first, (unsigned long long)last,
+                (unsigned long long)applied);
+    return n;
+  }
+  if (first > applied + 1)
+    orc_panic("entry hole found: %llu, want: %llu", (unsigned long long)first,
+              (unsigned long long)(applied + 1));
+  if (applied - first + 1 < (uint64_t)n) return (size_t)(applied - first + 1);
+  return n;
+}
+
+/* StateMachine.Handle -> handle (statemachine.go:599-645, 877-906) for the
+ * pushed tasks (one task per round here), then setLastApplied. */
+static void sm_handle(orc_node *n, int is_leader, drb_round_out *out) {
+  if (n->applyq.n == 0) return;
+  size_t off = entries_to_apply_off(n->applyq.v, n->applyq.n, n->sm_index, 0);
+  const orc_entry *e = n->applyq.v + off;
+  size_t cnt = n->applyq.n - off;
+  for (size_t i = 0; i < cnt; i++) {
+    int upd = sm_handle_entry(n, &e[i]);
+    if (out) {
+      out->applied_entries++;
+      if (is_leader && upd) out->committed_entries++;
+    }
+  }
+  /* setLastApplied (statemachine.go:727-760) */
+  if (cnt > 0) {
+    for (size_t i = 1; i < cnt; i++) {
+      if (e[i].index != e[i - 1].index + 1) orc_panic("index gap found");
+      if (e[i].term < e[i - 1].term) orc_panic("term moving backward");
+    }
+    if (n->la_index + 1 != e[0].index) orc_panic("gap between batches");
+    if (n->la_term > e[0].term) orc_panic("invalid term");
+    n->la_index = e[cnt - 1].index;
+    n->la_term = e[cnt - 1].term;
+  }
+  ev_truncate(&n->applyq, 0);
+}
+
+/* ---- node-level event handling -------------------------------------- */
+static void node_tick(orc_node *n) {
+  /* node.tick (node.go:1562-1579): quiesce disabled -> Peer.Tick */
+  n->current_tick++;
+  raft_tick_public(n->r, 0);
+}
+
+/* stable order: all Replicate messages by sender slot, then every other
+ * message by sender slot (node_test.go:311-339 delivery order) */
+static void node_sort_inbox(orc_node *n) {
+  size_t cnt = n->inbox.n;
+  if (cnt < 2) return;
+  orc_msg *tmp = (orc_msg *)malloc(cnt * sizeof(orc_msg));
+  uint32_t *ts = (uint32_t *)malloc(cnt * sizeof(uint32_t));
+  size_t k = 0;
+  for (int pass = 0; pass < 2; pass++)
+    for (uint32_t s = 0; s <= ORC_MAX_PEERS; s++)
+      for (size_t i = 0; i < cnt; i++) {
+        int isrep = n->inbox.v[i].type == DRB_MSG_REPLICATE;
+        if ((pass == 0) != isrep) continue;
+        if (n->inbox_from_slot[i] != s) continue;
+        tmp[k] = n->inbox.v[i];
+        ts[k] = s;
+        k++;
+      }
+  memcpy(n->inbox.v, tmp, cnt * sizeof(orc_msg));
+  memcpy(n->inbox_from_slot, ts, cnt * sizeof(uint32_t));
+  free(tmp);
+  free(ts);
+}
+
+/* handleEvents (node.go:1161-1223) */
+static int node_handle_events(orc_node *n, int tick) {
+  orc_raft *r = n->r;
+  int has_event = 0;
+  /* updateAppliedIndex (node.go:1133-1137) */
+  n->applied_index = n->la_index;
+  r->applied = n->applied_index;
+  if (n->applied_index != n->confirmed_index) has_event = 1;
+  if (log_has_entries_to_apply(&r->log)) has_event = 1;
+  /* handleReadIndex (node.go:1296-1307) -> Peer.ReadIndex (peer.go:309) */
+  if (n->has_ri) {
+    orc_msg m;
+    memset(&m, 0, sizeof(m));
+    m.type = DRB_MSG_READ_INDEX;
+    m.hint = n->ri.low;
+    m.hint_high = n->ri.high;
+    raft_handle_msg(r, &m);
+    n->has_ri = 0;
+    has_event = 1;
+  }
+  /* handleReceivedMessages (node.go:1347-1377) */
+  node_sort_inbox(n);
+  if (tick) {
+    orc_msg t;
+    memset(&t, 0, sizeof(t));
+    t.type = DRB_MSG_LOCAL_TICK;
+    node_enqueue(n, &t, ORC_MAX_PEERS + 1);
+  }
+  size_t cnt = n->inbox.n;
+  for (size_t i = 0; i < cnt; i++) {
+    orc_msg *m = &n->inbox.v[i];
+    if (m->type == DRB_MSG_LOCAL_TICK)
+      node_tick(n);
+    else
+      peer_handle(r, m);
+  }
+  if (cnt > 0) has_event = 1;
+  mv_clear(&n->inbox);
+  /* handleProposals (node.go:1275-1294) -> Peer.ProposeEntries */
+  if (n->props.n > 0) {
+    orc_msg m;
+    memset(&m, 0, sizeof(m));
+    m.type = DRB_MSG_PROPOSE;
+    m.from = r->replica_id;
+    m.ents = n->props;
+    memset(&n->props, 0, sizeof(n->props));
+    raft_handle_msg(r, &m);
+    msg_free(&m);
+    has_event = 1;
+  }
+  return has_event;
+}
+
+typedef struct orc_update {
+  orc_evec save;
+  orc_evec committed;
+  orc_mvec msgs;
+  uint64_t last_applied;
+  int has_state;
+  uint64_t st_term, st_vote, st_commit;
+  size_t nrtr;
+  uint64_t uc_ready, uc_last_applied, uc_processed, uc_stable_to,
+      uc_stable_term;
+} orc_update;
+
+/* Peer.HasUpdate (peer.go:254-289) with moreToApply = true */
+static int peer_has_update(orc_node *n) {
+  orc_raft *r = n->r;
+  size_t ns;
+  log_entries_to_save(&r->log, &ns);
+  if (ns > 0) return 1;
+  if (r->leader_update) return 1;
+  if (r->msgs.n > 0) return 1;
+  if (log_has_entries_to_apply(&r->log)) return 1;
+  uint64_t t = r->term, v = r->vote, c = r->log.committed;
+  if (!(t == 0 && v == 0 && c == 0) &&
+      !(t == n->prev_term && v == n->prev_vote && c == n->prev_commit))
+    return 1;
+  if (r->nrtr != 0) return 1;
+  if (r->ndropped_entries > 0) return 1;
+  if (r->ndropped_ri > 0) return 1;
+  return 0;
+}
+
+/* node.getUpdate (node.go:1025-1042) -> Peer.GetUpdate (peer.go:198-208) */
+static int node_get_update(orc_node *n, orc_update *ud) {
+  orc_raft *r = n->r;
+  if (!(peer_has_update(n) || n->confirmed_index != n->applied_index))
+    return 0;
+  memset(ud, 0, sizeof(*ud));
+  size_t ns;
+  const orc_entry *s = log_entries_to_save(&r->log, &ns);
+  ev_copy_range(&ud->save, s, ns);
+  ud->msgs = r->msgs;
+  memset(&r->msgs, 0, sizeof(r->msgs));
+  for (size_t i = 0; i < ud->msgs.n; i++) ud->msgs.v[i].shard_id = r->shard_id;
+  ud->last_applied = n->applied_index;
+  if (log_entries_to_apply(&r->log, &ud->committed))
+    orc_panic("entriesToApply: log error");
+  if (!(r->term == n->prev_term && r->vote == n->prev_vote &&
+        r->log.committed == n->prev_commit)) {
+    ud->has_state = 1;
+    ud->st_term = r->term;
+    ud->st_vote = r->vote;
+    ud->st_commit = r->log.committed;
+  }
+  ud->nrtr = r->nrtr;
+  /* validateUpdate (peer.go:228-245) */
+  if (r->log.committed > 0 && ud->committed.n > 0 &&
+      ud->committed.v[ud->committed.n - 1].index > r->log.committed)
+    orc_panic("trying to apply not committed entry");
+  if (ud->committed.n > 0 && ud->save.n > 0 &&
+      ud->committed.v[ud->committed.n - 1].index >
+          ud->save.v[ud->save.n - 1].index)
+    orc_panic("trying to apply not saved entry");
+  /* getUpdateCommit (peer.go:432-449) */
+  ud->uc_ready = ud->nrtr;
+  ud->uc_last_applied = ud->last_applied;
+  if (ud->committed.n > 0)
+    ud->uc_processed = ud->committed.v[ud->committed.n - 1].index;
+  if (ud->save.n > 0) {
+    ud->uc_stable_to = ud->save.v[ud->save.n - 1].index;
+    ud->uc_stable_term = ud->save.v[ud->save.n - 1].term;
+  }
+  n->confirmed_index = n->applied_index;
+  return 1;
+}
+
+/* Peer.Commit (peer.go:292-305) */
+static void peer_commit(orc_node *n, orc_update *ud) {
+  orc_raft *r = n->r;
+  raft_clear_msgs(r);
+  r->leader_update = 0;
+  r->ndropped_entries = 0;
+  r->ndropped_ri = 0;
+  if (ud->has_state && !(ud->st_term == 0 && ud->st_vote == 0 &&
+                         ud->st_commit == 0)) {
+    n->prev_term = ud->st_term;
+    n->prev_vote = ud->st_vote;
+    n->prev_commit = ud->st_commit;
+  }
+  if (ud->uc_ready > 0) r->nrtr = 0; /* clearReadyToRead */
+  log_commit_update(&r->log, ud->uc_stable_to, ud->uc_stable_term,
+                    ud->uc_processed, ud->uc_last_applied);
+}
+
+static void update_free(orc_update *ud) {
+  ev_free(&ud->save);
+  ev_free(&ud->committed);
+  mv_free(&ud->msgs);
+}
+
+/* deliver one message to its target replica of the same group */
+static void deliver(orc_cluster *c, uint64_t g, uint32_t from_slot,
+                    const orc_msg *m) {
+  if (m->to < 1 || m->to > c->cfg.num_replicas) return;
+  /* an unhosted target is served by the outbound boundary; what sits in
+   * its queue is dropped unless it is hosted again for the next round
+   * (the device mailbox has the same lifetime) */
+  node_enqueue(node_at(c, g, (uint32_t)(m->to - 1)), m, from_slot);
+}
+
+/* one step() (node_test.go:274-353) for group g */
+static void group_round(orc_cluster *c, uint64_t g, int tick,
+                        drb_round_out *out) {
+  uint32_t R = c->cfg.num_replicas;
+  orc_update uds[ORC_MAX_PEERS];
+  int have[ORC_MAX_PEERS];
+  memset(have, 0, sizeof(have));
+  for (uint32_t s = 0; s < R; s++) {
+    orc_node *n = node_at(c, g, s);
+    mv_clear(&n->out);
+    n->nrtr = 0;
+    if (!n->hosted) {
+      mv_clear(&n->inbox);
+      continue;
+    }
+    if (node_handle_events(n, tick)) have[s] = node_get_update(n, &uds[s]);
+  }
+  /* applyRaftUpdates / sendReplicateMessages / processReadyToRead */
+  for (uint32_t s = 0; s < R; s++) {
+    if (!have[s]) continue;
+    orc_node *n = node_at(c, g, s);
+    orc_update *ud = &uds[s];
+    size_t off = entries_to_apply_off(ud->committed.v, ud->committed.n,
+                                      n->pushed_index, 1);
+    if (off < ud->committed.n) {
+      ev_copy_range(&n->applyq, ud->committed.v + off, ud->committed.n - off);
+      n->pushed_index = ud->committed.v[ud->committed.n - 1].index;
+    }
+    for (size_t i = 0; i < ud->msgs.n; i++)
+      if (ud->msgs.v[i].type == DRB_MSG_REPLICATE)
+        deliver(c, g, s, &ud->msgs.v[i]);
+    orc_raft *r = n->r;
+    if (ud->nrtr) {
+      if (n->caprtr < ud->nrtr) {
+        n->caprtr = ud->nrtr;
+        n->rtr = (orc_rtr *)realloc(n->rtr, n->caprtr * sizeof(orc_rtr));
+      }
+      memcpy(n->rtr, r->rtr, ud->nrtr * sizeof(orc_rtr));
+      n->nrtr = ud->nrtr;
+      if (out) out->ready_to_reads += ud->nrtr;
+    }
+    if (out) {
+      out->messages += ud->msgs.n;
+      out->dropped_read_indexes += r->ndropped_ri;
+    }
+  }
+  /* SaveRaftState, processRaftUpdate, commitRaftUpdate, sm.Handle */
+  for (uint32_t s = 0; s < R; s++) {
+    if (!have[s]) continue;
+    orc_node *n = node_at(c, g, s);
+    orc_update *ud = &uds[s];
+    db_append(n->db, ud->save.v, ud->save.n); /* LogReader.Append */
+    for (size_t i = 0; i < ud->msgs.n; i++)
+      if (ud->msgs.v[i].type != DRB_MSG_REPLICATE)
+        deliver(c, g, s, &ud->msgs.v[i]);
+    peer_commit(n, ud);
+    sm_handle(n, n->r->state == DRB_LEADER, out);
+    if (c->cfg.logdb_keep && n->db->ents.n > 2 * c->cfg.logdb_keep) {
+      uint64_t keep_from = n->r->log.processed;
+      uint64_t lim = n->db->marker_index + n->db->ents.n - c->cfg.logdb_keep;
+      if (keep_from > lim) keep_from = lim;
+      if (keep_from > n->db->marker_index) orc_logdb_compact(n->db, keep_from);
+    }
+    /* the outbox of this round (ud.Messages) */
+    n->out = ud->msgs;
+    memset(&ud->msgs, 0, sizeof(ud->msgs));
+    update_free(ud);
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* cluster API                                                          */
+/* ------------------------------------------------------------------ */
+static uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg) {
+  if (cfg->num_replicas < 1 || cfg->num_replicas > DRB_MAX_REPLICAS)
+    return NULL;
+  orc_cluster *c = (orc_cluster *)calloc(1, sizeof(orc_cluster));
+  c->cfg = *cfg;
+  uint64_t R = cfg->num_replicas;
+  c->nodes = (orc_node *)calloc(cfg->num_groups * R, sizeof(orc_node));
+  jmp_buf jb;
+  jmp_buf *prev = orc_jb;
+  orc_jb = &jb;
+  if (setjmp(jb)) {
+    orc_jb = prev;
+    return NULL;
+  }
+  for (uint64_t g = 0; g < cfg->num_groups; g++)
+    for (uint32_t s = 0; s < R; s++) {
+      orc_node *n = node_at(c, g, s);
+      n->db = orc_logdb_new();
+      n->r = raft_new(cfg->first_shard_id + g, s + 1, cfg->election_rtt,
+                      cfg->heartbeat_rtt, (int)cfg->check_quorum, n->db,
+                      mix64(cfg->seed ^ (g * R + s)));
+      n->hosted = 1;
+    }
+  orc_jb = prev;
+  return c;
+}
+
+void orc_cluster_free(orc_cluster *c) {
+  if (!c) return;
+  uint64_t N = c->cfg.num_groups * c->cfg.num_replicas;
+  for (uint64_t i = 0; i < N; i++) {
+    orc_node *n = &c->nodes[i];
+    raft_free(n->r);
+    orc_logdb_free(n->db);
+    kv_free(&n->kv);
+    mv_free(&n->inbox);
+    free(n->inbox_from_slot);
+    ev_free(&n->props);
+    mv_free(&n->out);
+    free(n->rtr);
+    ev_free(&n->applyq);
+  }
+  free(c->nodes);
+  free(c);
+}
+
+/* Launch (peer.go:64-79) with initial && newNode, then bootstrap, then an
+ * election of leader_slot (its election timer fired), then rounds until
+ * no messages move.  The randomized election timeouts are finally set to
+ * a documented formula so the device-side initialiser can reproduce them
+ * (they are random in the reference: raft.go:658-661). */
+int orc_cluster_setup_steady(orc_cluster *c, uint32_t leader_slot) {
+  ORC_TRY(-1);
+  uint32_t R = c->cfg.num_replicas;
+  if (leader_slot >= R) orc_panic("bad leader slot");
+  uint64_t ids[ORC_MAX_PEERS];
+  orc_blob *cmds[ORC_MAX_PEERS];
+  for (uint32_t s = 0; s < R; s++) {
+    ids[s] = s + 1;
+    char addr[32];
+    uint8_t buf[64];
+    snprintf(addr, sizeof(addr), "localhost:%u", 26000 + s);
+    size_t l = orc_configchange_marshal_addnode(s + 1, addr, buf);
+    cmds[s] = blob_new(buf, (uint32_t)l);
+  }
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++)
+    for (uint32_t s = 0; s < R; s++) {
+      orc_node *n = node_at(c, g, s);
+      /* Launch: becomeFollower(1, NoLeader) then bootstrap */
+      raft_become_follower(n->r, 1, 0);
+      raft_bootstrap(n->r, ids, (int)R, cmds);
+    }
+  for (uint32_t s = 0; s < R; s++) blob_unref(cmds[s]);
+  ORC_END;
+  /* round: apply the bootstrap entries */
+  drb_round_out o;
+  memset(&o, 0, sizeof(o));
+  if (orc_cluster_round(c, 0, &o)) return -1;
+  /* leader's election timer fires on the next tick */
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++) {
+    orc_raft *r = node_at(c, g, leader_slot)->r;
+    r->election_tick = r->randomized_election_timeout - 1;
+  }
+  if (orc_cluster_round(c, 1, &o)) return -1;
+  for (int i = 0; i < 64; i++) {
+    memset(&o, 0, sizeof(o));
+    if (orc_cluster_round(c, 0, &o)) return -1;
+    if (o.messages == 0) break;
+  }
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++)
+    for (uint32_t s = 0; s < R; s++) {
+      orc_raft *r = node_at(c, g, s)->r;
+      uint64_t e = c->cfg.election_rtt;
+      r->randomized_election_timeout =
+          e + mix64(c->cfg.seed ^ (0xE1ull << 56) ^ (g * R + s)) % e;
+    }
+  return 0;
+}
+
+int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
+                                uint32_t max_per_group, const drb_entry *ents,
+                                const uint8_t *pool) {
+  uint32_t R = c->cfg.num_replicas;
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++) {
+    if (!counts[g]) continue;
+    /* routed to the group's leader replica (the NodeHost holding it) */
+    orc_node *ln = NULL;
+    for (uint32_t s = 0; s < R; s++) {
+      orc_node *n = node_at(c, g, s);
+      if (n->hosted && n->r->state == DRB_LEADER) ln = n;
+    }
+    if (!ln) continue;
+    for (uint32_t j = 0; j < counts[g]; j++) {
+      orc_entry e = entry_from_view(&ents[g * max_per_group + j], pool);
+      e.term = 0;
+      e.index = 0;
+      ev_push(&ln->props, &e);
+      blob_unref(e.cmd);
+    }
+  }
+  return 0;
+}
+
+int orc_cluster_stage_read_index(orc_cluster *c, const uint64_t *low,
+                                 const uint64_t *high) {
+  uint32_t R = c->cfg.num_replicas;
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++) {
+    if (!low[g]) continue;
+    for (uint32_t s = 0; s < R; s++) {
+      orc_node *n = node_at(c, g, s);
+      if (n->hosted && n->r->state == DRB_LEADER) {
+        n->has_ri = 1;
+        n->ri.low = low[g];
+        n->ri.high = high[g];
+      }
+    }
+  }
+  return 0;
+}
+
+int orc_cluster_ingest(orc_cluster *c, const drb_message *m, size_t n,
+                       const drb_entry *ents, const uint8_t *pool) {
+  for (size_t i = 0; i < n; i++) {
+    uint64_t g = m[i].shard_id - c->cfg.first_shard_id;
+    if (g >= c->cfg.num_groups) continue;
+    if (m[i].to < 1 || m[i].to > c->cfg.num_replicas) continue;
+    if (m[i].from < 1 || m[i].from > c->cfg.num_replicas) continue;
+    orc_node *t = node_at(c, g, (uint32_t)(m[i].to - 1));
+    if (!t->hosted) continue;
+    if (node_at(c, g, (uint32_t)(m[i].from - 1))->hosted) continue;
+    orc_msg mm = orc_msg_from_view(&m[i], ents, pool);
+    node_enqueue(t, &mm, (uint32_t)(m[i].from - 1));
+    msg_free(&mm);
+  }
+  return 0;
+}
+
+int orc_cluster_round_range(orc_cluster *c, int tick, uint64_t g0, uint64_t g1,
+                            drb_round_out *out) {
+  ORC_TRY(-1);
+  for (uint64_t g = g0; g < g1 && g < c->cfg.num_groups; g++)
+    group_round(c, g, tick, out);
+  ORC_END;
+  return 0;
+}
+
+int orc_cluster_end_round(orc_cluster *c) {
+  c->round++;
+  return 0;
+}
+
+int orc_cluster_round(orc_cluster *c, int tick, drb_round_out *out) {
+  if (out) out->round = c->round;
+  int rc = orc_cluster_round_range(c, tick, 0, c->cfg.num_groups, out);
+  orc_cluster_end_round(c);
+  return rc;
+}
+
+int orc_cluster_export(orc_cluster *c, uint64_t g, uint32_t slot,
+                       drb_replica_state *st) {
+  if (g >= c->cfg.num_groups || slot >= c->cfg.num_replicas) return -1;
+  orc_node *n = node_at(c, g, slot);
+  orc_raft_info(n->r, st);
+  st->applied_index = n->applied_index;
+  st->confirmed_index = n->confirmed_index;
+  st->pushed_index = n->pushed_index;
+  st->prev_term = n->prev_term;
+  st->prev_vote = n->prev_vote;
+  st->prev_commit = n->prev_commit;
+  st->sm_index = n->sm_index;
+  st->sm_term = n->sm_term;
+  st->kv_count = n->kv.count;
+  st->flags = n->hosted ? DRB_F_HOSTED : 0;
+  return 0;
+}
+
+long orc_cluster_export_log(orc_cluster *c, uint64_t g, uint32_t slot,
+                            uint64_t lo, uint64_t hi, drb_entry *out,
+                            uint8_t *pool, size_t pool_cap) {
+  orc_node *n = node_at(c, g, slot);
+  orc_log *l = &n->r->log;
+  size_t pu = 0, k = 0;
+  for (uint64_t i = lo; i <= hi; i++) {
+    const orc_entry *e = NULL;
+    if (i >= l->im.marker_index && i < l->im.marker_index + l->im.ents.n)
+      e = &l->im.ents.v[i - l->im.marker_index];
+    else if (i > l->db->marker_index &&
+             i <= l->db->marker_index + l->db->ents.n)
+      e = &l->db->ents.v[i - l->db->marker_index - 1];
+    if (!e) return -1;
+    if (entry_to_view(e, &out[k++], pool, pool_cap, &pu)) return -2;
+  }
+  return (long)k;
+}
+
+long orc_cluster_export_outbox(orc_cluster *c, uint64_t g, uint32_t slot,
+                               drb_message *out, size_t cap, drb_entry *ents,
+                               size_t ent_cap, uint8_t *pool,
+                               size_t pool_cap) {
+  orc_node *n = node_at(c, g, slot);
+  if (n->out.n > cap) return (long)n->out.n;
+  size_t eu = 0, pu = 0;
+  for (size_t i = 0; i < n->out.n; i++)
+    if (msg_to_view(&n->out.v[i], &out[i], ents, ent_cap, &eu, pool, pool_cap,
+                    &pu))
+      return -2;
+  return (long)n->out.n;
+}
+
+long orc_cluster_export_kv(orc_cluster *c, uint64_t g, uint32_t slot,
+                           uint8_t *keys, uint32_t *klens, uint8_t *vals,
+                           uint32_t *vlens, size_t cap, size_t key_cap,
+                           size_t val_cap) {
+  orc_node *n = node_at(c, g, slot);
+  size_t k = 0;
+  for (size_t i = 0; i < n->kv.cap; i++) {
+    kv_item *it = &n->kv.t[i];
+    if (!it->used) continue;
+    if (k >= cap) return (long)n->kv.n;
+    if (it->klen > key_cap || it->vlen > val_cap) return -2;
+    memcpy(keys + k * key_cap, it->key, it->klen);
+    klens[k] = it->klen;
+    memcpy(vals + k * val_cap, it->val, it->vlen);
+    vlens[k] = it->vlen;
+    k++;
+  }
+  return (long)k;
+}
+
+long orc_cluster_export_ready(orc_cluster *c, uint64_t g, uint32_t slot,
+                              drb_ready_to_read *out, size_t cap) {
+  orc_node *n = node_at(c, g, slot);
+  size_t k = n->nrtr < cap ? n->nrtr : cap;
+  for (size_t i = 0; i < k; i++) {
+    out[i].shard_id = n->r->shard_id;
+    out[i].replica_id = n->r->replica_id;
+    out[i].index = n->rtr[i].index;
+    out[i].ctx_low = n->rtr[i].ctx.low;
+    out[i].ctx_high = n->rtr[i].ctx.high;
+  }
+  return (long)n->nrtr;
+}
+
+int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
+                           int hosted) {
+  node_at(c, g, slot)->hosted = hosted;
+  return 0;
+}
+
+int orc_cluster_kv_lookup(orc_cluster *c, uint64_t g, uint32_t slot,
+                          const uint8_t *key, uint32_t klen, uint8_t *val,
+                          uint32_t cap, uint32_t *vlen) {
+  const kv_item *it = kv_find(&node_at(c, g, slot)->kv, key, klen);
+  if (!it) return 1;
+  *vlen = it->vlen;
+  if (it->vlen > cap) return -1;
+  memcpy(val, it->val, it->vlen);
+  return 0;
+}

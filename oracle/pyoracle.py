@@ -1,0 +1,669 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never by the dragonboat_amd product path.
+"""
+import ctypes as C
+import os
+import subprocess
+
+from dragonboat_amd.abi import (Entry, Message, ReadyToRead, ReplicaState,
+                                RoundOut, entry_to_tuple, message_to_tuple)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+class Remote(C.Structure):
+    """remote (internal/raft/remote.go:72-80)."""
+    _fields_ = [("match", C.c_uint64), ("next", C.c_uint64),
+                ("snapshot_index", C.c_uint64), ("state", C.c_uint32),
+                ("active", C.c_int)]
+
+
+class ClusterCfg(C.Structure):
+    _fields_ = [("num_groups", C.c_uint64), ("first_shard_id", C.c_uint64),
+                ("num_replicas", C.c_uint32), ("election_rtt", C.c_uint32),
+                ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
+                ("seed", C.c_uint64), ("logdb_keep", C.c_uint64)]
+
+
+P = C.c_void_p
+U64 = C.c_uint64
+U32 = C.c_uint32
+PU64 = C.POINTER(C.c_uint64)
+PU32 = C.POINTER(C.c_uint32)
+PU8 = C.POINTER(C.c_uint8)
+PE = C.POINTER(Entry)
+PM = C.POINTER(Message)
+PR = C.POINTER(Remote)
+
+
+def _declare(L):
+    sig = {
+        "orc_last_error": (C.c_char_p, []),
+        "orc_remote_become_retry": (None, [PR]),
+        "orc_remote_retry_to_wait": (None, [PR]),
+        "orc_remote_wait_to_retry": (None, [PR]),
+        "orc_remote_become_wait": (None, [PR]),
+        "orc_remote_become_replicate": (None, [PR]),
+        "orc_remote_become_snapshot": (None, [PR, U64]),
+        "orc_remote_try_update": (C.c_int, [PR, U64]),
+        "orc_remote_progress": (C.c_int, [PR, U64]),
+        "orc_remote_responded_to": (None, [PR]),
+        "orc_remote_decrease_to": (C.c_int, [PR, U64, U64]),
+        "orc_remote_is_paused": (C.c_int, [PR]),
+        "orc_readindex_new": (P, []),
+        "orc_readindex_free": (None, [P]),
+        "orc_readindex_add_request": (C.c_int, [P, U64, U64, U64, U64]),
+        "orc_readindex_len": (C.c_size_t, [P]),
+        "orc_readindex_get": (C.c_int, [P, C.c_size_t, PU64, PU64, PU64, PU64]),
+        "orc_readindex_confirm": (C.c_int, [P, U64, U64, U64, C.c_int, PU64,
+                                            PU64, PU64, PU64, C.c_int]),
+        "orc_readindex_push_raw_queue": (C.c_int, [P, U64, U64, C.c_int]),
+        "orc_sort_match_values": (None, [PU64, C.c_int]),
+        "orc_logdb_new": (P, []),
+        "orc_logdb_free": (None, [P]),
+        "orc_logdb_append": (C.c_int, [P, PE, C.c_size_t, PU8]),
+        "orc_logdb_compact": (C.c_int, [P, U64]),
+        "orc_logdb_set_state": (None, [P, U64, U64, U64]),
+        "orc_raft_new_test": (P, [U64, PU64, C.c_int, U64, U64, P]),
+        "orc_raft_free": (None, [P]),
+        "orc_raft_handle": (C.c_int, [P, PM, PE, PU8]),
+        "orc_raft_peer_handle": (C.c_int, [P, PM, PE, PU8]),
+        "orc_raft_become_follower": (C.c_int, [P, U64, U64]),
+        "orc_raft_become_candidate": (C.c_int, [P]),
+        "orc_raft_become_leader": (C.c_int, [P]),
+        "orc_raft_load_state": (C.c_int, [P, U64, U64, U64]),
+        "orc_raft_broadcast_replicate": (C.c_int, [P]),
+        "orc_raft_broadcast_heartbeat": (C.c_int, [P]),
+        "orc_raft_try_commit": (C.c_int, [P]),
+        "orc_raft_tick": (C.c_int, [P]),
+        "orc_raft_campaign": (C.c_int, [P]),
+        "orc_raft_set_randomized_election_timeout": (None, [P, U64]),
+        "orc_raft_network_reset": (C.c_int, [P, U64, PU64, C.c_int]),
+        "orc_raft_read_messages": (C.c_long, [P, PM, C.c_size_t, PE,
+                                              C.c_size_t, PU8, C.c_size_t]),
+        "orc_raft_log_entries": (C.c_long, [P, C.c_int, PE, C.c_size_t, PU8,
+                                            C.c_size_t]),
+        "orc_raft_log_term": (C.c_int, [P, U64, PU64]),
+        "orc_raft_info": (None, [P, C.POINTER(ReplicaState)]),
+        "orc_raft_remote": (C.c_int, [P, U64, PR]),
+        "orc_raft_set_remote": (C.c_int, [P, U64, PR]),
+        "orc_raft_ready_to_read": (C.c_size_t, [P, PU64, PU64, PU64,
+                                                C.c_size_t]),
+        "orc_raft_dropped_read_indexes": (C.c_size_t, [P]),
+        "orc_log_commit_to": (C.c_int, [P, U64]),
+        "orc_log_try_commit": (C.c_int, [P, U64, U64]),
+        "orc_log_match_term": (C.c_int, [P, U64, U64]),
+        "orc_log_up_to_date": (C.c_int, [P, U64, U64]),
+        "orc_log_conflict_index": (C.c_long, [P, PE, C.c_size_t]),
+        "orc_log_try_append": (C.c_int, [P, U64, PE, C.c_size_t, PU8]),
+        "orc_log_append": (C.c_int, [P, PE, C.c_size_t, PU8]),
+        "orc_log_commit_update": (C.c_int, [P, U64, U64, U64, U64]),
+        "orc_cluster_new": (P, [C.POINTER(ClusterCfg)]),
+        "orc_cluster_free": (None, [P]),
+        "orc_cluster_setup_steady": (C.c_int, [P, U32]),
+        "orc_cluster_stage_proposals": (C.c_int, [P, PU32, U32, PE, PU8]),
+        "orc_cluster_stage_read_index": (C.c_int, [P, PU64, PU64]),
+        "orc_cluster_ingest": (C.c_int, [P, PM, C.c_size_t, PE, PU8]),
+        "orc_cluster_round": (C.c_int, [P, C.c_int, C.POINTER(RoundOut)]),
+        "orc_cluster_round_range": (C.c_int, [P, C.c_int, U64, U64,
+                                              C.POINTER(RoundOut)]),
+        "orc_cluster_end_round": (C.c_int, [P]),
+        "orc_cluster_export": (C.c_int, [P, U64, U32,
+                                         C.POINTER(ReplicaState)]),
+        "orc_cluster_export_log": (C.c_long, [P, U64, U32, U64, U64, PE, PU8,
+                                              C.c_size_t]),
+        "orc_cluster_export_outbox": (C.c_long, [P, U64, U32, PM, C.c_size_t,
+                                                 PE, C.c_size_t, PU8,
+                                                 C.c_size_t]),
+        "orc_cluster_export_kv": (C.c_long, [P, U64, U32, PU8, PU32, PU8, PU32,
+                                             C.c_size_t, C.c_size_t,
+                                             C.c_size_t]),
+        "orc_cluster_export_ready": (C.c_long, [P, U64, U32,
+                                                C.POINTER(ReadyToRead),
+                                                C.c_size_t]),
+        "orc_cluster_set_hosted": (C.c_int, [P, U64, U32, C.c_int]),
+        "orc_cluster_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32,
+                                            PU32]),
+        "orc_entry_size": (C.c_size_t, [PE]),
+        "orc_entry_marshal": (C.c_size_t, [PE, PU8, PU8]),
+        "orc_entry_unmarshal": (C.c_long, [PU8, C.c_size_t, PE, PU8,
+                                           C.c_size_t, C.POINTER(C.c_size_t)]),
+        "orc_entrybatch_size": (C.c_size_t, [PE, C.c_size_t]),
+        "orc_entrybatch_marshal": (C.c_size_t, [PE, C.c_size_t, PU8, PU8]),
+        "orc_entrybatch_unmarshal": (C.c_long, [PU8, C.c_size_t, PE,
+                                                C.c_size_t, PU8, C.c_size_t]),
+        "orc_crc32_ieee": (C.c_uint32, [PU8, C.c_size_t]),
+        "orc_pbkv_marshal": (C.c_size_t, [PU8, U32, PU8, U32, PU8]),
+        "orc_pbkv_unmarshal": (C.c_int, [PU8, C.c_size_t,
+                                         C.POINTER(PU8), PU32,
+                                         C.POINTER(PU8), PU32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+class OracleError(RuntimeError):
+    """The reference would have panicked (plog.Panicf / panic)."""
+
+
+def _check(rc):
+    if rc == -1:
+        raise OracleError(lib().orc_last_error().decode())
+    return rc
+
+
+def _u8(buf):
+    return (C.c_uint8 * max(1, len(buf))).from_buffer_copy(buf or b"\0")
+
+
+# ---------------------------------------------------------------- entries
+class EntryPool:
+    """Builds drb_entry arrays + a Cmd byte pool from python tuples/dicts."""
+
+    def __init__(self, entries=()):
+        self.items = []
+        self.pool = bytearray()
+        for e in entries:
+            self.add(**e) if isinstance(e, dict) else self.add(*e)
+
+    def add(self, term=0, index=0, type=0, key=0, client_id=0, series_id=0,
+            responded_to=0, cmd=b""):
+        self.items.append(Entry(term, index, key, client_id, series_id,
+                                responded_to, type, len(cmd), len(self.pool)))
+        self.pool += bytes(cmd)
+
+    def arrays(self):
+        n = len(self.items)
+        arr = (Entry * max(1, n))(*self.items)
+        return arr, _u8(bytes(self.pool)), n
+
+
+def ent(term=0, index=0, type=0, key=0, client_id=0, series_id=0,
+        responded_to=0, cmd=b""):
+    return dict(term=term, index=index, type=type, key=key,
+                client_id=client_id, series_id=series_id,
+                responded_to=responded_to, cmd=cmd)
+
+
+def msg(type, from_=0, to=0, term=0, log_term=0, log_index=0, commit=0,
+        reject=False, hint=0, hint_high=0, entries=(), shard_id=0):
+    return dict(type=type, from_=from_, to=to, term=term, log_term=log_term,
+                log_index=log_index, commit=commit, reject=int(bool(reject)),
+                hint=hint, hint_high=hint_high, entries=list(entries),
+                shard_id=shard_id)
+
+
+def build_messages(msgs):
+    ep = EntryPool()
+    out = []
+    for m in msgs:
+        off = len(ep.items)
+        for e in m["entries"]:
+            ep.add(**e)
+        out.append(Message(m["shard_id"], m["from_"], m["to"], m["term"],
+                           m["log_term"], m["log_index"], m["commit"],
+                           m["hint"], m["hint_high"], m["type"], m["reject"],
+                           len(m["entries"]), off))
+    marr = (Message * max(1, len(out)))(*out)
+    earr, pool, _ = ep.arrays()
+    return marr, len(out), earr, pool
+
+
+def _unpack_messages(marr, n, earr, pool):
+    res = []
+    for i in range(n):
+        m = marr[i]
+        t = message_to_tuple(m, earr, pool)
+        res.append(dict(shard_id=t[0], from_=t[1], to=t[2], type=t[3],
+                        term=t[4], log_term=t[5], log_index=t[6], commit=t[7],
+                        reject=bool(t[8]), hint=t[9], hint_high=t[10],
+                        entries=[_etuple_to_dict(x) for x in t[11]]))
+    return res
+
+
+def _etuple_to_dict(t):
+    return dict(term=t[0], index=t[1], type=t[2], key=t[3], client_id=t[4],
+                series_id=t[5], responded_to=t[6], cmd=t[7])
+
+
+# ---------------------------------------------------------------- remote
+def new_remote(match=0, next=0, state=0, snapshot_index=0, active=0):
+    return Remote(match, next, snapshot_index, state, active)
+
+
+# ---------------------------------------------------------------- readIndex
+class ReadIndexQ:
+    def __init__(self):
+        self.p = lib().orc_readindex_new()
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_readindex_free(self.p)
+
+    def add_request(self, index, ctx, from_):
+        _check(lib().orc_readindex_add_request(self.p, index, ctx[0], ctx[1],
+                                               from_))
+
+    def __len__(self):
+        return lib().orc_readindex_len(self.p)
+
+    def items(self):
+        out = []
+        for i in range(len(self)):
+            a, b, c, d = U64(), U64(), U64(), U64()
+            lib().orc_readindex_get(self.p, i, a, b, c, d)
+            out.append(((a.value, b.value), c.value, d.value))
+        return out
+
+    def confirm(self, ctx, from_, quorum):
+        cap = 64
+        lo, hi, ix, fr = [(U64 * cap)() for _ in range(4)]
+        n = _check(lib().orc_readindex_confirm(self.p, ctx[0], ctx[1], from_,
+                                               quorum, lo, hi, ix, fr, cap))
+        return [((lo[i], hi[i]), ix[i], fr[i]) for i in range(n)]
+
+    def push_raw(self, ctx, front=False):
+        lib().orc_readindex_push_raw_queue(self.p, ctx[0], ctx[1], int(front))
+
+
+def sort_match_values(vals):
+    arr = (U64 * len(vals))(*vals)
+    lib().orc_sort_match_values(arr, len(vals))
+    return list(arr)
+
+
+# ---------------------------------------------------------------- raft
+class LogDB:
+    """TestLogDB (internal/raft/logdb_test.go:24-170)."""
+
+    def __init__(self, entries=()):
+        self.p = lib().orc_logdb_new()
+        if entries:
+            self.append(entries)
+
+    def append(self, entries):
+        arr, pool, n = EntryPool(entries).arrays()
+        _check(lib().orc_logdb_append(self.p, arr, n, pool))
+
+    def compact(self, index):
+        return lib().orc_logdb_compact(self.p, index)
+
+    def set_state(self, term=0, vote=0, commit=0):
+        lib().orc_logdb_set_state(self.p, term, vote, commit)
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_logdb_free(self.p)
+
+
+class TestRaft:
+    """newTestRaft (internal/raft/raft_etcd_test.go:3071)."""
+
+    __test__ = False  # not a pytest class
+
+    def __init__(self, id, peers, election, heartbeat, logdb=None):
+        self.logdb = logdb or LogDB()
+        ps = (U64 * max(1, len(peers)))(*peers)
+        self.p = lib().orc_raft_new_test(id, ps, len(peers), election,
+                                         heartbeat, self.logdb.p)
+        if not self.p:
+            raise OracleError(lib().orc_last_error().decode())
+        self.id = id
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_raft_free(self.p)
+
+    def handle(self, m):
+        marr, n, earr, pool = build_messages([m])
+        _check(lib().orc_raft_handle(self.p, marr, earr, pool))
+
+    def peer_handle(self, m):
+        marr, n, earr, pool = build_messages([m])
+        _check(lib().orc_raft_peer_handle(self.p, marr, earr, pool))
+
+    def become_follower(self, term, leader):
+        _check(lib().orc_raft_become_follower(self.p, term, leader))
+
+    def become_candidate(self):
+        _check(lib().orc_raft_become_candidate(self.p))
+
+    def become_leader(self):
+        _check(lib().orc_raft_become_leader(self.p))
+
+    def load_state(self, term=0, vote=0, commit=0):
+        _check(lib().orc_raft_load_state(self.p, term, vote, commit))
+
+    def broadcast_replicate(self):
+        _check(lib().orc_raft_broadcast_replicate(self.p))
+
+    def broadcast_heartbeat(self):
+        _check(lib().orc_raft_broadcast_heartbeat(self.p))
+
+    def try_commit(self):
+        return bool(_check(lib().orc_raft_try_commit(self.p)))
+
+    def tick(self):
+        _check(lib().orc_raft_tick(self.p))
+
+    def campaign(self):
+        _check(lib().orc_raft_campaign(self.p))
+
+    def set_randomized_election_timeout(self, v):
+        lib().orc_raft_set_randomized_election_timeout(self.p, v)
+
+    def network_reset(self, id, ids):
+        arr = (U64 * len(ids))(*ids)
+        _check(lib().orc_raft_network_reset(self.p, id, arr, len(ids)))
+        self.id = id
+
+    def read_messages(self):
+        cap, ecap, pcap = 256, 4096, 1 << 20
+        marr = (Message * cap)()
+        earr = (Entry * ecap)()
+        pool = (C.c_uint8 * pcap)()
+        n = lib().orc_raft_read_messages(self.p, marr, cap, earr, ecap, pool,
+                                         pcap)
+        if n < 0 or n > cap:
+            raise OracleError("read_messages failed %d" % n)
+        return _unpack_messages(marr, n, earr, pool)
+
+    def _entries(self, which):
+        cap, pcap = 4096, 1 << 20
+        arr = (Entry * cap)()
+        pool = (C.c_uint8 * pcap)()
+        n = lib().orc_raft_log_entries(self.p, which, arr, cap, pool, pcap)
+        if n == -1:
+            raise OracleError(lib().orc_last_error().decode())
+        if n < 0:
+            raise OracleError("log entries failed %d" % n)
+        return [_etuple_to_dict(entry_to_tuple(arr[i], pool))
+                for i in range(n)]
+
+    def entries_to_apply(self):
+        return self._entries(0)
+
+    def entries_to_save(self):
+        return self._entries(1)
+
+    def all_entries(self):
+        return self._entries(2)
+
+    def term(self, index):
+        t = U64()
+        rc = _check(lib().orc_raft_log_term(self.p, index, t))
+        return rc, t.value
+
+    def info(self):
+        st = ReplicaState()
+        lib().orc_raft_info(self.p, st)
+        return st
+
+    def remote(self, id):
+        r = Remote()
+        if lib().orc_raft_remote(self.p, id, r):
+            raise KeyError(id)
+        return r
+
+    def set_remote(self, id, r):
+        lib().orc_raft_set_remote(self.p, id, r)
+
+    def ready_to_read(self):
+        cap = 64
+        a, b, c = (U64 * cap)(), (U64 * cap)(), (U64 * cap)()
+        n = lib().orc_raft_ready_to_read(self.p, a, b, c, cap)
+        return [(a[i], (b[i], c[i])) for i in range(min(n, cap))]
+
+    def dropped_read_indexes(self):
+        return lib().orc_raft_dropped_read_indexes(self.p)
+
+    # entryLog hooks
+    def commit_to(self, index):
+        _check(lib().orc_log_commit_to(self.p, index))
+
+    def log_try_commit(self, index, term):
+        return bool(_check(lib().orc_log_try_commit(self.p, index, term)))
+
+    def match_term(self, index, term):
+        return bool(_check(lib().orc_log_match_term(self.p, index, term)))
+
+    def up_to_date(self, index, term):
+        return bool(_check(lib().orc_log_up_to_date(self.p, index, term)))
+
+    def conflict_index(self, entries):
+        arr, pool, n = EntryPool(entries).arrays()
+        return _check(lib().orc_log_conflict_index(self.p, arr, n))
+
+    def try_append(self, index, entries):
+        arr, pool, n = EntryPool(entries).arrays()
+        return bool(_check(lib().orc_log_try_append(self.p, index, arr, n,
+                                                    pool)))
+
+    def append(self, entries):
+        arr, pool, n = EntryPool(entries).arrays()
+        _check(lib().orc_log_append(self.p, arr, n, pool))
+
+    def commit_update(self, stable_log_to=0, stable_log_term=0, processed=0,
+                      last_applied=0):
+        _check(lib().orc_log_commit_update(self.p, stable_log_to,
+                                           stable_log_term, processed,
+                                           last_applied))
+
+    @property
+    def committed(self):
+        return self.info().committed
+
+    @property
+    def last_index(self):
+        return self.info().last_index
+
+
+class BlackHole:
+    """blackHole / nopStepper (raft_etcd_test.go:3036-3041)."""
+
+    def handle(self, m):
+        pass
+
+    def read_messages(self):
+        return []
+
+
+class Network:
+    """network (raft_etcd_test.go:2896-3030): synchronous delivery."""
+
+    def __init__(self, *peers):
+        ids = list(range(1, len(peers) + 1))
+        self.peers = {}
+        for i, p in zip(ids, peers):
+            if p is None:
+                p = TestRaft(i, ids, 10, 1)
+            elif isinstance(p, TestRaft):
+                p.network_reset(i, ids)
+            self.peers[i] = p
+
+    def send(self, *msgs):
+        q = list(msgs)
+        while q:
+            m = q.pop(0)
+            p = self.peers[m["to"]]
+            p.handle(m)
+            q.extend(p.read_messages())
+
+
+# ---------------------------------------------------------------- cluster
+class Cluster:
+    """The node_test.go step() loop over G groups x R replicas."""
+
+    def __init__(self, num_groups, num_replicas=3, election_rtt=10,
+                 heartbeat_rtt=1, check_quorum=1, seed=0x5EEDD8B0,
+                 first_shard_id=1, logdb_keep=0):
+        cfg = ClusterCfg(num_groups, first_shard_id, num_replicas,
+                         election_rtt, heartbeat_rtt, check_quorum, seed,
+                         logdb_keep)
+        self.cfg = cfg
+        self.G = num_groups
+        self.R = num_replicas
+        self.p = lib().orc_cluster_new(cfg)
+        if not self.p:
+            raise OracleError(lib().orc_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_cluster_free(self.p)
+
+    def setup_steady(self, leader_slot=0):
+        _check(lib().orc_cluster_setup_steady(self.p, leader_slot))
+
+    def stage_proposals(self, counts, max_per_group, ents, pool):
+        """counts: uint32[G] array; ents: Entry[G*max] array; pool: uint8."""
+        _check(lib().orc_cluster_stage_proposals(self.p, counts,
+                                                 max_per_group, ents, pool))
+
+    def stage_read_index(self, low, high):
+        _check(lib().orc_cluster_stage_read_index(self.p, low, high))
+
+    def ingest(self, msgs):
+        marr, n, earr, pool = build_messages(msgs)
+        _check(lib().orc_cluster_ingest(self.p, marr, n, earr, pool))
+
+    def round(self, tick=False):
+        out = RoundOut()
+        _check(lib().orc_cluster_round(self.p, int(bool(tick)), out))
+        return out
+
+    def export(self, g, slot):
+        st = ReplicaState()
+        if lib().orc_cluster_export(self.p, g, slot, st):
+            raise IndexError((g, slot))
+        return st
+
+    def export_log(self, g, slot, lo, hi):
+        cap = hi - lo + 1
+        if cap <= 0:
+            return []
+        arr = (Entry * cap)()
+        pcap = 1 << 20
+        pool = (C.c_uint8 * pcap)()
+        n = lib().orc_cluster_export_log(self.p, g, slot, lo, hi, arr, pool,
+                                         pcap)
+        if n < 0:
+            raise OracleError("export_log %d" % n)
+        return [entry_to_tuple(arr[i], pool) for i in range(n)]
+
+    def export_outbox(self, g, slot):
+        cap, ecap, pcap = 256, 8192, 1 << 20
+        marr = (Message * cap)()
+        earr = (Entry * ecap)()
+        pool = (C.c_uint8 * pcap)()
+        n = lib().orc_cluster_export_outbox(self.p, g, slot, marr, cap, earr,
+                                            ecap, pool, pcap)
+        if n < 0 or n > cap:
+            raise OracleError("export_outbox %d" % n)
+        return [message_to_tuple(marr[i], earr, pool) for i in range(n)]
+
+    def export_kv(self, g, slot, key_cap=64, val_cap=2048, cap=4096):
+        keys = (C.c_uint8 * (cap * key_cap))()
+        vals = (C.c_uint8 * (cap * val_cap))()
+        kl, vl = (U32 * cap)(), (U32 * cap)()
+        n = lib().orc_cluster_export_kv(self.p, g, slot, keys, kl, vals, vl,
+                                        cap, key_cap, val_cap)
+        if n < 0 or n > cap:
+            raise OracleError("export_kv %d" % n)
+        kb, vb = bytes(keys), bytes(vals)
+        return {kb[i * key_cap:i * key_cap + kl[i]]:
+                vb[i * val_cap:i * val_cap + vl[i]] for i in range(n)}
+
+    def export_ready(self, g, slot):
+        cap = 64
+        arr = (ReadyToRead * cap)()
+        n = lib().orc_cluster_export_ready(self.p, g, slot, arr, cap)
+        return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high)
+                for i in range(min(n, cap))]
+
+    def set_hosted(self, g, slot, hosted):
+        lib().orc_cluster_set_hosted(self.p, g, slot, int(bool(hosted)))
+
+
+# ---------------------------------------------------------------- codecs
+def entry_size(e):
+    arr, pool, _ = EntryPool([e]).arrays()
+    return lib().orc_entry_size(arr)
+
+
+def entry_marshal(e):
+    arr, pool, _ = EntryPool([e]).arrays()
+    buf = (C.c_uint8 * (lib().orc_entry_size(arr) + 16))()
+    n = lib().orc_entry_marshal(arr, pool, buf)
+    return bytes(buf[:n])
+
+
+def entry_unmarshal(data):
+    e = Entry()
+    pool = (C.c_uint8 * max(1, len(data)))()
+    used = C.c_size_t(0)
+    n = lib().orc_entry_unmarshal(_u8(data), len(data), e, pool, len(data),
+                                  C.byref(used))
+    if n < 0:
+        raise ValueError("entry unmarshal failed")
+    return _etuple_to_dict(entry_to_tuple(e, pool)), n
+
+
+def entrybatch_marshal(entries):
+    arr, pool, n = EntryPool(entries).arrays()
+    size = lib().orc_entrybatch_size(arr, n)
+    buf = (C.c_uint8 * max(1, size))()
+    w = lib().orc_entrybatch_marshal(arr, n, pool, buf)
+    assert w == size
+    return bytes(buf[:w])
+
+
+def entrybatch_unmarshal(data, cap=4096):
+    arr = (Entry * cap)()
+    pool = (C.c_uint8 * max(1, len(data)))()
+    n = lib().orc_entrybatch_unmarshal(_u8(data), len(data), arr, cap, pool,
+                                       len(data))
+    if n < 0:
+        raise ValueError("entrybatch unmarshal failed")
+    return [_etuple_to_dict(entry_to_tuple(arr[i], pool)) for i in range(n)]
+
+
+def crc32_ieee(data):
+    return lib().orc_crc32_ieee(_u8(data), len(data))
+
+
+def pbkv_marshal(key, val):
+    buf = (C.c_uint8 * (len(key) + len(val) + 24))()
+    n = lib().orc_pbkv_marshal(_u8(key), len(key), _u8(val), len(val), buf)
+    return bytes(buf[:n])
+
+
+def pbkv_unmarshal(data):
+    kp, vp = PU8(), PU8()
+    kl, vl = U32(), U32()
+    src = _u8(data)
+    rc = lib().orc_pbkv_unmarshal(src, len(data), C.byref(kp), kl,
+                                  C.byref(vp), vl)
+    if rc:
+        raise ValueError("pbkv unmarshal failed")
+    return bytes(kp[:kl.value]), bytes(vp[:vl.value])

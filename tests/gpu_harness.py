@@ -1,0 +1,137 @@
+"""Shared harness for the GPU parity tests: drive the HIP engine and the CPU
+oracle with the same inputs and compare everything the round produces.
+
+Parity bar (bit-exact, integer state): every field of drb_replica_state,
+the resident log window, the KV contents, the messages each replica sent
+(compared per destination, in send order -- the reference's cross-
+destination order depends on Go map iteration, raft.go:828) and the
+ReadyToRead records.
+"""
+import ctypes as C
+
+from dragonboat_amd import abi, workload
+from dragonboat_amd.engine import Engine
+from oracle import pyoracle as po
+
+STATE_FIELDS = [
+    "term", "vote", "leader_id", "applied", "election_tick",
+    "heartbeat_tick", "randomized_election_timeout", "tick_count",
+    "committed", "processed", "last_index", "marker_index", "saved_to",
+    "applied_to_index", "applied_to_term", "applied_index",
+    "confirmed_index", "pushed_index", "prev_term", "prev_vote",
+    "prev_commit", "sm_index", "sm_term", "kv_count", "role"]
+
+
+def state_diff(a, b, R):
+    d = {}
+    for f in STATE_FIELDS:
+        if getattr(a, f) != getattr(b, f):
+            d[f] = (getattr(a, f), getattr(b, f))
+    if a.role == abi.LEADER:
+        for s in range(R):
+            x, y = a.remotes[s], b.remotes[s]
+            if (x.match, x.next, x.state, x.active) != \
+                    (y.match, y.next, y.state, y.active):
+                d["remote%d" % s] = ((x.match, x.next, x.state, x.active),
+                                     (y.match, y.next, y.state, y.active))
+    if a.ri_count != b.ri_count:
+        d["ri_count"] = (a.ri_count, b.ri_count)
+    else:
+        for i in range(a.ri_count):
+            x, y = a.ri[i], b.ri[i]
+            tx = (x.ctx_low, x.ctx_high, x.index, x.from_, x.confirmed)
+            ty = (y.ctx_low, y.ctx_high, y.index, y.from_, y.confirmed)
+            if tx != ty:
+                d["ri%d" % i] = (tx, ty)
+    return d
+
+
+def by_dest(msgs):
+    out = {}
+    for m in msgs:
+        out.setdefault(m[2], []).append(m)
+    return out
+
+
+class Pair:
+    """An engine and an oracle cluster stepped in lock-step."""
+
+    def __init__(self, G, R=3, seed=0x5EEDD8B0, window=32, leader_slot=0,
+                 **engine_kw):
+        self.G, self.R, self.seed = G, R, seed
+        self.eng = Engine(num_groups=G, num_replicas=R, window=window,
+                          **engine_kw)
+        self.orc = po.Cluster(G, R, seed=seed)
+        self.orc.setup_steady(leader_slot)
+        self.eng.init_steady(term=2, leader_slot=leader_slot, seed=seed)
+        self.rounds = 0
+
+    def stage(self, k=1, salt=None, read_index=False, groups=None,
+              key_space=256, val_len=4, prop_slot=0, ri_slot=0):
+        salt = self.rounds if salt is None else salt
+        pin = ri_in = abi.DRB_NONE
+        if k:
+            counts, ents, pool = workload.build_batch(
+                self.G, k, self.seed, salt, key_space, val_len, groups)
+            self.orc.stage_proposals(counts, k, ents, pool)
+            # the engine's staging layout is [g][max_props]
+            mp = self.eng.cfg["max_props"]
+            eents = (abi.Entry * (self.G * mp))()
+            for g in range(self.G):
+                for j in range(counts[g]):
+                    eents[g * mp + j] = ents[g * k + j]
+            self.eng.stage_proposals(prop_slot, counts, eents, pool)
+            pin = prop_slot
+        if read_index:
+            lo, hi = workload.build_read_index(self.G, self.seed, salt,
+                                               salt + 30, groups)
+            self.orc.stage_read_index(lo, hi)
+            self.eng.stage_read_index(ri_slot, lo, hi)
+            ri_in = ri_slot
+        return pin, ri_in
+
+    def round(self, k=1, tick=False, read_index=False, groups=None, **kw):
+        pin, ri_in = self.stage(k, read_index=read_index, groups=groups, **kw)
+        o = self.orc.round(tick=tick)
+        e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in)
+        self.rounds += 1
+        return o, e
+
+    def check(self, groups=None, logs=True, kv=True, msgs=True,
+              ready=True):
+        errs = []
+        gs = range(self.G) if groups is None else groups
+        for g in gs:
+            est = self.eng.export_replicas(g, 1)
+            for s in range(self.R):
+                a, b = est[s], self.orc.export(g, s)
+                if a.flags & (abi.F_FALLBACK | abi.F_ERROR):
+                    errs.append((g, s, "flags", a.flags, a.fallback_reason))
+                    continue
+                d = state_diff(a, b, self.R)
+                if d:
+                    errs.append((g, s, "state", d))
+                    continue
+                if logs:
+                    lo = max(1, b.last_index - self.eng.cfg["window"] + 1)
+                    lo = max(lo, b.last_index - 8)
+                    el = self.eng.export_log(g, s, lo, b.last_index)
+                    ol = self.orc.export_log(g, s, lo, b.last_index)
+                    if el != ol:
+                        errs.append((g, s, "log", el, ol))
+                if kv:
+                    ek = self.eng.kv_export(g, s)
+                    ok = self.orc.export_kv(g, s)
+                    if ek != ok:
+                        errs.append((g, s, "kv", len(ek), len(ok)))
+                if msgs:
+                    em = by_dest(self.eng.export_outbox(g, s))
+                    om = by_dest(self.orc.export_outbox(g, s))
+                    if em != om:
+                        errs.append((g, s, "msgs", em, om))
+                if ready:
+                    er = self.eng.export_ready(g, s)
+                    orr = self.orc.export_ready(g, s)
+                    if er != orr:
+                        errs.append((g, s, "ready", er, orr))
+        return errs

@@ -1,0 +1,109 @@
+"""GPU parity: the HIP step round against the CPU oracle, bit-exact.
+
+Every test drives dragonboat_amd (through the C ABI) and the oracle with
+the same seeded inputs (SURVEY 8d workload) and compares the full
+per-replica state, resident log, KV contents, sent messages and
+ReadyToReads after every round (tests/gpu_harness.py).
+"""
+import pytest
+
+from dragonboat_amd import abi
+from tests.gpu_harness import Pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pair, rounds, k=1, tick_every=1, ri_every=0, check_every=1):
+    for r in range(rounds):
+        tick = tick_every and (r % tick_every == 0)
+        ri = bool(ri_every) and (r % ri_every == 0)
+        o, e = pair.round(k=k, tick=tick, read_index=ri)
+        assert (e.committed_entries, e.applied_entries, e.messages,
+                e.ready_to_reads, e.dropped_read_indexes) == \
+            (o.committed_entries, o.applied_entries, o.messages,
+             o.ready_to_reads, o.dropped_read_indexes), (r, e.to_dict(),
+                                                         o.to_dict())
+        assert e.fallbacks == 0 and e.errors == 0, e.to_dict()
+        if check_every and r % check_every == 0:
+            errs = pair.check()
+            assert not errs, (r, errs[:3])
+
+
+def test_init_steady_matches_oracle_setup():
+    p = Pair(G=64, R=3)
+    errs = p.check(msgs=False, ready=False)
+    assert not errs, errs[:3]
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 5])
+def test_init_steady_all_sizes(R):
+    p = Pair(G=16, R=R)
+    assert not p.check(msgs=False, ready=False)
+
+
+def test_write_rounds_r3():
+    _run(Pair(G=96, R=3), rounds=12, k=1, tick_every=0)
+
+
+def test_write_rounds_with_ticks_r3():
+    _run(Pair(G=96, R=3), rounds=25, k=1, tick_every=1)
+
+
+def test_write_rounds_batched_k3():
+    _run(Pair(G=64, R=3), rounds=12, k=3, tick_every=2)
+
+
+@pytest.mark.parametrize("R", [1, 5])
+def test_write_rounds_other_sizes(R):
+    _run(Pair(G=64, R=R), rounds=15, k=1, tick_every=1)
+
+
+def test_read_index_mix_c3():
+    # 9:1 ReadIndex:write batched into one ctx per group per round
+    _run(Pair(G=64, R=3), rounds=20, k=1, tick_every=1, ri_every=1)
+
+
+def test_idle_groups_and_ragged_proposals():
+    p = Pair(G=80, R=3)
+    for r in range(14):
+        groups = [g for g in range(p.G) if (g * 7 + r) % 3 != 0]
+        o, e = p.round(k=2 if r % 2 else 1, tick=(r % 3 == 0),
+                       read_index=(r % 4 == 1), groups=groups)
+        assert e.fallbacks == 0 and e.errors == 0
+        assert (e.committed_entries, e.messages) == \
+            (o.committed_entries, o.messages)
+        errs = p.check()
+        assert not errs, (r, errs[:3])
+
+
+def test_empty_rounds_then_resume():
+    p = Pair(G=32, R=3)
+    for r in range(6):
+        p.round(k=0, tick=False)
+    assert not p.check()
+    _run(p, rounds=6, k=1, tick_every=1)
+
+
+def test_lagging_follower_catches_up_via_reject_and_retry():
+    # follower slot 2 of every group stops stepping for a few rounds (its
+    # messages are lost), then rejoins: the leader's optimistic Replicate is
+    # rejected (raft.go:1465-1470), decreaseTo/Retry (remote.go:182-198)
+    # probes back and the follower catches up (logentry.go:296-310).
+    p = Pair(G=48, R=3)
+    _run(p, rounds=3, k=1, tick_every=0)
+    for g in range(p.G):
+        p.orc.set_hosted(g, 2, False)
+    sts = p.eng.export_replicas(0, p.G)
+    for i in range(2, len(sts), 3):
+        sts[i].flags &= ~abi.F_HOSTED
+    p.eng.import_replicas(0, sts)
+    for r in range(5):
+        p.round(k=1, tick=False)
+        assert not p.check(groups=range(0, p.G, 7))
+    for g in range(p.G):
+        p.orc.set_hosted(g, 2, True)
+    sts = p.eng.export_replicas(0, p.G)
+    for i in range(2, len(sts), 3):
+        sts[i].flags |= abi.F_HOSTED
+    p.eng.import_replicas(0, sts)
+    _run(p, rounds=10, k=1, tick_every=2)

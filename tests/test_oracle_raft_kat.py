@@ -1,0 +1,393 @@
+"""Raft known-answer tests restated from the reference's own test files.
+
+Sources (all in /root/reference/internal/raft):
+  raft_etcd_paper_test.go  commit / replicate KATs (section 5.3, 5.4.2)
+  logentry_test.go         matchTerm / upToDate / getConflictIndex /
+                           commitTo / commitUpdate tables
+  readindex_test.go        readIndex queue / confirm KATs
+They pin the oracle (oracle/*.c) to the reference's expected values; the
+oracle is then the checker for the GPU path (tests/test_gpu_*.py).
+"""
+import pytest
+
+from oracle import pyoracle as po
+from oracle.pyoracle import ent, msg
+from dragonboat_amd.abi import MSG, LEADER, FOLLOWER, CANDIDATE
+
+REPLICATE = MSG["Replicate"]
+REPLICATE_RESP = MSG["ReplicateResp"]
+PROPOSE = MSG["Propose"]
+
+
+def ids_by_size(n):  # raft_etcd_test.go:3043
+    return list(range(1, n + 1))
+
+
+def accept_and_reply(m):  # raft_etcd_paper_test.go:969-980
+    assert m["type"] == REPLICATE
+    return msg(REPLICATE_RESP, from_=m["to"], to=m["from_"], term=m["term"],
+               log_index=m["log_index"] + len(m["entries"]))
+
+
+def commit_noop_entry(r, s):  # raft_etcd_paper_test.go:938-967
+    assert r.info().role == LEADER
+    r.broadcast_replicate()
+    for m in r.read_messages():
+        assert (m["type"] == REPLICATE and len(m["entries"]) == 1 and
+                m["entries"][0]["cmd"] == b"")
+        r.handle(accept_and_reply(m))
+    r.read_messages()
+    s.append(r.entries_to_save())
+    rc, term = r.term(r.last_index)
+    r.commit_update(processed=r.committed, stable_log_to=r.last_index,
+                    stable_log_term=term)
+
+
+def _strip(e):
+    return (e["term"], e["index"], e["cmd"])
+
+
+def test_leader_commit_entry():  # raft_etcd_paper_test.go:411-451
+    s = po.LogDB()
+    r = po.TestRaft(1, [1, 2, 3], 10, 1, s)
+    r.become_candidate()
+    r.become_leader()
+    commit_noop_entry(r, s)
+    li = r.last_index
+    r.handle(msg(PROPOSE, from_=1, to=1, entries=[ent(cmd=b"some data")]))
+    for m in r.read_messages():
+        r.handle(accept_and_reply(m))
+    assert r.committed == li + 1
+    assert [_strip(e) for e in r.entries_to_apply()] == \
+        [(1, li + 1, b"some data")]
+    msgs = sorted(r.read_messages(), key=lambda m: m["to"])
+    for i, m in enumerate(msgs):
+        assert m["to"] == i + 2
+        assert m["type"] == REPLICATE
+        assert m["commit"] == li + 1
+
+
+@pytest.mark.parametrize("size,acceptors,wack", [
+    (1, set(), True), (3, set(), False), (3, {2}, True), (3, {2, 3}, True),
+    (5, set(), False), (5, {2}, False), (5, {2, 3}, True),
+    (5, {2, 3, 4}, True), (5, {2, 3, 4, 5}, True)])
+def test_leader_acknowledge_commit(size, acceptors, wack):
+    # raft_etcd_paper_test.go:453-490
+    s = po.LogDB()
+    r = po.TestRaft(1, ids_by_size(size), 10, 1, s)
+    r.become_candidate()
+    r.become_leader()
+    commit_noop_entry(r, s)
+    li = r.last_index
+    r.handle(msg(PROPOSE, from_=1, to=1, entries=[ent(cmd=b"some data")]))
+    for m in r.read_messages():
+        if m["to"] in acceptors:
+            r.handle(accept_and_reply(m))
+    assert (r.committed > li) == wack
+
+
+@pytest.mark.parametrize("tt", [
+    [], [ent(term=2, index=1)], [ent(term=1, index=1), ent(term=2, index=2)],
+    [ent(term=1, index=1)]])
+def test_leader_commit_preceding_entries(tt):
+    # raft_etcd_paper_test.go:495-529
+    storage = po.LogDB(tt)
+    r = po.TestRaft(1, [1, 2, 3], 10, 1, storage)
+    r.load_state(term=2)
+    r.become_candidate()
+    r.become_leader()
+    r.handle(msg(PROPOSE, from_=1, to=1, entries=[ent(cmd=b"some data")]))
+    for m in r.read_messages():
+        r.handle(accept_and_reply(m))
+    li = len(tt)
+    want = [(e["term"], e["index"], b"") for e in tt] + \
+        [(3, li + 1, b""), (3, li + 2, b"some data")]
+    assert [_strip(e) for e in r.entries_to_apply()] == want
+
+
+@pytest.mark.parametrize("ents,commit", [
+    ([ent(term=1, index=1, cmd=b"some data")], 1),
+    ([ent(term=1, index=1, cmd=b"some data"),
+      ent(term=1, index=2, cmd=b"some data2")], 2),
+    ([ent(term=1, index=1, cmd=b"some data2"),
+      ent(term=1, index=2, cmd=b"some data")], 2),
+    ([ent(term=1, index=1, cmd=b"some data"),
+      ent(term=1, index=2, cmd=b"some data2")], 1)])
+def test_follower_commit_entry(ents, commit):
+    # raft_etcd_paper_test.go:532-588
+    r = po.TestRaft(1, [1, 2, 3], 10, 1)
+    r.become_follower(1, 2)
+    r.handle(msg(REPLICATE, from_=2, to=1, term=1, entries=ents,
+                 commit=commit))
+    assert r.committed == commit
+    assert [_strip(e) for e in r.entries_to_apply()] == \
+        [_strip(e) for e in ents[:commit]]
+
+
+@pytest.mark.parametrize("term,index,windex,wreject,whint", [
+    (0, 0, 1, False, 0), (1, 1, 1, False, 0), (2, 2, 2, False, 0),
+    (1, 2, 2, True, 2), (3, 3, 3, True, 2)])
+def test_follower_check_replicate(term, index, windex, wreject, whint):
+    # raft_etcd_paper_test.go:590-630
+    storage = po.LogDB([ent(term=1, index=1), ent(term=2, index=2)])
+    r = po.TestRaft(1, [1, 2, 3], 10, 1, storage)
+    r.load_state(commit=1)
+    r.become_follower(2, 2)
+    r.handle(msg(REPLICATE, from_=2, to=1, term=2, log_term=term,
+                 log_index=index))
+    msgs = r.read_messages()
+    assert len(msgs) == 1
+    m = msgs[0]
+    assert (m["from_"], m["to"], m["type"], m["term"], m["log_index"],
+            m["reject"], m["hint"]) == (1, 2, REPLICATE_RESP, 2, windex,
+                                        wreject, whint)
+
+
+@pytest.mark.parametrize("index,term,ents,wents,wunstable", [
+    (2, 2, [ent(term=3, index=3)],
+     [(1, 1), (2, 2), (3, 3)], [(3, 3)]),
+    (1, 1, [ent(term=3, index=2), ent(term=4, index=3)],
+     [(1, 1), (3, 2), (4, 3)], [(3, 2), (4, 3)]),
+    (0, 0, [ent(term=1, index=1)], [(1, 1), (2, 2)], []),
+    (0, 0, [ent(term=3, index=1)], [(3, 1)], [(3, 1)])])
+def test_follower_append_entries(index, term, ents, wents, wunstable):
+    # raft_etcd_paper_test.go:636-688
+    storage = po.LogDB([ent(term=1, index=1), ent(term=2, index=2)])
+    r = po.TestRaft(1, [1, 2, 3], 10, 1, storage)
+    r.become_follower(2, 2)
+    r.handle(msg(REPLICATE, from_=2, to=1, term=2, log_term=term,
+                 log_index=index, entries=ents))
+    assert [(e["term"], e["index"]) for e in r.all_entries()] == wents
+    assert [(e["term"], e["index"]) for e in r.entries_to_save()] == \
+        wunstable
+
+
+def _e(pairs):
+    return [ent(term=t, index=i) for t, i in pairs]
+
+
+LEAD_ENTS = _e([(1, 1), (1, 2), (1, 3), (4, 4), (4, 5), (5, 6), (5, 7),
+                (6, 8), (6, 9), (6, 10)])
+SYNC_CASES = [
+    _e([(1, 1), (1, 2), (1, 3), (4, 4), (4, 5), (5, 6), (5, 7), (6, 8),
+        (6, 9)]),
+    _e([(1, 1), (1, 2), (1, 3), (4, 4)]),
+    _e([(1, 1), (1, 2), (1, 3), (4, 4), (4, 5), (5, 6), (5, 7), (6, 8),
+        (6, 9), (6, 10), (6, 11)]),
+    _e([(1, 1), (1, 2), (1, 3), (4, 4), (4, 5), (5, 6), (5, 7), (6, 8),
+        (6, 9), (6, 10), (7, 11), (7, 12)]),
+    _e([(1, 1), (1, 2), (1, 3), (4, 4), (4, 5), (4, 6), (4, 7)]),
+    _e([(1, 1), (1, 2), (1, 3), (2, 4), (2, 5), (2, 6), (3, 7), (3, 8),
+        (3, 9), (3, 10), (3, 11)]),
+]
+
+
+@pytest.mark.parametrize("tt", SYNC_CASES)
+def test_leader_sync_follower_log(tt):
+    # raft_etcd_paper_test.go:690-770 (figure 7)
+    term = 8
+    lead_storage = po.LogDB(LEAD_ENTS)
+    lead = po.TestRaft(1, [1, 2, 3], 10, 1, lead_storage)
+    lead.load_state(commit=lead.last_index, term=term)
+    follower = po.TestRaft(2, [1, 2, 3], 10, 1, po.LogDB(tt))
+    follower.load_state(term=term - 1)
+    n = po.Network(lead, follower, po.BlackHole())
+    n.send(msg(MSG["Election"], from_=1, to=1))
+    n.send(msg(MSG["RequestVoteResp"], from_=3, to=1, term=term + 1))
+    n.send(msg(PROPOSE, from_=1, to=1, entries=[ent()]))
+    li, fi = lead.info(), follower.info()
+    assert (li.committed, li.processed) == (fi.committed, fi.processed)
+    assert [_strip(e) for e in lead.all_entries()] == \
+        [_strip(e) for e in follower.all_entries()]
+
+
+@pytest.mark.parametrize("index,wcommit", [(1, 0), (2, 0), (3, 3)])
+def test_leader_only_commits_log_from_current_term(index, wcommit):
+    # raft_etcd_paper_test.go:867-899 (section 5.4.2)
+    storage = po.LogDB([ent(term=1, index=1), ent(term=2, index=2)])
+    r = po.TestRaft(1, [1, 2], 10, 1, storage)
+    r.load_state(term=2)
+    r.become_candidate()
+    r.become_leader()
+    r.read_messages()
+    r.handle(msg(PROPOSE, from_=1, to=1, entries=[ent()]))
+    r.handle(msg(REPLICATE_RESP, from_=2, to=1, term=r.info().term,
+                 log_index=index))
+    assert r.committed == wcommit
+
+
+def test_leader_start_replication():  # raft_etcd_paper_test.go:900-935
+    s = po.LogDB()
+    r = po.TestRaft(1, [1, 2, 3], 10, 1, s)
+    r.become_candidate()
+    r.become_leader()
+    commit_noop_entry(r, s)
+    li = r.last_index
+    r.handle(msg(PROPOSE, from_=1, to=1, entries=[ent(cmd=b"some data")]))
+    assert r.last_index == li + 1
+    assert r.committed == li
+    msgs = sorted(r.read_messages(), key=lambda m: m["to"])
+    want_ents = [dict(ent(term=1, index=li + 1, cmd=b"some data"))]
+    assert len(msgs) == 2
+    for to, m in zip((2, 3), msgs):
+        assert (m["from_"], m["to"], m["term"], m["type"], m["log_index"],
+                m["log_term"], m["commit"]) == (1, to, 1, REPLICATE, li, 1, li)
+        assert m["entries"] == want_ents
+
+
+@pytest.mark.parametrize("ents,logterm,index,wreject", [
+    (_e([(1, 1)]), 1, 1, False), (_e([(1, 1)]), 1, 2, False),
+    (_e([(1, 1), (1, 2)]), 1, 1, True),
+    (_e([(1, 1)]), 2, 1, False), (_e([(1, 1)]), 2, 2, False),
+    (_e([(1, 1), (1, 2)]), 2, 1, False),
+    (_e([(2, 1)]), 1, 1, True), (_e([(2, 1)]), 1, 2, True),
+    (_e([(2, 1), (1, 2)]), 1, 1, True)])
+def test_voter(ents, logterm, index, wreject):
+    # raft_etcd_paper_test.go:811-864 (election used by the setup path)
+    r = po.TestRaft(1, [1, 2], 10, 1, po.LogDB(ents))
+    r.handle(msg(MSG["RequestVote"], from_=2, to=1, term=3, log_term=logterm,
+                 log_index=index))
+    msgs = r.read_messages()
+    assert len(msgs) == 1
+    assert msgs[0]["type"] == MSG["RequestVoteResp"]
+    assert msgs[0]["reject"] == wreject
+
+
+# ---------------------------------------------------------------- entryLog
+def _log_fixture():
+    # logentry_test.go:409-425 (shared setup of the matchTerm/upToDate/...
+    # tables): logdb holds 1..4, the in-memory part holds 5..7
+    r = po.TestRaft(1, [1], 10, 1,
+                    po.LogDB(_e([(1, 1), (1, 2), (2, 3), (3, 4)])))
+    r.append(_e([(3, 5), (3, 6), (4, 7)]))
+    return r
+
+
+@pytest.mark.parametrize("index,term,match", [
+    (1, 1, True), (1, 2, False), (4, 4, False), (4, 3, True), (5, 3, True),
+    (5, 4, False), (7, 4, True), (8, 5, False)])
+def test_log_match_term(index, term, match):  # logentry_test.go:409-447
+    assert _log_fixture().match_term(index, term) == match
+
+
+@pytest.mark.parametrize("index,term,ok", [
+    (1, 2, False), (8, 2, False), (1, 4, False), (7, 4, True), (8, 4, True),
+    (8, 5, True), (2, 5, True)])
+def test_log_up_to_date(index, term, ok):  # logentry_test.go:449-487
+    assert _log_fixture().up_to_date(index, term) == ok
+
+
+@pytest.mark.parametrize("ents,conflict", [
+    ([], 0), (_e([(2, 1)]), 1), (_e([(1, 1), (1, 2)]), 0),
+    (_e([(1, 1), (2, 2)]), 2), (_e([(3, 6), (4, 7)]), 0),
+    (_e([(3, 6), (5, 7)]), 7), (_e([(4, 7), (4, 8)]), 8)])
+def test_log_get_conflict_index(ents, conflict):  # logentry_test.go:489-530
+    assert _log_fixture().conflict_index(ents) == conflict
+
+
+def test_log_commit_to():  # logentry_test.go:532-556
+    r = _log_fixture()
+    r.commit_to(3)
+    assert r.committed == 3
+    r.commit_to(2)
+    assert r.committed == 3
+
+
+def test_log_commit_to_panics_on_unavailable_index():  # :558-583
+    with pytest.raises(po.OracleError):
+        _log_fixture().commit_to(8)
+
+
+def test_log_commit_update_sets_applied():  # logentry_test.go:608-618
+    r = _log_fixture()
+    r.commit_to(7)
+    r.commit_update(processed=5)
+    assert r.info().processed == 5
+
+
+def test_log_commit_update_panics_when_apply_twice():  # :620-633
+    r = _log_fixture()
+    r.commit_to(7)
+    r.commit_update(processed=6)
+    with pytest.raises(po.OracleError):
+        r.commit_update(processed=5)
+
+
+def test_log_commit_update_panics_when_applying_not_committed():  # :635-648
+    r = _log_fixture()
+    r.commit_to(7)
+    r.commit_update(processed=6)
+    with pytest.raises(po.OracleError):
+        r.commit_update(processed=12)
+
+
+@pytest.mark.parametrize("index,term,committed,ok", [
+    (5, 3, 5, True), (5, 4, 0, False), (7, 4, 7, True), (3, 2, 3, True)])
+def test_log_try_commit_term_rule(index, term, committed, ok):
+    # logentry.go:395-410 -- commit only at the leader's current term
+    r = _log_fixture()
+    assert r.log_try_commit(index, term) == ok
+    assert r.committed == committed
+
+
+# ---------------------------------------------------------------- readIndex
+def ctx(v):  # readindex_test.go:20-25 getTestSystemCtx
+    return (v, v + 1)
+
+
+def test_same_ctx_can_not_be_added_twice():  # readindex_test.go:30-40
+    r = po.ReadIndexQ()
+    r.add_request(1, ctx(10001), 1)
+    assert len(r) == 1
+    r.add_request(2, ctx(10001), 2)
+    assert len(r) == 1
+
+
+def test_inconsistent_pending_queue():  # readindex_test.go:42-53
+    r = po.ReadIndexQ()
+    r.add_request(1, ctx(10001), 1)
+    r.push_raw(ctx(10003))
+    with pytest.raises(po.OracleError):
+        r.add_request(2, ctx(10002), 2)
+
+
+def test_read_index_request_can_be_added():  # readindex_test.go:55-84
+    r = po.ReadIndexQ()
+    r.add_request(1, ctx(10001), 1)
+    r.add_request(2, ctx(10002), 2)
+    items = r.items()
+    assert len(items) == 2
+    assert items[1] == (ctx(10002), 2, 2)
+    assert items[-1][0] == ctx(10002)  # peepCtx
+
+
+def test_read_index_checks_input_index():  # readindex_test.go:86-103
+    r = po.ReadIndexQ()
+    r.add_request(3, ctx(10001), 1)
+    r.add_request(5, ctx(10002), 3)
+    with pytest.raises(po.OracleError):
+        r.add_request(4, ctx(10003), 2)
+
+
+def test_add_confirmation_checks_inconsistent_pending_queue():  # :105-124
+    r = po.ReadIndexQ()
+    r.add_request(3, ctx(10002), 1)
+    r.add_request(4, ctx(10001), 3)
+    r.add_request(5, ctx(10003), 2)
+    r.push_raw(ctx(10004), front=True)
+    r.confirm(ctx(10001), 1, 3)
+    with pytest.raises(po.OracleError):
+        r.confirm(ctx(10001), 3, 3)
+
+
+def test_read_index_leader_can_be_confirmed():  # readindex_test.go:126-164
+    r = po.ReadIndexQ()
+    r.add_request(3, ctx(10002), 1)
+    r.add_request(4, ctx(10001), 3)
+    r.add_request(5, ctx(10003), 2)
+    assert r.confirm(ctx(10001), 1, 3) == []
+    ris = r.confirm(ctx(10001), 3, 3)
+    assert len(ris) == 2
+    assert ris[1] == (ctx(10001), 4, 3)
+    assert ris[0] == (ctx(10002), 4, 1)
+    assert len(r) == 1
