@@ -47,7 +47,11 @@ def parse():
     ap.add_argument("--replicas", type=int, default=3)
     ap.add_argument("--k", type=int, default=1, help="writes/group/round")
     ap.add_argument("--no-read-index", action="store_true")
-    ap.add_argument("--tick-every", type=int, default=1)
+    ap.add_argument("--tick-every", type=int, default=0,
+                    help="LocalTick every N rounds (0: derive from --tick-ms)")
+    ap.add_argument("--tick-ms", type=float, default=1.0,
+                    help="RTTMillisecond: one LocalTick per this much wall "
+                         "time (nodehost.go:1824-1914)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -78,7 +82,7 @@ def cpu_baseline(args, seconds):
             lo, hi = workload.build_read_index(G, seed, rounds, rounds + 30)
             c.stage_read_index(lo, hi)
         outs = [RoundOut() for _ in parts]
-        tick = int(args.tick_every > 0 and rounds % args.tick_every == 0)
+        tick = 1  # a CPU round takes longer than RTTMillisecond = 1 ms
         t0 = time.perf_counter()
         th = [threading.Thread(target=L.orc_cluster_round_range,
                                args=(c.p, tick, a, b, C.byref(o)))
@@ -94,11 +98,11 @@ def cpu_baseline(args, seconds):
     return dict(value=committed / t_run if t_run else 0.0,
                 unit="committed entries/s", cores=cores, kind="port",
                 sample="%d groups x %d replicas, %d rounds of the same "
-                       "workload (k=%d, %s, tick every %d), CPU "
+                       "workload (k=%d, %s, a LocalTick every round), CPU "
                        "restatement (oracle/), not dragonboat" % (
                            G, args.replicas, rounds, args.k,
                            "9:1 ReadIndex" if not args.no_read_index
-                           else "writes only", args.tick_every))
+                           else "writes only"))
 
 
 def main():
@@ -126,14 +130,31 @@ def main():
         eng.gen_read_index(b, seed, b + 30)
     stream = torch.cuda.ExternalStream(eng.stream)
 
+    tick_every = [max(1, args.tick_every)]
+
     def step(i):
-        tick = args.tick_every > 0 and i % args.tick_every == 0
+        tick = i % tick_every[0] == 0
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF)
 
+    # warmup (ticking every round); the tick cadence then follows the
+    # reference's wall-clock tick worker: one LocalTick per RTTMillisecond
+    tw0 = time.perf_counter()
     for i in range(args.warmup):
         step(i)
     eng.sync()
+    warm_ms = (time.perf_counter() - tw0) * 1e3 / max(1, args.warmup)
+    if args.tick_every <= 0:
+        te = max(1, int(round(args.tick_ms / max(warm_ms, 1e-6))))
+        if world > 1:
+            t = torch.tensor([te], dtype=torch.int64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            te = int(t.item())
+        tick_every[0] = te
+        for i in range(args.warmup, 2 * args.warmup):
+            step(i)
+        eng.sync()
+    args.tick_every = tick_every[0]
     eng.read_counters(reset=True)
     K = args.steps
     ev = [(torch.cuda.Event(enable_timing=True),
@@ -145,7 +166,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(K):
         ev[i][0].record(stream)
-        step(args.warmup + i)
+        step(2 * args.warmup + i)
         ev[i][1].record(stream)
     eng.sync()
     torch.cuda.synchronize()

@@ -13,6 +13,7 @@
 
 #include "../../include/drb_engine.h"
 #include "drb_layout.hpp"
+#include "drb_msg.hpp"
 #include "drb_step.hpp"
 
 using namespace drb;
@@ -206,7 +207,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.ri_conf, R * DRB_RI_DEPTH * G);
   rc |= dalloc(e, &v.ring, R * v.W * (ENT_META + v.C16) * G);
   rc |= dalloc(e, &v.mbox, 2 * R * R * v.MB * MSG_CHUNKS * G);
-  rc |= dalloc(e, &v.mbox_meta, 2 * R * G);
+  rc |= dalloc(e, &v.mbox_meta, 2 * R * G);  // uint4
   rc |= dalloc(e, &v.kv, R * G * v.KS * v.KVW);
   rc |= dalloc(e, &v.props,
                (uint64_t)cfg->prop_slots * v.max_props * (PROP_META + v.C16) *
@@ -262,7 +263,7 @@ extern "C" uint64_t drb_engine_round(const drb_engine *e) {
 }
 
 // ---------------------------------------------------------------- state
-static const int kU64Order[NUM_U64 - 2] = {
+static const int kU64Order[NUM_U64_EXPORTED] = {
     F_TERM,           F_VOTE,          F_LEADER_ID,       F_APPLIED,
     F_ELECTION_TICK,  F_HEARTBEAT_TICK, F_RAND_TIMEOUT,   F_TICK_COUNT,
     F_COMMITTED,      F_PROCESSED,     F_LAST_INDEX,      F_MARKER_INDEX,
@@ -299,10 +300,13 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
     uint64_t g = first_group + gi;
     for (uint32_t s = 0; s < R; ++s) {
       drb_replica_state c = st[gi * R + s];
-      for (int k = 0; k < NUM_U64 - 2; ++k) {
+      for (int k = 0; k < NUM_U64_EXPORTED; ++k) {
         i64.push_back(u64_ix(v, kU64Order[k], s, g));
         d64.push_back(*st_u64(&c, k));
       }
+      // the term cache restarts empty: [last+1, last]
+      i64.push_back(u64_ix(v, F_TERM_START, s, g));
+      d64.push_back(c.last_index + 1);
       uint32_t w[NUM_U32] = {c.role, c.flags, c.fallback_reason, c.ri_count};
       for (int k = 0; k < NUM_U32; ++k) {
         i32.push_back(u32_ix(v, k, s, g));
@@ -345,7 +349,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
   for (uint64_t gi = 0; gi < n_groups; ++gi) {
     uint64_t g = first_group + gi;
     for (uint32_t s = 0; s < R; ++s) {
-      for (int k = 0; k < NUM_U64 - 2; ++k)
+      for (int k = 0; k < NUM_U64_EXPORTED; ++k)
         i64.push_back(u64_ix(v, kU64Order[k], s, g));
       for (int k = 0; k < NUM_U32; ++k) i32.push_back(u32_ix(v, k, s, g));
       for (uint32_t p = 0; p < R; ++p) irm.push_back(rem_ix(v, s, p, g));
@@ -375,7 +379,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       memset(&o, 0, sizeof(o));
       o.shard_id = v.first_shard_id + g;
       o.replica_id = s + 1;
-      for (int k = 0; k < NUM_U64 - 2; ++k) *st_u64(&o, k) = d64[a++];
+      for (int k = 0; k < NUM_U64_EXPORTED; ++k) *st_u64(&o, k) = d64[a++];
       o.role = d32[b++];
       o.flags = d32[b++];
       o.fallback_reason = d32[b++];
@@ -544,6 +548,7 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   SET(F_KV_COUNT, 0);
   SET(F_RING_LO, 1);
   SET(F_RING_GUARD, ~0ull);
+  SET(F_TERM_START, L1);  // the leader's no-op opened the term
 #undef SET
   v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
   v.u32[u32_ix(v, W_FLAGS, s, g)] = DRB_F_HOSTED;
@@ -761,11 +766,14 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     }
     uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
     std::vector<uint64_t> mi = {mmeta_ix(v, buf, from, g)};
-    std::vector<uint64_t> meta;
+    std::vector<uint4> meta;
     if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
-    uint64_t cur = meta[0];
-    if ((uint32_t)(cur >> 32) != tag) cur = (uint64_t)tag << 32;
-    uint32_t k = (uint32_t)(cur >> (4 * to)) & 15u;
+    uint4 cur = meta[0];
+    if (cur.x != tag) {
+      cur = pack2(0, 0);
+      cur.x = tag;
+    }
+    uint32_t k = (cur.y >> (4 * to)) & 15u;
     if (k >= v.MB) {  // MessageQueue full (message.go:105-123)
       drop++;
       continue;
@@ -782,22 +790,37 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       int rc = drb_import_log(e, g, from, es.data(), es.size(), pool);
       if (rc) return rc;
     }
-    std::vector<uint64_t> idx;
-    std::vector<uint4> val;
-    uint4 c0;
-    c0.x = msg_meta(m.type, m.reject ? 1 : 0, (uint32_t)m.n_entries);
-    c0.y = 0;
-    c0.z = (uint32_t)m.term;
-    c0.w = (uint32_t)(m.term >> 32);
-    uint4 c[4] = {c0, mk4h(m.log_index, m.log_term), mk4h(m.commit, m.hint),
-                  mk4h(m.hint_high, 0)};
-    for (uint32_t q = 0; q < MSG_CHUNKS; ++q) {
-      idx.push_back(mbox_ix(v, buf, from, to, k, q, g));
-      val.push_back(c[q]);
+    Msg mm;
+    mm.type = m.type;
+    mm.reject = m.reject ? 1 : 0;
+    mm.n = (uint32_t)m.n_entries;
+    mm.term = m.term;
+    mm.log_index = m.log_index;
+    mm.log_term = m.log_term;
+    mm.commit = m.commit;
+    mm.hint = m.hint;
+    mm.hint_high = m.hint_high;
+    uint4 c0, c1;
+    msg_encode(mm, c0, c1);
+    // the sender's term is stored once per round in the meta word
+    bool zero = (c0.x & MF_TERM_ZERO) != 0;
+    if (!zero && m.term != 0) {
+      if (q_hi(cur) == 0 && (cur.y == 0)) {
+        uint64_t t = m.term;
+        cur.z = (uint32_t)t;
+        cur.w = (uint32_t)(t >> 32);
+      } else if (q_hi(cur) != m.term) {
+        c0.x |= MF_TERM_OTHER;  // receiver treats it as a term mismatch
+      }
+    } else if (!zero && m.term == 0 && q_hi(cur) != 0) {
+      c0.x |= MF_TERM_OTHER;
     }
+    std::vector<uint64_t> idx = {mbox_ix(v, buf, from, to, k, 0, g),
+                                 mbox_ix(v, buf, from, to, k, 1, g)};
+    std::vector<uint4> val = {c0, c1};
     if (scatter(e, v.mbox, idx, val)) return DRB_EDEVICE;
-    cur += 1ull << (4 * to);
-    std::vector<uint64_t> mv = {cur};
+    cur.y += 1u << (4 * to);
+    std::vector<uint4> mv = {cur};
     if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
     acc++;
   }
@@ -876,13 +899,13 @@ extern "C" int drb_step_round(drb_engine *e, const drb_round_in *in,
 }
 
 // ---------------------------------------------------------------- outputs
-static int export_pair(drb_engine *e, uint32_t buf, uint32_t tag, uint64_t g,
+static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
                        uint32_t from, uint32_t to, drb_message *out,
                        size_t cap, size_t *nm, drb_entry *ents, size_t ecap,
                        size_t *ne, uint8_t *pool, size_t pcap, size_t *np,
-                       uint64_t cnt) {
-  const View &v = *&e->v;
-  uint32_t k = (uint32_t)(cnt >> (4 * to)) & 15u;
+                       uint4 meta) {
+  const View &v = e->v;
+  uint32_t k = (meta.y >> (4 * to)) & 15u;
   if (!k) return DRB_OK;
   std::vector<uint64_t> idx;
   for (uint32_t q = 0; q < k; ++q)
@@ -890,43 +913,24 @@ static int export_pair(drb_engine *e, uint32_t buf, uint32_t tag, uint64_t g,
       idx.push_back(mbox_ix(v, buf, from, to, q, c, g));
   std::vector<uint4> val;
   if (gather(e, v.mbox, idx, val)) return DRB_EDEVICE;
-  (void)tag;
   for (uint32_t q = 0; q < k; ++q) {
     if (*nm >= cap) return DRB_ERANGE;
     const uint4 *c = &val[q * MSG_CHUNKS];
+    Msg mm = msg_decode(c[0], c[1], (c[0].x & MF_HAS_C1) != 0, q_hi(meta));
     drb_message &m = out[(*nm)++];
     memset(&m, 0, sizeof(m));
     m.shard_id = v.first_shard_id + g;
     m.from = from + 1;
     m.to = to + 1;
-    m.type = c[0].x & 0xffu;
-    m.reject = (c[0].x >> 8) & 1u;
-    m.term = hi64h(c[0]);
-    uint64_t ne_ = c[0].x >> 16;
-    switch (m.type) {
-      case DRB_MSG_REPLICATE:
-        m.log_index = lo64h(c[1]);
-        m.log_term = hi64h(c[1]);
-        m.commit = lo64h(c[2]);
-        break;
-      case DRB_MSG_REPLICATE_RESP:
-        m.log_index = lo64h(c[1]);
-        m.hint = hi64h(c[2]);
-        break;
-      case DRB_MSG_HEARTBEAT:
-      case DRB_MSG_HEARTBEAT_RESP:
-        m.commit = lo64h(c[2]);
-        m.hint = hi64h(c[2]);
-        m.hint_high = lo64h(c[3]);
-        break;
-      default:
-        m.log_index = lo64h(c[1]);
-        m.log_term = hi64h(c[1]);
-        m.commit = lo64h(c[2]);
-        m.hint = hi64h(c[2]);
-        m.hint_high = lo64h(c[3]);
-        break;
-    }
+    m.type = mm.type;
+    m.reject = mm.reject;
+    m.term = mm.term;
+    m.log_index = mm.log_index;
+    m.log_term = mm.log_term;
+    m.commit = mm.commit;
+    m.hint = mm.hint;
+    m.hint_high = mm.hint_high;
+    uint64_t ne_ = mm.n;
     m.n_entries = ne_;
     m.entries_off = *ne;
     if (m.type == DRB_MSG_REPLICATE && ne_) {
@@ -956,16 +960,15 @@ extern "C" int drb_export_outbox(drb_engine *e, uint64_t group,
   const View &v = e->v;
   const uint32_t buf = (uint32_t)(e->round & 1);
   std::vector<uint64_t> mi = {mmeta_ix(v, buf, from_slot, group)};
-  std::vector<uint64_t> meta;
+  std::vector<uint4> meta;
   if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
   size_t nm = 0, ne = 0, np = 0;
-  if ((uint32_t)(meta[0] >> 32) == (uint32_t)e->round && e->round > 0) {
+  if (meta[0].x == (uint32_t)e->round && e->round > 0) {
     // send order across destinations is not recorded per message; the
     // per-destination order is (messages are compared per destination)
     for (uint32_t to = 0; to < v.R; ++to) {
-      int rc = export_pair(e, buf, (uint32_t)e->round, group, from_slot, to,
-                           out, cap, &nm, ents, ent_cap, &ne, pool, pool_cap,
-                           &np, meta[0]);
+      int rc = export_pair(e, buf, group, from_slot, to, out, cap, &nm, ents,
+                           ent_cap, &ne, pool, pool_cap, &np, meta[0]);
       if (rc) return rc;
     }
   }

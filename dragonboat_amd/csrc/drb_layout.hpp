@@ -38,20 +38,19 @@ enum U64Field : int {
   F_SM_INDEX,
   F_SM_TERM,
   F_KV_COUNT,
-  F_RING_LO,     // lowest index still resident in the window (internal)
+  // internal (not part of drb_replica_state)
+  F_RING_LO,     // lowest index still resident in the window
   F_RING_GUARD,  // lowest index referenced by last round's Replicates
+  F_TERM_START,  // every entry in [term_start, last] has term == r.term
   NUM_U64
 };
+constexpr int NUM_U64_EXPORTED = F_RING_LO;
 
 // per-replica u32 fields, array [F][slot][g]
 enum U32Field : int { W_ROLE = 0, W_FLAGS, W_FB_REASON, W_RI_COUNT, NUM_U32 };
 
-// message record: 4 x uint4 = 64 B, chunks written only as the type needs
-//   c0 = {meta u32 (type | reject<<8 | n_entries<<16), 0, term u64}
-//   c1 = {log_index, log_term}
-//   c2 = {commit, hint}
-//   c3 = {hint_high, 0}
-constexpr int MSG_CHUNKS = 4;
+// message record: 1-2 x uint4 (drb_msg.hpp)
+constexpr int MSG_CHUNKS = 2;
 // entry meta in the ring: 3 x uint4 = 48 B (+ cmd_cap bytes of Cmd)
 //   m0 = {term, key}  m1 = {client_id, series_id}
 //   m2 = {responded_to, type u32 | cmd_len u32 << 32}
@@ -87,7 +86,7 @@ struct View {
   uint32_t *ri_conf;      // [R][D][G]
   uint4 *ring;            // [R][W][ENT_META + C16][G]
   uint4 *mbox;            // [2][R*R][MB][MSG_CHUNKS][G]
-  uint64_t *mbox_meta;    // [2][R][G] (tag << 32 | 4-bit counts per dest)
+  uint4 *mbox_meta;       // [2][R][G] {tag, 4-bit count per dest, term}
   uint4 *kv;              // [R][G][KS][KVW]
   uint4 *props;           // [P][max_props][PROP_META + C16][G]
   uint32_t *prop_count;   // [P][G]

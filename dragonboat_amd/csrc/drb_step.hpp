@@ -17,6 +17,7 @@
 #pragma once
 #include "../../include/drb_engine.h"
 #include "drb_layout.hpp"
+#include "drb_msg.hpp"
 
 namespace drb {
 
@@ -44,7 +45,7 @@ struct Rep {
   uint64_t rand_timeout, tick_count, committed, processed, last, marker;
   uint64_t saved_to, applied_to_index, applied_to_term, applied_index;
   uint64_t confirmed_index, pushed_index, prev_term, prev_vote, prev_commit;
-  uint64_t sm_index, sm_term, kv_count, ring_lo, ring_guard;
+  uint64_t sm_index, sm_term, kv_count, ring_lo, ring_guard, term_start;
   uint32_t role, flags, fb, ri_count;
   // leader remotes live in LDS (RemLds), see rem_get/rem_put
   // leader: readIndex queue
@@ -102,6 +103,7 @@ DRB_DEV void set_error(Rep<R> &r, uint32_t reason) {
 template <int R>
 DRB_DEV uint64_t log_term(const Lane &L, Rep<R> &r, uint64_t index) {
   if (index == 0 || index > r.last) return 0;  // first-1 == 0 on this path
+  if (index >= r.term_start) return r.term;    // no HBM access on the tail
   if (index < r.ring_lo) {
     set_error(r, DRB_ERR_LOG_RANGE);
     return 0;
@@ -120,17 +122,8 @@ DRB_DEV uint64_t ring_term(const Lane &L, uint32_t slot, uint64_t index) {
 }
 
 // ------------------------------------------------------------ messages
-struct Msg {
-  uint32_t type, reject, n;
-  uint64_t term, log_index, log_term, commit, hint, hint_high;
-};
-
-__host__ __device__ inline uint32_t msg_meta(uint32_t type, uint32_t reject,
-                                             uint32_t n) {
-  return type | (reject << 8) | (n << 16);
-}
-
-// send (raft.go:683-687): From = self, Term = r.term for non-request types
+// send (raft.go:683-687): From = self; the Term of every non-request
+// message is r.term and lives in the outbox meta word
 template <int R>
 DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   const View &v = *L.v;
@@ -141,91 +134,22 @@ DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   }
   r.out_cnt += 1u << (4 * to_slot);
   r.nmsgs++;
-  uint64_t term = (m.type == DRB_MSG_READ_INDEX) ? 0 : r.term;
-  v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] =
-      make_uint4(msg_meta(m.type, m.reject, m.n), 0, (uint32_t)term,
-                 (uint32_t)(term >> 32));
-  switch (m.type) {
-    case DRB_MSG_REPLICATE:
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] =
-          mk4(m.log_index, m.log_term);
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] =
-          mk4(m.commit, 0);
-      break;
-    case DRB_MSG_REPLICATE_RESP:
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] =
-          mk4(m.log_index, 0);
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] = mk4(0, m.hint);
-      break;
-    case DRB_MSG_HEARTBEAT:
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] =
-          mk4(m.commit, m.hint);
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 3, L.g)] =
-          mk4(m.hint_high, 0);
-      break;
-    case DRB_MSG_HEARTBEAT_RESP:
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] = mk4(0, m.hint);
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 3, L.g)] =
-          mk4(m.hint_high, 0);
-      break;
-    default:  // ReadIndexResp / ReadIndex: every field
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] =
-          mk4(m.log_index, m.log_term);
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 2, L.g)] =
-          mk4(m.commit, m.hint);
-      v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 3, L.g)] =
-          mk4(m.hint_high, 0);
-      break;
-  }
+  Msg mm = m;
+  mm.term = is_request_type(m.type) ? 0 : r.term;
+  uint4 c0, c1;
+  bool has = msg_encode(mm, c0, c1);
+  v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] = c0;
+  if (has) v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] = c1;
 }
 
-DRB_DEV Msg read_msg(const Lane &L, uint32_t from, uint32_t k) {
+DRB_DEV Msg read_msg(const Lane &L, uint32_t from, uint32_t k,
+                     uint64_t sender_term) {
   const View &v = *L.v;
-  Msg m;
   uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 0, L.g)];
-  m.type = c0.x & 0xffu;
-  m.reject = (c0.x >> 8) & 1u;
-  m.n = c0.x >> 16;
-  m.term = hi64(c0);
-  m.log_index = m.log_term = m.commit = m.hint = m.hint_high = 0;
-  switch (m.type) {
-    case DRB_MSG_REPLICATE: {
-      uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
-      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
-      m.log_index = lo64(c1);
-      m.log_term = hi64(c1);
-      m.commit = lo64(c2);
-      break;
-    }
-    case DRB_MSG_REPLICATE_RESP: {
-      uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
-      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
-      m.log_index = lo64(c1);
-      m.hint = hi64(c2);
-      break;
-    }
-    case DRB_MSG_HEARTBEAT:
-    case DRB_MSG_HEARTBEAT_RESP: {
-      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
-      uint4 c3 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 3, L.g)];
-      m.commit = lo64(c2);
-      m.hint = hi64(c2);
-      m.hint_high = lo64(c3);
-      break;
-    }
-    default: {
-      uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
-      uint4 c2 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 2, L.g)];
-      uint4 c3 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 3, L.g)];
-      m.log_index = lo64(c1);
-      m.log_term = hi64(c1);
-      m.commit = lo64(c2);
-      m.hint = hi64(c2);
-      m.hint_high = lo64(c3);
-      break;
-    }
-  }
-  return m;
+  bool has = (c0.x & MF_HAS_C1) != 0;
+  uint4 c1 = make_uint4(0, 0, 0, 0);
+  if (has) c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
+  return msg_decode(c0, c1, has, sender_term);
 }
 
 // ------------------------------------------------------------ remote FSM
@@ -635,13 +559,20 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
           set_error(r, DRB_ERR_APPEND);
         r.saved_to = umin64(r.saved_to, ci - 1);
       }
-      // copy entries [ci, new_last] from the leader's window
+      // copy entries [ci, new_last] from the leader's window; keep the
+      // [term_start, last] == r.term invariant (terms never decrease
+      // along a log and never exceed the leader's term)
       const uint32_t chunks = ENT_META + v.C16;
+      uint64_t ts = new_last + 1;
       for (uint64_t idx = ci; idx <= new_last; ++idx) {
-        for (uint32_t c = 0; c < chunks; ++c)
+        uint4 m0 = v.ring[ring_ix(v, (uint32_t)s, idx, 0, L.g)];
+        v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = m0;
+        if (ts > new_last && lo64(m0) == r.term) ts = idx;
+        for (uint32_t c = 1; c < chunks; ++c)
           v.ring[ring_ix(v, L.slot, idx, c, L.g)] =
               v.ring[ring_ix(v, (uint32_t)s, idx, c, L.g)];
       }
+      if (ci <= r.term_start) r.term_start = ts;
       r.last = new_last;
       if (new_last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, new_last + 1 - v.W);
     }
@@ -861,6 +792,7 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   LD(F_KV_COUNT, kv_count);
   LD(F_RING_LO, ring_lo);
   LD(F_RING_GUARD, ring_guard);
+  LD(F_TERM_START, term_start);
 #undef LD
   r.role = v.u32[u32_ix(v, W_ROLE, L.slot, L.g)];
   r.flags = v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)];
@@ -940,6 +872,7 @@ DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, const Cold &o) {
   ST(F_KV_COUNT, kv_count);
   ST(F_RING_LO, ring_lo);
   ST(F_RING_GUARD, ring_guard);
+  ST(F_TERM_START, term_start);
 #undef ST
 #undef STC
   if (r.flags != o.flags) v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)] = r.flags;
@@ -1022,20 +955,21 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
     const bool is_leader = r.role == DRB_LEADER;
     if (!is_leader && r.role != DRB_FOLLOWER) fb = DRB_FB_ROLE;
     uint32_t nin_packed = 0;  // 4-bit inbox count per sender slot
-    uint32_t total_in = 0, n_ri_msgs = 0, resp_from = 0;
+    uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
     uint64_t max_app = 0;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot) continue;
-      uint64_t meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, g)];
+      const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, g)];
       uint32_t ns = 0;
-      if ((uint32_t)(meta >> 32) == tag_prev)
-        ns = (uint32_t)(meta >> (4 * slot)) & 15u;
+      if (meta.x == tag_prev) ns = (meta.y >> (4 * slot)) & 15u;
       nin_packed |= ns << (4 * s);
+      const uint64_t sterm = hi64(meta);
       for (uint32_t k = 0; k < ns; ++k) {
         uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
         uint32_t type = c0.x & 0xffu;
-        uint64_t mterm = hi64(c0);
+        uint64_t mterm = (c0.x & MF_TERM_ZERO) ? 0 : sterm;
+        if (c0.x & MF_TERM_OTHER) mterm = ~0ull;
         bool ok;
         if (is_leader)
           ok = type == DRB_MSG_REPLICATE_RESP ||
@@ -1047,17 +981,14 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
         if (mterm != 0 && mterm != r.term && fb == DRB_FB_NONE)
           fb = DRB_FB_TERM_MISMATCH;
         if (type == DRB_MSG_READ_INDEX) n_ri_msgs++;
+        if (type == DRB_MSG_REPLICATE_RESP) n_rr++;
         if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)
           resp_from |= 1u << s;
-        if (type == DRB_MSG_REPLICATE) {
-          uint4 c1 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
-          max_app = umax64(max_app, lo64(c1) + (c0.x >> 16));
-        }
+        if (type == DRB_MSG_REPLICATE)
+          max_app = umax64(max_app, hi64(c0) + (c0.x >> 16));
       }
       total_in += ns;
     }
-    // messages per destination <= inbox + readIndex + tick + proposal
-    if (total_in + 3 > v.MB && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
     uint32_t nprops = 0;
     uint64_t in_lo = 0, in_hi = 0;
     // lowest index the round may still read: apply cursor, commit term,
@@ -1090,6 +1021,24 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
         if ((uint32_t)s != slot) keep = umin64(keep, rem_get<R>(L, s).n - 1);
       if (nprops && r.last + nprops >= keep + v.W && fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
+      // mailbox: messages the round can send to each follower s.  Each
+      // message from s triggers at most one send back to s (resend,
+      // retry, raft.go:1878-1923); a broadcast to everyone needs a commit
+      // advance (raft.go:1885), so there are at most min(#ReplicateResp,
+      // last - committed) of them; plus the ReadIndex / tick heartbeats,
+      // the proposal broadcast and ReadIndexResps of queued requests.
+      {
+        uint64_t adv = r.last > r.committed ? r.last - r.committed : 0;
+        uint32_t nb = (uint32_t)umin64((uint64_t)n_rr, adv);
+        uint32_t base = (in_lo != 0) + (p.tick ? 1 : 0) + (nprops ? 1 : 0) +
+                        n_ri_msgs * 2 + r.ri_count + nb;
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          if ((uint32_t)s == slot) continue;
+          uint32_t bound = base + ((nin_packed >> (4 * s)) & 15u);
+          if (bound > v.MB && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
+        }
+      }
       // tick: CheckQuorum (raft.go:623-633)
       if (p.tick && v.check_quorum &&
           r.election_tick + 1 >= v.election_rtt) {
@@ -1130,11 +1079,14 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
         for (int s = 0; s < R; ++s) {
           if ((uint32_t)s == slot) continue;
           const uint32_t ns = (nin_packed >> (4 * s)) & 15u;
+          if (!ns) continue;
+          const uint64_t sterm =
+              hi64(v.mbox_meta[mmeta_ix(v, L.rbuf, s, g)]);
           for (uint32_t k = 0; k < ns; ++k) {
             uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
             bool isrep = (c0.x & 0xffu) == DRB_MSG_REPLICATE;
             if (isrep != (pass == 0)) continue;
-            Msg m = read_msg(L, s, k);
+            Msg m = read_msg(L, s, k, sterm);
             dispatch(L, r, s, m);
           }
         }
@@ -1263,8 +1215,12 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
       c_drop = r.ndropped_ri;
     }
     // outbox meta for this round (tag = round): written even when empty
-    v.mbox_meta[mmeta_ix(v, L.wbuf, slot, g)] =
-        ((uint64_t)(uint32_t)p.round << 32) | r.out_cnt;
+    {
+      uint4 meta = mk4(0, r.term);
+      meta.x = (uint32_t)p.round;
+      meta.y = r.out_cnt;
+      v.mbox_meta[mmeta_ix(v, L.wbuf, slot, g)] = meta;
+    }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
   }
   wave_add(&v.counters[C_COMMITTED], c_commit);
