@@ -109,9 +109,8 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from dragonboat_amd import dist as ddist
+    world, rank, local = ddist.env()
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -119,11 +118,11 @@ def main():
     G, R, k = args.groups, args.replicas, args.k
     reads = not args.no_read_index
     NP = 8  # staged input batches (resident in HBM before timing)
+    first_shard, seed = ddist.shard_plan(rank, G)
     eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                  max_props=max(1, k), prop_slots=NP, ri_slots=NP,
                  mailbox=15, kv_slots=512, kv_val_cap=4,
-                 first_shard_id=1 + rank * G, device=local)
-    seed = 0x5EEDD8B0 ^ rank
+                 first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
         eng.gen_kv_proposals(b, k, 256, 4, seed, b)
@@ -146,11 +145,7 @@ def main():
     warm_ms = (time.perf_counter() - tw0) * 1e3 / max(1, args.warmup)
     if args.tick_every <= 0:
         te = max(1, int(round(args.tick_ms / max(warm_ms, 1e-6))))
-        if world > 1:
-            t = torch.tensor([te], dtype=torch.int64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            te = int(t.item())
-        tick_every[0] = te
+        tick_every[0] = ddist.agree_min(te, "cuda")
         for i in range(args.warmup, 2 * args.warmup):
             step(i)
         eng.sync()
@@ -159,8 +154,7 @@ def main():
     K = args.steps
     ev = [(torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    if world > 1:
-        dist.barrier()
+    ddist.barrier()
     torch.cuda.synchronize()
     eng.sync()
     t0 = time.perf_counter()
@@ -170,20 +164,14 @@ def main():
         ev[i][1].record(stream)
     eng.sync()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    ddist.barrier()
     t1 = time.perf_counter()
     out = eng.read_counters(reset=True)
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
     elapsed = t1 - t0
     committed = out.committed_entries
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        c = torch.tensor([committed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(c)
-        committed = int(c.item())
+    elapsed = ddist.reduce_max(elapsed, "cuda")
+    committed = ddist.reduce_sum(committed, "cuda")
     value = committed / elapsed
     alg = alg_bytes_per_group_round(R, k, 16, reads) * G
     achieved = alg / (kern_ms * 1e-3) / 1e9
