@@ -12,7 +12,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libdrb_engine.so")
 SOURCES = ["drb_engine.hip"]
-HEADERS = ["drb_layout.hpp", "drb_step.hpp"]
+HEADERS = ["drb_layout.hpp", "drb_msg.hpp", "drb_step.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
@@ -29,7 +29,15 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in _deps())
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, out=None, defines=()):
+    """Builds the engine; `out`/`defines` build a tuning variant elsewhere."""
+    if out is not None:
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
+               "-shared", "-Wno-pass-failed", "-o", out] + \
+            ["-D" + d for d in defines] + \
+            [os.path.join(CSRC, f) for f in SOURCES]
+        subprocess.check_call(cmd)
+        return out
     if not force and up_to_date():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)

@@ -36,6 +36,8 @@ struct drb_engine {
   uint64_t round;
   uint64_t bytes;
   std::vector<void *> allocs;
+  uint64_t ctr_rows = 0;                     // workgroup counter rows
+  unsigned long long *ctr_total = nullptr;   // their sum (read_counters)
   void *scratch;
   size_t scratch_bytes;
 };
@@ -216,7 +218,9 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.ri_in, (uint64_t)cfg->ri_slots * G);
   rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
   rc |= dalloc(e, &v.rtr_count, R * G);
-  rc |= dalloc(e, &v.counters, NUM_COUNTERS);
+  e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
+  rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
+  rc |= dalloc(e, &e->ctr_total, NUM_COUNTERS);
   rc |= dalloc(e, &e->dview, 1);
   if (!rc) {  // no Replicate in flight: ring_guard = +inf
     k_fill_u64<<<(unsigned)((R * G + 255) / 256), 256, 0, e->stream>>>(
@@ -833,7 +837,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
 template <int R>
 static void launch_step(drb_engine *e, const RoundParams &p) {
   dim3 grid((unsigned)((e->v.G + 255) / 256), R);
-  step_kernel<R><<<grid, 256, 0, e->stream>>>(e->dview, p);
+  step_kernel<R, true><<<grid, 256, 0, e->stream>>>(e->v, p);
+  step_kernel<R, false><<<grid, 256, 0, e->stream>>>(e->v, p);
 }
 
 extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
@@ -864,11 +869,33 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   return DRB_OK;
 }
 
+// sums the per-workgroup counter rows of the step kernels
+__global__ void k_sum_counters(const unsigned long long *rows, uint64_t n,
+                               unsigned long long *total) {
+  __shared__ unsigned long long part[256];
+  for (int c = 0; c < NUM_COUNTERS; ++c) {
+    unsigned long long s = 0;
+    for (uint64_t r = threadIdx.x; r < n; r += blockDim.x)
+      s += rows[r * NUM_COUNTERS + c];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < (unsigned)o) part[threadIdx.x] += part[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) total[c] = part[0];
+    __syncthreads();
+  }
+}
+
 extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
                                  int reset) {
   if (!e || !out) return DRB_EINVAL;
   unsigned long long c[NUM_COUNTERS];
-  HIPCHK(hipMemcpyAsync(c, e->v.counters, sizeof(c), hipMemcpyDeviceToHost,
+  k_sum_counters<<<1, 256, 0, e->stream>>>(e->v.counters, e->ctr_rows,
+                                           e->ctr_total);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(c, e->ctr_total, sizeof(c), hipMemcpyDeviceToHost,
                         e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   out->round = e->round;
@@ -880,7 +907,9 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->fallbacks = c[C_FALLBACKS];
   out->errors = c[C_ERRORS];
   if (reset) {
-    HIPCHK(hipMemsetAsync(e->v.counters, 0, sizeof(c), e->stream));
+    HIPCHK(hipMemsetAsync(e->v.counters, 0,
+                          e->ctr_rows * NUM_COUNTERS * sizeof(c[0]),
+                          e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
   }
   return DRB_OK;
@@ -890,7 +919,8 @@ extern "C" int drb_step_round(drb_engine *e, const drb_round_in *in,
                               drb_round_out *out) {
   if (!e || !in) return DRB_EINVAL;
   HIPCHK(hipMemsetAsync(e->v.counters, 0,
-                        NUM_COUNTERS * sizeof(unsigned long long), e->stream));
+                        e->ctr_rows * NUM_COUNTERS * sizeof(unsigned long long),
+                        e->stream));
   int rc = drb_step_round_async(e, in);
   if (rc) return rc;
   if (out) return drb_read_counters(e, out, 1);

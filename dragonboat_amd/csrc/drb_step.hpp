@@ -23,6 +23,11 @@ namespace drb {
 
 #define DRB_DEV __device__ __forceinline__
 
+// minimum waves per SIMD the step kernels are compiled for (register cap)
+#ifndef DRB_STEP_WAVES
+#define DRB_STEP_WAVES 1
+#endif
+
 constexpr uint64_t MAX_ENTRY_SIZE = 64ull * 1024 * 1024;  // soft.go:186
 
 // counters[] slots
@@ -646,12 +651,30 @@ struct Cmd4 {
   uint4 c0, c1, c2, c3;
 };
 
-DRB_DEV uint8_t chunk_byte(const Cmd4 &c, uint32_t i) {
-  const uint32_t qi = i >> 4;
-  const uint4 q = qi == 0 ? c.c0 : qi == 1 ? c.c1 : qi == 2 ? c.c2 : c.c3;
-  uint32_t w = (i >> 2) & 3;
-  uint32_t word = w == 0 ? q.x : w == 1 ? q.y : w == 2 ? q.z : q.w;
-  return (uint8_t)(word >> (8 * (i & 3)));
+// 32-bit word w (0..15) of the Cmd through a select tree on values (by-
+// value operands: a select between two lvalues becomes a select between
+// addresses, and the Cmd then lives in scratch memory).
+DRB_DEV uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+DRB_DEV uint32_t sel4(uint32_t w, uint4 q) {
+  return sel(w & 2, sel(w & 1, q.w, q.z), sel(w & 1, q.y, q.x));
+}
+DRB_DEV uint32_t cmd_word(const Cmd4 &c, uint32_t w) {
+  const uint32_t a = sel4(w, c.c0), b = sel4(w, c.c1), d = sel4(w, c.c2),
+                 e = sel4(w, c.c3);
+  const uint32_t x = sel(w & 8, sel(w & 4, e, d), sel(w & 4, b, a));
+  return sel(w & 16, 0u, x);
+}
+DRB_DEV uint32_t cmd_byte(const Cmd4 &c, uint32_t i) {
+  return (cmd_word(c, i >> 2) >> (8 * (i & 3))) & 0xffu;
+}
+// 4 bytes starting at byte offset o (little endian)
+DRB_DEV uint32_t cmd_u32_at(const Cmd4 &c, uint32_t o) {
+  const uint64_t x = (uint64_t)cmd_word(c, o >> 2) |
+                     ((uint64_t)cmd_word(c, (o >> 2) + 1) << 32);
+  return (uint32_t)(x >> (8 * (o & 3)));
+}
+DRB_DEV uint32_t byte_mask(uint32_t n) {  // low n (<= 4) bytes
+  return n >= 4 ? 0xffffffffu : ((1u << (8 * n)) - 1u);
 }
 
 // handleEntry (statemachine.go:935-969) -> update (1057-1103) ->
@@ -676,18 +699,15 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   if (series_id != 0) return -1;  // sessions stay on the CPU path
   // the Cmd, staged in registers (cmd_cap <= 64 B on this path: C16 <= 4)
   Cmd4 cmd;
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
   cmd.c0 = v.ring[ring_ix(v, L.slot, index, ENT_META, L.g)];
-  cmd.c1 = v.C16 > 1 ? v.ring[ring_ix(v, L.slot, index, ENT_META + 1, L.g)]
-                     : z4;
-  cmd.c2 = v.C16 > 2 ? v.ring[ring_ix(v, L.slot, index, ENT_META + 2, L.g)]
-                     : z4;
-  cmd.c3 = v.C16 > 3 ? v.ring[ring_ix(v, L.slot, index, ENT_META + 3, L.g)]
-                     : z4;
+  cmd.c1 = cmd.c2 = cmd.c3 = make_uint4(0, 0, 0, 0);
+  if (v.C16 > 1) cmd.c1 = v.ring[ring_ix(v, L.slot, index, ENT_META + 1, L.g)];
+  if (v.C16 > 2) cmd.c2 = v.ring[ring_ix(v, L.slot, index, ENT_META + 2, L.g)];
+  if (v.C16 > 3) cmd.c3 = v.ring[ring_ix(v, L.slot, index, ENT_META + 3, L.g)];
   uint32_t off = 0, plen = clen;
   if (type == DRB_ENTRY_ENCODED) {
     if (clen == 0) return -1;
-    uint8_t h = chunk_byte(cmd, 0);
+    uint32_t h = cmd_byte(cmd, 0);
     if ((h & 0xf0) != 0 || (h & 0x0e) != 0 || (h & 1)) return -1;
     off = 1;
     plen = clen - 1;
@@ -700,16 +720,17 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   bool have_k = false, have_v = false;
   uint32_t i = 0;
   while (i < plen) {
-    uint8_t tag = chunk_byte(cmd, off + i);
+    uint32_t tag = cmd_byte(cmd, off + i);
     if (i + 1 >= plen) return -1;
-    uint8_t l = chunk_byte(cmd, off + i + 1);
+    uint32_t l = cmd_byte(cmd, off + i + 1);
     if (l >= 0x80) return -1;
     if (i + 2 + l > plen) return -1;
     if (tag == 0x0a) {
       if (l > 8) return -1;
-      key8 = 0;
-      for (uint32_t b = 0; b < l; ++b)
-        key8 |= (uint64_t)chunk_byte(cmd, off + i + 2 + b) << (8 * b);
+      const uint32_t ko = off + i + 2;
+      key8 = (uint64_t)(cmd_u32_at(cmd, ko) & byte_mask(l)) |
+             ((uint64_t)(cmd_u32_at(cmd, ko + 4) &
+                         byte_mask(l > 4 ? l - 4 : 0)) << 32);
       klen = l;
       have_k = true;
     } else if (tag == 0x12) {
@@ -735,19 +756,17 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
     bool hit = used && sklen == klen && lo64(h) == key8;
     if (!used || hit) {
       // value bytes: first 4 in h.w, the rest in the following chunks
-      uint32_t w0 = 0;
-      for (uint32_t b = 0; b < vlen && b < 4; ++b)
-        w0 |= (uint32_t)chunk_byte(cmd, voff + b) << (8 * b);
+      const uint32_t w0 = cmd_u32_at(cmd, voff) & byte_mask(vlen);
       sl[0] = make_uint4((uint32_t)key8, (uint32_t)(key8 >> 32),
                          (1u << 31) | (vlen << 8) | klen, w0);
       for (uint32_t c = 1; c < v.KVW; ++c) {
-        uint32_t wv[4] = {0, 0, 0, 0};
+        uint32_t wv[4];
 #pragma unroll
-        for (uint32_t b = 0; b < 16; ++b) {
-          uint32_t src = 4 + (c - 1) * 16 + b;
-          if (src < vlen)
-            wv[b >> 2] |= (uint32_t)chunk_byte(cmd, voff + src)
-                          << (8 * (b & 3));
+        for (uint32_t t = 0; t < 4; ++t) {
+          const uint32_t src = 4 + (c - 1) * 16 + 4 * t;  // value byte
+          wv[t] = src < vlen ? cmd_u32_at(cmd, voff + src) &
+                                   byte_mask(vlen - src)
+                             : 0u;
         }
         sl[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
       }
@@ -762,7 +781,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
 }
 
 // ------------------------------------------------------------ load/store
-template <int R>
+template <int R, bool LEAD>
 DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   const View &v = *L.v;
 #define LD(F, x) r.x = v.u64[u64_ix(v, F, L.slot, L.g)]
@@ -794,11 +813,10 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   LD(F_RING_GUARD, ring_guard);
   LD(F_TERM_START, term_start);
 #undef LD
-  r.role = v.u32[u32_ix(v, W_ROLE, L.slot, L.g)];
   r.flags = v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)];
   r.fb = v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)];
   r.ri_count = v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)];
-  if (r.role == DRB_LEADER) {
+  if (LEAD) {
 #pragma unroll
     for (int s = 0; s < R; ++s)
       rem_put<R>(L, s,
@@ -809,7 +827,7 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   }
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d) {
-    if ((uint32_t)d < r.ri_count) {
+    if (LEAD && (uint32_t)d < r.ri_count) {
       uint4 c = v.ri_ctx[ri_ix(v, L.slot, d, L.g)];
       uint4 i = v.ri_idx[ri_ix(v, L.slot, d, L.g)];
       r.ri_lo[d] = lo64(c);
@@ -840,7 +858,7 @@ DRB_DEV Cold cold_of(const Rep<R> &r) {
               r.flags,     r.fb};
 }
 
-template <int R>
+template <int R, bool LEAD>
 DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, const Cold &o) {
   const View &v = *L.v;
 #define STC(F, x) \
@@ -877,8 +895,9 @@ DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, const Cold &o) {
 #undef STC
   if (r.flags != o.flags) v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)] = r.flags;
   if (r.fb != o.fb) v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)] = r.fb;
+  if (!LEAD) return;  // followers keep no remotes and no readIndex queue
   v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)] = r.ri_count;
-  if (r.role == DRB_LEADER) {
+  {
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       RemoteV x = rem_get<R>(L, s);
@@ -906,19 +925,52 @@ struct RoundParams {
   uint32_t pad;
 };
 
-DRB_DEV void wave_add(unsigned long long *ctr, uint64_t val) {
-  // one atomic per wavefront: reduce over the 64 lanes first
-  uint64_t s = val;
+// Round counters: each workgroup owns one row of NUM_COUNTERS u64 in
+// v.counters ([2 roles][R slots][gridDim.x][NUM_COUNTERS]) and adds its
+// totals to it with plain loads and stores; drb_read_counters sums the rows.
+// (Global atomics from every wave onto 8 shared addresses serialise at the
+// memory side -- ~14 ns each -- and were the round's critical path.)
+DRB_DEV uint32_t wave_sum(uint32_t x) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(ctr, (unsigned long long)s);
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
 }
 
-template <int R>
-__global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
+template <bool LEAD>
+DRB_DEV void block_counters(const View &v, const uint32_t (&c)[NUM_COUNTERS]) {
+  __shared__ uint32_t red[4][NUM_COUNTERS];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < C_ROUNDS; ++i) {
+    const uint32_t s = wave_sum(c[i]);
+    if (lane == 0) red[wave][i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < C_ROUNDS) {
+    const uint32_t i = threadIdx.x;
+    const uint64_t s = (uint64_t)red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if (s) {
+      const uint64_t row =
+          ((uint64_t)(LEAD ? 0 : 1) * gridDim.y + blockIdx.y) * gridDim.x +
+          blockIdx.x;
+      v.counters[row * NUM_COUNTERS + i] += s;
+    }
+  }
+}
+
+// LEAD selects the role this launch steps: the leader kernel takes the
+// replicas whose role is LEADER, the follower kernel every other replica
+// (non-FOLLOWER roles fall back).  Both read round t-1's mailbox and write
+// round t's, so the two launches of a round are independent; compiling the
+// roles apart keeps each one's register footprint (and so its occupancy)
+// to what its own handlers need.
+template <int R, bool LEAD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
-  // the View lives in HBM: every field load is wave-uniform (s_load)
-  const View &v = *vp;
+  // the View is a by-value kernel argument: its fields are wave-uniform
+  // kernarg loads, and the pointers loaded from it are known to address
+  // global memory (global_load/store, not flat: no LDS-counter waits)
+  const View *vp = &v;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t slot = blockIdx.y;
   __shared__ RemLds<R> rl;
@@ -935,11 +987,14 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
   uint64_t c_rtr = 0, c_drop = 0;
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
-  if (!(flags & DRB_F_HOSTED) || (flags & (DRB_F_FALLBACK | DRB_F_ERROR)))
+  uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
+  if (!(flags & DRB_F_HOSTED) || (flags & (DRB_F_FALLBACK | DRB_F_ERROR)) ||
+      ((role == DRB_LEADER) != LEAD))
     active = false;
   if (active) {
     Rep<R> r;
-    load_rep(L, r);
+    load_rep<R, LEAD>(L, r);
+    r.role = LEAD ? DRB_LEADER : DRB_FOLLOWER;
     r.out_cnt = 0;
     r.nmsgs = 0;
     r.nrtr = 0;
@@ -952,8 +1007,8 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
 
     // ---------------------------------------------- pre-pass (read only)
     uint32_t fb = DRB_FB_NONE;
-    const bool is_leader = r.role == DRB_LEADER;
-    if (!is_leader && r.role != DRB_FOLLOWER) fb = DRB_FB_ROLE;
+    constexpr bool is_leader = LEAD;
+    if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) fb = DRB_FB_ROLE;
     uint32_t nin_packed = 0;  // 4-bit inbox count per sender slot
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
     uint64_t max_app = 0;
@@ -1209,7 +1264,7 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
         r.flags |= DRB_F_ERROR;
         c_err = 1;
       }
-      store_rep(L, r, orig);
+      store_rep<R, LEAD>(L, r, orig);
       c_msgs = r.nmsgs;
       c_rtr = r.nrtr;
       c_drop = r.ndropped_ri;
@@ -1223,13 +1278,11 @@ __global__ __launch_bounds__(256) void step_kernel(const View *__restrict__ vp,
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
   }
-  wave_add(&v.counters[C_COMMITTED], c_commit);
-  wave_add(&v.counters[C_APPLIED], c_applied);
-  wave_add(&v.counters[C_MESSAGES], c_msgs);
-  wave_add(&v.counters[C_RTR], c_rtr);
-  wave_add(&v.counters[C_DROPPED_RI], c_drop);
-  wave_add(&v.counters[C_FALLBACKS], c_fb);
-  wave_add(&v.counters[C_ERRORS], c_err);
+  const uint32_t cnt[NUM_COUNTERS] = {
+      (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,
+      (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
+      (uint32_t)c_err,    0u};
+  block_counters<LEAD>(v, cnt);
 }
 
 }  // namespace drb

@@ -12,7 +12,8 @@ from .abi import (Config, Entry, Message, ReadyToRead, ReplicaState, RoundIn,
                   RoundOut, entry_to_tuple, message_to_tuple)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libdrb_engine.so")
+LIB_PATH = os.environ.get("DRB_ENGINE_LIB") or \
+    os.path.join(HERE, "_lib", "libdrb_engine.so")
 
 _lib = None
 
