@@ -43,14 +43,20 @@ enum : int {
   NUM_COUNTERS
 };
 
+// The fields a round reads or writes on most of its paths live in
+// registers; the rest (vote, tick_count, the randomized timeout, Peer's
+// prevState, node's confirmed/pushed indexes, appliedTo*, sm_term,
+// kv_count) are loaded and stored in place where the round touches them
+// (ld_f / st_f), which keeps both the register file and the HBM traffic of
+// a round to what that round actually uses.
 template <int R>
 struct Rep {
-  // raft / entryLog / inMemory / node / rsm state
-  uint64_t term, vote, leader_id, applied, election_tick, heartbeat_tick;
-  uint64_t rand_timeout, tick_count, committed, processed, last, marker;
-  uint64_t saved_to, applied_to_index, applied_to_term, applied_index;
-  uint64_t confirmed_index, pushed_index, prev_term, prev_vote, prev_commit;
-  uint64_t sm_index, sm_term, kv_count, ring_lo, ring_guard, term_start;
+  uint64_t term, leader_id, election_tick, heartbeat_tick;
+  uint64_t committed, processed, last, marker, saved_to;
+  uint64_t applied_index, sm_index, ring_lo, ring_guard, term_start;
+  uint64_t sm_term;      // valid when kv_added / applied_any
+  uint32_t kv_added;     // KVTest.Count increments this round
+  bool applied_any, lid_dirty;
   uint32_t role, flags, fb, ri_count;
   // leader remotes live in LDS (RemLds), see rem_get/rem_put
   // leader: readIndex queue
@@ -124,6 +130,22 @@ DRB_DEV uint4 mk4(uint64_t a, uint64_t b) {
 template <int R>
 DRB_DEV uint64_t ring_term(const Lane &L, uint32_t slot, uint64_t index) {
   return lo64(L.v->ring[ring_ix(*L.v, slot, index, 0, L.g)]);
+}
+
+template <int R>
+DRB_DEV void set_leader(Rep<R> &r, uint64_t id) {
+  if (r.leader_id != id) {
+    r.leader_id = id;
+    r.lid_dirty = true;
+  }
+}
+
+// cold fields: loaded / stored in place
+DRB_DEV uint64_t ld_f(const Lane &L, int f) {
+  return L.v->u64[u64_ix(*L.v, f, L.slot, L.g)];
+}
+DRB_DEV void st_f(const Lane &L, int f, uint64_t x) {
+  L.v->u64[u64_ix(*L.v, f, L.slot, L.g)] = x;
 }
 
 // ------------------------------------------------------------ messages
@@ -519,7 +541,7 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
                                 const Msg &m) {
   const View &v = *L.v;
   r.election_tick = 0;  // leaderIsAvailable
-  r.leader_id = (uint64_t)s + 1;
+  set_leader(r, (uint64_t)s + 1);
   r.leader_update = true;
   Msg resp = {};
   resp.type = DRB_MSG_REPLICATE_RESP;
@@ -597,7 +619,7 @@ template <int R>
 DRB_DEV void follower_heartbeat(const Lane &L, Rep<R> &r, int s,
                                 const Msg &m) {
   r.election_tick = 0;
-  r.leader_id = (uint64_t)s + 1;
+  set_leader(r, (uint64_t)s + 1);
   r.leader_update = true;
   commit_to(r, m.commit);
   Msg resp = {};
@@ -612,7 +634,7 @@ template <int R>
 DRB_DEV void follower_read_index_resp(const Lane &L, Rep<R> &r, int s,
                                       const Msg &m) {
   r.election_tick = 0;
-  r.leader_id = (uint64_t)s + 1;
+  set_leader(r, (uint64_t)s + 1);
   r.leader_update = true;
   add_ready(L, r, m.log_index, m.hint, m.hint_high);
 }
@@ -694,6 +716,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
     if (clen != 0) return -1;  // reference panics
     r.sm_index = index;
     r.sm_term = term;
+    r.applied_any = true;
     return 0;
   }
   if (series_id != 0) return -1;  // sessions stay on the CPU path
@@ -770,9 +793,10 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
         }
         sl[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
       }
-      r.kv_count++;
+      r.kv_added++;
       r.sm_index = index;
       r.sm_term = term;
+      r.applied_any = true;
       return 1;
     }
     ks = (ks + 1) & mask;
@@ -786,32 +810,23 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   const View &v = *L.v;
 #define LD(F, x) r.x = v.u64[u64_ix(v, F, L.slot, L.g)]
   LD(F_TERM, term);
-  LD(F_VOTE, vote);
   LD(F_LEADER_ID, leader_id);
-  LD(F_APPLIED, applied);
   LD(F_ELECTION_TICK, election_tick);
-  LD(F_HEARTBEAT_TICK, heartbeat_tick);
-  LD(F_RAND_TIMEOUT, rand_timeout);
-  LD(F_TICK_COUNT, tick_count);
+  if (LEAD) LD(F_HEARTBEAT_TICK, heartbeat_tick);
   LD(F_COMMITTED, committed);
   LD(F_PROCESSED, processed);
   LD(F_LAST_INDEX, last);
   LD(F_MARKER_INDEX, marker);
   LD(F_SAVED_TO, saved_to);
-  LD(F_APPLIED_TO_INDEX, applied_to_index);
-  LD(F_APPLIED_TO_TERM, applied_to_term);
   LD(F_APPLIED_INDEX, applied_index);
-  LD(F_CONFIRMED_INDEX, confirmed_index);
-  LD(F_PUSHED_INDEX, pushed_index);
-  LD(F_PREV_TERM, prev_term);
-  LD(F_PREV_VOTE, prev_vote);
-  LD(F_PREV_COMMIT, prev_commit);
   LD(F_SM_INDEX, sm_index);
-  LD(F_SM_TERM, sm_term);
-  LD(F_KV_COUNT, kv_count);
   LD(F_RING_LO, ring_lo);
   LD(F_RING_GUARD, ring_guard);
   LD(F_TERM_START, term_start);
+  r.sm_term = 0;
+  r.kv_added = 0;
+  r.applied_any = false;
+  r.lid_dirty = false;
 #undef LD
   r.flags = v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)];
   r.fb = v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)];
@@ -842,59 +857,30 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   }
 }
 
-// fields that stay constant on the steady-state path: stored only when
-// they changed (keeps their HBM writes, and the registers of a full copy of
-// the pre-round state, off the hot path)
-struct Cold {
-  uint64_t term, vote, leader_id, rand_timeout, prev_term, prev_vote;
-  uint64_t sm_term, applied_to_term;
-  uint32_t flags, fb;
-};
-
-template <int R>
-DRB_DEV Cold cold_of(const Rep<R> &r) {
-  return Cold{r.term,      r.vote,      r.leader_id, r.rand_timeout,
-              r.prev_term, r.prev_vote, r.sm_term,   r.applied_to_term,
-              r.flags,     r.fb};
-}
-
 template <int R, bool LEAD>
-DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, const Cold &o) {
+DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, uint32_t flags0,
+                       uint32_t fb0) {
   const View &v = *L.v;
-#define STC(F, x) \
-  if (r.x != o.x) v.u64[u64_ix(v, F, L.slot, L.g)] = r.x
 #define ST(F, x) v.u64[u64_ix(v, F, L.slot, L.g)] = r.x
-  STC(F_TERM, term);
-  STC(F_VOTE, vote);
-  STC(F_LEADER_ID, leader_id);
-  STC(F_RAND_TIMEOUT, rand_timeout);
-  STC(F_PREV_TERM, prev_term);
-  STC(F_PREV_VOTE, prev_vote);
-  STC(F_SM_TERM, sm_term);
-  STC(F_APPLIED_TO_TERM, applied_to_term);
-  ST(F_APPLIED, applied);
+  // term, vote, prevVote, randomizedElectionTimeout never change on the
+  // fast path (a round that would change them falls back first)
+  if (r.lid_dirty) ST(F_LEADER_ID, leader_id);
   ST(F_ELECTION_TICK, election_tick);
-  ST(F_HEARTBEAT_TICK, heartbeat_tick);
-  ST(F_TICK_COUNT, tick_count);
+  if (LEAD) ST(F_HEARTBEAT_TICK, heartbeat_tick);
   ST(F_COMMITTED, committed);
   ST(F_PROCESSED, processed);
   ST(F_LAST_INDEX, last);
   ST(F_MARKER_INDEX, marker);
   ST(F_SAVED_TO, saved_to);
-  ST(F_APPLIED_TO_INDEX, applied_to_index);
-  ST(F_APPLIED_INDEX, applied_index);
-  ST(F_CONFIRMED_INDEX, confirmed_index);
-  ST(F_PUSHED_INDEX, pushed_index);
-  ST(F_PREV_COMMIT, prev_commit);
   ST(F_SM_INDEX, sm_index);
-  ST(F_KV_COUNT, kv_count);
   ST(F_RING_LO, ring_lo);
   ST(F_RING_GUARD, ring_guard);
   ST(F_TERM_START, term_start);
+  if (r.applied_any) ST(F_SM_TERM, sm_term);
+  if (r.kv_added) st_f(L, F_KV_COUNT, ld_f(L, F_KV_COUNT) + r.kv_added);
 #undef ST
-#undef STC
-  if (r.flags != o.flags) v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)] = r.flags;
-  if (r.fb != o.fb) v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)] = r.fb;
+  if (r.flags != flags0) v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)] = r.flags;
+  if (r.fb != fb0) v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)] = r.fb;
   if (!LEAD) return;  // followers keep no remotes and no readIndex queue
   v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)] = r.ri_count;
   {
@@ -1002,7 +988,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
     r.guard_new = ~0ull;
     r.leader_update = false;
     r.err = false;
-    const Cold orig = cold_of(r);
+    const uint32_t flags0 = r.flags, fb0 = r.fb;
     const uint32_t tag_prev = (uint32_t)(p.round - 1);
 
     // ---------------------------------------------- pre-pass (read only)
@@ -1111,7 +1097,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
         fb = DRB_FB_CAPACITY;
       if (p.tick) {
         uint64_t et = (total_in ? 0 : r.election_tick) + 1;
-        if (et >= r.rand_timeout && fb == DRB_FB_NONE) fb = DRB_FB_ELECTION;
+        if (et >= ld_f(L, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
+          fb = DRB_FB_ELECTION;
       }
     }
     if (fb != DRB_FB_NONE) {
@@ -1124,7 +1111,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
       // ---------------------------------------- handleEvents (node.go)
       // updateAppliedIndex (node.go:1133-1137)
       r.applied_index = r.sm_index;
-      r.applied = r.applied_index;
+      st_f(L, F_APPLIED, r.applied_index);
+      st_f(L, F_APPLIED_INDEX, r.applied_index);
       // handleReadIndex (node.go:1296) -> Peer.ReadIndex (peer.go:309)
       if (is_leader && in_lo != 0) leader_read_index(L, r, in_lo, in_hi, 0);
       // handleReceivedMessages: Replicates by sender, then the rest
@@ -1148,7 +1136,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
       }
       // LocalTick (node.tick node.go:1562 -> raft.tick raft.go:571-648)
       if (p.tick) {
-        r.tick_count++;
+        st_f(L, F_TICK_COUNT, ld_f(L, F_TICK_COUNT) + 1);
         if (is_leader) {
           r.election_tick++;
           if (r.election_tick >= v.election_rtt) {
@@ -1197,34 +1185,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
       uint64_t save_lo = r.saved_to + 1;
       bool has_save = inmem_nonempty && save_lo >= r.marker && save_lo <= r.last;
       bool has_apply = r.committed > r.processed;
-      bool state_changed = !(r.term == r.prev_term && r.vote == r.prev_vote &&
-                             r.committed == r.prev_commit);
-      bool state_empty = r.term == 0 && r.vote == 0 && r.committed == 0;
+      // Peer.prevState (peer.go:59) and node's cursors, in place
+      const uint64_t vote = ld_f(L, F_VOTE);
+      const uint64_t prev_term = ld_f(L, F_PREV_TERM);
+      const uint64_t prev_vote = ld_f(L, F_PREV_VOTE);
+      const uint64_t prev_commit = ld_f(L, F_PREV_COMMIT);
+      const uint64_t confirmed_index = ld_f(L, F_CONFIRMED_INDEX);
+      bool state_changed = !(r.term == prev_term && vote == prev_vote &&
+                             r.committed == prev_commit);
+      bool state_empty = r.term == 0 && vote == 0 && r.committed == 0;
       bool has_update = has_save || r.leader_update || r.nmsgs > 0 ||
                         has_apply || (!state_empty && state_changed) ||
                         r.nrtr > 0 || r.ndropped_ri > 0;
       uint64_t apply_lo = 0, apply_hi = 0;
-      if (has_update || r.confirmed_index != r.applied_index) {
+      if (has_update || confirmed_index != r.applied_index) {
         // validateUpdate / pushEntries (node.go:1100) / Peer.Commit
         if (has_apply) {
           // pb.EntriesToApply(CommittedEntries, pushedIndex, strict)
           // (raftpb/entry.go:27-47) then node.pushEntries (node.go:625)
+          const uint64_t pushed = ld_f(L, F_PUSHED_INDEX);
           apply_lo = r.processed + 1;
           apply_hi = r.committed;
-          if (apply_hi <= r.pushed_index || apply_lo > r.pushed_index + 1) {
+          if (apply_hi <= pushed || apply_lo > pushed + 1) {
             set_error(r, DRB_ERR_APPLY);
             apply_lo = 0;
           } else {
-            apply_lo = r.pushed_index + 1;
-            r.pushed_index = apply_hi;
+            apply_lo = pushed + 1;
+            st_f(L, F_PUSHED_INDEX, apply_hi);
           }
         }
         if (state_changed && !state_empty) {
-          r.prev_term = r.term;
-          r.prev_vote = r.vote;
-          r.prev_commit = r.committed;
+          if (prev_term != r.term) st_f(L, F_PREV_TERM, r.term);
+          if (prev_vote != vote) st_f(L, F_PREV_VOTE, vote);
+          st_f(L, F_PREV_COMMIT, r.committed);
         }
-        r.confirmed_index = r.applied_index;
+        if (confirmed_index != r.applied_index)
+          st_f(L, F_CONFIRMED_INDEX, r.applied_index);
         // Peer.Commit -> entryLog.commitUpdate (logentry.go:351-371)
         if (has_save) r.saved_to = r.last;  // savedLogTo(last, term(last))
         if (has_apply) r.processed = apply_hi;
@@ -1234,8 +1230,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
             set_error(r, DRB_ERR_COMMIT);
           // inMemory.appliedLogTo (inmemory.go:138-164)
           if (la >= r.marker && r.last >= r.marker && la <= r.last) {
-            r.applied_to_index = la;
-            r.applied_to_term = log_term(L, r, la);
+            st_f(L, F_APPLIED_TO_INDEX, la);
+            st_f(L, F_APPLIED_TO_TERM, log_term(L, r, la));
             r.marker = la + 1;
           }
         }
@@ -1264,7 +1260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
         r.flags |= DRB_F_ERROR;
         c_err = 1;
       }
-      store_rep<R, LEAD>(L, r, orig);
+      store_rep<R, LEAD>(L, r, flags0, fb0);
       c_msgs = r.nmsgs;
       c_rtr = r.nrtr;
       c_drop = r.ndropped_ri;
