@@ -25,6 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+READS_PER_CTX = 9      # C3: 9 ReadIndex reads per write, one ctx per round
+KEY_SPACE = 256        # K = 256 keys per group
 
 
 def alg_bytes_per_group_round(R=3, k=1, P=16, reads=True):
@@ -73,6 +75,7 @@ def cpu_baseline(args, seconds):
     parts = [(i * G // cores, (i + 1) * G // cores) for i in range(cores)]
     committed = 0
     rounds = 0
+    sums = (C.c_uint64 * (G * args.replicas))()
     t_start = time.perf_counter()
     t_run = 0.0
     while time.perf_counter() - t_start < seconds:
@@ -92,6 +95,15 @@ def cpu_baseline(args, seconds):
         for t in th:
             t.join()
         L.orc_cluster_end_round(c.p)
+        if not args.no_read_index:
+            th = [threading.Thread(target=L.orc_cluster_serve_reads,
+                                   args=(c.p, READS_PER_CTX, KEY_SPACE, a, b,
+                                         sums, None, None))
+                  for (a, b) in parts]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
         t_run += time.perf_counter() - t0
         committed += sum(o.committed_entries for o in outs)
         rounds += 1
@@ -101,7 +113,8 @@ def cpu_baseline(args, seconds):
                        "workload (k=%d, %s, a LocalTick every round), CPU "
                        "restatement (oracle/), not dragonboat" % (
                            G, args.replicas, rounds, args.k,
-                           "9:1 ReadIndex" if not args.no_read_index
+                           "9:1 ReadIndex + 9 KV lookups per released ctx"
+                           if not args.no_read_index
                            else "writes only"))
 
 
@@ -135,6 +148,8 @@ def main():
         tick = i % tick_every[0] == 0
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF)
+        if reads:  # ReadLocalNode for the 9 reads of each released ctx
+            eng.serve_reads(READS_PER_CTX, KEY_SPACE)
 
     # warmup (ticking every round); the tick cadence then follows the
     # reference's wall-clock tick worker: one LocalTick per RTTMillisecond
@@ -210,6 +225,8 @@ def main():
             "counters": {"committed_per_round": committed / K / world,
                          "messages": out.messages,
                          "ready_to_reads": out.ready_to_reads,
+                         "reads_served": out.reads_served,
+                         "reads_deferred": out.reads_deferred,
                          "fallbacks": out.fallbacks, "errors": out.errors},
         }
         if not args.no_cpu_baseline:

@@ -134,7 +134,8 @@ class RoundOut(C.Structure):
                 ("applied_entries", C.c_uint64), ("messages", C.c_uint64),
                 ("ready_to_reads", C.c_uint64),
                 ("dropped_read_indexes", C.c_uint64),
-                ("fallbacks", C.c_uint64), ("errors", C.c_uint64)]
+                ("fallbacks", C.c_uint64), ("errors", C.c_uint64),
+                ("reads_served", C.c_uint64), ("reads_deferred", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

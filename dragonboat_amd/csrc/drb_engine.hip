@@ -218,6 +218,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.ri_in, (uint64_t)cfg->ri_slots * G);
   rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
   rc |= dalloc(e, &v.rtr_count, R * G);
+  rc |= dalloc(e, &v.read_sum, R * G);
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
   rc |= dalloc(e, &e->ctr_total, NUM_COUNTERS);
@@ -906,6 +907,8 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->dropped_read_indexes = c[C_DROPPED_RI];
   out->fallbacks = c[C_FALLBACKS];
   out->errors = c[C_ERRORS];
+  out->reads_served = c[C_READS];
+  out->reads_deferred = c[C_READS_DEFERRED];
   if (reset) {
     HIPCHK(hipMemsetAsync(e->v.counters, 0,
                           e->ctr_rows * NUM_COUNTERS * sizeof(c[0]),
@@ -1108,6 +1111,87 @@ extern "C" int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot,
   }
   if (n_out) *n_out = n;
   return n > cap ? DRB_ERANGE : DRB_OK;
+}
+
+// ---------------------------------------------------------------- reads
+// KVTest.Lookup (kvtest.go:164-175) on the device table: the slot word
+// folded into the served-read checksum (found: vlen << 32 | LE32(value)).
+__device__ uint64_t kv_read_word(const View &v, uint32_t slot, uint64_t g,
+                                 uint64_t key8, uint32_t klen) {
+  const uint32_t mask = v.KS - 1;
+  uint32_t ks = (uint32_t)kv_hash(key8, klen) & mask;
+  const uint4 *tbl = v.kv + kv_ix(v, slot, g, 0);
+  for (uint32_t p = 0; p < v.KS; ++p) {
+    const uint4 h = tbl[(uint64_t)ks * v.KVW];
+    if (!((h.z >> 31) & 1u)) break;
+    if ((h.z & 0xffu) == klen && lo64(h) == key8) {
+      const uint32_t vlen = (h.z >> 8) & 0xfffu;
+      return ((uint64_t)vlen << 32) | (h.w & byte_mask(vlen));
+    }
+    ks = (ks + 1) & mask;
+  }
+  return ~0ull;
+}
+
+// one lane per replica: the reads of this round's ReadyToReads
+__global__ __launch_bounds__(256) void k_serve_reads(const View v,
+                                                     uint32_t n_reads,
+                                                     uint32_t key_space) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t slot = blockIdx.y;
+  uint32_t served = 0, deferred = 0;
+  if (g < v.G && (v.u32[u32_ix(v, W_FLAGS, slot, g)] & DRB_F_HOSTED)) {
+    const uint32_t n = v.rtr_count[ix(v, slot, g)];
+    if (n) {
+      const uint64_t sm_index = v.u64[u64_ix(v, F_SM_INDEX, slot, g)];
+      uint64_t sum = 0;
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+        if (lo64(c0) > sm_index) {  // pendingReadIndex: not applied yet
+          deferred += n_reads;
+          continue;
+        }
+        const uint64_t low = hi64(c0);
+        for (uint32_t j = 0; j < n_reads; ++j) {
+          const uint64_t key =
+              mix64(low ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull)) %
+              key_space;
+          const uint64_t w = kv_read_word(v, slot, g, key, 8);
+          sum += mix64(w ^ key ^ ((uint64_t)j << 56));
+          served++;
+        }
+      }
+      v.read_sum[ix(v, slot, g)] = sum;
+    }
+  }
+  const uint32_t cnt[2] = {served, deferred};
+  block_counters<true, C_READS, 2>(v, cnt);
+}
+
+extern "C" int drb_serve_reads(drb_engine *e, uint32_t reads_per_ctx,
+                               uint32_t key_space) {
+  if (!e || key_space == 0) return DRB_EINVAL;
+  dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
+  k_serve_reads<<<grid, 256, 0, e->stream>>>(e->v, reads_per_ctx, key_space);
+  HIPCHK(hipGetLastError());
+  return DRB_OK;
+}
+
+extern "C" int drb_export_read_sums(drb_engine *e, uint64_t first_group,
+                                    uint64_t n_groups, uint64_t *sums) {
+  if (!e || !sums) return DRB_EINVAL;
+  if (int rc = check_range(e, first_group, n_groups)) return rc;
+  const View &v = e->v;
+  const uint32_t R = v.R;
+  std::vector<uint64_t> host(n_groups);
+  for (uint32_t s = 0; s < R; ++s) {
+    HIPCHK(hipMemcpyAsync(host.data(), v.read_sum + ix(v, s, first_group),
+                          n_groups * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (uint64_t i = 0; i < n_groups; ++i) sums[i * R + s] = host[i];
+  }
+  return DRB_OK;
 }
 
 // ---------------------------------------------------------------- CRC32

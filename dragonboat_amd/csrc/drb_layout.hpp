@@ -93,6 +93,7 @@ struct View {
   uint4 *ri_in;           // [RS][G] {low, high}
   uint4 *rtr;             // [R][RTR_CAP][G] x 2 chunks {index, low},{high,0}
   uint32_t *rtr_count;    // [R][G]
+  uint64_t *read_sum;     // [R][G] served-read checksum (drb_serve_reads)
   unsigned long long *counters;  // [8] (drb_round_out order from index 1)
 };
 

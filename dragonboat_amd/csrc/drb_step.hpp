@@ -39,7 +39,8 @@ enum : int {
   C_DROPPED_RI,
   C_FALLBACKS,
   C_ERRORS,
-  C_ROUNDS,
+  C_READS,        // drb_serve_reads
+  C_READS_DEFERRED,
   NUM_COUNTERS
 };
 
@@ -922,24 +923,25 @@ DRB_DEV uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
-template <bool LEAD>
-DRB_DEV void block_counters(const View &v, const uint32_t (&c)[NUM_COUNTERS]) {
-  __shared__ uint32_t red[4][NUM_COUNTERS];
+// counters [FIRST, FIRST + N) of this workgroup's row (256 threads)
+template <bool LEAD, int FIRST, int N>
+DRB_DEV void block_counters(const View &v, const uint32_t (&c)[N]) {
+  __shared__ uint32_t red[4][N];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < C_ROUNDS; ++i) {
+  for (int i = 0; i < N; ++i) {
     const uint32_t s = wave_sum(c[i]);
     if (lane == 0) red[wave][i] = s;
   }
   __syncthreads();
-  if (threadIdx.x < C_ROUNDS) {
+  if (threadIdx.x < N) {
     const uint32_t i = threadIdx.x;
     const uint64_t s = (uint64_t)red[0][i] + red[1][i] + red[2][i] + red[3][i];
     if (s) {
       const uint64_t row =
           ((uint64_t)(LEAD ? 0 : 1) * gridDim.y + blockIdx.y) * gridDim.x +
           blockIdx.x;
-      v.counters[row * NUM_COUNTERS + i] += s;
+      v.counters[row * NUM_COUNTERS + FIRST + i] += s;
     }
   }
 }
@@ -974,9 +976,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
   uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
-  if (!(flags & DRB_F_HOSTED) || (flags & (DRB_F_FALLBACK | DRB_F_ERROR)) ||
-      ((role == DRB_LEADER) != LEAD))
+  if (!(flags & DRB_F_HOSTED) || ((role == DRB_LEADER) != LEAD))
     active = false;
+  if (active && (flags & (DRB_F_FALLBACK | DRB_F_ERROR))) {
+    // left the fast path in an earlier round: no round output
+    v.rtr_count[ix(v, slot, g)] = 0;
+    active = false;
+  }
   if (active) {
     Rep<R> r;
     load_rep<R, LEAD>(L, r);
@@ -1274,11 +1280,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
   }
-  const uint32_t cnt[NUM_COUNTERS] = {
+  const uint32_t cnt[C_READS] = {
       (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
-      (uint32_t)c_err,    0u};
-  block_counters<LEAD>(v, cnt);
+      (uint32_t)c_err};
+  block_counters<LEAD, 0, C_READS>(v, cnt);
 }
 
 }  // namespace drb

@@ -57,6 +57,8 @@ SIGNATURES = {
     "drb_export_ready_to_reads": (C.c_int, [P, U64, U32,
                                             C.POINTER(ReadyToRead), SZ,
                                             C.POINTER(SZ)]),
+    "drb_serve_reads": (C.c_int, [P, U32, U32]),
+    "drb_export_read_sums": (C.c_int, [P, U64, U64, PU64]),
     "drb_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32, PU32]),
     "drb_kv_export": (C.c_int, [P, U64, U32, PU8, PU32, PU8, PU32, SZ,
                                 C.POINTER(SZ)]),
@@ -258,6 +260,16 @@ class Engine:
         kb, vb = bytes(keys), bytes(vals)
         return {kb[i * 8:i * 8 + kl[i]]: vb[i * vcap:i * vcap + vl[i]]
                 for i in range(n.value)}
+
+    def serve_reads(self, reads_per_ctx=9, key_space=256):
+        _ck(lib().drb_serve_reads(self.h, reads_per_ctx, key_space),
+            "drb_serve_reads")
+
+    def export_read_sums(self, first_group, n_groups):
+        arr = (U64 * (n_groups * self.R))()
+        _ck(lib().drb_export_read_sums(self.h, first_group, n_groups, arr),
+            "drb_export_read_sums")
+        return list(arr)
 
     def kv_lookup(self, g, slot, key):
         vcap = self.cfg["kv_val_cap"]

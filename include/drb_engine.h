@@ -276,6 +276,8 @@ typedef struct drb_round_out {
   uint64_t dropped_read_indexes;  /* raft.droppedReadIndexes */
   uint64_t fallbacks;             /* replicas newly marked DRB_F_FALLBACK */
   uint64_t errors;                /* replicas newly marked DRB_F_ERROR */
+  uint64_t reads_served;          /* ReadLocalNode lookups done (drb_serve_reads) */
+  uint64_t reads_deferred;        /* reads whose index is not applied yet */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;
@@ -376,6 +378,24 @@ int drb_export_outbox(drb_engine *e, uint64_t group, uint32_t from_slot,
 int drb_export_ready_to_reads(drb_engine *e, uint64_t group, uint32_t slot,
                               drb_ready_to_read *out, size_t cap,
                               size_t *n_out);
+
+/*
+ * Serves the linearizable reads behind the ReadyToReads of the last round:
+ * pendingReadIndex.applied releases a read once the replica applied its
+ * index (request.go:930-953), and the client then calls ReadLocalNode ->
+ * IStateMachine.Lookup (nodehost.go:849, kvtest.go:164-175).  Each released
+ * ctx carries `reads_per_ctx` reads (the batch of node.go:1296-1305); read j
+ * of ctx {low, high} looks up key LE64(mix64(low ^ (j+1)*0x9E3779B97F4A7C15)
+ * % key_space).  Results fold into one checksum per replica (see
+ * drb_export_read_sums); reads whose index is not yet applied are counted
+ * as deferred.  Stream-ordered after drb_step_round*.
+ */
+int drb_serve_reads(drb_engine *e, uint32_t reads_per_ctx, uint32_t key_space);
+/* sums[(g - first_group) * R + slot]: sum over served reads j of
+ * mix64(word ^ key ^ (j << 56)), word = found ? vlen << 32 | LE32(value)
+ * : ~0; written by the last drb_serve_reads for replicas it served. */
+int drb_export_read_sums(drb_engine *e, uint64_t first_group,
+                         uint64_t n_groups, uint64_t *sums);
 
 /* IStateMachine.Lookup used by NodeHost.ReadLocalNode (nodehost.go:849). */
 int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,

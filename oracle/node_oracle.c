@@ -839,6 +839,54 @@ int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
   return 0;
 }
 
+/* ReadLocalNode for the reads behind each replica's ReadyToReads of the
+ * last round: pendingReadIndex.applied releases a read once the replica
+ * applied its index (request.go:930-953); the client's ReadLocalNode then
+ * runs KVTest.Lookup (nodehost.go:849, kvtest.go:164-175).  Read j of ctx
+ * {low, high} looks up LE64(mix64(low ^ (j+1)*GOLDEN) % key_space); results
+ * fold into sums[g * R + slot] (drb_serve_reads in include/drb_engine.h). */
+int orc_cluster_serve_reads(orc_cluster *c, uint32_t reads_per_ctx,
+                            uint32_t key_space, uint64_t g0, uint64_t g1,
+                            uint64_t *sums, uint64_t *served,
+                            uint64_t *deferred) {
+  const uint32_t R = c->cfg.num_replicas;
+  uint64_t sv = 0, df = 0;
+  if (g1 > c->cfg.num_groups) g1 = c->cfg.num_groups;
+  for (uint64_t g = g0; g < g1; ++g)
+    for (uint32_t s = 0; s < R; ++s) {
+      orc_node *n = node_at(c, g, s);
+      uint64_t sum = 0;
+      if (!n->hosted) continue;
+      for (size_t k = 0; k < n->nrtr; ++k) {
+        if (n->rtr[k].index > n->sm_index) {
+          df += reads_per_ctx;
+          continue;
+        }
+        for (uint32_t j = 0; j < reads_per_ctx; ++j) {
+          uint64_t key = mix64(n->rtr[k].ctx.low ^
+                               ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull)) %
+                         key_space;
+          uint8_t kb[8];
+          for (int b = 0; b < 8; ++b) kb[b] = (uint8_t)(key >> (8 * b));
+          const kv_item *it = kv_find(&n->kv, kb, 8);
+          uint64_t word = ~0ull;
+          if (it) {
+            uint32_t v0 = 0;
+            for (uint32_t b = 0; b < it->vlen && b < 4; ++b)
+              v0 |= (uint32_t)it->val[b] << (8 * b);
+            word = ((uint64_t)it->vlen << 32) | v0;
+          }
+          sum += mix64(word ^ key ^ ((uint64_t)j << 56));
+          sv++;
+        }
+      }
+      if (n->nrtr) sums[g * R + s] = sum;
+    }
+  if (served) *served = sv;
+  if (deferred) *deferred = df;
+  return 0;
+}
+
 int orc_cluster_kv_lookup(orc_cluster *c, uint64_t g, uint32_t slot,
                           const uint8_t *key, uint32_t klen, uint8_t *val,
                           uint32_t cap, uint32_t *vlen) {

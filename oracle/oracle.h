@@ -296,6 +296,10 @@ long orc_cluster_export_ready(orc_cluster *c, uint64_t g, uint32_t slot,
 int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
                            int hosted);
 /* make an engine-importable image of replica (g,slot) */
+int orc_cluster_serve_reads(orc_cluster *c, uint32_t reads_per_ctx,
+                            uint32_t key_space, uint64_t g0, uint64_t g1,
+                            uint64_t *sums, uint64_t *served,
+                            uint64_t *deferred);
 int orc_cluster_kv_lookup(orc_cluster *c, uint64_t g, uint32_t slot,
                           const uint8_t *key, uint32_t klen, uint8_t *val,
                           uint32_t cap, uint32_t *vlen);

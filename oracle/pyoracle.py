@@ -143,6 +143,10 @@ def _declare(L):
         "orc_cluster_set_hosted": (C.c_int, [P, U64, U32, C.c_int]),
         "orc_cluster_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32,
                                             PU32]),
+        "orc_cluster_serve_reads": (C.c_int, [P, U32, U32, U64, U64,
+                                              C.POINTER(C.c_uint64),
+                                              C.POINTER(C.c_uint64),
+                                              C.POINTER(C.c_uint64)]),
         "orc_entry_size": (C.c_size_t, [PE]),
         "orc_entry_marshal": (C.c_size_t, [PE, PU8, PU8]),
         "orc_entry_unmarshal": (C.c_long, [PU8, C.c_size_t, PE, PU8,
@@ -600,6 +604,19 @@ class Cluster:
         n = lib().orc_cluster_export_ready(self.p, g, slot, arr, cap)
         return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high)
                 for i in range(min(n, cap))]
+
+    def serve_reads(self, reads_per_ctx=9, key_space=256):
+        """Returns (sums[G*R] -- None where nothing was served, served,
+        deferred)."""
+        n = self.G * self.R
+        marker = (1 << 64) - 1
+        sums = (C.c_uint64 * n)(*([marker] * n))
+        sv, df = C.c_uint64(), C.c_uint64()
+        _check(lib().orc_cluster_serve_reads(self.p, reads_per_ctx, key_space,
+                                             0, self.G, sums, C.byref(sv),
+                                             C.byref(df)))
+        return ([None if x == marker else x for x in sums], sv.value,
+                df.value)
 
     def set_hosted(self, g, slot, hosted):
         lib().orc_cluster_set_hosted(self.p, g, slot, int(bool(hosted)))

@@ -107,3 +107,23 @@ def test_lagging_follower_catches_up_via_reject_and_retry():
         sts[i].flags |= abi.F_HOSTED
     p.eng.import_replicas(0, sts)
     _run(p, rounds=10, k=1, tick_every=2)
+
+
+def test_served_reads_c3():
+    """ReadLocalNode for the 9 reads behind every released ReadIndex ctx
+    (request.go:930-953 -> kvtest.go:164-175), drb_serve_reads vs oracle."""
+    p = Pair(G=64, R=3)
+    total = 0
+    for r in range(12):
+        o, e = p.round(k=1, tick=True, read_index=True)
+        assert e.ready_to_reads == o.ready_to_reads
+        p.eng.serve_reads(9, 256)
+        got = p.eng.read_counters(reset=True)
+        sums, served, deferred = p.orc.serve_reads(9, 256)
+        assert (got.reads_served, got.reads_deferred) == (served, deferred)
+        esums = p.eng.export_read_sums(0, p.G)
+        for i, x in enumerate(sums):
+            if x is not None:
+                assert esums[i] == x, (r, i)
+        total += served
+    assert total >= 9 * p.G * 8
