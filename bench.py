@@ -39,6 +39,22 @@ def alg_bytes_per_group_round(R=3, k=1, P=16, reads=True):
     return b_round + b_entries + b_apply + b_read
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
+
+
+def pmc_traffic(G, R):
+    """HBM bytes per round from the committed rocprofv3 PMC passes of this
+    workload (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE over the
+    round's kernels), or None when none matches this configuration."""
+    try:
+        s = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    if s.get("groups") != G or s.get("replicas") != R:
+        return None
+    return s.get("round_hbm_bytes")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,7 +150,7 @@ def main():
     first_shard, seed = ddist.shard_plan(rank, G)
     eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                  max_props=max(1, k), prop_slots=NP, ri_slots=NP,
-                 mailbox=15, kv_slots=512, kv_val_cap=4,
+                 mailbox=14, kv_slots=512, kv_val_cap=4,
                  first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
@@ -219,7 +235,10 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": pmc_traffic(G, R),
+                "traffic_source": "profiles/pmc_current.json (rocprofv3 "
+                                  "FETCH_SIZE x2 + WRITE_SIZE, bytes per "
+                                  "round)",
                 "alg_bytes_per_launch": alg,
                 "kernel_ms": kern_ms},
             "counters": {"committed_per_round": committed / K / world,

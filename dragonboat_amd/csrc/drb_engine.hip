@@ -159,7 +159,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (cfg->cmd_cap == 0 || cfg->cmd_cap % 16 || cfg->cmd_cap > 64)
     return DRB_ENOSYS;  // longer inline Cmds are a later round (C5)
-  if (cfg->mailbox < 4 || cfg->mailbox > 15) return DRB_EINVAL;
+  if (cfg->mailbox < 4 || cfg->mailbox > MB_MAX) return DRB_EINVAL;
   if (!is_pow2(cfg->kv_slots) || cfg->kv_val_cap == 0 ||
       cfg->kv_val_cap > 124)
     return DRB_EINVAL;
@@ -209,7 +209,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.ri_conf, R * DRB_RI_DEPTH * G);
   rc |= dalloc(e, &v.ring, R * v.W * (ENT_META + v.C16) * G);
   rc |= dalloc(e, &v.mbox, 2 * R * R * v.MB * MSG_CHUNKS * G);
-  rc |= dalloc(e, &v.mbox_meta, 2 * R * G);  // uint4
+  rc |= dalloc(e, &v.mbox_meta, 2 * R * R * G);  // uint4
+  rc |= dalloc(e, &v.mbox_maxapp, 2 * R * R * G);
   rc |= dalloc(e, &v.kv, R * G * v.KS * v.KVW);
   rc |= dalloc(e, &v.props,
                (uint64_t)cfg->prop_slots * v.max_props * (PROP_META + v.C16) *
@@ -770,7 +771,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       continue;
     }
     uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
-    std::vector<uint64_t> mi = {mmeta_ix(v, buf, from, g)};
+    std::vector<uint64_t> mi = {mmeta_ix(v, buf, from, to, g)};
     std::vector<uint4> meta;
     if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
     uint4 cur = meta[0];
@@ -778,7 +779,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       cur = pack2(0, 0);
       cur.x = tag;
     }
-    uint32_t k = (cur.y >> (4 * to)) & 15u;
+    uint32_t k = cur.y & MI_COUNT;
     if (k >= v.MB) {  // MessageQueue full (message.go:105-123)
       drop++;
       continue;
@@ -806,25 +807,39 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     mm.hint = m.hint;
     mm.hint_high = m.hint_high;
     uint4 c0, c1;
-    msg_encode(mm, c0, c1);
-    // the sender's term is stored once per round in the meta word
-    bool zero = (c0.x & MF_TERM_ZERO) != 0;
-    if (!zero && m.term != 0) {
-      if (q_hi(cur) == 0 && (cur.y == 0)) {
-        uint64_t t = m.term;
-        cur.z = (uint32_t)t;
-        cur.w = (uint32_t)(t >> 32);
+    msg_encode(mm, to, nullptr, c0, c1);
+    // the sender's term is stored once per (sender, receiver, round) in the
+    // header; a record whose term differs from it makes the receiver fall
+    // back (term gate, raft.go:1596-1609)
+    const bool zero = (c0.x & MF_TERM_ZERO) != 0;
+    bool other = false;
+    if (!zero) {
+      if (!(cur.y & MI_TERM)) {
+        cur.z = (uint32_t)m.term;
+        cur.w = (uint32_t)(m.term >> 32);
       } else if (q_hi(cur) != m.term) {
-        c0.x |= MF_TERM_OTHER;  // receiver treats it as a term mismatch
+        other = true;
+        c0.x |= MF_TERM_OTHER;
       }
-    } else if (!zero && m.term == 0 && q_hi(cur) != 0) {
-      c0.x |= MF_TERM_OTHER;
     }
     std::vector<uint64_t> idx = {mbox_ix(v, buf, from, to, k, 0, g),
                                  mbox_ix(v, buf, from, to, k, 1, g)};
     std::vector<uint4> val = {c0, c1};
     if (scatter(e, v.mbox, idx, val)) return DRB_EDEVICE;
-    cur.y += 1u << (4 * to);
+    constexpr uint32_t cnts = MI_COUNT | (0xfu << MI_NRI) | (0xfu << MI_NRR);
+    const uint32_t inf = msg_info(m.type, zero) | (other ? MI_TERM_OTHER : 0);
+    cur.y = (cur.y + (inf & cnts)) | (inf & ~cnts);
+    if (m.type == DRB_MSG_REPLICATE) {
+      cur.y |= 1u << (MI_REPMASK + k);
+      std::vector<uint64_t> xi = {mi[0]};
+      std::vector<uint64_t> xv;
+      if (gather(e, v.mbox_maxapp, xi, xv)) return DRB_EDEVICE;
+      uint64_t ma = m.log_index + m.n_entries;
+      if (k > 0 && (cur.y & (((1u << k) - 1u) << MI_REPMASK)))
+        ma = std::max(ma, xv[0]);
+      std::vector<uint64_t> nv = {ma};
+      if (scatter(e, v.mbox_maxapp, xi, nv)) return DRB_EDEVICE;
+    }
     std::vector<uint4> mv = {cur};
     if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
     acc++;
@@ -938,7 +953,7 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
                        size_t *ne, uint8_t *pool, size_t pcap, size_t *np,
                        uint4 meta) {
   const View &v = e->v;
-  uint32_t k = (meta.y >> (4 * to)) & 15u;
+  const uint32_t k = meta.x == (uint32_t)e->round ? (meta.y & MI_COUNT) : 0;
   if (!k) return DRB_OK;
   std::vector<uint64_t> idx;
   for (uint32_t q = 0; q < k; ++q)
@@ -946,10 +961,11 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
       idx.push_back(mbox_ix(v, buf, from, to, q, c, g));
   std::vector<uint4> val;
   if (gather(e, v.mbox, idx, val)) return DRB_EDEVICE;
+  uint64_t prev_lo = 0, prev_hi = 0;
   for (uint32_t q = 0; q < k; ++q) {
     if (*nm >= cap) return DRB_ERANGE;
     const uint4 *c = &val[q * MSG_CHUNKS];
-    Msg mm = msg_decode(c[0], c[1], (c[0].x & MF_HAS_C1) != 0, q_hi(meta));
+    Msg mm = msg_decode(c[0], c[1], q_hi(meta), prev_lo, prev_hi);
     drb_message &m = out[(*nm)++];
     memset(&m, 0, sizeof(m));
     m.shard_id = v.first_shard_id + g;
@@ -992,16 +1008,19 @@ extern "C" int drb_export_outbox(drb_engine *e, uint64_t group,
     return DRB_ERANGE;
   const View &v = e->v;
   const uint32_t buf = (uint32_t)(e->round & 1);
-  std::vector<uint64_t> mi = {mmeta_ix(v, buf, from_slot, group)};
+  std::vector<uint64_t> mi;
+  for (uint32_t to = 0; to < v.R; ++to)
+    mi.push_back(mmeta_ix(v, buf, from_slot, to, group));
   std::vector<uint4> meta;
   if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
   size_t nm = 0, ne = 0, np = 0;
-  if (meta[0].x == (uint32_t)e->round && e->round > 0) {
+  if (e->round > 0) {
     // send order across destinations is not recorded per message; the
     // per-destination order is (messages are compared per destination)
     for (uint32_t to = 0; to < v.R; ++to) {
+      if (to == from_slot) continue;
       int rc = export_pair(e, buf, group, from_slot, to, out, cap, &nm, ents,
-                           ent_cap, &ne, pool, pool_cap, &np, meta[0]);
+                           ent_cap, &ne, pool, pool_cap, &np, meta[to]);
       if (rc) return rc;
     }
   }

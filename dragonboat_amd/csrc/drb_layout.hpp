@@ -86,7 +86,8 @@ struct View {
   uint32_t *ri_conf;      // [R][D][G]
   uint4 *ring;            // [R][W][ENT_META + C16][G]
   uint4 *mbox;            // [2][R*R][MB][MSG_CHUNKS][G]
-  uint4 *mbox_meta;       // [2][R][G] {tag, 4-bit count per dest, term}
+  uint4 *mbox_meta;       // [2][R(from)][R(to)][G] {tag, info, term}
+  uint64_t *mbox_maxapp;  // [2][R][R][G] max LogIndex+n of the Replicates
   uint4 *kv;              // [R][G][KS][KVW]
   uint4 *props;           // [P][max_props][PROP_META + C16][G]
   uint32_t *prop_count;   // [P][G]
@@ -132,8 +133,9 @@ __host__ __device__ inline uint64_t mbox_ix(const View &v, uint32_t buf,
           chunk) * v.G + g;
 }
 __host__ __device__ inline uint64_t mmeta_ix(const View &v, uint32_t buf,
-                                             uint32_t from, uint64_t g) {
-  return ((uint64_t)buf * v.R + from) * v.G + g;
+                                             uint32_t from, uint32_t to,
+                                             uint64_t g) {
+  return (((uint64_t)buf * v.R + from) * v.R + to) * v.G + g;
 }
 __host__ __device__ inline uint64_t kv_ix(const View &v, uint32_t slot,
                                           uint64_t g, uint32_t ks) {

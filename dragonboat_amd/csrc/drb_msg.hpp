@@ -1,23 +1,29 @@
 // drb_msg.hpp -- compact in-HBM encoding of pb.Message (raftpb/message.go)
 // for the messages of the fast path.
 //
-// A record is one 16 B chunk, plus a second 16 B chunk only when the type
-// carries more than one 64-bit field.  The sender's term is stored once per
-// (sender, round) in the mailbox meta word instead of in every message:
-// within a fast-path round every message a replica sends carries its
-// current term (raft.go:667-681), except request types (ReadIndex), which
-// carry 0 and set TERM_ZERO.
+// A record is one 16 B chunk, plus a second 16 B chunk only when the fields
+// do not fit the first.  Per (sender, receiver, round) the mailbox holds a
+// header {round tag, info, sender term}: every fast-path message carries the
+// sender's current term (raft.go:667-681) -- request types (ReadIndex)
+// carry 0 and set TERM_ZERO -- so the term is stored once per header, and
+// the info word summarises the records so a receiver decides whether the
+// round stays on the fast path from the header alone.
 //
-//   c0 = {meta u32, 0, a u64}       c1 = {b u64, c u64}
+//   c0 = {meta u32, x u32, a u64}       c1 = {b u64, c u64}
 //   meta: type[0:8] reject[8] has_c1[9] term_zero[10] term_other[11]
-//         n_entries[16:32]
-//   Replicate      a=LogIndex  c1={LogTerm, Commit}
-//   ReplicateResp  a=LogIndex  c1={Hint, 0}            (only when Reject)
-//   Heartbeat      a=Commit    c1={Hint, HintHigh}     (only when Hint set)
-//   HeartbeatResp  a=0         c1={Hint, HintHigh}     (only when Hint set)
-//   ReadIndexResp  a=LogIndex  c1={Hint, HintHigh}
+//         lt_self[12] c_delta[13] hint_prev[14] hh32[15] n_entries[16:32]
+//   Replicate      a=LogIndex; LogTerm = sender term (lt_self) else c1.b;
+//                  Commit = LogIndex + (int32)x (c_delta) else c1.c
+//   ReplicateResp  a=LogIndex  c1={Hint, 0}           (only when Reject/Hint)
+//   Heartbeat      a=Commit    c1={Hint, HintHigh}    (when Hint set)
+//   HeartbeatResp  a=Hint x=HintHigh (hh32)  else c1={Hint, HintHigh}
 //   ReadIndex      a=Commit    c1={Hint, HintHigh}
+//   ReadIndexResp  a=LogIndex  c1={Hint, HintHigh}
 //   other          a=LogIndex  c1={Hint, HintHigh}
+// hint_prev: the ReadIndex ctx {Hint, HintHigh} equals the last ctx written
+// explicitly in this (sender, receiver) record sequence (a leader sends the
+// same ctx twice per round: with the ReadIndex broadcast and, as peepCtx,
+// with the tick heartbeat, raft.go:849-871; followers echo both).
 #pragma once
 #include <stdint.h>
 
@@ -30,11 +36,35 @@ namespace drb {
 constexpr uint32_t MF_REJECT = 1u << 8;
 constexpr uint32_t MF_HAS_C1 = 1u << 9;
 constexpr uint32_t MF_TERM_ZERO = 1u << 10;
-constexpr uint32_t MF_TERM_OTHER = 1u << 11;  // ingest: term != meta term
+constexpr uint32_t MF_TERM_OTHER = 1u << 11;  // ingest: term != header term
+constexpr uint32_t MF_LT_SELF = 1u << 12;
+constexpr uint32_t MF_C_DELTA = 1u << 13;
+constexpr uint32_t MF_HINT_PREV = 1u << 14;
+constexpr uint32_t MF_HH32 = 1u << 15;
+
+// header info word, per (sender, receiver, round)
+constexpr uint32_t MI_COUNT = 0xfu;       // [0:4] records
+constexpr int MI_NRI = 4;                 // [4:8] ReadIndex records
+constexpr int MI_NRR = 8;                 // [8:12] ReplicateResp records
+constexpr uint32_t MI_RESP = 1u << 12;    // a ReplicateResp / HeartbeatResp
+constexpr uint32_t MI_REP = 1u << 13;     // a Replicate (max_app is valid)
+constexpr uint32_t MI_OFF_LEADER = 1u << 14;    // a type a leader leaves
+constexpr uint32_t MI_OFF_FOLLOWER = 1u << 15;  // the fast path for / a
+                                                // follower does
+constexpr uint32_t MI_TERM = 1u << 16;        // a record carries the term
+constexpr uint32_t MI_TERM_OTHER = 1u << 17;  // a record's term != header's
+constexpr int MI_REPMASK = 18;  // [18:32] bit k: record k is a Replicate
+constexpr uint32_t MB_MAX = 14;  // records per (sender, receiver, round)
 
 struct Msg {
   uint32_t type, reject, n;
   uint64_t term, log_index, log_term, commit, hint, hint_high;
+};
+
+// ctx last written explicitly, per sender, with the receivers it went to
+struct HintCtx {
+  uint64_t lo, hi;
+  uint32_t dests;  // bit d: receiver d's last explicit ctx is {lo, hi}
 };
 
 __host__ __device__ inline uint4 pack2(uint64_t a, uint64_t b) {
@@ -56,18 +86,67 @@ __host__ __device__ inline bool is_request_type(uint32_t t) {
   return t == DRB_MSG_PROPOSE || t == DRB_MSG_READ_INDEX ||
          t == DRB_MSG_LEADER_TRANSFER;
 }
+// types whose {Hint, HintHigh} is a ReadIndex ctx (dedup candidates)
+__host__ __device__ inline bool is_ctx_type(uint32_t t) {
+  return t == DRB_MSG_HEARTBEAT || t == DRB_MSG_HEARTBEAT_RESP ||
+         t == DRB_MSG_READ_INDEX || t == DRB_MSG_READ_INDEX_RESP;
+}
 
-// returns true when c1 is needed
-__host__ __device__ inline bool msg_encode(const Msg &m, uint4 &c0, uint4 &c1) {
+// header info contribution of one record
+__host__ __device__ inline uint32_t msg_info(uint32_t type, bool term_zero) {
+  uint32_t i = 1;  // count
+  if (type == DRB_MSG_READ_INDEX) i += 1u << MI_NRI;
+  if (type == DRB_MSG_REPLICATE_RESP) i += 1u << MI_NRR;
+  if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)
+    i |= MI_RESP;
+  if (type == DRB_MSG_REPLICATE) i |= MI_REP;
+  if (!(type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP ||
+        type == DRB_MSG_READ_INDEX))
+    i |= MI_OFF_LEADER;
+  if (!(type == DRB_MSG_REPLICATE || type == DRB_MSG_HEARTBEAT ||
+        type == DRB_MSG_READ_INDEX_RESP))
+    i |= MI_OFF_FOLLOWER;
+  if (!term_zero) i |= MI_TERM;
+  return i;
+}
+
+// Encodes m (m.term must be the header term or 0 for request types) to
+// receiver `dest`.  hc may be null (no ctx dedup).  Returns has_c1.
+__host__ __device__ inline bool msg_encode(const Msg &m, uint32_t dest,
+                                           HintCtx *hc, uint4 &c0, uint4 &c1) {
   uint64_t a = 0, b = 0, c = 0;
+  uint32_t x = 0, fl = 0;
   bool has = false;
+  const bool ctx = is_ctx_type(m.type) && (m.hint | m.hint_high) != 0;
+  bool dedup = false;
+  if (ctx && hc) {
+    dedup = hc->lo == m.hint && hc->hi == m.hint_high &&
+            ((hc->dests >> dest) & 1u);
+    if (!dedup) {
+      if (hc->lo == m.hint && hc->hi == m.hint_high) {
+        hc->dests |= 1u << dest;
+      } else {
+        hc->lo = m.hint;
+        hc->hi = m.hint_high;
+        hc->dests = 1u << dest;
+      }
+    }
+  }
   switch (m.type) {
-    case DRB_MSG_REPLICATE:
+    case DRB_MSG_REPLICATE: {
       a = m.log_index;
-      b = m.log_term;
-      c = m.commit;
-      has = true;
+      const int64_t d = (int64_t)(m.commit - m.log_index);
+      if (m.log_term == m.term && m.term != 0 && d >= INT32_MIN &&
+          d <= INT32_MAX) {
+        fl |= MF_LT_SELF | MF_C_DELTA;
+        x = (uint32_t)(int32_t)d;
+      } else {
+        b = m.log_term;
+        c = m.commit;
+        has = true;
+      }
       break;
+    }
     case DRB_MSG_REPLICATE_RESP:
       a = m.log_index;
       b = m.hint;
@@ -77,18 +156,32 @@ __host__ __device__ inline bool msg_encode(const Msg &m, uint4 &c0, uint4 &c1) {
       a = m.commit;
       b = m.hint;
       c = m.hint_high;
-      has = m.hint || m.hint_high;
+      has = ctx && !dedup;
       break;
     case DRB_MSG_HEARTBEAT_RESP:
-      b = m.hint;
-      c = m.hint_high;
-      has = m.hint || m.hint_high;
+      if (ctx && !dedup) {
+        if (m.hint_high <= 0xffffffffull) {
+          fl |= MF_HH32;
+          a = m.hint;
+          x = (uint32_t)m.hint_high;
+        } else {
+          b = m.hint;
+          c = m.hint_high;
+          has = true;
+        }
+      }
       break;
     case DRB_MSG_READ_INDEX:
       a = m.commit;
       b = m.hint;
       c = m.hint_high;
-      has = true;
+      has = !dedup;
+      break;
+    case DRB_MSG_READ_INDEX_RESP:
+      a = m.log_index;
+      b = m.hint;
+      c = m.hint_high;
+      has = !dedup;
       break;
     default:
       a = m.log_index;
@@ -97,33 +190,43 @@ __host__ __device__ inline bool msg_encode(const Msg &m, uint4 &c0, uint4 &c1) {
       has = true;
       break;
   }
-  uint32_t meta = (m.type & 0xffu) | (m.reject ? MF_REJECT : 0) |
-                  (has ? MF_HAS_C1 : 0) | (m.n << 16);
-  if (is_request_type(m.type) && m.term == 0) meta |= MF_TERM_ZERO;
+  if (dedup) fl |= MF_HINT_PREV;
+  fl |= (m.type & 0xffu) | (m.reject ? MF_REJECT : 0) | (has ? MF_HAS_C1 : 0) |
+        (m.n << 16);
+  if (is_request_type(m.type) && m.term == 0) fl |= MF_TERM_ZERO;
   c0 = pack2(0, a);
-  c0.x = meta;
-  c0.y = 0;
+  c0.x = fl;
+  c0.y = x;
   c1 = pack2(b, c);
   return has;
 }
 
-// c1 is only read by the caller when MF_HAS_C1 is set
-__host__ __device__ inline Msg msg_decode(uint4 c0, uint4 c1, bool has_c1,
-                                          uint64_t sender_term) {
+// c1 is only read when MF_HAS_C1 is set.  prev_lo/prev_hi: the receiver's
+// last explicit ctx of this (sender, receiver) sequence, updated here.
+__host__ __device__ inline Msg msg_decode(uint4 c0, uint4 c1,
+                                          uint64_t sender_term,
+                                          uint64_t &prev_lo,
+                                          uint64_t &prev_hi) {
   Msg m;
-  uint32_t meta = c0.x;
+  const uint32_t meta = c0.x;
+  const bool has = (meta & MF_HAS_C1) != 0;
   m.type = meta & 0xffu;
   m.reject = (meta & MF_REJECT) ? 1 : 0;
   m.n = meta >> 16;
   m.term = (meta & MF_TERM_ZERO) ? 0 : sender_term;
-  uint64_t a = q_hi(c0);
-  uint64_t b = has_c1 ? q_lo(c1) : 0, c = has_c1 ? q_hi(c1) : 0;
+  const uint64_t a = q_hi(c0);
+  const uint64_t b = has ? q_lo(c1) : 0, c = has ? q_hi(c1) : 0;
   m.log_index = m.log_term = m.commit = m.hint = m.hint_high = 0;
   switch (m.type) {
     case DRB_MSG_REPLICATE:
       m.log_index = a;
-      m.log_term = b;
-      m.commit = c;
+      if (meta & MF_LT_SELF) {
+        m.log_term = sender_term;
+        m.commit = a + (uint64_t)(int64_t)(int32_t)c0.y;
+      } else {
+        m.log_term = b;
+        m.commit = c;
+      }
       break;
     case DRB_MSG_REPLICATE_RESP:
       m.log_index = a;
@@ -135,8 +238,13 @@ __host__ __device__ inline Msg msg_decode(uint4 c0, uint4 c1, bool has_c1,
       m.hint_high = c;
       break;
     case DRB_MSG_HEARTBEAT_RESP:
-      m.hint = b;
-      m.hint_high = c;
+      if (meta & MF_HH32) {
+        m.hint = a;
+        m.hint_high = c0.y;
+      } else {
+        m.hint = b;
+        m.hint_high = c;
+      }
       break;
     case DRB_MSG_READ_INDEX:
       m.commit = a;
@@ -148,6 +256,15 @@ __host__ __device__ inline Msg msg_decode(uint4 c0, uint4 c1, bool has_c1,
       m.hint = b;
       m.hint_high = c;
       break;
+  }
+  if (is_ctx_type(m.type)) {
+    if (meta & MF_HINT_PREV) {
+      m.hint = prev_lo;
+      m.hint_high = prev_hi;
+    } else if ((m.hint | m.hint_high) != 0) {
+      prev_lo = m.hint;
+      prev_hi = m.hint_high;
+    }
   }
   return m;
 }

@@ -65,7 +65,7 @@ struct Rep {
       ri_fr[DRB_RI_DEPTH];
   uint32_t ri_cf[DRB_RI_DEPTH];
   // round-local
-  uint32_t out_cnt;   // 4-bit message count per destination slot
+  HintCtx hc;          // ctx dedup state of this sender (drb_msg.hpp)
   uint32_t nmsgs;
   uint32_t nrtr;
   uint32_t ndropped_ri;
@@ -87,6 +87,7 @@ struct RemLds {
 
 struct Lane {
   void *rl;       // RemLds<R> of this workgroup
+  uint32_t *oi;   // [R][256] outbox header info per destination (LDS)
   uint32_t tid;   // lane within the workgroup
   const View *v;
   uint32_t slot;
@@ -152,32 +153,34 @@ DRB_DEV void st_f(const Lane &L, int f, uint64_t x) {
 // ------------------------------------------------------------ messages
 // send (raft.go:683-687): From = self; the Term of every non-request
 // message is r.term and lives in the outbox meta word
+// The header info of each destination accumulates in LDS ([dest][lane]:
+// a runtime destination slot indexes it without scratch); the headers are
+// written at the end of the round for the destinations that got records.
 template <int R>
 DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   const View &v = *L.v;
-  uint32_t k = (r.out_cnt >> (4 * to_slot)) & 15u;
+  uint32_t &w = L.oi[to_slot * 256 + L.tid];
+  const uint32_t k = w & MI_COUNT;
   if (k >= v.MB) {  // bounded by the pre-pass; never expected
     set_error(r, DRB_FB_CAPACITY);
     return;
   }
-  r.out_cnt += 1u << (4 * to_slot);
   r.nmsgs++;
   Msg mm = m;
   mm.term = is_request_type(m.type) ? 0 : r.term;
   uint4 c0, c1;
-  bool has = msg_encode(mm, c0, c1);
+  const bool has = msg_encode(mm, to_slot, &r.hc, c0, c1);
+  constexpr uint32_t cnts = MI_COUNT | (0xfu << MI_NRI) | (0xfu << MI_NRR);
+  const uint32_t inf = msg_info(mm.type, mm.term == 0);
+  w = (w + (inf & cnts)) | (inf & ~cnts);
   v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] = c0;
   if (has) v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] = c1;
-}
-
-DRB_DEV Msg read_msg(const Lane &L, uint32_t from, uint32_t k,
-                     uint64_t sender_term) {
-  const View &v = *L.v;
-  uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 0, L.g)];
-  bool has = (c0.x & MF_HAS_C1) != 0;
-  uint4 c1 = make_uint4(0, 0, 0, 0);
-  if (has) c1 = v.mbox[mbox_ix(v, L.rbuf, from, L.slot, k, 1, L.g)];
-  return msg_decode(c0, c1, has, sender_term);
+  if (m.type == DRB_MSG_REPLICATE) {
+    w |= 1u << (MI_REPMASK + k);
+    // LogIndex + n of successive Replicates never decreases in a round
+    v.mbox_maxapp[mmeta_ix(v, L.wbuf, L.slot, to_slot, L.g)] =
+        m.log_index + m.n;
+  }
 }
 
 // ------------------------------------------------------------ remote FSM
@@ -962,8 +965,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t slot = blockIdx.y;
   __shared__ RemLds<R> rl;
+  __shared__ uint32_t oinfo[R * 256];
   Lane L;
   L.rl = &rl;
+  L.oi = oinfo;
   L.tid = threadIdx.x;
   L.v = vp;
   L.slot = slot;
@@ -987,7 +992,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
     Rep<R> r;
     load_rep<R, LEAD>(L, r);
     r.role = LEAD ? DRB_LEADER : DRB_FOLLOWER;
-    r.out_cnt = 0;
+#pragma unroll
+    for (int s = 0; s < R; ++s) oinfo[s * 256 + threadIdx.x] = 0;
+    r.hc.lo = r.hc.hi = 0;
+    r.hc.dests = 0;
     r.nmsgs = 0;
     r.nrtr = 0;
     r.ndropped_ri = 0;
@@ -1001,39 +1009,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
     uint32_t fb = DRB_FB_NONE;
     constexpr bool is_leader = LEAD;
     if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) fb = DRB_FB_ROLE;
+    // the inbox, from the per-sender headers alone (drb_msg.hpp)
     uint32_t nin_packed = 0;  // 4-bit inbox count per sender slot
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
     uint64_t max_app = 0;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot) continue;
-      const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, g)];
-      uint32_t ns = 0;
-      if (meta.x == tag_prev) ns = (meta.y >> (4 * slot)) & 15u;
+      const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)];
+      const uint32_t info = meta.x == tag_prev ? meta.y : 0u;
+      const uint32_t ns = info & MI_COUNT;
       nin_packed |= ns << (4 * s);
-      const uint64_t sterm = hi64(meta);
-      for (uint32_t k = 0; k < ns; ++k) {
-        uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
-        uint32_t type = c0.x & 0xffu;
-        uint64_t mterm = (c0.x & MF_TERM_ZERO) ? 0 : sterm;
-        if (c0.x & MF_TERM_OTHER) mterm = ~0ull;
-        bool ok;
-        if (is_leader)
-          ok = type == DRB_MSG_REPLICATE_RESP ||
-               type == DRB_MSG_HEARTBEAT_RESP || type == DRB_MSG_READ_INDEX;
-        else
-          ok = type == DRB_MSG_REPLICATE || type == DRB_MSG_HEARTBEAT ||
-               type == DRB_MSG_READ_INDEX_RESP;
-        if (!ok && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
-        if (mterm != 0 && mterm != r.term && fb == DRB_FB_NONE)
-          fb = DRB_FB_TERM_MISMATCH;
-        if (type == DRB_MSG_READ_INDEX) n_ri_msgs++;
-        if (type == DRB_MSG_REPLICATE_RESP) n_rr++;
-        if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)
-          resp_from |= 1u << s;
-        if (type == DRB_MSG_REPLICATE)
-          max_app = umax64(max_app, hi64(c0) + (c0.x >> 16));
-      }
+      if ((info & (LEAD ? MI_OFF_LEADER : MI_OFF_FOLLOWER)) &&
+          fb == DRB_FB_NONE)
+        fb = DRB_FB_MESSAGE_TYPE;
+      if (((info & MI_TERM_OTHER) ||
+           ((info & MI_TERM) && hi64(meta) != r.term)) &&
+          fb == DRB_FB_NONE)
+        fb = DRB_FB_TERM_MISMATCH;
+      n_ri_msgs += (info >> MI_NRI) & 15u;
+      n_rr += (info >> MI_NRR) & 15u;
+      if (info & MI_RESP) resp_from |= 1u << s;
+      if (!LEAD && (info & MI_REP))
+        max_app = umax64(max_app,
+                         v.mbox_maxapp[mmeta_ix(v, L.rbuf, s, slot, g)]);
       total_in += ns;
     }
     uint32_t nprops = 0;
@@ -1129,13 +1128,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
           if ((uint32_t)s == slot) continue;
           const uint32_t ns = (nin_packed >> (4 * s)) & 15u;
           if (!ns) continue;
-          const uint64_t sterm =
-              hi64(v.mbox_meta[mmeta_ix(v, L.rbuf, s, g)]);
-          for (uint32_t k = 0; k < ns; ++k) {
-            uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
-            bool isrep = (c0.x & 0xffu) == DRB_MSG_REPLICATE;
-            if (isrep != (pass == 0)) continue;
-            Msg m = read_msg(L, s, k, sterm);
+          const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)];
+          const uint64_t sterm = hi64(meta);
+          // records of this pass: the header's Replicate mask
+          const uint32_t reps = meta.y >> MI_REPMASK;
+          uint32_t todo = (pass == 0 ? reps : ~reps) & ((1u << ns) - 1u);
+          uint64_t prev_lo = 0, prev_hi = 0;
+          while (todo) {
+            const uint32_t k = __builtin_ctz(todo);
+            todo &= todo - 1;
+            const uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
+            uint4 c1 = make_uint4(0, 0, 0, 0);
+            if (c0.x & MF_HAS_C1)
+              c1 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
+            const Msg m = msg_decode(c0, c1, sterm, prev_lo, prev_hi);
             dispatch(L, r, s, m);
           }
         }
@@ -1271,12 +1277,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
       c_rtr = r.nrtr;
       c_drop = r.ndropped_ri;
     }
-    // outbox meta for this round (tag = round): written even when empty
-    {
-      uint4 meta = mk4(0, r.term);
-      meta.x = (uint32_t)p.round;
-      meta.y = r.out_cnt;
-      v.mbox_meta[mmeta_ix(v, L.wbuf, slot, g)] = meta;
+    // outbox headers for this round (tag = round), for the destinations
+    // that got records: a receiver reads a stale tag as an empty inbox
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      const uint32_t w = oinfo[s * 256 + threadIdx.x];
+      if (w & MI_COUNT) {
+        uint4 meta = mk4(0, r.term);
+        meta.x = (uint32_t)p.round;
+        meta.y = w;
+        v.mbox_meta[mmeta_ix(v, L.wbuf, slot, (uint32_t)s, g)] = meta;
+      }
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
   }

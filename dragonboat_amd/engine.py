@@ -99,7 +99,7 @@ def _u8(b):
 
 DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 cmd_cap=32, max_props=4, prop_slots=2, ri_slots=2,
-                mailbox=15, kv_slots=512, kv_val_cap=4, election_rtt=10,
+                mailbox=14, kv_slots=512, kv_val_cap=4, election_rtt=10,
                 heartbeat_rtt=1, check_quorum=1, device=0)
 
 

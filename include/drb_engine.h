@@ -247,7 +247,7 @@ typedef struct drb_config {
   uint32_t max_props;        /* max proposals per group per round */
   uint32_t prop_slots;       /* staged proposal batches */
   uint32_t ri_slots;         /* staged ReadIndex batches */
-  uint32_t mailbox;          /* messages per (sender, receiver) per round */
+  uint32_t mailbox;          /* records per (sender, receiver) per round, 4..14 */
   uint32_t kv_slots;         /* KV open-addressing slots per replica (pow2) */
   uint32_t kv_val_cap;       /* max value bytes stored inline per KV slot */
   uint32_t election_rtt;     /* Config.ElectionRTT */
