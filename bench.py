@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--tick-ms", type=float, default=1.0,
                     help="RTTMillisecond: one LocalTick per this much wall "
                          "time (nodehost.go:1824-1914)")
+    ap.add_argument("--reads-mode", default="fused",
+                    choices=["fused", "separate"],
+                    help="served reads inside the round's kernels or as "
+                         "their own launch (drb_serve_reads)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -162,9 +166,14 @@ def main():
 
     def step(i):
         tick = i % tick_every[0] == 0
+        # with reads: ReadLocalNode for the 9 reads behind every released
+        # ctx, served inside the round (drb_round_in.reads_per_ctx)
+        fused = reads and args.reads_mode == "fused"
         eng.step_async(tick=tick, prop_slot=i % NP,
-                       ri_slot=(i % NP) if reads else 0xFFFFFFFF)
-        if reads:  # ReadLocalNode for the 9 reads of each released ctx
+                       ri_slot=(i % NP) if reads else 0xFFFFFFFF,
+                       reads_per_ctx=READS_PER_CTX if fused else 0,
+                       key_space=KEY_SPACE)
+        if reads and not fused:
             eng.serve_reads(READS_PER_CTX, KEY_SPACE)
 
     # warmup (ticking every round); the tick cadence then follows the

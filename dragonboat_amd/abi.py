@@ -126,7 +126,9 @@ class Config(C.Structure):
 
 class RoundIn(C.Structure):
     _fields_ = [("tick", C.c_uint32), ("prop_slot", C.c_uint32),
-                ("ri_slot", C.c_uint32), ("reserved", C.c_uint32)]
+                ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),
+                ("read_key_space", C.c_uint32),
+                ("reserved", C.c_uint32 * 3)]
 
 
 class RoundOut(C.Structure):

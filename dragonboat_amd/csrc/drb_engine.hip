@@ -33,6 +33,8 @@ struct drb_engine {
   View v;
   View *dview;  // device copy of v (kernels read it with scalar loads)
   hipStream_t stream;
+  hipStream_t stream2;            // the follower kernel of a round
+  hipEvent_t ev_fork, ev_join;    // stream -> stream2 -> stream
   uint64_t round;
   uint64_t bytes;
   std::vector<void *> allocs;
@@ -41,13 +43,6 @@ struct drb_engine {
   void *scratch;
   size_t scratch_bytes;
 };
-
-static __host__ __device__ uint64_t mix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
 
 static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 
@@ -177,6 +172,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->scratch_bytes = 0;
   if (hipSetDevice(cfg->device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
+          hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) !=
           hipSuccess) {
     delete e;
     return DRB_EDEVICE;
@@ -243,8 +244,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
 extern "C" int drb_engine_destroy(drb_engine *e) {
   if (!e) return DRB_EINVAL;
   (void)hipStreamSynchronize(e->stream);
+  (void)hipStreamSynchronize(e->stream2);
   for (void *p : e->allocs) (void)hipFree(p);
   if (e->scratch) (void)hipFree(e->scratch);
+  (void)hipEventDestroy(e->ev_fork);
+  (void)hipEventDestroy(e->ev_join);
+  (void)hipStreamDestroy(e->stream2);
   (void)hipStreamDestroy(e->stream);
   delete e;
   return DRB_OK;
@@ -850,11 +855,29 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
 }
 
 // ---------------------------------------------------------------- step
+// The leader and follower kernels of a round touch disjoint state (each
+// reads round t-1's mailbox and writes round t's), so they may run
+// concurrently (DRB_ROLE_STREAMS=1: the follower kernel on a second
+// stream, forked from and joined back into the engine stream).  Measured
+// on MI355X at C3 that was 3 % slower than back-to-back launches, so the
+// default is one stream.
+#ifndef DRB_ROLE_STREAMS
+#define DRB_ROLE_STREAMS 0
+#endif
 template <int R>
 static void launch_step(drb_engine *e, const RoundParams &p) {
   dim3 grid((unsigned)((e->v.G + 255) / 256), R);
-  step_kernel<R, true><<<grid, 256, 0, e->stream>>>(e->v, p);
-  step_kernel<R, false><<<grid, 256, 0, e->stream>>>(e->v, p);
+  if (DRB_ROLE_STREAMS) {
+    (void)hipEventRecord(e->ev_fork, e->stream);
+    (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
+    step_kernel<R, true><<<grid, 256, 0, e->stream>>>(e->v, p);
+    step_kernel<R, false><<<grid, 256, 0, e->stream2>>>(e->v, p);
+    (void)hipEventRecord(e->ev_join, e->stream2);
+    (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
+  } else {
+    step_kernel<R, true><<<grid, 256, 0, e->stream>>>(e->v, p);
+    step_kernel<R, false><<<grid, 256, 0, e->stream>>>(e->v, p);
+  }
 }
 
 extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
@@ -868,7 +891,10 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.tick = in->tick ? 1 : 0;
   p.prop_slot = in->prop_slot;
   p.ri_slot = in->ri_slot;
+  p.n_reads = in->reads_per_ctx;
+  p.key_space = in->read_key_space;
   p.pad = 0;
+  if (p.n_reads && !p.key_space) return DRB_EINVAL;
   switch (e->v.R) {
     case 1: launch_step<1>(e, p); break;
     case 2: launch_step<2>(e, p); break;
@@ -1133,26 +1159,8 @@ extern "C" int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot,
 }
 
 // ---------------------------------------------------------------- reads
-// KVTest.Lookup (kvtest.go:164-175) on the device table: the slot word
-// folded into the served-read checksum (found: vlen << 32 | LE32(value)).
-__device__ uint64_t kv_read_word(const View &v, uint32_t slot, uint64_t g,
-                                 uint64_t key8, uint32_t klen) {
-  const uint32_t mask = v.KS - 1;
-  uint32_t ks = (uint32_t)kv_hash(key8, klen) & mask;
-  const uint4 *tbl = v.kv + kv_ix(v, slot, g, 0);
-  for (uint32_t p = 0; p < v.KS; ++p) {
-    const uint4 h = tbl[(uint64_t)ks * v.KVW];
-    if (!((h.z >> 31) & 1u)) break;
-    if ((h.z & 0xffu) == klen && lo64(h) == key8) {
-      const uint32_t vlen = (h.z >> 8) & 0xfffu;
-      return ((uint64_t)vlen << 32) | (h.w & byte_mask(vlen));
-    }
-    ks = (ks + 1) & mask;
-  }
-  return ~0ull;
-}
-
-// one lane per replica: the reads of this round's ReadyToReads
+// one lane per replica: the reads of the last round's ReadyToReads
+// (the step kernels do the same in-round when drb_round_in.reads_per_ctx)
 __global__ __launch_bounds__(256) void k_serve_reads(const View v,
                                                      uint32_t n_reads,
                                                      uint32_t key_space) {
@@ -1161,27 +1169,9 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
   uint32_t served = 0, deferred = 0;
   if (g < v.G && (v.u32[u32_ix(v, W_FLAGS, slot, g)] & DRB_F_HOSTED)) {
     const uint32_t n = v.rtr_count[ix(v, slot, g)];
-    if (n) {
-      const uint64_t sm_index = v.u64[u64_ix(v, F_SM_INDEX, slot, g)];
-      uint64_t sum = 0;
-      for (uint32_t k = 0; k < n; ++k) {
-        const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
-        if (lo64(c0) > sm_index) {  // pendingReadIndex: not applied yet
-          deferred += n_reads;
-          continue;
-        }
-        const uint64_t low = hi64(c0);
-        for (uint32_t j = 0; j < n_reads; ++j) {
-          const uint64_t key =
-              mix64(low ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull)) %
-              key_space;
-          const uint64_t w = kv_read_word(v, slot, g, key, 8);
-          sum += mix64(w ^ key ^ ((uint64_t)j << 56));
-          served++;
-        }
-      }
-      v.read_sum[ix(v, slot, g)] = sum;
-    }
+    if (n)
+      serve_reads_lane(v, slot, g, n, v.u64[u64_ix(v, F_SM_INDEX, slot, g)],
+                       n_reads, key_space, served, deferred);
   }
   const uint32_t cnt[2] = {served, deferred};
   block_counters<true, C_READS, 2>(v, cnt);

@@ -12,6 +12,14 @@
 
 namespace drb {
 
+// splitmix64 finaliser: seeded synthetic inputs and the served-read keys
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 // per-replica u64 fields (drb_replica_state order), array [F][slot][g]
 enum U64Field : int {
   F_TERM = 0,

@@ -23,9 +23,18 @@ namespace drb {
 
 #define DRB_DEV __device__ __forceinline__
 
-// minimum waves per SIMD the step kernels are compiled for (register cap)
-#ifndef DRB_STEP_WAVES
-#define DRB_STEP_WAVES 1
+// minimum waves per SIMD the step kernels are compiled for, per role
+// (caps the registers the compiler may allocate)
+#ifndef DRB_LEAD_WAVES
+#define DRB_LEAD_WAVES 1
+#endif
+#ifndef DRB_FOLLOW_WAVES
+#define DRB_FOLLOW_WAVES 1
+#endif
+// timing experiments only (tools/variants.sh), never in a shipped build:
+// bit 0 skips the KV apply, bit 1 the in-round served reads
+#ifndef DRB_ABLATE
+#define DRB_ABLATE 0
 #endif
 
 constexpr uint64_t MAX_ENTRY_SIZE = 64ull * 1024 * 1024;  // soft.go:186
@@ -808,6 +817,94 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   return -1;  // table full
 }
 
+// ------------------------------------------------------------ served reads
+// ReadLocalNode for the reads behind each ReadyToRead of the round
+// (request.go:930-953 -> KVTest.Lookup kvtest.go:164-175): read j of a
+// released ctx {low, high} looks up the 8-byte LE key
+// mix64(low ^ (j+1)*GOLDEN) % key_space and folds the slot word
+// (found: vlen << 32 | LE32(value), else ~0) into read_sum[slot][g].
+// A lookup first reads two adjacent slots (one 128 B line unless the
+// first is the last slot of a line), and the lookups of a batch are all
+// issued before any is resolved: one memory round trip per batch.
+DRB_DEV bool kv_used(uint4 h) { return (h.z >> 31) & 1u; }
+DRB_DEV bool kv_match(uint4 h, uint64_t key8, uint32_t klen) {
+  return kv_used(h) && (h.z & 0xffu) == klen && lo64(h) == key8;
+}
+DRB_DEV uint64_t kv_word(uint4 h) {
+  const uint32_t vlen = (h.z >> 8) & 0xfffu;
+  return ((uint64_t)vlen << 32) | (h.w & byte_mask(vlen));
+}
+// linear probing from slot ks for at most `probes` slots
+DRB_DEV uint64_t kv_probe_word(const uint4 *tbl, uint32_t KVW, uint32_t mask,
+                               uint32_t ks, uint64_t key8, uint32_t klen,
+                               uint32_t probes) {
+  for (uint32_t p = 0; p < probes; ++p) {
+    const uint4 h = tbl[(uint64_t)ks * KVW];
+    if (!kv_used(h)) break;
+    if (kv_match(h, key8, klen)) return kv_word(h);
+    ks = (ks + 1) & mask;
+  }
+  return ~0ull;
+}
+
+constexpr uint32_t READ_BATCH = 5;
+
+DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
+                              uint32_t nrtr, uint64_t sm_index,
+                              uint32_t n_reads, uint32_t key_space,
+                              uint32_t &served, uint32_t &deferred) {
+  if (!nrtr) return;
+  const uint32_t mask = v.KS - 1;
+  const uint4 *tbl = v.kv + kv_ix(v, slot, g, 0);
+  const bool ks_pow2 = (key_space & (key_space - 1)) == 0;
+  uint64_t sum = 0;
+  for (uint32_t k = 0; k < nrtr; ++k) {
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    if (lo64(c0) > sm_index) {  // pendingReadIndex: index not applied yet
+      deferred += n_reads;
+      continue;
+    }
+    const uint64_t low = hi64(c0);
+    for (uint32_t j0 = 0; j0 < n_reads; j0 += READ_BATCH) {
+      uint64_t key[READ_BATCH];
+      uint32_t ks[READ_BATCH];
+      uint4 h0[READ_BATCH], h1[READ_BATCH];
+#pragma unroll
+      for (uint32_t t = 0; t < READ_BATCH; ++t) {
+        const uint64_t x =
+            mix64(low ^ ((uint64_t)(j0 + t + 1) * 0x9E3779B97F4A7C15ull));
+        key[t] = ks_pow2 ? (x & (key_space - 1)) : x % key_space;
+        ks[t] = (uint32_t)kv_hash(key[t], 8) & mask;
+        h0[t] = h1[t] = make_uint4(0, 0, 0, 0);
+        if (j0 + t < n_reads) {
+          h0[t] = tbl[(uint64_t)ks[t] * v.KVW];
+          h1[t] = tbl[(uint64_t)((ks[t] + 1) & mask) * v.KVW];
+        }
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < READ_BATCH; ++t) {
+        const uint32_t j = j0 + t;
+        if (j >= n_reads) continue;
+        uint64_t w;
+        if (!kv_used(h0[t]))
+          w = ~0ull;
+        else if (kv_match(h0[t], key[t], 8))
+          w = kv_word(h0[t]);
+        else if (v.KS < 2 || !kv_used(h1[t]))
+          w = ~0ull;
+        else if (kv_match(h1[t], key[t], 8))
+          w = kv_word(h1[t]);
+        else
+          w = kv_probe_word(tbl, v.KVW, mask, (ks[t] + 2) & mask, key[t], 8,
+                            v.KS - 2);
+        sum += mix64(w ^ key[t] ^ ((uint64_t)j << 56));
+        served++;
+      }
+    }
+  }
+  v.read_sum[ix(v, slot, g)] = sum;
+}
+
 // ------------------------------------------------------------ load/store
 template <int R, bool LEAD>
 DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
@@ -912,6 +1009,8 @@ struct RoundParams {
   uint32_t tick;
   uint32_t prop_slot;  // DRB_NONE: none
   uint32_t ri_slot;    // DRB_NONE: none
+  uint32_t n_reads;    // reads served per released ctx (0: none)
+  uint32_t key_space;  // served-read key space
   uint32_t pad;
 };
 
@@ -956,7 +1055,7 @@ DRB_DEV void block_counters(const View &v, const uint32_t (&c)[N]) {
 // roles apart keeps each one's register footprint (and so its occupancy)
 // to what its own handlers need.
 template <int R, bool LEAD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WAVES))) void step_kernel(const View v,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_LEAD_WAVES : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
   // kernarg loads, and the pointers loaded from it are known to address
@@ -978,6 +1077,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
   L.wbuf = (uint32_t)(p.round & 1);
   uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint64_t c_rtr = 0, c_drop = 0;
+  uint32_t c_served = 0, c_deferred = 0;
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
   uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
@@ -1250,7 +1350,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
         // clearReadyToRead: records stay in the round output buffer
       }
       // ---------------------------------------- StateMachine.Handle
-      if (apply_hi >= apply_lo && apply_lo != 0) {
+      if (apply_hi >= apply_lo && apply_lo != 0 && !(DRB_ABLATE & 1)) {
         uint64_t from = umax64(apply_lo, r.sm_index + 1);
         for (uint64_t idx = from; idx <= apply_hi; ++idx) {
           int rc = apply_entry(L, r, idx);
@@ -1290,12 +1390,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRB_STEP_WA
       }
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
+    // ReadLocalNode of the released reads, against the state just applied
+    if (p.n_reads && !(DRB_ABLATE & 2))
+      serve_reads_lane(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
+                       p.key_space, c_served, c_deferred);
   }
-  const uint32_t cnt[C_READS] = {
+  const uint32_t cnt[NUM_COUNTERS] = {
       (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
-      (uint32_t)c_err};
-  block_counters<LEAD, 0, C_READS>(v, cnt);
+      (uint32_t)c_err,    c_served,            c_deferred};
+  block_counters<LEAD, 0, NUM_COUNTERS>(v, cnt);
 }
 
 }  // namespace drb

@@ -206,16 +206,21 @@ class Engine:
         return acc.value, drop.value
 
     # ---------------------------------------------------------- round
-    def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE):
-        rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, 0)
+    def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE,
+             reads_per_ctx=0, key_space=0):
+        rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
+                      key_space)
         out = RoundOut()
         _ck(lib().drb_step_round(self.h, C.byref(rin), C.byref(out)),
             "drb_step_round")
         return out
 
     def step_async(self, tick=False, prop_slot=abi.DRB_NONE,
-                   ri_slot=abi.DRB_NONE):
-        rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, 0)
+                   ri_slot=abi.DRB_NONE, reads_per_ctx=0, key_space=0):
+        """One round, stream-ordered; reads_per_ctx > 0 also serves the
+        reads behind the round's ReadyToReads (drb_round_in)."""
+        rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
+                      key_space)
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
 

@@ -262,7 +262,12 @@ typedef struct drb_round_in {
   uint32_t tick;       /* 1: one LocalTick per hosted replica (nodehost.go:1903) */
   uint32_t prop_slot;  /* staged proposal batch to consume, DRB_NONE for none */
   uint32_t ri_slot;    /* staged ReadIndex batch, DRB_NONE for none */
-  uint32_t reserved;
+  /* ReadLocalNode reads served in-round behind every ReadyToRead the round
+   * releases, with drb_serve_reads semantics (0: none; then
+   * drb_serve_reads can serve them after the round) */
+  uint32_t reads_per_ctx;
+  uint32_t read_key_space; /* key space of those reads (> 0 if reads) */
+  uint32_t reserved[3];
 } drb_round_in;
 
 #define DRB_NONE 0xffffffffu

@@ -90,10 +90,12 @@ class Pair:
             ri_in = ri_slot
         return pin, ri_in
 
-    def round(self, k=1, tick=False, read_index=False, groups=None, **kw):
+    def round(self, k=1, tick=False, read_index=False, groups=None,
+              reads=0, read_key_space=256, **kw):
         pin, ri_in = self.stage(k, read_index=read_index, groups=groups, **kw)
         o = self.orc.round(tick=tick)
-        e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in)
+        e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in,
+                          reads_per_ctx=reads, key_space=read_key_space)
         self.rounds += 1
         return o, e
 

@@ -127,3 +127,26 @@ def test_served_reads_c3():
                 assert esums[i] == x, (r, i)
         total += served
     assert total >= 9 * p.G * 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_space", [256, 200])
+def test_served_reads_in_round(key_space):
+    """The same reads served inside the step round (drb_round_in.
+    reads_per_ctx), against the oracle's serve after its round; the key
+    space 200 (not a power of two) takes the modulo path."""
+    p = Pair(G=96, R=3)
+    total = 0
+    for r in range(10):
+        o, e = p.round(k=1, tick=(r % 3 != 1), read_index=(r % 4 != 3),
+                       reads=9, read_key_space=key_space)
+        assert e.ready_to_reads == o.ready_to_reads
+        sums, served, deferred = p.orc.serve_reads(9, key_space)
+        assert (e.reads_served, e.reads_deferred) == (served, deferred), r
+        esums = p.eng.export_read_sums(0, p.G)
+        for i, x in enumerate(sums):
+            if x is not None:
+                assert esums[i] == x, (r, i)
+        total += served
+    assert total >= 9 * p.G * 5
+    assert not p.check()
