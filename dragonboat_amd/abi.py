@@ -121,14 +121,15 @@ class Config(C.Structure):
                 ("mailbox", C.c_uint32), ("kv_slots", C.c_uint32),
                 ("kv_val_cap", C.c_uint32), ("election_rtt", C.c_uint32),
                 ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
-                ("device", C.c_int32), ("reserved", C.c_uint32)]
+                ("device", C.c_int32), ("save_cap", C.c_uint32)]
 
 
 class RoundIn(C.Structure):
     _fields_ = [("tick", C.c_uint32), ("prop_slot", C.c_uint32),
                 ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),
                 ("read_key_space", C.c_uint32),
-                ("reserved", C.c_uint32 * 3)]
+                ("encode_saves", C.c_uint32),
+                ("reserved", C.c_uint32 * 2)]
 
 
 class RoundOut(C.Structure):
@@ -137,7 +138,8 @@ class RoundOut(C.Structure):
                 ("ready_to_reads", C.c_uint64),
                 ("dropped_read_indexes", C.c_uint64),
                 ("fallbacks", C.c_uint64), ("errors", C.c_uint64),
-                ("reads_served", C.c_uint64), ("reads_deferred", C.c_uint64)]
+                ("reads_served", C.c_uint64), ("reads_deferred", C.c_uint64),
+                ("saved_entries", C.c_uint64), ("saved_bytes", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

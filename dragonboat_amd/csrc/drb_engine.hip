@@ -160,6 +160,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (cfg->max_props == 0 || cfg->prop_slots == 0 || cfg->ri_slots == 0)
     return DRB_EINVAL;
+  if (cfg->save_cap % 16) return DRB_EINVAL;
   if (cfg->election_rtt == 0 || cfg->heartbeat_rtt == 0) return DRB_EINVAL;
   // limitSize never binds inside the window (entryutils.go:50-63)
   if ((uint64_t)cfg->window * (128 + cfg->cmd_cap) > MAX_ENTRY_SIZE)
@@ -221,6 +222,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
   rc |= dalloc(e, &v.rtr_count, R * G);
   rc |= dalloc(e, &v.read_sum, R * G);
+  v.save_cap16 = cfg->save_cap / 16;
+  if (v.save_cap16) {
+    rc |= dalloc(e, &v.save_buf, R * G * v.save_cap16);
+    rc |= dalloc(e, &v.save_len, R * G);
+    rc |= dalloc(e, &v.save_crc, R * G);
+  }
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
   rc |= dalloc(e, &e->ctr_total, NUM_COUNTERS);
@@ -893,8 +900,9 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.ri_slot = in->ri_slot;
   p.n_reads = in->reads_per_ctx;
   p.key_space = in->read_key_space;
-  p.pad = 0;
   if (p.n_reads && !p.key_space) return DRB_EINVAL;
+  p.encode_saves = in->encode_saves ? 1 : 0;
+  if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
   switch (e->v.R) {
     case 1: launch_step<1>(e, p); break;
     case 2: launch_step<2>(e, p); break;
@@ -950,6 +958,8 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->errors = c[C_ERRORS];
   out->reads_served = c[C_READS];
   out->reads_deferred = c[C_READS_DEFERRED];
+  out->saved_entries = c[C_SAVED_ENTRIES];
+  out->saved_bytes = c[C_SAVED_BYTES];
   if (reset) {
     HIPCHK(hipMemsetAsync(e->v.counters, 0,
                           e->ctr_rows * NUM_COUNTERS * sizeof(c[0]),
@@ -1077,6 +1087,41 @@ extern "C" int drb_export_ready_to_reads(drb_engine *e, uint64_t group,
     out[k].ctx_high = lo64h(val[2 * k + 1]);
   }
   if (n_out) *n_out = n;
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- saves
+extern "C" int drb_export_saved(drb_engine *e, uint64_t group, uint32_t slot,
+                                uint8_t *buf, size_t cap, uint32_t *len,
+                                uint32_t *crc) {
+  if (!e || !len || (cap && !buf)) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!v.save_cap16) return DRB_EINVAL;
+  if (group >= v.G || slot >= v.R) return DRB_ERANGE;
+  uint32_t l = 0, c = 0;
+  HIPCHK(hipMemcpyAsync(&l, v.save_len + ix(v, slot, group), 4,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&c, v.save_crc + ix(v, slot, group), 4,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *len = l;
+  if (crc) *crc = l ? c : 0;
+  if (l > cap) return DRB_ERANGE;
+  if (l) {
+    HIPCHK(hipMemcpyAsync(buf, v.save_buf + ix(v, slot, group) * v.save_cap16,
+                          l, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_saved_buffers(drb_engine *e, void **bytes, uint32_t **lens,
+                                 uint32_t **crcs) {
+  if (!e || !bytes || !lens || !crcs) return DRB_EINVAL;
+  if (!e->v.save_cap16) return DRB_EINVAL;
+  *bytes = e->v.save_buf;
+  *lens = e->v.save_len;
+  *crcs = e->v.save_crc;
   return DRB_OK;
 }
 

@@ -103,6 +103,11 @@ struct View {
   uint4 *rtr;             // [R][RTR_CAP][G] x 2 chunks {index, low},{high,0}
   uint32_t *rtr_count;    // [R][G]
   uint64_t *read_sum;     // [R][G] served-read checksum (drb_serve_reads)
+  uint4 *save_buf;        // [R][G][save_cap16] EntryBatch of EntriesToSave
+  uint32_t *save_len;     // [R][G] bytes (0: nothing saved)
+  uint32_t *save_crc;     // [R][G] CRC32-IEEE of those bytes
+  uint32_t save_cap16;    // save_buf chunks per replica (0: no encoding)
+  uint32_t pad1;
   unsigned long long *counters;  // [8] (drb_round_out order from index 1)
 };
 

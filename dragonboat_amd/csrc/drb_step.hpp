@@ -16,6 +16,7 @@
 // DRB_F_FALLBACK and returns WITHOUT mutating anything.
 #pragma once
 #include "../../include/drb_engine.h"
+#include "drb_codec.hpp"
 #include "drb_layout.hpp"
 #include "drb_msg.hpp"
 
@@ -50,6 +51,8 @@ enum : int {
   C_ERRORS,
   C_READS,        // drb_serve_reads
   C_READS_DEFERRED,
+  C_SAVED_ENTRIES,  // encode_saves
+  C_SAVED_BYTES,
   NUM_COUNTERS
 };
 
@@ -817,6 +820,70 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   return -1;  // table full
 }
 
+// ------------------------------------------------------------ saves
+// SaveRaftState's input for this replica (engine.go:1343): the round's
+// pb.Update.EntriesToSave [lo, hi] (inMemory.entriesToSave,
+// inmemory.go:116-122) encoded as one EntryBatch (entrybatch.go:25-58) of
+// colfer Entries (raft_optimized.go:166-300) straight from the resident
+// window, with its CRC32-IEEE.
+template <int R>
+DRB_DEV void encode_saves(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
+                          const uint32_t *crc_tab, uint32_t &n_ent,
+                          uint32_t &n_bytes) {
+  const View &v = *L.v;
+  ByteOut o;
+  bo_init(o, v.save_buf + ix(v, L.slot, L.g) * v.save_cap16, v.save_cap16,
+          crc_tab);
+  for (uint64_t idx = lo; idx <= hi; ++idx) {
+    const uint4 m0 = v.ring[ring_ix(v, L.slot, idx, 0, L.g)];
+    const uint4 m1 = v.ring[ring_ix(v, L.slot, idx, 1, L.g)];
+    const uint4 m2 = v.ring[ring_ix(v, L.slot, idx, 2, L.g)];
+    EntryHdr e;
+    e.term = lo64(m0);
+    e.index = idx;
+    e.key = hi64(m0);
+    e.client_id = lo64(m1);
+    e.series_id = hi64(m1);
+    e.responded_to = lo64(m2);
+    e.type = m2.z;
+    e.cmd_len = m2.w;
+    bo_byte(o, 0x0a);  // EntryBatch.Entries, wire type 2
+    bo_varint(o, entry_size(e));
+    colfer_u64(o, 0, e.term);
+    colfer_u64(o, 1, e.index);
+    if (e.type != 0) {
+      bo_byte(o, 2);
+      bo_varint(o, e.type);
+    }
+    colfer_u64(o, 3, e.key);
+    colfer_u64(o, 4, e.client_id);
+    colfer_u64(o, 5, e.series_id);
+    colfer_u64(o, 6, e.responded_to);
+    if (e.cmd_len != 0) {
+      bo_byte(o, 7);
+      bo_varint(o, e.cmd_len);
+      for (uint32_t c = 0; c * 16 < e.cmd_len; ++c) {
+        const uint4 q = v.ring[ring_ix(v, L.slot, idx, ENT_META + c, L.g)];
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b)
+          if (c * 16 + b < e.cmd_len) bo_byte(o, w[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+    bo_byte(o, 0x7f);
+    n_ent++;
+  }
+  const uint32_t crc = bo_finish(o);
+  if (o.overflow) {  // bounded by the pre-pass; never expected
+    set_error(r, DRB_FB_CAPACITY);
+    v.save_len[ix(v, L.slot, L.g)] = 0;
+    return;
+  }
+  v.save_len[ix(v, L.slot, L.g)] = o.total;
+  v.save_crc[ix(v, L.slot, L.g)] = crc;
+  n_bytes += o.total;
+}
+
 // ------------------------------------------------------------ served reads
 // ReadLocalNode for the reads behind each ReadyToRead of the round
 // (request.go:930-953 -> KVTest.Lookup kvtest.go:164-175): read j of a
@@ -1011,7 +1078,7 @@ struct RoundParams {
   uint32_t ri_slot;    // DRB_NONE: none
   uint32_t n_reads;    // reads served per released ctx (0: none)
   uint32_t key_space;  // served-read key space
-  uint32_t pad;
+  uint32_t encode_saves;
 };
 
 // Round counters: each workgroup owns one row of NUM_COUNTERS u64 in
@@ -1065,6 +1132,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   const uint32_t slot = blockIdx.y;
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
+  __shared__ uint32_t crc_tab[256];
+  if (p.encode_saves) {  // uniform: every thread reaches the barrier
+    crc32_table_init(crc_tab, threadIdx.x);
+    __syncthreads();
+  }
   Lane L;
   L.rl = &rl;
   L.oi = oinfo;
@@ -1077,7 +1149,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   L.wbuf = (uint32_t)(p.round & 1);
   uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint64_t c_rtr = 0, c_drop = 0;
-  uint32_t c_served = 0, c_deferred = 0;
+  uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
   uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
@@ -1086,6 +1158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   if (active && (flags & (DRB_F_FALLBACK | DRB_F_ERROR))) {
     // left the fast path in an earlier round: no round output
     v.rtr_count[ix(v, slot, g)] = 0;
+    if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
     active = false;
   }
   if (active) {
@@ -1205,6 +1278,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         if (et >= ld_f(L, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
           fb = DRB_FB_ELECTION;
       }
+    }
+    if (p.encode_saves && fb == DRB_FB_NONE) {
+      // EntriesToSave lie in [min(committed, saved_to) + 1, new last]
+      const uint64_t top = umax64(r.last + nprops, max_app);
+      const uint64_t base = umin64(r.committed, r.saved_to);
+      const uint64_t n_save = top > base ? top - base : 0;
+      if (n_save * entrybatch_elem_bound(v.C16 * 16) >
+          (uint64_t)v.save_cap16 * 16)
+        fb = DRB_FB_CAPACITY;
     }
     if (fb != DRB_FB_NONE) {
       r.flags |= DRB_F_FALLBACK;
@@ -1333,6 +1415,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         }
         if (confirmed_index != r.applied_index)
           st_f(L, F_CONFIRMED_INDEX, r.applied_index);
+        // SaveRaftState (engine.go:1343) of EntriesToSave
+        if (has_save && p.encode_saves)
+          encode_saves(L, r, save_lo, r.last, crc_tab, c_saved,
+                       c_saved_bytes);
         // Peer.Commit -> entryLog.commitUpdate (logentry.go:351-371)
         if (has_save) r.saved_to = r.last;  // savedLogTo(last, term(last))
         if (has_apply) r.processed = apply_hi;
@@ -1390,6 +1476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       }
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
+    if (p.encode_saves && c_saved == 0) v.save_len[ix(v, slot, g)] = 0;
     // ReadLocalNode of the released reads, against the state just applied
     if (p.n_reads && !(DRB_ABLATE & 2))
       serve_reads_lane(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
@@ -1398,7 +1485,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   const uint32_t cnt[NUM_COUNTERS] = {
       (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
-      (uint32_t)c_err,    c_served,            c_deferred};
+      (uint32_t)c_err,    c_served,            c_deferred,
+      c_saved,            c_saved_bytes};
   block_counters<LEAD, 0, NUM_COUNTERS>(v, cnt);
 }
 

@@ -63,6 +63,9 @@ SIGNATURES = {
     "drb_kv_export": (C.c_int, [P, U64, U32, PU8, PU32, PU8, PU32, SZ,
                                 C.POINTER(SZ)]),
     "drb_crc32_ieee_batch": (C.c_int, [P, PU8, SZ, PU64, PU32, SZ, PU32]),
+    "drb_export_saved": (C.c_int, [P, U64, U32, PU8, SZ, PU32, PU32]),
+    "drb_saved_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(PU32),
+                                    C.POINTER(PU32)]),
 }
 
 
@@ -100,7 +103,7 @@ def _u8(b):
 DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 cmd_cap=32, max_props=4, prop_slots=2, ri_slots=2,
                 mailbox=14, kv_slots=512, kv_val_cap=4, election_rtt=10,
-                heartbeat_rtt=1, check_quorum=1, device=0)
+                heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0)
 
 
 class Engine:
@@ -115,7 +118,7 @@ class Engine:
                    cfg["max_props"], cfg["prop_slots"], cfg["ri_slots"],
                    cfg["mailbox"], cfg["kv_slots"], cfg["kv_val_cap"],
                    cfg["election_rtt"], cfg["heartbeat_rtt"],
-                   cfg["check_quorum"], cfg["device"], 0)
+                   cfg["check_quorum"], cfg["device"], cfg["save_cap"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -207,20 +210,22 @@ class Engine:
 
     # ---------------------------------------------------------- round
     def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE,
-             reads_per_ctx=0, key_space=0):
+             reads_per_ctx=0, key_space=0, encode_saves=False):
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
-                      key_space)
+                      key_space, int(bool(encode_saves)))
         out = RoundOut()
         _ck(lib().drb_step_round(self.h, C.byref(rin), C.byref(out)),
             "drb_step_round")
         return out
 
     def step_async(self, tick=False, prop_slot=abi.DRB_NONE,
-                   ri_slot=abi.DRB_NONE, reads_per_ctx=0, key_space=0):
+                   ri_slot=abi.DRB_NONE, reads_per_ctx=0, key_space=0,
+                   encode_saves=False):
         """One round, stream-ordered; reads_per_ctx > 0 also serves the
-        reads behind the round's ReadyToReads (drb_round_in)."""
+        reads behind the round's ReadyToReads, encode_saves encodes the
+        EntriesToSave (drb_round_in)."""
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
-                      key_space)
+                      key_space, int(bool(encode_saves)))
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
 
@@ -265,6 +270,15 @@ class Engine:
         kb, vb = bytes(keys), bytes(vals)
         return {kb[i * 8:i * 8 + kl[i]]: vb[i * vcap:i * vcap + vl[i]]
                 for i in range(n.value)}
+
+    def export_saved(self, g, slot):
+        """(EntryBatch bytes, crc32) of one replica's last EntriesToSave."""
+        cap = self.cfg["save_cap"]
+        buf = (C.c_uint8 * max(1, cap))()
+        ln, crc = U32(), U32()
+        _ck(lib().drb_export_saved(self.h, g, slot, buf, cap, C.byref(ln),
+                                   C.byref(crc)), "drb_export_saved")
+        return bytes(buf[:ln.value]), crc.value
 
     def serve_reads(self, reads_per_ctx=9, key_space=256):
         _ck(lib().drb_serve_reads(self.h, reads_per_ctx, key_space),

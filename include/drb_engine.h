@@ -254,7 +254,9 @@ typedef struct drb_config {
   uint32_t heartbeat_rtt;    /* Config.HeartbeatRTT */
   uint32_t check_quorum;     /* Config.CheckQuorum */
   int32_t device;            /* HIP device ordinal */
-  uint32_t reserved;
+  /* bytes per replica for the round's EntriesToSave encoded as an
+   * EntryBatch (drb_round_in.encode_saves; multiple of 16, 0: none) */
+  uint32_t save_cap;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -267,7 +269,10 @@ typedef struct drb_round_in {
    * drb_serve_reads can serve them after the round) */
   uint32_t reads_per_ctx;
   uint32_t read_key_space; /* key space of those reads (> 0 if reads) */
-  uint32_t reserved[3];
+  /* 1: encode every replica's pb.Update.EntriesToSave as EntryBatch bytes
+   * + CRC32 for the LogDB writer (drb_export_saved; needs save_cap) */
+  uint32_t encode_saves;
+  uint32_t reserved[2];
 } drb_round_in;
 
 #define DRB_NONE 0xffffffffu
@@ -283,6 +288,8 @@ typedef struct drb_round_out {
   uint64_t errors;                /* replicas newly marked DRB_F_ERROR */
   uint64_t reads_served;          /* ReadLocalNode lookups done (drb_serve_reads) */
   uint64_t reads_deferred;        /* reads whose index is not applied yet */
+  uint64_t saved_entries;         /* EntriesToSave encoded (encode_saves) */
+  uint64_t saved_bytes;           /* EntryBatch bytes of those */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;
@@ -401,6 +408,21 @@ int drb_serve_reads(drb_engine *e, uint32_t reads_per_ctx, uint32_t key_space);
  * : ~0; written by the last drb_serve_reads for replicas it served. */
 int drb_export_read_sums(drb_engine *e, uint64_t first_group,
                          uint64_t n_groups, uint64_t *sums);
+
+/* Persistence boundary (ILogDB.SaveRaftState, raftio/logdb.go:83, called
+ * once per round by engine.processSteps, engine.go:1343): one replica's
+ * pb.Update.EntriesToSave of the last round that ran with encode_saves,
+ * as EntryBatch bytes (EntryBatch.MarshalTo, raftpb/entrybatch.go:25-58,
+ * with Entry.MarshalTo, raftpb/raft_optimized.go:166-300) and their
+ * crc32.ChecksumIEEE (the checksum of internal/transport/tcp.go:146).
+ * *len = 0 when the replica saved nothing that round. */
+int drb_export_saved(drb_engine *e, uint64_t group, uint32_t slot,
+                     uint8_t *buf, size_t cap, uint32_t *len, uint32_t *crc);
+/* The whole round's save output on the device, for a GPU-side writer or
+ * one D2H copy: replica (slot, g) owns bytes[(slot * G + g) * save_cap ..]
+ * with lens[slot * G + g] and crcs[slot * G + g]. */
+int drb_saved_buffers(drb_engine *e, void **bytes, uint32_t **lens,
+                      uint32_t **crcs);
 
 /* IStateMachine.Lookup used by NodeHost.ReadLocalNode (nodehost.go:849). */
 int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,

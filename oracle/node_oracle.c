@@ -140,6 +140,7 @@ typedef struct orc_node {
   orc_rtr *rtr;   /* ud.ReadyToReads of the last round */
   size_t nrtr, caprtr;
   orc_evec applyq; /* tasks pushed for the apply worker */
+  orc_evec saved;  /* ud.EntriesToSave of the last round (SaveRaftState) */
 } orc_node;
 
 struct orc_cluster {
@@ -501,6 +502,7 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
     orc_node *n = node_at(c, g, s);
     mv_clear(&n->out);
     n->nrtr = 0;
+    n->saved.n = 0;
     if (!n->hosted) {
       mv_clear(&n->inbox);
       continue;
@@ -542,6 +544,7 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
     orc_node *n = node_at(c, g, s);
     orc_update *ud = &uds[s];
     db_append(n->db, ud->save.v, ud->save.n); /* LogReader.Append */
+    ev_copy_range(&n->saved, ud->save.v, ud->save.n);
     for (size_t i = 0; i < ud->msgs.n; i++)
       if (ud->msgs.v[i].type != DRB_MSG_REPLICATE)
         deliver(c, g, s, &ud->msgs.v[i]);
@@ -611,6 +614,7 @@ void orc_cluster_free(orc_cluster *c) {
     mv_free(&n->out);
     free(n->rtr);
     ev_free(&n->applyq);
+    ev_free(&n->saved);
   }
   free(c->nodes);
   free(c);
@@ -831,6 +835,49 @@ long orc_cluster_export_ready(orc_cluster *c, uint64_t g, uint32_t slot,
     out[i].ctx_high = n->rtr[i].ctx.high;
   }
   return (long)n->nrtr;
+}
+
+/* The last round's EntriesToSave of one replica as the bytes
+ * ILogDB.SaveRaftState persists: EntryBatch.MarshalTo (entrybatch.go:25-58)
+ * of the colfer Entries (raft_optimized.go:166-300), and their
+ * crc32.ChecksumIEEE.  Returns the byte count (0: nothing saved), or -1
+ * when cap is too small. */
+long orc_cluster_export_saved(orc_cluster *c, uint64_t g, uint32_t slot,
+                              uint8_t *buf, size_t cap, uint32_t *crc) {
+  orc_node *n = node_at(c, g, slot);
+  const size_t ne = n->saved.n;
+  if (crc) *crc = 0;
+  if (ne == 0) return 0;
+  drb_entry *de = (drb_entry *)calloc(ne, sizeof(drb_entry));
+  size_t pool_n = 0;
+  for (size_t i = 0; i < ne; i++)
+    pool_n += n->saved.v[i].cmd ? n->saved.v[i].cmd->len : 0;
+  uint8_t *pool = (uint8_t *)malloc(pool_n + 1);
+  size_t off = 0;
+  for (size_t i = 0; i < ne; i++) {
+    const orc_entry *e = &n->saved.v[i];
+    de[i].term = e->term;
+    de[i].index = e->index;
+    de[i].key = e->key;
+    de[i].client_id = e->client_id;
+    de[i].series_id = e->series_id;
+    de[i].responded_to = e->responded_to;
+    de[i].type = e->type;
+    de[i].cmd_len = e->cmd ? e->cmd->len : 0;
+    de[i].cmd_off = off;
+    if (de[i].cmd_len) memcpy(pool + off, e->cmd->data, de[i].cmd_len);
+    off += de[i].cmd_len;
+  }
+  long rc = -1;
+  const size_t sz = orc_entrybatch_size(de, ne);
+  if (sz <= cap) {
+    orc_entrybatch_marshal(de, ne, pool, buf);
+    if (crc) *crc = orc_crc32_ieee(buf, sz);
+    rc = (long)sz;
+  }
+  free(de);
+  free(pool);
+  return rc;
 }
 
 int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,

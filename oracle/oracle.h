@@ -293,6 +293,8 @@ long orc_cluster_export_kv(orc_cluster *c, uint64_t g, uint32_t slot,
                            size_t val_cap);
 long orc_cluster_export_ready(orc_cluster *c, uint64_t g, uint32_t slot,
                               drb_ready_to_read *out, size_t cap);
+long orc_cluster_export_saved(orc_cluster *c, uint64_t g, uint32_t slot,
+                              uint8_t *buf, size_t cap, uint32_t *crc);
 int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
                            int hosted);
 /* make an engine-importable image of replica (g,slot) */

@@ -141,6 +141,8 @@ def _declare(L):
                                                 C.POINTER(ReadyToRead),
                                                 C.c_size_t]),
         "orc_cluster_set_hosted": (C.c_int, [P, U64, U32, C.c_int]),
+        "orc_cluster_export_saved": (C.c_long, [P, U64, U32, PU8,
+                                                C.c_size_t, PU32]),
         "orc_cluster_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32,
                                             PU32]),
         "orc_cluster_serve_reads": (C.c_int, [P, U32, U32, U64, U64,
@@ -604,6 +606,16 @@ class Cluster:
         n = lib().orc_cluster_export_ready(self.p, g, slot, arr, cap)
         return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high)
                 for i in range(min(n, cap))]
+
+    def export_saved(self, g, slot, cap=1 << 16):
+        """(EntryBatch bytes, crc32) of one replica's last EntriesToSave."""
+        buf = (C.c_uint8 * cap)()
+        crc = C.c_uint32()
+        n = lib().orc_cluster_export_saved(self.p, g, slot, buf, cap,
+                                           C.byref(crc))
+        if n < 0:
+            raise RuntimeError("export_saved: buffer too small")
+        return bytes(buf[:n]), crc.value
 
     def serve_reads(self, reads_per_ctx=9, key_space=256):
         """Returns (sums[G*R] -- None where nothing was served, served,

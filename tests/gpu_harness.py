@@ -91,13 +91,25 @@ class Pair:
         return pin, ri_in
 
     def round(self, k=1, tick=False, read_index=False, groups=None,
-              reads=0, read_key_space=256, **kw):
+              reads=0, read_key_space=256, encode_saves=False, **kw):
         pin, ri_in = self.stage(k, read_index=read_index, groups=groups, **kw)
         o = self.orc.round(tick=tick)
         e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in,
-                          reads_per_ctx=reads, key_space=read_key_space)
+                          reads_per_ctx=reads, key_space=read_key_space,
+                          encode_saves=encode_saves)
         self.rounds += 1
         return o, e
+
+    def check_saves(self, groups=None):
+        """EntriesToSave of the last round: EntryBatch bytes and CRC32."""
+        errs = []
+        for g in (range(self.G) if groups is None else groups):
+            for s in range(self.R):
+                eb = self.eng.export_saved(g, s)
+                ob = self.orc.export_saved(g, s)
+                if eb != ob:
+                    errs.append((g, s, "saved", eb, ob))
+        return errs
 
     def check(self, groups=None, logs=True, kv=True, msgs=True,
               ready=True):

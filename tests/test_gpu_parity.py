@@ -150,3 +150,41 @@ def test_served_reads_in_round(key_space):
         total += served
     assert total >= 9 * p.G * 5
     assert not p.check()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 3])
+def test_entries_to_save_entrybatch_crc(k):
+    """SaveRaftState input (engine.go:1343): every replica's EntriesToSave
+    encoded on the GPU as EntryBatch bytes (entrybatch.go:25-58, colfer
+    Entry raft_optimized.go:166-300) with CRC32-IEEE, byte-identical to the
+    oracle codec; the CRC also checked against zlib."""
+    import zlib
+    p = Pair(G=40, R=3, save_cap=1024, max_props=4)
+    n = 0
+    for r in range(8):
+        o, e = p.round(k=k if r % 3 != 2 else 0, tick=(r % 2 == 0),
+                       read_index=(r % 3 == 0), encode_saves=True)
+        assert e.fallbacks == 0 and e.errors == 0, e.to_dict()
+        assert not p.check_saves(), r
+        for g in range(0, p.G, 7):
+            for s in range(3):
+                b, crc = p.eng.export_saved(g, s)
+                assert crc == (zlib.crc32(b) if b else 0)
+                n += len(b) > 0
+        assert e.saved_bytes == sum(len(p.eng.export_saved(g, s)[0])
+                                    for g in range(p.G) for s in range(3))
+    assert n > 0
+    assert not p.check()
+
+
+@pytest.mark.gpu
+def test_entries_to_save_capacity_falls_back():
+    """A save buffer too small for the round's bound hands the replica to
+    the CPU path before it mutates (DRB_FB_CAPACITY)."""
+    p = Pair(G=8, R=3, save_cap=128, max_props=4)
+    o, e = p.round(k=3, encode_saves=True)
+    assert e.fallbacks > 0
+    st = p.eng.export_replicas(0, 1)
+    assert st[0].flags & abi.F_FALLBACK
+    assert st[0].fallback_reason == abi.FB["CAPACITY"]

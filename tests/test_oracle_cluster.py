@@ -127,3 +127,31 @@ def test_workload_definition():
     assert lo & 1 and hi == 33
     # splitmix64 reference value (Steele et al.; seed 0 -> first output)
     assert workload.mix64(0) == 0xE220A8397B1DCDAF
+
+
+def test_oracle_saved_entrybatch_decodes_to_the_round_entries():
+    """The oracle's SaveRaftState output (EntryBatch of EntriesToSave +
+    CRC32) decodes back to entries with contiguous indexes at the leader's
+    term, and the CRC is zlib's crc32 (Go crc32.ChecksumIEEE)."""
+    import zlib
+    from dragonboat_amd import workload
+    c = po.Cluster(6, 3, seed=7)
+    c.setup_steady(0)
+    seen = 0
+    for r in range(5):
+        counts, ents, pool = workload.build_batch(6, 2, 7, r)
+        c.stage_proposals(counts, 2, ents, pool)
+        c.round(tick=(r % 2 == 0))
+        for g in range(6):
+            for s in range(3):
+                b, crc = c.export_saved(g, s)
+                if not b:
+                    continue
+                assert crc == zlib.crc32(b)
+                es = po.entrybatch_unmarshal(b)
+                idx = [e["index"] for e in es]
+                assert idx == list(range(idx[0], idx[0] + len(idx)))
+                assert all(e["term"] == 2 for e in es)
+                assert po.entrybatch_marshal(es) == b
+                seen += 1
+    assert seen >= 6 * 3 * 3
