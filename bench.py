@@ -154,7 +154,7 @@ def main():
     first_shard, seed = ddist.shard_plan(rank, G)
     eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                  max_props=max(1, k), prop_slots=NP, ri_slots=NP,
-                 mailbox=14, kv_slots=512, kv_val_cap=4,
+                 mailbox=13, kv_slots=512, kv_val_cap=4,
                  first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):

@@ -121,7 +121,19 @@ class Config(C.Structure):
                 ("mailbox", C.c_uint32), ("kv_slots", C.c_uint32),
                 ("kv_val_cap", C.c_uint32), ("election_rtt", C.c_uint32),
                 ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
-                ("device", C.c_int32), ("save_cap", C.c_uint32)]
+                ("device", C.c_int32), ("save_cap", C.c_uint32),
+                ("total_groups", C.c_uint64), ("place_world", C.c_uint32),
+                ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
+                ("reserved2", C.c_uint32)]
+
+
+class Region(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
+
+
+PLANE_REGIONS = 6
+PLANE_C1 = 1 << 16
+PLANE_REP = 1 << 17
 
 
 class RoundIn(C.Structure):

@@ -39,6 +39,7 @@ struct drb_engine {
   uint64_t bytes;
   std::vector<void *> allocs;
   uint64_t ctr_rows = 0;                     // workgroup counter rows
+  uint32_t *xcount = nullptr;                // [R][R] plane summaries
   unsigned long long *ctr_total = nullptr;   // their sum (read_counters)
   void *scratch;
   size_t scratch_bytes;
@@ -161,6 +162,10 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   if (cfg->max_props == 0 || cfg->prop_slots == 0 || cfg->ri_slots == 0)
     return DRB_EINVAL;
   if (cfg->save_cap % 16) return DRB_EINVAL;
+  if (cfg->place_world > 1 &&
+      (cfg->place_rank >= cfg->place_world || cfg->entry_mbox == 0 ||
+       cfg->entry_mbox > cfg->window))
+    return DRB_EINVAL;
   if (cfg->election_rtt == 0 || cfg->heartbeat_rtt == 0) return DRB_EINVAL;
   // limitSize never binds inside the window (entryutils.go:50-63)
   if ((uint64_t)cfg->window * (128 + cfg->cmd_cap) > MAX_ENTRY_SIZE)
@@ -199,6 +204,21 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   v.heartbeat_rtt = cfg->heartbeat_rtt;
   v.check_quorum = cfg->check_quorum;
   v.first_shard_id = cfg->first_shard_id;
+  v.place_world = cfg->place_world > 1 ? cfg->place_world : 1;
+  v.place_rank = v.place_world > 1 ? cfg->place_rank : 0;
+  v.total_groups = cfg->total_groups ? cfg->total_groups : G * v.place_world;
+  if (v.total_groups > G * v.place_world) {
+    delete e;
+    return DRB_EINVAL;
+  }
+  v.remote_mask = 0;
+  if (v.place_world > 1)
+    for (uint32_t a = 0; a < R; ++a)
+      for (uint32_t b = 0; b < R; ++b)
+        if (a != b && b % v.place_world != a % v.place_world)
+          v.remote_mask |= 1ull << (a * R + b);
+  v.E = v.remote_mask ? cfg->entry_mbox : 0;
+  v.stage_slot = 0;
   int rc = 0;
   rc |= dalloc(e, &v.u64, (uint64_t)NUM_U64 * R * G);
   rc |= dalloc(e, &v.u32, (uint64_t)NUM_U32 * R * G);
@@ -222,6 +242,19 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
   rc |= dalloc(e, &v.rtr_count, R * G);
   rc |= dalloc(e, &v.read_sum, R * G);
+  if (v.remote_mask) {  // inbound copies of the remote planes
+    rc |= dalloc(e, &v.mbox_in, 2 * R * R * v.MB * MSG_CHUNKS * G);
+    rc |= dalloc(e, &v.meta_in, 2 * R * R * G);
+    rc |= dalloc(e, &v.maxapp_in, 2 * R * R * G);
+    rc |= dalloc(e, &v.elo, 2 * R * R * G);
+    rc |= dalloc(e, &v.elo_in, 2 * R * R * G);
+    rc |= dalloc(e, &v.embox,
+                 2 * R * R * (uint64_t)v.E * (ENT_META + v.C16) * G);
+    rc |= dalloc(e, &v.embox_in,
+                 2 * R * R * (uint64_t)v.E * (ENT_META + v.C16) * G);
+    rc |= dalloc(e, &v.xrows, 2 * R * R * ((G + 255) / 256));
+    rc |= dalloc(e, &e->xcount, R * R);
+  }
   v.save_cap16 = cfg->save_cap / 16;
   if (v.save_cap16) {
     rc |= dalloc(e, &v.save_buf, R * G * v.save_cap16);
@@ -395,7 +428,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
     for (uint32_t s = 0; s < R; ++s) {
       drb_replica_state &o = st[gi * R + s];
       memset(&o, 0, sizeof(o));
-      o.shard_id = v.first_shard_id + g;
+      o.shard_id = v.first_shard_id + gid(v, s, g);
       o.replica_id = s + 1;
       for (int k = 0; k < NUM_U64_EXPORTED; ++k) *st_u64(&o, k) = d64[a++];
       o.role = d32[b++];
@@ -546,7 +579,8 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   SET(F_HEARTBEAT_TICK, 0);
   SET(F_RAND_TIMEOUT,
       v.election_rtt +
-          mix64(seed ^ (0xE1ull << 56) ^ (g * R + s)) % v.election_rtt);
+          mix64(seed ^ (0xE1ull << 56) ^ (gid(v, s, g) * R + s)) %
+              v.election_rtt);
   SET(F_TICK_COUNT, 1);
   SET(F_COMMITTED, L1);
   SET(F_PROCESSED, L1);
@@ -569,7 +603,8 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   SET(F_TERM_START, L1);  // the leader's no-op opened the term
 #undef SET
   v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
-  v.u32[u32_ix(v, W_FLAGS, s, g)] = DRB_F_HOSTED;
+  v.u32[u32_ix(v, W_FLAGS, s, g)] =
+      gid(v, s, g) < v.total_groups ? DRB_F_HOSTED : 0u;
   v.u32[u32_ix(v, W_FB_REASON, s, g)] = 0;
   v.u32[u32_ix(v, W_RI_COUNT, s, g)] = 0;
   for (uint32_t p = 0; p < v.R; ++p) {
@@ -619,6 +654,7 @@ extern "C" int drb_init_steady(drb_engine *e, uint64_t term,
   if (!e || leader_slot >= e->cfg.num_replicas || term < 2) return DRB_EINVAL;
   if (e->cfg.cmd_cap < 32 || e->v.W < e->cfg.num_replicas + 2)
     return DRB_EINVAL;
+  e->v.stage_slot = leader_slot;  // staged inputs go to the leaders
   dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
   k_init_steady<<<grid, 256, 0, e->stream>>>(e->v, term, leader_slot, seed);
   HIPCHK(hipGetLastError());
@@ -667,8 +703,9 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
 // SURVEY 8(d) synthetic writes; bit-identical to dragonboat_amd/workload.py
 __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
                          uint32_t val_len, uint64_t seed, uint64_t salt) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= v.G) return;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= v.G) return;
+  const uint64_t g = gid(v, v.stage_slot, lane);  // the seeded group
   const uint64_t cid = mix64(seed ^ 0xC11E47C11E47C11Eull ^ g) | 1;
   for (uint32_t j = 0; j < k; ++j) {
     uint64_t r0 = mix64(seed ^ (g * 0x9E3779B97F4A7C15ull) ^ (salt << 32) ^
@@ -690,19 +727,19 @@ __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
       b[13 + q] = (uint8_t)(x >> (8 * (q % 8)));
     }
     uint32_t clen = 13 + val_len;
-    v.props[prop_ix(v, ps, j, 0, g)] = mk4(r0 | 1, cid);
-    v.props[prop_ix(v, ps, j, 1, g)] = mk4(0, 0);
-    v.props[prop_ix(v, ps, j, 2, g)] =
+    v.props[prop_ix(v, ps, j, 0, lane)] = mk4(r0 | 1, cid);
+    v.props[prop_ix(v, ps, j, 1, lane)] = mk4(0, 0);
+    v.props[prop_ix(v, ps, j, 2, lane)] =
         make_uint4(DRB_ENTRY_ENCODED, clen, 0, 0);
     for (uint32_t c = 0; c < v.C16; ++c) {
       uint32_t w[4] = {0, 0, 0, 0};
       for (uint32_t q = 0; q < 16; ++q)
         w[q >> 2] |= (uint32_t)b[c * 16 + q] << (8 * (q & 3));
-      v.props[prop_ix(v, ps, j, PROP_META + c, g)] =
+      v.props[prop_ix(v, ps, j, PROP_META + c, lane)] =
           make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
-  v.prop_count[(uint64_t)ps * v.G + g] = k;
+  v.prop_count[(uint64_t)ps * v.G + lane] = k;
 }
 
 extern "C" int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
@@ -733,12 +770,13 @@ extern "C" int drb_stage_read_index(drb_engine *e, uint32_t slot,
 
 __global__ void k_gen_ri(View v, uint32_t rs, uint64_t seed, uint64_t salt,
                          uint64_t high) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= v.G) return;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= v.G) return;
+  const uint64_t g = gid(v, v.stage_slot, lane);
   uint64_t low = mix64(seed ^ 0x5EAD1DE85EAD1DE8ull ^
                        (g * 0x9E3779B97F4A7C15ull) ^ (salt << 40)) |
                  1;
-  v.ri_in[(uint64_t)rs * v.G + g] = mk4(low, high);
+  v.ri_in[(uint64_t)rs * v.G + lane] = mk4(low, high);
 }
 
 extern "C" int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
@@ -765,6 +803,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                           uint64_t *accepted, uint64_t *dropped) {
   if (!e) return DRB_EINVAL;
   const View &v = e->v;
+  // replicas spread over ranks exchange whole mailbox planes instead
+  if (v.remote_mask) return DRB_ENOSYS;
   const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
   const uint32_t tag = (uint32_t)e->round;
   uint64_t acc = 0, drop = 0;
@@ -839,7 +879,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     std::vector<uint4> val = {c0, c1};
     if (scatter(e, v.mbox, idx, val)) return DRB_EDEVICE;
     constexpr uint32_t cnts = MI_COUNT | (0xfu << MI_NRI) | (0xfu << MI_NRR);
-    const uint32_t inf = msg_info(m.type, zero) | (other ? MI_TERM_OTHER : 0);
+    const uint32_t inf =
+        msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0);
     cur.y = (cur.y + (inf & cnts)) | (inf & ~cnts);
     if (m.type == DRB_MSG_REPLICATE) {
       cur.y |= 1u << (MI_REPMASK + k);
@@ -1004,7 +1045,7 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
     Msg mm = msg_decode(c[0], c[1], q_hi(meta), prev_lo, prev_hi);
     drb_message &m = out[(*nm)++];
     memset(&m, 0, sizeof(m));
-    m.shard_id = v.first_shard_id + g;
+    m.shard_id = v.first_shard_id + gid(v, from, g);
     m.from = from + 1;
     m.to = to + 1;
     m.type = mm.type;
@@ -1080,13 +1121,130 @@ extern "C" int drb_export_ready_to_reads(drb_engine *e, uint64_t group,
   std::vector<uint4> val;
   if (gather(e, v.rtr, idx, val)) return DRB_EDEVICE;
   for (uint32_t k = 0; k < n && k < cap; ++k) {
-    out[k].shard_id = v.first_shard_id + group;
+    out[k].shard_id = v.first_shard_id + gid(v, slot, group);
     out[k].replica_id = slot + 1;
     out[k].index = lo64h(val[2 * k]);
     out[k].ctx_low = hi64h(val[2 * k]);
     out[k].ctx_high = lo64h(val[2 * k + 1]);
   }
   if (n_out) *n_out = n;
+  return DRB_OK;
+}
+
+// ---------------------------------------------------------------- exchange
+__global__ void k_plane_sum(const uint32_t *rows, uint32_t RR,
+                            uint32_t blocks, uint32_t *out) {
+  __shared__ uint32_t red[3][256];
+  const uint32_t pair = blockIdx.x;
+  uint32_t k = 0, en = 0, f = 0;
+  for (uint32_t role = 0; role < 2; ++role)
+    for (uint32_t b = threadIdx.x; b < blocks; b += blockDim.x) {
+      const uint32_t w = rows[((uint64_t)role * RR + pair) * blocks + b];
+      k = max(k, w & 0xffu);
+      en = max(en, (w >> 8) & 0xffu);
+      f |= w >> 16;
+    }
+  red[0][threadIdx.x] = k;
+  red[1][threadIdx.x] = en;
+  red[2][threadIdx.x] = f;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] = max(red[0][threadIdx.x], red[0][threadIdx.x + o]);
+      red[1][threadIdx.x] = max(red[1][threadIdx.x], red[1][threadIdx.x + o]);
+      red[2][threadIdx.x] |= red[2][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[pair] = red[0][0] | (red[1][0] << 8) | (red[2][0] << 16);
+}
+
+extern "C" int drb_plane_counts(drb_engine *e, uint32_t *words) {
+  if (!e || !words) return DRB_EINVAL;
+  const View &v = e->v;
+  const uint32_t RR = v.R * v.R;
+  if (!v.remote_mask || e->round == 0) {
+    memset(words, 0, RR * sizeof(uint32_t));
+    return DRB_OK;
+  }
+  const uint32_t blocks = (uint32_t)((v.G + 255) / 256);
+  k_plane_sum<<<RR, 256, 0, e->stream>>>(v.xrows, RR, blocks, e->xcount);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(words, e->xcount, RR * sizeof(uint32_t),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (uint32_t q = 0; q < RR; ++q)
+    if (!((v.remote_mask >> q) & 1ull)) words[q] = 0;
+  return DRB_OK;
+}
+
+extern "C" int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to,
+                              int dir) {
+  if (!e || from >= e->v.R || to >= e->v.R) return -1;
+  const View &v = e->v;
+  if (!pair_remote(v, from, to)) return -1;
+  const uint32_t N = v.place_world, d = (to % N + N - from % N) % N;
+  return (int)(dir == 0 ? (v.place_rank + d) % N : (v.place_rank + N - d) % N);
+}
+
+extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
+                                 uint32_t word, int dir, drb_region *out) {
+  if (!e || !out || from >= e->v.R || to >= e->v.R) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!pair_remote(v, from, to) || e->round == 0) return 0;
+  const uint32_t buf = (uint32_t)(e->round & 1);  // the last round's outbox
+  const uint32_t K = DRB_PLANE_K(word), En = DRB_PLANE_E(word);
+  if (K > v.MB || En > v.E) return DRB_ERANGE;
+  uint4 *mb = dir ? v.mbox_in : v.mbox;
+  uint4 *meta = dir ? v.meta_in : v.mbox_meta;
+  uint64_t *mx = dir ? v.maxapp_in : v.mbox_maxapp;
+  uint64_t *elo = dir ? v.elo_in : v.elo;
+  uint4 *eb = dir ? v.embox_in : v.embox;
+  const uint64_t G = v.G;
+  int n = 0;
+  if (K) {
+    out[n++] = {mb + mbox_ix(v, buf, from, to, 0, 0, 0), K * G * 16};
+    if (word & DRB_PLANE_C1)
+      out[n++] = {mb + mbox_ix(v, buf, from, to, 0, 1, 0), K * G * 16};
+    out[n++] = {meta + mmeta_ix(v, buf, from, to, 0), G * 16};
+    if (word & DRB_PLANE_REP)
+      out[n++] = {mx + mmeta_ix(v, buf, from, to, 0), G * 8};
+  }
+  if (En) {
+    out[n++] = {elo + mmeta_ix(v, buf, from, to, 0), G * 8};
+    out[n++] = {eb + embox_ix(v, buf, from, to, 0, 0, 0),
+                (uint64_t)En * (ENT_META + v.C16) * G * 16};
+  }
+  return n;
+}
+
+extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
+  if (!engines || n == 0) return DRB_EINVAL;
+  const uint32_t R = engines[0]->v.R;
+  std::vector<std::vector<uint32_t>> words(n, std::vector<uint32_t>(R * R));
+  for (uint32_t r = 0; r < n; ++r) {
+    const drb_engine *e = engines[r];
+    if (!e || e->v.R != R || e->v.place_world != n || e->v.place_rank != r ||
+        e->round != engines[0]->round || e->v.G != engines[0]->v.G)
+      return DRB_EINVAL;
+    if (int rc = drb_plane_counts(engines[r], words[r].data())) return rc;
+  }
+  for (uint32_t r = 0; r < n; ++r)
+    for (uint32_t a = 0; a < R; ++a)
+      for (uint32_t b = 0; b < R; ++b) {
+        const uint32_t w = words[r][a * R + b];
+        const int peer = drb_plane_peer(engines[r], a, b, 0);
+        if (peer < 0 || !w) continue;
+        drb_engine *dst = engines[peer];
+        drb_region src[DRB_PLANE_REGIONS], dreg[DRB_PLANE_REGIONS];
+        const int ns = drb_plane_regions(engines[r], a, b, w, 0, src);
+        const int nd = drb_plane_regions(dst, a, b, w, 1, dreg);
+        if (ns < 0 || ns != nd) return DRB_EINVAL;
+        for (int q = 0; q < ns; ++q)
+          HIPCHK(hipMemcpyAsync(dreg[q].ptr, src[q].ptr, src[q].bytes,
+                                hipMemcpyDefault, dst->stream));
+      }
+  for (uint32_t r = 0; r < n; ++r) HIPCHK(hipStreamSynchronize(engines[r]->stream));
   return DRB_OK;
 }
 

@@ -107,7 +107,20 @@ struct View {
   uint32_t *save_len;     // [R][G] bytes (0: nothing saved)
   uint32_t *save_crc;     // [R][G] CRC32-IEEE of those bytes
   uint32_t save_cap16;    // save_buf chunks per replica (0: no encoding)
-  uint32_t pad1;
+  // placement (drb_config) and the cross-rank planes (world >= 2)
+  uint32_t place_world, place_rank;
+  uint64_t total_groups;
+  uint64_t remote_mask;   // bit from*R+to: that plane is on another rank
+  uint32_t E;             // entry rows per remote plane
+  uint32_t stage_slot;    // world >= 2: the slot staged inputs go to
+  uint4 *mbox_in;         // inbound remote planes, shaped as mbox
+  uint4 *meta_in;         // shaped as mbox_meta
+  uint64_t *maxapp_in;    // shaped as mbox_maxapp
+  uint64_t *elo;          // [2][R][R][G] first entry index in embox rows
+  uint64_t *elo_in;
+  uint4 *embox;           // [2][R][R][E][ENT_META + C16][G] entries
+  uint4 *embox_in;
+  uint32_t *xrows;        // [2 roles][R][R][blocks] per-block plane summary
   unsigned long long *counters;  // [8] (drb_round_out order from index 1)
 };
 
@@ -137,13 +150,37 @@ __host__ __device__ inline uint64_t ring_ix(const View &v, uint32_t slot,
   uint64_t rs = index & (v.W - 1);
   return (((uint64_t)slot * v.W + rs) * (ENT_META + v.C16) + chunk) * v.G + g;
 }
+// [buf][pair][chunk][k][g]: the first K records of a (sender, receiver)
+// plane are one contiguous region per chunk (what a cross-rank exchange
+// ships)
 __host__ __device__ inline uint64_t mbox_ix(const View &v, uint32_t buf,
                                             uint32_t from, uint32_t to,
                                             uint32_t k, uint32_t chunk,
                                             uint64_t g) {
   uint64_t pair = (uint64_t)from * v.R + to;
-  return ((((uint64_t)buf * v.R * v.R + pair) * v.MB + k) * MSG_CHUNKS +
-          chunk) * v.G + g;
+  return ((((uint64_t)buf * v.R * v.R + pair) * MSG_CHUNKS + chunk) * v.MB +
+          k) * v.G + g;
+}
+// entry rows of a remote (leader, follower) plane: [buf][pair][e][chunk][g]
+__host__ __device__ inline uint64_t embox_ix(const View &v, uint32_t buf,
+                                             uint32_t from, uint32_t to,
+                                             uint32_t e, uint32_t chunk,
+                                             uint64_t g) {
+  uint64_t pair = (uint64_t)from * v.R + to;
+  return ((((uint64_t)buf * v.R * v.R + pair) * v.E + e) *
+              (ENT_META + v.C16) + chunk) * v.G + g;
+}
+// placement: is the (from, to) plane on another rank?
+__host__ __device__ inline bool pair_remote(const View &v, uint32_t from,
+                                            uint32_t to) {
+  return (v.remote_mask >> (from * v.R + to)) & 1ull;
+}
+// the global group of replica slot s at lane g (include/drb_engine.h)
+__host__ __device__ inline uint64_t gid(const View &v, uint32_t s,
+                                        uint64_t g) {
+  if (v.place_world <= 1) return g;
+  const uint32_t N = v.place_world;
+  return (uint64_t)N * g + (v.place_rank + N - (s % N)) % N;
 }
 __host__ __device__ inline uint64_t mmeta_ix(const View &v, uint32_t buf,
                                              uint32_t from, uint32_t to,

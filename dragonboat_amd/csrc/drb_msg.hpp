@@ -53,8 +53,9 @@ constexpr uint32_t MI_OFF_FOLLOWER = 1u << 15;  // the fast path for / a
                                                 // follower does
 constexpr uint32_t MI_TERM = 1u << 16;        // a record carries the term
 constexpr uint32_t MI_TERM_OTHER = 1u << 17;  // a record's term != header's
-constexpr int MI_REPMASK = 18;  // [18:32] bit k: record k is a Replicate
-constexpr uint32_t MB_MAX = 14;  // records per (sender, receiver, round)
+constexpr int MI_REPMASK = 18;  // [18:31] bit k: record k is a Replicate
+constexpr uint32_t MI_REJECT = 1u << 31;  // a rejecting ReplicateResp
+constexpr uint32_t MB_MAX = 13;  // records per (sender, receiver, round)
 
 struct Msg {
   uint32_t type, reject, n;
@@ -93,8 +94,10 @@ __host__ __device__ inline bool is_ctx_type(uint32_t t) {
 }
 
 // header info contribution of one record
-__host__ __device__ inline uint32_t msg_info(uint32_t type, bool term_zero) {
+__host__ __device__ inline uint32_t msg_info(uint32_t type, bool term_zero,
+                                             bool reject = false) {
   uint32_t i = 1;  // count
+  if (reject && type == DRB_MSG_REPLICATE_RESP) i |= MI_REJECT;
   if (type == DRB_MSG_READ_INDEX) i += 1u << MI_NRI;
   if (type == DRB_MSG_REPLICATE_RESP) i += 1u << MI_NRR;
   if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)

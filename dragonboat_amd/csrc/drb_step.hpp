@@ -79,6 +79,7 @@ struct Rep {
   // round-local
   HintCtx hc;          // ctx dedup state of this sender (drb_msg.hpp)
   uint32_t nmsgs;
+  uint32_t c1mask;     // destinations that got a record with a c1 chunk
   uint32_t nrtr;
   uint32_t ndropped_ri;
   uint64_t guard_new;
@@ -100,6 +101,8 @@ struct RemLds {
 struct Lane {
   void *rl;       // RemLds<R> of this workgroup
   uint32_t *oi;   // [R][256] outbox header info per destination (LDS)
+  uint64_t *elo;  // [R][256] leader: lowest entry index sent to a remote
+                  // follower this round (~0: none), LDS
   uint32_t tid;   // lane within the workgroup
   const View *v;
   uint32_t slot;
@@ -183,12 +186,21 @@ DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   uint4 c0, c1;
   const bool has = msg_encode(mm, to_slot, &r.hc, c0, c1);
   constexpr uint32_t cnts = MI_COUNT | (0xfu << MI_NRI) | (0xfu << MI_NRR);
-  const uint32_t inf = msg_info(mm.type, mm.term == 0);
+  const uint32_t inf = msg_info(mm.type, mm.term == 0, m.reject != 0);
   w = (w + (inf & cnts)) | (inf & ~cnts);
   v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] = c0;
-  if (has) v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] = c1;
+  if (has) {
+    v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] = c1;
+    r.c1mask |= 1u << to_slot;
+  }
   if (m.type == DRB_MSG_REPLICATE) {
     w |= 1u << (MI_REPMASK + k);
+    // entries to a replica on another rank travel by value: the rows
+    // [lowest index sent, last] ship with the plane (end of the round)
+    if (m.n && pair_remote(v, L.slot, to_slot)) {
+      uint64_t &lo = L.elo[to_slot * 256 + L.tid];
+      lo = umin64(lo, m.log_index + 1);
+    }
     // LogIndex + n of successive Replicates never decreases in a round
     v.mbox_maxapp[mmeta_ix(v, L.wbuf, L.slot, to_slot, L.g)] =
         m.log_index + m.n;
@@ -549,12 +561,29 @@ DRB_DEV void leader_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
   }
 }
 
+// Where the entries of a Replicate from sender slot s are read: the
+// sender's window when it is co-resident (the ring guard keeps them
+// resident until the follower has read them), else the entry rows that
+// came with the sender's plane (entry index lo at row 0).
+struct EntSrc {
+  bool remote;
+  uint64_t lo;
+};
+DRB_DEV uint4 ent_chunk(const Lane &L, const EntSrc &src, uint32_t s,
+                        uint64_t idx, uint32_t c) {
+  const View &v = *L.v;
+  if (src.remote)
+    return v.embox_in[embox_ix(v, L.rbuf, s, L.slot, (uint32_t)(idx - src.lo),
+                               c, L.g)];
+  return v.ring[ring_ix(v, s, idx, c, L.g)];
+}
+
 // handleFollowerReplicate (raft.go:2122) -> handleReplicateMessage
 // (raft.go:1444-1484) -> tryAppend (logentry.go:296-310) -> merge
 // (inmemory.go:199-230)
 template <int R>
 DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
-                                const Msg &m) {
+                                const Msg &m, const EntSrc &src) {
   const View &v = *L.v;
   r.election_tick = 0;  // leaderIsAvailable
   set_leader(r, (uint64_t)s + 1);
@@ -571,7 +600,7 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
     uint64_t ci = 0;
     for (uint32_t i = 0; i < m.n; ++i) {
       uint64_t idx = m.log_index + 1 + i;
-      uint64_t et = ring_term<R>(L, (uint32_t)s, idx);
+      uint64_t et = lo64(ent_chunk(L, src, (uint32_t)s, idx, 0));
       if (log_term(L, r, idx) != et) {
         ci = idx;
         break;
@@ -583,7 +612,7 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
         return;
       }
       uint64_t new_last = m.log_index + m.n;
-      uint64_t first_term = ring_term<R>(L, (uint32_t)s, ci);
+      uint64_t first_term = lo64(ent_chunk(L, src, (uint32_t)s, ci, 0));
       bool inmem_nonempty = r.last >= r.marker;
       if (ci == r.marker + (inmem_nonempty ? r.last - r.marker + 1 : 0)) {
         // append at the end: checkEntriesToAppend(existing, ents)
@@ -608,12 +637,12 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
       const uint32_t chunks = ENT_META + v.C16;
       uint64_t ts = new_last + 1;
       for (uint64_t idx = ci; idx <= new_last; ++idx) {
-        uint4 m0 = v.ring[ring_ix(v, (uint32_t)s, idx, 0, L.g)];
+        uint4 m0 = ent_chunk(L, src, (uint32_t)s, idx, 0);
         v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = m0;
         if (ts > new_last && lo64(m0) == r.term) ts = idx;
         for (uint32_t c = 1; c < chunks; ++c)
           v.ring[ring_ix(v, L.slot, idx, c, L.g)] =
-              v.ring[ring_ix(v, (uint32_t)s, idx, c, L.g)];
+              ent_chunk(L, src, (uint32_t)s, idx, c);
       }
       if (ci <= r.term_start) r.term_start = ts;
       r.last = new_last;
@@ -656,7 +685,8 @@ DRB_DEV void follower_read_index_resp(const Lane &L, Rep<R> &r, int s,
 }
 
 template <int R>
-DRB_DEV void dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m) {
+DRB_DEV void dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
+                      const EntSrc &src) {
   if (r.role == DRB_LEADER) {
     if (m.type == DRB_MSG_REPLICATE_RESP)
       leader_replicate_resp(L, r, s, m);
@@ -666,7 +696,7 @@ DRB_DEV void dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m) {
       leader_read_index(L, r, m.hint, m.hint_high, (uint64_t)s + 1);
   } else {
     if (m.type == DRB_MSG_REPLICATE)
-      follower_replicate(L, r, s, m);
+      follower_replicate(L, r, s, m, src);
     else if (m.type == DRB_MSG_HEARTBEAT)
       follower_heartbeat(L, r, s, m);
     else if (m.type == DRB_MSG_READ_INDEX_RESP)
@@ -1115,6 +1145,40 @@ DRB_DEV void block_counters(const View &v, const uint32_t (&c)[N]) {
   }
 }
 
+// one row per workgroup of xrows[role][from][to][block]:
+// K | E << 8 | flags << 16 (max, max, or over the block's lanes)
+template <bool LEAD>
+DRB_DEV void block_plane_summary(const View &v, uint32_t from, uint32_t to,
+                                 uint32_t K, uint32_t E, uint32_t fl) {
+  __shared__ uint32_t red[4][3];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    K = max(K, (uint32_t)__shfl_xor(K, o, 64));
+    E = max(E, (uint32_t)__shfl_xor(E, o, 64));
+    fl |= (uint32_t)__shfl_xor(fl, o, 64);
+  }
+  __syncthreads();  // red[] is reused across destinations
+  if (lane == 0) {
+    red[wave][0] = K;
+    red[wave][1] = E;
+    red[wave][2] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t k = 0, e = 0, f = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      k = max(k, red[w][0]);
+      e = max(e, red[w][1]);
+      f |= red[w][2];
+    }
+    const uint64_t row = (((uint64_t)(LEAD ? 0 : 1) * v.R + from) * v.R + to) *
+                             gridDim.x + blockIdx.x;
+    v.xrows[row] = k | (e << 8) | (f << 16);
+  }
+}
+
 // LEAD selects the role this launch steps: the leader kernel takes the
 // replicas whose role is LEADER, the follower kernel every other replica
 // (non-FOLLOWER roles fall back).  Both read round t-1's mailbox and write
@@ -1133,6 +1197,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
+  __shared__ uint64_t elo_lds[LEAD ? R : 1][256];
   if (p.encode_saves) {  // uniform: every thread reaches the barrier
     crc32_table_init(crc_tab, threadIdx.x);
     __syncthreads();
@@ -1140,6 +1205,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   Lane L;
   L.rl = &rl;
   L.oi = oinfo;
+  L.elo = &elo_lds[0][0];
   L.tid = threadIdx.x;
   L.v = vp;
   L.slot = slot;
@@ -1150,6 +1216,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint64_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
+  uint32_t sent_c1 = 0;     // remote planes: destinations given a c1 chunk
+  uint64_t last_final = 0;  // leader: last index at the end of the round
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
   uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
@@ -1166,7 +1234,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
     load_rep<R, LEAD>(L, r);
     r.role = LEAD ? DRB_LEADER : DRB_FOLLOWER;
 #pragma unroll
-    for (int s = 0; s < R; ++s) oinfo[s * 256 + threadIdx.x] = 0;
+    for (int s = 0; s < R; ++s) {
+      oinfo[s * 256 + threadIdx.x] = 0;
+      if (LEAD) elo_lds[LEAD ? s : 0][threadIdx.x] = ~0ull;
+    }
+    r.c1mask = 0;
     r.hc.lo = r.hc.hi = 0;
     r.hc.dests = 0;
     r.nmsgs = 0;
@@ -1185,11 +1257,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
     // the inbox, from the per-sender headers alone (drb_msg.hpp)
     uint32_t nin_packed = 0;  // 4-bit inbox count per sender slot
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
+    uint32_t rej_from = 0;  // senders with a rejecting ReplicateResp
     uint64_t max_app = 0;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot) continue;
-      const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)];
+      const bool rm = pair_remote(v, s, slot);
+      const uint4 meta = (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(v, L.rbuf, s,
+                                                                 slot, g)];
       const uint32_t info = meta.x == tag_prev ? meta.y : 0u;
       const uint32_t ns = info & MI_COUNT;
       nin_packed |= ns << (4 * s);
@@ -1203,9 +1278,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       n_ri_msgs += (info >> MI_NRI) & 15u;
       n_rr += (info >> MI_NRR) & 15u;
       if (info & MI_RESP) resp_from |= 1u << s;
+      if (info & MI_REJECT) rej_from |= 1u << s;
       if (!LEAD && (info & MI_REP))
-        max_app = umax64(max_app,
-                         v.mbox_maxapp[mmeta_ix(v, L.rbuf, s, slot, g)]);
+        max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
+                                      v, L.rbuf, s, slot, g)]);
       total_in += ns;
     }
     uint32_t nprops = 0;
@@ -1215,9 +1291,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
     const uint64_t keep_common =
         umin64(umin64(r.processed + 1, r.committed), r.sm_index);
     if (is_leader) {
-      if (p.prop_slot != DRB_NONE)
+      // staged inputs are per lane: with replicas spread over ranks a lane
+      // holds R different groups, and they go to the stage slot's leader
+      const bool stage = v.place_world <= 1 || slot == v.stage_slot;
+      if (p.prop_slot != DRB_NONE && stage)
         nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
-      if (p.ri_slot != DRB_NONE) {
+      if (p.ri_slot != DRB_NONE && stage) {
         uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
         in_lo = lo64(c);
         in_hi = hi64(c);
@@ -1240,6 +1319,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         if ((uint32_t)s != slot) keep = umin64(keep, rem_get<R>(L, s).n - 1);
       if (nprops && r.last + nprops >= keep + v.W && fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
+      // entry rows of a remote follower's plane: the round sends it
+      // entries [floor, new last], floor = its next, or above its match
+      // where a reject or respondedTo (remote.go:170-198) may lower next
+      if (v.remote_mask) {
+#pragma unroll
+        for (int s = 0; s < R; ++s)
+          if ((uint32_t)s != slot && pair_remote(v, slot, s)) {
+            const RemoteV x = rem_get<R>(L, s);
+            const bool lowers = ((rej_from >> s) & 1) ||
+                                (((resp_from >> s) & 1) &&
+                                 x.st != DRB_REMOTE_REPLICATE);
+            const uint64_t floor = lowers ? x.m + 1 : x.n;
+            if (r.last + nprops + 1 > floor + v.E && fb == DRB_FB_NONE)
+              fb = DRB_FB_CAPACITY;
+          }
+      }
       // mailbox: messages the round can send to each follower s.  Each
       // message from s triggers at most one send back to s (resend,
       // retry, raft.go:1878-1923); a broadcast to everyone needs a commit
@@ -1310,21 +1405,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
           if ((uint32_t)s == slot) continue;
           const uint32_t ns = (nin_packed >> (4 * s)) & 15u;
           if (!ns) continue;
-          const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)];
+          const bool rm = pair_remote(v, s, slot);
+          const uint4 *mb = rm ? v.mbox_in : v.mbox;
+          const uint4 meta = (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(
+              v, L.rbuf, s, slot, g)];
           const uint64_t sterm = hi64(meta);
           // records of this pass: the header's Replicate mask
           const uint32_t reps = meta.y >> MI_REPMASK;
           uint32_t todo = (pass == 0 ? reps : ~reps) & ((1u << ns) - 1u);
+          EntSrc src;
+          src.remote = rm;
+          src.lo = 0;
+          if (rm && pass == 0 && todo)
+            src.lo = v.elo_in[mmeta_ix(v, L.rbuf, s, slot, g)];
           uint64_t prev_lo = 0, prev_hi = 0;
           while (todo) {
             const uint32_t k = __builtin_ctz(todo);
             todo &= todo - 1;
-            const uint4 c0 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
+            const uint4 c0 = mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
             uint4 c1 = make_uint4(0, 0, 0, 0);
-            if (c0.x & MF_HAS_C1)
-              c1 = v.mbox[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
+            if (c0.x & MF_HAS_C1) c1 = mb[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
             const Msg m = msg_decode(c0, c1, sterm, prev_lo, prev_hi);
-            dispatch(L, r, s, m);
+            dispatch(L, r, s, m, src);
           }
         }
       }
@@ -1452,6 +1554,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
           if (rc == 1 && is_leader) c_commit++;
         }
       }
+      // the entry rows of remote followers' planes: [lowest sent, last]
+      if (LEAD && v.remote_mask) {
+        const uint32_t chunks = ENT_META + v.C16;
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          if ((uint32_t)s == slot || !pair_remote(v, slot, s)) continue;
+          const uint64_t lo = elo_lds[LEAD ? s : 0][threadIdx.x];
+          if (lo == ~0ull) continue;
+          if (r.last + 1 - lo > v.E || lo < r.ring_lo) {  // pre-pass bound
+            set_error(r, DRB_FB_CAPACITY);
+            elo_lds[LEAD ? s : 0][threadIdx.x] = ~0ull;
+            continue;
+          }
+          for (uint64_t idx = lo; idx <= r.last; ++idx)
+            for (uint32_t c = 0; c < chunks; ++c)
+              v.embox[embox_ix(v, L.wbuf, slot, s, (uint32_t)(idx - lo), c,
+                               g)] = v.ring[ring_ix(v, slot, idx, c, g)];
+          v.elo[mmeta_ix(v, L.wbuf, slot, s, g)] = lo;
+        }
+        last_final = r.last;
+      }
+      sent_c1 = r.c1mask;
       // ring guard for the next round's appends
       r.ring_guard = r.guard_new;
       if (r.err) {
@@ -1481,6 +1605,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
     if (p.n_reads && !(DRB_ABLATE & 2))
       serve_reads_lane(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
                        p.key_space, c_served, c_deferred);
+  }
+  // per-block summary of this rank's remote planes (drb_exchange_*): max
+  // records, max entry rows, c1 / Replicate flags
+  if (v.remote_mask) {  // uniform
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if ((uint32_t)s == slot || !pair_remote(v, slot, s)) continue;
+      uint32_t K = 0, E = 0, fl = 0;
+      if (active) {
+        const uint32_t w = oinfo[s * 256 + threadIdx.x];
+        K = w & MI_COUNT;
+        fl = ((sent_c1 >> s) & 1u) | ((w & MI_REP) ? 2u : 0u);
+        if (LEAD) {
+          const uint64_t lo = elo_lds[LEAD ? s : 0][threadIdx.x];
+          if (lo != ~0ull) E = (uint32_t)(last_final + 1 - lo);
+        }
+      }
+      block_plane_summary<LEAD>(v, slot, (uint32_t)s, K, E, fl);
+    }
   }
   const uint32_t cnt[NUM_COUNTERS] = {
       (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,

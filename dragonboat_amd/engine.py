@@ -8,8 +8,8 @@ import ctypes as C
 import os
 
 from . import abi
-from .abi import (Config, Entry, Message, ReadyToRead, ReplicaState, RoundIn,
-                  RoundOut, entry_to_tuple, message_to_tuple)
+from .abi import (Config, Entry, Message, ReadyToRead, Region, ReplicaState,
+                  RoundIn, RoundOut, entry_to_tuple, message_to_tuple)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DRB_ENGINE_LIB") or \
@@ -66,6 +66,11 @@ SIGNATURES = {
     "drb_export_saved": (C.c_int, [P, U64, U32, PU8, SZ, PU32, PU32]),
     "drb_saved_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(PU32),
                                     C.POINTER(PU32)]),
+    "drb_plane_counts": (C.c_int, [P, PU32]),
+    "drb_plane_peer": (C.c_int, [P, U32, U32, C.c_int]),
+    "drb_plane_regions": (C.c_int, [P, U32, U32, U32, C.c_int,
+                                    C.POINTER(Region)]),
+    "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
 }
 
 
@@ -102,8 +107,9 @@ def _u8(b):
 
 DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 cmd_cap=32, max_props=4, prop_slots=2, ri_slots=2,
-                mailbox=14, kv_slots=512, kv_val_cap=4, election_rtt=10,
-                heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0)
+                mailbox=13, kv_slots=512, kv_val_cap=4, election_rtt=10,
+                heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
+                total_groups=0, place_world=1, place_rank=0, entry_mbox=0)
 
 
 class Engine:
@@ -118,7 +124,9 @@ class Engine:
                    cfg["max_props"], cfg["prop_slots"], cfg["ri_slots"],
                    cfg["mailbox"], cfg["kv_slots"], cfg["kv_val_cap"],
                    cfg["election_rtt"], cfg["heartbeat_rtt"],
-                   cfg["check_quorum"], cfg["device"], cfg["save_cap"])
+                   cfg["check_quorum"], cfg["device"], cfg["save_cap"],
+                   cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
+                   cfg["entry_mbox"], 0)
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -279,6 +287,29 @@ class Engine:
         _ck(lib().drb_export_saved(self.h, g, slot, buf, cap, C.byref(ln),
                                    C.byref(crc)), "drb_export_saved")
         return bytes(buf[:ln.value]), crc.value
+
+    # ---------------------------------------------------------- exchange
+    def plane_counts(self):
+        """Summary words [from * R + to] of the last round's remote planes."""
+        w = (C.c_uint32 * (self.R * self.R))()
+        _ck(lib().drb_plane_counts(self.h, w), "drb_plane_counts")
+        return list(w)
+
+    def plane_peer(self, a, b, direction):
+        return lib().drb_plane_peer(self.h, a, b, direction)
+
+    def plane_regions(self, a, b, word, direction):
+        """[(device address, bytes)] of plane (a, b) for the last round."""
+        arr = (Region * abi.PLANE_REGIONS)()
+        n = _ck(lib().drb_plane_regions(self.h, a, b, word, direction, arr),
+                "drb_plane_regions")
+        return [(arr[i].ptr, arr[i].bytes) for i in range(n)]
+
+    @staticmethod
+    def exchange_local(engines):
+        """One process holding every rank's engine: move the planes."""
+        arr = (P * len(engines))(*[e.h for e in engines])
+        _ck(lib().drb_exchange_local(arr, len(engines)), "drb_exchange_local")
 
     def serve_reads(self, reads_per_ctx=9, key_space=256):
         _ck(lib().drb_serve_reads(self.h, reads_per_ctx, key_space),

@@ -247,7 +247,7 @@ typedef struct drb_config {
   uint32_t max_props;        /* max proposals per group per round */
   uint32_t prop_slots;       /* staged proposal batches */
   uint32_t ri_slots;         /* staged ReadIndex batches */
-  uint32_t mailbox;          /* records per (sender, receiver) per round, 4..14 */
+  uint32_t mailbox;          /* records per (sender, receiver) per round, 4..13 */
   uint32_t kv_slots;         /* KV open-addressing slots per replica (pow2) */
   uint32_t kv_val_cap;       /* max value bytes stored inline per KV slot */
   uint32_t election_rtt;     /* Config.ElectionRTT */
@@ -257,6 +257,17 @@ typedef struct drb_config {
   /* bytes per replica for the round's EntriesToSave encoded as an
    * EntryBatch (drb_round_in.encode_saves; multiple of 16, 0: none) */
   uint32_t save_cap;
+  /* Placement.  place_world <= 1: co-resident, every replica
+   * of group g at lane g.  place_world = N >= 2: replica slot s of global
+   * group g lives on rank (g + s) mod N at lane g / N (C4); this engine is
+   * rank place_rank, num_groups is its lane count and the round's
+   * cross-rank mailbox planes move with drb_exchange_* (RCCL / P2P). */
+  uint64_t total_groups;     /* global groups (0: num_groups * N) */
+  uint32_t place_world;
+  uint32_t place_rank;
+  uint32_t entry_mbox;       /* entries per remote (sender, receiver) and
+                              * round that travel by value (N >= 2) */
+  uint32_t reserved2;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -423,6 +434,41 @@ int drb_export_saved(drb_engine *e, uint64_t group, uint32_t slot,
  * with lens[slot * G + g] and crcs[slot * G + g]. */
 int drb_saved_buffers(drb_engine *e, void **bytes, uint32_t **lens,
                       uint32_t **crcs);
+
+/* --- cross-rank mailbox exchange (place_world >= 2) ------
+ * The round's messages to replicas on other ranks stay in this engine's
+ * outbox planes; plane (from, to) moves whole to rank
+ * (place_rank + to - from) mod N, whose next round reads it as its inbox
+ * plane (from, to).  This replaces the reference transport
+ * (Transport.Send, transport.go:346 -> handleRequest, :305) for
+ * GPU-resident replicas: per round, drb_plane_counts, exchange the count
+ * words with the peers, then move drb_plane_regions (RCCL send/recv, or
+ * drb_exchange_local in one process). */
+typedef struct drb_region {
+  void *ptr;       /* device address */
+  uint64_t bytes;
+} drb_region;
+
+#define DRB_PLANE_REGIONS 6
+#define DRB_PLANE_K(w) ((w) & 0xffu)          /* records per lane (max) */
+#define DRB_PLANE_E(w) (((w) >> 8) & 0xffu)   /* entry rows (max) */
+#define DRB_PLANE_C1 (1u << 16)               /* a record has a 2nd chunk */
+#define DRB_PLANE_REP (1u << 17)              /* a Replicate */
+
+/* words[from * R + to] for this rank's remote planes of the last round
+ * (0 for local or empty ones).  Synchronises the engine stream. */
+int drb_plane_counts(drb_engine *e, uint32_t *words);
+/* The rank a plane goes to (dir 0) or comes from (dir 1); -1 if local. */
+int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to, int dir);
+/* The device regions of plane (from, to) for the last round, sized by the
+ * SENDER's word: dir 0 in this engine's outbox planes, dir 1 in its inbox
+ * planes.  Sender and receiver list identical sizes in the same order.
+ * Returns the region count (<= DRB_PLANE_REGIONS) or < 0. */
+int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
+                      uint32_t word, int dir, drb_region *out);
+/* The whole exchange among engines[rank] of one process (peer copies on
+ * the receivers' streams); every engine must have run the same round. */
+int drb_exchange_local(drb_engine *const *engines, uint32_t n);
 
 /* IStateMachine.Lookup used by NodeHost.ReadLocalNode (nodehost.go:849). */
 int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,

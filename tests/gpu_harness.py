@@ -149,3 +149,106 @@ class Pair:
                     if er != orr:
                         errs.append((g, s, "ready", er, orr))
         return errs
+
+
+class DistPair:
+    """C4 placement on one GPU: N engines (one per rank) hold replica slot s
+    of global group g at rank (g + s) mod N, lane g // N (drb_config
+    place_world); the mailbox planes move between them after every round
+    with drb_exchange_local -- the same regions RCCL moves between GPUs.
+    Stepped in lock-step with one oracle cluster of all G groups."""
+
+    def __init__(self, G, R=5, N=8, seed=0x5EEDD8B0, window=32, E=4,
+                 **engine_kw):
+        self.G, self.R, self.N, self.seed = G, R, N, seed
+        self.lanes = (G + N - 1) // N
+        self.engs = [Engine(num_groups=self.lanes, num_replicas=R,
+                            window=window, total_groups=G, place_world=N,
+                            place_rank=r, entry_mbox=E, **engine_kw)
+                     for r in range(N)]
+        self.orc = po.Cluster(G, R, seed=seed)
+        self.orc.setup_steady(0)
+        for e in self.engs:
+            e.init_steady(term=2, leader_slot=0, seed=seed)
+        self.rounds = 0
+
+    def where(self, g, s):
+        """(rank, lane) of replica slot s of group g."""
+        return (g + s) % self.N, g // self.N
+
+    def lane_group(self, r, s, j):
+        return self.N * j + (r - s) % self.N
+
+    def round(self, k=1, tick=False, read_index=False, groups=None):
+        salt = self.rounds
+        pin = ri_in = abi.DRB_NONE
+        if k:
+            counts, ents, pool = workload.build_batch(
+                self.G, k, self.seed, salt, 256, 4, groups)
+            self.orc.stage_proposals(counts, k, ents, pool)
+            for r, e in enumerate(self.engs):
+                mp = e.cfg["max_props"]
+                ec = (C.c_uint32 * self.lanes)()
+                ee = (abi.Entry * (self.lanes * mp))()
+                for j in range(self.lanes):
+                    g = self.lane_group(r, 0, j)  # the stage slot's group
+                    if g >= self.G:
+                        continue
+                    ec[j] = counts[g]
+                    for q in range(counts[g]):
+                        ee[j * mp + q] = ents[g * k + q]
+                e.stage_proposals(0, ec, ee, pool)
+            pin = 0
+        if read_index:
+            lo, hi = workload.build_read_index(self.G, self.seed, salt,
+                                               salt + 30, groups)
+            self.orc.stage_read_index(lo, hi)
+            for r, e in enumerate(self.engs):
+                el = (C.c_uint64 * self.lanes)()
+                eh = (C.c_uint64 * self.lanes)()
+                for j in range(self.lanes):
+                    g = self.lane_group(r, 0, j)
+                    if g < self.G:
+                        el[j], eh[j] = lo[g], hi[g]
+                e.stage_read_index(0, el, eh)
+            ri_in = 0
+        o = self.orc.round(tick=tick)
+        outs = [e.step(tick=tick, prop_slot=pin, ri_slot=ri_in)
+                for e in self.engs]
+        Engine.exchange_local(self.engs)
+        self.rounds += 1
+        tot = {}
+        for f in ("committed_entries", "applied_entries", "messages",
+                  "ready_to_reads", "fallbacks", "errors"):
+            tot[f] = sum(getattr(x, f) for x in outs)
+        return o, tot
+
+    def check(self, groups=None, logs=True, kv=True, msgs=True):
+        errs = []
+        for g in (range(self.G) if groups is None else groups):
+            for s in range(self.R):
+                r, j = self.where(g, s)
+                e = self.engs[r]
+                a, b = e.export_replicas(j, 1)[s], self.orc.export(g, s)
+                if a.flags & (abi.F_FALLBACK | abi.F_ERROR):
+                    errs.append((g, s, "flags", a.flags, a.fallback_reason))
+                    continue
+                d = state_diff(a, b, self.R)
+                if a.shard_id != b.shard_id:
+                    d["shard_id"] = (a.shard_id, b.shard_id)
+                if d:
+                    errs.append((g, s, "state", d))
+                    continue
+                if logs:
+                    lo = max(1, b.last_index - 8)
+                    if e.export_log(j, s, lo, b.last_index) != \
+                            self.orc.export_log(g, s, lo, b.last_index):
+                        errs.append((g, s, "log"))
+                if kv and e.kv_export(j, s) != self.orc.export_kv(g, s):
+                    errs.append((g, s, "kv"))
+                if msgs:
+                    em = by_dest(e.export_outbox(j, s))
+                    om = by_dest(self.orc.export_outbox(g, s))
+                    if em != om:
+                        errs.append((g, s, "msgs", em, om))
+        return errs

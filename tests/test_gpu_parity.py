@@ -188,3 +188,27 @@ def test_entries_to_save_capacity_falls_back():
     st = p.eng.export_replicas(0, 1)
     assert st[0].flags & abi.F_FALLBACK
     assert st[0].fallback_reason == abi.FB["CAPACITY"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,R,G", [(8, 5, 44), (2, 3, 30), (3, 5, 31),
+                                   (4, 3, 20)])
+def test_replicas_spread_over_ranks_c4(N, R, G):
+    """C4 placement: replica slot s of group g on rank
+    (g + s) mod N; every cross-rank message and its entries travel in the
+    mailbox planes moved between the ranks' engines (drb_plane_regions --
+    what RCCL moves between GPUs, here drb_exchange_local on one GPU).
+    Bit-exact against one oracle cluster of all G groups."""
+    from tests.gpu_harness import DistPair
+    p = DistPair(G=G, R=R, N=N, max_props=4)
+    assert not p.check(), "init"
+    for r in range(12):
+        k = 1 if r % 5 != 4 else (3 if r % 2 else 0)
+        o, e = p.round(k=k, tick=(r % 2 == 0), read_index=(r % 3 == 0))
+        assert e["fallbacks"] == 0 and e["errors"] == 0, (r, e)
+        assert (e["committed_entries"], e["applied_entries"], e["messages"],
+                e["ready_to_reads"]) == \
+            (o.committed_entries, o.applied_entries, o.messages,
+             o.ready_to_reads), (r, e, o.to_dict())
+        errs = p.check()
+        assert not errs, (r, errs[:3])
