@@ -29,14 +29,16 @@ READS_PER_CTX = 9      # C3: 9 ReadIndex reads per write, one ctx per round
 KEY_SPACE = 256        # K = 256 keys per group
 
 
-def alg_bytes_per_group_round(R=3, k=1, P=16, reads=True):
-    """SURVEY.md 8(d) algorithmic bytes for one group-round (co-resident)."""
+def alg_bytes_per_group_round(R=3, k=1, P=16, reads=True, spread=False):
+    """SURVEY.md 8(d) algorithmic bytes for one group-round (co-resident;
+    spread=True adds C4's B_msg for replicas on other GPUs)."""
     e = 56 + ((P + 1 + 15) // 16) * 16          # entry record
     b_round = 96 + 48 * R + 96 * (R - 1)        # leader core, remotes, flw
     b_entries = k * e * (1 + 2 * (R - 1))       # leader write, flw r+w
     b_apply = k * R * ((P + 1) + 2 * 16)        # Cmd read + slot r/w
     b_read = (64 + 9 * 16) if reads else 0      # ctx push/confirm + lookups
-    return b_round + b_entries + b_apply + b_read
+    b_msg = 3 * ((R - 1) * (48 + k * e) + (R - 1) * 24) if spread else 0
+    return b_round + b_entries + b_apply + b_read + b_msg
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
@@ -60,9 +62,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c4"],
+                    help="c3: groups sharded over GPUs, replicas "
+                         "co-resident (BASELINE metric); c4: --groups "
+                         "groups in total, replica slot s of group g on "
+                         "GPU (g + s) mod N, planes exchanged over RCCL")
     ap.add_argument("--groups", type=int, default=1 << 20,
-                    help="groups per GPU")
-    ap.add_argument("--replicas", type=int, default=3)
+                    help="groups per GPU (c3) / in total (c4)")
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="default 3 (c3) / 5 (c4)")
     ap.add_argument("--k", type=int, default=1, help="writes/group/round")
     ap.add_argument("--no-read-index", action="store_true")
     ap.add_argument("--tick-every", type=int, default=0,
@@ -148,14 +156,32 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     from dragonboat_amd.engine import Engine
+    c4 = args.workload == "c4"
+    if not args.replicas:
+        args.replicas = 5 if c4 else 3
     G, R, k = args.groups, args.replicas, args.k
+    if c4:
+        args.no_read_index = True  # 16 B writes, k_w = 1
     reads = not args.no_read_index
     NP = 8  # staged input batches (resident in HBM before timing)
-    first_shard, seed = ddist.shard_plan(rank, G)
-    eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
-                 max_props=max(1, k), prop_slots=NP, ri_slots=NP,
-                 mailbox=13, kv_slots=512, kv_val_cap=4,
-                 first_shard_id=first_shard, device=local)
+    xch = None
+    if c4:  # one global set of G groups spread over the world
+        lanes = (G + world - 1) // world
+        seed = ddist.BASE_SEED
+        eng = Engine(num_groups=lanes, num_replicas=R, window=32, cmd_cap=32,
+                     max_props=max(1, k), prop_slots=NP, ri_slots=NP,
+                     mailbox=8, kv_slots=512, kv_val_cap=4, total_groups=G,
+                     place_world=world, place_rank=rank, entry_mbox=k + 2,
+                     device=local)
+        if world > 1:
+            from dragonboat_amd.exchange import PlaneExchange
+            xch = PlaneExchange(eng, world, rank, torch.device("cuda", local))
+    else:
+        first_shard, seed = ddist.shard_plan(rank, G)
+        eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                     max_props=max(1, k), prop_slots=NP, ri_slots=NP,
+                     mailbox=13, kv_slots=512, kv_val_cap=4,
+                     first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
         eng.gen_kv_proposals(b, k, 256, 4, seed, b)
@@ -175,6 +201,8 @@ def main():
                        key_space=KEY_SPACE)
         if reads and not fused:
             eng.serve_reads(READS_PER_CTX, KEY_SPACE)
+        if xch is not None:  # C4: this round's cross-GPU planes
+            xch.step()
 
     # warmup (ticking every round); the tick cadence then follows the
     # reference's wall-clock tick worker: one LocalTick per RTTMillisecond
@@ -191,6 +219,8 @@ def main():
         eng.sync()
     args.tick_every = tick_every[0]
     eng.read_counters(reset=True)
+    if xch is not None:
+        xch.bytes_sent = 0
     K = args.steps
     ev = [(torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(K)]
@@ -213,15 +243,37 @@ def main():
     elapsed = ddist.reduce_max(elapsed, "cuda")
     committed = ddist.reduce_sum(committed, "cuda")
     value = committed / elapsed
-    alg = alg_bytes_per_group_round(R, k, 16, reads) * G
+    # algorithmic bytes of one round on this GPU (its groups; C4: its
+    # share of the global groups, plus the message bytes it moves)
+    g_here = G if not c4 else (G + world - 1) // world
+    alg = alg_bytes_per_group_round(R, k, 16, reads, c4 and world > 1) * \
+        g_here
     achieved = alg / (kern_ms * 1e-3) / 1e9
     if out.fallbacks or out.errors:
         print("WARNING: fallbacks=%d errors=%d" % (out.fallbacks, out.errors),
               file=sys.stderr)
     if rank == 0:
+        if c4:
+            metric = ("committed entries/sec (node) at %d 5-replica groups "
+                      "spread over %d GPU(s), 16B payload; %%HBM BW" % (
+                          G, world))
+            wl = ("C4: %d groups x %d replicas in total, replica slot s of "
+                  "group g on GPU (g + s) mod %d, 16B PBKV writes "
+                  "k=%d/group/round, tick every %d round(s)" % (
+                      G, R, world, k, args.tick_every))
+            par = ("replicas spread over GPUs; one plane exchange per round "
+                   "(RCCL send/recv over xGMI)" if world > 1 else
+                   "replicas co-resident (N=1)")
+        else:
+            metric = ("committed entries/sec (node) at 1M active 3-replica "
+                      "groups, 16B payload; %HBM BW")
+            wl = ("C3: %d active groups x %d replicas per GPU, 16B PBKV "
+                  "writes k=%d/group/round%s, tick every %d round(s)" % (
+                      G, R, k, ", 9:1 ReadIndex:write" if reads else "",
+                      args.tick_every))
+            par = "groups sharded, replicas co-resident"
         res = {
-            "metric": "committed entries/sec (node) at 1M active 3-replica "
-                      "groups, 16B payload; %HBM BW",
+            "metric": metric,
             "value": value,
             "unit": "committed entries/s",
             "n_gpus": world,
@@ -229,22 +281,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / K,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c4 else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (SURVEY 8d seeded PBKV writes + ReadIndex)",
             "config": {
-                "workload": "C3: %d active groups x %d replicas per GPU, "
-                            "16B PBKV writes k=%d/group/round%s, tick every "
-                            "%d round(s)" % (
-                                G, R, k, ", 9:1 ReadIndex:write" if reads
-                                else "", args.tick_every),
-                "groups_per_gpu": G, "replicas": R,
-                "parallelism": "groups sharded, replicas co-resident"},
+                "workload": wl,
+                "groups_per_gpu": g_here, "replicas": R,
+                "parallelism": par},
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(G, R),
+                "traffic": None if c4 else pmc_traffic(G, R),
                 "traffic_source": "profiles/pmc_current.json (rocprofv3 "
                                   "FETCH_SIZE x2 + WRITE_SIZE, bytes per "
                                   "round)",
@@ -257,6 +305,9 @@ def main():
                          "reads_deferred": out.reads_deferred,
                          "fallbacks": out.fallbacks, "errors": out.errors},
         }
+        if xch is not None:
+            res["exchange"] = {"bytes_sent_per_round_rank0":
+                               xch.bytes_sent / K}
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(res))

@@ -40,12 +40,15 @@ struct drb_engine {
   std::vector<void *> allocs;
   uint64_t ctr_rows = 0;                     // workgroup counter rows
   uint32_t *xcount = nullptr;                // [R][R] plane summaries
+  uint32_t role_slots[2] = {0, 0};           // role map (launch_step)
+  uint32_t *role_dev = nullptr;
   unsigned long long *ctr_total = nullptr;   // their sum (read_counters)
   void *scratch;
   size_t scratch_bytes;
 };
 
 static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+static int refresh_roles(drb_engine *e);
 
 template <typename T>
 static int dalloc(drb_engine *e, T **p, uint64_t count) {
@@ -264,6 +267,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
   rc |= dalloc(e, &e->ctr_total, NUM_COUNTERS);
+  rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
   if (!rc) {  // no Replicate in flight: ring_guard = +inf
     k_fill_u64<<<(unsigned)((R * G + 255) / 256), 256, 0, e->stream>>>(
@@ -388,7 +392,8 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
   rc |= scatter(e, v.ri_ctx, iri, dric);
   rc |= scatter(e, v.ri_idx, iri, drii);
   rc |= scatter(e, v.ri_conf, iri, dricf);
-  return rc ? DRB_EDEVICE : DRB_OK;
+  if (rc) return DRB_EDEVICE;
+  return refresh_roles(e);
 }
 
 extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
@@ -659,7 +664,7 @@ extern "C" int drb_init_steady(drb_engine *e, uint64_t term,
   k_init_steady<<<grid, 256, 0, e->stream>>>(e->v, term, leader_slot, seed);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(e->stream));
-  return DRB_OK;
+  return refresh_roles(e);
 }
 
 // ---------------------------------------------------------------- inputs
@@ -912,20 +917,58 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
 #ifndef DRB_ROLE_STREAMS
 #define DRB_ROLE_STREAMS 0
 #endif
+// Each role's launch covers only the slots where that role occurs (the
+// role map, refreshed after every host-side state change): in the steady
+// state the leader kernel's grid is one slot high, not R.
+static uint32_t slot_list(uint32_t mask, uint32_t *n) {
+  uint32_t l = 0;
+  *n = 0;
+  for (uint32_t s = 0; s < 8; ++s)
+    if ((mask >> s) & 1u) l |= s << (4 * (*n)++);
+  return l;
+}
+
 template <int R>
-static void launch_step(drb_engine *e, const RoundParams &p) {
-  dim3 grid((unsigned)((e->v.G + 255) / 256), R);
+static void launch_step(drb_engine *e, const RoundParams &p0) {
+  const unsigned gx = (unsigned)((e->v.G + 255) / 256);
+  RoundParams pl = p0, pf = p0;
+  uint32_t nl = 0, nf = 0;
+  pl.slots = slot_list(e->role_slots[0], &nl);
+  pf.slots = slot_list(e->role_slots[1], &nf);
+  hipStream_t sf = DRB_ROLE_STREAMS ? e->stream2 : e->stream;
   if (DRB_ROLE_STREAMS) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
-    step_kernel<R, true><<<grid, 256, 0, e->stream>>>(e->v, p);
-    step_kernel<R, false><<<grid, 256, 0, e->stream2>>>(e->v, p);
+  }
+  if (nl) step_kernel<R, true><<<dim3(gx, nl), 256, 0, e->stream>>>(e->v, pl);
+  if (nf) step_kernel<R, false><<<dim3(gx, nf), 256, 0, sf>>>(e->v, pf);
+  if (DRB_ROLE_STREAMS) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
-  } else {
-    step_kernel<R, true><<<grid, 256, 0, e->stream>>>(e->v, p);
-    step_kernel<R, false><<<grid, 256, 0, e->stream>>>(e->v, p);
   }
+}
+
+// role map: bit s of role_slots[0] when a hosted replica of slot s is a
+// leader, of role_slots[1] when one is not (roles change on the host side
+// only: init, import; a replica whose role would change falls back)
+__global__ void k_role_scan(View v, uint32_t *out) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t s = blockIdx.y;
+  if (g >= v.G) return;
+  if (!(v.u32[u32_ix(v, W_FLAGS, s, g)] & DRB_F_HOSTED)) return;
+  const bool lead = v.u32[u32_ix(v, W_ROLE, s, g)] == DRB_LEADER;
+  atomicOr(&out[lead ? 0 : 1], 1u << s);
+}
+
+static int refresh_roles(drb_engine *e) {
+  HIPCHK(hipMemsetAsync(e->role_dev, 0, 8, e->stream));
+  dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
+  k_role_scan<<<grid, 256, 0, e->stream>>>(e->v, e->role_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->role_slots, e->role_dev, 8, hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
 }
 
 extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
@@ -935,6 +978,8 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (in->ri_slot != DRB_NONE && in->ri_slot >= e->cfg.ri_slots)
     return DRB_ERANGE;
   RoundParams p;
+  p.slots = 0;
+  p.pad = 0;
   p.round = e->round + 1;
   p.tick = in->tick ? 1 : 0;
   p.prop_slot = in->prop_slot;
@@ -944,6 +989,10 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (p.n_reads && !p.key_space) return DRB_EINVAL;
   p.encode_saves = in->encode_saves ? 1 : 0;
   if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
+  if (e->v.remote_mask)  // plane summaries of this round only
+    HIPCHK(hipMemsetAsync(e->v.xrows, 0,
+                          2ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
+                          e->stream));
   switch (e->v.R) {
     case 1: launch_step<1>(e, p); break;
     case 2: launch_step<2>(e, p); break;
@@ -1178,13 +1227,18 @@ extern "C" int drb_plane_counts(drb_engine *e, uint32_t *words) {
   return DRB_OK;
 }
 
+extern "C" int drb_place_peer(uint32_t world, uint32_t rank, uint32_t from,
+                              uint32_t to, int dir) {
+  if (world <= 1 || rank >= world) return -1;
+  const uint32_t N = world, d = (to % N + N - from % N) % N;
+  if (d == 0) return -1;  // both replicas of the group on this rank
+  return (int)(dir == 0 ? (rank + d) % N : (rank + N - d) % N);
+}
+
 extern "C" int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to,
                               int dir) {
-  if (!e || from >= e->v.R || to >= e->v.R) return -1;
-  const View &v = e->v;
-  if (!pair_remote(v, from, to)) return -1;
-  const uint32_t N = v.place_world, d = (to % N + N - from % N) % N;
-  return (int)(dir == 0 ? (v.place_rank + d) % N : (v.place_rank + N - d) % N);
+  if (!e || from >= e->v.R || to >= e->v.R || from == to) return -1;
+  return drb_place_peer(e->v.place_world, e->v.place_rank, from, to, dir);
 }
 
 extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
@@ -1377,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
                        n_reads, key_space, served, deferred);
   }
   const uint32_t cnt[2] = {served, deferred};
-  block_counters<true, C_READS, 2>(v, cnt);
+  block_counters<true, C_READS, 2>(v, slot, cnt);
 }
 
 extern "C" int drb_serve_reads(drb_engine *e, uint32_t reads_per_ctx,

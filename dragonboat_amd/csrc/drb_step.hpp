@@ -26,11 +26,14 @@ namespace drb {
 
 // minimum waves per SIMD the step kernels are compiled for, per role
 // (caps the registers the compiler may allocate)
+// (measured at C3 on MI355X, tools/exp_variants.sh: leader 3 / follower 4
+// waves per SIMD ran 3-6 % faster than the unconstrained 2 / 3, the
+// leader's few spilled values notwithstanding)
 #ifndef DRB_LEAD_WAVES
-#define DRB_LEAD_WAVES 1
+#define DRB_LEAD_WAVES 3
 #endif
 #ifndef DRB_FOLLOW_WAVES
-#define DRB_FOLLOW_WAVES 1
+#define DRB_FOLLOW_WAVES 4
 #endif
 // timing experiments only (tools/variants.sh), never in a shipped build:
 // bit 0 skips the KV apply, bit 1 the in-round served reads
@@ -1109,6 +1112,8 @@ struct RoundParams {
   uint32_t n_reads;    // reads served per released ctx (0: none)
   uint32_t key_space;  // served-read key space
   uint32_t encode_saves;
+  uint32_t slots;  // slot of blockIdx.y = (slots >> 4 * blockIdx.y) & 15
+  uint32_t pad;
 };
 
 // Round counters: each workgroup owns one row of NUM_COUNTERS u64 in
@@ -1124,7 +1129,8 @@ DRB_DEV uint32_t wave_sum(uint32_t x) {
 
 // counters [FIRST, FIRST + N) of this workgroup's row (256 threads)
 template <bool LEAD, int FIRST, int N>
-DRB_DEV void block_counters(const View &v, const uint32_t (&c)[N]) {
+DRB_DEV void block_counters(const View &v, uint32_t slot,
+                            const uint32_t (&c)[N]) {
   __shared__ uint32_t red[4][N];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -1138,7 +1144,7 @@ DRB_DEV void block_counters(const View &v, const uint32_t (&c)[N]) {
     const uint64_t s = (uint64_t)red[0][i] + red[1][i] + red[2][i] + red[3][i];
     if (s) {
       const uint64_t row =
-          ((uint64_t)(LEAD ? 0 : 1) * gridDim.y + blockIdx.y) * gridDim.x +
+          ((uint64_t)(LEAD ? 0 : 1) * v.R + slot) * gridDim.x +
           blockIdx.x;
       v.counters[row * NUM_COUNTERS + FIRST + i] += s;
     }
@@ -1193,7 +1199,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   // global memory (global_load/store, not flat: no LDS-counter waits)
   const View *vp = &v;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t slot = blockIdx.y;
+  // the slots this launch steps (4 bits each): a role's launch covers only
+  // the slots where that role occurs (drb_engine.hip role map)
+  const uint32_t slot = (p.slots >> (4 * blockIdx.y)) & 0xfu;
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
@@ -1630,7 +1638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
       (uint32_t)c_err,    c_served,            c_deferred,
       c_saved,            c_saved_bytes};
-  block_counters<LEAD, 0, NUM_COUNTERS>(v, cnt);
+  block_counters<LEAD, 0, NUM_COUNTERS>(v, slot, cnt);
 }
 
 }  // namespace drb

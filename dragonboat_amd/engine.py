@@ -68,6 +68,7 @@ SIGNATURES = {
                                     C.POINTER(PU32)]),
     "drb_plane_counts": (C.c_int, [P, PU32]),
     "drb_plane_peer": (C.c_int, [P, U32, U32, C.c_int]),
+    "drb_place_peer": (C.c_int, [U32, U32, U32, U32, C.c_int]),
     "drb_plane_regions": (C.c_int, [P, U32, U32, U32, C.c_int,
                                     C.POINTER(Region)]),
     "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
@@ -83,7 +84,10 @@ def lib():
                 "python -c 'import __graft_entry__; __graft_entry__.build()'"
                 % LIB_PATH)
         L = C.CDLL(LIB_PATH)
+        variant = bool(os.environ.get("DRB_ENGINE_LIB"))
         for name, (res, args) in SIGNATURES.items():
+            if variant and not hasattr(L, name):
+                continue  # an older timing variant (tools/variants.sh)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -460,6 +460,9 @@ typedef struct drb_region {
 int drb_plane_counts(drb_engine *e, uint32_t *words);
 /* The rank a plane goes to (dir 0) or comes from (dir 1); -1 if local. */
 int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to, int dir);
+/* The same routing as a pure function of the placement (no device). */
+int drb_place_peer(uint32_t world, uint32_t rank, uint32_t from, uint32_t to,
+                   int dir);
 /* The device regions of plane (from, to) for the last round, sized by the
  * SENDER's word: dir 0 in this engine's outbox planes, dir 1 in its inbox
  * planes.  Sender and receiver list identical sizes in the same order.

@@ -1,0 +1,144 @@
+"""The C4 exchange step (dragonboat_amd/exchange.py) on the CPU: world_size
+2 and 3 gloo ranks move mailbox planes exactly as the RCCL run does.
+
+Each rank holds fake outbox/inbox planes in host memory, sized per plane by
+a summary word the way drb_plane_regions sizes the engine's (records K,
+entry rows E, c1 / Replicate flags).  The routing is the engine's own
+(drb_place_peer from the C ABI library, no device needed); the send/recv
+lists come from exchange.plan and run as one gloo batch_isend_irecv.
+After the step, inbox plane (a, b) of every rank must hold the bytes rank
+(rank - d) wrote into its outbox plane (a, b), d = (b - a) mod N.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+R, LANES = 5, 24
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _word(rank, a, b):
+    rng = np.random.default_rng(rank * 1000 + a * 10 + b)
+    K = int(rng.integers(0, 4))
+    E = int(rng.integers(0, 3)) if a == 0 else 0
+    fl = (1 << 16 if rng.integers(0, 2) else 0) | (1 << 17 if E else 0)
+    return K | (E << 8) | fl if (K or E) else 0
+
+
+class FakePlanes:
+    """Host-memory planes with the engine's region sizing."""
+
+    def __init__(self, rank):
+        self.out, self.inb = {}, {}
+        for a in range(R):
+            for b in range(R):
+                rng = np.random.default_rng(7 + rank * 100 + a * 10 + b)
+                self.out[(a, b)] = [rng.integers(0, 256, n, dtype=np.uint8)
+                                    for n in self._sizes(13 | (3 << 8) |
+                                                         (3 << 16))]
+                self.inb[(a, b)] = [np.zeros_like(x) for x in self.out[(a, b)]]
+
+    @staticmethod
+    def _sizes(word):
+        K, E = word & 0xff, (word >> 8) & 0xff
+        s = []
+        if K:
+            s.append(K * LANES * 16)
+            if word & (1 << 16):
+                s.append(K * LANES * 16)
+            s.append(LANES * 16)
+            if word & (1 << 17):
+                s.append(LANES * 8)
+        if E:
+            s += [LANES * 8, E * 5 * LANES * 16]
+        return s
+
+    def _pick(self, word, bufs):
+        # the full-capacity buffers in region order; take the first n bytes
+        K, E = word & 0xff, (word >> 8) & 0xff
+        order = []
+        if K:
+            order.append(0)
+            if word & (1 << 16):
+                order.append(1)
+            order.append(2)
+            if word & (1 << 17):
+                order.append(3)
+        if E:
+            order += [4, 5]
+        return [bufs[i] for i in order]
+
+    def regions(self, a, b, word, direction):
+        bufs = self._pick(word, (self.out if direction == 0 else
+                                 self.inb)[(a, b)])
+        return [(x.ctypes.data, n) for x, n in zip(bufs, self._sizes(word))]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dragonboat_amd import exchange as X
+        fp = FakePlanes(rank)
+        mine = [_word(rank, a, b) if X.place_peer(world, rank, a, b, 0) >= 0
+                else 0 for a in range(R) for b in range(R)]
+        t = torch.tensor(mine, dtype=torch.int64)
+        allw = torch.empty(world * R * R, dtype=torch.int64)
+        dist.all_gather_into_tensor(allw, t)
+        flat = allw.tolist()
+        words = [flat[k * R * R:(k + 1) * R * R] for k in range(world)]
+        ops = X.plan(R, world, rank, words, fp.regions)
+        X.run_ops(ops, X.host_bytes)
+        got = {k: [x.copy() for x in v] for k, v in fp.inb.items()}
+        q.put((rank, words, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_plane_exchange_gloo(world):
+    from dragonboat_amd import exchange as X
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, words, got = q.get(timeout=240)
+        res[r] = (words, got)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    moved = 0
+    for r in range(world):
+        words, got = res[r]
+        for a in range(R):
+            for b in range(R):
+                src = X.place_peer(world, r, a, b, 1)
+                if src < 0:
+                    assert all(not x.any() for x in got[(a, b)])
+                    continue
+                w = words[src][a * R + b]
+                sent = FakePlanes(src)
+                exp = sent._pick(w, sent.out[(a, b)])
+                dst = FakePlanes(r)._pick(w, got[(a, b)])
+                for e, d, n in zip(exp, dst, FakePlanes._sizes(w)):
+                    assert (d[:n] == e[:n]).all(), (r, a, b)
+                    moved += n
+    assert moved > 0
