@@ -82,24 +82,50 @@ def run_ops(ops, to_tensor, group=None):
             req.wait()
 
 
-class PlaneExchange:
-    """The exchange step of one rank's engine (torch.distributed group)."""
+def run_ops_staged(ops, device, group=None):
+    """The same step for a backend without device tensors (gloo): each
+    region goes through host memory."""
+    sends, recvs = [], []
+    p2p = []
+    for op, peer, (ptr, nbytes) in ops:
+        d = device_bytes(ptr, nbytes, device)
+        h = torch.empty(int(nbytes), dtype=torch.uint8)
+        if op == "send":
+            h.copy_(d)
+            p2p.append(dist.P2POp(dist.isend, h, peer, group))
+        else:
+            recvs.append((d, h))
+            p2p.append(dist.P2POp(dist.irecv, h, peer, group))
+    if p2p:
+        for req in dist.batch_isend_irecv(p2p):
+            req.wait()
+    for d, h in recvs:
+        d.copy_(h)
 
-    def __init__(self, eng, world, rank, device, group=None):
+
+class PlaneExchange:
+    """The exchange step of one rank's engine (torch.distributed group).
+    staged=True moves the regions through host memory (gloo)."""
+
+    def __init__(self, eng, world, rank, device, group=None, staged=False):
         self.eng, self.world, self.rank = eng, world, rank
-        self.device, self.group = device, group
+        self.device, self.group, self.staged = device, group, staged
         self.bytes_sent = 0
 
     def step(self):
         R = self.eng.R
         mine = self.eng.plane_counts()  # synchronises the engine stream
-        t = torch.tensor(mine, dtype=torch.int64, device=self.device)
-        allw = torch.empty(self.world * R * R, dtype=torch.int64,
-                           device=self.device)
+        dev = "cpu" if self.staged else self.device
+        t = torch.tensor(mine, dtype=torch.int64, device=dev)
+        allw = torch.empty(self.world * R * R, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allw, t, group=self.group)
         flat = allw.tolist()
         words = [flat[q * R * R:(q + 1) * R * R] for q in range(self.world)]
         ops = plan(R, self.world, self.rank, words, self.eng.plane_regions)
         self.bytes_sent += sum(n for op, _, (_, n) in ops if op == "send")
-        run_ops(ops, lambda p, n: device_bytes(p, n, self.device), self.group)
+        if self.staged:
+            run_ops_staged(ops, self.device, self.group)
+        else:
+            run_ops(ops, lambda p, n: device_bytes(p, n, self.device),
+                    self.group)
         torch.cuda.current_stream(self.device).synchronize()
