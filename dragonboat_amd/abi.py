@@ -124,7 +124,7 @@ class Config(C.Structure):
                 ("device", C.c_int32), ("save_cap", C.c_uint32),
                 ("total_groups", C.c_uint64), ("place_world", C.c_uint32),
                 ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
-                ("reserved2", C.c_uint32)]
+                ("kv_pool_blocks", C.c_uint32)]
 
 
 class Region(C.Structure):

@@ -156,11 +156,11 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (!is_pow2(cfg->window) || cfg->window < 4 || cfg->window > 65535)
     return DRB_EINVAL;
-  if (cfg->cmd_cap == 0 || cfg->cmd_cap % 16 || cfg->cmd_cap > 64)
-    return DRB_ENOSYS;  // longer inline Cmds are a later round (C5)
+  if (cfg->cmd_cap == 0 || cfg->cmd_cap % 16 || cfg->cmd_cap > 1040)
+    return DRB_ENOSYS;
   if (cfg->mailbox < 4 || cfg->mailbox > MB_MAX) return DRB_EINVAL;
   if (!is_pow2(cfg->kv_slots) || cfg->kv_val_cap == 0 ||
-      cfg->kv_val_cap > 124)
+      cfg->kv_val_cap > 1024)
     return DRB_EINVAL;
   if (cfg->max_props == 0 || cfg->prop_slots == 0 || cfg->ri_slots == 0)
     return DRB_EINVAL;
@@ -201,7 +201,18 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   v.MB = cfg->mailbox;
   v.KS = cfg->kv_slots;
   v.kv_val_cap = cfg->kv_val_cap;
-  v.KVW = 1 + (cfg->kv_val_cap > 4 ? (cfg->kv_val_cap - 4 + 15) / 16 : 0);
+  v.kv_ool = cfg->kv_val_cap > 124;
+  v.KVW = v.kv_ool ? 2
+                   : 1 + (cfg->kv_val_cap > 4 ? (cfg->kv_val_cap - 4 + 15) / 16
+                                              : 0);
+  v.VB = v.kv_ool ? (cfg->kv_val_cap + 15) / 16 : 0;
+  // default: a block for every slot (the pool never runs out before the
+  // table does); large configurations size it to their key count
+  v.kv_pool_blocks =
+      v.kv_ool ? (cfg->kv_pool_blocks ? cfg->kv_pool_blocks
+                                      : std::min<uint64_t>(G * R * v.KS,
+                                                           0xffffffffull))
+               : 0;
   v.max_props = cfg->max_props;
   v.election_rtt = cfg->election_rtt;
   v.heartbeat_rtt = cfg->heartbeat_rtt;
@@ -236,7 +247,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.mbox, 2 * R * R * v.MB * MSG_CHUNKS * G);
   rc |= dalloc(e, &v.mbox_meta, 2 * R * R * G);  // uint4
   rc |= dalloc(e, &v.mbox_maxapp, 2 * R * R * G);
+  rc |= dalloc(e, &v.inbox_tag, 2 * R * G);
   rc |= dalloc(e, &v.kv, R * G * v.KS * v.KVW);
+  if (v.kv_ool) {
+    rc |= dalloc(e, &v.kv_pool, v.kv_pool_blocks * v.VB);
+    rc |= dalloc(e, &v.kv_pool_next, 1);
+  }
   rc |= dalloc(e, &v.props,
                (uint64_t)cfg->prop_slots * v.max_props * (PROP_META + v.C16) *
                    G);
@@ -362,7 +378,8 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
       // the term cache restarts empty: [last+1, last]
       i64.push_back(u64_ix(v, F_TERM_START, s, g));
       d64.push_back(c.last_index + 1);
-      uint32_t w[NUM_U32] = {c.role, c.flags, c.fallback_reason, c.ri_count};
+      uint32_t w[NUM_U32] = {c.role, c.flags & F_PUBLIC, c.fallback_reason,
+                             c.ri_count};
       for (int k = 0; k < NUM_U32; ++k) {
         i32.push_back(u32_ix(v, k, s, g));
         d32.push_back(w[k]);
@@ -437,7 +454,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       o.replica_id = s + 1;
       for (int k = 0; k < NUM_U64_EXPORTED; ++k) *st_u64(&o, k) = d64[a++];
       o.role = d32[b++];
-      o.flags = d32[b++];
+      o.flags = d32[b++] & F_PUBLIC;
       o.fallback_reason = d32[b++];
       o.ri_count = d32[b++];
       for (uint32_t p = 0; p < R; ++p, ++c2) {
@@ -717,32 +734,41 @@ __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
                         ((uint64_t)j << 16));
     uint64_t r1 = mix64(r0), r2 = mix64(r1);
     uint64_t kv_key = r1 % key_space;
-    // Cmd = 00 | 0a 08 <key8 LE> 12 <vlen> <val>
-    uint8_t b[64];
-    for (int q = 0; q < 64; ++q) b[q] = 0;
-    b[0] = 0x00;
-    b[1] = 0x0a;
-    b[2] = 8;
-    for (int q = 0; q < 8; ++q) b[3 + q] = (uint8_t)(kv_key >> (8 * q));
-    b[11] = 0x12;
-    b[12] = (uint8_t)val_len;
+    // Cmd = 00 | 0a 08 <key8 LE> 12 <varint vlen> <val>, built 16 B at a
+    // time; val = the LE64 words of the chain r2, mix64(r2), ...
+    const uint32_t vs = val_len < 128 ? 1 : 2;
+    const uint32_t hdr = 12 + vs, clen = hdr + val_len;
     uint64_t x = r2;
-    for (uint32_t q = 0; q < val_len; ++q) {
-      if (q && (q % 8) == 0) x = mix64(x);
-      b[13 + q] = (uint8_t)(x >> (8 * (q % 8)));
+    uint32_t xi = 0;  // x is chain element xi
+    for (uint32_t c = 0; c < v.C16; ++c) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t t = 0; t < 16; ++t) {
+        const uint32_t q = c * 16 + t;
+        uint32_t b = 0;
+        if (q < hdr) {
+          if (q == 1) b = 0x0a;
+          else if (q == 2) b = 8;
+          else if (q >= 3 && q < 11) b = (uint32_t)(kv_key >> (8 * (q - 3))) & 0xff;
+          else if (q == 11) b = 0x12;
+          else if (q == 12) b = vs == 1 ? val_len : ((val_len & 0x7f) | 0x80);
+          else if (q == 13) b = val_len >> 7;
+        } else if (q < clen) {
+          const uint32_t pv = q - hdr;
+          while (xi < pv / 8) {
+            x = mix64(x);
+            xi++;
+          }
+          b = (uint32_t)(x >> (8 * (pv % 8))) & 0xff;
+        }
+        w[t >> 2] |= b << (8 * (t & 3));
+      }
+      v.props[prop_ix(v, ps, j, PROP_META + c, lane)] =
+          make_uint4(w[0], w[1], w[2], w[3]);
     }
-    uint32_t clen = 13 + val_len;
     v.props[prop_ix(v, ps, j, 0, lane)] = mk4(r0 | 1, cid);
     v.props[prop_ix(v, ps, j, 1, lane)] = mk4(0, 0);
     v.props[prop_ix(v, ps, j, 2, lane)] =
         make_uint4(DRB_ENTRY_ENCODED, clen, 0, 0);
-    for (uint32_t c = 0; c < v.C16; ++c) {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t q = 0; q < 16; ++q)
-        w[q >> 2] |= (uint32_t)b[c * 16 + q] << (8 * (q & 3));
-      v.props[prop_ix(v, ps, j, PROP_META + c, lane)] =
-          make_uint4(w[0], w[1], w[2], w[3]);
-    }
   }
   v.prop_count[(uint64_t)ps * v.G + lane] = k;
 }
@@ -750,9 +776,10 @@ __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
 extern "C" int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
                                     uint32_t key_space, uint32_t val_len,
                                     uint64_t seed, uint64_t salt) {
-  if (!e || slot >= e->cfg.prop_slots || k > e->cfg.max_props || !key_space)
+  if (!e || slot >= e->cfg.prop_slots || k > e->cfg.max_props || !key_space ||
+      val_len > 16383 ||
+      12 + (val_len < 128 ? 1 : 2) + val_len > e->cfg.cmd_cap)
     return DRB_EINVAL;
-  if (13 + val_len > e->cfg.cmd_cap || val_len > 50) return DRB_EINVAL;
   k_gen_kv<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
       e->v, slot, k, key_space, val_len, seed, salt);
   HIPCHK(hipGetLastError());
@@ -900,6 +927,15 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     }
     std::vector<uint4> mv = {cur};
     if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
+    // the receiver's round tag for this sender (idle-round check)
+    {
+      std::vector<uint64_t> ti = {((uint64_t)buf * v.R + to) * v.G + g};
+      std::vector<uint64_t> tv;
+      if (gather(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
+      tv[0] = (tv[0] & ~(0xffull << (8 * from))) |
+              ((uint64_t)(tag & 0xffu) << (8 * from));
+      if (scatter(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
+    }
     acc++;
   }
   if (accepted) *accepted = acc;
@@ -940,8 +976,19 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
   }
-  if (nl) step_kernel<R, true><<<dim3(gx, nl), 256, 0, e->stream>>>(e->v, pl);
-  if (nf) step_kernel<R, false><<<dim3(gx, nf), 256, 0, sf>>>(e->v, pf);
+  // the EXT instantiation only where its paths can run (drb_step.hpp)
+  const bool ext = e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves;
+  if (ext) {
+    if (nl)
+      step_kernel<R, true, true><<<dim3(gx, nl), 256, 0, e->stream>>>(e->v, pl);
+    if (nf) step_kernel<R, false, true><<<dim3(gx, nf), 256, 0, sf>>>(e->v, pf);
+  } else {
+    if (nl)
+      step_kernel<R, true, false><<<dim3(gx, nl), 256, 0, e->stream>>>(e->v,
+                                                                       pl);
+    if (nf)
+      step_kernel<R, false, false><<<dim3(gx, nf), 256, 0, sf>>>(e->v, pf);
+  }
   if (DRB_ROLE_STREAMS) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
@@ -1348,12 +1395,21 @@ static int read_kv_table(drb_engine *e, uint64_t group, uint32_t slot,
   return DRB_OK;
 }
 
-static void slot_value(const View &v, const uint4 *sl, uint8_t *val,
-                       uint32_t vlen) {
+static int slot_value(drb_engine *e, const uint4 *sl, uint8_t *val,
+                      uint32_t vlen) {
+  const View &v = e->v;
+  if (v.kv_ool) {  // the key's value block
+    if (sl[1].x >= v.kv_pool_blocks) return DRB_EDEVICE;
+    HIPCHK(hipMemcpyAsync(val, v.kv_pool + (uint64_t)sl[1].x * v.VB, vlen,
+                          hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return DRB_OK;
+  }
   uint8_t tmp[16 * 9];
   memcpy(tmp, &sl[0].w, 4);
   for (uint32_t c = 1; c < v.KVW; ++c) memcpy(tmp + 4 + (c - 1) * 16, &sl[c], 16);
   memcpy(val, tmp, vlen);
+  return DRB_OK;
 }
 
 extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
@@ -1381,8 +1437,7 @@ extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
     if (klen == key_len && lo64h(sl[0]) == k8) {
       if (val_len) *val_len = vlen;
       if (vlen > val_cap) return DRB_ERANGE;
-      slot_value(v, sl, val, vlen);
-      return DRB_OK;
+      return slot_value(e, sl, val, vlen);
     }
     ks = (ks + 1) & (v.KS - 1);
   }
@@ -1406,7 +1461,7 @@ extern "C" int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot,
       uint64_t k8 = lo64h(sl[0]);
       for (uint32_t i = 0; i < 8; ++i) keys[n * 8 + i] = (uint8_t)(k8 >> (8 * i));
       key_lens[n] = klen;
-      slot_value(v, sl, vals + n * v.kv_val_cap, vlen);
+      if (int rc = slot_value(e, sl, vals + n * v.kv_val_cap, vlen)) return rc;
       val_lens[n] = vlen;
     }
     n++;

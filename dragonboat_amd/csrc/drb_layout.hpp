@@ -57,6 +57,10 @@ constexpr int NUM_U64_EXPORTED = F_RING_LO;
 // per-replica u32 fields, array [F][slot][g]
 enum U32Field : int { W_ROLE = 0, W_FLAGS, W_FB_REASON, W_RI_COUNT, NUM_U32 };
 
+// internal W_FLAGS bits (masked out of drb_replica_state.flags)
+constexpr uint32_t F_AT_REST = 1u << 16;  // a round without input is a no-op
+constexpr uint32_t F_PUBLIC = 0xffffu;
+
 // message record: 1-2 x uint4 (drb_msg.hpp)
 constexpr int MSG_CHUNKS = 2;
 // entry meta in the ring: 3 x uint4 = 48 B (+ cmd_cap bytes of Cmd)
@@ -95,8 +99,16 @@ struct View {
   uint4 *ring;            // [R][W][ENT_META + C16][G]
   uint4 *mbox;            // [2][R*R][MB][MSG_CHUNKS][G]
   uint4 *mbox_meta;       // [2][R(from)][R(to)][G] {tag, info, term}
+  uint64_t *inbox_tag;    // [2][R(to)][G]: byte `from` = round & 0xff of
+                          // the sender's last records to this replica
   uint64_t *mbox_maxapp;  // [2][R][R][G] max LogIndex+n of the Replicates
   uint4 *kv;              // [R][G][KS][KVW]
+  // out-of-line values (kv_val_cap > 124): slot = {key8, meta, val0} +
+  // {block}, the value in block chunks [VB] of kv_pool
+  uint4 *kv_pool;
+  unsigned long long *kv_pool_next;  // bump allocator
+  uint64_t kv_pool_blocks;
+  uint32_t kv_ool, VB;
   uint4 *props;           // [P][max_props][PROP_META + C16][G]
   uint32_t *prop_count;   // [P][G]
   uint4 *ri_in;           // [RS][G] {low, high}

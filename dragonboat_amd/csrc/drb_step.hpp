@@ -748,10 +748,83 @@ DRB_DEV uint32_t byte_mask(uint32_t n) {  // low n (<= 4) bytes
   return n >= 4 ? 0xffffffffu : ((1u << (8 * n)) - 1u);
 }
 
+// 16 bytes at byte offset s (0..15) of the 32-byte window q0 || q1
+DRB_DEV uint32_t sel8(uint32_t i, uint4 a, uint4 b) {
+  return sel(i & 4, sel4(i, b), sel4(i, a));
+}
+DRB_DEV uint4 extract16(uint4 q0, uint4 q1, uint32_t s) {
+  const uint32_t w = s >> 2, sh = 8 * (s & 3);
+  uint32_t o[4];
+#pragma unroll
+  for (uint32_t t = 0; t < 4; ++t) {
+    const uint32_t a = sel8(w + t, q0, q1);
+    const uint32_t b = sel8(w + t + 1, q0, q1);  // w + t + 1 <= 7
+    o[t] = sh ? (a >> sh) | (b << (32 - sh)) : a;
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+// keep the low n (0..16) bytes of q
+DRB_DEV uint4 mask16(uint4 q, uint32_t n) {
+  return make_uint4(q.x & byte_mask(n), q.y & byte_mask(n > 4 ? n - 4 : 0),
+                    q.z & byte_mask(n > 8 ? n - 8 : 0),
+                    q.w & byte_mask(n > 12 ? n - 12 : 0));
+}
+
+// value bytes [16 c + base, 16 c + base + 16) of an entry's PBKV value at
+// Cmd offset voff: two ring chunks and a byte shift
+DRB_DEV uint4 value_chunk(const Lane &L, uint64_t index, uint32_t voff,
+                          uint32_t vlen, uint32_t base, uint32_t c) {
+  const View &v = *L.v;
+  const uint32_t o = voff + base + 16 * c;  // Cmd byte offset
+  const uint32_t q = o >> 4;
+  const uint4 q0 = v.ring[ring_ix(v, L.slot, index, ENT_META + q, L.g)];
+  const uint4 q1 = q + 1 < v.C16
+                       ? v.ring[ring_ix(v, L.slot, index, ENT_META + q + 1, L.g)]
+                       : make_uint4(0, 0, 0, 0);
+  const uint32_t have = vlen > base + 16 * c ? vlen - base - 16 * c : 0;
+  return mask16(extract16(q0, q1, o & 15), have > 16 ? 16 : have);
+}
+
+// Values of longer Cmds (C5's 128 B / 1 KB payloads), read 16 B at a time
+// from the resident window: into the slot's following chunks (inline) or
+// into the key's value block (out of line, allocated on insert).  Only the
+// EXT instantiation of the step kernel carries this path.
+DRB_DEV bool put_value_long(const View &v, uint32_t slot,
+                                            uint64_t g, uint64_t index,
+                                            uint4 *sl, bool hit,
+                                            uint32_t voff, uint32_t vlen) {
+  Lane L;
+  L.v = &v;
+  L.slot = slot;
+  L.g = g;
+  if (v.kv_ool) {
+    uint32_t blk;
+    if (hit) {
+      blk = sl[1].x;
+    } else {
+      const uint64_t b = atomicAdd(v.kv_pool_next, 1ull);
+      if (b >= v.kv_pool_blocks) return false;
+      blk = (uint32_t)b;
+      sl[1] = make_uint4(blk, 0, 0, 0);
+    }
+    uint4 *dst = v.kv_pool + (uint64_t)blk * v.VB;
+    for (uint32_t c = 0; c * 16 < vlen; ++c)
+      dst[c] = value_chunk(L, index, voff, vlen, 0, c);
+  } else {
+    for (uint32_t c = 1; c < v.KVW; ++c)
+      sl[c] = value_chunk(L, index, voff, vlen, 4, c - 1);
+  }
+  return true;
+}
+
 // handleEntry (statemachine.go:935-969) -> update (1057-1103) ->
 // GetPayload (encoded.go:55-65) -> KVTest.Update (kvtest.go:145-162).
 // Returns: 0 noop applied, 1 KV updated, -1 not on the fast path.
-template <int R>
+// The PBKV header is parsed from the Cmd's first 64 bytes (registers); the
+// value is copied 16 B at a time straight from the window into the slot
+// (inline values) or the slot's value block (out-of-line, kv_val_cap >
+// 124: 128 B / 1 KB payloads).
+template <int R, bool EXT>
 DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   const View &v = *L.v;
   uint4 m0 = v.ring[ring_ix(v, L.slot, index, 0, L.g)];
@@ -769,7 +842,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
     return 0;
   }
   if (series_id != 0) return -1;  // sessions stay on the CPU path
-  // the Cmd, staged in registers (cmd_cap <= 64 B on this path: C16 <= 4)
+  // the Cmd's first 64 bytes in registers: the PBKV header lies there
   Cmd4 cmd;
   cmd.c0 = v.ring[ring_ix(v, L.slot, index, ENT_META, L.g)];
   cmd.c1 = cmd.c2 = cmd.c3 = make_uint4(0, 0, 0, 0);
@@ -786,20 +859,27 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   } else if (type != DRB_ENTRY_APPLICATION) {
     return -1;
   }
-  // PBKV.Unmarshal (kvpb/kv.go:76-283) restricted to single-byte varints
+  // PBKV.Unmarshal (kvpb/kv.go:76-283): fields 1 (key) and 2 (value),
+  // lengths as varints of up to two bytes, headers inside the first 64 B
   uint64_t key8 = 0;
   uint32_t klen = 0, voff = 0, vlen = 0;
   bool have_k = false, have_v = false;
   uint32_t i = 0;
   while (i < plen) {
+    if (off + i + 3 > 64) return -1;
     uint32_t tag = cmd_byte(cmd, off + i);
     if (i + 1 >= plen) return -1;
-    uint32_t l = cmd_byte(cmd, off + i + 1);
-    if (l >= 0x80) return -1;
-    if (i + 2 + l > plen) return -1;
+    uint32_t l = cmd_byte(cmd, off + i + 1), hl = 2;
+    if (l >= 0x80) {
+      const uint32_t b2 = cmd_byte(cmd, off + i + 2);
+      if (b2 >= 0x80 || i + 2 >= plen) return -1;
+      l = (l & 0x7f) | (b2 << 7);
+      hl = 3;
+    }
+    if (i + hl + l > plen) return -1;
     if (tag == 0x0a) {
-      if (l > 8) return -1;
-      const uint32_t ko = off + i + 2;
+      if (l > 8 || off + i + hl + l > 64) return -1;
+      const uint32_t ko = off + i + hl;
       key8 = (uint64_t)(cmd_u32_at(cmd, ko) & byte_mask(l)) |
              ((uint64_t)(cmd_u32_at(cmd, ko + 4) &
                          byte_mask(l > 4 ? l - 4 : 0)) << 32);
@@ -807,15 +887,20 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       have_k = true;
     } else if (tag == 0x12) {
       if (l > v.kv_val_cap) return -1;
-      voff = off + i + 2;
+      voff = off + i + hl;
       vlen = l;
       have_v = true;
     } else {
       return -1;
     }
-    i += 2 + l;
+    i += hl + l;
   }
   if (!have_k || !have_v) return -1;
+  // the value's first 4 bytes (kept in the slot header word either way)
+  const uint32_t w0 =
+      (!EXT || voff + 4 <= 64 ? cmd_u32_at(cmd, voff)
+                              : value_chunk(L, index, voff, vlen, 0, 0).x) &
+      byte_mask(vlen);
   // open-addressing upsert into this replica's table
   uint32_t mask = v.KS - 1;
   uint32_t ks = (uint32_t)kv_hash(key8, klen) & mask;
@@ -827,21 +912,26 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
     uint32_t sklen = h.z & 0xffu;
     bool hit = used && sklen == klen && lo64(h) == key8;
     if (!used || hit) {
-      // value bytes: first 4 in h.w, the rest in the following chunks
-      const uint32_t w0 = cmd_u32_at(cmd, voff) & byte_mask(vlen);
+      if (!EXT) {
+        // inline value of a Cmd inside the 64 B register window: bytes 4..
+        // in the slot's following chunks
+        for (uint32_t c = 1; c < v.KVW; ++c) {
+          uint32_t wv[4];
+#pragma unroll
+          for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t src = 4 + (c - 1) * 16 + 4 * t;  // value byte
+            wv[t] = src < vlen ? cmd_u32_at(cmd, voff + src) &
+                                     byte_mask(vlen - src)
+                               : 0u;
+          }
+          sl[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+      } else if (!put_value_long(v, L.slot, L.g, index, sl, hit, voff,
+                                 vlen)) {
+        return -1;  // value pool exhausted
+      }
       sl[0] = make_uint4((uint32_t)key8, (uint32_t)(key8 >> 32),
                          (1u << 31) | (vlen << 8) | klen, w0);
-      for (uint32_t c = 1; c < v.KVW; ++c) {
-        uint32_t wv[4];
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) {
-          const uint32_t src = 4 + (c - 1) * 16 + 4 * t;  // value byte
-          wv[t] = src < vlen ? cmd_u32_at(cmd, voff + src) &
-                                   byte_mask(vlen - src)
-                             : 0u;
-        }
-        sl[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      }
       r.kv_added++;
       r.sm_index = index;
       r.sm_term = term;
@@ -1191,7 +1281,9 @@ DRB_DEV void block_plane_summary(const View &v, uint32_t from, uint32_t to,
 // round t's, so the two launches of a round are independent; compiling the
 // roles apart keeps each one's register footprint (and so its occupancy)
 // to what its own handlers need.
-template <int R, bool LEAD>
+// EXT: the instantiation for Cmds longer than 64 B, out-of-line values or
+// encode_saves (C5); the other one keeps the common path lean
+template <int R, bool LEAD, bool EXT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_LEAD_WAVES : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
@@ -1206,7 +1298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
   __shared__ uint64_t elo_lds[LEAD ? R : 1][256];
-  if (p.encode_saves) {  // uniform: every thread reaches the barrier
+  if (EXT && p.encode_saves) {  // uniform: every thread reaches the barrier
     crc32_table_init(crc_tab, threadIdx.x);
     __syncthreads();
   }
@@ -1236,6 +1328,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
     v.rtr_count[ix(v, slot, g)] = 0;
     if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
     active = false;
+  }
+  // Idle rounds: a replica at rest -- its last round left
+  // nothing pending, see the end of the round -- whose round brings no
+  // input changes nothing (node.stepNode finds no event, node.go:1139-1159):
+  // no tick, no staged proposal or ReadIndex, and no record from a
+  // co-resident sender, which the senders' one-byte round tags tell
+  // without reading the mailbox headers.  Its round outputs are already
+  // empty (a round that produced any does not leave the replica at rest).
+  if (active && !p.tick && (flags & F_AT_REST) && !v.remote_mask) {
+    const uint64_t tags = v.inbox_tag[((uint64_t)L.rbuf * v.R + slot) * v.G + g];
+    const uint32_t want = (uint32_t)(p.round - 1) & 0xffu;
+    bool input = false;
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+      if ((uint32_t)s != slot && ((tags >> (8 * s)) & 0xffu) == want)
+        input = true;
+    if (LEAD && (v.place_world <= 1 || slot == v.stage_slot)) {
+      if (p.prop_slot != DRB_NONE &&
+          v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
+        input = true;
+      if (p.ri_slot != DRB_NONE && v.ri_in[(uint64_t)p.ri_slot * v.G + g].x |
+                                       v.ri_in[(uint64_t)p.ri_slot * v.G + g].y)
+        input = true;
+    }
+    if (!input) active = false;
   }
   if (active) {
     Rep<R> r;
@@ -1526,7 +1643,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         if (confirmed_index != r.applied_index)
           st_f(L, F_CONFIRMED_INDEX, r.applied_index);
         // SaveRaftState (engine.go:1343) of EntriesToSave
-        if (has_save && p.encode_saves)
+        if (EXT && has_save && p.encode_saves)
           encode_saves(L, r, save_lo, r.last, crc_tab, c_saved,
                        c_saved_bytes);
         // Peer.Commit -> entryLog.commitUpdate (logentry.go:351-371)
@@ -1549,7 +1666,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       if (apply_hi >= apply_lo && apply_lo != 0 && !(DRB_ABLATE & 1)) {
         uint64_t from = umax64(apply_lo, r.sm_index + 1);
         for (uint64_t idx = from; idx <= apply_hi; ++idx) {
-          int rc = apply_entry(L, r, idx);
+          int rc = apply_entry<R, EXT>(L, r, idx);
           if (rc < 0) {
             // the rsm apply of this replica leaves the fast path at idx;
             // the raft round itself completed
@@ -1590,6 +1707,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         r.flags |= DRB_F_ERROR;
         c_err = 1;
       }
+      // at rest: with no input the next round would change nothing --
+      // updateAppliedIndex finds applied == sm index, nothing to apply, no
+      // Replicate in flight to guard, and no round output to clear
+      const bool rest = r.sm_index == r.applied_index &&
+                        r.committed == r.processed && r.guard_new == ~0ull &&
+                        r.nrtr == 0 && !has_save &&
+                        !(r.flags & (DRB_F_FALLBACK | DRB_F_ERROR));
+      r.flags = rest ? (r.flags | F_AT_REST) : (r.flags & ~F_AT_REST);
       store_rep<R, LEAD>(L, r, flags0, fb0);
       c_msgs = r.nmsgs;
       c_rtr = r.nrtr;
@@ -1605,6 +1730,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         meta.x = (uint32_t)p.round;
         meta.y = w;
         v.mbox_meta[mmeta_ix(v, L.wbuf, slot, (uint32_t)s, g)] = meta;
+        // the receiver's round tag byte for this sender (a byte store: the
+        // other senders own the other bytes of the word)
+        ((uint8_t *)&v.inbox_tag[((uint64_t)L.wbuf * v.R + s) * v.G + g])
+            [slot] = (uint8_t)p.round;
       }
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;

@@ -113,7 +113,8 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 cmd_cap=32, max_props=4, prop_slots=2, ri_slots=2,
                 mailbox=13, kv_slots=512, kv_val_cap=4, election_rtt=10,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
-                total_groups=0, place_world=1, place_rank=0, entry_mbox=0)
+                total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
+                kv_pool_blocks=0)
 
 
 class Engine:
@@ -130,7 +131,7 @@ class Engine:
                    cfg["election_rtt"], cfg["heartbeat_rtt"],
                    cfg["check_quorum"], cfg["device"], cfg["save_cap"],
                    cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
-                   cfg["entry_mbox"], 0)
+                   cfg["entry_mbox"], cfg["kv_pool_blocks"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")

@@ -36,8 +36,19 @@ def client_id(seed, g):
     return mix64(seed ^ CLIENT ^ g) | 1
 
 
+def varint(n):
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7f) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
 def pbkv16(key8, val):
-    return b"\x0a" + bytes([len(key8)]) + key8 + b"\x12" + bytes([len(val)]) \
+    """PBKV{Key, Val} (internal/tests/kvpb/kv.go) -- 16 B at the default
+    4-byte value; longer values take a multi-byte length varint."""
+    return b"\x0a" + varint(len(key8)) + key8 + b"\x12" + varint(len(val)) \
         + val
 
 

@@ -243,13 +243,15 @@ typedef struct drb_config {
   uint64_t first_shard_id;   /* ShardID of group g = first_shard_id + g */
   uint32_t num_replicas;     /* R, 1..DRB_MAX_REPLICAS; replica IDs 1..R */
   uint32_t window;           /* W resident entries per replica (power of 2) */
-  uint32_t cmd_cap;          /* max Cmd bytes per resident entry (mult. of 16) */
+  uint32_t cmd_cap;          /* max Cmd bytes per resident entry (mult. of
+                              * 16, <= 1040) */
   uint32_t max_props;        /* max proposals per group per round */
   uint32_t prop_slots;       /* staged proposal batches */
   uint32_t ri_slots;         /* staged ReadIndex batches */
   uint32_t mailbox;          /* records per (sender, receiver) per round, 4..13 */
   uint32_t kv_slots;         /* KV open-addressing slots per replica (pow2) */
-  uint32_t kv_val_cap;       /* max value bytes stored inline per KV slot */
+  uint32_t kv_val_cap;       /* max value bytes per KV slot (<= 124 inline,
+                              * else out of line, <= 1024) */
   uint32_t election_rtt;     /* Config.ElectionRTT */
   uint32_t heartbeat_rtt;    /* Config.HeartbeatRTT */
   uint32_t check_quorum;     /* Config.CheckQuorum */
@@ -267,7 +269,10 @@ typedef struct drb_config {
   uint32_t place_rank;
   uint32_t entry_mbox;       /* entries per remote (sender, receiver) and
                               * round that travel by value (N >= 2) */
-  uint32_t reserved2;
+  /* kv_val_cap > 124 keeps values out of line (C5: 128 B / 1 KB
+   * payloads) in a pool of this many value blocks (0: one per KV slot);
+   * a replica whose apply finds the pool empty falls back */
+  uint32_t kv_pool_blocks;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */

@@ -212,3 +212,55 @@ def test_replicas_spread_over_ranks_c4(N, R, G):
              o.ready_to_reads), (r, e, o.to_dict())
         errs = p.check()
         assert not errs, (r, errs[:3])
+
+
+def _long_payload_rounds(p, val_len, rounds=8, encode=False, device_gen=False):
+    from dragonboat_amd import workload
+    for r in range(rounds):
+        k = 1 if r % 4 != 3 else 2
+        if device_gen:  # the bench's on-device generator, same definition
+            counts, ents, pool = workload.build_batch(p.G, k, p.seed, r, 256,
+                                                      val_len)
+            p.orc.stage_proposals(counts, k, ents, pool)
+            p.eng.gen_kv_proposals(0, k, 256, val_len, p.seed, r)
+            o = p.orc.round(tick=(r % 2 == 0))
+            e = p.eng.step(tick=(r % 2 == 0), prop_slot=0,
+                           encode_saves=encode)
+            p.rounds += 1
+        else:
+            o, e = p.round(k=k, tick=(r % 2 == 0), read_index=(r % 3 == 0),
+                           val_len=val_len, encode_saves=encode)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        assert (e.committed_entries, e.applied_entries, e.messages) == \
+            (o.committed_entries, o.applied_entries, o.messages), r
+        errs = p.check()
+        assert not errs, (r, errs[:2])
+        if encode:
+            assert not p.check_saves(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("val_len,cmd_cap,val_cap", [
+    (116, 144, 124),     # C5 128 B payload, value inline (9-chunk slots)
+    (116, 144, 128),     # the same value out of line
+    (1011, 1040, 1024),  # C5 1 KB payload, out of line
+    (60, 80, 64)])       # a value crossing the 64 B header window, inline
+def test_long_payloads_kv_apply(val_len, cmd_cap, val_cap):
+    """SURVEY 8d C5 payloads: PBKV values of 116 / 1011 bytes (2-byte
+    length varint), applied from the resident window 16 B at a time into
+    inline slots or out-of-line value blocks; bit-exact KV, logs and the
+    EntryBatch + CRC of every round's EntriesToSave."""
+    p = Pair(G=24, R=3, cmd_cap=cmd_cap, kv_val_cap=val_cap, kv_slots=64,
+             max_props=4, save_cap=8192)
+    _long_payload_rounds(p, val_len, encode=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("val_len,cmd_cap,val_cap", [(4, 32, 4),
+                                                     (1011, 1040, 1024)])
+def test_device_generator_matches_workload(val_len, cmd_cap, val_cap):
+    """drb_gen_kv_proposals (what bench.py stages) builds exactly the
+    proposals of dragonboat_amd/workload.py (the SURVEY 8d definition)."""
+    p = Pair(G=40, R=3, cmd_cap=cmd_cap, kv_val_cap=val_cap, kv_slots=64,
+             max_props=4)
+    _long_payload_rounds(p, val_len, rounds=5, device_gen=True)
