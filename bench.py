@@ -62,11 +62,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c4"],
+    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
                     help="c3: groups sharded over GPUs, replicas "
                          "co-resident (BASELINE metric); c4: --groups "
                          "groups in total, replica slot s of group g on "
-                         "GPU (g + s) mod N, planes exchanged over RCCL")
+                         "GPU (g + s) mod N, planes exchanged over RCCL; "
+                         "c5: 4M groups per GPU, --active-ppm of them "
+                         "proposing --payload byte entries per round, "
+                         "EntriesToSave encoded as EntryBatch + CRC32")
+    ap.add_argument("--payload", type=int, default=128, choices=[128, 1024],
+                    help="c5 entry payload (PBKV value 116 / 1011 B)")
+    ap.add_argument("--active-ppm", type=int, default=10000,
+                    help="c5: groups proposing per round, per million")
     ap.add_argument("--groups", type=int, default=1 << 20,
                     help="groups per GPU (c3) / in total (c4)")
     ap.add_argument("--replicas", type=int, default=0,
@@ -85,6 +92,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
+
+
+C5_VAL = {128: 116, 1024: 1011}
 
 
 def cpu_baseline(args, seconds):
@@ -107,7 +117,13 @@ def cpu_baseline(args, seconds):
     t_start = time.perf_counter()
     t_run = 0.0
     while time.perf_counter() - t_start < seconds:
-        counts, ents, pool = workload.build_batch(G, args.k, seed, rounds)
+        if args.workload == "c5":
+            act = workload.active_groups(G, seed, rounds, args.active_ppm)
+            counts, ents, pool = workload.build_batch(
+                G, args.k, seed, rounds, 256, C5_VAL[args.payload], act)
+        else:
+            counts, ents, pool = workload.build_batch(G, args.k, seed,
+                                                      rounds)
         c.stage_proposals(counts, args.k, ents, pool)
         if not args.no_read_index:
             lo, hi = workload.build_read_index(G, seed, rounds, rounds + 30)
@@ -157,8 +173,13 @@ def main():
     torch.cuda.set_device(local)
     from dragonboat_amd.engine import Engine
     c4 = args.workload == "c4"
+    c5 = args.workload == "c5"
     if not args.replicas:
         args.replicas = 5 if c4 else 3
+    if c5:
+        args.no_read_index = True  # writes, no reads
+        if args.groups == 1 << 20:
+            args.groups = 4 << 20
     G, R, k = args.groups, args.replicas, args.k
     if c4:
         args.no_read_index = True  # 16 B writes, k_w = 1
@@ -176,6 +197,18 @@ def main():
         if world > 1:
             from dragonboat_amd.exchange import PlaneExchange
             xch = PlaneExchange(eng, world, rank, torch.device("cuda", local))
+    elif c5:  # 128 B / 1 KB entries, values out of line, saves encoded
+        first_shard, seed = ddist.shard_plan(rank, G)
+        vlen = C5_VAL[args.payload]
+        cmd_cap = ((12 + (1 if vlen < 128 else 2) + vlen) + 15) // 16 * 16
+        NP = 8 if args.payload == 128 else 4
+        bound = 73 + cmd_cap  # EntryBatch element bound (drb_codec.hpp)
+        eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
+                     max_props=max(1, k), prop_slots=NP, ri_slots=1,
+                     mailbox=6, kv_slots=16, kv_val_cap=vlen + 13 & ~15,
+                     kv_pool_blocks=2 * G * R if args.payload == 128
+                     else G * R, save_cap=(4 * bound + 15) // 16 * 16,
+                     first_shard_id=first_shard, device=local)
     else:
         first_shard, seed = ddist.shard_plan(rank, G)
         eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
@@ -184,6 +217,10 @@ def main():
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
+        if c5:
+            eng.gen_kv_proposals(b, k, 256, C5_VAL[args.payload], seed, b,
+                                 active_ppm=args.active_ppm)
+            continue
         eng.gen_kv_proposals(b, k, 256, 4, seed, b)
         eng.gen_read_index(b, seed, b + 30)
     stream = torch.cuda.ExternalStream(eng.stream)
@@ -198,7 +235,7 @@ def main():
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF,
                        reads_per_ctx=READS_PER_CTX if fused else 0,
-                       key_space=KEY_SPACE)
+                       key_space=KEY_SPACE, encode_saves=c5)
         if reads and not fused:
             eng.serve_reads(READS_PER_CTX, KEY_SPACE)
         if xch is not None:  # C4: this round's cross-GPU planes
@@ -246,14 +283,32 @@ def main():
     # algorithmic bytes of one round on this GPU (its groups; C4: its
     # share of the global groups, plus the message bytes it moves)
     g_here = G if not c4 else (G + world - 1) // world
-    alg = alg_bytes_per_group_round(R, k, 16, reads, c4 and world > 1) * \
-        g_here
+    if c5:  # per committed entry: the round's work for its group plus the
+        # EntryBatch bytes of R replicas, written and read by the CRC
+        P = args.payload
+        per = alg_bytes_per_group_round(R, k, P, False) / k + \
+            2 * R * (P + 30)
+        alg = per * out.committed_entries / K
+    else:
+        alg = alg_bytes_per_group_round(R, k, 16, reads, c4 and world > 1) * \
+            g_here
     achieved = alg / (kern_ms * 1e-3) / 1e9
     if out.fallbacks or out.errors:
         print("WARNING: fallbacks=%d errors=%d" % (out.fallbacks, out.errors),
               file=sys.stderr)
     if rank == 0:
-        if c4:
+        if c5:
+            metric = ("committed entries/sec (node) at %d 3-replica groups, "
+                      "%d B payload, %g %% active per round, EntryBatch + "
+                      "CRC32 of EntriesToSave; %%HBM BW" % (
+                          G, args.payload, args.active_ppm / 1e4))
+            wl = ("C5: %d groups x %d replicas per GPU, %d B PBKV writes "
+                  "(values out of line), %d ppm of the groups proposing per "
+                  "round, EntriesToSave encoded (EntryBatch + CRC32), tick "
+                  "every %d round(s); Quiesce off" % (
+                      G, R, args.payload, args.active_ppm, args.tick_every))
+            par = "groups sharded, replicas co-resident"
+        elif c4:
             metric = ("committed entries/sec (node) at %d 5-replica groups "
                       "spread over %d GPU(s), 16B payload; %%HBM BW" % (
                           G, world))
@@ -284,7 +339,8 @@ def main():
             "scaling": "strong" if c4 else "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (SURVEY 8d seeded PBKV writes + ReadIndex)",
+            "data": "synthetic (SURVEY 8d seeded PBKV writes%s)" % (
+                " + ReadIndex" if reads else ""),
             "config": {
                 "workload": wl,
                 "groups_per_gpu": g_here, "replicas": R,
@@ -292,7 +348,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None if c4 else pmc_traffic(G, R),
+                "traffic": None if (c4 or c5) else pmc_traffic(G, R),
                 "traffic_source": "profiles/pmc_current.json (rocprofv3 "
                                   "FETCH_SIZE x2 + WRITE_SIZE, bytes per "
                                   "round)",
@@ -303,7 +359,9 @@ def main():
                          "ready_to_reads": out.ready_to_reads,
                          "reads_served": out.reads_served,
                          "reads_deferred": out.reads_deferred,
-                         "fallbacks": out.fallbacks, "errors": out.errors},
+                         "fallbacks": out.fallbacks, "errors": out.errors,
+                         "saved_entries": out.saved_entries,
+                         "saved_bytes": out.saved_bytes},
         }
         if xch is not None:
             res["exchange"] = {"bytes_sent_per_round_rank0":

@@ -723,11 +723,20 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
 }
 
 // SURVEY 8(d) synthetic writes; bit-identical to dragonboat_amd/workload.py
+constexpr uint64_t ACTIVE_SALT = 0xAC71BE5EAC71BE5Eull;
+
 __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
-                         uint32_t val_len, uint64_t seed, uint64_t salt) {
+                         uint32_t val_len, uint64_t seed, uint64_t salt,
+                         uint32_t active_ppm) {
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= v.G) return;
   const uint64_t g = gid(v, v.stage_slot, lane);  // the seeded group
+  if (active_ppm < 1000000u &&
+      mix64(seed ^ ACTIVE_SALT ^ (g * 0x9E3779B97F4A7C15ull) ^ (salt << 24)) %
+              1000000u >= active_ppm) {
+    v.prop_count[(uint64_t)ps * v.G + lane] = 0;
+    return;
+  }
   const uint64_t cid = mix64(seed ^ 0xC11E47C11E47C11Eull ^ g) | 1;
   for (uint32_t j = 0; j < k; ++j) {
     uint64_t r0 = mix64(seed ^ (g * 0x9E3779B97F4A7C15ull) ^ (salt << 32) ^
@@ -773,18 +782,26 @@ __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
   v.prop_count[(uint64_t)ps * v.G + lane] = k;
 }
 
-extern "C" int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
-                                    uint32_t key_space, uint32_t val_len,
-                                    uint64_t seed, uint64_t salt) {
+extern "C" int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot,
+                                           uint32_t k, uint32_t key_space,
+                                           uint32_t val_len, uint64_t seed,
+                                           uint64_t salt, uint32_t active_ppm) {
   if (!e || slot >= e->cfg.prop_slots || k > e->cfg.max_props || !key_space ||
       val_len > 16383 ||
       12 + (val_len < 128 ? 1 : 2) + val_len > e->cfg.cmd_cap)
     return DRB_EINVAL;
   k_gen_kv<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
-      e->v, slot, k, key_space, val_len, seed, salt);
+      e->v, slot, k, key_space, val_len, seed, salt, active_ppm);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(e->stream));
   return DRB_OK;
+}
+
+extern "C" int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
+                                    uint32_t key_space, uint32_t val_len,
+                                    uint64_t seed, uint64_t salt) {
+  return drb_gen_kv_proposals_active(e, slot, k, key_space, val_len, seed,
+                                     salt, 1000000u);
 }
 
 extern "C" int drb_stage_read_index(drb_engine *e, uint32_t slot,

@@ -43,6 +43,8 @@ SIGNATURES = {
     "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
     "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
+    "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
+                                              U64, U32]),
     "drb_stage_read_index": (C.c_int, [P, U32, PU64, PU64]),
     "drb_gen_read_index": (C.c_int, [P, U32, U64, U64]),
     "drb_ingest": (C.c_int, [P, C.POINTER(Message), SZ, C.POINTER(Entry),
@@ -203,9 +205,12 @@ class Engine:
         _ck(lib().drb_stage_proposals(self.h, slot, counts, ents, pool),
             "drb_stage_proposals")
 
-    def gen_kv_proposals(self, slot, k, key_space, val_len, seed, salt):
-        _ck(lib().drb_gen_kv_proposals(self.h, slot, k, key_space, val_len,
-                                       seed, salt), "drb_gen_kv_proposals")
+    def gen_kv_proposals(self, slot, k, key_space, val_len, seed, salt,
+                         active_ppm=1000000):
+        _ck(lib().drb_gen_kv_proposals_active(self.h, slot, k, key_space,
+                                              val_len, seed, salt,
+                                              active_ppm),
+            "drb_gen_kv_proposals_active")
 
     def stage_read_index(self, slot, low, high):
         _ck(lib().drb_stage_read_index(self.h, slot, low, high),

@@ -23,6 +23,7 @@ MASK = (1 << 64) - 1
 GOLDEN = 0x9E3779B97F4A7C15
 CLIENT = 0xC11E47C11E47C11E
 RI_SALT = 0x5EAD1DE85EAD1DE8
+ACTIVE_SALT = 0xAC71BE5EAC71BE5E
 
 
 def mix64(z):
@@ -99,3 +100,13 @@ def build_read_index(num_groups, seed, salt, high, groups=None):
     for g in gs:
         lo[g], hi[g] = read_index_ctx(seed, g, salt, high)
     return lo, hi
+
+
+def active_groups(num_groups, seed, salt, active_ppm):
+    """The seeded Bernoulli subset of groups that propose in batch `salt`
+    (drb_gen_kv_proposals_active; SURVEY 8d C5: 1 % active per round)."""
+    if active_ppm >= 1000000:
+        return list(range(num_groups))
+    return [g for g in range(num_groups)
+            if mix64(seed ^ ACTIVE_SALT ^ ((g * GOLDEN) & MASK) ^
+                     ((salt << 24) & MASK)) % 1000000 < active_ppm]

@@ -362,6 +362,13 @@ int drb_stage_proposals(drb_engine *e, uint32_t slot, const uint32_t *counts,
 int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
                          uint32_t key_space, uint32_t val_len, uint64_t seed,
                          uint64_t salt);
+/* The same for a seeded Bernoulli subset of the groups (C5: 1 % active
+ * per round): group g proposes in batch `salt` iff
+ * mix64(seed ^ ACTIVE ^ g * GOLDEN ^ salt << 24) % 1000000 < active_ppm. */
+int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot, uint32_t k,
+                                uint32_t key_space, uint32_t val_len,
+                                uint64_t seed, uint64_t salt,
+                                uint32_t active_ppm);
 /* Stage one ReadIndex ctx per group (ctx_low[g] == 0: none).  Replaces
  * pendingReadIndex.read + node.handleReadIndex (request.go:845,
  * node.go:1296). */

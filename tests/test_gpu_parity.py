@@ -264,3 +264,33 @@ def test_device_generator_matches_workload(val_len, cmd_cap, val_cap):
     p = Pair(G=40, R=3, cmd_cap=cmd_cap, kv_val_cap=val_cap, kv_slots=64,
              max_props=4)
     _long_payload_rounds(p, val_len, rounds=5, device_gen=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("val_len,cmd_cap,val_cap", [(116, 144, 128),
+                                                     (1011, 1040, 1024)])
+def test_c5_sparse_activity_idle_rounds(val_len, cmd_cap, val_cap):
+    """C5 in miniature: a seeded 10 % of the groups propose per round
+    (drb_gen_kv_proposals_active), 128 B / 1 KB payloads, EntriesToSave
+    encoded with CRC, ticks only every 4th round -- replicas at rest skip
+    the idle rounds; state, logs, KV, messages and saves stay bit-exact."""
+    from dragonboat_amd import workload
+    p = Pair(G=64, R=3, cmd_cap=cmd_cap, kv_val_cap=val_cap, kv_slots=32,
+             max_props=2, save_cap=8192, prop_slots=2)
+    for r in range(16):
+        act = workload.active_groups(p.G, p.seed, r, 100000)
+        counts, ents, pool = workload.build_batch(p.G, 1, p.seed, r, 256,
+                                                  val_len, groups=act)
+        p.orc.stage_proposals(counts, 1, ents, pool)
+        p.eng.gen_kv_proposals(r % 2, 1, 256, val_len, p.seed, r,
+                               active_ppm=100000)
+        tick = r % 4 == 0
+        o = p.orc.round(tick=tick)
+        e = p.eng.step(tick=tick, prop_slot=r % 2, encode_saves=True)
+        p.rounds += 1
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        assert (e.committed_entries, e.applied_entries, e.messages) == \
+            (o.committed_entries, o.applied_entries, o.messages), r
+        errs = p.check()
+        assert not errs, (r, errs[:2])
+        assert not p.check_saves(), r
