@@ -142,6 +142,11 @@ static uint4 mk4h(uint64_t a, uint64_t b) {
 static uint64_t lo64h(uint4 q) { return (uint64_t)q.x | ((uint64_t)q.y << 32); }
 static uint64_t hi64h(uint4 q) { return (uint64_t)q.z | ((uint64_t)q.w << 32); }
 
+__global__ void k_fill_u4(uint4 *p, uint64_t n, uint4 val) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = val;
+}
+
 __global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t val) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = val;
@@ -235,6 +240,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   v.stage_slot = 0;
   int rc = 0;
   rc |= dalloc(e, &v.u64, (uint64_t)NUM_U64 * R * G);
+  rc |= dalloc(e, &v.pk, 4ull * R * G);
   rc |= dalloc(e, &v.u32, (uint64_t)NUM_U32 * R * G);
   rc |= dalloc(e, &v.rem_match, R * R * G);
   rc |= dalloc(e, &v.rem_next, R * R * G);
@@ -286,8 +292,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
   if (!rc) {  // no Replicate in flight: ring_guard = +inf
-    k_fill_u64<<<(unsigned)((R * G + 255) / 256), 256, 0, e->stream>>>(
-        v.u64 + u64_ix(v, F_RING_GUARD, 0, 0), R * G, ~0ull);
+    k_fill_u4<<<(unsigned)((R * G + 255) / 256), 256, 0, e->stream>>>(
+        v.pk + pk_ix(v, 1, 0, 0), R * G, make_uint4(0, 0, 0, PK_INF16 << 16));
     if (hipGetLastError() != hipSuccess) rc = 1;
   }
   if (!rc && hipMemcpyAsync(e->dview, &e->v, sizeof(View),
@@ -354,6 +360,38 @@ static int check_range(drb_engine *e, uint64_t first, uint64_t n) {
   return DRB_OK;
 }
 
+// decoded field values [replica][NUM_U64] of groups [first, first + n)
+// from the packed records and the u64 array (overflow, counters)
+static int read_records(drb_engine *e, uint64_t first, uint64_t n,
+                        std::vector<uint64_t> &vals) {
+  const View &v = e->v;
+  const uint32_t R = v.R;
+  std::vector<uint64_t> ipk, i64;
+  for (uint64_t gi = 0; gi < n; ++gi)
+    for (uint32_t s = 0; s < R; ++s) {
+      for (int ch = 0; ch < 4; ++ch) ipk.push_back(pk_ix(v, ch, s, first + gi));
+      for (int k = 0; k < NUM_U64; ++k)
+        i64.push_back(u64_ix(v, k, s, first + gi));
+    }
+  std::vector<uint4> pk;
+  std::vector<uint64_t> over;
+  if (gather(e, v.pk, ipk, pk) || gather(e, v.u64, i64, over))
+    return DRB_EDEVICE;
+  vals.assign(n * R * NUM_U64, 0);
+  for (uint64_t q = 0; q < n * R; ++q) {
+    uint32_t w[16];
+    for (int ch = 0; ch < 4; ++ch) {
+      const uint4 c = pk[q * 4 + ch];
+      w[4 * ch] = c.x;
+      w[4 * ch + 1] = c.y;
+      w[4 * ch + 2] = c.z;
+      w[4 * ch + 3] = c.w;
+    }
+    pk_decode(w, &over[q * NUM_U64], &vals[q * NUM_U64]);
+  }
+  return DRB_OK;
+}
+
 extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
                                    uint64_t n_groups,
                                    const drb_replica_state *st) {
@@ -367,22 +405,42 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
   std::vector<uint64_t> iri;
   std::vector<uint4> dric, drii;
   std::vector<uint32_t> dricf;
+  // the window bounds are engine state (drb_import_log sets ring_lo): keep
+  // the current ones across the re-encoding of the packed records
+  std::vector<uint64_t> cur;
+  if (read_records(e, first_group, n_groups, cur)) return DRB_EDEVICE;
+  std::vector<uint64_t> ipk;
+  std::vector<uint4> dpk;
   for (uint64_t gi = 0; gi < n_groups; ++gi) {
     uint64_t g = first_group + gi;
     for (uint32_t s = 0; s < R; ++s) {
       drb_replica_state c = st[gi * R + s];
-      for (int k = 0; k < NUM_U64_EXPORTED; ++k) {
-        i64.push_back(u64_ix(v, kU64Order[k], s, g));
-        d64.push_back(*st_u64(&c, k));
+      uint64_t vals[NUM_U64], over[NUM_U64];
+      for (int k = 0; k < NUM_U64; ++k) vals[k] = over[k] = 0;
+      for (int k = 0; k < NUM_U64_EXPORTED; ++k)
+        vals[kU64Order[k]] = *st_u64(&c, k);
+      const uint64_t *old = &cur[(gi * R + s) * NUM_U64];
+      vals[F_RING_LO] = old[F_RING_LO];
+      vals[F_RING_GUARD] = old[F_RING_GUARD];
+      vals[F_TERM_START] = c.last_index + 1;  // the term cache restarts empty
+      uint32_t w[16];
+      pk_encode(w, vals, over);
+      for (int ch = 0; ch < 4; ++ch) {
+        ipk.push_back(pk_ix(v, ch, s, g));
+        dpk.push_back(make_uint4(w[4 * ch], w[4 * ch + 1], w[4 * ch + 2],
+                                 w[4 * ch + 3]));
       }
-      // the term cache restarts empty: [last+1, last]
-      i64.push_back(u64_ix(v, F_TERM_START, s, g));
-      d64.push_back(c.last_index + 1);
-      uint32_t w[NUM_U32] = {c.role, c.flags & F_PUBLIC, c.fallback_reason,
-                             c.ri_count};
+      // overflow of escaped fields and the u64 counters
+      for (int k = 0; k < NUM_U64; ++k) {
+        const bool counter = k == F_TICK_COUNT || k == F_KV_COUNT;
+        i64.push_back(u64_ix(v, k, s, g));
+        d64.push_back(counter ? vals[k] : (over[k] ? over[k] : vals[k]));
+      }
+      const uint32_t w32[NUM_U32] = {c.role, c.flags & F_PUBLIC,
+                                     c.fallback_reason, c.ri_count};
       for (int k = 0; k < NUM_U32; ++k) {
         i32.push_back(u32_ix(v, k, s, g));
-        d32.push_back(w[k]);
+        d32.push_back(w32[k]);
       }
       for (uint32_t p = 0; p < R; ++p) {
         irm.push_back(rem_ix(v, s, p, g));
@@ -401,6 +459,7 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
   }
   int rc = 0;
   rc |= scatter(e, v.u64, i64, d64);
+  rc |= scatter(e, v.pk, ipk, dpk);
   rc |= scatter(e, v.u32, i32, d32);
   rc |= scatter(e, v.rem_match, irm, drm);
   rc |= scatter(e, v.rem_next, irm, drn);
@@ -422,8 +481,6 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
   for (uint64_t gi = 0; gi < n_groups; ++gi) {
     uint64_t g = first_group + gi;
     for (uint32_t s = 0; s < R; ++s) {
-      for (int k = 0; k < NUM_U64_EXPORTED; ++k)
-        i64.push_back(u64_ix(v, kU64Order[k], s, g));
       for (int k = 0; k < NUM_U32; ++k) i32.push_back(u32_ix(v, k, s, g));
       for (uint32_t p = 0; p < R; ++p) irm.push_back(rem_ix(v, s, p, g));
       for (uint32_t d = 0; d < DRB_RI_DEPTH; ++d)
@@ -434,7 +491,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
   std::vector<uint32_t> d32, drs, dra, dricf;
   std::vector<uint4> dric, drii;
   int rc = 0;
-  rc |= gather(e, v.u64, i64, d64);
+  rc |= read_records(e, first_group, n_groups, d64);
   rc |= gather(e, v.u32, i32, d32);
   rc |= gather(e, v.rem_match, irm, drm);
   rc |= gather(e, v.rem_next, irm, drn);
@@ -452,7 +509,9 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       memset(&o, 0, sizeof(o));
       o.shard_id = v.first_shard_id + gid(v, s, g);
       o.replica_id = s + 1;
-      for (int k = 0; k < NUM_U64_EXPORTED; ++k) *st_u64(&o, k) = d64[a++];
+      for (int k = 0; k < NUM_U64_EXPORTED; ++k)
+        *st_u64(&o, k) = d64[a + kU64Order[k]];
+      a += NUM_U64;
       o.role = d32[b++];
       o.flags = d32[b++] & F_PUBLIC;
       o.fallback_reason = d32[b++];
@@ -514,10 +573,22 @@ extern "C" int drb_import_log(drb_engine *e, uint64_t group, uint32_t slot,
     }
   }
   if (scatter(e, v.ring, idx, val)) return DRB_EDEVICE;
-  if (n) {
+  if (n) {  // the window now starts at the first imported entry
+    std::vector<uint64_t> cur;
+    if (read_records(e, group, 1, cur)) return DRB_EDEVICE;
+    uint64_t *vals = &cur[slot * NUM_U64];
+    vals[F_RING_LO] = ents[0].index;
+    uint64_t over[NUM_U64] = {0};
+    uint32_t w[16];
+    pk_encode(w, vals, over);
+    std::vector<uint64_t> ipk = {pk_ix(v, 1, slot, group),
+                                 pk_ix(v, 2, slot, group)};
+    std::vector<uint4> dpk = {make_uint4(w[4], w[5], w[6], w[7]),
+                              make_uint4(w[8], w[9], w[10], w[11])};
     std::vector<uint64_t> ri = {u64_ix(v, F_RING_LO, slot, group)};
     std::vector<uint64_t> rv = {ents[0].index};
-    if (scatter(e, v.u64, ri, rv)) return DRB_EDEVICE;
+    if (scatter(e, v.pk, ipk, dpk) || scatter(e, v.u64, ri, rv))
+      return DRB_EDEVICE;
   }
   return DRB_OK;
 }
@@ -591,8 +662,9 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   if (g >= v.G) return;
   const uint64_t R = v.R, L1 = R + 1;  // last index: R config + 1 no-op
   const bool is_leader = s == leader;
-  uint64_t *u = v.u64;
-#define SET(F, x) u[u64_ix(v, F, s, g)] = (x)
+  uint64_t vals[NUM_U64], over[NUM_U64];
+  for (int k = 0; k < NUM_U64; ++k) vals[k] = over[k] = 0;
+#define SET(F, x) vals[F] = (x)
   SET(F_TERM, term);
   SET(F_VOTE, leader + 1);
   SET(F_LEADER_ID, leader + 1);
@@ -624,6 +696,15 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   SET(F_RING_GUARD, ~0ull);
   SET(F_TERM_START, L1);  // the leader's no-op opened the term
 #undef SET
+  uint32_t w[16];
+  pk_encode(w, vals, over);
+  for (int k = 0; k < NUM_U64; ++k)  // escaped values (large ElectionRTT)
+    if (over[k]) v.u64[u64_ix(v, k, s, g)] = over[k];
+  for (int ch = 0; ch < 4; ++ch)
+    v.pk[pk_ix(v, ch, s, g)] =
+        make_uint4(w[4 * ch], w[4 * ch + 1], w[4 * ch + 2], w[4 * ch + 3]);
+  v.u64[u64_ix(v, F_TICK_COUNT, s, g)] = vals[F_TICK_COUNT];
+  v.u64[u64_ix(v, F_KV_COUNT, s, g)] = 0;
   v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
   v.u32[u32_ix(v, W_FLAGS, s, g)] =
       gid(v, s, g) < v.total_groups ? DRB_F_HOSTED : 0u;
@@ -1532,8 +1613,17 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
   if (g < v.G && (v.u32[u32_ix(v, W_FLAGS, slot, g)] & DRB_F_HOSTED)) {
     const uint32_t n = v.rtr_count[ix(v, slot, g)];
     if (n)
-      serve_reads_lane(v, slot, g, n, v.u64[u64_ix(v, F_SM_INDEX, slot, g)],
-                       n_reads, key_space, served, deferred);
+    {
+      const uint4 c0 = v.pk[pk_ix(v, 0, slot, g)];
+      const uint4 c1 = v.pk[pk_ix(v, 1, slot, g)];
+      const uint64_t last = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+      const uint32_t code = c1.z & 0xffffu;  // PI_SM_INDEX: word 6, low
+      const uint64_t sm = code == PK_ESC16
+                              ? v.u64[u64_ix(v, F_SM_INDEX, slot, g)]
+                              : pk_idx_value(code, last, false);
+      serve_reads_lane(v, slot, g, n, sm, n_reads, key_space, served,
+                       deferred);
+    }
   }
   const uint32_t cnt[2] = {served, deferred};
   block_counters<true, C_READS, 2>(v, slot, cnt);

@@ -54,6 +54,160 @@ enum U64Field : int {
 };
 constexpr int NUM_U64_EXPORTED = F_RING_LO;
 
+// ---- packed per-replica state ------------------------------------------
+// One 64 B record per replica (v.pk, [4 chunks][R][G] uint4 = words w0..15):
+//   w0-1 last, w2-3 term,
+//   w4..w10  the PIdx fields as signed 16-bit offsets from last (2 a word),
+//   w11 term - appliedToTerm | (term - prevTerm) << 16,
+//   w12 term - smTerm | electionTick << 16,
+//   w13 heartbeatTick | randomizedElectionTimeout << 16,
+//   w14 vote | leaderID << 8 | prevVote << 16, w15 0.
+// A value that does not fit stores the field's escape code and lives in
+// the u64 field array, which also keeps tick_count and kv_count.  A round
+// reads and writes 64 B of state per replica instead of ~340 B of u64
+// fields.
+enum PIdx : int {
+  PI_COMMITTED = 0,
+  PI_PROCESSED,
+  PI_MARKER,
+  PI_SAVED_TO,
+  PI_SM_INDEX,
+  PI_APPLIED_INDEX,
+  PI_RING_LO,
+  PI_RING_GUARD,  // ~0 (no Replicate in flight) is PK_INF16
+  PI_TERM_START,
+  PI_APPLIED,
+  PI_APPLIED_TO_INDEX,
+  PI_CONFIRMED,
+  PI_PUSHED,
+  PI_PREV_COMMIT,
+  NUM_PI
+};
+constexpr uint32_t PK_ESC16 = 0x8000u;  // index offset escape
+constexpr uint32_t PK_INF16 = 0x7fffu;  // ring guard +inf
+constexpr uint32_t PK_ESCU16 = 0xffffu;  // term distance / tick escape
+constexpr uint32_t PK_ESC8 = 0xffu;      // replica id escape
+
+// the u64 field that holds a PIdx field's overflow
+__host__ __device__ constexpr int pi_field(int i) {
+  return i == PI_COMMITTED          ? F_COMMITTED
+         : i == PI_PROCESSED        ? F_PROCESSED
+         : i == PI_MARKER           ? F_MARKER_INDEX
+         : i == PI_SAVED_TO         ? F_SAVED_TO
+         : i == PI_SM_INDEX         ? F_SM_INDEX
+         : i == PI_APPLIED_INDEX    ? F_APPLIED_INDEX
+         : i == PI_RING_LO          ? F_RING_LO
+         : i == PI_RING_GUARD       ? F_RING_GUARD
+         : i == PI_TERM_START       ? F_TERM_START
+         : i == PI_APPLIED          ? F_APPLIED
+         : i == PI_APPLIED_TO_INDEX ? F_APPLIED_TO_INDEX
+         : i == PI_CONFIRMED        ? F_CONFIRMED_INDEX
+         : i == PI_PUSHED           ? F_PUSHED_INDEX
+                                    : F_PREV_COMMIT;
+}
+__host__ __device__ inline uint32_t pk_half(const uint32_t *w, int word,
+                                            int hi) {
+  return (w[word] >> (16 * hi)) & 0xffffu;
+}
+__host__ __device__ inline void pk_set_half(uint32_t *w, int word, int hi,
+                                            uint32_t x) {
+  w[word] = (w[word] & ~(0xffffu << (16 * hi))) | ((x & 0xffffu) << (16 * hi));
+}
+// index field codes relative to base (the record's last)
+__host__ __device__ inline uint32_t pk_idx_code(uint64_t x, uint64_t base,
+                                                bool guard) {
+  if (guard && x == ~0ull) return PK_INF16;
+  const int64_t d = (int64_t)(x - base);
+  if (d < -32767 || d > (guard ? 32766 : 32767)) return PK_ESC16;
+  return (uint32_t)(uint16_t)(int16_t)d;
+}
+__host__ __device__ inline uint64_t pk_idx_value(uint32_t code,
+                                                 uint64_t base, bool guard) {
+  if (guard && code == PK_INF16) return ~0ull;
+  return base + (uint64_t)(int64_t)(int16_t)code;
+}
+__host__ __device__ inline uint32_t pk_term_code(uint64_t x, uint64_t term) {
+  return (x <= term && term - x < PK_ESCU16) ? (uint32_t)(term - x) : PK_ESCU16;
+}
+__host__ __device__ inline uint32_t pk_u16_code(uint64_t x) {
+  return x < PK_ESCU16 ? (uint32_t)x : PK_ESCU16;
+}
+__host__ __device__ inline uint32_t pk_id_code(uint64_t x) {
+  return x < PK_ESC8 ? (uint32_t)x : PK_ESC8;
+}
+
+// the whole record from / to field values indexed by U64Field (vals),
+// escapes through the overflow array `over` (same index); tick_count and
+// kv_count are not in the record
+__host__ __device__ inline void pk_encode(uint32_t *w, const uint64_t *vals,
+                                          uint64_t *over) {
+  const uint64_t last = vals[F_LAST_INDEX], term = vals[F_TERM];
+  for (int q = 0; q < 16; ++q) w[q] = 0;
+  w[0] = (uint32_t)last;
+  w[1] = (uint32_t)(last >> 32);
+  w[2] = (uint32_t)term;
+  w[3] = (uint32_t)(term >> 32);
+  for (int i = 0; i < NUM_PI; ++i) {
+    const uint64_t x = vals[pi_field(i)];
+    const uint32_t c = pk_idx_code(x, last, i == PI_RING_GUARD);
+    if (c == PK_ESC16) over[pi_field(i)] = x;
+    pk_set_half(w, 4 + i / 2, i & 1, c);
+  }
+  const int tf[3] = {F_APPLIED_TO_TERM, F_PREV_TERM, F_SM_TERM};
+  const int tw[3] = {11, 11, 12}, th[3] = {0, 1, 0};
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = pk_term_code(vals[tf[k]], term);
+    if (c == PK_ESCU16) over[tf[k]] = vals[tf[k]];
+    pk_set_half(w, tw[k], th[k], c);
+  }
+  const int uf[3] = {F_ELECTION_TICK, F_HEARTBEAT_TICK, F_RAND_TIMEOUT};
+  const int uw[3] = {12, 13, 13}, uh[3] = {1, 0, 1};
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = pk_u16_code(vals[uf[k]]);
+    if (c == PK_ESCU16) over[uf[k]] = vals[uf[k]];
+    pk_set_half(w, uw[k], uh[k], c);
+  }
+  const int df[3] = {F_VOTE, F_LEADER_ID, F_PREV_VOTE};
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = pk_id_code(vals[df[k]]);
+    if (c == PK_ESC8) over[df[k]] = vals[df[k]];
+    w[14] |= c << (8 * k);
+  }
+}
+__host__ __device__ inline void pk_decode(const uint32_t *w,
+                                          const uint64_t *over,
+                                          uint64_t *vals) {
+  const uint64_t last = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  const uint64_t term = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  vals[F_LAST_INDEX] = last;
+  vals[F_TERM] = term;
+  for (int i = 0; i < NUM_PI; ++i) {
+    const uint32_t c = pk_half(w, 4 + i / 2, i & 1);
+    vals[pi_field(i)] = c == PK_ESC16
+                            ? over[pi_field(i)]
+                            : pk_idx_value(c, last, i == PI_RING_GUARD);
+  }
+  const int tf[3] = {F_APPLIED_TO_TERM, F_PREV_TERM, F_SM_TERM};
+  const int tw[3] = {11, 11, 12}, th[3] = {0, 1, 0};
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = pk_half(w, tw[k], th[k]);
+    vals[tf[k]] = c == PK_ESCU16 ? over[tf[k]] : term - c;
+  }
+  const int uf[3] = {F_ELECTION_TICK, F_HEARTBEAT_TICK, F_RAND_TIMEOUT};
+  const int uw[3] = {12, 13, 13}, uh[3] = {1, 0, 1};
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = pk_half(w, uw[k], uh[k]);
+    vals[uf[k]] = c == PK_ESCU16 ? over[uf[k]] : c;
+  }
+  const int df[3] = {F_VOTE, F_LEADER_ID, F_PREV_VOTE};
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t c = (w[14] >> (8 * k)) & 0xffu;
+    vals[df[k]] = c == PK_ESC8 ? over[df[k]] : c;
+  }
+  vals[F_TICK_COUNT] = over[F_TICK_COUNT];
+  vals[F_KV_COUNT] = over[F_KV_COUNT];
+}
+
 // per-replica u32 fields, array [F][slot][g]
 enum U32Field : int { W_ROLE = 0, W_FLAGS, W_FB_REASON, W_RI_COUNT, NUM_U32 };
 
@@ -87,7 +241,8 @@ struct View {
   uint32_t pad0;
   uint64_t first_shard_id;
 
-  uint64_t *u64;          // [NUM_U64][R][G]
+  uint64_t *u64;          // [NUM_U64][R][G] (overflow, tick/kv counts)
+  uint4 *pk;              // [4][R][G] packed state records (see PIdx)
   uint32_t *u32;          // [NUM_U32][R][G]
   uint64_t *rem_match;    // [R(self)][R(peer)][G]
   uint64_t *rem_next;     // [R][R][G]
@@ -143,6 +298,10 @@ __host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,
 __host__ __device__ inline uint64_t u64_ix(const View &v, int f,
                                            uint32_t slot, uint64_t g) {
   return ((uint64_t)f * v.R + slot) * v.G + g;
+}
+__host__ __device__ inline uint64_t pk_ix(const View &v, int chunk,
+                                          uint32_t slot, uint64_t g) {
+  return ((uint64_t)chunk * v.R + slot) * v.G + g;
 }
 __host__ __device__ inline uint64_t u32_ix(const View &v, int f,
                                            uint32_t slot, uint64_t g) {

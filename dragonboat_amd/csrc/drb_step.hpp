@@ -59,14 +59,17 @@ enum : int {
   NUM_COUNTERS
 };
 
-// The fields a round reads or writes on most of its paths live in
-// registers; the rest (vote, tick_count, the randomized timeout, Peer's
-// prevState, node's confirmed/pushed indexes, appliedTo*, sm_term,
-// kv_count) are loaded and stored in place where the round touches them
-// (ld_f / st_f), which keeps both the register file and the HBM traffic of
-// a round to what that round actually uses.
+// A replica's state is one 64 B packed record (drb_layout.hpp, PIdx),
+// loaded whole at the start of its round and stored whole at the end.  The
+// fields most of the round uses are decoded into registers; the rest
+// (vote, the randomized timeout, Peer's prevState, node's confirmed/pushed
+// indexes, appliedTo*, sm_term) stay encoded in the record words and are
+// read / written through ld_f / st_f.  tick_count and kv_count are plain
+// u64 counters, read-modify-written where the round changes them.
 template <int R>
 struct Rep {
+  uint32_t pw[16];  // the packed record (index offsets relative to base0)
+  uint64_t base0;   // last at the start of the round
   uint64_t term, leader_id, election_tick, heartbeat_tick;
   uint64_t committed, processed, last, marker, saved_to;
   uint64_t applied_index, sm_index, ring_lo, ring_guard, term_start;
@@ -160,12 +163,99 @@ DRB_DEV void set_leader(Rep<R> &r, uint64_t id) {
   }
 }
 
-// cold fields: loaded / stored in place
-DRB_DEV uint64_t ld_f(const Lane &L, int f) {
+// ------------------------------------------------------------ packed state
+// the u64 array: overflow of escaped record fields, tick/kv counters
+DRB_DEV uint64_t over_ld(const Lane &L, int f) {
   return L.v->u64[u64_ix(*L.v, f, L.slot, L.g)];
 }
-DRB_DEV void st_f(const Lane &L, int f, uint64_t x) {
+DRB_DEV void over_st(const Lane &L, int f, uint64_t x) {
   L.v->u64[u64_ix(*L.v, f, L.slot, L.g)] = x;
+}
+// index field i (a PIdx constant): offset from `base` in the record
+template <int R>
+DRB_DEV uint64_t pi_get(const Lane &L, const Rep<R> &r, int i) {
+  const uint32_t c = pk_half(r.pw, 4 + i / 2, i & 1);
+  return c == PK_ESC16 ? over_ld(L, pi_field(i))
+                       : pk_idx_value(c, r.base0, i == PI_RING_GUARD);
+}
+template <int R>
+DRB_DEV void pi_put(const Lane &L, Rep<R> &r, int i, uint64_t x,
+                    uint64_t base) {
+  const uint32_t c = pk_idx_code(x, base, i == PI_RING_GUARD);
+  if (c == PK_ESC16) over_st(L, pi_field(i), x);
+  pk_set_half(r.pw, 4 + i / 2, i & 1, c);
+}
+// term distances (word, half), ticks (word, half), replica ids (byte)
+template <int R>
+DRB_DEV uint64_t pt_get(const Lane &L, const Rep<R> &r, int w, int h, int f) {
+  const uint32_t c = pk_half(r.pw, w, h);
+  return c == PK_ESCU16 ? over_ld(L, f) : r.term - c;
+}
+template <int R>
+DRB_DEV void pt_put(const Lane &L, Rep<R> &r, int w, int h, int f,
+                    uint64_t x) {
+  const uint32_t c = pk_term_code(x, r.term);
+  if (c == PK_ESCU16) over_st(L, f, x);
+  pk_set_half(r.pw, w, h, c);
+}
+template <int R>
+DRB_DEV uint64_t pu_get(const Lane &L, const Rep<R> &r, int w, int h, int f) {
+  const uint32_t c = pk_half(r.pw, w, h);
+  return c == PK_ESCU16 ? over_ld(L, f) : c;
+}
+template <int R>
+DRB_DEV void pu_put(const Lane &L, Rep<R> &r, int w, int h, int f,
+                    uint64_t x) {
+  const uint32_t c = pk_u16_code(x);
+  if (c == PK_ESCU16) over_st(L, f, x);
+  pk_set_half(r.pw, w, h, c);
+}
+template <int R>
+DRB_DEV uint64_t pd_get(const Lane &L, const Rep<R> &r, int b, int f) {
+  const uint32_t c = (r.pw[14] >> (8 * b)) & 0xffu;
+  return c == PK_ESC8 ? over_ld(L, f) : c;
+}
+template <int R>
+DRB_DEV void pd_put(const Lane &L, Rep<R> &r, int b, int f, uint64_t x) {
+  const uint32_t c = pk_id_code(x);
+  if (c == PK_ESC8) over_st(L, f, x);
+  r.pw[14] = (r.pw[14] & ~(0xffu << (8 * b))) | (c << (8 * b));
+}
+
+// the record fields a round does not keep decoded (f: a U64Field constant)
+template <int R>
+DRB_DEV uint64_t ld_f(const Lane &L, const Rep<R> &r, int f) {
+  switch (f) {
+    case F_VOTE: return pd_get(L, r, 0, f);
+    case F_PREV_VOTE: return pd_get(L, r, 2, f);
+    case F_APPLIED_TO_TERM: return pt_get(L, r, 11, 0, f);
+    case F_PREV_TERM: return pt_get(L, r, 11, 1, f);
+    case F_SM_TERM: return pt_get(L, r, 12, 0, f);
+    case F_RAND_TIMEOUT: return pu_get(L, r, 13, 1, f);
+    case F_APPLIED: return pi_get(L, r, PI_APPLIED);
+    case F_APPLIED_TO_INDEX: return pi_get(L, r, PI_APPLIED_TO_INDEX);
+    case F_CONFIRMED_INDEX: return pi_get(L, r, PI_CONFIRMED);
+    case F_PUSHED_INDEX: return pi_get(L, r, PI_PUSHED);
+    case F_PREV_COMMIT: return pi_get(L, r, PI_PREV_COMMIT);
+    default: return over_ld(L, f);  // tick_count, kv_count
+  }
+}
+template <int R>
+DRB_DEV void st_f(const Lane &L, Rep<R> &r, int f, uint64_t x) {
+  switch (f) {
+    case F_VOTE: pd_put(L, r, 0, f, x); break;
+    case F_PREV_VOTE: pd_put(L, r, 2, f, x); break;
+    case F_APPLIED_TO_TERM: pt_put(L, r, 11, 0, f, x); break;
+    case F_PREV_TERM: pt_put(L, r, 11, 1, f, x); break;
+    case F_SM_TERM: pt_put(L, r, 12, 0, f, x); break;
+    case F_RAND_TIMEOUT: pu_put(L, r, 13, 1, f, x); break;
+    case F_APPLIED: pi_put(L, r, PI_APPLIED, x, r.base0); break;
+    case F_APPLIED_TO_INDEX: pi_put(L, r, PI_APPLIED_TO_INDEX, x, r.base0); break;
+    case F_CONFIRMED_INDEX: pi_put(L, r, PI_CONFIRMED, x, r.base0); break;
+    case F_PUSHED_INDEX: pi_put(L, r, PI_PUSHED, x, r.base0); break;
+    case F_PREV_COMMIT: pi_put(L, r, PI_PREV_COMMIT, x, r.base0); break;
+    default: over_st(L, f, x); break;  // tick_count, kv_count
+  }
 }
 
 // ------------------------------------------------------------ messages
@@ -1099,26 +1189,33 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
 template <int R, bool LEAD>
 DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
   const View &v = *L.v;
-#define LD(F, x) r.x = v.u64[u64_ix(v, F, L.slot, L.g)]
-  LD(F_TERM, term);
-  LD(F_LEADER_ID, leader_id);
-  LD(F_ELECTION_TICK, election_tick);
-  if (LEAD) LD(F_HEARTBEAT_TICK, heartbeat_tick);
-  LD(F_COMMITTED, committed);
-  LD(F_PROCESSED, processed);
-  LD(F_LAST_INDEX, last);
-  LD(F_MARKER_INDEX, marker);
-  LD(F_SAVED_TO, saved_to);
-  LD(F_APPLIED_INDEX, applied_index);
-  LD(F_SM_INDEX, sm_index);
-  LD(F_RING_LO, ring_lo);
-  LD(F_RING_GUARD, ring_guard);
-  LD(F_TERM_START, term_start);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint4 q = v.pk[pk_ix(v, c, L.slot, L.g)];
+    r.pw[4 * c] = q.x;
+    r.pw[4 * c + 1] = q.y;
+    r.pw[4 * c + 2] = q.z;
+    r.pw[4 * c + 3] = q.w;
+  }
+  r.last = (uint64_t)r.pw[0] | ((uint64_t)r.pw[1] << 32);
+  r.term = (uint64_t)r.pw[2] | ((uint64_t)r.pw[3] << 32);
+  r.base0 = r.last;
+  r.leader_id = pd_get(L, r, 1, F_LEADER_ID);
+  r.election_tick = pu_get(L, r, 12, 1, F_ELECTION_TICK);
+  if (LEAD) r.heartbeat_tick = pu_get(L, r, 13, 0, F_HEARTBEAT_TICK);
+  r.committed = pi_get(L, r, PI_COMMITTED);
+  r.processed = pi_get(L, r, PI_PROCESSED);
+  r.marker = pi_get(L, r, PI_MARKER);
+  r.saved_to = pi_get(L, r, PI_SAVED_TO);
+  r.applied_index = pi_get(L, r, PI_APPLIED_INDEX);
+  r.sm_index = pi_get(L, r, PI_SM_INDEX);
+  r.ring_lo = pi_get(L, r, PI_RING_LO);
+  r.ring_guard = pi_get(L, r, PI_RING_GUARD);
+  r.term_start = pi_get(L, r, PI_TERM_START);
   r.sm_term = 0;
   r.kv_added = 0;
   r.applied_any = false;
   r.lid_dirty = false;
-#undef LD
   r.flags = v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)];
   r.fb = v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)];
   r.ri_count = v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)];
@@ -1149,27 +1246,42 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
 }
 
 template <int R, bool LEAD>
-DRB_DEV void store_rep(const Lane &L, const Rep<R> &r, uint32_t flags0,
+DRB_DEV void store_rep(const Lane &L, Rep<R> &r, uint32_t flags0,
                        uint32_t fb0) {
   const View &v = *L.v;
-#define ST(F, x) v.u64[u64_ix(v, F, L.slot, L.g)] = r.x
+  // re-base the record on the final last: the cold index fields first
+  // (still relative to base0), then the decoded ones
+  const uint64_t base = r.last;
+#pragma unroll
+  for (int i = PI_APPLIED; i < NUM_PI; ++i) {
+    const uint32_t c = pk_half(r.pw, 4 + i / 2, i & 1);
+    if (c != PK_ESC16)
+      pi_put(L, r, i, pk_idx_value(c, r.base0, false), base);
+  }
+  pi_put(L, r, PI_COMMITTED, r.committed, base);
+  pi_put(L, r, PI_PROCESSED, r.processed, base);
+  pi_put(L, r, PI_MARKER, r.marker, base);
+  pi_put(L, r, PI_SAVED_TO, r.saved_to, base);
+  pi_put(L, r, PI_SM_INDEX, r.sm_index, base);
+  pi_put(L, r, PI_APPLIED_INDEX, r.applied_index, base);
+  pi_put(L, r, PI_RING_LO, r.ring_lo, base);
+  pi_put(L, r, PI_RING_GUARD, r.ring_guard, base);
+  pi_put(L, r, PI_TERM_START, r.term_start, base);
   // term, vote, prevVote, randomizedElectionTimeout never change on the
   // fast path (a round that would change them falls back first)
-  if (r.lid_dirty) ST(F_LEADER_ID, leader_id);
-  ST(F_ELECTION_TICK, election_tick);
-  if (LEAD) ST(F_HEARTBEAT_TICK, heartbeat_tick);
-  ST(F_COMMITTED, committed);
-  ST(F_PROCESSED, processed);
-  ST(F_LAST_INDEX, last);
-  ST(F_MARKER_INDEX, marker);
-  ST(F_SAVED_TO, saved_to);
-  ST(F_SM_INDEX, sm_index);
-  ST(F_RING_LO, ring_lo);
-  ST(F_RING_GUARD, ring_guard);
-  ST(F_TERM_START, term_start);
-  if (r.applied_any) ST(F_SM_TERM, sm_term);
-  if (r.kv_added) st_f(L, F_KV_COUNT, ld_f(L, F_KV_COUNT) + r.kv_added);
-#undef ST
+  if (r.lid_dirty) pd_put(L, r, 1, F_LEADER_ID, r.leader_id);
+  pu_put(L, r, 12, 1, F_ELECTION_TICK, r.election_tick);
+  if (LEAD) pu_put(L, r, 13, 0, F_HEARTBEAT_TICK, r.heartbeat_tick);
+  if (r.applied_any) pt_put(L, r, 12, 0, F_SM_TERM, r.sm_term);
+  if (r.kv_added)
+    over_st(L, F_KV_COUNT, over_ld(L, F_KV_COUNT) + r.kv_added);
+  r.pw[0] = (uint32_t)r.last;
+  r.pw[1] = (uint32_t)(r.last >> 32);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    v.pk[pk_ix(v, c, L.slot, L.g)] =
+        make_uint4(r.pw[4 * c], r.pw[4 * c + 1], r.pw[4 * c + 2],
+                   r.pw[4 * c + 3]);
   if (r.flags != flags0) v.u32[u32_ix(v, W_FLAGS, L.slot, L.g)] = r.flags;
   if (r.fb != fb0) v.u32[u32_ix(v, W_FB_REASON, L.slot, L.g)] = r.fb;
   if (!LEAD) return;  // followers keep no remotes and no readIndex queue
@@ -1495,7 +1607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         fb = DRB_FB_CAPACITY;
       if (p.tick) {
         uint64_t et = (total_in ? 0 : r.election_tick) + 1;
-        if (et >= ld_f(L, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
+        if (et >= ld_f(L, r, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
           fb = DRB_FB_ELECTION;
       }
     }
@@ -1518,8 +1630,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       // ---------------------------------------- handleEvents (node.go)
       // updateAppliedIndex (node.go:1133-1137)
       r.applied_index = r.sm_index;
-      st_f(L, F_APPLIED, r.applied_index);
-      st_f(L, F_APPLIED_INDEX, r.applied_index);
+      st_f(L, r, F_APPLIED, r.applied_index);  // applied_index: hot
       // handleReadIndex (node.go:1296) -> Peer.ReadIndex (peer.go:309)
       if (is_leader && in_lo != 0) leader_read_index(L, r, in_lo, in_hi, 0);
       // handleReceivedMessages: Replicates by sender, then the rest
@@ -1557,7 +1668,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       }
       // LocalTick (node.tick node.go:1562 -> raft.tick raft.go:571-648)
       if (p.tick) {
-        st_f(L, F_TICK_COUNT, ld_f(L, F_TICK_COUNT) + 1);
+        over_st(L, F_TICK_COUNT, over_ld(L, F_TICK_COUNT) + 1);
         if (is_leader) {
           r.election_tick++;
           if (r.election_tick >= v.election_rtt) {
@@ -1607,11 +1718,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
       bool has_save = inmem_nonempty && save_lo >= r.marker && save_lo <= r.last;
       bool has_apply = r.committed > r.processed;
       // Peer.prevState (peer.go:59) and node's cursors, in place
-      const uint64_t vote = ld_f(L, F_VOTE);
-      const uint64_t prev_term = ld_f(L, F_PREV_TERM);
-      const uint64_t prev_vote = ld_f(L, F_PREV_VOTE);
-      const uint64_t prev_commit = ld_f(L, F_PREV_COMMIT);
-      const uint64_t confirmed_index = ld_f(L, F_CONFIRMED_INDEX);
+      const uint64_t vote = ld_f(L, r, F_VOTE);
+      const uint64_t prev_term = ld_f(L, r, F_PREV_TERM);
+      const uint64_t prev_vote = ld_f(L, r, F_PREV_VOTE);
+      const uint64_t prev_commit = ld_f(L, r, F_PREV_COMMIT);
+      const uint64_t confirmed_index = ld_f(L, r, F_CONFIRMED_INDEX);
       bool state_changed = !(r.term == prev_term && vote == prev_vote &&
                              r.committed == prev_commit);
       bool state_empty = r.term == 0 && vote == 0 && r.committed == 0;
@@ -1624,7 +1735,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         if (has_apply) {
           // pb.EntriesToApply(CommittedEntries, pushedIndex, strict)
           // (raftpb/entry.go:27-47) then node.pushEntries (node.go:625)
-          const uint64_t pushed = ld_f(L, F_PUSHED_INDEX);
+          const uint64_t pushed = ld_f(L, r, F_PUSHED_INDEX);
           apply_lo = r.processed + 1;
           apply_hi = r.committed;
           if (apply_hi <= pushed || apply_lo > pushed + 1) {
@@ -1632,16 +1743,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
             apply_lo = 0;
           } else {
             apply_lo = pushed + 1;
-            st_f(L, F_PUSHED_INDEX, apply_hi);
+            st_f(L, r, F_PUSHED_INDEX, apply_hi);
           }
         }
         if (state_changed && !state_empty) {
-          if (prev_term != r.term) st_f(L, F_PREV_TERM, r.term);
-          if (prev_vote != vote) st_f(L, F_PREV_VOTE, vote);
-          st_f(L, F_PREV_COMMIT, r.committed);
+          if (prev_term != r.term) st_f(L, r, F_PREV_TERM, r.term);
+          if (prev_vote != vote) st_f(L, r, F_PREV_VOTE, vote);
+          st_f(L, r, F_PREV_COMMIT, r.committed);
         }
         if (confirmed_index != r.applied_index)
-          st_f(L, F_CONFIRMED_INDEX, r.applied_index);
+          st_f(L, r, F_CONFIRMED_INDEX, r.applied_index);
         // SaveRaftState (engine.go:1343) of EntriesToSave
         if (EXT && has_save && p.encode_saves)
           encode_saves(L, r, save_lo, r.last, crc_tab, c_saved,
@@ -1655,8 +1766,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
             set_error(r, DRB_ERR_COMMIT);
           // inMemory.appliedLogTo (inmemory.go:138-164)
           if (la >= r.marker && r.last >= r.marker && la <= r.last) {
-            st_f(L, F_APPLIED_TO_INDEX, la);
-            st_f(L, F_APPLIED_TO_TERM, log_term(L, r, la));
+            st_f(L, r, F_APPLIED_TO_INDEX, la);
+            st_f(L, r, F_APPLIED_TO_TERM, log_term(L, r, la));
             r.marker = la + 1;
           }
         }
