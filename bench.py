@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--replicas", type=int, default=0,
                     help="default 3 (c3) / 5 (c4)")
     ap.add_argument("--k", type=int, default=1, help="writes/group/round")
+    ap.add_argument("--kv-slots", type=int, default=0,
+                    help="KV table slots per replica (0: the workload's)")
     ap.add_argument("--no-read-index", action="store_true")
     ap.add_argument("--tick-every", type=int, default=0,
                     help="LocalTick every N rounds (0: derive from --tick-ms)")
@@ -213,7 +215,7 @@ def main():
         first_shard, seed = ddist.shard_plan(rank, G)
         eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                      max_props=max(1, k), prop_slots=NP, ri_slots=NP,
-                     mailbox=13, kv_slots=512, kv_val_cap=4,
+                     mailbox=13, kv_slots=args.kv_slots or 512, kv_val_cap=4,
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):

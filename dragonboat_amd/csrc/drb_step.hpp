@@ -32,11 +32,30 @@ namespace drb {
 #ifndef DRB_LEAD_WAVES
 #define DRB_LEAD_WAVES 3
 #endif
+// the EXT leader (C5 payloads, EntryBatch encoding) carries the most state.
+// Two waves per SIMD spill nothing but measured slower at C5 128 B (3.83 vs
+// 3.35 ms / round).  Note: the three-wave EXT leader built with
+// DRB_PROBE_W=4 produced wrong EntriesToSave on the GPU (every W <= 2 build,
+// and the two-wave build, were exact; tests/test_gpu_parity.py
+// test_entries_to_save_entrybatch_crc catches it)
+#ifndef DRB_EXT_LEAD_WAVES
+#define DRB_EXT_LEAD_WAVES 3
+#endif
 #ifndef DRB_FOLLOW_WAVES
 #define DRB_FOLLOW_WAVES 4
 #endif
 // timing experiments only (tools/variants.sh), never in a shipped build:
 // bit 0 skips the KV apply, bit 1 the in-round served reads
+// KV slots loaded per probe step (apply upserts, lookups past the first two).
+// Measured at C3 (same box): W=1 1.016, 2 1.033, 4 1.063, 8 1.240 ms/round,
+// and kv_slots 1024 no faster than 512: the probe chains are not what the
+// KV accesses wait on (the random line fetches are)
+#ifndef DRB_PROBE_W
+#define DRB_PROBE_W 1
+#endif
+#ifndef DRB_PROBE_WR
+#define DRB_PROBE_WR DRB_PROBE_W
+#endif
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
@@ -991,17 +1010,37 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       (!EXT || voff + 4 <= 64 ? cmd_u32_at(cmd, voff)
                               : value_chunk(L, index, voff, vlen, 0, 0).x) &
       byte_mask(vlen);
-  // open-addressing upsert into this replica's table
+  if (DRB_ABLATE & 4) {  // timing only: parse, no table access
+    r.sm_index = index;
+    r.sm_term = term;
+    r.applied_any = true;
+    return (int)(w0 & 1) | 1;
+  }
+  // open-addressing upsert into this replica's table: DRB_PROBE_W slots
+  // are loaded per step (one memory round trip), then resolved in order
   uint32_t mask = v.KS - 1;
   uint32_t ks = (uint32_t)kv_hash(key8, klen) & mask;
   uint4 *tbl = v.kv + kv_ix(v, L.slot, L.g, 0);
-  for (uint32_t probe = 0; probe < v.KS; ++probe) {
-    uint4 *sl = tbl + (uint64_t)ks * v.KVW;
-    uint4 h = sl[0];
-    bool used = (h.z >> 31) & 1u;
-    uint32_t sklen = h.z & 0xffu;
-    bool hit = used && sklen == klen && lo64(h) == key8;
-    if (!used || hit) {
+  for (uint32_t p0 = 0; p0 < v.KS; p0 += DRB_PROBE_W) {
+    uint4 hs[DRB_PROBE_W];
+#pragma unroll
+    for (uint32_t t = 0; t < DRB_PROBE_W; ++t)
+      hs[t] = p0 + t < v.KS ? tbl[(uint64_t)((ks + t) & mask) * v.KVW]
+                            : make_uint4(0, 0, 0, 1u << 31);
+    uint32_t found = DRB_PROBE_W;
+    bool hit = false;
+#pragma unroll
+    for (int t = DRB_PROBE_W - 1; t >= 0; --t) {
+      const bool used = (hs[t].z >> 31) & 1u;
+      const bool h = used && (hs[t].z & 0xffu) == klen && lo64(hs[t]) == key8;
+      const bool pad = p0 + t >= v.KS;
+      if (!pad && (!used || h)) {
+        found = (uint32_t)t;
+        hit = h;
+      }
+    }
+    if (found < DRB_PROBE_W) {
+      uint4 *sl = tbl + (uint64_t)((ks + found) & mask) * v.KVW;
       if (!EXT) {
         // inline value of a Cmd inside the 64 B register window: bytes 4..
         // in the slot's following chunks
@@ -1028,7 +1067,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       r.applied_any = true;
       return 1;
     }
-    ks = (ks + 1) & mask;
+    ks = (ks + DRB_PROBE_W) & mask;
   }
   return -1;  // table full
 }
@@ -1114,20 +1153,31 @@ DRB_DEV uint64_t kv_word(uint4 h) {
   const uint32_t vlen = (h.z >> 8) & 0xfffu;
   return ((uint64_t)vlen << 32) | (h.w & byte_mask(vlen));
 }
-// linear probing from slot ks for at most `probes` slots
+// linear probing from slot ks for at most `probes` slots, DRB_PROBE_W
+// slots per memory round trip
 DRB_DEV uint64_t kv_probe_word(const uint4 *tbl, uint32_t KVW, uint32_t mask,
                                uint32_t ks, uint64_t key8, uint32_t klen,
                                uint32_t probes) {
-  for (uint32_t p = 0; p < probes; ++p) {
-    const uint4 h = tbl[(uint64_t)ks * KVW];
-    if (!kv_used(h)) break;
-    if (kv_match(h, key8, klen)) return kv_word(h);
-    ks = (ks + 1) & mask;
+  for (uint32_t p0 = 0; p0 < probes; p0 += DRB_PROBE_WR) {
+    uint4 hs[DRB_PROBE_WR];
+#pragma unroll
+    for (uint32_t t = 0; t < DRB_PROBE_WR; ++t)
+      hs[t] = p0 + t < probes ? tbl[(uint64_t)((ks + t) & mask) * KVW]
+                              : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t t = 0; t < DRB_PROBE_WR; ++t) {
+      if (!kv_used(hs[t])) return ~0ull;  // also the padding past probes
+      if (kv_match(hs[t], key8, klen)) return kv_word(hs[t]);
+    }
+    ks = (ks + DRB_PROBE_WR) & mask;
   }
   return ~0ull;
 }
 
-constexpr uint32_t READ_BATCH = 5;
+#ifndef DRB_READ_BATCH
+#define DRB_READ_BATCH 5
+#endif
+constexpr uint32_t READ_BATCH = DRB_READ_BATCH;
 
 DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
                               uint32_t nrtr, uint64_t sm_index,
@@ -1396,7 +1446,7 @@ DRB_DEV void block_plane_summary(const View &v, uint32_t from, uint32_t to,
 // EXT: the instantiation for Cmds longer than 64 B, out-of-line values or
 // encode_saves (C5); the other one keeps the common path lean
 template <int R, bool LEAD, bool EXT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_LEAD_WAVES : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT ? DRB_EXT_LEAD_WAVES : DRB_LEAD_WAVES) : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
   // kernarg loads, and the pointers loaded from it are known to address
@@ -1774,10 +1824,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? DRB_
         // clearReadyToRead: records stay in the round output buffer
       }
       // ---------------------------------------- StateMachine.Handle
-      if (apply_hi >= apply_lo && apply_lo != 0 && !(DRB_ABLATE & 1)) {
+      if (apply_hi >= apply_lo && apply_lo != 0) {
         uint64_t from = umax64(apply_lo, r.sm_index + 1);
         for (uint64_t idx = from; idx <= apply_hi; ++idx) {
-          int rc = apply_entry<R, EXT>(L, r, idx);
+          int rc;
+          if (DRB_ABLATE & 1) {  // timing only: no state machine access
+            r.sm_index = idx;
+            r.applied_any = true;
+            rc = 1;
+          } else {
+            rc = apply_entry<R, EXT>(L, r, idx);
+          }
           if (rc < 0) {
             // the rsm apply of this replica leaves the fast path at idx;
             // the raft round itself completed
