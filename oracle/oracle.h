@@ -323,6 +323,34 @@ long orc_entrybatch_unmarshal(const uint8_t *buf, size_t len, drb_entry *out,
                               size_t cap, uint8_t *pool, size_t pool_cap);
 /* crc32.ChecksumIEEE (Go hash/crc32, tcp.go:146) */
 uint32_t orc_crc32_ieee(const uint8_t *p, size_t n);
+/* pb.Message Size / MarshalTo (message.go:32-124), the embedded Snapshot
+ * empty; Unmarshal (raft_optimized.go:659-983): bytes consumed, -1
+ * malformed, -2 non-empty Snapshot */
+size_t orc_message_size(const drb_message *m, const drb_entry *ents);
+size_t orc_message_marshal(const drb_message *m, const drb_entry *ents,
+                           const uint8_t *pool, uint8_t *buf);
+long orc_message_unmarshal(const uint8_t *buf, size_t len, drb_message *m,
+                           drb_entry *ents, size_t ent_cap, size_t *n_ents,
+                           uint8_t *pool, size_t pool_cap, size_t *pool_used);
+/* pb.MessageBatch MarshalTo (messagebatch.go:23-70) / Unmarshal
+ * (raft_optimized.go:1056-1207) */
+size_t orc_messagebatch_marshal(const drb_message *ms, size_t n,
+                                const drb_entry *ents, const uint8_t *pool,
+                                uint64_t deployment_id, const char *src,
+                                size_t src_len, uint32_t bin_ver,
+                                uint8_t *buf);
+long orc_messagebatch_unmarshal(const uint8_t *buf, size_t len,
+                                drb_message *ms, size_t cap, drb_entry *ents,
+                                size_t ent_cap, uint8_t *pool, size_t pool_cap,
+                                uint64_t *deployment_id, uint32_t *bin_ver,
+                                char *src, size_t src_cap, size_t *src_len);
+/* requestHeader encode / decode (internal/transport/tcp.go:64-112) and the
+ * writeMessage frame (tcp.go:142-178) */
+void orc_request_header_encode(uint16_t method, uint64_t size, uint32_t crc,
+                               uint8_t *buf18);
+int orc_request_header_decode(const uint8_t *buf18, uint16_t *method,
+                              uint64_t *size, uint32_t *crc);
+size_t orc_wire_frame(const uint8_t *payload, size_t n, uint8_t *out);
 /* PBKV codec (internal/tests/kvpb/kv.go) */
 size_t orc_pbkv_marshal(const uint8_t *key, uint32_t klen, const uint8_t *val,
                         uint32_t vlen, uint8_t *buf);

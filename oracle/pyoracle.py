@@ -159,6 +159,27 @@ def _declare(L):
                                                 C.c_size_t, PU8, C.c_size_t]),
         "orc_crc32_ieee": (C.c_uint32, [PU8, C.c_size_t]),
         "orc_pbkv_marshal": (C.c_size_t, [PU8, U32, PU8, U32, PU8]),
+        "orc_message_size": (C.c_size_t, [PM, PE]),
+        "orc_message_marshal": (C.c_size_t, [PM, PE, PU8, PU8]),
+        "orc_message_unmarshal": (C.c_long, [PU8, C.c_size_t, PM, PE,
+                                             C.c_size_t,
+                                             C.POINTER(C.c_size_t), PU8,
+                                             C.c_size_t,
+                                             C.POINTER(C.c_size_t)]),
+        "orc_messagebatch_marshal": (C.c_size_t, [PM, C.c_size_t, PE, PU8,
+                                                  U64, C.c_char_p,
+                                                  C.c_size_t, U32, PU8]),
+        "orc_messagebatch_unmarshal": (C.c_long, [PU8, C.c_size_t, PM,
+                                                  C.c_size_t, PE, C.c_size_t,
+                                                  PU8, C.c_size_t,
+                                                  C.POINTER(U64), PU32,
+                                                  C.c_char_p, C.c_size_t,
+                                                  C.POINTER(C.c_size_t)]),
+        "orc_request_header_encode": (None, [C.c_uint16, U64, U32, PU8]),
+        "orc_request_header_decode": (C.c_int, [PU8,
+                                                C.POINTER(C.c_uint16),
+                                                C.POINTER(U64), PU32]),
+        "orc_wire_frame": (C.c_size_t, [PU8, C.c_size_t, PU8]),
         "orc_pbkv_unmarshal": (C.c_int, [PU8, C.c_size_t,
                                          C.POINTER(PU8), PU32,
                                          C.POINTER(PU8), PU32]),
@@ -696,3 +717,74 @@ def pbkv_unmarshal(data):
     if rc:
         raise ValueError("pbkv unmarshal failed")
     return bytes(kp[:kl.value]), bytes(vp[:vl.value])
+
+
+# pb.Message / pb.MessageBatch (raftpb/message.go, messagebatch.go,
+# raft_optimized.go:659-1207) and the TCP frame (internal/transport/tcp.go)
+TRANSPORT_BIN_VERSION = 210  # raftio/binversion.go:30
+
+
+def _msg_cmd_bytes(msgs):
+    return sum(len(e["cmd"]) for m in msgs for e in m["entries"])
+
+
+def message_marshal(m):
+    marr, n, earr, pool = build_messages([m])
+    size = lib().orc_message_size(marr, earr)
+    buf = (C.c_uint8 * max(1, size))()
+    w = lib().orc_message_marshal(marr, earr, pool, buf)
+    assert w == size
+    return bytes(buf[:w])
+
+
+def messagebatch_marshal(msgs, deployment_id=0, source=b"",
+                         bin_ver=TRANSPORT_BIN_VERSION):
+    marr, n, earr, pool = build_messages(msgs)
+    cap = 64 + len(source) + sum(
+        32 + 12 * 11 + 26 + sum(64 + len(e["cmd"]) for e in m["entries"])
+        for m in msgs)
+    buf = (C.c_uint8 * cap)()
+    w = lib().orc_messagebatch_marshal(marr, n, earr, pool, deployment_id,
+                                       source, len(source), bin_ver, buf)
+    assert w <= cap
+    return bytes(buf[:w])
+
+
+def messagebatch_unmarshal(data, cap=4096):
+    """-> (messages, deployment_id, source, bin_ver); ValueError when
+    malformed, NotImplementedError for a non-empty Snapshot."""
+    marr = (Message * cap)()
+    earr = (Entry * cap)()
+    pool = (C.c_uint8 * max(1, len(data)))()
+    did, bv, sl = U64(), U32(), C.c_size_t()
+    src = C.create_string_buffer(max(1, len(data)))
+    n = lib().orc_messagebatch_unmarshal(_u8(data), len(data), marr, cap,
+                                         earr, cap, pool, len(data),
+                                         C.byref(did), bv, src, len(data),
+                                         C.byref(sl))
+    if n == -2:
+        raise NotImplementedError("non-empty snapshot")
+    if n < 0:
+        raise ValueError("messagebatch unmarshal failed")
+    return (_unpack_messages(marr, n, earr, pool), did.value,
+            src.raw[:sl.value], bv.value)
+
+
+def request_header_encode(method, size, crc):
+    b = (C.c_uint8 * 18)()
+    lib().orc_request_header_encode(method, size, crc, b)
+    return bytes(b)
+
+
+def request_header_decode(b):
+    me, sz, crc = C.c_uint16(), U64(), U32()
+    if lib().orc_request_header_decode(_u8(b), C.byref(me), C.byref(sz),
+                                       crc):
+        return None
+    return me.value, sz.value, crc.value
+
+
+def wire_frame(payload):
+    out = (C.c_uint8 * (len(payload) + 20))()
+    n = lib().orc_wire_frame(_u8(payload), len(payload), out)
+    return bytes(out[:n])
