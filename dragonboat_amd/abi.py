@@ -136,6 +136,17 @@ PLANE_C1 = 1 << 16
 PLANE_REP = 1 << 17
 
 
+class WireCfg(C.Structure):
+    _fields_ = [("deployment_id", C.c_uint64),
+                ("source_address", C.c_char_p), ("source_len", C.c_uint32),
+                ("bin_ver", C.c_uint32), ("max_batch_bytes", C.c_uint64)]
+
+
+class WireOut(C.Structure):
+    _fields_ = [("n_msgs", C.c_uint64), ("n_frames", C.c_uint64),
+                ("n_bytes", C.c_uint64)]
+
+
 class RoundIn(C.Structure):
     _fields_ = [("tick", C.c_uint32), ("prop_slot", C.c_uint32),
                 ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),

@@ -12,7 +12,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libdrb_engine.so")
 SOURCES = ["drb_engine.hip"]
-HEADERS = ["drb_layout.hpp", "drb_msg.hpp", "drb_step.hpp", "drb_codec.hpp"]
+HEADERS = ["drb_layout.hpp", "drb_msg.hpp", "drb_step.hpp", "drb_codec.hpp",
+           "drb_wire.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 

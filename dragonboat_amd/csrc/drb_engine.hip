@@ -45,8 +45,10 @@ struct drb_engine {
   unsigned long long *ctr_total = nullptr;   // their sum (read_counters)
   void *scratch;
   size_t scratch_bytes;
+  struct WireState *wire = nullptr;          // drb_encode_wire (drb_wire.hpp)
 };
 
+static void wire_free(drb_engine *e);
 static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 static int refresh_roles(drb_engine *e);
 
@@ -313,6 +315,7 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   (void)hipStreamSynchronize(e->stream2);
   for (void *p : e->allocs) (void)hipFree(p);
   if (e->scratch) (void)hipFree(e->scratch);
+  wire_free(e);
   (void)hipEventDestroy(e->ev_fork);
   (void)hipEventDestroy(e->ev_join);
   (void)hipStreamDestroy(e->stream2);
@@ -1731,3 +1734,6 @@ extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
   HIPCHK(hipStreamSynchronize(e->stream));
   return DRB_OK;
 }
+
+// ---------------------------------------------------------------- wire
+#include "drb_wire.hpp"

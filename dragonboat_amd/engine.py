@@ -9,7 +9,8 @@ import os
 
 from . import abi
 from .abi import (Config, Entry, Message, ReadyToRead, Region, ReplicaState,
-                  RoundIn, RoundOut, entry_to_tuple, message_to_tuple)
+                  RoundIn, RoundOut, WireCfg, WireOut, entry_to_tuple,
+                  message_to_tuple)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DRB_ENGINE_LIB") or \
@@ -74,6 +75,10 @@ SIGNATURES = {
     "drb_plane_regions": (C.c_int, [P, U32, U32, U32, C.c_int,
                                     C.POINTER(Region)]),
     "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
+    "drb_encode_wire": (C.c_int, [P, U32, U32, C.POINTER(WireCfg),
+                                  C.POINTER(WireOut)]),
+    "drb_wire_buffer": (C.c_int, [P, C.POINTER(P), PU64]),
+    "drb_export_wire": (C.c_int, [P, PU8, SZ, C.POINTER(SZ)]),
 }
 
 
@@ -338,6 +343,24 @@ class Engine:
         rc = _ck(lib().drb_kv_lookup(self.h, g, slot, _u8(key), len(key),
                                      val, vcap, C.byref(vl)), "drb_kv_lookup")
         return None if rc == 1 else bytes(val[:vl.value])
+
+    def encode_wire(self, from_slot, to_slot, deployment_id=0,
+                    source=b"", bin_ver=210, max_batch=0, fetch=True):
+        """drb_encode_wire: the TCP byte stream (framed MessageBatches) of
+        the messages slot from_slot sent to slot to_slot last round.
+        Returns (WireOut dict, bytes or None)."""
+        cfg = WireCfg(deployment_id, source, len(source), bin_ver, max_batch)
+        out = WireOut()
+        _ck(lib().drb_encode_wire(self.h, from_slot, to_slot, C.byref(cfg),
+                                  C.byref(out)), "drb_encode_wire")
+        res = {f: getattr(out, f) for f, _ in WireOut._fields_}
+        if not fetch:
+            return res, None
+        buf = (C.c_uint8 * max(1, out.n_bytes))()
+        n = SZ()
+        _ck(lib().drb_export_wire(self.h, buf, out.n_bytes, C.byref(n)),
+            "drb_export_wire")
+        return res, bytes(buf[:n.value])
 
     def crc32_batch(self, buffers):
         data = b"".join(buffers)

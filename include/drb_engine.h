@@ -505,6 +505,44 @@ int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data, size_t data_len,
                          const uint64_t *off, const uint32_t *len, size_t n,
                          uint32_t *crc);
 
+/* --- wire path to replicas on other machines (raftpb MessageBatch) ---- */
+
+/* MessageBatch fields Transport.processMessages sets
+ * (internal/transport/transport.go:447-458) and the batch cut it applies. */
+typedef struct drb_wire_cfg {
+  uint64_t deployment_id;      /* NodeHostConfig.GetDeploymentID() */
+  const char *source_address;  /* Transport.sourceID (RaftAddress) */
+  uint32_t source_len;         /* <= 256 */
+  uint32_t bin_ver;            /* raftio.TransportBinVersion = 210 */
+  uint64_t max_batch_bytes;    /* settings.MaxMessageBatchSize; 0 = 64 MiB */
+} drb_wire_cfg;
+
+typedef struct drb_wire_out {
+  uint64_t n_msgs;    /* pb.Messages encoded */
+  uint64_t n_frames;  /* MessageBatches (TCP frames) */
+  uint64_t n_bytes;   /* stream length */
+} drb_wire_out;
+
+/* Replaces, for every group, Transport.Send (transport.go:346) of the
+ * messages replica slot from_slot sent to replica slot to_slot in the last
+ * round, through processMessages -> sendMessageBatch -> writeMessage
+ * (transport.go:443-508, tcp.go:142-178): encodes them on the device as
+ * the byte stream of the TCP connection to the NodeHost hosting slot
+ * to_slot -- per batch magic 0xAE7D, the 18-byte requestHeader (method
+ * 100, size, header CRC32, payload CRC32) and the MessageBatch payload
+ * (messagebatch.go:23-51, message.go:32-90, colfer Entries
+ * raft_optimized.go:166-300).  Messages are taken group by group in shard
+ * order, in send order within a group; a batch is cut where the sum of
+ * Message.SizeUpperLimit (raft_optimized.go:1210) reaches max_batch_bytes,
+ * the crossing message travelling alone (transport.go:481-500).  The
+ * stream stays in an engine-owned device buffer until the next call. */
+int drb_encode_wire(drb_engine *e, uint32_t from_slot, uint32_t to_slot,
+                    const drb_wire_cfg *cfg, drb_wire_out *out);
+/* Device pointer and length of the last drb_encode_wire stream. */
+int drb_wire_buffer(drb_engine *e, const uint8_t **dev, uint64_t *len);
+/* Copies that stream to host memory (synchronises the engine stream). */
+int drb_export_wire(drb_engine *e, uint8_t *out, size_t cap, size_t *len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,8 @@ STRUCTS = {
     "drb_config": abi.Config,
     "drb_round_in": abi.RoundIn,
     "drb_round_out": abi.RoundOut,
+    "drb_wire_cfg": abi.WireCfg,
+    "drb_wire_out": abi.WireOut,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}
