@@ -147,6 +147,13 @@ class WireOut(C.Structure):
                 ("n_bytes", C.c_uint64)]
 
 
+class WireIn(C.Structure):
+    _fields_ = [("frames", C.c_uint64), ("messages", C.c_uint64),
+                ("accepted", C.c_uint64), ("dropped", C.c_uint64),
+                ("snapshots", C.c_uint64), ("consumed", C.c_uint64),
+                ("bad", C.c_uint64)]
+
+
 class RoundIn(C.Structure):
     _fields_ = [("tick", C.c_uint32), ("prop_slot", C.c_uint32),
                 ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),

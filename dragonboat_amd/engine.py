@@ -9,7 +9,7 @@ import os
 
 from . import abi
 from .abi import (Config, Entry, Message, ReadyToRead, Region, ReplicaState,
-                  RoundIn, RoundOut, WireCfg, WireOut, entry_to_tuple,
+                  RoundIn, RoundOut, WireCfg, WireIn, WireOut, entry_to_tuple,
                   message_to_tuple)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -79,6 +79,7 @@ SIGNATURES = {
                                   C.POINTER(WireOut)]),
     "drb_wire_buffer": (C.c_int, [P, C.POINTER(P), PU64]),
     "drb_export_wire": (C.c_int, [P, PU8, SZ, C.POINTER(SZ)]),
+    "drb_ingest_wire": (C.c_int, [P, PU8, SZ, U64, C.POINTER(WireIn)]),
 }
 
 
@@ -361,6 +362,13 @@ class Engine:
         _ck(lib().drb_export_wire(self.h, buf, out.n_bytes, C.byref(n)),
             "drb_export_wire")
         return res, bytes(buf[:n.value])
+
+    def ingest_wire(self, data, deployment_id=0):
+        """drb_ingest_wire: a TCP byte stream of framed MessageBatches."""
+        res = WireIn()
+        _ck(lib().drb_ingest_wire(self.h, _u8(data), len(data), deployment_id,
+                                  C.byref(res)), "drb_ingest_wire")
+        return {f: getattr(res, f) for f, _ in WireIn._fields_}
 
     def crc32_batch(self, buffers):
         data = b"".join(buffers)

@@ -543,6 +543,26 @@ int drb_wire_buffer(drb_engine *e, const uint8_t **dev, uint64_t *len);
 /* Copies that stream to host memory (synchronises the engine stream). */
 int drb_export_wire(drb_engine *e, uint8_t *out, size_t cap, size_t *len);
 
+typedef struct drb_wire_in {
+  uint64_t frames;     /* frames read */
+  uint64_t messages;   /* pb.Messages decoded and handed to drb_ingest */
+  uint64_t accepted;   /* placed into the next round's inbox */
+  uint64_t dropped;    /* DeploymentId / BinVer mismatch or drb_ingest drop */
+  uint64_t snapshots;  /* snapshot chunks / InstallSnapshot (CPU path) */
+  uint64_t consumed;   /* stream bytes consumed */
+  uint64_t bad;        /* 1: stopped at a bad frame (ErrBadMessage) */
+} drb_wire_in;
+
+/* The receiving end of that connection, for replicas hosted here whose
+ * peers are elsewhere: readMessage (tcp.go:180-237: header and payload
+ * CRC32), MessageBatch / Message / colfer Entry Unmarshal
+ * (raft_optimized.go:308-656, 659-983, 1056-1207), the DeploymentId /
+ * BinVer filter of Transport.handleRequest (transport.go:305-316), then
+ * drb_ingest.  Frames are consumed in order; a bad frame stops the stream
+ * as ErrBadMessage closes the connection. */
+int drb_ingest_wire(drb_engine *e, const uint8_t *stream, size_t len,
+                    uint64_t deployment_id, drb_wire_in *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,7 @@ STRUCTS = {
     "drb_round_out": abi.RoundOut,
     "drb_wire_cfg": abi.WireCfg,
     "drb_wire_out": abi.WireOut,
+    "drb_wire_in": abi.WireIn,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}

@@ -116,3 +116,131 @@ def test_wire_large_plane_properties():
         exp = [wr.tuple_to_msg(t) for t in eng.export_outbox(g, 0)
                if t[2] == 2]
         assert by_shard.get(first + g, []) == exp, g
+
+
+class TwoNodes:
+    """Two engines as two NodeHosts joined by the wire path: `lead` hosts
+    replica slot 0 (the leaders) of every group, `foll` hosts the other
+    slots.  After each round every plane crosses as a TCP byte stream
+    (drb_encode_wire -> drb_ingest_wire); one oracle cluster with every
+    replica co-resident is the reference."""
+
+    def __init__(self, G, R=3, seed=0x5EEDD8B0, did=0xD1D):
+        from dragonboat_amd import abi
+        from dragonboat_amd.engine import Engine
+        self.G, self.R, self.seed, self.did = G, R, seed, did
+        self.orc = po.Cluster(G, R, seed=seed)
+        self.orc.setup_steady(0)
+        self.lead = Engine(num_groups=G, num_replicas=R)
+        self.foll = Engine(num_groups=G, num_replicas=R)
+        for eng, mine in ((self.lead, {0}), (self.foll, set(range(1, R)))):
+            eng.init_steady(term=2, leader_slot=0, seed=seed)
+            sts = eng.export_replicas(0, G)
+            for i in range(len(sts)):
+                if i % R not in mine:
+                    sts[i].flags &= ~abi.F_HOSTED
+            eng.import_replicas(0, sts)
+        self.rounds = 0
+        self.wire_bytes = 0
+
+    def round(self, k=1, tick=False, read_index=False):
+        from dragonboat_amd import abi, workload
+        pin = ri_in = abi.DRB_NONE
+        if k:
+            counts, ents, pool = workload.build_batch(
+                self.G, k, self.seed, self.rounds, 256, 4, None)
+            self.orc.stage_proposals(counts, k, ents, pool)
+            mp = self.lead.cfg["max_props"]
+            eents = (abi.Entry * (self.G * mp))()
+            for g in range(self.G):
+                for j in range(counts[g]):
+                    eents[g * mp + j] = ents[g * k + j]
+            self.lead.stage_proposals(0, counts, eents, pool)
+            pin = 0
+        if read_index:
+            lo, hi = workload.build_read_index(self.G, self.seed, self.rounds,
+                                               self.rounds + 30, None)
+            self.orc.stage_read_index(lo, hi)
+            self.lead.stage_read_index(0, lo, hi)
+            ri_in = 0
+        o = self.orc.round(tick=tick)
+        a = self.lead.step(tick=tick, prop_slot=pin, ri_slot=ri_in)
+        b = self.foll.step(tick=tick)
+        self.rounds += 1
+        for s in range(1, self.R):
+            self._cross(self.lead, self.foll, 0, s)
+            self._cross(self.foll, self.lead, s, 0)
+        return o, a, b
+
+    def _cross(self, src, dst, frm, to):
+        res, data = src.encode_wire(frm, to, self.did, SRC)
+        self.wire_bytes += len(data)
+        got = dst.ingest_wire(data, self.did)
+        assert got["bad"] == 0 and got["consumed"] == len(data), got
+        assert got["messages"] == res["n_msgs"] == got["accepted"], got
+
+    def check(self):
+        errs = []
+        from tests.gpu_harness import by_dest, state_diff
+        for g in range(self.G):
+            for s in range(self.R):
+                eng = self.lead if s == 0 else self.foll
+                a, b = eng.export_replicas(g, 1)[s], self.orc.export(g, s)
+                d = state_diff(a, b, self.R)
+                if d:
+                    errs.append((g, s, "state", d))
+                    continue
+                if eng.kv_export(g, s) != self.orc.export_kv(g, s):
+                    errs.append((g, s, "kv"))
+                em = by_dest(eng.export_outbox(g, s))
+                om = by_dest(self.orc.export_outbox(g, s))
+                if em != om:
+                    errs.append((g, s, "msgs", em, om))
+                if eng.export_ready(g, s) != self.orc.export_ready(g, s):
+                    errs.append((g, s, "ready"))
+        return errs
+
+
+@pytest.mark.parametrize("R", [3, 5])
+def test_two_nodehosts_over_the_wire(R):
+    """Leaders on one engine, followers on another, every message crossing
+    as dragonboat TCP bytes: bit-exact with one co-resident oracle cluster
+    (writes, ticks, ReadIndex)."""
+    t = TwoNodes(G=32, R=R)
+    for r in range(8):
+        o, a, b = t.round(k=1 + (r % 3 == 2), tick=(r % 2 == 0),
+                          read_index=(r % 3 == 1))
+        for x in (a, b):
+            assert x.fallbacks == 0 and x.errors == 0, (r, x.to_dict())
+        assert a.committed_entries + b.committed_entries == \
+            o.committed_entries, r
+        errs = t.check()
+        assert not errs, (r, errs[:2])
+    assert t.wire_bytes > 0
+
+
+def test_ingest_wire_filters_and_bad_frames():
+    """transport.go:305-316: a batch of another deployment (or BinVer) is
+    dropped whole; tcp.go:180-237: a corrupted frame stops the stream
+    (ErrBadMessage), frames before it are delivered."""
+    t = TwoNodes(G=16)
+    t.round(k=1, tick=True)
+    # the round's wire traffic was delivered by round(); make a fresh
+    # stream of the same round and deliver it with the wrong deployment
+    res, data = t.lead.encode_wire(0, 1, t.did + 1, SRC)
+    got = t.foll.ingest_wire(data, t.did)
+    assert got["accepted"] == 0 and got["dropped"] == res["n_msgs"] > 0
+    # two frames (one message each, max_batch=1), the second corrupted
+    res, data = t.lead.encode_wire(0, 1, t.did, SRC, max_batch=1)
+    frames = wr.parse_stream(data)
+    first = 20 + len(frames[0])
+    bad = bytearray(data)
+    bad[first + 25] ^= 0x40
+    got = t.foll.ingest_wire(bytes(bad), t.did)
+    assert got["bad"] == 1 and got["frames"] == 1
+    assert got["consumed"] == first and got["messages"] == 1
+    # a snapshot-chunk frame (method 200) is skipped, not fatal
+    chunk = b"\xae\x7d" + po.request_header_encode(200, 3, wr.zlib.crc32(
+        b"abc")) + b"abc"
+    got = t.foll.ingest_wire(chunk + data[:first], t.did)
+    assert got["bad"] == 0 and got["snapshots"] == 1 and got["frames"] == 2
