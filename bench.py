@@ -92,6 +92,8 @@ def parse():
                     help="served reads inside the round's kernels or as "
                          "their own launch (drb_serve_reads)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-wire", action="store_true",
+                    help="skip the off-GPU wire encode measurement (C3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -295,6 +297,26 @@ def main():
         alg = alg_bytes_per_group_round(R, k, 16, reads, c4 and world > 1) * \
             g_here
     achieved = alg / (kern_ms * 1e-3) / 1e9
+    wire = None
+    if not (c4 or c5 or args.no_wire):
+        # after the timed region: the last round's leader -> follower-slot-1
+        # plane as dragonboat's TCP stream (drb_encode_wire), as if every
+        # slot-1 replica lived on one remote NodeHost
+        reps, wt = 5, []
+        for _ in range(reps):
+            w0 = time.perf_counter()
+            wres, _ = eng.encode_wire(0, 1, 1, b"10.0.0.1:26001", fetch=False)
+            eng.sync()
+            wt.append(time.perf_counter() - w0)
+        wms = sorted(wt)[reps // 2] * 1e3
+        wire = {"plane": "slot 0 -> slot 1 (leaders -> one follower host)",
+                "messages": wres["n_msgs"], "frames": wres["n_frames"],
+                "bytes": wres["n_bytes"], "ms": wms,
+                "GB_per_s": wres["n_bytes"] / (wms * 1e-3) / 1e9,
+                "messages_per_s": wres["n_msgs"] / (wms * 1e-3),
+                "note": "median of %d drb_encode_wire calls (5 kernels + one "
+                        "host sync for the plan), outside the timed "
+                        "region" % reps}
     if out.fallbacks or out.errors:
         print("WARNING: fallbacks=%d errors=%d" % (out.fallbacks, out.errors),
               file=sys.stderr)
@@ -365,6 +387,8 @@ def main():
                          "saved_entries": out.saved_entries,
                          "saved_bytes": out.saved_bytes},
         }
+        if wire is not None:
+            res["wire"] = wire
         if xch is not None:
             res["exchange"] = {"bytes_sent_per_round_rank0":
                                xch.bytes_sent / K}

@@ -48,7 +48,15 @@ constexpr uint32_t WIRE_EMPTY_SNAPSHOT_FIELD = 26;  // 0x62 0x18 + 24 B
 
 // x^(2^k) mod P, k = 0..31, reflected (zlib x2n_table)
 __constant__ uint32_t c_x2n[32];
-__constant__ uint32_t c_crc_byte[256];
+// slicing-by-4 tables (c_crc_s4[0..255]: the byte table), staged into LDS
+// per block
+__constant__ uint32_t c_crc_s4[4 * 256];
+
+DRB_DEV void crc_s4_stage(uint32_t *t) {
+  for (uint32_t i = threadIdx.x; i < 4 * 256; i += blockDim.x)
+    t[i] = c_crc_s4[i];
+  __syncthreads();
+}
 
 __host__ __device__ inline uint32_t gf2_multmodp(uint32_t a, uint32_t b) {
   uint32_t m = 1u << 31, p = 0;
@@ -192,18 +200,24 @@ DRB_DEV void wire_sizes(const View &v, const WireArgs &a, uint64_t g,
 // Bytes at absolute stream offsets.  A lane owns [start, pos); chunks it
 // owns entirely leave as 16 B stores, the chunks it shares with its
 // neighbours (its first and last) as byte stores of its own bytes.
+// The CRC advances a 32-bit word at a time through slicing-by-4 tables in
+// LDS (one dependent table step per 4 bytes).
 struct StreamOut {
   uint8_t *base;
+  const uint32_t *tab;  // LDS: 4 x 256 slicing tables
   uint64_t start, pos;
   uint64_t lo, hi;
-  uint32_t crc;
+  uint32_t crc, cw, cn;
 };
 
-DRB_DEV void so_init(StreamOut &o, uint8_t *base, uint64_t at) {
+DRB_DEV void so_init(StreamOut &o, uint8_t *base, uint64_t at,
+                     const uint32_t *tab) {
   o.base = base;
+  o.tab = tab;
   o.start = o.pos = at;
   o.lo = o.hi = 0;
   o.crc = 0xffffffffu;
+  o.cw = o.cn = 0;
 }
 
 DRB_DEV void so_store(StreamOut &o, uint64_t cbase, uint32_t end) {
@@ -222,7 +236,13 @@ DRB_DEV void so_store(StreamOut &o, uint64_t cbase, uint32_t end) {
 
 DRB_DEV void so_byte(StreamOut &o, uint32_t b) {
   b &= 0xffu;
-  o.crc = c_crc_byte[(o.crc ^ b) & 0xffu] ^ (o.crc >> 8);
+  o.cw |= b << (8 * o.cn);
+  if (++o.cn == 4) {
+    const uint32_t x = o.crc ^ o.cw;
+    o.crc = o.tab[3 * 256 + (x & 0xffu)] ^ o.tab[2 * 256 + ((x >> 8) & 0xffu)] ^
+            o.tab[256 + ((x >> 16) & 0xffu)] ^ o.tab[x >> 24];
+    o.cw = o.cn = 0;
+  }
   const uint32_t s = (uint32_t)(o.pos & 15);
   if (s < 8)
     o.lo |= (uint64_t)b << (8 * s);
@@ -235,6 +255,9 @@ DRB_DEV void so_byte(StreamOut &o, uint32_t b) {
 // flushes the partial tail chunk; returns the run's CRC32-IEEE
 DRB_DEV uint32_t so_finish(StreamOut &o) {
   if (o.pos & 15) so_store(o, o.pos & ~15ull, (uint32_t)(o.pos & 15));
+  for (uint32_t i = 0; i < o.cn; ++i)
+    o.crc = o.tab[(o.crc ^ (o.cw >> (8 * i))) & 0xffu] ^ (o.crc >> 8);
+  o.cw = o.cn = 0;
   return o.crc ^ 0xffffffffu;
 }
 
@@ -453,62 +476,18 @@ DRB_DEV uint64_t wire_group_of(const uint64_t *pcnt, uint64_t G,
   return lo;
 }
 
-// message-level prefix inside group g: byte / upper offsets of message q
-DRB_DEV void wire_msg_prefix(const View &v, const WireArgs &a, uint64_t g,
-                             uint32_t q, const uint64_t *pbytes,
-                             const uint64_t *pupper, uint64_t &boff,
-                             uint64_t &uoff, uint64_t &ub) {
-  WireCursor c;
-  wc_init(c, v, a, g);
-  boff = pbytes[g];
-  uoff = pupper[g];
-  for (uint32_t k = 0; k <= q && k < c.k; ++k) {
-    const WireMsg w = wc_next(c, v, a, g);
-    uint64_t ms, mb, mu;
-    wire_sizes(v, a, g, w, ms, mb, mu);
-    if (k == q) {
-      ub = mu;
-      return;
-    }
-    boff += mb;
-    uoff += mu;
-  }
-  ub = 0;
-}
-
-// upper-limit prefix through message ordinal j (inclusive)
-DRB_DEV uint64_t wire_upper_incl(const View &v, const WireArgs &a,
-                                 const uint64_t *pcnt, const uint64_t *pbytes,
-                                 const uint64_t *pupper, uint64_t j) {
-  const uint64_t g = wire_group_of(pcnt, v.G, j);
-  uint64_t bo, uo, ub;
-  wire_msg_prefix(v, a, g, (uint32_t)(j - pcnt[g]), pbytes, pupper, bo, uo,
-                  ub);
-  return uo + ub;
-}
-
-DRB_DEV uint64_t wire_byte_off(const View &v, const WireArgs &a,
-                               const uint64_t *pcnt, const uint64_t *pbytes,
-                               const uint64_t *pupper, uint64_t j,
-                               uint64_t total_msgs, uint64_t total_bytes) {
-  if (j >= total_msgs) return total_bytes;
-  const uint64_t g = wire_group_of(pcnt, v.G, j);
-  uint64_t bo, uo, ub;
-  wire_msg_prefix(v, a, g, (uint32_t)(j - pcnt[g]), pbytes, pupper, bo, uo,
-                  ub);
-  return bo;
-}
-
 // Transport.processMessages' cut points (transport.go:459-500) with the
-// queue drained in one go
+// queue drained in one go.  One thread; per frame one binary search over
+// the group-level upper-limit prefix and one walk of the group where the
+// limit is reached.
 __global__ void k_wire_plan(const View v, const WireArgs a,
                             const uint64_t *pcnt, const uint64_t *pbytes,
                             const uint64_t *pupper, const uint64_t *tot,
                             WireFrame *fr, WirePlan *plan) {
   if (threadIdx.x || blockIdx.x) return;
-  const uint64_t M = tot[0], B = tot[1];
-  uint64_t nf = 0, off = 0, s = 0, ovf = 0;
-  auto emit = [&](uint64_t first, uint64_t last) {
+  const uint64_t M = tot[0], B = tot[1], U = tot[2];
+  uint64_t nf = 0, off = 0, ovf = 0;
+  auto emit = [&](uint64_t first, uint64_t last, uint64_t b0, uint64_t b1) {
     if (nf >= WIRE_MAX_FRAMES) {
       ovf = 1;
       return;
@@ -516,41 +495,55 @@ __global__ void k_wire_plan(const View v, const WireArgs a,
     WireFrame f;
     f.first = first;
     f.last = last;
-    f.msg_off = wire_byte_off(v, a, pcnt, pbytes, pupper, first, M, B);
-    f.msg_bytes =
-        wire_byte_off(v, a, pcnt, pbytes, pupper, last + 1, M, B) - f.msg_off;
+    f.msg_off = b0;
+    f.msg_bytes = b1 - b0;
     f.off = off;
     f.crc = 0;
     f.pad = 0;
     fr[nf++] = f;
     off += 20 + f.msg_bytes + a.trailer;
   };
+  // s: first message of the next batch; bs: its byte offset; base: the
+  // upper-limit prefix before it
+  uint64_t s = 0, bs = 0, base = 0;
   while (s < M && !ovf) {
-    const uint64_t base =
-        s ? wire_upper_incl(v, a, pcnt, pbytes, pupper, s - 1) : 0;
-    // smallest j >= s whose inclusive upper prefix reaches base + max
-    uint64_t lo = s, hi = M;  // first j in [lo, hi] with the property; M =
-                              // none
+    const uint64_t T = base + a.max_batch;
+    if (U < T) {  // the queue drains before the limit: one batch
+      emit(s, M - 1, bs, B);
+      break;
+    }
+    // the group whose messages reach T: smallest g with prefix(g+1) >= T
+    uint64_t lo = wire_group_of(pcnt, v.G, s), hi = v.G - 1;
     while (lo < hi) {
       const uint64_t mid = lo + (hi - lo) / 2;
-      if (wire_upper_incl(v, a, pcnt, pbytes, pupper, mid) - base >=
-          a.max_batch)
+      if ((mid + 1 < v.G ? pupper[mid + 1] : U) >= T)
         hi = mid;
       else
         lo = mid + 1;
     }
-    const uint64_t j = lo;
-    if (j >= M) {
-      emit(s, M - 1);
-      s = M;
-    } else if (j == s) {
-      emit(s, s);
-      s = s + 1;
-    } else {
-      emit(s, j - 1);
-      emit(j, j);
-      s = j + 1;
+    WireCursor c;
+    wc_init(c, v, a, lo);
+    uint64_t u = pupper[lo], bj = pbytes[lo], mbj = 0;
+    uint32_t q = 0;
+    for (; q < c.k; ++q) {
+      const WireMsg w = wc_next(c, v, a, lo);
+      uint64_t ms, mb, mu;
+      wire_sizes(v, a, lo, w, ms, mb, mu);
+      u += mu;
+      mbj = mb;
+      if (u >= T) break;
+      bj += mb;
     }
+    const uint64_t j = pcnt[lo] + q;  // the message that reaches the limit
+    if (j == s) {
+      emit(s, s, bs, bj + mbj);
+    } else {
+      emit(s, j - 1, bs, bj);
+      emit(j, j, bj, bj + mbj);
+    }
+    s = j + 1;
+    bs = bj + mbj;
+    base = u;
   }
   plan->n_msgs = M;
   plan->n_frames = nf;
@@ -577,6 +570,8 @@ __global__ __launch_bounds__(256) void k_wire_encode(
     uint8_t *out) {
   __shared__ uint32_t blk_crc;
   __shared__ uint32_t blk_frame;
+  __shared__ uint32_t tab[4 * 256];
+  crc_s4_stage(tab);
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nf = (uint32_t)plan->n_frames;
   const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x;
@@ -618,7 +613,7 @@ __global__ __launch_bounds__(256) void k_wire_encode(
       const WireFrame &F = fr[f];
       const uint64_t at = F.off + 20 + (boff - F.msg_off);
       if (!open) {
-        so_init(o, out, at);
+        so_init(o, out, at, tab);
         open = true;
       }
       so_message(o, v, a, g, w, ms);
@@ -639,12 +634,14 @@ DRB_DEV void put_be(uint8_t *p, uint64_t x, int n) {
 __global__ void k_wire_finish(const WireArgs a, const uint8_t *src,
                               WireFrame *fr, const WirePlan *plan,
                               uint8_t *out) {
+  __shared__ uint32_t tab[4 * 256];
+  crc_s4_stage(tab);
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= plan->n_frames) return;
   const WireFrame F = fr[f];
   // MessageBatch trailer (messagebatch.go:41-50)
   StreamOut o;
-  so_init(o, out, F.off + 20 + F.msg_bytes);
+  so_init(o, out, F.off + 20 + F.msg_bytes, tab);
   so_byte(o, 0x10);
   so_varint(o, a.deployment_id);
   so_byte(o, 0x1a);
@@ -662,7 +659,7 @@ __global__ void k_wire_finish(const WireArgs a, const uint8_t *src,
   put_be(h + 12, 0, 4);
   put_be(h + 16, pcrc, 4);
   uint32_t c = 0xffffffffu;
-  for (int k = 2; k < 20; ++k) c = c_crc_byte[(c ^ h[k]) & 0xffu] ^ (c >> 8);
+  for (int k = 2; k < 20; ++k) c = tab[(c ^ h[k]) & 0xffu] ^ (c >> 8);
   put_be(h + 12, c ^ 0xffffffffu, 4);
   for (int k = 0; k < 20; ++k) out[F.off + k] = h[k];
   fr[f].crc = pcrc;
@@ -697,7 +694,7 @@ static int wire_tables_ready = 0;
 
 static int wire_init(drb_engine *e) {
   if (!wire_tables_ready) {
-    uint32_t x2n[32], tab[256];
+    uint32_t x2n[32], tab[256], s4[4 * 256];
     uint32_t p = 1u << 30;  // x^1
     x2n[0] = p;
     for (int n = 1; n < 32; ++n) x2n[n] = p = drb::gf2_multmodp(p, p);
@@ -708,7 +705,13 @@ static int wire_init(drb_engine *e) {
       tab[i] = c;
     }
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(drb::c_x2n), x2n, sizeof(x2n)));
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(drb::c_crc_byte), tab, sizeof(tab)));
+    for (uint32_t i = 0; i < 256; ++i) {
+      s4[i] = tab[i];
+      for (int k = 1; k < 4; ++k)
+        s4[k * 256 + i] =
+            tab[s4[(k - 1) * 256 + i] & 0xff] ^ (s4[(k - 1) * 256 + i] >> 8);
+    }
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(drb::c_crc_s4), s4, sizeof(s4)));
     wire_tables_ready = 1;
   }
   if (e->wire) return DRB_OK;
