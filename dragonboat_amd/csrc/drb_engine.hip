@@ -1093,12 +1093,14 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   if (split) pl.n_reads = 0;
   // the EXT instantiation only where its paths can run (drb_step.hpp)
   const bool ext = e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves;
+  pl.nrows = nl;
+  pf.nrows = nf;
+  // one-dimensional grids, rows interleaved per XCD (block_pos)
   if (nl) {
     if (ext)
-      step_kernel<R, true, true><<<dim3(gx, nl), 256, 0, e->stream>>>(e->v, pl);
+      step_kernel<R, true, true><<<gx * nl, 256, 0, e->stream>>>(e->v, pl);
     else
-      step_kernel<R, true, false><<<dim3(gx, nl), 256, 0, e->stream>>>(e->v,
-                                                                       pl);
+      step_kernel<R, true, false><<<gx * nl, 256, 0, e->stream>>>(e->v, pl);
   }
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
@@ -1108,9 +1110,9 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   }
   if (nf) {
     if (ext)
-      step_kernel<R, false, true><<<dim3(gx, nf), 256, 0, sf>>>(e->v, pf);
+      step_kernel<R, false, true><<<gx * nf, 256, 0, sf>>>(e->v, pf);
     else
-      step_kernel<R, false, false><<<dim3(gx, nf), 256, 0, sf>>>(e->v, pf);
+      step_kernel<R, false, false><<<gx * nf, 256, 0, sf>>>(e->v, pf);
   }
   if (split) {
     (void)hipEventRecord(e->ev_join, e->stream2);
@@ -1159,7 +1161,7 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
     return DRB_ERANGE;
   RoundParams p;
   p.slots = 0;
-  p.pad = 0;
+  p.nrows = 1;
   p.round = e->round + 1;
   p.tick = in->tick ? 1 : 0;
   p.prop_slot = in->prop_slot;
@@ -1629,7 +1631,8 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
     }
   }
   const uint32_t cnt[2] = {served, deferred};
-  block_counters<true, C_READS, 2>(v, slot, cnt);
+  const BlockPos bp = {blockIdx.x, blockIdx.y, gridDim.x};
+  block_counters<true, C_READS, 2>(v, slot, bp, cnt);
 }
 
 extern "C" int drb_serve_reads(drb_engine *e, uint32_t reads_per_ctx,

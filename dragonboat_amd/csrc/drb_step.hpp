@@ -59,6 +59,10 @@ namespace drb {
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
+// interleave a launch's slot rows per XCD (block_pos); 0: row-major
+#ifndef DRB_PAIR_XCD
+#define DRB_PAIR_XCD 1
+#endif
 
 constexpr uint64_t MAX_ENTRY_SIZE = 64ull * 1024 * 1024;  // soft.go:186
 
@@ -1364,9 +1368,36 @@ struct RoundParams {
   uint32_t n_reads;    // reads served per released ctx (0: none)
   uint32_t key_space;  // served-read key space
   uint32_t encode_saves;
-  uint32_t slots;  // slot of blockIdx.y = (slots >> 4 * blockIdx.y) & 15
-  uint32_t pad;
+  uint32_t slots;  // slot of block row y = (slots >> 4 * y) & 15
+  uint32_t nrows;  // block rows (slots) of this launch; see block_pos
 };
+
+// The logical (x = group block, y = slot row) of this workgroup.  The
+// launch is one-dimensional, gx * nrows workgroups, and the dispatcher
+// deals consecutive workgroups round-robin over the 8 XCDs.  With gx a
+// multiple of 8 the rows are interleaved in runs of 8: workgroups 8k..8k+7
+// of a run of 8 * nrows are group blocks 8c..8c+7 of row k, so the R - 1
+// follower replicas of one group block land on the same XCD (same L2)
+// back to back and share the leader's window rows and mailbox lines there
+// (MI355X_MICROARCH.md: one L2 per XCD).  Otherwise rows are row-major.
+struct BlockPos {
+  uint32_t x, y, gx;
+};
+DRB_DEV BlockPos block_pos(const RoundParams &p) {
+  const uint32_t n = p.nrows ? p.nrows : 1u;
+  const uint32_t b = blockIdx.x, gx = gridDim.x / n;
+  BlockPos bp;
+  bp.gx = gx;
+  if (DRB_PAIR_XCD && n > 1 && (gx & 7u) == 0) {
+    const uint32_t run = b / (8u * n), w = b % (8u * n);
+    bp.y = w >> 3;
+    bp.x = run * 8u + (w & 7u);
+  } else {
+    bp.y = b / gx;
+    bp.x = b % gx;
+  }
+  return bp;
+}
 
 // Round counters: each workgroup owns one row of NUM_COUNTERS u64 in
 // v.counters ([2 roles][R slots][gridDim.x][NUM_COUNTERS]) and adds its
@@ -1381,7 +1412,7 @@ DRB_DEV uint32_t wave_sum(uint32_t x) {
 
 // counters [FIRST, FIRST + N) of this workgroup's row (256 threads)
 template <bool LEAD, int FIRST, int N>
-DRB_DEV void block_counters(const View &v, uint32_t slot,
+DRB_DEV void block_counters(const View &v, uint32_t slot, BlockPos bp,
                             const uint32_t (&c)[N]) {
   __shared__ uint32_t red[4][N];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1396,8 +1427,7 @@ DRB_DEV void block_counters(const View &v, uint32_t slot,
     const uint64_t s = (uint64_t)red[0][i] + red[1][i] + red[2][i] + red[3][i];
     if (s) {
       const uint64_t row =
-          ((uint64_t)(LEAD ? 0 : 1) * v.R + slot) * gridDim.x +
-          blockIdx.x;
+          ((uint64_t)(LEAD ? 0 : 1) * v.R + slot) * bp.gx + bp.x;
       v.counters[row * NUM_COUNTERS + FIRST + i] += s;
     }
   }
@@ -1406,8 +1436,9 @@ DRB_DEV void block_counters(const View &v, uint32_t slot,
 // one row per workgroup of xrows[role][from][to][block]:
 // K | E << 8 | flags << 16 (max, max, or over the block's lanes)
 template <bool LEAD>
-DRB_DEV void block_plane_summary(const View &v, uint32_t from, uint32_t to,
-                                 uint32_t K, uint32_t E, uint32_t fl) {
+DRB_DEV void block_plane_summary(const View &v, BlockPos bp, uint32_t from,
+                                 uint32_t to, uint32_t K, uint32_t E,
+                                 uint32_t fl) {
   __shared__ uint32_t red[4][3];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -1432,7 +1463,7 @@ DRB_DEV void block_plane_summary(const View &v, uint32_t from, uint32_t to,
       f |= red[w][2];
     }
     const uint64_t row = (((uint64_t)(LEAD ? 0 : 1) * v.R + from) * v.R + to) *
-                             gridDim.x + blockIdx.x;
+                             bp.gx + bp.x;
     v.xrows[row] = k | (e << 8) | (f << 16);
   }
 }
@@ -1452,10 +1483,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   // kernarg loads, and the pointers loaded from it are known to address
   // global memory (global_load/store, not flat: no LDS-counter waits)
   const View *vp = &v;
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const BlockPos bp = block_pos(p);
+  const uint64_t g = (uint64_t)bp.x * blockDim.x + threadIdx.x;
   // the slots this launch steps (4 bits each): a role's launch covers only
   // the slots where that role occurs (drb_engine.hip role map)
-  const uint32_t slot = (p.slots >> (4 * blockIdx.y)) & 0xfu;
+  const uint32_t slot = (p.slots >> (4 * bp.y)) & 0xfu;
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
@@ -1927,7 +1959,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           if (lo != ~0ull) E = (uint32_t)(last_final + 1 - lo);
         }
       }
-      block_plane_summary<LEAD>(v, slot, (uint32_t)s, K, E, fl);
+      block_plane_summary<LEAD>(v, bp, slot, (uint32_t)s, K, E, fl);
     }
   }
   const uint32_t cnt[NUM_COUNTERS] = {
@@ -1935,7 +1967,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
       (uint32_t)c_err,    c_served,            c_deferred,
       c_saved,            c_saved_bytes};
-  block_counters<LEAD, 0, NUM_COUNTERS>(v, slot, cnt);
+  block_counters<LEAD, 0, NUM_COUNTERS>(v, slot, bp, cnt);
 }
 
 }  // namespace drb
