@@ -59,9 +59,11 @@ namespace drb {
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
-// interleave a launch's slot rows per XCD (block_pos); 0: row-major
+// interleave a launch's slot rows per XCD (block_pos); 0: row-major.
+// Measured (profiles/r01_pair_xcd, r01_c4_pair): neutral at C3, 7 % slower
+// at C4 N=1 (four follower rows), so off by default
 #ifndef DRB_PAIR_XCD
-#define DRB_PAIR_XCD 1
+#define DRB_PAIR_XCD 0
 #endif
 
 constexpr uint64_t MAX_ENTRY_SIZE = 64ull * 1024 * 1024;  // soft.go:186
