@@ -205,11 +205,13 @@ def main():
         first_shard, seed = ddist.shard_plan(rank, G)
         vlen = C5_VAL[args.payload]
         cmd_cap = ((12 + (1 if vlen < 128 else 2) + vlen) + 15) // 16 * 16
-        NP = 8 if args.payload == 128 else 4
+        # proposals are drawn per round (seeded Bernoulli over the groups,
+        # salt = round) into two alternating staged batches
+        NP = 2
         bound = 73 + cmd_cap  # EntryBatch element bound (drb_codec.hpp)
         eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
                      max_props=max(1, k), prop_slots=NP, ri_slots=1,
-                     mailbox=6, kv_slots=16, kv_val_cap=vlen + 13 & ~15,
+                     mailbox=8, kv_slots=16, kv_val_cap=vlen + 13 & ~15,
                      kv_pool_blocks=2 * G * R if args.payload == 128
                      else G * R, save_cap=(4 * bound + 15) // 16 * 16,
                      first_shard_id=first_shard, device=local)
@@ -222,9 +224,7 @@ def main():
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
         if c5:
-            eng.gen_kv_proposals(b, k, 256, C5_VAL[args.payload], seed, b,
-                                 active_ppm=args.active_ppm)
-            continue
+            continue  # generated per round inside step()
         eng.gen_kv_proposals(b, k, 256, 4, seed, b)
         eng.gen_read_index(b, seed, b + 30)
     stream = torch.cuda.ExternalStream(eng.stream)
@@ -236,6 +236,9 @@ def main():
         # with reads: ReadLocalNode for the 9 reads behind every released
         # ctx, served inside the round (drb_round_in.reads_per_ctx)
         fused = reads and args.reads_mode == "fused"
+        if c5:  # this round's 1 % (an independent draw every round)
+            eng.gen_kv_proposals(i % NP, k, 256, C5_VAL[args.payload], seed,
+                                 i, active_ppm=args.active_ppm)
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF,
                        reads_per_ctx=READS_PER_CTX if fused else 0,
@@ -260,6 +263,7 @@ def main():
         eng.sync()
     args.tick_every = tick_every[0]
     eng.read_counters(reset=True)
+    warm_flagged = len(eng.take_flagged(reset=True)[0])
     if xch is not None:
         xch.bytes_sent = 0
     K = args.steps
@@ -317,9 +321,21 @@ def main():
                 "note": "median of %d drb_encode_wire calls (5 kernels + one "
                         "host sync for the plan), outside the timed "
                         "region" % reps}
+    # the replicas that left the fast path during the run, by reason
+    # (drb_take_flagged): a run with any is not a pure fast-path number
+    from dragonboat_amd import abi as _abi
+    flagged, lost = eng.take_flagged(reset=True)
+    by_reason = {}
+    for (_, _, reason, flags, _, _) in flagged:
+        name = _abi.FB_NAME.get(reason, str(reason))
+        if flags & _abi.F_APPLY_STOPPED:
+            name += "/apply"
+        by_reason[name] = by_reason.get(name, 0) + 1
+    if lost:
+        by_reason["unlisted"] = lost
     if out.fallbacks or out.errors:
-        print("WARNING: fallbacks=%d errors=%d" % (out.fallbacks, out.errors),
-              file=sys.stderr)
+        print("WARNING: fallbacks=%d errors=%d %s" % (
+            out.fallbacks, out.errors, by_reason), file=sys.stderr)
     if rank == 0:
         if c5:
             metric = ("committed entries/sec (node) at %d 3-replica groups, "
@@ -328,7 +344,8 @@ def main():
                           G, args.payload, args.active_ppm / 1e4))
             wl = ("C5: %d groups x %d replicas per GPU, %d B PBKV writes "
                   "(values out of line), %d ppm of the groups proposing per "
-                  "round, EntriesToSave encoded (EntryBatch + CRC32), tick "
+                  "round (independent seeded draw each round, generated "
+                  "inside the timed loop), EntriesToSave encoded (EntryBatch + CRC32), tick "
                   "every %d round(s); Quiesce off" % (
                       G, R, args.payload, args.active_ppm, args.tick_every))
             par = "groups sharded, replicas co-resident"
@@ -384,6 +401,10 @@ def main():
                          "reads_served": out.reads_served,
                          "reads_deferred": out.reads_deferred,
                          "fallbacks": out.fallbacks, "errors": out.errors,
+                         "fallbacks_by_reason": by_reason,
+                         "fast_path_only": not (out.fallbacks or
+                                                out.errors),
+                         "flagged_in_warmup": warm_flagged,
                          "saved_entries": out.saved_entries,
                          "saved_bytes": out.saved_bytes},
         }

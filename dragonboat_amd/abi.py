@@ -43,11 +43,13 @@ REMOTE_RETRY, REMOTE_WAIT, REMOTE_REPLICATE, REMOTE_SNAPSHOT = range(4)
 F_HOSTED = 1
 F_FALLBACK = 2
 F_ERROR = 4
+F_APPLY_STOPPED = 8
 
 FB = dict(NONE=0, TERM_MISMATCH=1, MESSAGE_TYPE=2, ELECTION=3,
-          CHECK_QUORUM=4, ENTRY_TYPE=5, CAPACITY=6, ROLE=7, PROPOSAL=8,
-          ERR_LOG_RANGE=100, ERR_COMMIT=101, ERR_CONFLICT=102,
-          ERR_APPEND=103, ERR_APPLY=104, ERR_READINDEX=105)
+          CHECK_QUORUM=4, ENTRY_TYPE=5, CAPACITY=6, ROLE=7, SNAPSHOT=9,
+          ERR_LOG_RANGE=100, ERR_COMMIT=101, ERR_APPEND=103, ERR_APPLY=104,
+          ERR_READINDEX=105)
+FB_NAME = {v: k for k, v in FB.items()}
 
 
 class RemoteState(C.Structure):
@@ -124,7 +126,16 @@ class Config(C.Structure):
                 ("device", C.c_int32), ("save_cap", C.c_uint32),
                 ("total_groups", C.c_uint64), ("place_world", C.c_uint32),
                 ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
-                ("kv_pool_blocks", C.c_uint32)]
+                ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
+                ("reserved0", C.c_uint32)]
+
+
+class Flagged(C.Structure):
+    """drb_flagged: a replica that left the fast path (drb_take_flagged)."""
+    _fields_ = [("group", C.c_uint64), ("shard_id", C.c_uint64),
+                ("round", C.c_uint64), ("slot", C.c_uint32),
+                ("reason", C.c_uint32), ("flags", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 class Region(C.Structure):

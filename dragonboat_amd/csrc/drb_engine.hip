@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "../../include/drb_engine.h"
@@ -46,6 +47,8 @@ struct drb_engine {
   void *scratch;
   size_t scratch_bytes;
   struct WireState *wire = nullptr;          // drb_encode_wire (drb_wire.hpp)
+  std::mutex ingest_mu;  // drb_ingest: concurrent transport threads
+  bool crc_tab_ready = false;  // c_crc_tab uploaded on this engine's device
 };
 
 static void wire_free(drb_engine *e);
@@ -172,9 +175,11 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   if (cfg->max_props == 0 || cfg->prop_slots == 0 || cfg->ri_slots == 0)
     return DRB_EINVAL;
   if (cfg->save_cap % 16) return DRB_EINVAL;
+  // entry_mbox travels as the 8-bit E of the plane summary word
+  // (block_plane_summary, DRB_PLANE_E)
   if (cfg->place_world > 1 &&
       (cfg->place_rank >= cfg->place_world || cfg->entry_mbox == 0 ||
-       cfg->entry_mbox > cfg->window))
+       cfg->entry_mbox > cfg->window || cfg->entry_mbox > 255))
     return DRB_EINVAL;
   if (cfg->election_rtt == 0 || cfg->heartbeat_rtt == 0) return DRB_EINVAL;
   // limitSize never binds inside the window (entryutils.go:50-63)
@@ -291,6 +296,9 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
   rc |= dalloc(e, &e->ctr_total, NUM_COUNTERS);
+  v.flog_cap = cfg->flagged_cap ? cfg->flagged_cap : 65536;
+  rc |= dalloc(e, &v.flog, v.flog_cap);
+  rc |= dalloc(e, &v.flog_n, 1);
   rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
   if (!rc) {  // no Replicate in flight: ring_guard = +inf
@@ -412,6 +420,14 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
   // the current ones across the re-encoding of the packed records
   std::vector<uint64_t> cur;
   if (read_records(e, first_group, n_groups, cur)) return DRB_EDEVICE;
+  // a replica coming back from the CPU path has nothing in flight on the
+  // device: its window guard restarts (no Replicate to keep resident)
+  std::vector<uint64_t> ifl;
+  std::vector<uint32_t> oldfl;
+  for (uint64_t gi = 0; gi < n_groups; ++gi)
+    for (uint32_t s = 0; s < R; ++s)
+      ifl.push_back(u32_ix(v, W_FLAGS, s, first_group + gi));
+  if (gather(e, v.u32, ifl, oldfl)) return DRB_EDEVICE;
   std::vector<uint64_t> ipk;
   std::vector<uint4> dpk;
   for (uint64_t gi = 0; gi < n_groups; ++gi) {
@@ -424,7 +440,9 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
         vals[kU64Order[k]] = *st_u64(&c, k);
       const uint64_t *old = &cur[(gi * R + s) * NUM_U64];
       vals[F_RING_LO] = old[F_RING_LO];
-      vals[F_RING_GUARD] = old[F_RING_GUARD];
+      vals[F_RING_GUARD] =
+          (oldfl[gi * R + s] & (DRB_F_FALLBACK | DRB_F_ERROR)) ? ~0ull
+                                                             : old[F_RING_GUARD];
       vals[F_TERM_START] = c.last_index + 1;  // the term cache restarts empty
       uint32_t w[16];
       pk_encode(w, vals, over);
@@ -787,7 +805,11 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
       uint64_t b = (uint64_t)j * chunks * G + g;
       host[b + 0 * G] = mk4h(en.key, en.client_id);
       host[b + 1 * G] = mk4h(en.series_id, en.responded_to);
-      uint4 p2 = {en.type, en.cmd_len, 0, 0};
+      const uint32_t b0 = en.cmd_len ? pool[en.cmd_off] : 0u;
+      uint4 p2 = {en.type, en.cmd_len,
+                  prop_fast(en.type, en.client_id, en.series_id, en.cmd_len,
+                            b0),
+                  0};
       host[b + 2 * G] = p2;
       for (uint32_t c = 0; c < v.C16; ++c) {
         uint8_t by[16] = {0};
@@ -860,8 +882,9 @@ __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
     }
     v.props[prop_ix(v, ps, j, 0, lane)] = mk4(r0 | 1, cid);
     v.props[prop_ix(v, ps, j, 1, lane)] = mk4(0, 0);
-    v.props[prop_ix(v, ps, j, 2, lane)] =
-        make_uint4(DRB_ENTRY_ENCODED, clen, 0, 0);
+    v.props[prop_ix(v, ps, j, 2, lane)] = make_uint4(
+        DRB_ENTRY_ENCODED, clen, prop_fast(DRB_ENTRY_ENCODED, cid, 0, clen, 0),
+        0);
   }
   v.prop_count[(uint64_t)ps * v.G + lane] = k;
 }
@@ -876,8 +899,7 @@ extern "C" int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot,
     return DRB_EINVAL;
   k_gen_kv<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
       e->v, slot, k, key_space, val_len, seed, salt, active_ppm);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipGetLastError());  // stream-ordered before the next round
   return DRB_OK;
 }
 
@@ -917,8 +939,7 @@ extern "C" int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
   if (!e || slot >= e->cfg.ri_slots) return DRB_ERANGE;
   k_gen_ri<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
       e->v, slot, seed, e->round + 1, high);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipGetLastError());  // stream-ordered before the next round
   return DRB_OK;
 }
 
@@ -938,6 +959,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   const View &v = e->v;
   // replicas spread over ranks exchange whole mailbox planes instead
   if (v.remote_mask) return DRB_ENOSYS;
+  std::lock_guard<std::mutex> lock(e->ingest_mu);
   const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
   const uint32_t tag = (uint32_t)e->round;
   uint64_t acc = 0, drop = 0;
@@ -1236,6 +1258,44 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
     HIPCHK(hipMemsetAsync(e->v.counters, 0,
                           e->ctr_rows * NUM_COUNTERS * sizeof(c[0]),
                           e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_take_flagged(drb_engine *e, drb_flagged *out, size_t cap,
+                                size_t *n_out, uint64_t *lost, int reset) {
+  if (!e || (cap && !out)) return DRB_EINVAL;
+  const View &v = e->v;
+  unsigned long long n = 0;
+  HIPCHK(hipMemcpyAsync(&n, v.flog_n, sizeof(n), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const uint64_t have = std::min<uint64_t>(n, v.flog_cap);
+  const uint64_t take = std::min<uint64_t>(have, cap);
+  std::vector<uint4> recs(take);
+  if (take) {
+    HIPCHK(hipMemcpyAsync(recs.data(), v.flog, take * sizeof(uint4),
+                          hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  for (uint64_t i = 0; i < take; ++i) {
+    const uint4 q = recs[i];
+    drb_flagged &o = out[i];
+    memset(&o, 0, sizeof(o));
+    o.group = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    o.slot = q.z & 0xffu;
+    o.reason = (q.z >> 8) & 0xffu;
+    o.flags = (q.z >> 16) & 0xffu;
+    o.shard_id = v.first_shard_id + gid(v, o.slot, o.group);
+    // the u32 round tag, widened against the engine's round counter
+    o.round = (e->round & ~0xffffffffull) | q.w;
+    if (o.round > e->round) o.round -= 1ull << 32;
+  }
+  if (n_out) *n_out = (size_t)take;
+  if (lost) *lost = n > take ? n - take : 0;
+  if (reset) {
+    HIPCHK(hipMemsetAsync(v.flog_n, 0, sizeof(unsigned long long), e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
   }
   return DRB_OK;
@@ -1579,6 +1639,75 @@ extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
   return 1;
 }
 
+extern "C" int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
+                             const uint8_t *keys, const uint32_t *key_lens,
+                             const uint8_t *vals, const uint32_t *val_lens,
+                             size_t val_stride, size_t n) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  if (n && (!keys || !key_lens || !vals || !val_lens)) return DRB_EINVAL;
+  const View &v = e->v;
+  if (n > v.KS) return DRB_ERANGE;
+  std::vector<uint4> tbl((uint64_t)v.KS * v.KVW, make_uint4(0, 0, 0, 0));
+  std::vector<std::pair<uint32_t, size_t>> ool;  // (slot index, pair)
+  const uint32_t mask = v.KS - 1;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t kl = key_lens[i], vl = val_lens[i];
+    if (kl > 8 || vl > v.kv_val_cap) return DRB_ERANGE;
+    uint64_t k8 = 0;
+    for (uint32_t b = 0; b < kl; ++b) k8 |= (uint64_t)keys[i * 8 + b] << (8 * b);
+    // the device's slot hash (drb_step.hpp kv_hash)
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (uint32_t b = 0; b < kl; ++b)
+      h = (h ^ ((k8 >> (8 * b)) & 0xff)) * 0x100000001b3ull;
+    h ^= h >> 29;
+    uint32_t ks = (uint32_t)h & mask, p = 0;
+    while (p < v.KS && (tbl[(uint64_t)ks * v.KVW].z >> 31)) {
+      ks = (ks + 1) & mask;
+      ++p;
+    }
+    if (p == v.KS) return DRB_ERANGE;
+    const uint8_t *val = vals + i * val_stride;
+    uint32_t w0 = 0;
+    for (uint32_t b = 0; b < 4 && b < vl; ++b) w0 |= (uint32_t)val[b] << (8 * b);
+    uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
+    sl[0] = make_uint4((uint32_t)k8, (uint32_t)(k8 >> 32),
+                       (1u << 31) | (vl << 8) | kl, w0);
+    if (v.kv_ool) {
+      ool.push_back({ks, i});
+    } else {
+      uint8_t tmp[16 * 9] = {0};
+      if (vl > 4) memcpy(tmp, val + 4, vl - 4);
+      for (uint32_t c = 1; c < v.KVW; ++c) memcpy(&sl[c], tmp + 16 * (c - 1), 16);
+    }
+  }
+  if (!ool.empty()) {  // fresh value blocks from the bump allocator
+    unsigned long long next = 0;
+    HIPCHK(hipMemcpyAsync(&next, v.kv_pool_next, 8, hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (next + ool.size() > v.kv_pool_blocks) return DRB_ERANGE;
+    std::vector<uint4> blocks(ool.size() * v.VB, make_uint4(0, 0, 0, 0));
+    for (size_t q = 0; q < ool.size(); ++q) {
+      const size_t i = ool[q].second;
+      tbl[(uint64_t)ool[q].first * v.KVW + 1] =
+          make_uint4((uint32_t)(next + q), 0, 0, 0);
+      memcpy(&blocks[q * v.VB], vals + i * val_stride, val_lens[i]);
+    }
+    HIPCHK(hipMemcpyAsync(v.kv_pool + next * v.VB, blocks.data(),
+                          blocks.size() * sizeof(uint4), hipMemcpyHostToDevice,
+                          e->stream));
+    const unsigned long long nn = next + ool.size();
+    HIPCHK(hipMemcpyAsync(v.kv_pool_next, &nn, 8, hipMemcpyHostToDevice,
+                          e->stream));
+  }
+  HIPCHK(hipMemcpyAsync(v.kv + kv_ix(v, slot, group, 0), tbl.data(),
+                        tbl.size() * sizeof(uint4), hipMemcpyHostToDevice,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
 extern "C" int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot,
                              uint8_t *keys, uint32_t *key_lens, uint8_t *vals,
                              uint32_t *val_lens, size_t cap, size_t *n_out) {
@@ -1697,8 +1826,6 @@ __global__ void k_crc32(const uint8_t *data, const uint64_t *off,
   crc[b] = c ^ 0xffffffffu;
 }
 
-static int crc_tab_ready = 0;
-
 extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
                                     size_t data_len, const uint64_t *off,
                                     const uint32_t *len, size_t n,
@@ -1707,7 +1834,7 @@ extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
   if (!n) return DRB_OK;
   for (size_t i = 0; i < n; ++i)
     if (off[i] + len[i] > data_len) return DRB_ERANGE;
-  if (!crc_tab_ready) {
+  if (!e->crc_tab_ready) {
     uint32_t tab[8][256];
     for (uint32_t i = 0; i < 256; ++i) {
       uint32_t c = i;
@@ -1718,7 +1845,7 @@ extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
       for (int s = 1; s < 8; ++s)
         tab[s][i] = tab[0][tab[s - 1][i] & 0xff] ^ (tab[s - 1][i] >> 8);
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
-    crc_tab_ready = 1;
+    e->crc_tab_ready = true;
   }
   size_t bytes = ((data_len + 15) & ~15ull) + n * 8 + ((n * 4 + 15) & ~15ull) * 2;
   void *s;

@@ -223,8 +223,27 @@ constexpr int MSG_CHUNKS = 2;
 constexpr int ENT_META = 3;
 // staged proposal: 3 x uint4 + cmd chunks
 //   p0 = {key, client_id} p1 = {series_id, responded_to}
-//   p2 = {type | cmd_len << 32, 0}
+//   p2 = {type, cmd_len, fast, 0}: fast = 1 when the rsm fast path can
+//   apply the entry (prop_fast; checked by the leader's pre-pass)
 constexpr int PROP_META = 3;
+
+// Whether the rsm fast path applies this proposal (statemachine.go:935-
+// 969, encoded.go:55-65, kvtest.go:145-162): an application or encoded
+// entry of the NoOP session (SeriesID 0; ClientID 0 only when empty), an
+// encoded Cmd carrying the v0 header byte 0x00 (no compression, no
+// session).  Computed when the proposal is staged; anything else (config
+// change, session management, regular sessions, Snappy) makes the leader
+// fall back before it appends (DRB_FB_ENTRY_TYPE).
+__host__ __device__ inline uint32_t prop_fast(uint32_t type, uint64_t client_id,
+                                              uint64_t series_id,
+                                              uint32_t cmd_len,
+                                              uint32_t first_byte) {
+  if (type != 0 /*APPLICATION*/ && type != 2 /*ENCODED*/) return 0;
+  if (series_id != 0) return 0;
+  if (client_id == 0) return cmd_len == 0;
+  if (type == 2 && (cmd_len == 0 || first_byte != 0)) return 0;
+  return 1;
+}
 constexpr int RTR_CAP = 8;  // ReadyToRead records per replica per round
 
 struct View {
@@ -289,6 +308,11 @@ struct View {
   uint4 *embox_in;
   uint32_t *xrows;        // [2 roles][R][R][blocks] per-block plane summary
   unsigned long long *counters;  // [8] (drb_round_out order from index 1)
+  // flagged-replica list (drb_take_flagged): {g lo, g hi, slot | reason
+  // << 8 | flags << 16, round}, appended with one atomic per marked lane
+  uint4 *flog;
+  unsigned long long *flog_n;
+  uint64_t flog_cap;
 };
 
 __host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,

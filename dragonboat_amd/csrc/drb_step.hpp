@@ -725,8 +725,11 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
       }
     }
     if (ci != 0) {
+      // tryAppend / append (logentry.go:296-321) panic when a committed
+      // entry would change; unreachable here (LogIndex >= committed, see
+      // above) but kept as the invariant it is
       if (ci <= r.committed) {
-        set_error(r, DRB_ERR_CONFLICT);
+        set_error(r, DRB_ERR_APPEND);
         return;
       }
       uint64_t new_last = m.log_index + m.n;
@@ -934,7 +937,8 @@ DRB_DEV bool put_value_long(const View &v, uint32_t slot,
 
 // handleEntry (statemachine.go:935-969) -> update (1057-1103) ->
 // GetPayload (encoded.go:55-65) -> KVTest.Update (kvtest.go:145-162).
-// Returns: 0 noop applied, 1 KV updated, -1 not on the fast path.
+// Returns: 0 noop applied, 1 KV updated, -1 not on the fast path, -2 the
+// KV table or the value pool is full.
 // The PBKV header is parsed from the Cmd's first 64 bytes (registers); the
 // value is copied 16 B at a time straight from the window into the slot
 // (inline values) or the slot's value block (out-of-line, kv_val_cap >
@@ -1063,7 +1067,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
         }
       } else if (!put_value_long(v, L.slot, L.g, index, sl, hit, voff,
                                  vlen)) {
-        return -1;  // value pool exhausted
+        return -2;  // value pool exhausted
       }
       sl[0] = make_uint4((uint32_t)key8, (uint32_t)(key8 >> 32),
                          (1u << 31) | (vlen << 8) | klen, w0);
@@ -1075,7 +1079,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
     }
     ks = (ks + DRB_PROBE_W) & mask;
   }
-  return -1;  // table full
+  return -2;  // table full
 }
 
 // ------------------------------------------------------------ saves
@@ -1361,6 +1365,19 @@ DRB_DEV void store_rep(const Lane &L, Rep<R> &r, uint32_t flags0,
   }
 }
 
+// ------------------------------------------------------------ flagged list
+// One record per replica newly marked FALLBACK / ERROR (drb_take_flagged);
+// rare, so one global atomic per marked lane
+DRB_DEV void flag_log(const View &v, uint64_t g, uint32_t slot,
+                      uint32_t reason, uint32_t flags, uint64_t round) {
+  const unsigned long long i = atomicAdd(v.flog_n, 1ull);
+  if (i < v.flog_cap)
+    v.flog[i] = make_uint4((uint32_t)g, (uint32_t)(g >> 32),
+                           slot | ((reason & 0xffu) << 8) |
+                               ((flags & 0xffu) << 16),
+                           (uint32_t)round);
+}
+
 // ------------------------------------------------------------ the kernel
 struct RoundParams {
   uint64_t round;      // t (>= 1)
@@ -1626,18 +1643,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
       for (uint32_t j = 0; j < nprops; ++j) {
+        // p2 = {type, cmd_len, fast}: the staging side's prop_fast check
+        // (drb_layout.hpp) -- config change, session and compressed
+        // entries go to the CPU path before anything is appended
         uint4 p2 = v.props[prop_ix(v, p.prop_slot, j, 2, g)];
-        uint32_t type = p2.x, clen = p2.y;
-        if ((type != DRB_ENTRY_APPLICATION && type != DRB_ENTRY_ENCODED) &&
-            fb == DRB_FB_NONE)
-          fb = DRB_FB_ENTRY_TYPE;
-        if (clen > v.C16 * 16 && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
+        if (!p2.z && fb == DRB_FB_NONE) fb = DRB_FB_ENTRY_TYPE;
+        if (p2.y > v.C16 * 16 && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
       }
-      // window: appended entries must not evict what is still needed
+      // The window: the lowest index a Replicate of this round may read
+      // for remote s is next - 1 (its LogTerm), or match - 1 after a
+      // rejection lowers next (decreaseTo / enterRetryState, remote.go:
+      // 182-198, raft.go:2013-2017).  Below the resident window the
+      // reference reads LogDB (logentry.go:180-195): the CPU path's job,
+      // so the leader falls back before it sends.  Appended entries must
+      // not evict anything still needed either.  A remote being sent a
+      // snapshot (remote.go:128-141) is the CPU path's as well.
       uint64_t keep = umin64(r.ring_guard, keep_common);
 #pragma unroll
-      for (int s = 0; s < R; ++s)
-        if ((uint32_t)s != slot) keep = umin64(keep, rem_get<R>(L, s).n - 1);
+      for (int s = 0; s < R; ++s) {
+        if ((uint32_t)s == slot) continue;
+        const RemoteV x = rem_get<R>(L, s);
+        if (x.st == DRB_REMOTE_SNAPSHOT && fb == DRB_FB_NONE)
+          fb = DRB_FB_SNAPSHOT;
+        const uint64_t lowest = ((rej_from >> s) & 1) ? umin64(x.m, x.n) : x.n;
+        const uint64_t need = lowest > 0 ? lowest - 1 : 0;  // LogTerm index
+        keep = umin64(keep, need);
+        const bool ents_below = need < r.last && need + 1 < r.ring_lo;
+        const bool term_below =
+            need != 0 && need < r.ring_lo && need < r.term_start;
+        if ((ents_below || term_below) && fb == DRB_FB_NONE)
+          fb = DRB_FB_CAPACITY;
+      }
       if (nprops && r.last + nprops >= keep + v.W && fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
       // entry rows of a remote follower's plane: the round sends it
@@ -1871,9 +1907,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           }
           if (rc < 0) {
             // the rsm apply of this replica leaves the fast path at idx;
-            // the raft round itself completed
-            r.flags |= DRB_F_FALLBACK;
-            r.fb = DRB_FB_ENTRY_TYPE;
+            // the raft round itself completed: (sm_index, pushed_index]
+            // stay pushed but unapplied (include/drb_engine.h)
+            r.flags |= DRB_F_FALLBACK | DRB_F_APPLY_STOPPED;
+            r.fb = rc == -2 ? DRB_FB_CAPACITY : DRB_FB_ENTRY_TYPE;
             c_fb = 1;
             break;
           }
@@ -1922,6 +1959,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       c_rtr = r.nrtr;
       c_drop = r.ndropped_ri;
     }
+    if (c_fb | c_err) flag_log(v, g, slot, r.fb, r.flags, p.round);
     // outbox headers for this round (tag = round), for the destinations
     // that got records: a receiver reads a stale tag as an empty inbox
 #pragma unroll

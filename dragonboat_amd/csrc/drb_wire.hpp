@@ -851,10 +851,9 @@ extern "C" int drb_export_wire(drb_engine *e, uint8_t *out, size_t cap,
 namespace wirehost {
 
 static uint32_t crc_tab[8][256];
-static bool crc_ready = false;
+static std::once_flag crc_once;
 
-static void crc_init() {
-  if (crc_ready) return;
+static void crc_build() {
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
     for (int k = 0; k < 8; ++k)
@@ -865,8 +864,9 @@ static void crc_init() {
     for (int s = 1; s < 8; ++s)
       crc_tab[s][i] = crc_tab[0][crc_tab[s - 1][i] & 0xff] ^
                       (crc_tab[s - 1][i] >> 8);
-  crc_ready = true;
 }
+// thread-safe: transport threads may call drb_ingest_wire concurrently
+static void crc_init() { std::call_once(crc_once, crc_build); }
 
 // slicing-by-8 CRC32-IEEE (Go crc32.ChecksumIEEE)
 static uint32_t crc32(const uint8_t *p, size_t n) {
@@ -1044,6 +1044,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                size_t len, uint64_t deployment_id,
                                drb_wire_in *out) {
   if (!e || (!stream && len)) return DRB_EINVAL;
+  // replicas spread over ranks: planes move by drb_exchange_* (drb_ingest)
+  if (e->v.remote_mask) return DRB_ENOSYS;
   wirehost::crc_init();
   drb_wire_in res;
   memset(&res, 0, sizeof(res));

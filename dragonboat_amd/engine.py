@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 from . import abi
-from .abi import (Config, Entry, Message, ReadyToRead, Region, ReplicaState,
+from .abi import (Config, Entry, Flagged, Message, ReadyToRead, Region, ReplicaState,
                   RoundIn, RoundOut, WireCfg, WireIn, WireOut, entry_to_tuple,
                   message_to_tuple)
 
@@ -54,6 +54,8 @@ SIGNATURES = {
                                  C.POINTER(RoundOut)]),
     "drb_step_round_async": (C.c_int, [P, C.POINTER(RoundIn)]),
     "drb_read_counters": (C.c_int, [P, C.POINTER(RoundOut), C.c_int]),
+    "drb_take_flagged": (C.c_int, [P, C.POINTER(Flagged), SZ, C.POINTER(SZ),
+                                   PU64, C.c_int]),
     "drb_export_outbox": (C.c_int, [P, U64, U32, C.POINTER(Message), SZ,
                                     C.POINTER(Entry), SZ, PU8, SZ,
                                     C.POINTER(SZ)]),
@@ -65,6 +67,7 @@ SIGNATURES = {
     "drb_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32, PU32]),
     "drb_kv_export": (C.c_int, [P, U64, U32, PU8, PU32, PU8, PU32, SZ,
                                 C.POINTER(SZ)]),
+    "drb_kv_import": (C.c_int, [P, U64, U32, PU8, PU32, PU8, PU32, SZ, SZ]),
     "drb_crc32_ieee_batch": (C.c_int, [P, PU8, SZ, PU64, PU32, SZ, PU32]),
     "drb_export_saved": (C.c_int, [P, U64, U32, PU8, SZ, PU32, PU32]),
     "drb_saved_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(PU32),
@@ -122,7 +125,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 mailbox=13, kv_slots=512, kv_val_cap=4, election_rtt=10,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
-                kv_pool_blocks=0)
+                kv_pool_blocks=0, flagged_cap=0)
 
 
 class Engine:
@@ -139,7 +142,8 @@ class Engine:
                    cfg["election_rtt"], cfg["heartbeat_rtt"],
                    cfg["check_quorum"], cfg["device"], cfg["save_cap"],
                    cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
-                   cfg["entry_mbox"], cfg["kv_pool_blocks"])
+                   cfg["entry_mbox"], cfg["kv_pool_blocks"],
+                   cfg["flagged_cap"], 0)
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -259,6 +263,18 @@ class Engine:
             "drb_read_counters")
         return out
 
+    def take_flagged(self, cap=65536, reset=True):
+        """[(group, slot, reason, flags, round, shard_id)] of the replicas
+        marked FALLBACK / ERROR since the last reset, and the count lost."""
+        arr = (Flagged * max(1, cap))()
+        n, lost = SZ(), U64()
+        _ck(lib().drb_take_flagged(self.h, arr, cap, C.byref(n),
+                                   C.byref(lost), int(reset)),
+            "drb_take_flagged")
+        return ([(arr[i].group, arr[i].slot, arr[i].reason, arr[i].flags,
+                  arr[i].round, arr[i].shard_id) for i in range(n.value)],
+                lost.value)
+
     # ---------------------------------------------------------- outputs
     def export_outbox(self, g, slot):
         cap, ecap = 16 * self.R, 16 * self.R * self.cfg["window"]
@@ -294,6 +310,21 @@ class Engine:
         kb, vb = bytes(keys), bytes(vals)
         return {kb[i * 8:i * 8 + kl[i]]: vb[i * vcap:i * vcap + vl[i]]
                 for i in range(n.value)}
+
+    def kv_import(self, g, slot, kv):
+        """Replaces replica (g, slot)'s KV with the {key: value} dict
+        (drb_kv_import, the state machine handed back after a fallback)."""
+        n = len(kv)
+        stride = max([len(x) for x in kv.values()] + [1])
+        keys = (C.c_uint8 * max(1, 8 * n))()
+        vals = (C.c_uint8 * max(1, stride * n))()
+        kl, vl = (U32 * max(1, n))(), (U32 * max(1, n))()
+        for i, (k, x) in enumerate(kv.items()):
+            C.memmove(C.addressof(keys) + 8 * i, bytes(k), len(k))
+            C.memmove(C.addressof(vals) + stride * i, bytes(x), len(x))
+            kl[i], vl[i] = len(k), len(x)
+        _ck(lib().drb_kv_import(self.h, g, slot, keys, kl, vals, vl, stride,
+                                n), "drb_kv_import")
 
     def export_saved(self, g, slot):
         """(EntryBatch bytes, crc32) of one replica's last EntriesToSave."""

@@ -19,15 +19,26 @@
  *   its in-memory KV state machine and commits the Update; messages it
  *   sends are delivered at the end of the round.
  *
- * Threading: an engine is not re-entrant; one host thread drives it (the
- * reference holds node.raftMu across stepNode, node.go:1140).
- *
  * Error behaviour: functions return DRB_OK (0) or a negative DRB_E* code.
  * Conditions the reference reports with plog.Panicf mark the replica
  * DRB_F_ERROR; paths that stay on the reference CPU code (election,
  * membership change, snapshot, session management, higher/lower term
  * messages) mark it DRB_F_FALLBACK *before* it mutates any state, so the
- * pre-round state can be exported to the CPU raft.Peer.
+ * pre-round state can be exported to the CPU raft.Peer.  One exception is
+ * the state machine: the rsm applies committed entries after the raft
+ * round (engine.go:1153 apply workers, statemachine.go:599), so an entry
+ * the fast path cannot apply (KV table or value pool full, an entry a
+ * proposal check could not see) stops the APPLY only: the replica is
+ * marked DRB_F_FALLBACK | DRB_F_APPLY_STOPPED, its raft state is the
+ * completed round's, and the committed entries (sm_index, pushed_index]
+ * are pushed but unapplied -- the rsm task queue a CPU StateMachine
+ * resumes from (drb_export_log reads them from the window).
+ *
+ * Threading: drb_ingest / drb_ingest_wire may be called from several
+ * transport threads at once (each call stages under the engine's ingest
+ * lock); every other entry point is driven by one host thread, which is
+ * not re-entrant (the reference holds node.raftMu across stepNode,
+ * node.go:1140).
  */
 #ifndef DRB_ENGINE_H
 #define DRB_ENGINE_H
@@ -113,6 +124,8 @@ enum drb_remote_fsm {
 #define DRB_F_HOSTED 1u    /* stepped by this engine */
 #define DRB_F_FALLBACK 2u  /* handed back to the CPU raft.Peer, frozen here */
 #define DRB_F_ERROR 4u     /* invariant violation (reference: plog.Panicf) */
+#define DRB_F_APPLY_STOPPED 8u /* with FALLBACK: the raft round completed,
+                                * the rsm apply stopped at sm_index + 1 */
 
 /* drb_replica_state.fallback_reason */
 enum drb_fallback_reason {
@@ -124,11 +137,15 @@ enum drb_fallback_reason {
   DRB_FB_ENTRY_TYPE = 5,        /* config change / session / compressed entry */
   DRB_FB_CAPACITY = 6,          /* window / mailbox / readIndex capacity */
   DRB_FB_ROLE = 7,              /* candidate / non-voting / witness */
-  DRB_FB_PROPOSAL = 8,          /* proposal at a non-leader replica */
-  DRB_ERR_LOG_RANGE = 100,      /* entry outside the resident window */
+  DRB_FB_SNAPSHOT = 9,          /* a remote in the Snapshot state
+                                 * (remote.go:54-59, 128-141) */
+  DRB_ERR_LOG_RANGE = 100,      /* internal invariant: a read below the
+                                 * resident window the pre-pass did not
+                                 * predict (it falls back with CAPACITY) */
   DRB_ERR_COMMIT = 101,         /* logentry.go:336-349 commitTo panic */
-  DRB_ERR_CONFLICT = 102,       /* logentry.go:296-310 conflict <= committed */
-  DRB_ERR_APPEND = 103,         /* entryutils.go:36-48 hole / term regress */
+  DRB_ERR_APPEND = 103,         /* entryutils.go:36-48 hole / term regress,
+                                 * logentry.go:296-321 committed entry
+                                 * changed */
   DRB_ERR_APPLY = 104,          /* statemachine.go:935-969 malformed entry */
   DRB_ERR_READINDEX = 105       /* readindex.go:43-115 invariant */
 };
@@ -268,11 +285,15 @@ typedef struct drb_config {
   uint32_t place_world;
   uint32_t place_rank;
   uint32_t entry_mbox;       /* entries per remote (sender, receiver) and
-                              * round that travel by value (N >= 2) */
+                              * round that travel by value (N >= 2;
+                              * 1..255: the plane summary's 8-bit E) */
   /* kv_val_cap > 124 keeps values out of line (C5: 128 B / 1 KB
    * payloads) in a pool of this many value blocks (0: one per KV slot);
    * a replica whose apply finds the pool empty falls back */
   uint32_t kv_pool_blocks;
+  /* records of the flagged-replica list (drb_take_flagged; 0: 65536) */
+  uint32_t flagged_cap;
+  uint32_t reserved0;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -399,6 +420,28 @@ int drb_step_round(drb_engine *e, const drb_round_in *in, drb_round_out *out);
 int drb_step_round_async(drb_engine *e, const drb_round_in *in);
 int drb_read_counters(drb_engine *e, drb_round_out *out, int reset);
 
+/*
+ * The replicas that left the fast path (DRB_F_FALLBACK / DRB_F_ERROR),
+ * appended by the step kernels in the round they were marked: the compact
+ * list a host walks to hand exactly those groups to the CPU raft.Peer
+ * (node.stepNode's error / CPU path, node.go:1139-1159) instead of
+ * exporting every replica.  drb_take_flagged copies up to cap records
+ * appended since the last reset (in no particular order), reports in
+ * *lost how many did not fit the device list (flagged_cap), and with
+ * reset != 0 empties it.  Synchronises the engine stream.
+ */
+typedef struct drb_flagged {
+  uint64_t group;      /* lane on this engine */
+  uint64_t shard_id;
+  uint64_t round;      /* drb_engine_round() of the round that marked it */
+  uint32_t slot;       /* replica slot (replica ID - 1) */
+  uint32_t reason;     /* drb_fallback_reason */
+  uint32_t flags;      /* DRB_F_FALLBACK | DRB_F_ERROR | DRB_F_APPLY_STOPPED */
+  uint32_t pad;
+} drb_flagged;
+int drb_take_flagged(drb_engine *e, drb_flagged *out, size_t cap,
+                     size_t *n_out, uint64_t *lost, int reset);
+
 /* --- outputs ----------------------------------------------------------- */
 
 /* Outbound boundary: the messages one replica sent in the last round
@@ -489,6 +532,18 @@ int drb_exchange_local(drb_engine *const *engines, uint32_t n);
 int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
                   const uint8_t *key, uint32_t key_len, uint8_t *val,
                   uint32_t val_cap, uint32_t *val_len);
+/* Replaces one replica's KV state machine with n pairs: the state machine
+ * a CPU StateMachine hands back with its group after a fallback, next to
+ * drb_import_replicas (IStateMachine.RecoverFromSnapshot,
+ * statemachine/rsm.go:189; KVTest.RecoverFromSnapshot,
+ * internal/tests/kvtest.go:200-239).  keys[i*8..] (key_lens[i] <= 8,
+ * distinct), vals[i*val_stride..] (val_lens[i] <= kv_val_cap).  Out-of-line
+ * values take fresh blocks from the value pool (the replica's old blocks
+ * are not reused).  DRB_ERANGE when the pairs do not fit. */
+int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
+                  const uint8_t *keys, const uint32_t *key_lens,
+                  const uint8_t *vals, const uint32_t *val_lens,
+                  size_t val_stride, size_t n);
 /* Dumps every KV pair of one replica: keys[i*8..], key_lens[i],
  * vals[i*kv_val_cap..], val_lens[i]; returns the count in *n_out. */
 int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot, uint8_t *keys,

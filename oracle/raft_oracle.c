@@ -1182,14 +1182,32 @@ static void raft_become_candidate(orc_raft *r) {
   r->vote = r->replica_id;
 }
 
-/* becomeLeader (raft.go:1038-1050); preLeaderPromotionHandleConfigChange
- * (raft.go:1075-1083) finds no pending config change on this path */
+/* getPendingConfigChangeCount (raft.go:1380-1398): config change entries
+ * in (committed, last] */
+static int raft_pending_config_change_count(orc_raft *r) {
+  const uint64_t lo = r->log.committed + 1, last = log_last(&r->log);
+  if (lo > last) return 0;
+  orc_evec ents = {0};
+  if (log_get_entries(&r->log, lo, last + 1, UINT64_MAX, &ents))
+    orc_panic("failed to get entries");
+  int n = 0;
+  for (size_t i = 0; i < ents.n; i++)
+    if (ents.v[i].type == DRB_ENTRY_CONFIG_CHANGE) n++;
+  ev_free(&ents);
+  return n;
+}
+
+/* becomeLeader (raft.go:1038-1050) + preLeaderPromotionHandleConfigChange
+ * (raft.go:1075-1083) */
 static void raft_become_leader(orc_raft *r) {
   if (r->state != DRB_LEADER && r->state != DRB_CANDIDATE)
     orc_panic("transitioning to leader state from %u", r->state);
   r->state = DRB_LEADER;
   raft_reset(r, r->term, 1);
   raft_set_leader_id(r, r->replica_id);
+  const int pcc = raft_pending_config_change_count(r);
+  if (pcc > 1) orc_panic("multiple uncommitted config change entries");
+  if (pcc == 1) r->pending_config_change = 1;
   orc_entry e;
   memset(&e, 0, sizeof(e));
   e.type = DRB_ENTRY_APPLICATION;
@@ -1464,9 +1482,18 @@ static void handle_leader_read_index(orc_raft *r, const orc_msg *m) {
 
 /* handleLeaderPropose (raft.go:1794-1815) */
 static void handle_leader_propose(orc_raft *r, orc_msg *m) {
+  /* leader transfer is not on this path (leaderTransfering() false) */
   for (size_t i = 0; i < m->ents.n; i++)
-    if (m->ents.v[i].type == DRB_ENTRY_CONFIG_CHANGE)
-      orc_panic("config change proposal is not on the fast path");
+    if (m->ents.v[i].type == DRB_ENTRY_CONFIG_CHANGE) {
+      if (r->pending_config_change) {
+        /* reportDroppedConfigChange: the entry becomes an empty
+         * application entry */
+        blob_unref(m->ents.v[i].cmd);
+        memset(&m->ents.v[i], 0, sizeof(orc_entry));
+        m->ents.v[i].type = DRB_ENTRY_APPLICATION;
+      }
+      r->pending_config_change = 1; /* setPendingConfigChange */
+    }
   raft_append_entries(r, m->ents.v, m->ents.n);
   raft_broadcast_replicate(r);
 }

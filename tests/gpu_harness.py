@@ -65,11 +65,15 @@ class Pair:
         self.orc.setup_steady(leader_slot)
         self.eng.init_steady(term=2, leader_slot=leader_slot, seed=seed)
         self.rounds = 0
+        self.cpu = set()  # groups handed to the CPU path (the oracle)
 
     def stage(self, k=1, salt=None, read_index=False, groups=None,
               key_space=256, val_len=4, prop_slot=0, ri_slot=0):
         salt = self.rounds if salt is None else salt
         pin = ri_in = abi.DRB_NONE
+        if self.cpu:  # no client input for groups on the CPU path
+            groups = [g for g in (range(self.G) if groups is None else groups)
+                      if g not in self.cpu]
         if k:
             counts, ents, pool = workload.build_batch(
                 self.G, k, self.seed, salt, key_space, val_len, groups)
@@ -111,10 +115,71 @@ class Pair:
                     errs.append((g, s, "saved", eb, ob))
         return errs
 
+    # ---------------------------------------------- fallback round trip
+    # SURVEY 8b "Fallback": a replica the engine flags hands its group to
+    # the CPU raft.Peer -- here the oracle, which is the reference step
+    # loop -- until the event is over; then the group's state and window
+    # are imported back (node.go:1139-1159, peer.go:64).
+    def snapshot(self):
+        """Oracle states before a round, {(g, s): ReplicaState}."""
+        return {(g, s): self.orc.export(g, s)
+                for g in range(self.G) for s in range(self.R)}
+
+    def to_cpu(self, g):
+        """Every replica of group g leaves the engine (marked FALLBACK)."""
+        sts = self.eng.export_replicas(g, 1)
+        for st in sts:
+            st.flags |= abi.F_FALLBACK
+        self.eng.import_replicas(g, sts)
+        self.cpu.add(g)
+
+    def settled(self, g):
+        """The CPU group has a leader, its log committed and applied
+        everywhere, nothing in flight and no readIndex work pending."""
+        lead = 0
+        for s in range(self.R):
+            st = self.orc.export(g, s)
+            if not st.flags & abi.F_HOSTED:
+                continue
+            if st.role == abi.LEADER:
+                lead += 1
+            elif st.role != abi.FOLLOWER:
+                return False
+            if self.orc.export_outbox(g, s) or st.ri_count:
+                return False
+            if not (st.committed == st.last_index == st.processed ==
+                    st.sm_index):
+                return False
+        return lead == 1
+
+    def from_cpu(self, g):
+        """Imports group g back from the oracle: states and the resident
+        window (the last W entries)."""
+        W = self.eng.cfg["window"]
+        sts = []
+        for s in range(self.R):
+            st = self.orc.export(g, s)
+            lo = max(1, st.last_index - W + 1)
+            ents = self.orc.export_log(g, s, lo, st.last_index)
+            ep = po.EntryPool([po._etuple_to_dict(t) for t in ents])
+            arr, pool, n = ep.arrays()
+            self.eng.import_log(g, s, arr, pool)
+            # the state machine comes back with the group (its CPU
+            # StateMachine applied what committed meanwhile)
+            self.eng.kv_import(g, s, self.orc.export_kv(g, s))
+            st.flags &= abi.F_HOSTED
+            st.fallback_reason = 0
+            sts.append(st)
+        self.eng.import_replicas(g, sts)
+        self.cpu.discard(g)
+
+    def live_groups(self):
+        return [g for g in range(self.G) if g not in self.cpu]
+
     def check(self, groups=None, logs=True, kv=True, msgs=True,
               ready=True):
         errs = []
-        gs = range(self.G) if groups is None else groups
+        gs = self.live_groups() if groups is None else groups
         for g in gs:
             est = self.eng.export_replicas(g, 1)
             for s in range(self.R):

@@ -60,6 +60,7 @@ STRUCTS = {
     "drb_wire_cfg": abi.WireCfg,
     "drb_wire_out": abi.WireOut,
     "drb_wire_in": abi.WireIn,
+    "drb_flagged": abi.Flagged,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}
