@@ -91,6 +91,12 @@ def parse():
                     choices=["fused", "separate"],
                     help="served reads inside the round's kernels or as "
                          "their own launch (drb_serve_reads)")
+    ap.add_argument("--reads-at", default="leader",
+                    choices=["leader", "follower"],
+                    help="C3: issue the ReadIndex batch at the leader or at "
+                         "a follower (forwarded, raft.go:2134-2164)")
+    ap.add_argument("--quiesce", type=int, default=-1,
+                    help="Config.Quiesce (default: on for c5, SURVEY 8d)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-wire", action="store_true",
                     help="skip the off-GPU wire encode measurement (C3)")
@@ -180,6 +186,8 @@ def main():
     c5 = args.workload == "c5"
     if not args.replicas:
         args.replicas = 5 if c4 else 3
+    if args.quiesce < 0:
+        args.quiesce = 1 if c5 else 0
     if c5:
         args.no_read_index = True  # writes, no reads
         if args.groups == 1 << 20:
@@ -209,17 +217,23 @@ def main():
         # salt = round) into two alternating staged batches
         NP = 2
         bound = 73 + cmd_cap  # EntryBatch element bound (drb_codec.hpp)
+        # the KV keeps up to kv_slots keys per replica, their values in a
+        # block pool: a block per slot at 128 B (26 GB); 4 per replica at
+        # 1 KB (52 GB) -- a run writing more new keys per replica than
+        # that shows CAPACITY/apply fallbacks in the histogram
+        ks = 16 if args.payload == 128 else 8
         eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
                      max_props=max(1, k), prop_slots=NP, ri_slots=1,
-                     mailbox=8, kv_slots=16, kv_val_cap=vlen + 13 & ~15,
-                     kv_pool_blocks=2 * G * R if args.payload == 128
-                     else G * R, save_cap=(4 * bound + 15) // 16 * 16,
-                     first_shard_id=first_shard, device=local)
+                     mailbox=8, kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
+                     kv_pool_blocks=ks * G * R if args.payload == 128
+                     else 4 * G * R, save_cap=(4 * bound + 15) // 16 * 16,
+                     quiesce=args.quiesce, first_shard_id=first_shard,
+                     device=local)
     else:
         first_shard, seed = ddist.shard_plan(rank, G)
         eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                      max_props=max(1, k), prop_slots=NP, ri_slots=NP,
-                     mailbox=13, kv_slots=args.kv_slots or 512, kv_val_cap=4,
+                     mailbox=16, kv_slots=args.kv_slots or 512, kv_val_cap=4,
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
@@ -242,7 +256,8 @@ def main():
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF,
                        reads_per_ctx=READS_PER_CTX if fused else 0,
-                       key_space=KEY_SPACE, encode_saves=c5)
+                       key_space=KEY_SPACE, encode_saves=c5,
+                       ri_replica=2 if args.reads_at == "follower" else 0)
         if reads and not fused:
             eng.serve_reads(READS_PER_CTX, KEY_SPACE)
         if xch is not None:  # C4: this round's cross-GPU planes
@@ -346,8 +361,9 @@ def main():
                   "(values out of line), %d ppm of the groups proposing per "
                   "round (independent seeded draw each round, generated "
                   "inside the timed loop), EntriesToSave encoded (EntryBatch + CRC32), tick "
-                  "every %d round(s); Quiesce off" % (
-                      G, R, args.payload, args.active_ppm, args.tick_every))
+                  "every %d round(s); Quiesce %s" % (
+                      G, R, args.payload, args.active_ppm, args.tick_every,
+                      "on" if args.quiesce else "off"))
             par = "groups sharded, replicas co-resident"
         elif c4:
             metric = ("committed entries/sec (node) at %d 5-replica groups "
@@ -365,7 +381,8 @@ def main():
                       "groups, 16B payload; %HBM BW")
             wl = ("C3: %d active groups x %d replicas per GPU, 16B PBKV "
                   "writes k=%d/group/round%s, tick every %d round(s)" % (
-                      G, R, k, ", 9:1 ReadIndex:write" if reads else "",
+                      G, R, k, (", 9:1 ReadIndex:write at the %s" %
+                                args.reads_at) if reads else "",
                       args.tick_every))
             par = "groups sharded, replicas co-resident"
         res = {
@@ -405,6 +422,8 @@ def main():
                          "fast_path_only": not (out.fallbacks or
                                                 out.errors),
                          "flagged_in_warmup": warm_flagged,
+                         "replicas_stepped_per_round":
+                             out.replicas_stepped / K,
                          "saved_entries": out.saved_entries,
                          "saved_bytes": out.saved_bytes},
         }

@@ -69,7 +69,8 @@ _REPLICA_U64 = [
     "tick_count", "committed", "processed", "last_index", "marker_index",
     "saved_to", "applied_to_index", "applied_to_term", "applied_index",
     "confirmed_index", "pushed_index", "prev_term", "prev_vote",
-    "prev_commit", "sm_index", "sm_term", "kv_count"]
+    "prev_commit", "sm_index", "sm_term", "kv_count", "qs_current_tick",
+    "qs_idle_since", "qs_quiesced_since", "qs_exit_quiesce_tick"]
 
 
 class ReplicaState(C.Structure):
@@ -127,7 +128,7 @@ class Config(C.Structure):
                 ("total_groups", C.c_uint64), ("place_world", C.c_uint32),
                 ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
                 ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
-                ("reserved0", C.c_uint32)]
+                ("quiesce", C.c_uint32)]
 
 
 class Flagged(C.Structure):
@@ -142,9 +143,20 @@ class Region(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
 
 
-PLANE_REGIONS = 6
-PLANE_C1 = 1 << 16
-PLANE_REP = 1 << 17
+PLANE_REGIONS = 8
+PLANE_C1 = 1 << 18
+
+
+def plane_krep(w):
+    return w & 0x1f
+
+
+def plane_koth(w):
+    return (w >> 5) & 0x1f
+
+
+def plane_e(w):
+    return (w >> 10) & 0xff
 
 
 class WireCfg(C.Structure):
@@ -169,8 +181,8 @@ class RoundIn(C.Structure):
     _fields_ = [("tick", C.c_uint32), ("prop_slot", C.c_uint32),
                 ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),
                 ("read_key_space", C.c_uint32),
-                ("encode_saves", C.c_uint32),
-                ("reserved", C.c_uint32 * 2)]
+                ("encode_saves", C.c_uint32), ("ri_replica", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class RoundOut(C.Structure):
@@ -180,7 +192,8 @@ class RoundOut(C.Structure):
                 ("dropped_read_indexes", C.c_uint64),
                 ("fallbacks", C.c_uint64), ("errors", C.c_uint64),
                 ("reads_served", C.c_uint64), ("reads_deferred", C.c_uint64),
-                ("saved_entries", C.c_uint64), ("saved_bytes", C.c_uint64)]
+                ("saved_entries", C.c_uint64), ("saved_bytes", C.c_uint64),
+                ("replicas_stepped", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

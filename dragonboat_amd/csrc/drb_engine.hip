@@ -37,6 +37,7 @@ struct drb_engine {
   hipStream_t stream2;            // the follower kernel of a round
   hipEvent_t ev_fork, ev_join;    // stream -> stream2 -> stream
   uint64_t round;
+  uint64_t ticks;  // LocalTicks delivered so far (RoundParams.tick_no)
   uint64_t bytes;
   std::vector<void *> allocs;
   uint64_t ctr_rows = 0;                     // workgroup counter rows
@@ -188,6 +189,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   drb_engine *e = new drb_engine();
   e->cfg = *cfg;
   e->round = 0;
+  e->ticks = 0;
   e->bytes = 0;
   e->scratch = nullptr;
   e->scratch_bytes = 0;
@@ -229,6 +231,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   v.election_rtt = cfg->election_rtt;
   v.heartbeat_rtt = cfg->heartbeat_rtt;
   v.check_quorum = cfg->check_quorum;
+  v.quiesce = cfg->quiesce ? 1u : 0u;
   v.first_shard_id = cfg->first_shard_id;
   v.place_world = cfg->place_world > 1 ? cfg->place_world : 1;
   v.place_rank = v.place_world > 1 ? cfg->place_rank : 0;
@@ -357,7 +360,8 @@ static const int kU64Order[NUM_U64_EXPORTED] = {
     F_COMMITTED,      F_PROCESSED,     F_LAST_INDEX,      F_MARKER_INDEX,
     F_SAVED_TO,       F_APPLIED_TO_INDEX, F_APPLIED_TO_TERM, F_APPLIED_INDEX,
     F_CONFIRMED_INDEX, F_PUSHED_INDEX, F_PREV_TERM,       F_PREV_VOTE,
-    F_PREV_COMMIT,    F_SM_INDEX,      F_SM_TERM,         F_KV_COUNT};
+    F_PREV_COMMIT,    F_SM_INDEX,      F_SM_TERM,         F_KV_COUNT,
+    F_QS_TICK,        F_QS_IDLE,       F_QS_SINCE,        F_QS_EXIT};
 
 // drb_replica_state fields 2.. in kU64Order order (after shard/replica id)
 static uint64_t *st_u64(drb_replica_state *s, int k) {
@@ -452,12 +456,18 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
                                  w[4 * ch + 3]));
       }
       // overflow of escaped fields and the u64 counters
+      // a quiesced replica's skipped ticks count from now
+      vals[F_QS_BASE] = e->ticks;
       for (int k = 0; k < NUM_U64; ++k) {
-        const bool counter = k == F_TICK_COUNT || k == F_KV_COUNT;
+        const bool counter = k == F_TICK_COUNT || k == F_KV_COUNT ||
+                             (k >= F_QS_TICK && k <= F_QS_EXIT) ||
+                             k == F_QS_BASE;
         i64.push_back(u64_ix(v, k, s, g));
         d64.push_back(counter ? vals[k] : (over[k] ? over[k] : vals[k]));
       }
-      const uint32_t w32[NUM_U32] = {c.role, c.flags & F_PUBLIC,
+      const uint32_t quiesced =
+          v.quiesce && c.qs_quiesced_since > 0 ? F_QUIESCED : 0u;
+      const uint32_t w32[NUM_U32] = {c.role, (c.flags & F_PUBLIC) | quiesced,
                                      c.fallback_reason, c.ri_count};
       for (int k = 0; k < NUM_U32; ++k) {
         i32.push_back(u32_ix(v, k, s, g));
@@ -532,6 +542,14 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       o.replica_id = s + 1;
       for (int k = 0; k < NUM_U64_EXPORTED; ++k)
         *st_u64(&o, k) = d64[a + kU64Order[k]];
+      const uint32_t fl = d32[b + 1];
+      if ((fl & F_QUIESCED) && (fl & DRB_F_HOSTED) &&
+          !(fl & (DRB_F_FALLBACK | DRB_F_ERROR))) {
+        // quiesced ticks not applied yet (drb_step.hpp, F_QS_BASE)
+        const uint64_t owed = e->ticks - d64[a + F_QS_BASE];
+        o.election_tick += owed;
+        o.qs_current_tick += owed;
+      }
       a += NUM_U64;
       o.role = d32[b++];
       o.flags = d32[b++] & F_PUBLIC;
@@ -716,6 +734,12 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   SET(F_RING_LO, 1);
   SET(F_RING_GUARD, ~0ull);
   SET(F_TERM_START, L1);  // the leader's no-op opened the term
+  if (v.quiesce) {
+    // the election round of the setup ticked once, and its messages were
+    // activity (quiesce.go:40-74)
+    SET(F_QS_TICK, 1);
+    SET(F_QS_IDLE, 1);
+  }
 #undef SET
   uint32_t w[16];
   pk_encode(w, vals, over);
@@ -726,6 +750,8 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
         make_uint4(w[4 * ch], w[4 * ch + 1], w[4 * ch + 2], w[4 * ch + 3]);
   v.u64[u64_ix(v, F_TICK_COUNT, s, g)] = vals[F_TICK_COUNT];
   v.u64[u64_ix(v, F_KV_COUNT, s, g)] = 0;
+  for (int f = F_QS_TICK; f <= F_QS_EXIT; ++f) v.u64[u64_ix(v, f, s, g)] = vals[f];
+  v.u64[u64_ix(v, F_QS_BASE, s, g)] = 0;
   v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
   v.u32[u32_ix(v, W_FLAGS, s, g)] =
       gid(v, s, g) < v.total_groups ? DRB_F_HOSTED : 0u;
@@ -779,6 +805,7 @@ extern "C" int drb_init_steady(drb_engine *e, uint64_t term,
   if (e->cfg.cmd_cap < 32 || e->v.W < e->cfg.num_replicas + 2)
     return DRB_EINVAL;
   e->v.stage_slot = leader_slot;  // staged inputs go to the leaders
+  e->ticks = 0;                   // every replica's ticks start here
   dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
   k_init_steady<<<grid, 256, 0, e->stream>>>(e->v, term, leader_slot, seed);
   HIPCHK(hipGetLastError());
@@ -982,12 +1009,27 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     std::vector<uint4> meta;
     if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
     uint4 cur = meta[0];
-    if (cur.x != tag) {
+    if (!tag_is(cur.x, tag)) {
       cur = pack2(0, 0);
-      cur.x = tag;
+      cur.x = tag & MQ_TAG;
     }
-    uint32_t k = cur.y & MI_COUNT;
-    if (k >= v.MB) {  // MessageQueue full (message.go:105-123)
+    if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
+      cur.x |= MQ_QUIESCE;
+      std::vector<uint4> mv = {cur};
+      if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
+      std::vector<uint64_t> ti = {((uint64_t)buf * v.R + to) * v.G + g};
+      std::vector<uint64_t> tv;
+      if (gather(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
+      tv[0] = (tv[0] & ~(0xffull << (8 * from))) |
+              ((uint64_t)(tag & 0xffu) << (8 * from));
+      if (scatter(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
+      acc++;
+      continue;
+    }
+    const bool rep = m.type == DRB_MSG_REPLICATE;
+    const uint32_t nrep0 = mi_nrep(cur.y);
+    const uint32_t k = rep ? nrep0 : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (mi_count(cur.y) >= v.MB) {  // MessageQueue full (message.go:105-123)
       drop++;
       continue;
     }
@@ -1033,18 +1075,15 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                                  mbox_ix(v, buf, from, to, k, 1, g)};
     std::vector<uint4> val = {c0, c1};
     if (scatter(e, v.mbox, idx, val)) return DRB_EDEVICE;
-    constexpr uint32_t cnts = MI_COUNT | (0xfu << MI_NRI) | (0xfu << MI_NRR);
     const uint32_t inf =
         msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0);
-    cur.y = (cur.y + (inf & cnts)) | (inf & ~cnts);
-    if (m.type == DRB_MSG_REPLICATE) {
-      cur.y |= 1u << (MI_REPMASK + k);
+    cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
+    if (rep) {
       std::vector<uint64_t> xi = {mi[0]};
       std::vector<uint64_t> xv;
       if (gather(e, v.mbox_maxapp, xi, xv)) return DRB_EDEVICE;
       uint64_t ma = m.log_index + m.n_entries;
-      if (k > 0 && (cur.y & (((1u << k) - 1u) << MI_REPMASK)))
-        ma = std::max(ma, xv[0]);
+      if (nrep0 > 0) ma = std::max(ma, xv[0]);
       std::vector<uint64_t> nv = {ma};
       if (scatter(e, v.mbox_maxapp, xi, nv)) return DRB_EDEVICE;
     }
@@ -1114,7 +1153,8 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const bool split = DRB_SERVE_SPLIT && !DRB_ROLE_STREAMS && nl && p0.n_reads;
   if (split) pl.n_reads = 0;
   // the EXT instantiation only where its paths can run (drb_step.hpp)
-  const bool ext = e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves;
+  const bool ext =
+      e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves || e->v.quiesce;
   pl.nrows = nl;
   pf.nrows = nf;
   // one-dimensional grids, rows interleaved per XCD (block_pos)
@@ -1186,6 +1226,7 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.nrows = 1;
   p.round = e->round + 1;
   p.tick = in->tick ? 1 : 0;
+  p.tick_no = e->ticks + p.tick;
   p.prop_slot = in->prop_slot;
   p.ri_slot = in->ri_slot;
   p.n_reads = in->reads_per_ctx;
@@ -1193,6 +1234,10 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (p.n_reads && !p.key_space) return DRB_EINVAL;
   p.encode_saves = in->encode_saves ? 1 : 0;
   if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
+  p.ri_replica = in->ri_replica;
+  p.pad = 0;
+  if (p.ri_replica > e->v.R || (p.ri_replica && e->v.place_world > 1))
+    return DRB_EINVAL;
   if (e->v.remote_mask)  // plane summaries of this round only
     HIPCHK(hipMemsetAsync(e->v.xrows, 0,
                           2ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
@@ -1210,6 +1255,7 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   }
   HIPCHK(hipGetLastError());
   e->round++;
+  e->ticks += p.tick;
   return DRB_OK;
 }
 
@@ -1254,6 +1300,7 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->reads_deferred = c[C_READS_DEFERRED];
   out->saved_entries = c[C_SAVED_ENTRIES];
   out->saved_bytes = c[C_SAVED_BYTES];
+  out->replicas_stepped = c[C_STEPPED];
   if (reset) {
     HIPCHK(hipMemsetAsync(e->v.counters, 0,
                           e->ctr_rows * NUM_COUNTERS * sizeof(c[0]),
@@ -1321,12 +1368,28 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
                        size_t *ne, uint8_t *pool, size_t pcap, size_t *np,
                        uint4 meta) {
   const View &v = e->v;
-  const uint32_t k = meta.x == (uint32_t)e->round ? (meta.y & MI_COUNT) : 0;
+  const bool cur = tag_is(meta.x, e->round);
+  const uint32_t k = cur ? mi_count(meta.y) : 0;
+  if (cur && (meta.x & MQ_QUIESCE)) {  // sendEnterQuiesceMessages
+    if (*nm >= cap) return DRB_ERANGE;
+    drb_message &m = out[(*nm)++];
+    memset(&m, 0, sizeof(m));
+    m.shard_id = v.first_shard_id + gid(v, from, g);
+    m.from = from + 1;
+    m.to = to + 1;
+    m.type = DRB_MSG_QUIESCE;
+    m.entries_off = *ne;
+  }
   if (!k) return DRB_OK;
+  // send order: the Replicates, then the others (drb_msg.hpp)
+  std::vector<uint32_t> pos;
+  for (uint32_t q = 0; q < mi_nrep(meta.y); ++q) pos.push_back(rec_pos(true, q, v.MB));
+  for (uint32_t q = 0; q < mi_noth(meta.y); ++q)
+    pos.push_back(rec_pos(false, q, v.MB));
   std::vector<uint64_t> idx;
   for (uint32_t q = 0; q < k; ++q)
     for (uint32_t c = 0; c < MSG_CHUNKS; ++c)
-      idx.push_back(mbox_ix(v, buf, from, to, q, c, g));
+      idx.push_back(mbox_ix(v, buf, from, to, pos[q], c, g));
   std::vector<uint4> val;
   if (gather(e, v.mbox, idx, val)) return DRB_EDEVICE;
   uint64_t prev_lo = 0, prev_hi = 0;
@@ -1423,31 +1486,36 @@ extern "C" int drb_export_ready_to_reads(drb_engine *e, uint64_t group,
 }
 
 // ---------------------------------------------------------------- exchange
+// the plane words (include/drb_engine.h DRB_PLANE_*) reduced over the
+// per-block rows of both roles: max counts, OR of the flags
 __global__ void k_plane_sum(const uint32_t *rows, uint32_t RR,
                             uint32_t blocks, uint32_t *out) {
-  __shared__ uint32_t red[3][256];
+  __shared__ uint32_t red[4][256];
   const uint32_t pair = blockIdx.x;
-  uint32_t k = 0, en = 0, f = 0;
+  uint32_t kr = 0, ko = 0, en = 0, f = 0;
   for (uint32_t role = 0; role < 2; ++role)
     for (uint32_t b = threadIdx.x; b < blocks; b += blockDim.x) {
       const uint32_t w = rows[((uint64_t)role * RR + pair) * blocks + b];
-      k = max(k, w & 0xffu);
-      en = max(en, (w >> 8) & 0xffu);
-      f |= w >> 16;
+      kr = max(kr, DRB_PLANE_KREP(w));
+      ko = max(ko, DRB_PLANE_KOTH(w));
+      en = max(en, DRB_PLANE_E(w));
+      f |= w & (DRB_PLANE_C1 | DRB_PLANE_HDR);
     }
-  red[0][threadIdx.x] = k;
-  red[1][threadIdx.x] = en;
-  red[2][threadIdx.x] = f;
+  red[0][threadIdx.x] = kr;
+  red[1][threadIdx.x] = ko;
+  red[2][threadIdx.x] = en;
+  red[3][threadIdx.x] = f;
   __syncthreads();
   for (uint32_t o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o) {
-      red[0][threadIdx.x] = max(red[0][threadIdx.x], red[0][threadIdx.x + o]);
-      red[1][threadIdx.x] = max(red[1][threadIdx.x], red[1][threadIdx.x + o]);
-      red[2][threadIdx.x] |= red[2][threadIdx.x + o];
+      for (int q = 0; q < 3; ++q)
+        red[q][threadIdx.x] = max(red[q][threadIdx.x], red[q][threadIdx.x + o]);
+      red[3][threadIdx.x] |= red[3][threadIdx.x + o];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[pair] = red[0][0] | (red[1][0] << 8) | (red[2][0] << 16);
+  if (threadIdx.x == 0)
+    out[pair] = red[0][0] | (red[1][0] << 5) | (red[2][0] << 10) | red[3][0];
 }
 
 extern "C" int drb_plane_counts(drb_engine *e, uint32_t *words) {
@@ -1489,8 +1557,9 @@ extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
   const View &v = e->v;
   if (!pair_remote(v, from, to) || e->round == 0) return 0;
   const uint32_t buf = (uint32_t)(e->round & 1);  // the last round's outbox
-  const uint32_t K = DRB_PLANE_K(word), En = DRB_PLANE_E(word);
-  if (K > v.MB || En > v.E) return DRB_ERANGE;
+  const uint32_t Kr = DRB_PLANE_KREP(word), Ko = DRB_PLANE_KOTH(word),
+                 En = DRB_PLANE_E(word);
+  if (Kr + Ko > v.MB || En > v.E) return DRB_ERANGE;
   uint4 *mb = dir ? v.mbox_in : v.mbox;
   uint4 *meta = dir ? v.meta_in : v.mbox_meta;
   uint64_t *mx = dir ? v.maxapp_in : v.mbox_maxapp;
@@ -1498,14 +1567,17 @@ extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
   uint4 *eb = dir ? v.embox_in : v.embox;
   const uint64_t G = v.G;
   int n = 0;
-  if (K) {
-    out[n++] = {mb + mbox_ix(v, buf, from, to, 0, 0, 0), K * G * 16};
-    if (word & DRB_PLANE_C1)
-      out[n++] = {mb + mbox_ix(v, buf, from, to, 0, 1, 0), K * G * 16};
-    out[n++] = {meta + mmeta_ix(v, buf, from, to, 0), G * 16};
-    if (word & DRB_PLANE_REP)
-      out[n++] = {mx + mmeta_ix(v, buf, from, to, 0), G * 8};
+  // Replicate records at positions [0, Kr), the others at [MB - Ko, MB)
+  // (drb_msg.hpp), per chunk
+  for (uint32_t c = 0; c < ((word & DRB_PLANE_C1) ? 2u : 1u); ++c) {
+    if (Kr) out[n++] = {mb + mbox_ix(v, buf, from, to, 0, c, 0), Kr * G * 16};
+    if (Ko)
+      out[n++] = {mb + mbox_ix(v, buf, from, to, v.MB - Ko, c, 0),
+                  Ko * G * 16};
   }
+  if (Kr || Ko || (word & DRB_PLANE_HDR))
+    out[n++] = {meta + mmeta_ix(v, buf, from, to, 0), G * 16};
+  if (Kr) out[n++] = {mx + mmeta_ix(v, buf, from, to, 0), G * 8};
   if (En) {
     out[n++] = {elo + mmeta_ix(v, buf, from, to, 0), G * 8};
     out[n++] = {eb + embox_ix(v, buf, from, to, 0, 0, 0),

@@ -46,10 +46,16 @@ enum U64Field : int {
   F_SM_INDEX,
   F_SM_TERM,
   F_KV_COUNT,
+  F_QS_TICK,     // quiesceState.currentTick (quiesce.go:23-33)
+  F_QS_IDLE,     // .idleSince
+  F_QS_SINCE,    // .quiescedSince (0: not quiesced)
+  F_QS_EXIT,     // .exitQuiesceTick
   // internal (not part of drb_replica_state)
   F_RING_LO,     // lowest index still resident in the window
   F_RING_GUARD,  // lowest index referenced by last round's Replicates
   F_TERM_START,  // every entry in [term_start, last] has term == r.term
+  F_QS_BASE,     // engine tick count the replica's ticks are applied up to
+                 // (a quiesced replica's ticks are applied lazily)
   NUM_U64
 };
 constexpr int NUM_U64_EXPORTED = F_RING_LO;
@@ -206,6 +212,8 @@ __host__ __device__ inline void pk_decode(const uint32_t *w,
   }
   vals[F_TICK_COUNT] = over[F_TICK_COUNT];
   vals[F_KV_COUNT] = over[F_KV_COUNT];
+  for (int f = F_QS_TICK; f <= F_QS_EXIT; ++f) vals[f] = over[f];
+  vals[F_QS_BASE] = over[F_QS_BASE];
 }
 
 // per-replica u32 fields, array [F][slot][g]
@@ -213,6 +221,7 @@ enum U32Field : int { W_ROLE = 0, W_FLAGS, W_FB_REASON, W_RI_COUNT, NUM_U32 };
 
 // internal W_FLAGS bits (masked out of drb_replica_state.flags)
 constexpr uint32_t F_AT_REST = 1u << 16;  // a round without input is a no-op
+constexpr uint32_t F_QUIESCED = 1u << 17;  // node.qs.quiesced() (Quiesce on)
 constexpr uint32_t F_PUBLIC = 0xffffu;
 
 // message record: 1-2 x uint4 (drb_msg.hpp)
@@ -257,7 +266,7 @@ struct View {
   uint32_t kv_val_cap;
   uint32_t max_props;
   uint32_t election_rtt, heartbeat_rtt, check_quorum;
-  uint32_t pad0;
+  uint32_t quiesce;  // Config.Quiesce; qs.electionTick = 2 x election_rtt
   uint64_t first_shard_id;
 
   uint64_t *u64;          // [NUM_U64][R][G] (overflow, tick/kv counts)

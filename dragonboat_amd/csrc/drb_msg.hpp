@@ -42,20 +42,47 @@ constexpr uint32_t MF_C_DELTA = 1u << 13;
 constexpr uint32_t MF_HINT_PREV = 1u << 14;
 constexpr uint32_t MF_HH32 = 1u << 15;
 
+// Records of a (sender, receiver, round) sit in send order: the
+// Replicates ascending from position 0 (node.sendReplicateMessages sends
+// them ahead of the rest, engine.go:1334-1336, node.go:1016-1023), the
+// other messages descending from position MB - 1 (processRaftUpdate ->
+// sendMessages, node.go:1104-1108).
 // header info word, per (sender, receiver, round)
-constexpr uint32_t MI_COUNT = 0xfu;       // [0:4] records
-constexpr int MI_NRI = 4;                 // [4:8] ReadIndex records
-constexpr int MI_NRR = 8;                 // [8:12] ReplicateResp records
-constexpr uint32_t MI_RESP = 1u << 12;    // a ReplicateResp / HeartbeatResp
-constexpr uint32_t MI_REP = 1u << 13;     // a Replicate (max_app is valid)
-constexpr uint32_t MI_OFF_LEADER = 1u << 14;    // a type a leader leaves
-constexpr uint32_t MI_OFF_FOLLOWER = 1u << 15;  // the fast path for / a
+constexpr uint32_t MI_NREP = 0x1fu;       // [0:5] Replicate records
+constexpr int MI_NOTH = 5;                // [5:10] other records
+constexpr int MI_NRI = 10;                // [10:15] ReadIndex records
+constexpr int MI_NRR = 15;                // [15:20] ReplicateResp records
+constexpr uint32_t MI_CNTS = MI_NREP | (0x1fu << MI_NOTH) |
+                             (0x1fu << MI_NRI) | (0x1fu << MI_NRR);
+constexpr uint32_t MI_RESP = 1u << 20;    // a ReplicateResp / HeartbeatResp
+constexpr uint32_t MI_OFF_LEADER = 1u << 21;    // a type a leader leaves
+constexpr uint32_t MI_OFF_FOLLOWER = 1u << 22;  // the fast path for / a
                                                 // follower does
-constexpr uint32_t MI_TERM = 1u << 16;        // a record carries the term
-constexpr uint32_t MI_TERM_OTHER = 1u << 17;  // a record's term != header's
-constexpr int MI_REPMASK = 18;  // [18:31] bit k: record k is a Replicate
-constexpr uint32_t MI_REJECT = 1u << 31;  // a rejecting ReplicateResp
-constexpr uint32_t MB_MAX = 13;  // records per (sender, receiver, round)
+constexpr uint32_t MI_TERM = 1u << 23;        // a record carries the term
+constexpr uint32_t MI_TERM_OTHER = 1u << 24;  // a record's term != header's
+constexpr uint32_t MI_REJECT = 1u << 25;  // a rejecting ReplicateResp
+constexpr uint32_t MB_MAX = 24;  // records per (sender, receiver, round)
+__host__ __device__ inline uint32_t mi_nrep(uint32_t w) { return w & MI_NREP; }
+__host__ __device__ inline uint32_t mi_noth(uint32_t w) {
+  return (w >> MI_NOTH) & 0x1fu;
+}
+__host__ __device__ inline uint32_t mi_count(uint32_t w) {
+  return mi_nrep(w) + mi_noth(w);
+}
+// position of the j-th record of its kind
+__host__ __device__ inline uint32_t rec_pos(bool rep, uint32_t j,
+                                            uint32_t MB) {
+  return rep ? j : MB - 1 - j;
+}
+// header tag word: bits [0:31] the round tag, bit 31 a Quiesce message
+// (node.sendEnterQuiesceMessages, node.go:993-1005) from the sender this
+// round; it precedes the sender's other non-Replicate messages (it is sent
+// straight from stepNode, before the Update's messages)
+constexpr uint32_t MQ_QUIESCE = 1u << 31;
+constexpr uint32_t MQ_TAG = 0x7fffffffu;
+__host__ __device__ inline bool tag_is(uint32_t word, uint64_t round) {
+  return (word & MQ_TAG) == ((uint32_t)round & MQ_TAG);
+}
 
 struct Msg {
   uint32_t type, reject, n;
@@ -96,13 +123,12 @@ __host__ __device__ inline bool is_ctx_type(uint32_t t) {
 // header info contribution of one record
 __host__ __device__ inline uint32_t msg_info(uint32_t type, bool term_zero,
                                              bool reject = false) {
-  uint32_t i = 1;  // count
+  uint32_t i = type == DRB_MSG_REPLICATE ? 1u : 1u << MI_NOTH;  // counts
   if (reject && type == DRB_MSG_REPLICATE_RESP) i |= MI_REJECT;
   if (type == DRB_MSG_READ_INDEX) i += 1u << MI_NRI;
   if (type == DRB_MSG_REPLICATE_RESP) i += 1u << MI_NRR;
   if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)
     i |= MI_RESP;
-  if (type == DRB_MSG_REPLICATE) i |= MI_REP;
   if (!(type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP ||
         type == DRB_MSG_READ_INDEX))
     i |= MI_OFF_LEADER;

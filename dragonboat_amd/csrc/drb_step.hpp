@@ -81,6 +81,7 @@ enum : int {
   C_READS_DEFERRED,
   C_SAVED_ENTRIES,  // encode_saves
   C_SAVED_BYTES,
+  C_STEPPED,  // replicas that ran the round (not skipped as idle)
   NUM_COUNTERS
 };
 
@@ -116,6 +117,9 @@ struct Rep {
   uint64_t guard_new;
   bool leader_update;
   bool err;
+  // node.qs (Quiesce on, EXT instantiation): quiesce.go:23-33
+  uint64_t qs_tick, qs_idle, qs_since, qs_exit;
+  bool qs_new;  // newQuiesceStateFlag: send Quiesce to the peers
 };
 
 // Per-lane remote progress table in LDS, [peer][lane]: dynamically
@@ -186,6 +190,58 @@ DRB_DEV void set_leader(Rep<R> &r, uint64_t id) {
     r.leader_id = id;
     r.lid_dirty = true;
   }
+}
+
+// ------------------------------------------------------------ quiesce
+// quiesceState (quiesce.go:23-120) with electionTick = 2 x ElectionRTT
+// (node.go:195-200); threshold = 10 x that.
+template <int R>
+DRB_DEV bool qs_quiesced(const Rep<R> &r) { return r.qs_since > 0; }
+template <int R>
+DRB_DEV void qs_enter(Rep<R> &r) {  // enterQuiesce (quiesce.go:104-109)
+  r.qs_since = r.qs_tick;
+  r.qs_idle = r.qs_tick;
+  r.qs_new = true;
+}
+template <int R>
+DRB_DEV void qs_exit(Rep<R> &r) {  // exitQuiesce (quiesce.go:111-114)
+  r.qs_since = 0;
+  r.qs_exit = r.qs_tick;
+}
+// record (quiesce.go:56-74); heartbeats carrying a ReadIndex ctx count as
+// ReadIndex (node.recordMessage, node.go:1339-1345)
+template <int R>
+DRB_DEV void qs_record(const View &v, Rep<R> &r, uint32_t type) {
+  if (type == DRB_MSG_HEARTBEAT || type == DRB_MSG_HEARTBEAT_RESP) {
+    if (!qs_quiesced(r)) return;
+    if (r.qs_tick - r.qs_since < 2ull * v.election_rtt) return;  // newToQuiesce
+  }
+  r.qs_idle = r.qs_tick;
+  if (qs_quiesced(r)) qs_exit(r);
+}
+// tryEnterQuiesce (quiesce.go:91-102): a Quiesce message
+template <int R>
+DRB_DEV void qs_try_enter(const View &v, Rep<R> &r) {
+  if (!qs_quiesced(r) && r.qs_tick - r.qs_exit < 20ull * v.election_rtt)
+    return;  // justExitedQuiesce
+  if (!qs_quiesced(r)) qs_enter(r);
+}
+// Whether this round's LocalTick is a quiesced tick, for a round whose
+// inbox holds no record and no staged ReadIndex (only Quiesce messages):
+// tryEnterQuiesce on a Quiesce, then tick (node.go:1385-1386, 1562-1570)
+template <int R>
+DRB_DEV bool qs_quiet_tick(const View &v, const Rep<R> &r, uint32_t qz_from) {
+  const uint64_t thr = 20ull * v.election_rtt;
+  bool q = qs_quiesced(r);
+  if (!q && qz_from && !(r.qs_tick - r.qs_exit < thr)) q = true;
+  return q || (r.qs_tick + 1 - r.qs_idle > thr);
+}
+// tick (quiesce.go:40-51)
+template <int R>
+DRB_DEV void qs_tick_once(const View &v, Rep<R> &r) {
+  r.qs_tick++;
+  if (!qs_quiesced(r) && r.qs_tick - r.qs_idle > 20ull * v.election_rtt)
+    qs_enter(r);
 }
 
 // ------------------------------------------------------------ packed state
@@ -293,26 +349,25 @@ template <int R>
 DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   const View &v = *L.v;
   uint32_t &w = L.oi[to_slot * 256 + L.tid];
-  const uint32_t k = w & MI_COUNT;
-  if (k >= v.MB) {  // bounded by the pre-pass; never expected
+  if (mi_count(w) >= v.MB) {  // bounded by the pre-pass; never expected
     set_error(r, DRB_FB_CAPACITY);
     return;
   }
+  const bool rep = m.type == DRB_MSG_REPLICATE;
+  const uint32_t k = rep ? mi_nrep(w) : rec_pos(false, mi_noth(w), v.MB);
   r.nmsgs++;
   Msg mm = m;
   mm.term = is_request_type(m.type) ? 0 : r.term;
   uint4 c0, c1;
   const bool has = msg_encode(mm, to_slot, &r.hc, c0, c1);
-  constexpr uint32_t cnts = MI_COUNT | (0xfu << MI_NRI) | (0xfu << MI_NRR);
   const uint32_t inf = msg_info(mm.type, mm.term == 0, m.reject != 0);
-  w = (w + (inf & cnts)) | (inf & ~cnts);
+  w = (w + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
   v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] = c0;
   if (has) {
     v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] = c1;
     r.c1mask |= 1u << to_slot;
   }
-  if (m.type == DRB_MSG_REPLICATE) {
-    w |= 1u << (MI_REPMASK + k);
+  if (rep) {
     // entries to a replica on another rank travel by value: the rows
     // [lowest index sent, last] ship with the plane (end of the round)
     if (m.n && pair_remote(v, L.slot, to_slot)) {
@@ -793,6 +848,22 @@ DRB_DEV void follower_heartbeat(const Lane &L, Rep<R> &r, int s,
   resp.hint = m.hint;
   resp.hint_high = m.hint_high;
   emit(L, r, s, resp);
+}
+
+// handleFollowerReadIndex (raft.go:2134-2144): forwarded to the leader
+// (From = self, Term 0: a request type, raft.go:667-687)
+template <int R>
+DRB_DEV void follower_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
+                                 uint64_t hi) {
+  if (r.leader_id == 0 || r.leader_id > (uint64_t)R) {
+    r.ndropped_ri++;  // reportDroppedReadIndex
+    return;
+  }
+  Msg m = {};
+  m.type = DRB_MSG_READ_INDEX;
+  m.hint = lo;
+  m.hint_high = hi;
+  emit(L, r, (uint32_t)(r.leader_id - 1), m);
 }
 
 // handleFollowerReadIndexResp (raft.go:2155-2164)
@@ -1389,7 +1460,24 @@ struct RoundParams {
   uint32_t encode_saves;
   uint32_t slots;  // slot of block row y = (slots >> 4 * y) & 15
   uint32_t nrows;  // block rows (slots) of this launch; see block_pos
+  uint64_t tick_no;  // engine ticks so far, this round's included
+  uint32_t ri_replica;  // staged ReadIndex at: 0 the leader, else ID
+  uint32_t pad;
 };
+
+// Whether this replica takes the lane's staged proposals / ReadIndex
+// (co-resident: the leader, or replica ri_replica for reads; replicas
+// spread over ranks: the stage slot's).
+template <bool LEAD>
+DRB_DEV bool stage_here(const View &v, uint32_t slot) {
+  return LEAD && (v.place_world <= 1 || slot == v.stage_slot);
+}
+template <bool LEAD>
+DRB_DEV bool ri_here(const View &v, const RoundParams &p, uint32_t slot) {
+  if (p.ri_slot == DRB_NONE) return false;
+  return p.ri_replica == 0 ? stage_here<LEAD>(v, slot)
+                           : slot + 1 == p.ri_replica;
+}
 
 // The logical (x = group block, y = slot row) of this workgroup.  The
 // launch is one-dimensional, gx * nrows workgroups, and the dispatcher
@@ -1456,34 +1544,38 @@ DRB_DEV void block_counters(const View &v, uint32_t slot, BlockPos bp,
 // K | E << 8 | flags << 16 (max, max, or over the block's lanes)
 template <bool LEAD>
 DRB_DEV void block_plane_summary(const View &v, BlockPos bp, uint32_t from,
-                                 uint32_t to, uint32_t K, uint32_t E,
-                                 uint32_t fl) {
-  __shared__ uint32_t red[4][3];
+                                 uint32_t to, uint32_t Kr, uint32_t Ko,
+                                 uint32_t E, uint32_t fl) {
+  __shared__ uint32_t red[4][4];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    K = max(K, (uint32_t)__shfl_xor(K, o, 64));
+    Kr = max(Kr, (uint32_t)__shfl_xor(Kr, o, 64));
+    Ko = max(Ko, (uint32_t)__shfl_xor(Ko, o, 64));
     E = max(E, (uint32_t)__shfl_xor(E, o, 64));
     fl |= (uint32_t)__shfl_xor(fl, o, 64);
   }
   __syncthreads();  // red[] is reused across destinations
   if (lane == 0) {
-    red[wave][0] = K;
-    red[wave][1] = E;
-    red[wave][2] = fl;
+    red[wave][0] = Kr;
+    red[wave][1] = Ko;
+    red[wave][2] = E;
+    red[wave][3] = fl;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t k = 0, e = 0, f = 0;
+    uint32_t kr = 0, ko = 0, e = 0, f = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      k = max(k, red[w][0]);
-      e = max(e, red[w][1]);
-      f |= red[w][2];
+      kr = max(kr, red[w][0]);
+      ko = max(ko, red[w][1]);
+      e = max(e, red[w][2]);
+      f |= red[w][3];
     }
     const uint64_t row = (((uint64_t)(LEAD ? 0 : 1) * v.R + from) * v.R + to) *
                              bp.gx + bp.x;
-    v.xrows[row] = k | (e << 8) | (f << 16);
+    // the DRB_PLANE_* word of include/drb_engine.h
+    v.xrows[row] = kr | (ko << 5) | (e << 10) | (f << 18);
   }
 }
 
@@ -1529,7 +1621,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint64_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
+  uint32_t c_stepped = 0;
   uint32_t sent_c1 = 0;     // remote planes: destinations given a c1 chunk
+  uint32_t qz_out = 0;      // destinations sent a Quiesce message
   uint64_t last_final = 0;  // leader: last index at the end of the round
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
@@ -1549,7 +1643,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   // co-resident sender, which the senders' one-byte round tags tell
   // without reading the mailbox headers.  Its round outputs are already
   // empty (a round that produced any does not leave the replica at rest).
-  if (active && !p.tick && (flags & F_AT_REST) && !v.remote_mask) {
+  // With Quiesce on, a quiesced replica at rest also skips tick rounds
+  // without input: a quiesced tick only advances its tick counters
+  // (node.tick node.go:1562-1579, raft.quiescedTick raft.go:650-656),
+  // which the next round it runs applies at once (F_QS_BASE).
+  if (active && (!p.tick || (EXT && (flags & F_QUIESCED))) &&
+      (flags & F_AT_REST) && !v.remote_mask) {
     const uint64_t tags = v.inbox_tag[((uint64_t)L.rbuf * v.R + slot) * v.G + g];
     const uint32_t want = (uint32_t)(p.round - 1) & 0xffu;
     bool input = false;
@@ -1557,17 +1656,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     for (int s = 0; s < R; ++s)
       if ((uint32_t)s != slot && ((tags >> (8 * s)) & 0xffu) == want)
         input = true;
-    if (LEAD && (v.place_world <= 1 || slot == v.stage_slot)) {
-      if (p.prop_slot != DRB_NONE &&
-          v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
-        input = true;
-      if (p.ri_slot != DRB_NONE && v.ri_in[(uint64_t)p.ri_slot * v.G + g].x |
-                                       v.ri_in[(uint64_t)p.ri_slot * v.G + g].y)
-        input = true;
-    }
+    if (stage_here<LEAD>(v, slot) && p.prop_slot != DRB_NONE &&
+        v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
+      input = true;
+    if (ri_here<LEAD>(v, p, slot) &&
+        (v.ri_in[(uint64_t)p.ri_slot * v.G + g].x |
+         v.ri_in[(uint64_t)p.ri_slot * v.G + g].y))
+      input = true;
     if (!input) active = false;
   }
   if (active) {
+    c_stepped = 1;
     Rep<R> r;
     load_rep<R, LEAD>(L, r);
     r.role = LEAD ? DRB_LEADER : DRB_FOLLOWER;
@@ -1585,17 +1684,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     r.guard_new = ~0ull;
     r.leader_update = false;
     r.err = false;
+    r.qs_new = false;
     const uint32_t flags0 = r.flags, fb0 = r.fb;
     const uint32_t tag_prev = (uint32_t)(p.round - 1);
+    const bool qon = EXT && v.quiesce;
+    uint64_t qs_owed = 0;
+    if (qon) {
+      r.qs_tick = over_ld(L, F_QS_TICK);
+      r.qs_idle = over_ld(L, F_QS_IDLE);
+      r.qs_since = over_ld(L, F_QS_SINCE);
+      r.qs_exit = over_ld(L, F_QS_EXIT);
+      // the quiesced ticks this replica skipped (only ever while quiesced)
+      qs_owed = p.tick_no - p.tick - over_ld(L, F_QS_BASE);
+      r.election_tick += qs_owed;
+      r.qs_tick += qs_owed;
+    }
 
     // ---------------------------------------------- pre-pass (read only)
     uint32_t fb = DRB_FB_NONE;
     constexpr bool is_leader = LEAD;
     if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) fb = DRB_FB_ROLE;
     // the inbox, from the per-sender headers alone (drb_msg.hpp)
-    uint32_t nin_packed = 0;  // 4-bit inbox count per sender slot
+    uint64_t nin_packed = 0;  // 5-bit inbox record count per sender
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
     uint32_t rej_from = 0;  // senders with a rejecting ReplicateResp
+    uint32_t qz_from = 0;   // senders whose Quiesce message arrived
+    uint64_t nri_packed = 0;  // 5-bit ReadIndex record count per sender
     uint64_t max_app = 0;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
@@ -1603,9 +1717,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       const bool rm = pair_remote(v, s, slot);
       const uint4 meta = (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(v, L.rbuf, s,
                                                                  slot, g)];
-      const uint32_t info = meta.x == tag_prev ? meta.y : 0u;
-      const uint32_t ns = info & MI_COUNT;
-      nin_packed |= ns << (4 * s);
+      const bool cur = tag_is(meta.x, tag_prev);
+      const uint32_t info = cur ? meta.y : 0u;
+      const uint32_t ns = mi_count(info);
+      nin_packed |= (uint64_t)ns << (5 * s);
+      if (cur && (meta.x & MQ_QUIESCE)) qz_from |= 1u << s;
       if ((info & (LEAD ? MI_OFF_LEADER : MI_OFF_FOLLOWER)) &&
           fb == DRB_FB_NONE)
         fb = DRB_FB_MESSAGE_TYPE;
@@ -1613,11 +1729,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
            ((info & MI_TERM) && hi64(meta) != r.term)) &&
           fb == DRB_FB_NONE)
         fb = DRB_FB_TERM_MISMATCH;
-      n_ri_msgs += (info >> MI_NRI) & 15u;
-      n_rr += (info >> MI_NRR) & 15u;
+      n_ri_msgs += (info >> MI_NRI) & 0x1fu;
+      nri_packed |= (uint64_t)((info >> MI_NRI) & 0x1fu) << (5 * s);
+      n_rr += (info >> MI_NRR) & 0x1fu;
       if (info & MI_RESP) resp_from |= 1u << s;
       if (info & MI_REJECT) rej_from |= 1u << s;
-      if (!LEAD && (info & MI_REP))
+      if (!LEAD && mi_nrep(info))
         max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
                                       v, L.rbuf, s, slot, g)]);
       total_in += ns;
@@ -1628,17 +1745,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     // applied-to term
     const uint64_t keep_common =
         umin64(umin64(r.processed + 1, r.committed), r.sm_index);
+    // staged inputs are per lane: with replicas spread over ranks a lane
+    // holds R different groups, and they go to the stage slot's leader
+    if (ri_here<LEAD>(v, p, slot)) {
+      uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
+      in_lo = lo64(c);
+      in_hi = hi64(c);
+    }
     if (is_leader) {
-      // staged inputs are per lane: with replicas spread over ranks a lane
-      // holds R different groups, and they go to the stage slot's leader
-      const bool stage = v.place_world <= 1 || slot == v.stage_slot;
-      if (p.prop_slot != DRB_NONE && stage)
+      if (p.prop_slot != DRB_NONE && stage_here<LEAD>(v, slot))
         nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
-      if (p.ri_slot != DRB_NONE && stage) {
-        uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
-        in_lo = lo64(c);
-        in_hi = hi64(c);
-      }
       if (r.ri_count + (in_lo != 0) + n_ri_msgs > DRB_RI_DEPTH &&
           fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
@@ -1706,12 +1822,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 #pragma unroll
         for (int s = 0; s < R; ++s) {
           if ((uint32_t)s == slot) continue;
-          uint32_t bound = base + ((nin_packed >> (4 * s)) & 15u);
+          // a ReadIndex from s is answered by the broadcast and the
+          // release counted in base, not by a send of its own
+          uint32_t bound = base + (uint32_t)((nin_packed >> (5 * s)) & 31u) -
+                           (uint32_t)((nri_packed >> (5 * s)) & 31u);
           if (bound > v.MB && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
         }
       }
-      // tick: CheckQuorum (raft.go:623-633)
-      if (p.tick && v.check_quorum &&
+      // tick: CheckQuorum (raft.go:623-633) -- not on a quiesced tick
+      const bool qtick = qon && p.tick && total_in == 0 && in_lo == 0 &&
+                         qs_quiet_tick(v, r, qz_from);
+      if (p.tick && !qtick && v.check_quorum &&
           r.election_tick + 1 >= v.election_rtt) {
         int c = 1;
 #pragma unroll
@@ -1725,7 +1846,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       if (max_app && max_app >= keep_common + v.W &&
           fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
-      if (p.tick) {
+      // mailbox: one response per message of a sender, plus the
+      // forwarded ReadIndex (handleFollowerReadIndex)
+#pragma unroll
+      for (int s = 0; s < R; ++s)
+        if ((uint32_t)s != slot &&
+            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) > v.MB &&
+            fb == DRB_FB_NONE)
+          fb = DRB_FB_CAPACITY;
+      const bool qtick =
+          qon && p.tick && total_in == 0 && qs_quiet_tick(v, r, qz_from);
+      if (p.tick && !qtick) {
         uint64_t et = (total_in ? 0 : r.election_tick) + 1;
         if (et >= ld_f(L, r, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
           fb = DRB_FB_ELECTION;
@@ -1746,48 +1877,74 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       v.u32[u32_ix(v, W_FLAGS, slot, g)] = r.flags;
       v.u32[u32_ix(v, W_FB_REASON, slot, g)] = r.fb;
       c_fb = 1;
+      if (qs_owed) {  // the pre-round state includes the skipped ticks
+        pu_put(L, r, 12, 1, F_ELECTION_TICK, r.election_tick);
+        v.pk[pk_ix(v, 3, slot, g)] =
+            make_uint4(r.pw[12], r.pw[13], r.pw[14], r.pw[15]);
+        over_st(L, F_QS_TICK, r.qs_tick);
+        over_st(L, F_QS_BASE, p.tick_no - p.tick);
+      }
     } else {
       // ---------------------------------------- handleEvents (node.go)
       // updateAppliedIndex (node.go:1133-1137)
       r.applied_index = r.sm_index;
       st_f(L, r, F_APPLIED, r.applied_index);  // applied_index: hot
       // handleReadIndex (node.go:1296) -> Peer.ReadIndex (peer.go:309)
-      if (is_leader && in_lo != 0) leader_read_index(L, r, in_lo, in_hi, 0);
+      if (in_lo != 0) {
+        if (qon) qs_record(v, r, DRB_MSG_READ_INDEX);
+        if (is_leader)
+          leader_read_index(L, r, in_lo, in_hi, 0);
+        else
+          follower_read_index(L, r, in_lo, in_hi);
+      }
       // handleReceivedMessages: Replicates by sender, then the rest
 #pragma unroll 1
       for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll 1
         for (int s = 0; s < R; ++s) {
           if ((uint32_t)s == slot) continue;
-          const uint32_t ns = (nin_packed >> (4 * s)) & 15u;
-          if (!ns) continue;
+          // a Quiesce from s precedes its other non-Replicate messages
+          // (node.handleMessage -> tryEnterQuiesce, node.go:1385-1386)
+          if (qon && pass == 1 && ((qz_from >> s) & 1)) qs_try_enter(v, r);
+          if (!((nin_packed >> (5 * s)) & 31u)) continue;
           const bool rm = pair_remote(v, s, slot);
           const uint4 *mb = rm ? v.mbox_in : v.mbox;
           const uint4 meta = (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(
               v, L.rbuf, s, slot, g)];
           const uint64_t sterm = hi64(meta);
-          // records of this pass: the header's Replicate mask
-          const uint32_t reps = meta.y >> MI_REPMASK;
-          uint32_t todo = (pass == 0 ? reps : ~reps) & ((1u << ns) - 1u);
+          // records of this pass: the Replicates, then the others
+          const uint32_t cnt = pass == 0 ? mi_nrep(meta.y) : mi_noth(meta.y);
           EntSrc src;
           src.remote = rm;
           src.lo = 0;
-          if (rm && pass == 0 && todo)
+          if (rm && pass == 0 && cnt)
             src.lo = v.elo_in[mmeta_ix(v, L.rbuf, s, slot, g)];
           uint64_t prev_lo = 0, prev_hi = 0;
-          while (todo) {
-            const uint32_t k = __builtin_ctz(todo);
-            todo &= todo - 1;
+          for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t k = rec_pos(pass == 0, j, v.MB);
             const uint4 c0 = mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
             uint4 c1 = make_uint4(0, 0, 0, 0);
             if (c0.x & MF_HAS_C1) c1 = mb[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
             const Msg m = msg_decode(c0, c1, sterm, prev_lo, prev_hi);
+            if (qon)  // node.recordMessage (node.go:1339-1345)
+              qs_record(v, r,
+                        (m.type == DRB_MSG_HEARTBEAT ||
+                         m.type == DRB_MSG_HEARTBEAT_RESP) && m.hint > 0
+                            ? (uint32_t)DRB_MSG_READ_INDEX
+                            : m.type);
             dispatch(L, r, s, m, src);
           }
         }
       }
       // LocalTick (node.tick node.go:1562 -> raft.tick raft.go:571-648)
-      if (p.tick) {
+      bool quiet = false;
+      if (p.tick && qon) {
+        qs_tick_once(v, r);
+        quiet = qs_quiesced(r);
+      }
+      if (p.tick && quiet) {
+        r.election_tick++;  // raft.quiescedTick (raft.go:650-656)
+      } else if (p.tick) {
         over_st(L, F_TICK_COUNT, over_ld(L, F_TICK_COUNT) + 1);
         if (is_leader) {
           r.election_tick++;
@@ -1830,6 +1987,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         rem_try_update<R>(L, (int)slot, r.last);  // self remote
         if (R == 1) try_commit(L, r);
         broadcast_replicate(L, r);
+      }
+      // stepNode: newQuiesceState -> sendEnterQuiesceMessages to every
+      // other member (node.go:993-1005, 1148-1150), sent ahead of the
+      // Update's messages (a header bit per destination, drb_msg.hpp)
+      if (qon && r.qs_new) {
+        qz_out = ((1u << R) - 1u) & ~(1u << slot);
+        r.nmsgs += R - 1;
       }
 
       // ---------------------------------------- getUpdate (node.go:1025)
@@ -1954,6 +2118,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
                         r.nrtr == 0 && !has_save &&
                         !(r.flags & (DRB_F_FALLBACK | DRB_F_ERROR));
       r.flags = rest ? (r.flags | F_AT_REST) : (r.flags & ~F_AT_REST);
+      if (qon) {
+        r.flags = qs_quiesced(r) ? (r.flags | F_QUIESCED)
+                                 : (r.flags & ~F_QUIESCED);
+        over_st(L, F_QS_TICK, r.qs_tick);
+        over_st(L, F_QS_IDLE, r.qs_idle);
+        over_st(L, F_QS_SINCE, r.qs_since);
+        over_st(L, F_QS_EXIT, r.qs_exit);
+        over_st(L, F_QS_BASE, p.tick_no);
+      }
       store_rep<R, LEAD>(L, r, flags0, fb0);
       c_msgs = r.nmsgs;
       c_rtr = r.nrtr;
@@ -1965,9 +2138,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       const uint32_t w = oinfo[s * 256 + threadIdx.x];
-      if (w & MI_COUNT) {
+      const bool qz = (qz_out >> s) & 1u;
+      if (mi_count(w) || qz) {
         uint4 meta = mk4(0, r.term);
-        meta.x = (uint32_t)p.round;
+        meta.x = ((uint32_t)p.round & MQ_TAG) | (qz ? MQ_QUIESCE : 0u);
         meta.y = w;
         v.mbox_meta[mmeta_ix(v, L.wbuf, slot, (uint32_t)s, g)] = meta;
         // the receiver's round tag byte for this sender (a byte store: the
@@ -1989,24 +2163,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot || !pair_remote(v, slot, s)) continue;
-      uint32_t K = 0, E = 0, fl = 0;
+      uint32_t Kr = 0, Ko = 0, E = 0, fl = 0;
       if (active) {
         const uint32_t w = oinfo[s * 256 + threadIdx.x];
-        K = w & MI_COUNT;
-        fl = ((sent_c1 >> s) & 1u) | ((w & MI_REP) ? 2u : 0u);
+        Kr = mi_nrep(w);
+        Ko = mi_noth(w);
+        fl = ((sent_c1 >> s) & 1u) | (((qz_out >> s) & 1u) << 1);
         if (LEAD) {
           const uint64_t lo = elo_lds[LEAD ? s : 0][threadIdx.x];
           if (lo != ~0ull) E = (uint32_t)(last_final + 1 - lo);
         }
       }
-      block_plane_summary<LEAD>(v, bp, slot, (uint32_t)s, K, E, fl);
+      block_plane_summary<LEAD>(v, bp, slot, (uint32_t)s, Kr, Ko, E, fl);
     }
   }
   const uint32_t cnt[NUM_COUNTERS] = {
       (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
       (uint32_t)c_err,    c_served,            c_deferred,
-      c_saved,            c_saved_bytes};
+      c_saved,            c_saved_bytes,       c_stepped};
   block_counters<LEAD, 0, NUM_COUNTERS>(v, slot, bp, cnt);
 }
 

@@ -122,25 +122,41 @@ struct WireMsg {
 };
 
 // walks the records of lane g's (from, to) plane in send order
+// (a Quiesce message -- a header bit, drb_msg.hpp -- comes first)
 struct WireCursor {
   uint4 meta;
   uint32_t k, q;
+  uint32_t qz;  // a Quiesce message still to produce
   uint64_t prev_lo, prev_hi;
 };
 
 DRB_DEV void wc_init(WireCursor &c, const View &v, const WireArgs &a,
                      uint64_t g) {
   c.meta = v.mbox_meta[mmeta_ix(v, a.buf, a.from, a.to, g)];
-  c.k = c.meta.x == a.round_tag ? (c.meta.y & MI_COUNT) : 0;
+  const bool cur = tag_is(c.meta.x, a.round_tag);
+  c.qz = cur && (c.meta.x & MQ_QUIESCE) ? 1u : 0u;
+  c.k = (cur ? mi_count(c.meta.y) : 0) + c.qz;
   c.q = 0;
   c.prev_lo = c.prev_hi = 0;
 }
 
 DRB_DEV WireMsg wc_next(WireCursor &c, const View &v, const WireArgs &a,
                         uint64_t g) {
-  const uint4 c0 = v.mbox[mbox_ix(v, a.buf, a.from, a.to, c.q, 0, g)];
+  if (c.qz) {  // node.sendEnterQuiesceMessages (node.go:993-1005)
+    c.qz = 0;
+    WireMsg w;
+    w.m = Msg{};
+    w.m.type = DRB_MSG_QUIESCE;
+    w.shard_id = v.first_shard_id + gid(v, a.from, g);
+    return w;
+  }
+  // send order: the Replicates, then the others (drb_msg.hpp)
+  const uint32_t nr = mi_nrep(c.meta.y);
+  const uint32_t k = c.q < nr ? rec_pos(true, c.q, v.MB)
+                              : rec_pos(false, c.q - nr, v.MB);
+  const uint4 c0 = v.mbox[mbox_ix(v, a.buf, a.from, a.to, k, 0, g)];
   uint4 c1 = make_uint4(0, 0, 0, 0);
-  if (c0.x & MF_HAS_C1) c1 = v.mbox[mbox_ix(v, a.buf, a.from, a.to, c.q, 1, g)];
+  if (c0.x & MF_HAS_C1) c1 = v.mbox[mbox_ix(v, a.buf, a.from, a.to, k, 1, g)];
   WireMsg w;
   w.m = msg_decode(c0, c1, q_hi(c.meta), c.prev_lo, c.prev_hi);
   w.shard_id = v.first_shard_id + gid(v, a.from, g);

@@ -122,10 +122,10 @@ def _u8(b):
 
 DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 cmd_cap=32, max_props=4, prop_slots=2, ri_slots=2,
-                mailbox=13, kv_slots=512, kv_val_cap=4, election_rtt=10,
+                mailbox=16, kv_slots=512, kv_val_cap=4, election_rtt=10,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
-                kv_pool_blocks=0, flagged_cap=0)
+                kv_pool_blocks=0, flagged_cap=0, quiesce=0)
 
 
 class Engine:
@@ -143,7 +143,7 @@ class Engine:
                    cfg["check_quorum"], cfg["device"], cfg["save_cap"],
                    cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
                    cfg["entry_mbox"], cfg["kv_pool_blocks"],
-                   cfg["flagged_cap"], 0)
+                   cfg["flagged_cap"], cfg["quiesce"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -238,9 +238,9 @@ class Engine:
 
     # ---------------------------------------------------------- round
     def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE,
-             reads_per_ctx=0, key_space=0, encode_saves=False):
+             reads_per_ctx=0, key_space=0, encode_saves=False, ri_replica=0):
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
-                      key_space, int(bool(encode_saves)))
+                      key_space, int(bool(encode_saves)), ri_replica)
         out = RoundOut()
         _ck(lib().drb_step_round(self.h, C.byref(rin), C.byref(out)),
             "drb_step_round")
@@ -248,12 +248,12 @@ class Engine:
 
     def step_async(self, tick=False, prop_slot=abi.DRB_NONE,
                    ri_slot=abi.DRB_NONE, reads_per_ctx=0, key_space=0,
-                   encode_saves=False):
+                   encode_saves=False, ri_replica=0):
         """One round, stream-ordered; reads_per_ctx > 0 also serves the
         reads behind the round's ReadyToReads, encode_saves encodes the
         EntriesToSave (drb_round_in)."""
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
-                      key_space, int(bool(encode_saves)))
+                      key_space, int(bool(encode_saves)), ri_replica)
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
 

@@ -203,6 +203,11 @@ typedef struct drb_replica_state {
   uint64_t sm_index;                   /* StateMachine.index (statemachine.go:716) */
   uint64_t sm_term;                    /* StateMachine.term */
   uint64_t kv_count;                   /* KVTest.Count (kvtest.go:146) */
+  /* node.qs, quiesceState (quiesce.go:23-33); all 0 with Quiesce off */
+  uint64_t qs_current_tick;
+  uint64_t qs_idle_since;
+  uint64_t qs_quiesced_since;          /* 0: not quiesced */
+  uint64_t qs_exit_quiesce_tick;
   uint32_t role;                       /* drb_role */
   uint32_t flags;                      /* DRB_F_* */
   uint32_t fallback_reason;            /* drb_fallback_reason */
@@ -265,7 +270,7 @@ typedef struct drb_config {
   uint32_t max_props;        /* max proposals per group per round */
   uint32_t prop_slots;       /* staged proposal batches */
   uint32_t ri_slots;         /* staged ReadIndex batches */
-  uint32_t mailbox;          /* records per (sender, receiver) per round, 4..13 */
+  uint32_t mailbox;          /* records per (sender, receiver) per round, 4..24 */
   uint32_t kv_slots;         /* KV open-addressing slots per replica (pow2) */
   uint32_t kv_val_cap;       /* max value bytes per KV slot (<= 124 inline,
                               * else out of line, <= 1024) */
@@ -293,7 +298,11 @@ typedef struct drb_config {
   uint32_t kv_pool_blocks;
   /* records of the flagged-replica list (drb_take_flagged; 0: 65536) */
   uint32_t flagged_cap;
-  uint32_t reserved0;
+  /* Config.Quiesce (config.go:195): node.qs (quiesce.go) enters quiesce
+   * after 20 x ElectionRTT idle ticks and stops heartbeating; quiesced
+   * replicas without input skip tick rounds (their ticks are applied
+   * when they next run) */
+  uint32_t quiesce;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -309,7 +318,12 @@ typedef struct drb_round_in {
   /* 1: encode every replica's pb.Update.EntriesToSave as EntryBatch bytes
    * + CRC32 for the LogDB writer (drb_export_saved; needs save_cap) */
   uint32_t encode_saves;
-  uint32_t reserved[2];
+  /* where the staged ReadIndex batch lands (node.handleReadIndex,
+   * node.go:1296-1307): 0 the group's leader; k >= 1 replica ID k, which
+   * forwards it to its leader when it is a follower (raft.go:2134-2164).
+   * Co-resident placement only. */
+  uint32_t ri_replica;
+  uint32_t reserved;
 } drb_round_in;
 
 #define DRB_NONE 0xffffffffu
@@ -327,6 +341,9 @@ typedef struct drb_round_out {
   uint64_t reads_deferred;        /* reads whose index is not applied yet */
   uint64_t saved_entries;         /* EntriesToSave encoded (encode_saves) */
   uint64_t saved_bytes;           /* EntryBatch bytes of those */
+  uint64_t replicas_stepped;      /* replicas that ran the round; the others
+                                   * were at rest with no input (or
+                                   * quiesced at rest on a tick round) */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;
@@ -504,11 +521,14 @@ typedef struct drb_region {
   uint64_t bytes;
 } drb_region;
 
-#define DRB_PLANE_REGIONS 6
-#define DRB_PLANE_K(w) ((w) & 0xffu)          /* records per lane (max) */
-#define DRB_PLANE_E(w) (((w) >> 8) & 0xffu)   /* entry rows (max) */
-#define DRB_PLANE_C1 (1u << 16)               /* a record has a 2nd chunk */
-#define DRB_PLANE_REP (1u << 17)              /* a Replicate */
+#define DRB_PLANE_REGIONS 8
+/* per lane (max): Replicate records (positions 0..), other records
+ * (positions mailbox-1 downwards), entry rows; a record's 2nd chunk */
+#define DRB_PLANE_KREP(w) ((w) & 0x1fu)
+#define DRB_PLANE_KOTH(w) (((w) >> 5) & 0x1fu)
+#define DRB_PLANE_E(w) (((w) >> 10) & 0xffu)
+#define DRB_PLANE_C1 (1u << 18)
+#define DRB_PLANE_HDR (1u << 19)  /* a header without records (Quiesce) */
 
 /* words[from * R + to] for this rank's remote planes of the last round
  * (0 for local or empty ones).  Synchronises the engine stream. */

@@ -12,6 +12,8 @@
  *                                getUpdateCommit 432-449
  *   Peer.Commit                  peer.go:292-305
  *   step() loop                  node_test.go:274-353
+ *   quiesceState                 quiesce.go:23-120 (node.go:195-200,
+ *                                993-1005, 1148-1150, 1339-1345, 1385)
  *   StateMachine.Handle/handle   internal/rsm/statemachine.go:599-906
  *   handleEntry/update/noop      statemachine.go:935-1103
  *   setApplied/setLastApplied    statemachine.go:716-760
@@ -120,8 +122,17 @@ static void kv_free(orc_kv *kv) {
 /* ------------------------------------------------------------------ */
 /* node                                                                 */
 /* ------------------------------------------------------------------ */
+/* quiesceState (quiesce.go:23-33) */
+typedef struct orc_qs {
+  uint64_t current_tick, election_tick, quiesced_since, idle_since,
+      exit_quiesce_tick;
+  int enabled, new_flag;
+} orc_qs;
+
 typedef struct orc_node {
   orc_raft *r;
+  orc_qs qs;
+  uint32_t quiesce_to; /* Quiesce messages of this round, bit per slot */
   orc_logdb *db;
   orc_kv kv;
   uint64_t sm_index, sm_term; /* StateMachine.index/term */
@@ -298,11 +309,77 @@ static void sm_handle(orc_node *n, int is_leader, drb_round_out *out) {
   ev_truncate(&n->applyq, 0);
 }
 
+/* ---- quiesceState (quiesce.go) ------------------------------------- */
+static int qs_quiesced(const orc_qs *q) {
+  return q->enabled && q->quiesced_since > 0;
+}
+static uint64_t qs_threshold(const orc_qs *q) { return q->election_tick * 10; }
+/* enterQuiesce (quiesce.go:104-109) */
+static void qs_enter(orc_qs *q) {
+  q->quiesced_since = q->current_tick;
+  q->idle_since = q->current_tick;
+  q->new_flag = 1;
+}
+/* exitQuiesce (quiesce.go:111-114) */
+static void qs_exit(orc_qs *q) {
+  q->quiesced_since = 0;
+  q->exit_quiesce_tick = q->current_tick;
+}
+/* tick (quiesce.go:40-51) */
+static void qs_tick(orc_qs *q) {
+  if (!q->enabled) return;
+  uint64_t threshold = qs_threshold(q);
+  q->current_tick++;
+  if (!qs_quiesced(q) && q->current_tick - q->idle_since > threshold)
+    qs_enter(q);
+}
+/* newToQuiesce (quiesce.go:80-85) */
+static int qs_new_to_quiesce(const orc_qs *q) {
+  if (!qs_quiesced(q)) return 0;
+  return q->current_tick - q->quiesced_since < q->election_tick;
+}
+/* justExitedQuiesce (quiesce.go:87-92) */
+static int qs_just_exited(const orc_qs *q) {
+  if (qs_quiesced(q)) return 0;
+  return q->current_tick - q->exit_quiesce_tick < qs_threshold(q);
+}
+/* record (quiesce.go:56-74) */
+static void qs_record(orc_qs *q, uint32_t type) {
+  if (!q->enabled) return;
+  if (type == DRB_MSG_HEARTBEAT || type == DRB_MSG_HEARTBEAT_RESP) {
+    if (!qs_quiesced(q)) return;
+    if (qs_new_to_quiesce(q)) return;
+  }
+  q->idle_since = q->current_tick;
+  if (qs_quiesced(q)) qs_exit(q);
+}
+/* tryEnterQuiesce (quiesce.go:94-102) */
+static void qs_try_enter(orc_qs *q) {
+  if (qs_just_exited(q)) return;
+  if (!qs_quiesced(q)) qs_enter(q);
+}
+/* newQuiesceState (quiesce.go:39-41) */
+static int qs_take_new(orc_qs *q) {
+  int f = q->new_flag;
+  q->new_flag = 0;
+  return f;
+}
+
 /* ---- node-level event handling -------------------------------------- */
 static void node_tick(orc_node *n) {
-  /* node.tick (node.go:1562-1579): quiesce disabled -> Peer.Tick */
+  /* node.tick (node.go:1562-1579) */
   n->current_tick++;
-  raft_tick_public(n->r, 0);
+  qs_tick(&n->qs);
+  raft_tick_public(n->r, qs_quiesced(&n->qs));
+}
+
+/* node.recordMessage (node.go:1339-1345) */
+static void node_record_message(orc_node *n, const orc_msg *m) {
+  if ((m->type == DRB_MSG_HEARTBEAT || m->type == DRB_MSG_HEARTBEAT_RESP) &&
+      m->hint > 0)
+    qs_record(&n->qs, DRB_MSG_READ_INDEX);
+  else
+    qs_record(&n->qs, m->type);
 }
 
 /* stable order: all Replicate messages by sender slot, then every other
@@ -340,6 +417,7 @@ static int node_handle_events(orc_node *n, int tick) {
   if (log_has_entries_to_apply(&r->log)) has_event = 1;
   /* handleReadIndex (node.go:1296-1307) -> Peer.ReadIndex (peer.go:309) */
   if (n->has_ri) {
+    qs_record(&n->qs, DRB_MSG_READ_INDEX);
     orc_msg m;
     memset(&m, 0, sizeof(m));
     m.type = DRB_MSG_READ_INDEX;
@@ -360,10 +438,16 @@ static int node_handle_events(orc_node *n, int tick) {
   size_t cnt = n->inbox.n;
   for (size_t i = 0; i < cnt; i++) {
     orc_msg *m = &n->inbox.v[i];
-    if (m->type == DRB_MSG_LOCAL_TICK)
+    /* node.handleMessage (node.go:1379-1401), else recordMessage +
+     * Peer.Handle */
+    if (m->type == DRB_MSG_LOCAL_TICK) {
       node_tick(n);
-    else
+    } else if (m->type == DRB_MSG_QUIESCE) {
+      qs_try_enter(&n->qs);
+    } else {
+      node_record_message(n, m);
       peer_handle(r, m);
+    }
   }
   if (cnt > 0) has_event = 1;
   mv_clear(&n->inbox);
@@ -503,11 +587,33 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
     mv_clear(&n->out);
     n->nrtr = 0;
     n->saved.n = 0;
+    n->quiesce_to = 0;
     if (!n->hosted) {
       mv_clear(&n->inbox);
       continue;
     }
-    if (node_handle_events(n, tick)) have[s] = node_get_update(n, &uds[s]);
+    if (node_handle_events(n, tick)) {
+      /* stepNode: newQuiesceState -> sendEnterQuiesceMessages
+       * (node.go:1148-1150, 993-1005), ahead of the Update's messages */
+      if (qs_take_new(&n->qs))
+        n->quiesce_to = ((1u << R) - 1u) & ~(1u << s);
+      have[s] = node_get_update(n, &uds[s]);
+    }
+  }
+  for (uint32_t s = 0; s < R; s++) {
+    orc_node *n = node_at(c, g, s);
+    for (uint32_t t = 0; t < R; t++) {
+      if (!((n->quiesce_to >> t) & 1u)) continue;
+      orc_msg q;
+      memset(&q, 0, sizeof(q));
+      q.type = DRB_MSG_QUIESCE;
+      q.from = s + 1;
+      q.to = t + 1;
+      q.shard_id = n->r->shard_id;
+      deliver(c, g, s, &q);
+      mv_push(&n->out, &q); /* this round's outbox, first */
+      if (out) out->messages++;
+    }
   }
   /* applyRaftUpdates / sendReplicateMessages / processReadyToRead */
   for (uint32_t s = 0; s < R; s++) {
@@ -556,9 +662,14 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
       if (keep_from > lim) keep_from = lim;
       if (keep_from > n->db->marker_index) orc_logdb_compact(n->db, keep_from);
     }
-    /* the outbox of this round (ud.Messages) */
-    n->out = ud->msgs;
-    memset(&ud->msgs, 0, sizeof(ud->msgs));
+    /* the outbox of this round in send order: the Quiesce messages, the
+     * Replicates (sendReplicateMessages, node.go:1016-1023), then the
+     * rest (processRaftUpdate -> sendMessages, node.go:1104-1108) */
+    for (int pass = 0; pass < 2; pass++)
+      for (size_t i = 0; i < ud->msgs.n; i++)
+        if ((ud->msgs.v[i].type == DRB_MSG_REPLICATE) == (pass == 0))
+          mv_push(&n->out, &ud->msgs.v[i]);
+    ud->msgs.n = 0;
     update_free(ud);
   }
 }
@@ -595,6 +706,9 @@ orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg) {
                       cfg->heartbeat_rtt, (int)cfg->check_quorum, n->db,
                       mix64(cfg->seed ^ (g * R + s)));
       n->hosted = 1;
+      /* quiesceState{electionTick: ElectionRTT * 2} (node.go:195-200) */
+      n->qs.election_tick = 2ull * cfg->election_rtt;
+      n->qs.enabled = cfg->quiesce != 0;
     }
   orc_jb = prev;
   return c;
@@ -699,12 +813,21 @@ int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
 
 int orc_cluster_stage_read_index(orc_cluster *c, const uint64_t *low,
                                  const uint64_t *high) {
+  return orc_cluster_stage_read_index_at(c, low, high, 0);
+}
+
+/* node.read / handleReadIndex (node.go:1296-1307) at replica ID `replica`
+ * (0: the group's leader) */
+int orc_cluster_stage_read_index_at(orc_cluster *c, const uint64_t *low,
+                                    const uint64_t *high, uint32_t replica) {
   uint32_t R = c->cfg.num_replicas;
   for (uint64_t g = 0; g < c->cfg.num_groups; g++) {
     if (!low[g]) continue;
     for (uint32_t s = 0; s < R; s++) {
       orc_node *n = node_at(c, g, s);
-      if (n->hosted && n->r->state == DRB_LEADER) {
+      const int here = replica ? s + 1 == replica
+                               : n->r->state == DRB_LEADER;
+      if (n->hosted && here) {
         n->has_ri = 1;
         n->ri.low = low[g];
         n->ri.high = high[g];
@@ -766,6 +889,10 @@ int orc_cluster_export(orc_cluster *c, uint64_t g, uint32_t slot,
   st->sm_index = n->sm_index;
   st->sm_term = n->sm_term;
   st->kv_count = n->kv.count;
+  st->qs_current_tick = n->qs.current_tick;
+  st->qs_idle_since = n->qs.idle_since;
+  st->qs_quiesced_since = n->qs.quiesced_since;
+  st->qs_exit_quiesce_tick = n->qs.exit_quiesce_tick;
   st->flags = n->hosted ? DRB_F_HOSTED : 0;
   return 0;
 }

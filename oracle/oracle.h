@@ -259,6 +259,8 @@ typedef struct orc_cluster_cfg {
   uint32_t election_rtt, heartbeat_rtt, check_quorum;
   uint64_t seed;
   uint64_t logdb_keep; /* 0: keep every saved entry; else compact behind */
+  uint32_t quiesce;    /* Config.Quiesce (config.go:195) */
+  uint32_t pad;
 } orc_cluster_cfg;
 
 orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg);
@@ -272,6 +274,8 @@ int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
 /* stage one ReadIndex ctx per group (low==0: none) for next round */
 int orc_cluster_stage_read_index(orc_cluster *c, const uint64_t *low,
                                  const uint64_t *high);
+int orc_cluster_stage_read_index_at(orc_cluster *c, const uint64_t *low,
+                                    const uint64_t *high, uint32_t replica);
 int orc_cluster_ingest(orc_cluster *c, const drb_message *m, size_t n,
                        const drb_entry *ents, const uint8_t *pool);
 /* one step round; groups [g0, g1) only (for threaded timing) */

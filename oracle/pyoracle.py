@@ -41,7 +41,8 @@ class ClusterCfg(C.Structure):
     _fields_ = [("num_groups", C.c_uint64), ("first_shard_id", C.c_uint64),
                 ("num_replicas", C.c_uint32), ("election_rtt", C.c_uint32),
                 ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
-                ("seed", C.c_uint64), ("logdb_keep", C.c_uint64)]
+                ("seed", C.c_uint64), ("logdb_keep", C.c_uint64),
+                ("quiesce", C.c_uint32), ("pad", C.c_uint32)]
 
 
 P = C.c_void_p
@@ -122,6 +123,7 @@ def _declare(L):
         "orc_cluster_setup_steady": (C.c_int, [P, U32]),
         "orc_cluster_stage_proposals": (C.c_int, [P, PU32, U32, PE, PU8]),
         "orc_cluster_stage_read_index": (C.c_int, [P, PU64, PU64]),
+        "orc_cluster_stage_read_index_at": (C.c_int, [P, PU64, PU64, U32]),
         "orc_cluster_ingest": (C.c_int, [P, PM, C.c_size_t, PE, PU8]),
         "orc_cluster_round": (C.c_int, [P, C.c_int, C.POINTER(RoundOut)]),
         "orc_cluster_round_range": (C.c_int, [P, C.c_int, U64, U64,
@@ -544,10 +546,10 @@ class Cluster:
 
     def __init__(self, num_groups, num_replicas=3, election_rtt=10,
                  heartbeat_rtt=1, check_quorum=1, seed=0x5EEDD8B0,
-                 first_shard_id=1, logdb_keep=0):
+                 first_shard_id=1, logdb_keep=0, quiesce=0):
         cfg = ClusterCfg(num_groups, first_shard_id, num_replicas,
                          election_rtt, heartbeat_rtt, check_quorum, seed,
-                         logdb_keep)
+                         logdb_keep, int(bool(quiesce)), 0)
         self.cfg = cfg
         self.G = num_groups
         self.R = num_replicas
@@ -567,8 +569,11 @@ class Cluster:
         _check(lib().orc_cluster_stage_proposals(self.p, counts,
                                                  max_per_group, ents, pool))
 
-    def stage_read_index(self, low, high):
-        _check(lib().orc_cluster_stage_read_index(self.p, low, high))
+    def stage_read_index(self, low, high, replica=0):
+        """One ReadIndex ctx per group at its leader, or at replica ID
+        `replica` (which forwards it when it is a follower)."""
+        _check(lib().orc_cluster_stage_read_index_at(self.p, low, high,
+                                                     replica))
 
     def ingest(self, msgs):
         marr, n, earr, pool = build_messages(msgs)

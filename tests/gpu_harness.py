@@ -19,7 +19,8 @@ STATE_FIELDS = [
     "committed", "processed", "last_index", "marker_index", "saved_to",
     "applied_to_index", "applied_to_term", "applied_index",
     "confirmed_index", "pushed_index", "prev_term", "prev_vote",
-    "prev_commit", "sm_index", "sm_term", "kv_count", "role"]
+    "prev_commit", "sm_index", "sm_term", "kv_count", "qs_current_tick",
+    "qs_idle_since", "qs_quiesced_since", "qs_exit_quiesce_tick", "role"]
 
 
 def state_diff(a, b, R):
@@ -57,18 +58,21 @@ class Pair:
     """An engine and an oracle cluster stepped in lock-step."""
 
     def __init__(self, G, R=3, seed=0x5EEDD8B0, window=32, leader_slot=0,
-                 **engine_kw):
+                 election_rtt=10, quiesce=False, **engine_kw):
         self.G, self.R, self.seed = G, R, seed
         self.eng = Engine(num_groups=G, num_replicas=R, window=window,
+                          election_rtt=election_rtt, quiesce=int(quiesce),
                           **engine_kw)
-        self.orc = po.Cluster(G, R, seed=seed)
+        self.orc = po.Cluster(G, R, seed=seed, election_rtt=election_rtt,
+                              quiesce=quiesce)
         self.orc.setup_steady(leader_slot)
         self.eng.init_steady(term=2, leader_slot=leader_slot, seed=seed)
         self.rounds = 0
         self.cpu = set()  # groups handed to the CPU path (the oracle)
 
     def stage(self, k=1, salt=None, read_index=False, groups=None,
-              key_space=256, val_len=4, prop_slot=0, ri_slot=0):
+              key_space=256, val_len=4, prop_slot=0, ri_slot=0,
+              ri_replica=0):
         salt = self.rounds if salt is None else salt
         pin = ri_in = abi.DRB_NONE
         if self.cpu:  # no client input for groups on the CPU path
@@ -89,20 +93,34 @@ class Pair:
         if read_index:
             lo, hi = workload.build_read_index(self.G, self.seed, salt,
                                                salt + 30, groups)
-            self.orc.stage_read_index(lo, hi)
+            self.orc.stage_read_index(lo, hi, ri_replica)
             self.eng.stage_read_index(ri_slot, lo, hi)
             ri_in = ri_slot
         return pin, ri_in
 
     def round(self, k=1, tick=False, read_index=False, groups=None,
-              reads=0, read_key_space=256, encode_saves=False, **kw):
-        pin, ri_in = self.stage(k, read_index=read_index, groups=groups, **kw)
+              reads=0, read_key_space=256, encode_saves=False, ri_replica=0,
+              **kw):
+        pin, ri_in = self.stage(k, read_index=read_index, groups=groups,
+                                ri_replica=ri_replica, **kw)
         o = self.orc.round(tick=tick)
         e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in,
                           reads_per_ctx=reads, key_space=read_key_space,
-                          encode_saves=encode_saves)
+                          encode_saves=encode_saves, ri_replica=ri_replica)
         self.rounds += 1
         return o, e
+
+    def why(self, n=3):
+        """The replicas flagged since the last call, by reason, with the
+        first few states (for assertion messages)."""
+        recs, lost = self.eng.take_flagged()
+        out = {}
+        for (g, s, reason, flags, rnd, _) in recs:
+            out.setdefault(abi.FB_NAME.get(reason, reason), []).append(
+                (g, s, flags, rnd))
+        first = [(g, s, self.eng.export_replicas(g, 1)[s].to_dict(self.R))
+                 for (g, s, *_r) in recs[:n]]
+        return out, lost, first
 
     def check_saves(self, groups=None):
         """EntriesToSave of the last round: EntryBatch bytes and CRC32."""

@@ -2,8 +2,8 @@
 2 and 3 gloo ranks move mailbox planes exactly as the RCCL run does.
 
 Each rank holds fake outbox/inbox planes in host memory, sized per plane by
-a summary word the way drb_plane_regions sizes the engine's (records K,
-entry rows E, c1 / Replicate flags).  The routing is the engine's own
+a summary word the way drb_plane_regions sizes the engine's (Replicate
+records, other records, entry rows, c1 / header-only flags).  The routing is the engine's own
 (drb_place_peer from the C ABI library, no device needed); the send/recv
 lists come from exchange.plan and run as one gloo batch_isend_irecv.
 After the step, inbox plane (a, b) of every rank must hold the bytes rank
@@ -30,12 +30,35 @@ def _free_port():
     return p
 
 
+C1, HDR = 1 << 18, 1 << 19
+
+
 def _word(rank, a, b):
     rng = np.random.default_rng(rank * 1000 + a * 10 + b)
-    K = int(rng.integers(0, 4))
+    kr, ko = int(rng.integers(0, 4)), int(rng.integers(0, 4))
     E = int(rng.integers(0, 3)) if a == 0 else 0
-    fl = (1 << 16 if rng.integers(0, 2) else 0) | (1 << 17 if E else 0)
-    return K | (E << 8) | fl if (K or E) else 0
+    fl = (C1 if rng.integers(0, 2) else 0) | \
+        (HDR if rng.integers(0, 4) == 0 else 0)
+    return kr | (ko << 5) | (E << 10) | fl if (kr or ko or E or fl & HDR) \
+        else 0
+
+
+def _layout(word):
+    """(buffer slot, bytes) of the regions drb_plane_regions lists."""
+    kr, ko, E = word & 0x1f, (word >> 5) & 0x1f, (word >> 10) & 0xff
+    s = []
+    for c in ((0, 1) if word & C1 else (0,)):
+        if kr:
+            s.append((2 * c, kr * LANES * 16))
+        if ko:
+            s.append((2 * c + 1, ko * LANES * 16))
+    if kr or ko or word & HDR:
+        s.append((4, LANES * 16))
+    if kr:
+        s.append((5, LANES * 8))
+    if E:
+        s += [(6, LANES * 8), (7, E * 5 * LANES * 16)]
+    return s
 
 
 class FakePlanes:
@@ -46,40 +69,18 @@ class FakePlanes:
         for a in range(R):
             for b in range(R):
                 rng = np.random.default_rng(7 + rank * 100 + a * 10 + b)
-                self.out[(a, b)] = [rng.integers(0, 256, n, dtype=np.uint8)
-                                    for n in self._sizes(13 | (3 << 8) |
-                                                         (3 << 16))]
+                self.out[(a, b)] = [
+                    rng.integers(0, 256, n, dtype=np.uint8)
+                    for n in self._sizes(13 | (13 << 5) | (3 << 10) | C1)]
                 self.inb[(a, b)] = [np.zeros_like(x) for x in self.out[(a, b)]]
 
     @staticmethod
     def _sizes(word):
-        K, E = word & 0xff, (word >> 8) & 0xff
-        s = []
-        if K:
-            s.append(K * LANES * 16)
-            if word & (1 << 16):
-                s.append(K * LANES * 16)
-            s.append(LANES * 16)
-            if word & (1 << 17):
-                s.append(LANES * 8)
-        if E:
-            s += [LANES * 8, E * 5 * LANES * 16]
-        return s
+        return [n for _, n in _layout(word)]
 
     def _pick(self, word, bufs):
         # the full-capacity buffers in region order; take the first n bytes
-        K, E = word & 0xff, (word >> 8) & 0xff
-        order = []
-        if K:
-            order.append(0)
-            if word & (1 << 16):
-                order.append(1)
-            order.append(2)
-            if word & (1 << 17):
-                order.append(3)
-        if E:
-            order += [4, 5]
-        return [bufs[i] for i in order]
+        return [bufs[i] for i, _ in _layout(word)]
 
     def regions(self, a, b, word, direction):
         bufs = self._pick(word, (self.out if direction == 0 else

@@ -230,7 +230,7 @@ def _long_payload_rounds(p, val_len, rounds=8, encode=False, device_gen=False):
         else:
             o, e = p.round(k=k, tick=(r % 2 == 0), read_index=(r % 3 == 0),
                            val_len=val_len, encode_saves=encode)
-        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        assert e.fallbacks == 0 and e.errors == 0, (r, p.why())
         assert (e.committed_entries, e.applied_entries, e.messages) == \
             (o.committed_entries, o.applied_entries, o.messages), r
         errs = p.check()
@@ -288,9 +288,40 @@ def test_c5_sparse_activity_idle_rounds(val_len, cmd_cap, val_cap):
         o = p.orc.round(tick=tick)
         e = p.eng.step(tick=tick, prop_slot=r % 2, encode_saves=True)
         p.rounds += 1
-        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        assert e.fallbacks == 0 and e.errors == 0, (r, p.why())
         assert (e.committed_entries, e.applied_entries, e.messages) == \
             (o.committed_entries, o.applied_entries, o.messages), r
         errs = p.check()
         assert not errs, (r, errs[:2])
         assert not p.check_saves(), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,at", [(3, 2), (3, 3), (5, 4)])
+def test_follower_read_index(R, at):
+    """ReadIndex issued at a follower (SURVEY 8d C3 follower variant):
+    handleFollowerReadIndex forwards the ctx to the leader
+    (raft.go:2134-2144), the leader's handleLeaderReadIndex queues it with
+    the follower as requester and confirms it by heartbeat quorum
+    (raft.go:1842-1876, 1955-1974), the ReadIndexResp comes back
+    (raft.go:2155-2164) and the follower serves the reads in-round."""
+    p = Pair(G=48, R=R)
+    total = 0
+    for r in range(14):
+        o, e = p.round(k=1, tick=(r % 2 == 0), read_index=True,
+                       ri_replica=at, reads=9)
+        assert e.fallbacks == 0 and e.errors == 0, (r, p.why())
+        assert (e.committed_entries, e.messages, e.ready_to_reads,
+                e.dropped_read_indexes) == \
+            (o.committed_entries, o.messages, o.ready_to_reads,
+             o.dropped_read_indexes), (r, e.to_dict(), o.to_dict())
+        sums, served, deferred = p.orc.serve_reads(9, 256)
+        assert (e.reads_served, e.reads_deferred) == (served, deferred), r
+        esums = p.eng.export_read_sums(0, p.G)
+        for i, x in enumerate(sums):
+            if x is not None:
+                assert esums[i] == x, (r, i)
+        total += e.ready_to_reads
+        errs = p.check()
+        assert not errs, (r, errs[:2])
+    assert total >= p.G * 8

@@ -155,3 +155,55 @@ def test_oracle_saved_entrybatch_decodes_to_the_round_entries():
                 assert po.entrybatch_marshal(es) == b
                 seen += 1
     assert seen >= 6 * 3 * 3
+
+
+# ---- Quiesce at the node level (node_test.go:858-1000) -----------------
+def _quiesced(c):
+    return [c.export(g, s).qs_quiesced_since > 0
+            for g in range(c.G) for s in range(c.R)]
+
+
+def _idle(c, n):
+    for _ in range(n):
+        c.round(tick=True)
+
+
+def test_quiesce_can_be_disabled():
+    """TestRaftNodeQuiesceCanBeDisabled (node_test.go:858-882)."""
+    c = po.Cluster(2, 3, quiesce=False)
+    c.setup_steady(0)
+    _idle(c, 2 * 200 + 1)
+    assert not any(_quiesced(c))
+
+
+def test_nodes_can_enter_quiesce():
+    """TestNodesCanEnterQuiesce (node_test.go:884-905): threshold() =
+    20 x ElectionRTT idle ticks, then every replica stays quiesced."""
+    c = po.Cluster(2, 3, quiesce=True)
+    c.setup_steady(0)
+    _idle(c, 2 * 200 + 1)
+    assert all(_quiesced(c))
+    _idle(c, 3 * 200 + 1)
+    assert all(_quiesced(c))
+    # quiesced ticks: no heartbeats, no LocalTick-driven messages
+    o = c.round(tick=True)
+    assert o.messages == 0
+
+
+def test_nodes_exit_quiesce_by_proposal_and_read_index():
+    """TestNodesCanExitQuiesceByMakingProposal / ...ByReadIndex
+    (node_test.go:907-972)."""
+    for how in ("propose", "read"):
+        c = po.Cluster(2, 3, quiesce=True)
+        c.setup_steady(0)
+        _idle(c, 2 * 200 + 1)
+        assert all(_quiesced(c))
+        if how == "propose":
+            counts, ents, pool = workload.build_batch(2, 1, 7, 1)
+            c.stage_proposals(counts, 1, ents, pool)
+        else:
+            lo, hi = workload.build_read_index(2, 7, 1, 31)
+            c.stage_read_index(lo, hi)
+        for _ in range(4):
+            c.round(tick=True)
+        assert not any(_quiesced(c)), how
