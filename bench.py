@@ -95,6 +95,9 @@ def parse():
                     choices=["leader", "follower"],
                     help="C3: issue the ReadIndex batch at the leader or at "
                          "a follower (forwarded, raft.go:2134-2164)")
+    ap.add_argument("--listed", type=int, default=-1,
+                    help="step only the replicas with work, packed "
+                         "(drb_round_in.listed; default: on for c5)")
     ap.add_argument("--quiesce", type=int, default=-1,
                     help="Config.Quiesce (default: on for c5, SURVEY 8d)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -188,6 +191,8 @@ def main():
         args.replicas = 5 if c4 else 3
     if args.quiesce < 0:
         args.quiesce = 1 if c5 else 0
+    if args.listed < 0:
+        args.listed = 1 if c5 else 0
     if c5:
         args.no_read_index = True  # writes, no reads
         if args.groups == 1 << 20:
@@ -257,7 +262,8 @@ def main():
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF,
                        reads_per_ctx=READS_PER_CTX if fused else 0,
                        key_space=KEY_SPACE, encode_saves=c5,
-                       ri_replica=2 if args.reads_at == "follower" else 0)
+                       ri_replica=2 if args.reads_at == "follower" else 0,
+                       listed=bool(args.listed))
         if reads and not fused:
             eng.serve_reads(READS_PER_CTX, KEY_SPACE)
         if xch is not None:  # C4: this round's cross-GPU planes
@@ -361,9 +367,10 @@ def main():
                   "(values out of line), %d ppm of the groups proposing per "
                   "round (independent seeded draw each round, generated "
                   "inside the timed loop), EntriesToSave encoded (EntryBatch + CRC32), tick "
-                  "every %d round(s); Quiesce %s" % (
+                  "every %d round(s); Quiesce %s%s" % (
                       G, R, args.payload, args.active_ppm, args.tick_every,
-                      "on" if args.quiesce else "off"))
+                      "on" if args.quiesce else "off",
+                      ", listed rounds" if args.listed else ""))
             par = "groups sharded, replicas co-resident"
         elif c4:
             metric = ("committed entries/sec (node) at %d 5-replica groups "

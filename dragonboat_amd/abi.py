@@ -182,7 +182,7 @@ class RoundIn(C.Structure):
                 ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),
                 ("read_key_space", C.c_uint32),
                 ("encode_saves", C.c_uint32), ("ri_replica", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("listed", C.c_uint32)]
 
 
 class RoundOut(C.Structure):

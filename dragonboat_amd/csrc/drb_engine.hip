@@ -302,6 +302,14 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   v.flog_cap = cfg->flagged_cap ? cfg->flagged_cap : 65536;
   rc |= dalloc(e, &v.flog, v.flog_cap);
   rc |= dalloc(e, &v.flog_n, 1);
+  {
+    const uint64_t nb = (G + 255) / 256;
+    rc |= dalloc(e, &v.act_list, 2 * R * G);
+    rc |= dalloc(e, &v.act_total, 2 * R);
+    rc |= dalloc(e, &v.act_cnt, 2 * R * nb);
+    rc |= dalloc(e, &v.act_off, 2 * R * nb);
+    rc |= dalloc(e, &v.act_mask, 2 * R * nb * 4);
+  }
   rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
   if (!rc) {  // no Replicate in flight: ring_guard = +inf
@@ -1138,9 +1146,105 @@ static uint32_t slot_list(uint32_t mask, uint32_t *n) {
   return l;
 }
 
+// ---------------------------------------------------------------- active list
+// A listed round (drb_round_in.listed) first lists, per (role, slot), the
+// lanes whose replica has work this round -- everything the step kernel's
+// idle rule (drb_step.hpp idle_round) would not skip -- in group order:
+// k_active_scan ballots the rule per wave, k_active_prefix turns the
+// per-block counts into offsets, k_active_scatter writes the lanes.  The
+// step kernels then take 256 listed lanes per block, so a round where most
+// replicas are at rest (C5 with Quiesce) runs dense waves; group order
+// keeps neighbouring lanes' SoA accesses in the same lines.
+template <int R>
+__global__ __launch_bounds__(256) void k_active_scan(const View v,
+                                                     RoundParams p) {
+  const uint32_t s = blockIdx.y;
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nb = gridDim.x;
+  bool lead = false, run = false;
+  if (g < v.G) {
+    const uint32_t flags = v.u32[u32_ix(v, W_FLAGS, s, g)];
+    lead = v.u32[u32_ix(v, W_ROLE, s, g)] == DRB_LEADER;
+    if (flags & DRB_F_HOSTED) {
+      if (flags & (DRB_F_FALLBACK | DRB_F_ERROR)) {
+        v.rtr_count[ix(v, s, g)] = 0;  // no round output (step kernel)
+        if (p.encode_saves) v.save_len[ix(v, s, g)] = 0;
+      } else {
+        run = !idle_round<R>(v, p, s, g, lead, flags);
+      }
+    }
+  }
+  const uint64_t bl = __ballot(run && lead), bf = __ballot(run && !lead);
+  __shared__ uint32_t c[2][4];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    v.act_mask[(((uint64_t)0 * v.R + s) * nb + blockIdx.x) * 4 + wave] = bl;
+    v.act_mask[(((uint64_t)1 * v.R + s) * nb + blockIdx.x) * 4 + wave] = bf;
+    c[0][wave] = (uint32_t)__popcll(bl);
+    c[1][wave] = (uint32_t)__popcll(bf);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const uint32_t t = threadIdx.x;
+    v.act_cnt[((uint64_t)t * v.R + s) * nb + blockIdx.x] =
+        c[t][0] + c[t][1] + c[t][2] + c[t][3];
+  }
+}
+
+// exclusive scan of one row's block counts (one workgroup per row)
+__global__ __launch_bounds__(1024) void k_active_prefix(const View v,
+                                                        uint64_t nb) {
+  const uint64_t row = blockIdx.x;
+  const uint32_t *cnt = v.act_cnt + row * nb;
+  uint32_t *off = v.act_off + row * nb;
+  const uint64_t chunk = (nb + 1023) / 1024;
+  const uint64_t lo = threadIdx.x * chunk;
+  const uint64_t hi = lo + chunk < nb ? lo + chunk : nb;
+  uint32_t sum = 0;
+  for (uint64_t i = lo; i < hi; ++i) sum += cnt[i];
+  __shared__ uint32_t part[1024];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
+    const uint32_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - sum;
+  for (uint64_t i = lo; i < hi; ++i) {
+    off[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 1023) v.act_total[row] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_active_scatter(const View v) {
+  const uint32_t s = blockIdx.y;
+  const uint64_t nb = gridDim.x;
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t t = 0; t < 2; ++t) {
+    const uint64_t row = (uint64_t)t * v.R + s;
+    const uint64_t *m = v.act_mask + (row * nb + blockIdx.x) * 4;
+    const uint64_t mw = m[wave];
+    if (!((mw >> lane) & 1ull)) continue;
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += (uint32_t)__popcll(m[w]);
+    const uint64_t pos = v.act_off[row * nb + blockIdx.x] + before +
+                         (uint32_t)__popcll(mw & ((1ull << lane) - 1ull));
+    v.act_list[row * v.G + pos] = (uint32_t)g;
+  }
+}
+
 template <int R>
 static void launch_step(drb_engine *e, const RoundParams &p0) {
   const unsigned gx = (unsigned)((e->v.G + 255) / 256);
+  if (p0.listed) {
+    k_active_scan<R><<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v, p0);
+    k_active_prefix<<<2 * e->v.R, 1024, 0, e->stream>>>(e->v, gx);
+    k_active_scatter<<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v);
+  }
   RoundParams pl = p0, pf = p0;
   uint32_t nl = 0, nf = 0;
   pl.slots = slot_list(e->role_slots[0], &nl);
@@ -1235,7 +1339,8 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.encode_saves = in->encode_saves ? 1 : 0;
   if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
   p.ri_replica = in->ri_replica;
-  p.pad = 0;
+  p.listed = in->listed ? 1 : 0;
+  if (p.listed && e->v.remote_mask) return DRB_EINVAL;
   if (p.ri_replica > e->v.R || (p.ri_replica && e->v.place_world > 1))
     return DRB_EINVAL;
   if (e->v.remote_mask)  // plane summaries of this round only

@@ -322,6 +322,12 @@ struct View {
   uint4 *flog;
   unsigned long long *flog_n;
   uint64_t flog_cap;
+  // listed rounds (drb_round_in.listed): per (role, slot) row the lanes
+  // with work this round in group order, and their count
+  uint32_t *act_list;               // [2][R][G]
+  unsigned long long *act_total;    // [2][R]
+  uint32_t *act_cnt, *act_off;      // [2][R][blocks]
+  uint64_t *act_mask;               // [2][R][blocks][4] (one word a wave)
 };
 
 __host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,

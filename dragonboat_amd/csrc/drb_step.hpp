@@ -1462,21 +1462,53 @@ struct RoundParams {
   uint32_t nrows;  // block rows (slots) of this launch; see block_pos
   uint64_t tick_no;  // engine ticks so far, this round's included
   uint32_t ri_replica;  // staged ReadIndex at: 0 the leader, else ID
-  uint32_t pad;
+  uint32_t listed;      // 1: step the active list (k_active_*), see below
 };
 
 // Whether this replica takes the lane's staged proposals / ReadIndex
 // (co-resident: the leader, or replica ri_replica for reads; replicas
 // spread over ranks: the stage slot's).
-template <bool LEAD>
-DRB_DEV bool stage_here(const View &v, uint32_t slot) {
-  return LEAD && (v.place_world <= 1 || slot == v.stage_slot);
+DRB_DEV bool stage_here(const View &v, uint32_t slot, bool lead) {
+  return lead && (v.place_world <= 1 || slot == v.stage_slot);
 }
-template <bool LEAD>
-DRB_DEV bool ri_here(const View &v, const RoundParams &p, uint32_t slot) {
+DRB_DEV bool ri_here(const View &v, const RoundParams &p, uint32_t slot,
+                     bool lead) {
   if (p.ri_slot == DRB_NONE) return false;
-  return p.ri_replica == 0 ? stage_here<LEAD>(v, slot)
+  return p.ri_replica == 0 ? stage_here(v, slot, lead)
                            : slot + 1 == p.ri_replica;
+}
+
+// Idle rounds: a replica at rest -- its last round left
+// nothing pending, see the end of the round -- whose round brings no
+// input changes nothing (node.stepNode finds no event, node.go:1139-1159):
+// no tick, no staged proposal or ReadIndex, and no record from a
+// co-resident sender, which the senders' one-byte round tags tell
+// without reading the mailbox headers.  Its round outputs are already
+// empty (a round that produced any does not leave the replica at rest).
+// With Quiesce on, a quiesced replica at rest also skips tick rounds
+// without input: a quiesced tick only advances its tick counters
+// (node.tick node.go:1562-1579, raft.quiescedTick raft.go:650-656),
+// which the next round it runs applies at once (F_QS_BASE).
+template <int R>
+DRB_DEV bool idle_round(const View &v, const RoundParams &p, uint32_t slot,
+                        uint64_t g, bool lead, uint32_t flags) {
+  if (!(flags & F_AT_REST) || v.remote_mask) return false;
+  if (p.tick && !(v.quiesce && (flags & F_QUIESCED))) return false;
+  const uint32_t rbuf = (uint32_t)((p.round - 1) & 1);
+  const uint64_t tags = v.inbox_tag[((uint64_t)rbuf * v.R + slot) * v.G + g];
+  const uint32_t want = (uint32_t)(p.round - 1) & 0xffu;
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if ((uint32_t)s != slot && ((tags >> (8 * s)) & 0xffu) == want)
+      return false;
+  if (stage_here(v, slot, lead) && p.prop_slot != DRB_NONE &&
+      v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
+    return false;
+  if (ri_here(v, p, slot, lead) &&
+      (v.ri_in[(uint64_t)p.ri_slot * v.G + g].x |
+       v.ri_in[(uint64_t)p.ri_slot * v.G + g].y))
+    return false;
+  return true;
 }
 
 // The logical (x = group block, y = slot row) of this workgroup.  The
@@ -1595,10 +1627,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   // global memory (global_load/store, not flat: no LDS-counter waits)
   const View *vp = &v;
   const BlockPos bp = block_pos(p);
-  const uint64_t g = (uint64_t)bp.x * blockDim.x + threadIdx.x;
   // the slots this launch steps (4 bits each): a role's launch covers only
   // the slots where that role occurs (drb_engine.hip role map)
   const uint32_t slot = (p.slots >> (4 * bp.y)) & 0xfu;
+  // Listed rounds step only the replicas k_active_scan found with work,
+  // packed in group order into dense waves (drb_engine.hip); the blocks
+  // past the list's end have nothing to do.
+  const uint64_t lrow = ((uint64_t)(LEAD ? 0 : 1) * v.R + slot);
+  const uint64_t li = (uint64_t)bp.x * blockDim.x + threadIdx.x;
+  uint64_t nlisted = 0;
+  if (p.listed) {
+    nlisted = v.act_total[lrow];
+    if ((uint64_t)bp.x * blockDim.x >= nlisted) return;  // uniform
+  }
+  const uint64_t g = p.listed ? (li < nlisted ? v.act_list[lrow * v.G + li]
+                                              : v.G)
+                              : li;
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
@@ -1636,35 +1680,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
     active = false;
   }
-  // Idle rounds: a replica at rest -- its last round left
-  // nothing pending, see the end of the round -- whose round brings no
-  // input changes nothing (node.stepNode finds no event, node.go:1139-1159):
-  // no tick, no staged proposal or ReadIndex, and no record from a
-  // co-resident sender, which the senders' one-byte round tags tell
-  // without reading the mailbox headers.  Its round outputs are already
-  // empty (a round that produced any does not leave the replica at rest).
-  // With Quiesce on, a quiesced replica at rest also skips tick rounds
-  // without input: a quiesced tick only advances its tick counters
-  // (node.tick node.go:1562-1579, raft.quiescedTick raft.go:650-656),
-  // which the next round it runs applies at once (F_QS_BASE).
-  if (active && (!p.tick || (EXT && (flags & F_QUIESCED))) &&
-      (flags & F_AT_REST) && !v.remote_mask) {
-    const uint64_t tags = v.inbox_tag[((uint64_t)L.rbuf * v.R + slot) * v.G + g];
-    const uint32_t want = (uint32_t)(p.round - 1) & 0xffu;
-    bool input = false;
-#pragma unroll
-    for (int s = 0; s < R; ++s)
-      if ((uint32_t)s != slot && ((tags >> (8 * s)) & 0xffu) == want)
-        input = true;
-    if (stage_here<LEAD>(v, slot) && p.prop_slot != DRB_NONE &&
-        v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
-      input = true;
-    if (ri_here<LEAD>(v, p, slot) &&
-        (v.ri_in[(uint64_t)p.ri_slot * v.G + g].x |
-         v.ri_in[(uint64_t)p.ri_slot * v.G + g].y))
-      input = true;
-    if (!input) active = false;
-  }
+  if (active && !p.listed && idle_round<R>(v, p, slot, g, LEAD, flags))
+    active = false;
   if (active) {
     c_stepped = 1;
     Rep<R> r;
@@ -1747,13 +1764,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         umin64(umin64(r.processed + 1, r.committed), r.sm_index);
     // staged inputs are per lane: with replicas spread over ranks a lane
     // holds R different groups, and they go to the stage slot's leader
-    if (ri_here<LEAD>(v, p, slot)) {
+    if (ri_here(v, p, slot, LEAD)) {
       uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
       in_lo = lo64(c);
       in_hi = hi64(c);
     }
     if (is_leader) {
-      if (p.prop_slot != DRB_NONE && stage_here<LEAD>(v, slot))
+      if (p.prop_slot != DRB_NONE && stage_here(v, slot, LEAD))
         nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
       if (r.ri_count + (in_lo != 0) + n_ri_msgs > DRB_RI_DEPTH &&
           fb == DRB_FB_NONE)

@@ -238,9 +238,11 @@ class Engine:
 
     # ---------------------------------------------------------- round
     def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE,
-             reads_per_ctx=0, key_space=0, encode_saves=False, ri_replica=0):
+             reads_per_ctx=0, key_space=0, encode_saves=False, ri_replica=0,
+             listed=False):
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
-                      key_space, int(bool(encode_saves)), ri_replica)
+                      key_space, int(bool(encode_saves)), ri_replica,
+                      int(bool(listed)))
         out = RoundOut()
         _ck(lib().drb_step_round(self.h, C.byref(rin), C.byref(out)),
             "drb_step_round")
@@ -248,12 +250,13 @@ class Engine:
 
     def step_async(self, tick=False, prop_slot=abi.DRB_NONE,
                    ri_slot=abi.DRB_NONE, reads_per_ctx=0, key_space=0,
-                   encode_saves=False, ri_replica=0):
+                   encode_saves=False, ri_replica=0, listed=False):
         """One round, stream-ordered; reads_per_ctx > 0 also serves the
         reads behind the round's ReadyToReads, encode_saves encodes the
         EntriesToSave (drb_round_in)."""
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
-                      key_space, int(bool(encode_saves)), ri_replica)
+                      key_space, int(bool(encode_saves)), ri_replica,
+                      int(bool(listed)))
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
 

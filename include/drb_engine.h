@@ -323,7 +323,11 @@ typedef struct drb_round_in {
    * forwards it to its leader when it is a follower (raft.go:2134-2164).
    * Co-resident placement only. */
   uint32_t ri_replica;
-  uint32_t reserved;
+  /* 1: first list the replicas with work this round (input, a tick for a
+   * replica not quiesced, anything pending) and step only those, packed
+   * into dense waves -- for rounds where most replicas are at rest (C5,
+   * Quiesce); the result is the same.  Co-resident placement only. */
+  uint32_t listed;
 } drb_round_in;
 
 #define DRB_NONE 0xffffffffu

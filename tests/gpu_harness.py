@@ -100,13 +100,14 @@ class Pair:
 
     def round(self, k=1, tick=False, read_index=False, groups=None,
               reads=0, read_key_space=256, encode_saves=False, ri_replica=0,
-              **kw):
+              listed=False, **kw):
         pin, ri_in = self.stage(k, read_index=read_index, groups=groups,
                                 ri_replica=ri_replica, **kw)
         o = self.orc.round(tick=tick)
         e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in,
                           reads_per_ctx=reads, key_space=read_key_space,
-                          encode_saves=encode_saves, ri_replica=ri_replica)
+                          encode_saves=encode_saves, ri_replica=ri_replica,
+                          listed=listed)
         self.rounds += 1
         return o, e
 

@@ -267,9 +267,10 @@ def test_device_generator_matches_workload(val_len, cmd_cap, val_cap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("val_len,cmd_cap,val_cap", [(116, 144, 128),
-                                                     (1011, 1040, 1024)])
-def test_c5_sparse_activity_idle_rounds(val_len, cmd_cap, val_cap):
+@pytest.mark.parametrize("val_len,cmd_cap,val_cap,listed", [
+    (116, 144, 128, False), (1011, 1040, 1024, False),
+    (116, 144, 128, True)])
+def test_c5_sparse_activity_idle_rounds(val_len, cmd_cap, val_cap, listed):
     """C5 in miniature: a seeded 10 % of the groups propose per round
     (drb_gen_kv_proposals_active), 128 B / 1 KB payloads, EntriesToSave
     encoded with CRC, ticks only every 4th round -- replicas at rest skip
@@ -286,7 +287,8 @@ def test_c5_sparse_activity_idle_rounds(val_len, cmd_cap, val_cap):
                                active_ppm=100000)
         tick = r % 4 == 0
         o = p.orc.round(tick=tick)
-        e = p.eng.step(tick=tick, prop_slot=r % 2, encode_saves=True)
+        e = p.eng.step(tick=tick, prop_slot=r % 2, encode_saves=True,
+                       listed=listed)
         p.rounds += 1
         assert e.fallbacks == 0 and e.errors == 0, (r, p.why())
         assert (e.committed_entries, e.applied_entries, e.messages) == \

@@ -24,13 +24,16 @@ def _quiesced(p):
     return n
 
 
-@pytest.mark.parametrize("ppm,ri", [(20000, False), (5000, True)])
-def test_quiesce_sparse_activity(ppm, ri):
+@pytest.mark.parametrize("ppm,ri,listed", [(20000, False, False),
+                                           (5000, True, False),
+                                           (5000, True, True)])
+def test_quiesce_sparse_activity(ppm, ri, listed):
     """Sparse proposals (a seeded ppm of the groups per round) and
     ReadIndex on a few groups, a LocalTick every round, ElectionRTT 4
     (threshold 80 ticks): groups quiesce, wake on proposals / reads and
     quiesce again; every field, log, KV, message (Quiesce messages
-    included) stays bit-exact."""
+    included) stays bit-exact -- also in listed rounds (only the replicas
+    with work stepped, drb_round_in.listed)."""
     p = Pair(G=40, R=3, election_rtt=4, quiesce=True, max_props=2,
              prop_slots=2)
     peak = woke = 0
@@ -39,7 +42,7 @@ def test_quiesce_sparse_activity(ppm, ri):
         act = workload.active_groups(p.G, p.seed, r, ppm)
         o, e = p.round(k=1, tick=True, groups=act,
                        read_index=ri and r % 7 == 3,
-                       prop_slot=r % 2)
+                       prop_slot=r % 2, listed=listed)
         assert e.fallbacks == 0 and e.errors == 0, (r, p.why())
         assert (e.committed_entries, e.applied_entries, e.messages,
                 e.ready_to_reads) == (o.committed_entries, o.applied_entries,
@@ -78,14 +81,18 @@ def test_quiesce_idle_then_wake_all():
     assert _quiesced(p) == 0
 
 
-def test_quiesced_replicas_skip_tick_rounds():
+@pytest.mark.parametrize("listed", [False, True])
+def test_quiesced_replicas_skip_tick_rounds(listed):
     """Quiesced replicas at rest do not run tick rounds at all
-    (replicas_stepped), yet export the ticks they skipped."""
+    (replicas_stepped), yet export the ticks they skipped; a round with a
+    few proposals steps just those groups' replicas."""
     p = Pair(G=64, R=3, election_rtt=4, quiesce=True)
     for r in range(100):
-        p.round(k=0, tick=True)
-    o, e = p.round(k=0, tick=True)
+        p.round(k=0, tick=True, listed=listed)
+    o, e = p.round(k=0, tick=True, listed=listed)
     assert e.replicas_stepped == 0, e.to_dict()
     for r in range(5):
-        p.round(k=0, tick=True)
+        o, e = p.round(k=1, tick=True, groups=[5, 40], listed=listed)
+        assert e.fallbacks == 0 and e.errors == 0, p.why()
+        assert e.replicas_stepped <= 2 * 3, e.to_dict()
     assert not p.check()
