@@ -128,7 +128,16 @@ class Config(C.Structure):
                 ("total_groups", C.c_uint64), ("place_world", C.c_uint32),
                 ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
                 ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
-                ("quiesce", C.c_uint32)]
+                ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
+                ("reserved1", C.c_uint32)]
+
+
+class ApplyResult(C.Structure):
+    """drb_apply_result: one entry applied in the last round."""
+    _fields_ = [("group", C.c_uint64), ("index", C.c_uint64),
+                ("key", C.c_uint64), ("client_id", C.c_uint64),
+                ("series_id", C.c_uint64), ("value", C.c_uint64),
+                ("slot", C.c_uint32), ("ignored", C.c_uint32)]
 
 
 class Flagged(C.Structure):

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/drb_engine.h"
@@ -38,6 +39,7 @@ struct drb_engine {
   hipEvent_t ev_fork, ev_join;    // stream -> stream2 -> stream
   uint64_t round;
   uint64_t ticks;  // LocalTicks delivered so far (RoundParams.tick_no)
+  uint64_t committed_round = 0;  // drb_commit_round (durable_log)
   uint64_t bytes;
   std::vector<void *> allocs;
   uint64_t ctr_rows = 0;                     // workgroup counter rows
@@ -979,18 +981,27 @@ extern "C" int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
 }
 
 // ---------------------------------------------------------------- ingest
-static bool slot_hosted(drb_engine *e, uint64_t g, uint32_t s, bool *ok) {
-  std::vector<uint64_t> idx = {u32_ix(e->v, W_FLAGS, s, g)};
-  std::vector<uint32_t> f;
-  *ok = gather(e, e->v.u32, idx, f) == DRB_OK;
-  return *ok && (f[0] & DRB_F_HOSTED) &&
-         !(f[0] & (DRB_F_FALLBACK | DRB_F_ERROR));
-}
+// drb_ingest: the whole batch in a fixed number of device transfers.  The
+// host decides every message's fate from one gather of the replicas'
+// flags and one of the current (sender, receiver) headers; then the
+// records, the Replicates' entries (into the unhosted sender's window, where
+// the receiver reads them), the headers, the max-append words and the round
+// tag bytes each go down in one scatter.  Messages keep their order within
+// a (sender, receiver) pair (the receiver handles them in that order).
+namespace {
+struct InPlane {  // one (group, from, to) plane of this call
+  uint64_t g;
+  uint32_t from, to;
+  uint4 cur;      // header: tag | quiesce, info, sender term
+  uint64_t maxapp;
+  bool maxapp_valid;
+};
+}  // namespace
 
 extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                           const drb_entry *ents, const uint8_t *pool,
                           uint64_t *accepted, uint64_t *dropped) {
-  if (!e) return DRB_EINVAL;
+  if (!e || (n && !msgs)) return DRB_EINVAL;
   const View &v = e->v;
   // replicas spread over ranks exchange whole mailbox planes instead
   if (v.remote_mask) return DRB_ENOSYS;
@@ -998,60 +1009,104 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
   const uint32_t tag = (uint32_t)e->round;
   uint64_t acc = 0, drop = 0;
+  // 1. shape checks, then the hosted flags of every target and sender
+  std::vector<uint8_t> ok(n, 0);
+  std::vector<uint64_t> fidx;
+  fidx.reserve(2 * n);
   for (size_t i = 0; i < n; ++i) {
     const drb_message &m = msgs[i];
-    uint64_t g = m.shard_id - v.first_shard_id;
-    bool ok = g < v.G && m.to >= 1 && m.to <= v.R && m.from >= 1 &&
-              m.from <= v.R && m.from != m.to && m.n_entries <= 0xffff;
-    bool okd = true;
-    if (ok) ok = slot_hosted(e, g, (uint32_t)(m.to - 1), &okd);
-    bool from_hosted = ok ? slot_hosted(e, g, (uint32_t)(m.from - 1), &okd)
-                          : false;
-    if (!okd) return DRB_EDEVICE;
-    if (!ok || from_hosted) {  // transport delivers only remote senders
+    const uint64_t g = m.shard_id - v.first_shard_id;
+    ok[i] = g < v.G && m.to >= 1 && m.to <= v.R && m.from >= 1 &&
+            m.from <= v.R && m.from != m.to && m.n_entries <= v.W;
+    if (!ok[i]) continue;
+    fidx.push_back(u32_ix(v, W_FLAGS, (uint32_t)(m.to - 1), g));
+    fidx.push_back(u32_ix(v, W_FLAGS, (uint32_t)(m.from - 1), g));
+  }
+  std::vector<uint32_t> fl;
+  if (gather(e, v.u32, fidx, fl)) return DRB_EDEVICE;
+  // 2. the planes touched and their current headers
+  std::unordered_map<uint64_t, uint32_t> pid;  // (g, from, to) -> plane
+  std::vector<InPlane> planes;
+  std::vector<uint32_t> mplane(n, ~0u);
+  size_t q = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) {
       drop++;
       continue;
     }
-    uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
-    std::vector<uint64_t> mi = {mmeta_ix(v, buf, from, to, g)};
-    std::vector<uint4> meta;
-    if (gather(e, v.mbox_meta, mi, meta)) return DRB_EDEVICE;
-    uint4 cur = meta[0];
-    if (!tag_is(cur.x, tag)) {
+    const drb_message &m = msgs[i];
+    const uint32_t ft = fl[q++], ff = fl[q++];
+    const bool live = (ft & DRB_F_HOSTED) &&
+                      !(ft & (DRB_F_FALLBACK | DRB_F_ERROR));
+    const bool from_hosted = (ff & DRB_F_HOSTED) &&
+                             !(ff & (DRB_F_FALLBACK | DRB_F_ERROR));
+    if (!live || from_hosted) {  // the transport delivers remote senders only
+      drop++;
+      ok[i] = 0;
+      continue;
+    }
+    const uint64_t g = m.shard_id - v.first_shard_id;
+    const uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
+    const uint64_t key = (g * v.R + from) * v.R + to;
+    auto it = pid.find(key);
+    if (it == pid.end()) {
+      it = pid.emplace(key, (uint32_t)planes.size()).first;
+      planes.push_back(InPlane{g, from, to, make_uint4(0, 0, 0, 0), 0, false});
+    }
+    mplane[i] = it->second;
+  }
+  std::vector<uint64_t> hidx, xidx;
+  for (const InPlane &pl : planes) {
+    hidx.push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
+    xidx.push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
+  }
+  std::vector<uint4> hdr;
+  std::vector<uint64_t> mx;
+  if (gather(e, v.mbox_meta, hidx, hdr) || gather(e, v.mbox_maxapp, xidx, mx))
+    return DRB_EDEVICE;
+  for (size_t p = 0; p < planes.size(); ++p) {
+    uint4 cur = hdr[p];
+    if (!tag_is(cur.x, tag)) {  // nothing there yet this round
       cur = pack2(0, 0);
       cur.x = tag & MQ_TAG;
     }
+    planes[p].cur = cur;
+    planes[p].maxapp = mx[p];
+    planes[p].maxapp_valid = mi_nrep(cur.y) > 0;
+  }
+  // 3. place every message in its plane, in order
+  std::vector<uint64_t> ridx, eidx;
+  std::vector<uint4> rval, eval;
+  std::vector<uint4> ch(ENT_META + v.C16);
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) continue;
+    const drb_message &m = msgs[i];
+    InPlane &pl = planes[mplane[i]];
+    uint4 &cur = pl.cur;
     if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
       cur.x |= MQ_QUIESCE;
-      std::vector<uint4> mv = {cur};
-      if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
-      std::vector<uint64_t> ti = {((uint64_t)buf * v.R + to) * v.G + g};
-      std::vector<uint64_t> tv;
-      if (gather(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
-      tv[0] = (tv[0] & ~(0xffull << (8 * from))) |
-              ((uint64_t)(tag & 0xffu) << (8 * from));
-      if (scatter(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
       acc++;
       continue;
     }
-    const bool rep = m.type == DRB_MSG_REPLICATE;
-    const uint32_t nrep0 = mi_nrep(cur.y);
-    const uint32_t k = rep ? nrep0 : rec_pos(false, mi_noth(cur.y), v.MB);
     if (mi_count(cur.y) >= v.MB) {  // MessageQueue full (message.go:105-123)
       drop++;
       continue;
     }
-    // entries travel in the sender's (unhosted) window slot
-    if (m.type == DRB_MSG_REPLICATE && m.n_entries) {
-      if (m.n_entries > v.W) {
-        drop++;
-        continue;
+    const bool rep = m.type == DRB_MSG_REPLICATE;
+    const uint32_t k = rep ? mi_nrep(cur.y)
+                           : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (rep && m.n_entries) {
+      // the entries travel in the sender's (unhosted) window slot
+      for (uint64_t x = 0; x < m.n_entries; ++x) {
+        drb_entry en = ents[m.entries_off + x];
+        if (en.cmd_len > v.C16 * 16) return DRB_ERANGE;
+        en.index = m.log_index + 1 + x;
+        entry_to_chunks(v, en, pool, ch.data());
+        for (uint32_t c = 0; c < ENT_META + v.C16; ++c) {
+          eidx.push_back(ring_ix(v, pl.from, en.index, c, pl.g));
+          eval.push_back(ch[c]);
+        }
       }
-      std::vector<drb_entry> es(ents + m.entries_off,
-                                ents + m.entries_off + m.n_entries);
-      for (size_t q = 0; q < es.size(); ++q) es[q].index = m.log_index + 1 + q;
-      int rc = drb_import_log(e, g, from, es.data(), es.size(), pool);
-      if (rc) return rc;
     }
     Msg mm;
     mm.type = m.type;
@@ -1064,7 +1119,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     mm.hint = m.hint;
     mm.hint_high = m.hint_high;
     uint4 c0, c1;
-    msg_encode(mm, to, nullptr, c0, c1);
+    msg_encode(mm, pl.to, nullptr, c0, c1);
     // the sender's term is stored once per (sender, receiver, round) in the
     // header; a record whose term differs from it makes the receiver fall
     // back (term gate, raft.go:1596-1609)
@@ -1079,35 +1134,50 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
         c0.x |= MF_TERM_OTHER;
       }
     }
-    std::vector<uint64_t> idx = {mbox_ix(v, buf, from, to, k, 0, g),
-                                 mbox_ix(v, buf, from, to, k, 1, g)};
-    std::vector<uint4> val = {c0, c1};
-    if (scatter(e, v.mbox, idx, val)) return DRB_EDEVICE;
+    ridx.push_back(mbox_ix(v, buf, pl.from, pl.to, k, 0, pl.g));
+    rval.push_back(c0);
+    ridx.push_back(mbox_ix(v, buf, pl.from, pl.to, k, 1, pl.g));
+    rval.push_back(c1);
     const uint32_t inf =
         msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0);
     cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
     if (rep) {
-      std::vector<uint64_t> xi = {mi[0]};
-      std::vector<uint64_t> xv;
-      if (gather(e, v.mbox_maxapp, xi, xv)) return DRB_EDEVICE;
-      uint64_t ma = m.log_index + m.n_entries;
-      if (nrep0 > 0) ma = std::max(ma, xv[0]);
-      std::vector<uint64_t> nv = {ma};
-      if (scatter(e, v.mbox_maxapp, xi, nv)) return DRB_EDEVICE;
-    }
-    std::vector<uint4> mv = {cur};
-    if (scatter(e, v.mbox_meta, mi, mv)) return DRB_EDEVICE;
-    // the receiver's round tag for this sender (idle-round check)
-    {
-      std::vector<uint64_t> ti = {((uint64_t)buf * v.R + to) * v.G + g};
-      std::vector<uint64_t> tv;
-      if (gather(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
-      tv[0] = (tv[0] & ~(0xffull << (8 * from))) |
-              ((uint64_t)(tag & 0xffu) << (8 * from));
-      if (scatter(e, v.inbox_tag, ti, tv)) return DRB_EDEVICE;
+      const uint64_t ma = m.log_index + m.n_entries;
+      pl.maxapp = pl.maxapp_valid ? std::max(pl.maxapp, ma) : ma;
+      pl.maxapp_valid = true;
     }
     acc++;
   }
+  // 4. down: entries, records, headers, max-append, the round tag bytes
+  std::vector<uint4> hval;
+  std::vector<uint64_t> xval, tidx;
+  for (const InPlane &pl : planes) {
+    hval.push_back(pl.cur);
+    xval.push_back(pl.maxapp);
+  }
+  // tag bytes: one u64 word per (receiver, group), a byte per sender
+  std::unordered_map<uint64_t, uint32_t> tw;
+  std::vector<uint64_t> tmask;  // sender bytes to set per word
+  for (const InPlane &pl : planes) {
+    if (!(mi_count(pl.cur.y) || (pl.cur.x & MQ_QUIESCE))) continue;
+    const uint64_t w = ((uint64_t)buf * v.R + pl.to) * v.G + pl.g;
+    auto it = tw.find(w);
+    if (it == tw.end()) {
+      it = tw.emplace(w, (uint32_t)tidx.size()).first;
+      tidx.push_back(w);
+      tmask.push_back(0);
+    }
+    tmask[it->second] |= 0xffull << (8 * pl.from);
+  }
+  std::vector<uint64_t> tv;
+  if (scatter(e, v.ring, eidx, eval) || scatter(e, v.mbox, ridx, rval) ||
+      scatter(e, v.mbox_meta, hidx, hval) ||
+      scatter(e, v.mbox_maxapp, xidx, xval) || gather(e, v.inbox_tag, tidx, tv))
+    return DRB_EDEVICE;
+  const uint64_t tb = tag & 0xffu;
+  for (size_t w = 0; w < tidx.size(); ++w)
+    tv[w] = (tv[w] & ~tmask[w]) | (tmask[w] & (tb * 0x0101010101010101ull));
+  if (scatter(e, v.inbox_tag, tidx, tv)) return DRB_EDEVICE;
   if (accepted) *accepted = acc;
   if (dropped) *dropped = drop;
   return DRB_OK;
@@ -1321,6 +1391,8 @@ static int refresh_roles(drb_engine *e) {
 
 extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (!e || !in) return DRB_EINVAL;
+  // a durable LogDB: the last round's messages wait for its persistence
+  if (e->cfg.durable_log && e->committed_round < e->round) return DRB_EINVAL;
   if (in->prop_slot != DRB_NONE && in->prop_slot >= e->cfg.prop_slots)
     return DRB_ERANGE;
   if (in->ri_slot != DRB_NONE && in->ri_slot >= e->cfg.ri_slots)
@@ -1413,6 +1485,119 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
     HIPCHK(hipStreamSynchronize(e->stream));
   }
   return DRB_OK;
+}
+
+extern "C" int drb_commit_round(drb_engine *e, uint64_t round) {
+  if (!e || round > e->round) return DRB_EINVAL;
+  if (round > e->committed_round) e->committed_round = round;
+  return DRB_OK;
+}
+
+extern "C" uint64_t drb_committed_round(const drb_engine *e) {
+  return e ? e->committed_round : 0;
+}
+
+// the PIdx field i of replica (slot, g) from its packed record (device)
+__device__ static uint64_t pk_field(const View &v, uint32_t slot, uint64_t g,
+                                    int i) {
+  const uint4 c0 = v.pk[pk_ix(v, 0, slot, g)];
+  const uint4 c = v.pk[pk_ix(v, (4 + i / 2) / 4, slot, g)];
+  const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+  const uint32_t code = (w[(4 + i / 2) % 4] >> (16 * (i & 1))) & 0xffffu;
+  const uint64_t last = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+  return code == PK_ESC16 ? v.u64[u64_ix(v, pi_field(i), slot, g)]
+                          : pk_idx_value(code, last, i == PI_RING_GUARD);
+}
+
+// drb_apply_results: the entries (applied_index, sm_index] a replica applied
+// in the round it last ran (updateAppliedIndex set applied_index to the
+// state machine's index at that round's start); one output slot range per
+// wave from a single atomic
+__global__ __launch_bounds__(256) void k_apply_results(
+    const View v, uint32_t slot, uint64_t first, uint64_t n,
+    drb_apply_result *out, unsigned long long *count, uint64_t cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t g = first + i;
+  uint64_t lo = 0, hi = 0;
+  if (i < n) {
+    const uint32_t fl = v.u32[u32_ix(v, W_FLAGS, slot, g)];
+    const bool frozen = (fl & (DRB_F_FALLBACK | DRB_F_ERROR)) &&
+                        !(fl & DRB_F_APPLY_STOPPED);
+    if ((fl & DRB_F_HOSTED) && !frozen) {
+      lo = pk_field(v, slot, g, PI_APPLIED_INDEX);
+      hi = pk_field(v, slot, g, PI_SM_INDEX);
+    }
+  }
+  const uint32_t cnt = hi > lo ? (uint32_t)(hi - lo) : 0u;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= (uint32_t)o) incl += t;
+  }
+  const uint32_t total = __shfl(incl, 63, 64);
+  unsigned long long b = 0;
+  if (lane == 0 && total) b = atomicAdd(count, (unsigned long long)total);
+  b = __shfl(b, 0, 64);
+  const uint64_t pos = b + incl - cnt;
+  for (uint32_t k = 0; k < cnt; ++k) {
+    if (pos + k >= cap) break;
+    const uint64_t idx = lo + 1 + k;
+    const uint4 m0 = v.ring[ring_ix(v, slot, idx, 0, g)];
+    const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
+    const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
+    drb_apply_result r;
+    r.group = g;
+    r.index = idx;
+    r.key = hi64(m0);
+    r.client_id = lo64(m1);
+    r.series_id = hi64(m1);
+    const uint32_t type = m2.z, clen = m2.w;
+    r.ignored = r.client_id == 0 ? 1u : 0u;  // an empty no-op entry
+    // KVTest.Update's Result.Value: the payload length (kvtest.go:161)
+    r.value = r.ignored ? 0
+                        : (type == DRB_ENTRY_ENCODED && clen ? clen - 1 : clen);
+    r.slot = slot;
+    out[pos + k] = r;
+  }
+}
+
+extern "C" int drb_apply_results(drb_engine *e, uint32_t slot,
+                                 uint64_t first_group, uint64_t n_groups,
+                                 drb_apply_result *out, size_t cap,
+                                 size_t *n_out) {
+  if (!e || slot >= e->v.R || (cap && !out)) return DRB_EINVAL;
+  if (check_range(e, first_group, n_groups)) return DRB_ERANGE;
+  if (!n_groups) {
+    if (n_out) *n_out = 0;
+    return DRB_OK;
+  }
+  void *s;
+  const size_t bytes = 64 + cap * sizeof(drb_apply_result);
+  if (scratch(e, bytes, &s)) return DRB_EDEVICE;
+  unsigned long long *cnt = (unsigned long long *)s;
+  drb_apply_result *dout = (drb_apply_result *)((char *)s + 64);
+  HIPCHK(hipMemsetAsync(cnt, 0, 8, e->stream));
+  k_apply_results<<<(unsigned)((n_groups + 255) / 256), 256, 0, e->stream>>>(
+      e->v, slot, first_group, n_groups, dout, cnt, cap);
+  HIPCHK(hipGetLastError());
+  unsigned long long n = 0;
+  HIPCHK(hipMemcpyAsync(&n, cnt, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const size_t take = std::min<size_t>(n, cap);
+  if (take) {
+    HIPCHK(hipMemcpyAsync(out, dout, take * sizeof(drb_apply_result),
+                          hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    std::sort(out, out + take,
+              [](const drb_apply_result &a, const drb_apply_result &b) {
+                return a.group != b.group ? a.group < b.group
+                                          : a.index < b.index;
+              });
+  }
+  if (n_out) *n_out = (size_t)n;
+  return n > cap ? DRB_ERANGE : DRB_OK;
 }
 
 extern "C" int drb_take_flagged(drb_engine *e, drb_flagged *out, size_t cap,

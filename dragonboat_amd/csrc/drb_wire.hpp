@@ -763,6 +763,9 @@ static int wire_init(drb_engine *e) {
 extern "C" int drb_encode_wire(drb_engine *e, uint32_t from_slot,
                                uint32_t to_slot, const drb_wire_cfg *cfg,
                                drb_wire_out *res) {
+  // a durable LogDB: the round's responses leave only once it is saved
+  if (e && e->cfg.durable_log && e->committed_round < e->round)
+    return DRB_EINVAL;
   if (!e || !cfg || from_slot >= e->cfg.num_replicas ||
       to_slot >= e->cfg.num_replicas || from_slot == to_slot ||
       cfg->source_len > drb::WIRE_MAX_SRC ||

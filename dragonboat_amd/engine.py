@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 from . import abi
-from .abi import (Config, Entry, Flagged, Message, ReadyToRead, Region, ReplicaState,
+from .abi import (ApplyResult, Config, Entry, Flagged, Message, ReadyToRead, Region, ReplicaState,
                   RoundIn, RoundOut, WireCfg, WireIn, WireOut, entry_to_tuple,
                   message_to_tuple)
 
@@ -56,6 +56,10 @@ SIGNATURES = {
     "drb_read_counters": (C.c_int, [P, C.POINTER(RoundOut), C.c_int]),
     "drb_take_flagged": (C.c_int, [P, C.POINTER(Flagged), SZ, C.POINTER(SZ),
                                    PU64, C.c_int]),
+    "drb_apply_results": (C.c_int, [P, U32, U64, U64, C.POINTER(ApplyResult),
+                                    SZ, C.POINTER(SZ)]),
+    "drb_commit_round": (C.c_int, [P, U64]),
+    "drb_committed_round": (U64, [P]),
     "drb_export_outbox": (C.c_int, [P, U64, U32, C.POINTER(Message), SZ,
                                     C.POINTER(Entry), SZ, PU8, SZ,
                                     C.POINTER(SZ)]),
@@ -125,7 +129,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 mailbox=16, kv_slots=512, kv_val_cap=4, election_rtt=10,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
-                kv_pool_blocks=0, flagged_cap=0, quiesce=0)
+                kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0)
 
 
 class Engine:
@@ -143,7 +147,8 @@ class Engine:
                    cfg["check_quorum"], cfg["device"], cfg["save_cap"],
                    cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
                    cfg["entry_mbox"], cfg["kv_pool_blocks"],
-                   cfg["flagged_cap"], cfg["quiesce"])
+                   cfg["flagged_cap"], cfg["quiesce"],
+                   cfg["durable_log"], 0)
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -277,6 +282,25 @@ class Engine:
         return ([(arr[i].group, arr[i].slot, arr[i].reason, arr[i].flags,
                   arr[i].round, arr[i].shard_id) for i in range(n.value)],
                 lost.value)
+
+    def apply_results(self, slot, first_group=0, n_groups=None, cap=None):
+        """[(group, index, key, client_id, series_id, value, ignored)] of
+        the entries replica slot applied in the last round."""
+        n_groups = self.G - first_group if n_groups is None else n_groups
+        cap = cap or n_groups * self.cfg["max_props"] * 4 + 16
+        arr = (ApplyResult * cap)()
+        n = SZ()
+        _ck(lib().drb_apply_results(self.h, slot, first_group, n_groups, arr,
+                                    cap, C.byref(n)), "drb_apply_results")
+        return [(a.group, a.index, a.key, a.client_id, a.series_id, a.value,
+                 a.ignored) for a in arr[:n.value]]
+
+    def commit_round(self, rnd):
+        _ck(lib().drb_commit_round(self.h, rnd), "drb_commit_round")
+
+    @property
+    def committed_round(self):
+        return lib().drb_committed_round(self.h)
 
     # ---------------------------------------------------------- outputs
     def export_outbox(self, g, slot):

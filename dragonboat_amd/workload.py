@@ -69,16 +69,18 @@ def proposal(seed, g, s, j, key_space, val_len):
 
 
 def build_batch(num_groups, k, seed, salt, key_space=256, val_len=4,
-                groups=None):
-    """Returns (counts[u32 G], ents[Entry G*k], pool, python list)."""
+                groups=None, gids=None):
+    """Returns (counts[u32 G], ents[Entry G*k], pool).  gids: entry i
+    carries the proposals of global group gids[i] (a sampled cluster)."""
     counts = (C.c_uint32 * num_groups)()
     ents = (Entry * max(1, num_groups * k))()
     pool = bytearray()
     gs = range(num_groups) if groups is None else groups
     for g in gs:
         counts[g] = k
+        gg = g if gids is None else gids[g]
         for j in range(k):
-            p = proposal(seed, g, salt, j, key_space, val_len)
+            p = proposal(seed, gg, salt, j, key_space, val_len)
             ents[g * k + j] = Entry(0, 0, p["key"], p["client_id"], 0, 0,
                                     p["type"], len(p["cmd"]), len(pool))
             pool += p["cmd"]
@@ -93,20 +95,23 @@ def read_index_ctx(seed, g, salt, high):
     return low, high
 
 
-def build_read_index(num_groups, seed, salt, high, groups=None):
+def build_read_index(num_groups, seed, salt, high, groups=None, gids=None):
     lo = (C.c_uint64 * num_groups)()
     hi = (C.c_uint64 * num_groups)()
     gs = range(num_groups) if groups is None else groups
     for g in gs:
-        lo[g], hi[g] = read_index_ctx(seed, g, salt, high)
+        lo[g], hi[g] = read_index_ctx(seed, g if gids is None else gids[g],
+                                      salt, high)
     return lo, hi
 
 
-def active_groups(num_groups, seed, salt, active_ppm):
+def active_groups(num_groups, seed, salt, active_ppm, gids=None):
     """The seeded Bernoulli subset of groups that propose in batch `salt`
-    (drb_gen_kv_proposals_active; SURVEY 8d C5: 1 % active per round)."""
+    (drb_gen_kv_proposals_active; SURVEY 8d C5: 1 % active per round);
+    with gids, the indices i whose global group gids[i] is active."""
     if active_ppm >= 1000000:
         return list(range(num_groups))
     return [g for g in range(num_groups)
-            if mix64(seed ^ ACTIVE_SALT ^ ((g * GOLDEN) & MASK) ^
+            if mix64(seed ^ ACTIVE_SALT ^
+                     (((g if gids is None else gids[g]) * GOLDEN) & MASK) ^
                      ((salt << 24) & MASK)) % 1000000 < active_ppm]

@@ -303,6 +303,11 @@ typedef struct drb_config {
    * replicas without input skip tick rounds (their ticks are applied
    * when they next run) */
   uint32_t quiesce;
+  /* 1: the host persists each round's EntriesToSave (a durable ILogDB)
+   * before the round's messages may be delivered: drb_step_round of round
+   * t+1 and drb_encode_wire of round t require drb_commit_round(t) */
+  uint32_t durable_log;
+  uint32_t reserved1;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -551,6 +556,41 @@ int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
 /* The whole exchange among engines[rank] of one process (peer copies on
  * the receivers' streams); every engine must have run the same round. */
 int drb_exchange_local(drb_engine *const *engines, uint32_t n);
+
+/*
+ * The entries one replica slot applied in the last round, for
+ * node.ApplyUpdate -> pendingProposals.applied (node.go:243-257,
+ * request.go:1041-1045; rsm handleEntry statemachine.go:935-969): per
+ * entry its Key / ClientID / SeriesID and sm.Result.Value, which KVTest
+ * sets to the length of the update's Cmd payload (kvtest.go:161).  Groups
+ * [first_group, first_group + n_groups), sorted by (group, index); *n_out
+ * is the count (DRB_ERANGE if more than cap).  Replicas handed to the CPU
+ * path report nothing, except those whose apply stopped
+ * (DRB_F_APPLY_STOPPED): their entries applied before the stop.
+ */
+typedef struct drb_apply_result {
+  uint64_t group;      /* lane */
+  uint64_t index;
+  uint64_t key;        /* pb.Entry.Key: the proposal's RequestState key */
+  uint64_t client_id;
+  uint64_t series_id;
+  uint64_t value;      /* sm.Result.Value */
+  uint32_t slot;
+  uint32_t ignored;    /* 1: an empty no-op entry (statemachine.go:939-942) */
+} drb_apply_result;
+int drb_apply_results(drb_engine *e, uint32_t slot, uint64_t first_group,
+                      uint64_t n_groups, drb_apply_result *out, size_t cap,
+                      size_t *n_out);
+
+/* Peer.Commit's ordering for a durable LogDB (engine.go:1343-1359,
+ * raftpb/update.go:60-69): the host calls this once round `round`'s
+ * EntriesToSave (drb_saved_buffers / drb_export_saved) are persisted; with
+ * drb_config.durable_log the round's non-Replicate messages (ReplicateResp
+ * and the rest, sent after SaveRaftState, node.go:1104-1108) are not
+ * delivered -- no later round runs, no wire stream is encoded -- before. */
+int drb_commit_round(drb_engine *e, uint64_t round);
+/* The last round committed so far (durable_log). */
+uint64_t drb_committed_round(const drb_engine *e);
 
 /* IStateMachine.Lookup used by NodeHost.ReadLocalNode (nodehost.go:849). */
 int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,

@@ -156,6 +156,7 @@ typedef struct orc_node {
 
 struct orc_cluster {
   orc_cluster_cfg cfg;
+  uint64_t *gids; /* [num_groups] global group ids */
   orc_node *nodes; /* [g * R + slot] */
   uint64_t round;
 };
@@ -689,6 +690,11 @@ orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg) {
     return NULL;
   orc_cluster *c = (orc_cluster *)calloc(1, sizeof(orc_cluster));
   c->cfg = *cfg;
+  c->gids = (uint64_t *)malloc((cfg->num_groups ? cfg->num_groups : 1) *
+                               sizeof(uint64_t));
+  for (uint64_t g = 0; g < cfg->num_groups; g++)
+    c->gids[g] = cfg->gids ? cfg->gids[g] : g;
+  c->cfg.gids = c->gids;
   uint64_t R = cfg->num_replicas;
   c->nodes = (orc_node *)calloc(cfg->num_groups * R, sizeof(orc_node));
   jmp_buf jb;
@@ -702,9 +708,10 @@ orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg) {
     for (uint32_t s = 0; s < R; s++) {
       orc_node *n = node_at(c, g, s);
       n->db = orc_logdb_new();
-      n->r = raft_new(cfg->first_shard_id + g, s + 1, cfg->election_rtt,
+      const uint64_t gid = c->gids[g];
+      n->r = raft_new(cfg->first_shard_id + gid, s + 1, cfg->election_rtt,
                       cfg->heartbeat_rtt, (int)cfg->check_quorum, n->db,
-                      mix64(cfg->seed ^ (g * R + s)));
+                      mix64(cfg->seed ^ (gid * R + s)));
       n->hosted = 1;
       /* quiesceState{electionTick: ElectionRTT * 2} (node.go:195-200) */
       n->qs.election_tick = 2ull * cfg->election_rtt;
@@ -731,6 +738,7 @@ void orc_cluster_free(orc_cluster *c) {
     ev_free(&n->saved);
   }
   free(c->nodes);
+  free(c->gids);
   free(c);
 }
 
@@ -782,7 +790,7 @@ int orc_cluster_setup_steady(orc_cluster *c, uint32_t leader_slot) {
       orc_raft *r = node_at(c, g, s)->r;
       uint64_t e = c->cfg.election_rtt;
       r->randomized_election_timeout =
-          e + mix64(c->cfg.seed ^ (0xE1ull << 56) ^ (g * R + s)) % e;
+          e + mix64(c->cfg.seed ^ (0xE1ull << 56) ^ (c->gids[g] * R + s)) % e;
     }
   return 0;
 }

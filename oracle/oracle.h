@@ -261,6 +261,10 @@ typedef struct orc_cluster_cfg {
   uint64_t logdb_keep; /* 0: keep every saved entry; else compact behind */
   uint32_t quiesce;    /* Config.Quiesce (config.go:195) */
   uint32_t pad;
+  /* NULL: group g is global group g.  Else group g of this cluster is
+   * global group gids[g] (ShardID, seeds): a sample of a large engine's
+   * groups, simulated alone (groups are independent) */
+  const uint64_t *gids;
 } orc_cluster_cfg;
 
 orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg);

@@ -42,7 +42,8 @@ class ClusterCfg(C.Structure):
                 ("num_replicas", C.c_uint32), ("election_rtt", C.c_uint32),
                 ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
                 ("seed", C.c_uint64), ("logdb_keep", C.c_uint64),
-                ("quiesce", C.c_uint32), ("pad", C.c_uint32)]
+                ("quiesce", C.c_uint32), ("pad", C.c_uint32),
+                ("gids", C.POINTER(C.c_uint64))]
 
 
 P = C.c_void_p
@@ -546,10 +547,16 @@ class Cluster:
 
     def __init__(self, num_groups, num_replicas=3, election_rtt=10,
                  heartbeat_rtt=1, check_quorum=1, seed=0x5EEDD8B0,
-                 first_shard_id=1, logdb_keep=0, quiesce=0):
+                 first_shard_id=1, logdb_keep=0, quiesce=0, gids=None):
+        """gids: simulate only these global group ids (group i of the
+        cluster is global group gids[i]; None: 0..num_groups-1)."""
+        self.gids = None if gids is None else \
+            (C.c_uint64 * len(gids))(*gids)
+        if gids is not None:
+            num_groups = len(gids)
         cfg = ClusterCfg(num_groups, first_shard_id, num_replicas,
                          election_rtt, heartbeat_rtt, check_quorum, seed,
-                         logdb_keep, int(bool(quiesce)), 0)
+                         logdb_keep, int(bool(quiesce)), 0, self.gids)
         self.cfg = cfg
         self.G = num_groups
         self.R = num_replicas

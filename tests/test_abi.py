@@ -61,6 +61,7 @@ STRUCTS = {
     "drb_wire_out": abi.WireOut,
     "drb_wire_in": abi.WireIn,
     "drb_flagged": abi.Flagged,
+    "drb_apply_result": abi.ApplyResult,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}

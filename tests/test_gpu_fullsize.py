@@ -1,0 +1,163 @@
+"""GPU: parity at the BASELINE sizes, on a sample of the groups.
+
+The engine runs the full configuration of a bench workload -- C3
+(1,048,576 groups x 3, 16 B, 9:1 ReadIndex with the reads served in the
+round), C4's replica count co-resident (1,048,576 x 5), C5 (4,194,304 x 3,
+128 B and 1 KB payloads, 1 % active per round, EntryBatch + CRC32, Quiesce,
+listed rounds) -- from the same device input generators bench.py uses.  The
+oracle simulates only a sample of ~1000 global group ids (including the
+first and the last), with the same per-group seeds (oracle/, gids; groups
+are independent, tests/test_oracle_cluster.py pins that), and the sampled
+groups must match bit-exactly: every replica field, the resident log, the
+KV contents, the outbox, the served-read checksums and the EntriesToSave
+bytes + CRC.
+"""
+import random
+
+import pytest
+
+from dragonboat_amd import workload
+from dragonboat_amd.engine import Engine
+from oracle import pyoracle as po
+from tests.gpu_harness import by_dest, state_diff
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EEDD8B0
+
+
+def _sample(G, n=1000):
+    rng = random.Random(G * 7 + 1)
+    return sorted(set([0, 1, 2, G // 2, G - 2, G - 1] +
+                      rng.sample(range(G), n)))
+
+
+def _compare(eng, orc, gids, R, logs=True, saves=False):
+    errs = []
+    for i, g in enumerate(gids):
+        est = eng.export_replicas(g, 1)
+        for s in range(R):
+            a, b = est[s], orc.export(i, s)
+            d = state_diff(a, b, R)
+            if a.shard_id != b.shard_id or a.flags != b.flags:
+                d["ids"] = ((a.shard_id, a.flags), (b.shard_id, b.flags))
+            if d:
+                errs.append((g, s, "state", d))
+                continue
+            if logs:
+                lo = max(1, b.last_index - 6)
+                if eng.export_log(g, s, lo, b.last_index) != \
+                        orc.export_log(i, s, lo, b.last_index):
+                    errs.append((g, s, "log"))
+            if eng.kv_export(g, s) != orc.export_kv(i, s):
+                errs.append((g, s, "kv"))
+            if by_dest(eng.export_outbox(g, s)) != \
+                    by_dest(orc.export_outbox(i, s)):
+                errs.append((g, s, "msgs"))
+            if saves and eng.export_saved(g, s) != orc.export_saved(i, s):
+                errs.append((g, s, "saved"))
+        if len(errs) > 4:
+            break
+    return errs
+
+
+def test_fullsize_c3_sampled():
+    """C3 as bench.py runs it (8 staged batches from the device
+    generators, a LocalTick every round, 9 served reads per ctx)."""
+    G, R, NP = 1 << 20, 3, 8
+    eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                 max_props=1, prop_slots=NP, ri_slots=NP, mailbox=16,
+                 kv_slots=512, kv_val_cap=4)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    for b in range(NP):
+        eng.gen_kv_proposals(b, 1, 256, 4, SEED, b)
+        eng.gen_read_index(b, SEED, b + 30)  # ctx salt: the round (1)
+    gids = _sample(G)
+    n = len(gids)
+    orc = po.Cluster(n, R, seed=SEED, gids=gids)
+    orc.setup_steady(0)
+    for r in range(24):
+        b = r % NP
+        counts, ents, pool = workload.build_batch(n, 1, SEED, b, gids=gids)
+        orc.stage_proposals(counts, 1, ents, pool)
+        lo, hi = workload.build_read_index(n, SEED, 1, b + 30, gids=gids)
+        orc.stage_read_index(lo, hi)
+        o = orc.round(tick=True)
+        e = eng.step(tick=True, prop_slot=b, ri_slot=b, reads_per_ctx=9,
+                     key_space=256)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        if r >= 3:
+            assert e.committed_entries == G, (r, e.committed_entries)
+        sums, served, deferred = orc.serve_reads(9, 256)
+        esum = eng.export_read_sums(0, G)
+        for i, g in enumerate(gids):
+            for s in range(R):
+                x = sums[i * R + s]
+                if x is not None:
+                    assert esum[g * R + s] == x, (r, g, s)
+        if r % 8 == 7:
+            errs = _compare(eng, orc, gids, R)
+            assert not errs, (r, errs[:3])
+
+
+def test_fullsize_five_replicas_sampled():
+    """C4's 5-replica groups at 1,048,576 lanes, co-resident (N = 1)."""
+    G, R, NP = 1 << 20, 5, 8
+    eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                 max_props=1, prop_slots=NP, ri_slots=NP, mailbox=16,
+                 kv_slots=512, kv_val_cap=4)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    for b in range(NP):
+        eng.gen_kv_proposals(b, 1, 256, 4, SEED, b)
+    gids = _sample(G, 600)
+    n = len(gids)
+    orc = po.Cluster(n, R, seed=SEED, gids=gids)
+    orc.setup_steady(0)
+    for r in range(20):
+        b = r % NP
+        counts, ents, pool = workload.build_batch(n, 1, SEED, b, gids=gids)
+        orc.stage_proposals(counts, 1, ents, pool)
+        o = orc.round(tick=(r % 2 == 0))
+        e = eng.step(tick=(r % 2 == 0), prop_slot=b)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+    errs = _compare(eng, orc, gids, R)
+    assert not errs, errs[:3]
+
+
+@pytest.mark.parametrize("payload,rounds", [(128, 240), (1024, 40)])
+def test_fullsize_c5_sampled(payload, rounds):
+    """C5 as bench.py runs it: 4,194,304 groups, a fresh seeded 1 % of
+    them proposing each round (device generator, salt = round), values out
+    of line, EntriesToSave encoded, Quiesce on, listed rounds."""
+    G, R = 4 << 20, 3
+    vlen = {128: 116, 1024: 1011}[payload]
+    cmd_cap = ((12 + (1 if vlen < 128 else 2) + vlen) + 15) // 16 * 16
+    bound = 73 + cmd_cap
+    ks = 16 if payload == 128 else 8
+    eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
+                 max_props=1, prop_slots=2, ri_slots=1, mailbox=8,
+                 kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
+                 kv_pool_blocks=ks * G * R if payload == 128 else 4 * G * R,
+                 save_cap=(4 * bound + 15) // 16 * 16, quiesce=1)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    gids = _sample(G, 1000)
+    n = len(gids)
+    orc = po.Cluster(n, R, seed=SEED, gids=gids, quiesce=True)
+    orc.setup_steady(0)
+    for r in range(rounds):
+        act = workload.active_groups(n, SEED, r, 10000, gids=gids)
+        counts, ents, pool = workload.build_batch(n, 1, SEED, r, 256, vlen,
+                                                  groups=act, gids=gids)
+        orc.stage_proposals(counts, 1, ents, pool)
+        eng.gen_kv_proposals(r % 2, 1, 256, vlen, SEED, r, active_ppm=10000)
+        o = orc.round(tick=True)
+        e = eng.step(tick=True, prop_slot=r % 2, encode_saves=True,
+                     listed=True)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        if r % 60 == 59 or r == rounds - 1:
+            errs = _compare(eng, orc, gids, R, saves=True)
+            assert not errs, (r, errs[:3])
+    qs = sum(orc.export(i, s).qs_quiesced_since > 0
+             for i in range(n) for s in range(R))
+    if rounds > 220:
+        assert qs > 0  # some sampled groups went quiet past the threshold

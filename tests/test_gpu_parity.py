@@ -327,3 +327,41 @@ def test_follower_read_index(R, at):
         errs = p.check()
         assert not errs, (r, errs[:2])
     assert total >= p.G * 8
+
+
+@pytest.mark.gpu
+def test_apply_results_and_durable_commit():
+    """drb_apply_results: per applied entry the Key / ClientID / SeriesID
+    and KVTest's Result.Value = len(payload) (kvtest.go:161) that
+    pendingProposals.applied completes the proposal with (node.go:243-257),
+    checked against the entries the oracle applied (its log from the
+    previous sm index).  drb_commit_round gates the next round under a
+    durable LogDB (engine.go:1343-1359)."""
+    from dragonboat_amd.engine import DrbError
+    p = Pair(G=32, R=3, durable_log=1)
+    seen = 0
+    for r in range(8):
+        prev = {(g, s): p.orc.export(g, s).sm_index
+                for g in range(p.G) for s in range(3)}
+        o, e = p.round(k=1 if r % 3 else 2, tick=(r % 2 == 0))
+        assert e.fallbacks == 0 and e.errors == 0
+        for s in range(3):
+            got = p.eng.apply_results(s)
+            exp = []
+            for g in range(p.G):
+                now = p.orc.export(g, s).sm_index
+                for t in p.orc.export_log(g, s, prev[(g, s)] + 1, now):
+                    term, index, typ, key, cid, sid, _, cmd = t
+                    ign = int(cid == 0)
+                    val = 0 if ign else (len(cmd) - 1 if typ == 2 else
+                                         len(cmd))
+                    exp.append((g, index, key, cid, sid, val, ign))
+            assert got == exp, (r, s, got[:3], exp[:3])
+            seen += len(got)
+        # the next round waits for this one's persistence
+        with pytest.raises(DrbError):
+            p.eng.step(tick=False)
+        p.eng.commit_round(p.eng.round)
+        assert p.eng.committed_round == p.eng.round
+        assert not p.check()
+    assert seen > 3 * p.G * 6

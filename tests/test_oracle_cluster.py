@@ -207,3 +207,28 @@ def test_nodes_exit_quiesce_by_proposal_and_read_index():
         for _ in range(4):
             c.round(tick=True)
         assert not any(_quiesced(c)), how
+
+
+def test_sampled_cluster_matches_full_cluster():
+    """A cluster simulating only some global group ids (the full-size
+    parity tests' oracle) steps those groups exactly like a cluster of
+    all the groups does: groups are independent."""
+    G, gids, seed = 40, [0, 3, 17, 39], 0x5EEDD8B0
+    full = po.Cluster(G, 3, seed=seed)
+    samp = po.Cluster(len(gids), 3, seed=seed, gids=gids)
+    full.setup_steady(0)
+    samp.setup_steady(0)
+    for r in range(12):
+        for c, n, kw in ((full, G, {}), (samp, len(gids), {"gids": gids})):
+            counts, ents, pool = workload.build_batch(n, 1, seed, r, **kw)
+            c.stage_proposals(counts, 1, ents, pool)
+            if r % 3 == 1:
+                lo, hi = workload.build_read_index(n, seed, r, r + 30, **kw)
+                c.stage_read_index(lo, hi)
+            c.round(tick=(r % 2 == 0))
+        for i, g in enumerate(gids):
+            for s in range(3):
+                a, b = full.export(g, s), samp.export(i, s)
+                assert a.to_dict(3) == b.to_dict(3), (r, g, s)
+                assert full.export_outbox(g, s) == samp.export_outbox(i, s)
+                assert full.export_kv(g, s) == samp.export_kv(i, s)
