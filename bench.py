@@ -104,6 +104,8 @@ def parse():
     ap.add_argument("--no-wire", action="store_true",
                     help="skip the off-GPU wire encode measurement (C3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="skip the receiving-side wire ingest measurement")
     return ap.parse_args()
 
 
@@ -342,6 +344,34 @@ def main():
                 "note": "median of %d drb_encode_wire calls (5 kernels + one "
                         "host sync for the plan), outside the timed "
                         "region" % reps}
+        if not args.no_ingest and world == 1:
+            # the receiving NodeHost: a second engine hosting the follower
+            # slot only takes that stream in (drb_ingest_wire: frame and
+            # payload CRCs, MessageBatch / Message / Entry decode, batched
+            # placement into the next round's mailbox)
+            _, stream = eng.encode_wire(0, 1, 1, b"10.0.0.1:26001")
+            rx = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                        max_props=1, prop_slots=1, ri_slots=1, mailbox=16,
+                        kv_slots=8, kv_val_cap=4, first_shard_id=first_shard,
+                        device=local)
+            rx.init_steady(term=2, leader_slot=0, seed=seed)
+            rx.host_slot(0, False)
+            rx.sync()
+            i0 = time.perf_counter()
+            res = rx.ingest_wire(stream, deployment_id=1)
+            rx.sync()
+            ims = (time.perf_counter() - i0) * 1e3
+            wire["ingest"] = {
+                "messages": res["messages"], "accepted": res["accepted"],
+                "dropped": res["dropped"], "ms": ims,
+                "messages_per_s": res["messages"] / (ims * 1e-3),
+                "GB_per_s": len(stream) / (ims * 1e-3) / 1e9,
+                "note": "drb_ingest_wire of that stream into a second "
+                        "engine hosting replica slot 1 (host decode, one "
+                        "batched device placement), outside the timed "
+                        "region"}
+            rx.close()
+            del stream
     # the replicas that left the fast path during the run, by reason
     # (drb_take_flagged): a run with any is not a pure fast-path number
     from dragonboat_amd import abi as _abi

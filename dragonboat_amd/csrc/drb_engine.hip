@@ -823,6 +823,21 @@ extern "C" int drb_init_steady(drb_engine *e, uint64_t term,
   return refresh_roles(e);
 }
 
+__global__ void k_host_slot(View v, uint32_t slot, uint32_t hosted) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G || gid(v, slot, g) >= v.total_groups) return;
+  uint32_t &f = v.u32[u32_ix(v, W_FLAGS, slot, g)];
+  f = hosted ? (f | DRB_F_HOSTED) : (f & ~(DRB_F_HOSTED | F_AT_REST));
+}
+
+extern "C" int drb_host_slot(drb_engine *e, uint32_t slot, int hosted) {
+  if (!e || slot >= e->v.R) return DRB_EINVAL;
+  k_host_slot<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
+      e->v, slot, hosted ? 1u : 0u);
+  HIPCHK(hipGetLastError());
+  return refresh_roles(e);
+}
+
 // ---------------------------------------------------------------- inputs
 extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
                                    const uint32_t *counts,
@@ -1028,6 +1043,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   std::unordered_map<uint64_t, uint32_t> pid;  // (g, from, to) -> plane
   std::vector<InPlane> planes;
   std::vector<uint32_t> mplane(n, ~0u);
+  uint64_t last_key = ~0ull;
+  uint32_t last_plane = 0;
   size_t q = 0;
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) {
@@ -1048,12 +1065,18 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     const uint64_t g = m.shard_id - v.first_shard_id;
     const uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
     const uint64_t key = (g * v.R + from) * v.R + to;
+    if (key == last_key) {  // a transport batch keeps a group's messages
+      mplane[i] = last_plane;  // together
+      continue;
+    }
     auto it = pid.find(key);
     if (it == pid.end()) {
       it = pid.emplace(key, (uint32_t)planes.size()).first;
       planes.push_back(InPlane{g, from, to, make_uint4(0, 0, 0, 0), 0, false});
     }
     mplane[i] = it->second;
+    last_key = key;
+    last_plane = it->second;
   }
   std::vector<uint64_t> hidx, xidx;
   for (const InPlane &pl : planes) {

@@ -42,6 +42,7 @@ SIGNATURES = {
     "drb_export_log": (C.c_int, [P, U64, U32, U64, U64, C.POINTER(Entry),
                                  PU8, SZ]),
     "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
+    "drb_host_slot": (C.c_int, [P, U32, C.c_int]),
     "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
     "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
@@ -210,6 +211,10 @@ class Engine:
         _ck(lib().drb_export_log(self.h, g, slot, lo, hi, arr, pool, pcap),
             "drb_export_log")
         return [entry_to_tuple(arr[i], pool) for i in range(n)]
+
+    def host_slot(self, slot, hosted):
+        _ck(lib().drb_host_slot(self.h, slot, int(bool(hosted))),
+            "drb_host_slot")
 
     def init_steady(self, term=2, leader_slot=0, seed=0x5EEDD8B0):
         _ck(lib().drb_init_steady(self.h, term, leader_slot, seed),

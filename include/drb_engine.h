@@ -388,6 +388,12 @@ int drb_export_log(drb_engine *e, uint64_t group, uint32_t slot, uint64_t lo,
                    uint64_t hi, drb_entry *out, uint8_t *pool,
                    size_t pool_cap);
 
+/* Which replicas this engine steps: replica slot `slot` of every group is
+ * hosted here (1) or lives on another NodeHost (0), whose messages arrive
+ * through drb_ingest / drb_ingest_wire (NodeHost.StartReplica /
+ * StopReplica for one replica of every shard, nodehost.go). */
+int drb_host_slot(drb_engine *e, uint32_t slot, int hosted);
+
 /* Device-side initialisation of every group to the post-election steady
  * state: bootstrap (peer.go:404-428) with R config-change entries at term
  * 1, replica `leader_slot` elected at `term` (raft.go:1176, 1038) and its

@@ -18,6 +18,9 @@
  *   handleEntry/update/noop      statemachine.go:935-1103
  *   setApplied/setLastApplied    statemachine.go:716-760
  *   GetPayload/getDecodedPayload internal/rsm/encoded.go:55-170
+ *   snappy block decode          github.com/golang/snappy v0.0.4 (go.mod:8,
+ *                                not vendored; dio.DecompressSnappyBlock
+ *                                internal/utils/dio/io.go:199-209)
  *   KVTest.Update                internal/tests/kvtest.go:145-162,311
  *   pb.EntriesToApply            raftpb/entry.go:27-47
  */
@@ -197,6 +200,114 @@ static void sm_set_applied(orc_node *n, uint64_t index, uint64_t term) {
   n->sm_term = term;
 }
 
+/* golang/snappy v0.0.4 Decode, restated from the published block format
+ * (the module is a go.mod dependency absent from /root/reference): a
+ * uvarint decoded length, then literal (tag&3 == 0) and copy elements with
+ * 1-, 2- or 4-byte offsets.  dlen is the exact decoded length
+ * (DecompressSnappyBlock panics on a mismatch).  0 ok, -1 corrupt. */
+static int snappy_decode(const uint8_t *s, size_t n, uint8_t *d, size_t dlen) {
+  size_t i = 0, o = 0;
+  uint64_t want = 0;
+  for (int sh = 0;; sh += 7) {
+    if (i >= n || sh > 63) return -1;
+    uint8_t b = s[i++];
+    want |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) break;
+  }
+  if (want != dlen) orc_panic("corrupted decodedLen in header");
+  while (i < n) {
+    uint8_t tag = s[i++];
+    size_t len, off;
+    switch (tag & 3) {
+      case 0: {
+        len = tag >> 2;
+        if (len >= 60) {
+          size_t nb = len - 59;
+          if (i + nb > n) return -1;
+          len = 0;
+          for (size_t k = 0; k < nb; k++) len |= (size_t)s[i + k] << (8 * k);
+          i += nb;
+        }
+        len += 1;
+        if (len > n - i || len > dlen - o) return -1;
+        memcpy(d + o, s + i, len);
+        i += len;
+        o += len;
+        continue;
+      }
+      case 1:
+        if (i >= n) return -1;
+        len = 4 + ((tag >> 2) & 7);
+        off = ((size_t)(tag >> 5) << 8) | s[i++];
+        break;
+      case 2:
+        if (i + 2 > n) return -1;
+        len = 1 + (tag >> 2);
+        off = (size_t)s[i] | ((size_t)s[i + 1] << 8);
+        i += 2;
+        break;
+      default:
+        if (i + 4 > n) return -1;
+        len = 1 + (tag >> 2);
+        off = (size_t)s[i] | ((size_t)s[i + 1] << 8) |
+              ((size_t)s[i + 2] << 16) | ((size_t)s[i + 3] << 24);
+        i += 4;
+        break;
+    }
+    if (off == 0 || off > o || len > dlen - o) return -1;
+    for (size_t k = 0; k < len; k++, o++) d[o] = d[o - off]; /* may overlap */
+  }
+  return o == dlen ? 0 : -1;
+}
+
+/* GetPayload (encoded.go:55-66) -> getDecodedPayload (encoded.go:127-160).
+ * *owned receives a malloc'd buffer when the payload was decompressed. */
+static const uint8_t *get_payload(uint32_t type, const uint8_t *cmd,
+                                  uint32_t clen, uint32_t *plen,
+                                  uint8_t **owned) {
+  *owned = NULL;
+  switch (type) {
+    case DRB_ENTRY_APPLICATION:
+    case DRB_ENTRY_CONFIG_CHANGE:
+      *plen = clen;
+      return clen ? cmd : NULL;
+    case DRB_ENTRY_ENCODED:
+      break;
+    default:
+      orc_panic("unknown entry type");
+  }
+  if (clen == 0) orc_panic("index out of range [0] with length 0");
+  uint8_t h = cmd[0]; /* parseEncodedHeader (encoded.go:119-125) */
+  uint8_t ver = h & 0xf0, ct = h & 0x0e;
+  if (ver != 0) orc_panic("unknown cmd encoding version");
+  if (h & 1) orc_panic("v0 cmd has session info");
+  if (ct == 0) { /* getV0NoCompressPayload (encoded.go:162-164) */
+    *plen = clen - 1;
+    return cmd + 1;
+  }
+  if (ct != 2) orc_panic("unknown compression type %d", ct);
+  /* getV0PayloadUncompressedSize (encoded.go:166-168): binary.Uvarint */
+  uint64_t sz = 0;
+  int ok = 0;
+  for (uint32_t i = 1, sh = 0; i < clen && i <= 10; i++, sh += 7) {
+    sz |= (uint64_t)(cmd[i] & 0x7f) << sh;
+    if (!(cmd[i] & 0x80)) {
+      ok = 1;
+      break;
+    }
+  }
+  if (!ok) sz = 0; /* Uvarint n <= 0: size 0 */
+  if (sz == 0) orc_panic("empty uncompressed size found");
+  uint8_t *buf = (uint8_t *)malloc((size_t)sz);
+  if (snappy_decode(cmd + 1, clen - 1, buf, (size_t)sz)) {
+    free(buf);
+    orc_panic("snappy: corrupt input"); /* the apply error stops the node */
+  }
+  *owned = buf;
+  *plen = (uint32_t)sz;
+  return buf;
+}
+
 static int entry_is_session_managed(const orc_entry *e) {
   /* IsSessionManaged (raftpb/raft.go:90-99) */
   if (e->type == DRB_ENTRY_CONFIG_CHANGE) return 0;
@@ -228,36 +339,23 @@ static int sm_handle_entry(orc_node *n, const orc_entry *e) {
     orc_panic("session management is not on the fast path");
   if (e->series_id != 0)
     orc_panic("regular client sessions are not on the fast path");
-  /* update(): NoOP session -> GetPayload -> sm.Update; setApplied deferred */
-  const uint8_t *payload;
+  /* update(): NoOP session -> GetPayload -> sm.Update; setApplied deferred.
+   * (The GPU path falls back before appending a Snappy entry; the oracle
+   * decodes it, as the CPU raft.Peer + rsm would.) */
+  uint8_t *owned;
   uint32_t plen;
-  switch (e->type) {
-    case DRB_ENTRY_APPLICATION:
-      payload = clen ? e->cmd->data : NULL;
-      plen = clen;
-      break;
-    case DRB_ENTRY_ENCODED: {
-      if (clen == 0) orc_panic("index out of range [0] with length 0");
-      uint8_t h = e->cmd->data[0];
-      uint8_t ver = h & 0xf0, ct = h & 0x0e;
-      int has_session = (h & 1) == 1;
-      if (ver != 0) orc_panic("unknown cmd encoding version");
-      if (has_session) orc_panic("v0 cmd has session info");
-      if (ct != 0) orc_panic("compressed payload is not on the fast path");
-      payload = e->cmd->data + 1;
-      plen = clen - 1;
-      break;
-    }
-    default:
-      orc_panic("unknown entry type");
-  }
+  const uint8_t *payload = get_payload(e->type, clen ? e->cmd->data : NULL,
+                                       clen, &plen, &owned);
   /* KVTest.Update */
   n->kv.count++;
   const uint8_t *k, *v;
   uint32_t kl, vl;
-  if (orc_pbkv_unmarshal(payload, plen, &k, &kl, &v, &vl))
+  if (orc_pbkv_unmarshal(payload, plen, &k, &kl, &v, &vl)) {
+    free(owned);
     orc_panic("PBKV unmarshal failed");
+  }
   kv_update_store(&n->kv, k, kl, v, vl);
+  free(owned);
   sm_set_applied(n, e->index, e->term);
   return 1;
 }
@@ -1073,6 +1171,78 @@ int orc_cluster_kv_lookup(orc_cluster *c, uint64_t g, uint32_t slot,
                           const uint8_t *key, uint32_t klen, uint8_t *val,
                           uint32_t cap, uint32_t *vlen) {
   const kv_item *it = kv_find(&node_at(c, g, slot)->kv, key, klen);
+  if (!it) return 1;
+  *vlen = it->vlen;
+  if (it->vlen > cap) return -1;
+  memcpy(val, it->val, it->vlen);
+  return 0;
+}
+
+/* ---- rsm KAT hooks (internal/rsm/statemachine_test.go, encoded_test.go) */
+/* GetPayload: payload length copied to out; -1 panic, -3 out of capacity */
+long orc_get_payload(uint32_t type, const uint8_t *cmd, size_t clen,
+                     uint8_t *out, size_t cap) {
+  ORC_TRY(-1);
+  uint8_t *owned;
+  uint32_t plen;
+  const uint8_t *p = get_payload(type, cmd, (uint32_t)clen, &plen, &owned);
+  long rc = plen > cap ? -3 : (long)plen;
+  if (rc >= 0 && plen) memcpy(out, p, plen);
+  free(owned);
+  ORC_END;
+  return rc;
+}
+
+/* A StateMachine over KVTest with sm.lastApplied.index = sm.index =
+ * applied (the tests' setup, statemachine_test.go:348-349). */
+void *orc_sm_new(uint64_t applied_index, uint64_t applied_term) {
+  orc_node *n = (orc_node *)calloc(1, sizeof(orc_node));
+  n->sm_index = n->la_index = applied_index;
+  n->sm_term = n->la_term = applied_term;
+  return n;
+}
+
+void orc_sm_free(void *h) {
+  orc_node *n = (orc_node *)h;
+  if (!n) return;
+  kv_free(&n->kv);
+  ev_free(&n->applyq);
+  free(n);
+}
+
+/* taskQ.Add(Task{Entries}) + Handle (statemachine.go:599-645).  Returns
+ * the number of entries that reached KVTest.Update; -1 panic. */
+long orc_sm_handle(void *h, const drb_entry *ents, size_t cnt,
+                   const uint8_t *pool) {
+  orc_node *n = (orc_node *)h;
+  for (size_t i = 0; i < cnt; i++) {
+    orc_entry e = entry_from_view(&ents[i], pool);
+    ev_push(&n->applyq, &e);
+    blob_unref(e.cmd);
+  }
+  drb_round_out out;
+  memset(&out, 0, sizeof(out));
+  jmp_buf jb;
+  jmp_buf *prev = orc_jb;
+  orc_jb = &jb;
+  if (setjmp(jb)) {
+    orc_jb = prev;
+    ev_truncate(&n->applyq, 0);
+    return -1;
+  }
+  sm_handle(n, 1, &out);
+  orc_jb = prev;
+  return (long)out.committed_entries;
+}
+
+/* GetLastApplied (statemachine.go:380-385) and KVTest.Count */
+uint64_t orc_sm_last_applied(void *h) { return ((orc_node *)h)->la_index; }
+uint64_t orc_sm_count(void *h) { return ((orc_node *)h)->kv.count; }
+
+/* Lookup (kvtest.go:120-130): 0 found, 1 missing, -1 out of capacity */
+int orc_sm_lookup(void *h, const uint8_t *key, uint32_t klen, uint8_t *val,
+                  uint32_t cap, uint32_t *vlen) {
+  const kv_item *it = kv_find(&((orc_node *)h)->kv, key, klen);
   if (!it) return 1;
   *vlen = it->vlen;
   if (it->vlen > cap) return -1;

@@ -248,6 +248,42 @@ int orc_log_append(orc_raft *r, const drb_entry *ents, size_t n,
 int orc_log_commit_update(orc_raft *r, uint64_t stable_log_to,
                           uint64_t stable_log_term, uint64_t processed,
                           uint64_t last_applied);
+/* raft KAT hooks (raft_test.go:1578-1611, 2952-3037) */
+long orc_raft_make_replicate(orc_raft *r, uint64_t to, uint64_t next,
+                             uint64_t max_size, drb_message *out,
+                             drb_entry *ents, size_t ent_cap, uint8_t *pool,
+                             size_t pool_cap);
+int orc_raft_append_entries(orc_raft *r, const drb_entry *ents, size_t n,
+                            const uint8_t *pool);
+int orc_raft_broadcast_heartbeat_hint(orc_raft *r, uint64_t low,
+                                      uint64_t high);
+int orc_raft_has_committed_entry_at_current_term(orc_raft *r);
+size_t orc_raft_read_index_len(orc_raft *r);
+
+/* ---- inMemory (inmemory.go) : KAT hooks (inmemory_test.go:260-548) ---- */
+orc_inmem *orc_inmem_new(uint64_t marker_index, const drb_entry *ents,
+                         size_t n, uint64_t saved_to, int shrunk);
+void orc_inmem_free(orc_inmem *im);
+int orc_inmem_merge(orc_inmem *im, const drb_entry *ents, size_t n);
+int orc_inmem_saved_log_to(orc_inmem *im, uint64_t index, uint64_t term);
+int orc_inmem_applied_log_to(orc_inmem *im, uint64_t index);
+void orc_inmem_restore(orc_inmem *im, uint64_t ss_index, uint64_t ss_term);
+long orc_inmem_entries_to_save(orc_inmem *im, uint64_t *first);
+int orc_inmem_last_index(orc_inmem *im, uint64_t *idx);
+int orc_inmem_get_term(orc_inmem *im, uint64_t index, uint64_t *term);
+void orc_inmem_info(orc_inmem *im, uint64_t *out5);
+
+/* ---- rsm (statemachine.go, encoded.go) : KAT hooks -------------------- */
+long orc_get_payload(uint32_t type, const uint8_t *cmd, size_t clen,
+                     uint8_t *out, size_t cap);
+void *orc_sm_new(uint64_t applied_index, uint64_t applied_term);
+void orc_sm_free(void *h);
+long orc_sm_handle(void *h, const drb_entry *ents, size_t cnt,
+                   const uint8_t *pool);
+uint64_t orc_sm_last_applied(void *h);
+uint64_t orc_sm_count(void *h);
+int orc_sm_lookup(void *h, const uint8_t *key, uint32_t klen, uint8_t *val,
+                  uint32_t cap, uint32_t *vlen);
 
 /* ---- BSP cluster: node_test.go step() over G groups x R replicas ------ */
 typedef struct orc_cluster orc_cluster;

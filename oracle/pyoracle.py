@@ -119,6 +119,30 @@ def _declare(L):
         "orc_log_try_append": (C.c_int, [P, U64, PE, C.c_size_t, PU8]),
         "orc_log_append": (C.c_int, [P, PE, C.c_size_t, PU8]),
         "orc_log_commit_update": (C.c_int, [P, U64, U64, U64, U64]),
+        "orc_raft_make_replicate": (C.c_long, [P, U64, U64, U64, PM, PE,
+                                               C.c_size_t, PU8, C.c_size_t]),
+        "orc_raft_append_entries": (C.c_int, [P, PE, C.c_size_t, PU8]),
+        "orc_raft_has_committed_entry_at_current_term": (C.c_int, [P]),
+        "orc_raft_broadcast_heartbeat_hint": (C.c_int, [P, U64, U64]),
+        "orc_raft_read_index_len": (C.c_size_t, [P]),
+        "orc_inmem_new": (P, [U64, PE, C.c_size_t, U64, C.c_int]),
+        "orc_inmem_free": (None, [P]),
+        "orc_inmem_merge": (C.c_int, [P, PE, C.c_size_t]),
+        "orc_inmem_saved_log_to": (C.c_int, [P, U64, U64]),
+        "orc_inmem_applied_log_to": (C.c_int, [P, U64]),
+        "orc_inmem_restore": (None, [P, U64, U64]),
+        "orc_inmem_entries_to_save": (C.c_long, [P, PU64]),
+        "orc_inmem_last_index": (C.c_int, [P, PU64]),
+        "orc_inmem_get_term": (C.c_int, [P, U64, PU64]),
+        "orc_inmem_info": (None, [P, PU64]),
+        "orc_get_payload": (C.c_long, [U32, PU8, C.c_size_t, PU8,
+                                       C.c_size_t]),
+        "orc_sm_new": (P, [U64, U64]),
+        "orc_sm_free": (None, [P]),
+        "orc_sm_handle": (C.c_long, [P, PE, C.c_size_t, PU8]),
+        "orc_sm_last_applied": (U64, [P]),
+        "orc_sm_count": (U64, [P]),
+        "orc_sm_lookup": (C.c_int, [P, PU8, U32, PU8, U32, PU32]),
         "orc_cluster_new": (P, [C.POINTER(ClusterCfg)]),
         "orc_cluster_free": (None, [P]),
         "orc_cluster_setup_steady": (C.c_int, [P, U32]),
@@ -500,6 +524,33 @@ class TestRaft:
                                            stable_log_term, processed,
                                            last_applied))
 
+    # raft KAT hooks (raft_test.go:1578-1611, 2952-3037)
+    def make_replicate(self, to, next, max_size):
+        """makeReplicateMessage(to, next, maxSize) (raft.go:738-769)."""
+        marr, earr = (Message * 1)(), (Entry * 4096)()
+        pool = (C.c_uint8 * (1 << 20))()
+        n = _check(lib().orc_raft_make_replicate(self.p, to, next, max_size,
+                                                 marr, earr, 4096, pool,
+                                                 1 << 20))
+        if n < 0:
+            raise OracleError("makeReplicateMessage failed %d" % n)
+        return _unpack_messages(marr, 1, earr, pool)[0]
+
+    def append_entries(self, entries):
+        """raft.appendEntries (raft.go:944-955)."""
+        arr, pool, n = EntryPool(entries).arrays()
+        _check(lib().orc_raft_append_entries(self.p, arr, n, pool))
+
+    def broadcast_heartbeat_hint(self, ctx):
+        _check(lib().orc_raft_broadcast_heartbeat_hint(self.p, ctx[0], ctx[1]))
+
+    def has_committed_entry_at_current_term(self):
+        return bool(_check(
+            lib().orc_raft_has_committed_entry_at_current_term(self.p)))
+
+    def read_index_len(self):
+        return lib().orc_raft_read_index_len(self.p)
+
     @property
     def committed(self):
         return self.info().committed
@@ -800,3 +851,96 @@ def wire_frame(payload):
     out = (C.c_uint8 * (len(payload) + 20))()
     n = lib().orc_wire_frame(_u8(payload), len(payload), out)
     return bytes(out[:n])
+
+
+# ---------------------------------------------------------------- inMemory
+class InMem:
+    """inMemory (internal/raft/inmemory.go) built the way the reference's
+    tests build it: markerIndex, entries, savedTo, shrunk."""
+
+    def __init__(self, marker_index, entries=(), saved_to=0, shrunk=False):
+        arr, _, n = EntryPool(entries).arrays()
+        self.p = lib().orc_inmem_new(marker_index, arr, n, saved_to,
+                                     int(shrunk))
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_inmem_free(self.p)
+
+    def merge(self, entries):
+        arr, _, n = EntryPool(entries).arrays()
+        _check(lib().orc_inmem_merge(self.p, arr, n))
+
+    def saved_log_to(self, index, term):
+        _check(lib().orc_inmem_saved_log_to(self.p, index, term))
+
+    def applied_log_to(self, index):
+        _check(lib().orc_inmem_applied_log_to(self.p, index))
+
+    def restore(self, index, term):
+        lib().orc_inmem_restore(self.p, index, term)
+
+    def entries_to_save(self):
+        """(count, first index)"""
+        f = U64()
+        n = lib().orc_inmem_entries_to_save(self.p, f)
+        return n, f.value
+
+    def last_index(self):
+        v = U64()
+        ok = lib().orc_inmem_last_index(self.p, v)
+        return v.value, bool(ok)
+
+    def term(self, index):
+        v = U64()
+        ok = _check(lib().orc_inmem_get_term(self.p, index, v))
+        return v.value, bool(ok)
+
+    def info(self):
+        o = (U64 * 5)()
+        lib().orc_inmem_info(self.p, o)
+        return dict(marker_index=o[0], saved_to=o[1], shrunk=bool(o[2]),
+                    n=o[3], first=o[4])
+
+
+# ---------------------------------------------------------------- rsm
+def get_payload(type, cmd):
+    """GetPayload (internal/rsm/encoded.go:55-66)."""
+    out = (C.c_uint8 * (len(cmd) * 64 + 1024))()
+    n = _check(lib().orc_get_payload(type, _u8(cmd), len(cmd), out,
+                                     len(out)))
+    if n < 0:
+        raise OracleError("GetPayload failed %d" % n)
+    return bytes(out[:n])
+
+
+class StateMachine:
+    """StateMachine over KVTest with sm.lastApplied.index = sm.index =
+    applied (internal/rsm/statemachine_test.go:348-349)."""
+
+    def __init__(self, applied_index=0, applied_term=0):
+        self.p = lib().orc_sm_new(applied_index, applied_term)
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_sm_free(self.p)
+
+    def handle(self, entries):
+        """taskQ.Add(Task{Entries}) + Handle; returns the number of entries
+        that reached the user state machine's Update."""
+        arr, pool, n = EntryPool(entries).arrays()
+        return _check(lib().orc_sm_handle(self.p, arr, n, pool))
+
+    @property
+    def last_applied(self):
+        return lib().orc_sm_last_applied(self.p)
+
+    @property
+    def count(self):
+        return lib().orc_sm_count(self.p)
+
+    def lookup(self, key):
+        buf = (C.c_uint8 * 4096)()
+        vl = U32()
+        rc = lib().orc_sm_lookup(self.p, _u8(key), len(key), buf, 4096, vl)
+        return None if rc else bytes(buf[:vl.value])

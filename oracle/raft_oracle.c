@@ -1038,13 +1038,12 @@ static orc_msg new_msg(uint32_t type, uint64_t to) {
 
 /* makeReplicateMessage (raft.go:738-769); returns log error code */
 static int raft_make_replicate(orc_raft *r, uint64_t to, uint64_t next,
-                               orc_msg *m) {
+                               uint64_t max_size, orc_msg *m) {
   uint64_t term;
   int err = log_term(&r->log, next - 1, &term);
   if (err) return err;
   orc_evec ents = {0};
-  err = log_entries(&r->log, next, 64ull * 1024 * 1024 /* maxEntrySize */,
-                    &ents);
+  err = log_entries(&r->log, next, max_size, &ents);
   if (err) {
     ev_free(&ents);
     return err;
@@ -1070,7 +1069,8 @@ static void raft_send_replicate(orc_raft *r, uint64_t to) {
   orc_remote *rp = &r->rem[i];
   if (remote_is_paused(rp)) return;
   orc_msg m;
-  int err = raft_make_replicate(r, to, rp->next, &m);
+  int err = raft_make_replicate(r, to, rp->next,
+                                64ull * 1024 * 1024 /* maxEntrySize */, &m);
   if (err) {
     /* log compacted: InstallSnapshot path -- not on this path */
     orc_panic("snapshot required for replica %llu (not on the fast path)",
@@ -2193,6 +2193,160 @@ int orc_log_commit_update(orc_raft *r, uint64_t stable_log_to,
                     last_applied);
   ORC_END;
   return 0;
+}
+
+/* makeReplicateMessage with an explicit maxSize (raft_test.go:1578-1611).
+ * Returns the entry count; -1 panic, -2 log error, -3 out of capacity. */
+long orc_raft_make_replicate(orc_raft *r, uint64_t to, uint64_t next,
+                             uint64_t max_size, drb_message *out,
+                             drb_entry *ents, size_t ent_cap, uint8_t *pool,
+                             size_t pool_cap) {
+  ORC_TRY(-1);
+  orc_msg m;
+  long rc;
+  if (raft_make_replicate(r, to, next, max_size, &m)) {
+    rc = -2;
+  } else {
+    size_t eu = 0, pu = 0;
+    rc = msg_to_view(&m, out, ents, ent_cap, &eu, pool, pool_cap, &pu)
+             ? -3
+             : (long)m.ents.n;
+    msg_free(&m);
+  }
+  ORC_END;
+  return rc;
+}
+
+/* raft.appendEntries (raft.go:944-955) */
+int orc_raft_append_entries(orc_raft *r, const drb_entry *ents, size_t n,
+                            const uint8_t *pool) {
+  orc_evec tmp = {0};
+  views_to_evec(ents, n, pool, &tmp);
+  jmp_buf jb;
+  jmp_buf *prev = orc_jb;
+  orc_jb = &jb;
+  if (setjmp(jb)) {
+    orc_jb = prev;
+    ev_free(&tmp);
+    return -1;
+  }
+  raft_append_entries(r, tmp.v, tmp.n);
+  orc_jb = prev;
+  ev_free(&tmp);
+  return 0;
+}
+
+/* broadcastHeartbeatMessageWithHint (raft.go:859-867) */
+int orc_raft_broadcast_heartbeat_hint(orc_raft *r, uint64_t low,
+                                      uint64_t high) {
+  ORC_TRY(-1);
+  orc_ctx ctx = {low, high};
+  raft_broadcast_heartbeat_hint(r, ctx);
+  ORC_END;
+  return 0;
+}
+
+/* hasCommittedEntryAtCurrentTerm (raft.go:1818-1827) */
+int orc_raft_has_committed_entry_at_current_term(orc_raft *r) {
+  ORC_TRY(-1);
+  int ok = raft_has_committed_at_term(r);
+  ORC_END;
+  return ok;
+}
+
+/* readIndex.pending / queue sizes: one queue in this restatement, so both
+ * lengths are the same (readindex.go:32-36) */
+size_t orc_raft_read_index_len(orc_raft *r) { return r->ri.n; }
+
+/* ---- inMemory KAT hooks (inmemory_test.go:260-548) ------------------ */
+/* restore (inmemory.go:232-243); the snapshot record itself is not kept */
+static void im_restore(orc_inmem *im, uint64_t ss_index, uint64_t ss_term) {
+  im->marker_index = ss_index + 1;
+  im->applied_to_index = ss_index;
+  im->applied_to_term = ss_term;
+  im->shrunk = 0;
+  ev_truncate(&im->ents, 0);
+  im->saved_to = ss_index;
+}
+
+orc_inmem *orc_inmem_new(uint64_t marker_index, const drb_entry *ents,
+                         size_t n, uint64_t saved_to, int shrunk) {
+  orc_inmem *im = (orc_inmem *)calloc(1, sizeof(orc_inmem));
+  im->marker_index = marker_index;
+  im->saved_to = saved_to;
+  im->shrunk = shrunk;
+  views_to_evec(ents, n, NULL, &im->ents);
+  return im;
+}
+
+void orc_inmem_free(orc_inmem *im) {
+  if (!im) return;
+  ev_free(&im->ents);
+  free(im);
+}
+
+int orc_inmem_merge(orc_inmem *im, const drb_entry *ents, size_t n) {
+  orc_evec tmp = {0};
+  views_to_evec(ents, n, NULL, &tmp);
+  jmp_buf jb;
+  jmp_buf *prev = orc_jb;
+  orc_jb = &jb;
+  if (setjmp(jb)) {
+    orc_jb = prev;
+    ev_free(&tmp);
+    return -1;
+  }
+  im_merge(im, tmp.v, tmp.n);
+  orc_jb = prev;
+  ev_free(&tmp);
+  return 0;
+}
+
+int orc_inmem_saved_log_to(orc_inmem *im, uint64_t index, uint64_t term) {
+  ORC_TRY(-1);
+  im_saved_log_to(im, index, term);
+  ORC_END;
+  return 0;
+}
+
+int orc_inmem_applied_log_to(orc_inmem *im, uint64_t index) {
+  ORC_TRY(-1);
+  im_applied_log_to(im, index);
+  ORC_END;
+  return 0;
+}
+
+void orc_inmem_restore(orc_inmem *im, uint64_t ss_index, uint64_t ss_term) {
+  im_restore(im, ss_index, ss_term);
+}
+
+/* entriesToSave: count, first index in *first (0 when none) */
+long orc_inmem_entries_to_save(orc_inmem *im, uint64_t *first) {
+  size_t n;
+  const orc_entry *e = im_entries_to_save(im, &n);
+  *first = n ? e[0].index : 0;
+  return (long)n;
+}
+
+/* getLastIndex / getTerm: 1 ok, 0 not found, -1 panic */
+int orc_inmem_last_index(orc_inmem *im, uint64_t *idx) {
+  return im_last_index(im, idx);
+}
+
+int orc_inmem_get_term(orc_inmem *im, uint64_t index, uint64_t *term) {
+  ORC_TRY(-1);
+  int ok = im_get_term(im, index, term);
+  ORC_END;
+  return ok;
+}
+
+/* marker index, savedTo, shrunk, len(entries), entries[0].Index */
+void orc_inmem_info(orc_inmem *im, uint64_t *out5) {
+  out5[0] = im->marker_index;
+  out5[1] = im->saved_to;
+  out5[2] = (uint64_t)im->shrunk;
+  out5[3] = im->ents.n;
+  out5[4] = im->ents.n ? im->ents.v[0].index : 0;
 }
 
 /* helpers used by node_oracle.c */

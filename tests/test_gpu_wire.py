@@ -125,7 +125,7 @@ class TwoNodes:
     (drb_encode_wire -> drb_ingest_wire); one oracle cluster with every
     replica co-resident is the reference."""
 
-    def __init__(self, G, R=3, seed=0x5EEDD8B0, did=0xD1D):
+    def __init__(self, G, R=3, seed=0x5EEDD8B0, did=0xD1D, by_slot=False):
         from dragonboat_amd import abi
         from dragonboat_amd.engine import Engine
         self.G, self.R, self.seed, self.did = G, R, seed, did
@@ -135,6 +135,11 @@ class TwoNodes:
         self.foll = Engine(num_groups=G, num_replicas=R)
         for eng, mine in ((self.lead, {0}), (self.foll, set(range(1, R)))):
             eng.init_steady(term=2, leader_slot=0, seed=seed)
+            if by_slot:  # drb_host_slot: one call per slot, no round trip
+                for s in range(R):
+                    if s not in mine:
+                        eng.host_slot(s, False)
+                continue
             sts = eng.export_replicas(0, G)
             for i in range(len(sts)):
                 if i % R not in mine:
@@ -201,12 +206,13 @@ class TwoNodes:
         return errs
 
 
-@pytest.mark.parametrize("R", [3, 5])
-def test_two_nodehosts_over_the_wire(R):
+@pytest.mark.parametrize("R,by_slot", [(3, False), (5, False), (3, True)])
+def test_two_nodehosts_over_the_wire(R, by_slot):
     """Leaders on one engine, followers on another, every message crossing
     as dragonboat TCP bytes: bit-exact with one co-resident oracle cluster
-    (writes, ticks, ReadIndex)."""
-    t = TwoNodes(G=32, R=R)
+    (writes, ticks, ReadIndex).  by_slot: hosting set with drb_host_slot
+    instead of an export/import of every replica record."""
+    t = TwoNodes(G=32, R=R, by_slot=by_slot)
     for r in range(8):
         o, a, b = t.round(k=1 + (r % 3 == 2), tick=(r % 2 == 0),
                           read_index=(r % 3 == 1))

@@ -5,6 +5,8 @@ Sources (all in /root/reference/internal/raft):
   logentry_test.go         matchTerm / upToDate / getConflictIndex /
                            commitTo / commitUpdate tables
   readindex_test.go        readIndex queue / confirm KATs
+  raft_test.go:1578-1666   make / broadcast Replicate and Heartbeat
+  raft_test.go:2952-3037   ReadIndex handled by the leader
 They pin the oracle (oracle/*.c) to the reference's expected values; the
 oracle is then the checker for the GPU path (tests/test_gpu_*.py).
 """
@@ -391,3 +393,104 @@ def test_read_index_leader_can_be_confirmed():  # readindex_test.go:126-164
     assert ris[1] == (ctx(10001), 4, 3)
     assert ris[0] == (ctx(10002), 4, 1)
     assert len(r) == 1
+
+
+# ---- raft_test.go:1578-1666: make / broadcast Replicate and Heartbeat ----
+HEARTBEAT = MSG["Heartbeat"]
+READ_INDEX = MSG["ReadIndex"]
+ENTRY_NON_CMD_FIELDS_SIZE = 128  # settings.EntryNonCmdFieldsSize (soft.go)
+
+
+def size_upper_limit(cmd_len):  # Entry.SizeUpperLimit (raft_optimized.go:77)
+    return ENTRY_NON_CMD_FIELDS_SIZE + cmd_len
+
+
+def test_make_replicate_message():
+    # raft_test.go:1578-1611
+    r = po.TestRaft(1, [1, 2], 5, 1)
+    r.become_candidate()
+    r.become_leader()
+    r.append_entries([ent(index=2, term=1, cmd=bytes(16)),
+                      ent(index=3, term=1, cmd=bytes(16))])
+    sz = size_upper_limit(0) + 2 * size_upper_limit(16) + 1
+    m = r.make_replicate(2, 1, sz)
+    assert m["type"] == REPLICATE and m["to"] == 2
+    assert len(m["entries"]) == 3  # the NoOP plus the two above
+    m = r.make_replicate(2, 1, size_upper_limit(0) + size_upper_limit(16))
+    assert len(m["entries"]) == 2
+
+
+def test_broadcast_replicate_message():
+    # raft_test.go:1613-1627
+    r = po.TestRaft(1, [1, 2, 3], 5, 1)
+    r.become_candidate()
+    r.become_leader()
+    r.broadcast_replicate()
+    assert sum(m["type"] == REPLICATE for m in r.read_messages()) == 2
+
+
+def test_broadcast_heartbeat_message():
+    # raft_test.go:1629-1643
+    r = po.TestRaft(1, [1, 2, 3], 5, 1)
+    r.become_candidate()
+    r.become_leader()
+    r.broadcast_heartbeat()
+    assert sum(m["type"] == HEARTBEAT for m in r.read_messages()) == 2
+
+
+def test_broadcast_heartbeat_message_with_hint():
+    # raft_test.go:1645-1666
+    r = po.TestRaft(1, [1, 2, 3], 5, 1)
+    r.become_candidate()
+    r.become_leader()
+    r.broadcast_heartbeat_hint((101, 1001))
+    msgs = r.read_messages()
+    assert sum(m["type"] == HEARTBEAT for m in msgs) == 2
+    assert all(m["hint"] == 101 and m["hint_high"] == 1001 for m in msgs)
+
+
+# ---- raft_test.go:2952-3037: ReadIndex inside raft -----------------------
+def test_leader_read_index_on_single_node_shard():
+    # raft_test.go:2952-2976
+    r = po.TestRaft(1, [1], 5, 1)
+    r.become_candidate()
+    r.become_leader()
+    r.handle(msg(READ_INDEX, hint=101, hint_high=1002))
+    assert r.read_messages() == []
+    assert r.ready_to_read() == [(r.committed, (101, 1002))]
+    assert r.read_index_len() == 0
+
+
+def test_leader_ignore_read_index_when_shard_committed_is_unknown():
+    # raft_test.go:2978-2997
+    r = po.TestRaft(1, [1, 2, 3], 5, 1)
+    r.become_candidate()
+    r.become_leader()
+    r.handle(msg(READ_INDEX, hint=101, hint_high=1002))
+    assert r.read_messages() == []
+    assert r.ready_to_read() == []
+    assert r.read_index_len() == 0
+
+
+def test_handle_leader_read_index():
+    # raft_test.go:2999-3037
+    r = po.TestRaft(1, [1, 2, 3], 5, 1)
+    r.become_follower(1, 0)
+    assert not r.has_committed_entry_at_current_term()
+    r.become_candidate()
+    r.become_leader()
+    assert not r.has_committed_entry_at_current_term()
+    rm = r.remote(2)
+    po.lib().orc_remote_try_update(rm, r.last_index)
+    r.set_remote(2, rm)
+    assert r.try_commit()
+    assert r.has_committed_entry_at_current_term()
+    r.handle(msg(READ_INDEX, hint=101, hint_high=1002))
+    hb = [m for m in r.read_messages() if m["type"] == HEARTBEAT and
+          m["to"] in (2, 3) and m["hint"] == 101 and m["hint_high"] == 1002]
+    assert len(hb) == 2
+    assert r.read_index_len() == 1
+
+# raft_test.go:3039-3063 (TestWitnessReadIndex) is not restated: witness
+# members are outside the GPU fast path, which only steps
+# voting members.
