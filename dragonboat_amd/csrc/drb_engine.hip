@@ -2008,9 +2008,9 @@ extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
   for (uint32_t i = 0; i < key_len; ++i)
     h = (h ^ ((k8 >> (8 * i)) & 0xff)) * 0x100000001b3ull;
   h ^= h >> 29;
-  uint32_t ks = (uint32_t)h & (v.KS - 1);
+  const uint32_t home = (uint32_t)h & (v.KS - 1);
   for (uint32_t p = 0; p < v.KS; ++p) {
-    const uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
+    const uint4 *sl = &tbl[(uint64_t)kv_probe(v, home, p) * v.KVW];
     bool used = (sl[0].z >> 31) & 1u;
     if (!used) return 1;
     uint32_t klen = sl[0].z & 0xffu, vlen = (sl[0].z >> 8) & 0xfffu;
@@ -2019,7 +2019,6 @@ extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
       if (vlen > val_cap) return DRB_ERANGE;
       return slot_value(e, sl, val, vlen);
     }
-    ks = (ks + 1) & (v.KS - 1);
   }
   return 1;
 }
@@ -2046,10 +2045,11 @@ extern "C" int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
     for (uint32_t b = 0; b < kl; ++b)
       h = (h ^ ((k8 >> (8 * b)) & 0xff)) * 0x100000001b3ull;
     h ^= h >> 29;
-    uint32_t ks = (uint32_t)h & mask, p = 0;
+    const uint32_t home = (uint32_t)h & mask;
+    uint32_t ks = home, p = 0;
     while (p < v.KS && (tbl[(uint64_t)ks * v.KVW].z >> 31)) {
-      ks = (ks + 1) & mask;
       ++p;
+      ks = kv_probe(v, home, p);
     }
     if (p == v.KS) return DRB_ERANGE;
     const uint8_t *val = vals + i * val_stride;

@@ -1099,14 +1099,13 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
   }
   // open-addressing upsert into this replica's table: DRB_PROBE_W slots
   // are loaded per step (one memory round trip), then resolved in order
-  uint32_t mask = v.KS - 1;
-  uint32_t ks = (uint32_t)kv_hash(key8, klen) & mask;
+  const uint32_t home = (uint32_t)kv_hash(key8, klen) & (v.KS - 1);
   uint4 *tbl = v.kv + kv_ix(v, L.slot, L.g, 0);
   for (uint32_t p0 = 0; p0 < v.KS; p0 += DRB_PROBE_W) {
     uint4 hs[DRB_PROBE_W];
 #pragma unroll
     for (uint32_t t = 0; t < DRB_PROBE_W; ++t)
-      hs[t] = p0 + t < v.KS ? tbl[(uint64_t)((ks + t) & mask) * v.KVW]
+      hs[t] = p0 + t < v.KS ? tbl[(uint64_t)kv_probe(v, home, p0 + t) * v.KVW]
                             : make_uint4(0, 0, 0, 1u << 31);
     uint32_t found = DRB_PROBE_W;
     bool hit = false;
@@ -1121,7 +1120,7 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       }
     }
     if (found < DRB_PROBE_W) {
-      uint4 *sl = tbl + (uint64_t)((ks + found) & mask) * v.KVW;
+      uint4 *sl = tbl + (uint64_t)kv_probe(v, home, p0 + found) * v.KVW;
       if (!EXT) {
         // inline value of a Cmd inside the 64 B register window: bytes 4..
         // in the slot's following chunks
@@ -1148,7 +1147,6 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       r.applied_any = true;
       return 1;
     }
-    ks = (ks + DRB_PROBE_W) & mask;
   }
   return -2;  // table full
 }
@@ -1223,9 +1221,9 @@ DRB_DEV void encode_saves(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
 // released ctx {low, high} looks up the 8-byte LE key
 // mix64(low ^ (j+1)*GOLDEN) % key_space and folds the slot word
 // (found: vlen << 32 | LE32(value), else ~0) into read_sum[slot][g].
-// A lookup first reads two adjacent slots (one 128 B line unless the
-// first is the last slot of a line), and the lookups of a batch are all
-// issued before any is resolved: one memory round trip per batch.
+// A lookup first reads its first two probes (one 128 B line: kv_probe
+// wraps inside the home line), and the lookups of a batch are all issued
+// before any is resolved: one memory round trip per batch.
 DRB_DEV bool kv_used(uint4 h) { return (h.z >> 31) & 1u; }
 DRB_DEV bool kv_match(uint4 h, uint64_t key8, uint32_t klen) {
   return kv_used(h) && (h.z & 0xffu) == klen && lo64(h) == key8;
@@ -1234,23 +1232,21 @@ DRB_DEV uint64_t kv_word(uint4 h) {
   const uint32_t vlen = (h.z >> 8) & 0xfffu;
   return ((uint64_t)vlen << 32) | (h.w & byte_mask(vlen));
 }
-// linear probing from slot ks for at most `probes` slots, DRB_PROBE_W
-// slots per memory round trip
-DRB_DEV uint64_t kv_probe_word(const uint4 *tbl, uint32_t KVW, uint32_t mask,
-                               uint32_t ks, uint64_t key8, uint32_t klen,
-                               uint32_t probes) {
-  for (uint32_t p0 = 0; p0 < probes; p0 += DRB_PROBE_WR) {
+// probes t0 .. KS-1 of home slot `home` (kv_probe), DRB_PROBE_WR slots
+// per memory round trip
+DRB_DEV uint64_t kv_probe_word(const View &v, const uint4 *tbl, uint32_t home,
+                               uint32_t t0, uint64_t key8, uint32_t klen) {
+  for (uint32_t p0 = t0; p0 < v.KS; p0 += DRB_PROBE_WR) {
     uint4 hs[DRB_PROBE_WR];
 #pragma unroll
     for (uint32_t t = 0; t < DRB_PROBE_WR; ++t)
-      hs[t] = p0 + t < probes ? tbl[(uint64_t)((ks + t) & mask) * KVW]
-                              : make_uint4(0, 0, 0, 0);
+      hs[t] = p0 + t < v.KS ? tbl[(uint64_t)kv_probe(v, home, p0 + t) * v.KVW]
+                            : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (uint32_t t = 0; t < DRB_PROBE_WR; ++t) {
-      if (!kv_used(hs[t])) return ~0ull;  // also the padding past probes
+      if (!kv_used(hs[t])) return ~0ull;  // also the padding past KS
       if (kv_match(hs[t], key8, klen)) return kv_word(hs[t]);
     }
-    ks = (ks + DRB_PROBE_WR) & mask;
   }
   return ~0ull;
 }
@@ -1288,8 +1284,10 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
         ks[t] = (uint32_t)kv_hash(key[t], 8) & mask;
         h0[t] = h1[t] = make_uint4(0, 0, 0, 0);
         if (j0 + t < n_reads) {
+          // (plain loads: with the nontemporal hint the step kernel fetched
+          // 7 % more bytes, profiles/r02_kvline)
           h0[t] = tbl[(uint64_t)ks[t] * v.KVW];
-          h1[t] = tbl[(uint64_t)((ks[t] + 1) & mask) * v.KVW];
+          h1[t] = tbl[(uint64_t)kv_probe(v, ks[t], 1) * v.KVW];
         }
       }
 #pragma unroll
@@ -1306,8 +1304,7 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
         else if (kv_match(h1[t], key[t], 8))
           w = kv_word(h1[t]);
         else
-          w = kv_probe_word(tbl, v.KVW, mask, (ks[t] + 2) & mask, key[t], 8,
-                            v.KS - 2);
+          w = kv_probe_word(v, tbl, ks[t], 2, key[t], 8);
         sum += mix64(w ^ key[t] ^ ((uint64_t)j << 56));
         served++;
       }

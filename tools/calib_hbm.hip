@@ -59,6 +59,60 @@ __global__ void rd_rand(const uint4 *p, uint64_t slots, uint64_t n,
   if (q.x == 0x12345679u) *sink = q.y;
 }
 
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ uint4 ld_nt(const uint4 *p) {
+  u4v v = __builtin_nontemporal_load((const u4v *)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ void st_nt(uint4 *p, uint4 q) {
+  u4v v = {q.x, q.y, q.z, q.w};
+  __builtin_nontemporal_store(v, (u4v *)p);
+}
+// 8 independent random 16 B reads per lane (memory-level parallelism);
+// NT: the loads carry the nontemporal hint (streaming, no L2 reuse)
+template <bool NT>
+__global__ void rd_rand8(const uint4 *p, uint64_t slots, uint64_t n,
+                         uint32_t salt, uint64_t *sink) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint4 q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint64_t s = mix((i * 8 + k) ^ ((uint64_t)salt << 40)) % slots;
+    q[k] = NT ? ld_nt(p + s) : p[s];
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x ^= q[k].x + q[k].w;
+  if (x == 0x12345679u) *sink = x;
+}
+// 8 random 8 B reads per lane
+__global__ void rd_rand8_u2(const uint2 *p, uint64_t slots, uint64_t n,
+                            uint32_t salt, uint64_t *sink) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint2 q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint64_t s = mix((i * 8 + k) ^ ((uint64_t)salt << 40)) % slots;
+    q[k] = p[s];
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x ^= q[k].x + q[k].y;
+  if (x == 0x12345679u) *sink = x;
+}
+// random 16 B RMW with a nontemporal store
+__global__ void rmw_rand_nt(uint4 *p, uint64_t slots, uint64_t n,
+                            uint32_t salt) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t s = mix(i ^ ((uint64_t)salt << 40)) % slots;
+  uint4 q = ld_nt(p + s);
+  q.x += 1;
+  st_nt(p + s, q);
+}
+
 int main() {
   const uint64_t bytes = 4ull << 30;  // 4 GiB streams (>> 256 MiB L3)
   void *buf;
@@ -88,6 +142,11 @@ int main() {
   const uint64_t n = 1ull << 24, slots = bytes / 16;  // 16M random slots
   TIME("rd_rand16", n * 16, (rd_rand<<<(unsigned)(n / 256), 256>>>((uint4 *)buf, slots, n, rep, sink)));
   TIME("rmw_rand16", n * 32, (rmw_rand<<<(unsigned)(n / 256), 256>>>((uint4 *)buf, slots, n, rep)));
+  const uint64_t n8 = 1ull << 24;  // 16M lanes x 8 reads
+  TIME("rd_rand8", n8 * 128, (rd_rand8<false><<<(unsigned)(n8 / 256), 256>>>((uint4 *)buf, slots, n8, rep, sink)));
+  TIME("rd_rand8nt", n8 * 128, (rd_rand8<true><<<(unsigned)(n8 / 256), 256>>>((uint4 *)buf, slots, n8, rep, sink)));
+  TIME("rd_rand8u2", n8 * 64, (rd_rand8_u2<<<(unsigned)(n8 / 256), 256>>>((uint2 *)buf, slots * 2, n8, rep, sink)));
+  TIME("rmw_randnt", n * 32, (rmw_rand_nt<<<(unsigned)(n / 256), 256>>>((uint4 *)buf, slots, n, rep)));
   CK(hipDeviceSynchronize());
   printf("done\n");
   return 0;
