@@ -62,9 +62,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
+    ap.add_argument("--workload", default="c3",
+                    choices=["c2", "c3", "c4", "c5"],
                     help="c3: groups sharded over GPUs, replicas "
-                         "co-resident (BASELINE metric); c4: --groups "
+                         "co-resident (BASELINE metric); c2: 64k groups per "
+                         "GPU, 16 B writes only; c4: --groups "
                          "groups in total, replica slot s of group g on "
                          "GPU (g + s) mod N, planes exchanged over RCCL; "
                          "c5: 4M groups per GPU, --active-ppm of them "
@@ -106,6 +108,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true",
                     help="skip the receiving-side wire ingest measurement")
+    ap.add_argument("--host-staged", type=int, default=-1,
+                    help="after the timed region, also time rounds whose "
+                         "proposals come from host memory through "
+                         "drb_stage_proposals (default: on for c2/c3, N=1)")
     return ap.parse_args()
 
 
@@ -189,6 +195,11 @@ def main():
     from dragonboat_amd.engine import Engine
     c4 = args.workload == "c4"
     c5 = args.workload == "c5"
+    c2 = args.workload == "c2"
+    if c2:  # 64k groups, 16 B writes, replicas co-resident
+        args.no_read_index = True
+        if args.groups == 1 << 20:
+            args.groups = 1 << 16
     if not args.replicas:
         args.replicas = 5 if c4 else 3
     if args.quiesce < 0:
@@ -372,9 +383,47 @@ def main():
                         "region"}
             rx.close()
             del stream
+    from dragonboat_amd import abi as _abi
+    host_staged = None
+    if args.host_staged < 0:
+        args.host_staged = int(world == 1 and not (c4 or c5) and k == 1)
+    if args.host_staged:
+        # the same rounds with this round's proposals staged from host
+        # memory (the entryQueue as the host holds it: drb_entry rows and a
+        # Cmd pool, uploaded and laid out on the device, one call a round)
+        import ctypes as C
+        from dragonboat_amd import workload
+        # the host arrays in pinned memory, so the upload overlaps the
+        # previous round (drb_stage_proposals copies on its own stream)
+        hb = [tuple(torch.from_numpy(x.view("u1")).pin_memory()
+                    for x in workload.build_batch_np(G, seed, b))
+              for b in range(NP)]
+        hp = [(C.cast(c.data_ptr(), C.POINTER(C.c_uint32)),
+               C.cast(e.data_ptr(), C.POINTER(_abi.Entry)),
+               C.cast(p.data_ptr(), C.POINTER(C.c_uint8))) for c, e, p in hb]
+        KH = max(5, min(K, 20))
+        eng.read_counters(reset=True)
+        eng.sync()
+        h0 = time.perf_counter()
+        for i in range(KH):
+            b = i % NP
+            eng.stage_proposals(b, *hp[b], pool_len=hb[b][2].numel())
+            step(2 * args.warmup + K + i)
+        eng.sync()
+        hms = (time.perf_counter() - h0) * 1e3 / KH
+        hout = eng.read_counters(reset=True)
+        host_staged = {
+            "ms_per_step": hms, "steps": KH,
+            "committed_entries_per_s": hout.committed_entries / (hms * KH *
+                                                                 1e-3),
+            "upload_bytes_per_round": int(sum(x.numel() for x in hb[0])),
+            "note": "proposals staged from pinned host memory every round "
+                    "(drb_stage_proposals: one H2D per array on a copy "
+                    "stream, overlapping the previous round, + a layout "
+                    "kernel), timed around the whole loop; not `value`"}
+        del hb, hp
     # the replicas that left the fast path during the run, by reason
     # (drb_take_flagged): a run with any is not a pure fast-path number
-    from dragonboat_amd import abi as _abi
     flagged, lost = eng.take_flagged(reset=True)
     by_reason = {}
     for (_, _, reason, flags, _, _) in flagged:
@@ -413,6 +462,14 @@ def main():
             par = ("replicas spread over GPUs; one plane exchange per round "
                    "(RCCL send/recv over xGMI)" if world > 1 else
                    "replicas co-resident (N=1)")
+        elif c2:
+            metric = ("committed entries/sec (node) at %d active 3-replica "
+                      "groups, 16B payload, replicas co-resident; %%HBM BW"
+                      % G)
+            wl = ("C2: %d active groups x %d replicas per GPU, 16B PBKV "
+                  "writes k=%d/group/round, tick every %d round(s)" % (
+                      G, R, k, args.tick_every))
+            par = "groups sharded, replicas co-resident"
         else:
             metric = ("committed entries/sec (node) at 1M active 3-replica "
                       "groups, 16B payload; %HBM BW")
@@ -443,7 +500,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None if (c4 or c5) else pmc_traffic(G, R),
+                "traffic": None if (c2 or c4 or c5) else pmc_traffic(G, R),
                 "traffic_source": "profiles/pmc_current.json (rocprofv3 "
                                   "FETCH_SIZE x2 + WRITE_SIZE, bytes per "
                                   "round)",
@@ -466,6 +523,8 @@ def main():
         }
         if wire is not None:
             res["wire"] = wire
+        if host_staged is not None:
+            res["host_staged"] = host_staged
         if xch is not None:
             res["exchange"] = {"bytes_sent_per_round_rank0":
                                xch.bytes_sent / K}

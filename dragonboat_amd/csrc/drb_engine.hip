@@ -37,6 +37,9 @@ struct drb_engine {
   hipStream_t stream;
   hipStream_t stream2;            // the follower kernel of a round
   hipEvent_t ev_fork, ev_join;    // stream -> stream2 -> stream
+  hipStream_t stream_h2d;         // drb_stage_proposals uploads
+  hipEvent_t ev_staged;           // upload done -> layout kernel
+  hipEvent_t ev_stage_free;       // layout kernel done -> next upload
   uint64_t round;
   uint64_t ticks;  // LocalTicks delivered so far (RoundParams.tick_no)
   uint64_t committed_round = 0;  // drb_commit_round (durable_log)
@@ -49,6 +52,8 @@ struct drb_engine {
   unsigned long long *ctr_total = nullptr;   // their sum (read_counters)
   void *scratch;
   size_t scratch_bytes;
+  void *stage_buf = nullptr;  // drb_stage_proposals upload (grow-only)
+  size_t stage_bytes = 0;
   struct WireState *wire = nullptr;          // drb_encode_wire (drb_wire.hpp)
   std::mutex ingest_mu;  // drb_ingest: concurrent transport threads
   bool crc_tab_ready = false;  // c_crc_tab uploaded on this engine's device
@@ -139,7 +144,7 @@ static int scatter(drb_engine *e, T *base, const std::vector<uint64_t> &idx,
   return DRB_OK;
 }
 
-static uint4 mk4h(uint64_t a, uint64_t b) {
+__host__ __device__ static inline uint4 mk4h(uint64_t a, uint64_t b) {
   uint4 q;
   q.x = (uint32_t)a;
   q.y = (uint32_t)(a >> 32);
@@ -203,6 +208,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
       hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) !=
           hipSuccess ||
       hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) !=
+          hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream_h2d, hipStreamNonBlocking) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_stage_free, hipEventDisableTiming) !=
           hipSuccess) {
     delete e;
     return DRB_EDEVICE;
@@ -336,9 +347,13 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   (void)hipStreamSynchronize(e->stream2);
   for (void *p : e->allocs) (void)hipFree(p);
   if (e->scratch) (void)hipFree(e->scratch);
+  if (e->stage_buf) (void)hipFree(e->stage_buf);
   wire_free(e);
   (void)hipEventDestroy(e->ev_fork);
   (void)hipEventDestroy(e->ev_join);
+  (void)hipEventDestroy(e->ev_staged);
+  (void)hipEventDestroy(e->ev_stage_free);
+  (void)hipStreamDestroy(e->stream_h2d);
   (void)hipStreamDestroy(e->stream2);
   (void)hipStreamDestroy(e->stream);
   delete e;
@@ -839,44 +854,86 @@ extern "C" int drb_host_slot(drb_engine *e, uint32_t slot, int hosted) {
 }
 
 // ---------------------------------------------------------------- inputs
+// The entry queue as the host holds it (drb_entry rows + Cmd pool) is
+// uploaded as-is and laid out in the staged-proposal planes on the device:
+// one lane per group, entries j < counts[g] (the step reads no others).
+__global__ void k_stage_props(View v, uint32_t slot, const uint32_t *counts,
+                              const drb_entry *ents, const uint8_t *pool,
+                              uint64_t pool_len) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  const uint32_t n = counts[g];
+  v.prop_count[(uint64_t)slot * v.G + g] = n;
+  for (uint32_t j = 0; j < n; ++j) {
+    const drb_entry en = ents[g * v.max_props + j];
+    const uint8_t *cmd = pool + en.cmd_off;
+    v.props[prop_ix(v, slot, j, 0, g)] = mk4h(en.key, en.client_id);
+    v.props[prop_ix(v, slot, j, 1, g)] = mk4h(en.series_id, en.responded_to);
+    if (en.cmd_len > v.C16 * 16 || en.cmd_off + en.cmd_len > pool_len) {
+      // a Cmd the staged planes cannot hold (or outside the pool): the
+      // leader's pre-pass sends the group to the CPU path (DRB_FB_CAPACITY)
+      v.props[prop_ix(v, slot, j, 2, g)] = make_uint4(en.type, ~0u, 1, 0);
+      continue;
+    }
+    const uint32_t b0 = en.cmd_len ? cmd[0] : 0u;
+    v.props[prop_ix(v, slot, j, 2, g)] = make_uint4(
+        en.type, en.cmd_len,
+        prop_fast(en.type, en.client_id, en.series_id, en.cmd_len, b0), 0);
+    for (uint32_t c = 0; c < v.C16; ++c) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t b = 0; b < 16 && c * 16 + b < en.cmd_len; ++b)
+        w[b >> 2] |= (uint32_t)cmd[c * 16 + b] << (8 * (b & 3));
+      v.props[prop_ix(v, slot, j, PROP_META + c, g)] =
+          make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
                                    const uint32_t *counts,
                                    const drb_entry *ents,
-                                   const uint8_t *pool) {
+                                   const uint8_t *pool, size_t pool_len) {
   if (!e || slot >= e->cfg.prop_slots) return DRB_ERANGE;
+  if (!counts || !ents || (pool_len && !pool)) return DRB_EINVAL;
   const View &v = e->v;
   const uint64_t G = v.G;
-  const uint32_t chunks = PROP_META + v.C16;
-  std::vector<uint4> host((uint64_t)v.max_props * chunks * G);
-  memset(host.data(), 0, host.size() * sizeof(uint4));
-  for (uint64_t g = 0; g < G; ++g) {
+  // the counts are checked here (DRB_ERANGE leaves the slot untouched);
+  // each entry's Cmd extent on the device (k_stage_props)
+  for (uint64_t g = 0; g < G; ++g)
     if (counts[g] > v.max_props) return DRB_ERANGE;
-    for (uint32_t j = 0; j < counts[g]; ++j) {
-      const drb_entry &en = ents[g * v.max_props + j];
-      if (en.cmd_len > v.C16 * 16) return DRB_ERANGE;
-      uint64_t b = (uint64_t)j * chunks * G + g;
-      host[b + 0 * G] = mk4h(en.key, en.client_id);
-      host[b + 1 * G] = mk4h(en.series_id, en.responded_to);
-      const uint32_t b0 = en.cmd_len ? pool[en.cmd_off] : 0u;
-      uint4 p2 = {en.type, en.cmd_len,
-                  prop_fast(en.type, en.client_id, en.series_id, en.cmd_len,
-                            b0),
-                  0};
-      host[b + 2 * G] = p2;
-      for (uint32_t c = 0; c < v.C16; ++c) {
-        uint8_t by[16] = {0};
-        for (uint32_t k = 0; k < 16; ++k)
-          if (c * 16 + k < en.cmd_len) by[k] = pool[en.cmd_off + c * 16 + k];
-        memcpy(&host[b + (PROP_META + c) * G], by, 16);
-      }
-    }
+  const size_t ent_b = (size_t)G * v.max_props * sizeof(drb_entry);
+  const size_t cnt_off = ent_b, pool_off = (cnt_off + G * 4 + 255) & ~(size_t)255;
+  const size_t need = pool_off + std::max<uint64_t>(pool_len, 16);
+  if (need > e->stage_bytes) {
+    HIPCHK(hipStreamSynchronize(e->stream));  // the buffer may be in use
+    if (e->stage_buf) HIPCHK(hipFree(e->stage_buf));
+    e->stage_buf = nullptr;
+    HIPCHK(hipMalloc(&e->stage_buf, need));
+    e->stage_bytes = need;
   }
-  uint4 *dst = v.props + prop_ix(v, slot, 0, 0, 0);
-  HIPCHK(hipMemcpyAsync(dst, host.data(), host.size() * sizeof(uint4),
-                        hipMemcpyHostToDevice, e->stream));
-  HIPCHK(hipMemcpyAsync(v.prop_count + (uint64_t)slot * G, counts, G * 4,
-                        hipMemcpyHostToDevice, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  uint8_t *d = (uint8_t *)e->stage_buf;
+  // The upload runs on its own stream, so it overlaps a round still
+  // running on the engine stream; it starts once the previous call's layout
+  // kernel has consumed the upload buffer.  The call returns when the host
+  // arrays have been read (they may be reused); the layout kernel is
+  // ordered on the engine stream after the upload, ahead of the round
+  // that reads the slot.
+  HIPCHK(hipStreamWaitEvent(e->stream_h2d, e->ev_stage_free, 0));
+  HIPCHK(hipMemcpyAsync(d, ents, ent_b, hipMemcpyHostToDevice,
+                        e->stream_h2d));
+  HIPCHK(hipMemcpyAsync(d + cnt_off, counts, G * 4, hipMemcpyHostToDevice,
+                        e->stream_h2d));
+  if (pool_len)
+    HIPCHK(hipMemcpyAsync(d + pool_off, pool, pool_len, hipMemcpyHostToDevice,
+                          e->stream_h2d));
+  HIPCHK(hipEventRecord(e->ev_staged, e->stream_h2d));
+  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_staged, 0));
+  k_stage_props<<<(unsigned)((G + 255) / 256), 256, 0, e->stream>>>(
+      v, slot, (const uint32_t *)(d + cnt_off), (const drb_entry *)d,
+      d + pool_off, (uint64_t)pool_len);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e->ev_stage_free, e->stream));
+  HIPCHK(hipEventSynchronize(e->ev_staged));
   return DRB_OK;
 }
 

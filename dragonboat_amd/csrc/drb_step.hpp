@@ -1934,6 +1934,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           if (rm && pass == 0 && cnt)
             src.lo = v.elo_in[mmeta_ix(v, L.rbuf, s, slot, g)];
           uint64_t prev_lo = 0, prev_hi = 0;
+          // (a window of prefetched records measured slower: the leader
+          // spills more, profiles/r02_kvline/README.md)
           for (uint32_t j = 0; j < cnt; ++j) {
             const uint32_t k = rec_pos(pass == 0, j, v.MB);
             const uint4 c0 = mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];

@@ -43,7 +43,8 @@ SIGNATURES = {
                                  PU8, SZ]),
     "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
     "drb_host_slot": (C.c_int, [P, U32, C.c_int]),
-    "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8]),
+    "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8,
+                                      SZ]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
     "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
                                               U64, U32]),
@@ -221,9 +222,13 @@ class Engine:
             "drb_init_steady")
 
     # ---------------------------------------------------------- inputs
-    def stage_proposals(self, slot, counts, ents, pool):
-        _ck(lib().drb_stage_proposals(self.h, slot, counts, ents, pool),
-            "drb_stage_proposals")
+    def stage_proposals(self, slot, counts, ents, pool, pool_len=None):
+        """pool: a ctypes byte array (its size is the pool length) or a
+        pointer with pool_len."""
+        if pool_len is None:
+            pool_len = C.sizeof(pool)
+        _ck(lib().drb_stage_proposals(self.h, slot, counts, ents, pool,
+                                      pool_len), "drb_stage_proposals")
 
     def gen_kv_proposals(self, slot, k, key_space, val_len, seed, salt,
                          active_ppm=1000000):

@@ -89,6 +89,45 @@ def build_batch(num_groups, k, seed, salt, key_space=256, val_len=4,
     return counts, ents, pbuf
 
 
+def _mix64_np(z):
+    import numpy as np
+    z = z + np.uint64(GOLDEN)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def build_batch_np(num_groups, seed, salt, key_space=256):
+    """build_batch(num_groups, 1, seed, salt, key_space, 4) vectorised with
+    numpy (the bench's host-staged rounds at 1M groups): the same Entry
+    rows and Cmd pool, 17 B per group (0x00 || PBKV{8 B key, 4 B value})."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        g = np.arange(num_groups, dtype=np.uint64)
+        r0 = _mix64_np(np.uint64(seed) ^ (g * np.uint64(GOLDEN)) ^
+                       np.uint64((salt << 32) & MASK))
+        r1 = _mix64_np(r0)
+        r2 = _mix64_np(r1)
+        cid = _mix64_np(np.uint64(seed ^ CLIENT) ^ g) | np.uint64(1)
+    ents = np.zeros(num_groups, dtype=np.dtype(
+        [("term", "<u8"), ("index", "<u8"), ("key", "<u8"),
+         ("client_id", "<u8"), ("series_id", "<u8"), ("responded_to", "<u8"),
+         ("type", "<u4"), ("cmd_len", "<u4"), ("cmd_off", "<u8")]))
+    assert ents.dtype.itemsize == C.sizeof(Entry)
+    ents["key"] = r0 | np.uint64(1)
+    ents["client_id"] = cid
+    ents["type"] = ENTRY_ENCODED
+    ents["cmd_len"] = 17
+    ents["cmd_off"] = g * np.uint64(17)
+    pool = np.zeros((num_groups, 17), dtype=np.uint8)
+    pool[:, 1:3] = (0x0A, 8)
+    pool[:, 3:11] = (r1 % np.uint64(key_space)).view(np.uint8).reshape(-1, 8)
+    pool[:, 11:13] = (0x12, 4)
+    pool[:, 13:17] = r2.view(np.uint8).reshape(-1, 8)[:, :4]
+    counts = np.ones(num_groups, dtype=np.uint32)
+    return counts, ents, pool.reshape(-1)
+
+
 def read_index_ctx(seed, g, salt, high):
     """pendingReadIndex.genCtx (request.go:864-875): Low random non-zero."""
     low = mix64(seed ^ RI_SALT ^ ((g * GOLDEN) & MASK) ^ (salt << 40)) | 1

@@ -407,9 +407,20 @@ int drb_init_steady(drb_engine *e, uint64_t term, uint32_t leader_slot,
 
 /* Stage proposals for one round: counts[g] entries for group g taken from
  * ents[g * max_props ...].  Replaces entryQueue.add (queue.go:60) feeding
- * node.handleProposals (node.go:1275).  Consumed by the group's leader. */
+ * node.handleProposals (node.go:1275).  Consumed by the group's leader.
+ * pool holds pool_len bytes of Cmd data (entries address it by
+ * cmd_off / cmd_len).  counts[g] > max_props is DRB_ERANGE (the slot is
+ * left as it was); an entry whose Cmd exceeds cmd_cap or the pool is
+ * staged as one the leader cannot take, so its group falls back before
+ * appending (DRB_FB_CAPACITY).  The arrays are uploaded as-is on a copy
+ * stream that overlaps a round still
+ * running, and laid out on the device by a kernel ordered on the engine
+ * stream ahead of the next round.  Returns once the host arrays have been
+ * read: the caller may reuse them.  Pinned host memory makes the upload
+ * asynchronous to the running round. */
 int drb_stage_proposals(drb_engine *e, uint32_t slot, const uint32_t *counts,
-                        const drb_entry *ents, const uint8_t *pool);
+                        const drb_entry *ents, const uint8_t *pool,
+                        size_t pool_len);
 /* Device-side synthetic proposal generator (bench / SURVEY 8d inputs):
  * k KVTest PBKV writes per group, NoOP session, EncodedEntry v0. */
 int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,

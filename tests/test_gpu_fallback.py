@@ -261,6 +261,27 @@ def test_non_fast_path_proposals_fall_back_before_append(kind):
     assert not p.check(groups=[g for g in range(p.G) if g != 3])
 
 
+def test_oversized_cmd_falls_back_before_append():
+    """A staged Cmd longer than cmd_cap (checked per entry by the device
+    layout of drb_stage_proposals) sends only its group to the CPU path,
+    before the leader appends: DRB_FB_CAPACITY; the other groups step."""
+    p = Pair(G=8, R=3, prop_slots=2)
+    _steady(p, 2)
+    big = bytes([0x00]) + po.pbkv_marshal(b"k" * 8, b"v" * 64)
+    assert len(big) > p.eng.cfg["cmd_cap"]
+    e = po.ent(type=abi.ENTRY_ENCODED, client_id=77, cmd=big)
+    _stage_engine_only(p, {5: [e]})
+    snap = p.snapshot()
+    p.orc.round(tick=False)
+    out = p.eng.step(tick=False, prop_slot=1)
+    p.rounds += 1
+    fl = _flagged(p)
+    assert fl == {(5, 0): (FB["CAPACITY"], abi.F_FALLBACK | 1)}, fl
+    _assert_pre_round(p, snap, fl)
+    assert out.fallbacks == 1
+    assert not p.check(groups=[g for g in range(p.G) if g != 5])
+
+
 def test_config_change_proposal_round_trip():
     """A ConfigChange proposal (AddNode of an existing member) goes to the
     CPU path before the leader appends (DRB_FB_ENTRY_TYPE); the oracle
