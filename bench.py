@@ -108,6 +108,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true",
                     help="skip the receiving-side wire ingest measurement")
+    ap.add_argument("--exchange", default="fixed",
+                    choices=["fixed", "counted"],
+                    help="c4 plane exchange: full-capacity planes enqueued "
+                         "behind the round (no host sync) or sized by an "
+                         "all_gather of per-plane counts (dragonboat_amd/"
+                         "exchange.py)")
     ap.add_argument("--host-staged", type=int, default=-1,
                     help="after the timed region, also time rounds whose "
                          "proposals come from host memory through "
@@ -226,7 +232,8 @@ def main():
                      device=local)
         if world > 1:
             from dragonboat_amd.exchange import PlaneExchange
-            xch = PlaneExchange(eng, world, rank, torch.device("cuda", local))
+            xch = PlaneExchange(eng, world, rank, torch.device("cuda", local),
+                                fixed=args.exchange == "fixed")
     elif c5:  # 128 B / 1 KB entries, values out of line, saves encoded
         first_shard, seed = ddist.shard_plan(rank, G)
         vlen = C5_VAL[args.payload]
@@ -526,7 +533,8 @@ def main():
         if host_staged is not None:
             res["host_staged"] = host_staged
         if xch is not None:
-            res["exchange"] = {"bytes_sent_per_round_rank0":
+            res["exchange"] = {"mode": args.exchange,
+                               "bytes_sent_per_round_rank0":
                                xch.bytes_sent / K}
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)

@@ -3,13 +3,26 @@
 After every round each rank's engine holds, per remote (sender slot,
 receiver slot) plane, the records, headers and entry rows its replicas sent
 to replicas on other ranks (include/drb_engine.h, drb_plane_*).  One
-exchange step per round moves them:
+exchange step per round moves them, in one of two modes:
 
-  1. drb_plane_counts: per plane a word {records K, entry rows E, flags};
-  2. all_gather of those words, so every receiver knows the sizes its
-     senders will ship;
-  3. one batched group of point-to-point send/recv (RCCL over xGMI when the
-     backend is "nccl"), plane regions straight out of / into engine memory.
+fixed (the default on RCCL): every remote plane moves at its full capacity
+  -- the mailbox's MB record positions (both chunks), the header, the max
+  LogIndex + n word, the entry-row base and E entry rows -- which the
+  leader's and the follower's pre-pass already bound (DRB_FB_CAPACITY
+  before a round could exceed them).  The receiver reads only what the
+  plane's header counts (stale positions are never read), so no sizes are
+  exchanged: the sends and receives are enqueued on the engine stream
+  right behind the round (torch's NCCL work waits on it, and the next
+  round waits on the work), with no host synchronisation at all;
+
+counted: 1. drb_plane_counts (a stream sync): per plane a word {records K,
+  entry rows E, flags}; 2. all_gather of those words, so every receiver
+  knows the sizes its senders will ship; 3. the regions at those sizes.
+  Fewer bytes, one host round trip per round.
+
+Both post one batched group of point-to-point send/recv (RCCL over xGMI
+when the backend is "nccl"), plane regions straight out of / into engine
+memory.
 
 This replaces the reference's Transport.Send -> handleRequest path
 (internal/transport/transport.go:346, :305) for GPU-resident replicas.
@@ -46,6 +59,13 @@ def host_bytes(ptr, nbytes):
 def place_peer(world, rank, a, b, direction):
     """Rank plane (a, b) goes to (0) / comes from (1); -1 when local."""
     return _engine.lib().drb_place_peer(world, rank, a, b, direction)
+
+
+def full_word(mailbox, entry_mbox):
+    """The summary word of a plane at full capacity (drb_plane_regions):
+    every record position, both chunks, the header and every entry row."""
+    return (mailbox & 0x1f) | ((entry_mbox & 0xff) << 10) | (1 << 18) | \
+        (1 << 19)
 
 
 def plan(R, world, rank, words, regions):
@@ -103,29 +123,60 @@ def run_ops_staged(ops, device, group=None):
         d.copy_(h)
 
 
+def run_ops_on_stream(ops, to_tensor, stream, group=None):
+    """The batch enqueued behind `stream` (the engine's): NCCL's work waits
+    on the stream, and the stream waits on the work; the host does not."""
+    with torch.cuda.stream(stream):
+        p2p = [dist.P2POp(dist.isend if op == "send" else dist.irecv,
+                          to_tensor(ptr, nbytes), peer, group)
+               for op, peer, (ptr, nbytes) in ops]
+        if p2p:
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()  # stream-side for NCCL
+
+
 class PlaneExchange:
     """The exchange step of one rank's engine (torch.distributed group).
-    staged=True moves the regions through host memory (gloo)."""
+    staged=True moves the regions through host memory (gloo); fixed=True
+    ships full-capacity planes with no host round trip (module doc)."""
 
-    def __init__(self, eng, world, rank, device, group=None, staged=False):
+    def __init__(self, eng, world, rank, device, group=None, staged=False,
+                 fixed=None):
         self.eng, self.world, self.rank = eng, world, rank
         self.device, self.group, self.staged = device, group, staged
+        self.fixed = (not staged) if fixed is None else fixed
         self.bytes_sent = 0
+        self._stream = None if staged else torch.cuda.ExternalStream(
+            eng.stream, device=device)
 
-    def step(self):
+    def words(self):
         R = self.eng.R
+        if self.fixed:
+            w = full_word(self.eng.cfg["mailbox"], self.eng.cfg["entry_mbox"])
+            return [[w if a != b else 0 for a in range(R) for b in range(R)]
+                    for _ in range(self.world)]
         mine = self.eng.plane_counts()  # synchronises the engine stream
         dev = "cpu" if self.staged else self.device
         t = torch.tensor(mine, dtype=torch.int64, device=dev)
         allw = torch.empty(self.world * R * R, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allw, t, group=self.group)
         flat = allw.tolist()
-        words = [flat[q * R * R:(q + 1) * R * R] for q in range(self.world)]
-        ops = plan(R, self.world, self.rank, words, self.eng.plane_regions)
+        return [flat[q * R * R:(q + 1) * R * R] for q in range(self.world)]
+
+    def step(self):
+        R = self.eng.R
+        ops = plan(R, self.world, self.rank, self.words(),
+                   self.eng.plane_regions)
         self.bytes_sent += sum(n for op, _, (_, n) in ops if op == "send")
         if self.staged:
+            self.eng.sync()
             run_ops_staged(ops, self.device, self.group)
+            torch.cuda.current_stream(self.device).synchronize()
+        elif self.fixed:
+            run_ops_on_stream(ops, lambda p, n: device_bytes(p, n,
+                                                             self.device),
+                              self._stream, self.group)
         else:
             run_ops(ops, lambda p, n: device_bytes(p, n, self.device),
                     self.group)
-        torch.cuda.current_stream(self.device).synchronize()
+            torch.cuda.current_stream(self.device).synchronize()

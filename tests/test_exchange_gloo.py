@@ -88,19 +88,24 @@ class FakePlanes:
         return [(x.ctypes.data, n) for x, n in zip(bufs, self._sizes(word))]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, fixed):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from dragonboat_amd import exchange as X
         fp = FakePlanes(rank)
-        mine = [_word(rank, a, b) if X.place_peer(world, rank, a, b, 0) >= 0
-                else 0 for a in range(R) for b in range(R)]
-        t = torch.tensor(mine, dtype=torch.int64)
-        allw = torch.empty(world * R * R, dtype=torch.int64)
-        dist.all_gather_into_tensor(allw, t)
-        flat = allw.tolist()
-        words = [flat[k * R * R:(k + 1) * R * R] for k in range(world)]
+        if fixed:  # full-capacity planes: no sizes are exchanged
+            w = X.full_word(13, 3)
+            words = [[w if a != b else 0 for a in range(R) for b in range(R)]
+                     for _ in range(world)]
+        else:
+            mine = [_word(rank, a, b) if X.place_peer(world, rank, a, b, 0)
+                    >= 0 else 0 for a in range(R) for b in range(R)]
+            t = torch.tensor(mine, dtype=torch.int64)
+            allw = torch.empty(world * R * R, dtype=torch.int64)
+            dist.all_gather_into_tensor(allw, t)
+            flat = allw.tolist()
+            words = [flat[k * R * R:(k + 1) * R * R] for k in range(world)]
         ops = X.plan(R, world, rank, words, fp.regions)
         X.run_ops(ops, X.host_bytes)
         got = {k: [x.copy() for x in v] for k, v in fp.inb.items()}
@@ -109,13 +114,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_plane_exchange_gloo(world):
+@pytest.mark.parametrize("world,fixed", [(2, False), (3, False), (3, True)])
+def test_plane_exchange_gloo(world, fixed):
     from dragonboat_amd import exchange as X
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, fixed))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -143,3 +148,14 @@ def test_plane_exchange_gloo(world):
                     assert (d[:n] == e[:n]).all(), (r, a, b)
                     moved += n
     assert moved > 0
+
+
+def test_full_word_layout():
+    """A full-capacity word lists every record position of both chunks,
+    the header, the max LogIndex word and E entry rows (drb_plane_regions
+    sizing, restated by _layout)."""
+    from dragonboat_amd import exchange as X
+    w = X.full_word(13, 3)
+    assert _layout(w) == [(0, 13 * LANES * 16), (2, 13 * LANES * 16),
+                          (4, LANES * 16), (5, LANES * 8), (6, LANES * 8),
+                          (7, 3 * 5 * LANES * 16)]

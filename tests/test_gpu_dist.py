@@ -51,7 +51,7 @@ def test_device_view_aliases_engine_memory():
     e.close()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, fixed):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -67,7 +67,7 @@ def _worker(rank, world, port, q):
                      max_props=2)
         eng.init_steady(term=2, leader_slot=0, seed=seed)
         xch = PlaneExchange(eng, world, rank, torch.device("cuda", 0),
-                            staged=True)
+                            staged=True, fixed=fixed)
         tot = 0
         for t in range(ROUNDS):
             counts, ents, pool = workload.build_batch(G, 1, seed, t)
@@ -100,14 +100,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_c4_processes_exchange_planes(world):
+@pytest.mark.parametrize("world,fixed", [(2, False), (3, False), (2, True),
+                                         (3, True)])
+def test_c4_processes_exchange_planes(world, fixed):
     from dragonboat_amd import workload
     from oracle import pyoracle as po
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, fixed))
              for r in range(world)]
     for p in procs:
         p.start()
