@@ -1469,6 +1469,14 @@ static int refresh_roles(drb_engine *e) {
   return DRB_OK;
 }
 
+extern "C" int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
+                              uint32_t *follower_slots) {
+  if (!e) return DRB_EINVAL;
+  if (leader_slots) *leader_slots = e->role_slots[0];
+  if (follower_slots) *follower_slots = e->role_slots[1];
+  return DRB_OK;
+}
+
 extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (!e || !in) return DRB_EINVAL;
   // a durable LogDB: the last round's messages wait for its persistence

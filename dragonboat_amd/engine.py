@@ -43,6 +43,7 @@ SIGNATURES = {
                                  PU8, SZ]),
     "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
     "drb_host_slot": (C.c_int, [P, U32, C.c_int]),
+    "drb_role_slots": (C.c_int, [P, PU32, PU32]),
     "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8,
                                       SZ]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
@@ -212,6 +213,13 @@ class Engine:
         _ck(lib().drb_export_log(self.h, g, slot, lo, hi, arr, pool, pcap),
             "drb_export_log")
         return [entry_to_tuple(arr[i], pool) for i in range(n)]
+
+    def role_slots(self):
+        """(leader slot mask, follower slot mask) of the hosted replicas."""
+        a, b = U32(), U32()
+        _ck(lib().drb_role_slots(self.h, C.byref(a), C.byref(b)),
+            "drb_role_slots")
+        return a.value, b.value
 
     def host_slot(self, slot, hosted):
         _ck(lib().drb_host_slot(self.h, slot, int(bool(hosted))),

@@ -61,11 +61,28 @@ def place_peer(world, rank, a, b, direction):
     return _engine.lib().drb_place_peer(world, rank, a, b, direction)
 
 
-def full_word(mailbox, entry_mbox):
+def full_word(mailbox, entry_mbox, leader_sender=True):
     """The summary word of a plane at full capacity (drb_plane_regions):
-    every record position, both chunks, the header and every entry row."""
-    return (mailbox & 0x1f) | ((entry_mbox & 0xff) << 10) | (1 << 18) | \
-        (1 << 19)
+    every record position, both chunks, the header, and -- when the sender
+    slot may hold leaders -- the max LogIndex word and every entry row.  A
+    follower-only sender slot sends responses (other records) only."""
+    if leader_sender:
+        return (mailbox & 0x1f) | ((entry_mbox & 0xff) << 10) | (1 << 18) | \
+            (1 << 19)
+    return ((mailbox & 0x1f) << 5) | (1 << 18) | (1 << 19)
+
+
+def fixed_words(R, world, leader_mask, mailbox, entry_mbox):
+    """Per-rank plane words of the fixed mode: plane (a, b) moves when a or
+    b is a leader slot on some rank (leader_mask: the OR over the ranks of
+    drb_role_slots), at full capacity."""
+    row = []
+    for a in range(R):
+        for b in range(R):
+            la, lb = (leader_mask >> a) & 1, (leader_mask >> b) & 1
+            row.append(0 if a == b or not (la or lb) else
+                       full_word(mailbox, entry_mbox, bool(la)))
+    return [row for _ in range(world)]
 
 
 def plan(R, world, rank, words, regions):
@@ -148,13 +165,25 @@ class PlaneExchange:
         self.bytes_sent = 0
         self._stream = None if staged else torch.cuda.ExternalStream(
             eng.stream, device=device)
+        self.leader_mask = 0
+        if self.fixed:
+            self.refresh_roles()
+
+    def refresh_roles(self):
+        """Collective: the OR of every rank's leader slots.  Call on every
+        rank after importing replicas (roles change only there)."""
+        dev = "cpu" if self.staged else self.device
+        t = torch.tensor([self.eng.role_slots()[0]], dtype=torch.int64,
+                         device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.BOR, group=self.group)
+        self.leader_mask = int(t.item())
 
     def words(self):
         R = self.eng.R
         if self.fixed:
-            w = full_word(self.eng.cfg["mailbox"], self.eng.cfg["entry_mbox"])
-            return [[w if a != b else 0 for a in range(R) for b in range(R)]
-                    for _ in range(self.world)]
+            return fixed_words(R, self.world, self.leader_mask,
+                               self.eng.cfg["mailbox"],
+                               self.eng.cfg["entry_mbox"])
         mine = self.eng.plane_counts()  # synchronises the engine stream
         dev = "cpu" if self.staged else self.device
         t = torch.tensor(mine, dtype=torch.int64, device=dev)

@@ -564,6 +564,14 @@ int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to, int dir);
 /* The same routing as a pure function of the placement (no device). */
 int drb_place_peer(uint32_t world, uint32_t rank, uint32_t from, uint32_t to,
                    int dir);
+/* The engine's role map, kept on the host (roles change only by init and
+ * import; a replica whose role would change in a round falls back): bit s
+ * of *leader_slots when a hosted replica at slot s is a leader, of
+ * *follower_slots when one is not.  No device work.  With fixed-capacity
+ * exchange, plane (from, to) can carry fast-path messages only when `from`
+ * or `to` is a leader slot on some rank (followers send only to leaders). */
+int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
+                   uint32_t *follower_slots);
 /* The device regions of plane (from, to) for the last round, sized by the
  * SENDER's word: dir 0 in this engine's outbox planes, dir 1 in its inbox
  * planes.  Sender and receiver list identical sizes in the same order.

@@ -95,9 +95,7 @@ def _worker(rank, world, port, q, fixed):
         from dragonboat_amd import exchange as X
         fp = FakePlanes(rank)
         if fixed:  # full-capacity planes: no sizes are exchanged
-            w = X.full_word(13, 3)
-            words = [[w if a != b else 0 for a in range(R) for b in range(R)]
-                     for _ in range(world)]
+            words = X.fixed_words(R, world, 0b101, 13, 3)
         else:
             mine = [_word(rank, a, b) if X.place_peer(world, rank, a, b, 0)
                     >= 0 else 0 for a in range(R) for b in range(R)]
@@ -159,3 +157,15 @@ def test_full_word_layout():
     assert _layout(w) == [(0, 13 * LANES * 16), (2, 13 * LANES * 16),
                           (4, LANES * 16), (5, LANES * 8), (6, LANES * 8),
                           (7, 3 * 5 * LANES * 16)]
+    # a follower-only sender: every record position as "other" records
+    # (positions MB - Ko .. MB - 1 = all of them) and the header
+    w = X.full_word(13, 3, leader_sender=False)
+    assert _layout(w) == [(1, 13 * LANES * 16), (3, 13 * LANES * 16),
+                          (4, LANES * 16)]
+    # leaders at slot 0: planes (0, b) and (a, 0) only
+    ws = X.fixed_words(R, 2, 1, 13, 3)
+    assert ws[0] == ws[1]
+    for a in range(R):
+        for b in range(R):
+            w = ws[0][a * R + b]
+            assert bool(w) == (a != b and 0 in (a, b)), (a, b)
