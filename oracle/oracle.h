@@ -273,6 +273,23 @@ int orc_inmem_last_index(orc_inmem *im, uint64_t *idx);
 int orc_inmem_get_term(orc_inmem *im, uint64_t index, uint64_t *term);
 void orc_inmem_info(orc_inmem *im, uint64_t *out5);
 
+/* ---- batched LogDB records (internal/logdb/batch.go) ------------------ */
+typedef struct orc_batchdb orc_batchdb;
+orc_batchdb *orc_batchdb_new(void);
+void orc_batchdb_free(orc_batchdb *db);
+/* batchedEntries.record of one Update's EntriesToSave: records Put, -1 */
+long orc_batchdb_record(orc_batchdb *db, uint64_t shard, uint64_t replica,
+                        const drb_entry *ents, size_t n, const uint8_t *pool);
+/* record i of the last call: value length (copied to buf), -1 no such
+ * record, < -1 buf too small (-(len) - 2) */
+long orc_batchdb_out(orc_batchdb *db, size_t i, uint64_t *batch, uint8_t *buf,
+                     size_t cap);
+void orc_batch_id_range(uint64_t low, uint64_t high, uint64_t *lo_id,
+                        uint64_t *hi_id);
+int orc_batch_compact(drb_entry *e, size_t n, int restore);
+long orc_batch_merged_first(const drb_entry *eb, size_t ne,
+                            const drb_entry *lb, size_t nl, drb_entry *out);
+
 /* ---- rsm (statemachine.go, encoded.go) : KAT hooks -------------------- */
 long orc_get_payload(uint32_t type, const uint8_t *cmd, size_t clen,
                      uint8_t *out, size_t cap);

@@ -137,6 +137,15 @@ def _declare(L):
         "orc_inmem_info": (None, [P, PU64]),
         "orc_get_payload": (C.c_long, [U32, PU8, C.c_size_t, PU8,
                                        C.c_size_t]),
+        "orc_batchdb_new": (P, []),
+        "orc_batchdb_free": (None, [P]),
+        "orc_batchdb_record": (C.c_long, [P, U64, U64, PE, C.c_size_t, PU8]),
+        "orc_batchdb_out": (C.c_long, [P, C.c_size_t, PU64, PU8,
+                                       C.c_size_t]),
+        "orc_batch_id_range": (None, [U64, U64, PU64, PU64]),
+        "orc_batch_compact": (C.c_int, [PE, C.c_size_t, C.c_int]),
+        "orc_batch_merged_first": (C.c_long, [PE, C.c_size_t, PE, C.c_size_t,
+                                              PE]),
         "orc_sm_new": (P, [U64, U64]),
         "orc_sm_free": (None, [P]),
         "orc_sm_handle": (C.c_long, [P, PE, C.c_size_t, PU8]),
@@ -944,3 +953,57 @@ class StateMachine:
         vl = U32()
         rc = lib().orc_sm_lookup(self.p, _u8(key), len(key), buf, 4096, vl)
         return None if rc else bytes(buf[:vl.value])
+
+
+# ---------------------------------------------------------------- LogDB
+class BatchDB:
+    """batchedEntries (internal/logdb/batch.go) over an in-memory store."""
+
+    def __init__(self):
+        self.p = lib().orc_batchdb_new()
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_batchdb_free(self.p)
+
+    def record(self, shard, replica, entries):
+        """SaveRaftState of one Update: [(batch id, record value)]."""
+        arr, pool, n = EntryPool(entries).arrays()
+        k = _check(lib().orc_batchdb_record(self.p, shard, replica, arr, n,
+                                            pool))
+        out = []
+        for i in range(k):
+            b = U64()
+            buf = (C.c_uint8 * (1 << 20))()
+            ln = lib().orc_batchdb_out(self.p, i, b, buf, len(buf))
+            assert ln >= 0
+            out.append((b.value, bytes(buf[:ln])))
+        return out
+
+
+def batch_id_range(low, high):
+    a, b = U64(), U64()
+    lib().orc_batch_id_range(low, high, a, b)
+    return a.value, b.value
+
+
+def _term_index(entries):
+    arr = (Entry * max(1, len(entries)))()
+    for i, (t, x) in enumerate(entries):
+        arr[i].term, arr[i].index = t, x
+    return arr
+
+
+def batch_compact(entries, restore=False):
+    """compactBatchFields / restoreBatchFields on [(term, index)]."""
+    arr = _term_index(entries)
+    _check(lib().orc_batch_compact(arr, len(entries), int(restore)))
+    return [(arr[i].term, arr[i].index) for i in range(len(entries))]
+
+
+def batch_merged_first(eb, lb):
+    """getMergedFirstBatch on [(term, index)] lists."""
+    a, b = _term_index(eb), _term_index(lb)
+    out = (Entry * max(1, len(eb) + len(lb)))()
+    n = _check(lib().orc_batch_merged_first(a, len(eb), b, len(lb), out))
+    return [(out[i].term, out[i].index) for i in range(n)]
