@@ -129,7 +129,7 @@ class Config(C.Structure):
                 ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
                 ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
                 ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
-                ("reserved1", C.c_uint32)]
+                ("save_batched", C.c_uint32)]
 
 
 class ApplyResult(C.Structure):
@@ -138,6 +138,13 @@ class ApplyResult(C.Structure):
                 ("key", C.c_uint64), ("client_id", C.c_uint64),
                 ("series_id", C.c_uint64), ("value", C.c_uint64),
                 ("slot", C.c_uint32), ("ignored", C.c_uint32)]
+
+
+class SaveRecord(C.Structure):
+    """drb_save_record: one batched LogDB record of the last round."""
+    _fields_ = [("batch", C.c_uint64), ("offset", C.c_uint32),
+                ("len", C.c_uint32), ("crc", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class Flagged(C.Structure):

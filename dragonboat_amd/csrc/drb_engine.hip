@@ -183,6 +183,10 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   if (cfg->max_props == 0 || cfg->prop_slots == 0 || cfg->ri_slots == 0)
     return DRB_EINVAL;
   if (cfg->save_cap % 16) return DRB_EINVAL;
+  // batched records merge from the window: a batch's 47 earlier entries
+  // plus the round's must be resident
+  if (cfg->save_batched && (cfg->save_cap == 0 || cfg->window < 64))
+    return DRB_EINVAL;
   // entry_mbox travels as the 8-bit E of the plane summary word
   // (block_plane_summary, DRB_PLANE_E)
   if (cfg->place_world > 1 &&
@@ -308,6 +312,11 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.save_buf, R * G * v.save_cap16);
     rc |= dalloc(e, &v.save_len, R * G);
     rc |= dalloc(e, &v.save_crc, R * G);
+  }
+  v.save_batched = cfg->save_batched ? 1u : 0u;
+  if (v.save_batched) {
+    rc |= dalloc(e, &v.save_rec, R * G * DRB_SAVE_RECS);
+    rc |= dalloc(e, &v.save_nrec, R * G);
   }
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
@@ -483,10 +492,11 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
       // overflow of escaped fields and the u64 counters
       // a quiesced replica's skipped ticks count from now
       vals[F_QS_BASE] = e->ticks;
+      vals[F_SAVE_BASE] = 0;  // its LogDB record stream restarts
       for (int k = 0; k < NUM_U64; ++k) {
         const bool counter = k == F_TICK_COUNT || k == F_KV_COUNT ||
                              (k >= F_QS_TICK && k <= F_QS_EXIT) ||
-                             k == F_QS_BASE;
+                             k == F_QS_BASE || k == F_SAVE_BASE;
         i64.push_back(u64_ix(v, k, s, g));
         d64.push_back(counter ? vals[k] : (over[k] ? over[k] : vals[k]));
       }
@@ -777,6 +787,7 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   v.u64[u64_ix(v, F_KV_COUNT, s, g)] = 0;
   for (int f = F_QS_TICK; f <= F_QS_EXIT; ++f) v.u64[u64_ix(v, f, s, g)] = vals[f];
   v.u64[u64_ix(v, F_QS_BASE, s, g)] = 0;
+  v.u64[u64_ix(v, F_SAVE_BASE, s, g)] = 0;
   v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
   v.u32[u32_ix(v, W_FLAGS, s, g)] =
       gid(v, s, g) < v.total_groups ? DRB_F_HOSTED : 0u;
@@ -2016,6 +2027,29 @@ extern "C" int drb_export_saved(drb_engine *e, uint64_t group, uint32_t slot,
                           l, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
   }
+  return DRB_OK;
+}
+
+extern "C" int drb_export_save_records(drb_engine *e, uint64_t group,
+                                       uint32_t slot, drb_save_record *out,
+                                       size_t cap, size_t *n) {
+  if (!e || !n || (cap && !out)) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!v.save_batched) return DRB_EINVAL;
+  if (group >= v.G || slot >= v.R) return DRB_ERANGE;
+  uint32_t l = 0, k = 0;
+  uint4 rec[DRB_SAVE_RECS];
+  HIPCHK(hipMemcpyAsync(&l, v.save_len + ix(v, slot, group), 4,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&k, v.save_nrec + ix(v, slot, group), 4,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(rec, v.save_rec + ix(v, slot, group) * DRB_SAVE_RECS,
+                        sizeof(rec), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *n = l ? k : 0;  // save_len 0: nothing saved this round
+  if (*n > cap) return DRB_ERANGE;
+  for (size_t i = 0; i < *n; ++i)
+    out[i] = {rec[i].x, rec[i].y * 16, rec[i].z, rec[i].w, 0};
   return DRB_OK;
 }
 

@@ -56,6 +56,8 @@ enum U64Field : int {
   F_TERM_START,  // every entry in [term_start, last] has term == r.term
   F_QS_BASE,     // engine tick count the replica's ticks are applied up to
                  // (a quiesced replica's ticks are applied lazily)
+  F_SAVE_BASE,   // save_batched: first index of the replica's record
+                 // stream (0: nothing saved yet)
   NUM_U64
 };
 constexpr int NUM_U64_EXPORTED = F_RING_LO;
@@ -302,6 +304,9 @@ struct View {
   uint32_t *save_len;     // [R][G] bytes (0: nothing saved)
   uint32_t *save_crc;     // [R][G] CRC32-IEEE of those bytes
   uint32_t save_cap16;    // save_buf chunks per replica (0: no encoding)
+  uint32_t save_batched;  // drb_config.save_batched
+  uint4 *save_rec;        // [R][G][DRB_SAVE_RECS] {batch, off16, len, crc}
+  uint32_t *save_nrec;    // [R][G] records of the round
   // placement (drb_config) and the cross-rank planes (world >= 2)
   uint32_t place_world, place_rank;
   uint64_t total_groups;

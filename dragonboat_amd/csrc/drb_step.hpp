@@ -1157,21 +1157,18 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
 // inmemory.go:116-122) encoded as one EntryBatch (entrybatch.go:25-58) of
 // colfer Entries (raft_optimized.go:166-300) straight from the resident
 // window, with its CRC32-IEEE.
-template <int R>
-DRB_DEV void encode_saves(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
-                          const uint32_t *crc_tab, uint32_t &n_ent,
-                          uint32_t &n_bytes) {
+// One EntryBatch.Entries element of window entry idx; `compact` writes it
+// with Term and Index zero (compactBatchFields, logdb/batch.go:100-113).
+DRB_DEV void encode_entry(ByteOut &o, const Lane &L, uint64_t idx,
+                          bool compact) {
   const View &v = *L.v;
-  ByteOut o;
-  bo_init(o, v.save_buf + ix(v, L.slot, L.g) * v.save_cap16, v.save_cap16,
-          crc_tab);
-  for (uint64_t idx = lo; idx <= hi; ++idx) {
+  {
     const uint4 m0 = v.ring[ring_ix(v, L.slot, idx, 0, L.g)];
     const uint4 m1 = v.ring[ring_ix(v, L.slot, idx, 1, L.g)];
     const uint4 m2 = v.ring[ring_ix(v, L.slot, idx, 2, L.g)];
     EntryHdr e;
-    e.term = lo64(m0);
-    e.index = idx;
+    e.term = compact ? 0 : lo64(m0);
+    e.index = compact ? 0 : idx;
     e.key = hi64(m0);
     e.client_id = lo64(m1);
     e.series_id = hi64(m1);
@@ -1202,6 +1199,19 @@ DRB_DEV void encode_saves(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
       }
     }
     bo_byte(o, 0x7f);
+  }
+}
+
+template <int R>
+DRB_DEV void encode_saves(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
+                          const uint32_t *crc_tab, uint32_t &n_ent,
+                          uint32_t &n_bytes) {
+  const View &v = *L.v;
+  ByteOut o;
+  bo_init(o, v.save_buf + ix(v, L.slot, L.g) * v.save_cap16, v.save_cap16,
+          crc_tab);
+  for (uint64_t idx = lo; idx <= hi; ++idx) {
+    encode_entry(o, L, idx, false);
     n_ent++;
   }
   const uint32_t crc = bo_finish(o);
@@ -1213,6 +1223,65 @@ DRB_DEV void encode_saves(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
   v.save_len[ix(v, L.slot, L.g)] = o.total;
   v.save_crc[ix(v, L.slot, L.g)] = crc;
   n_bytes += o.total;
+}
+
+// The batched LogDB's records of EntriesToSave [lo, hi]
+// (batchedEntries.record / recordBatch, logdb/batch.go:288-346): one
+// EntryBatch per batch id = index / 48 touched; the first is merged with
+// the batch's entries this replica saved before (getMergedFirstBatch and
+// getLastBatch, :115-141, :369-393 -- in a LogDB fed only by these saves
+// that is the log from max(batch start, first saved index), resident in
+// the window), then compactBatchFields when it holds more than one entry.
+// Records start 16 B aligned in the replica's save buffer.
+constexpr uint64_t LOGDB_BATCH = 48;  // LogDBEntryBatchSize (hard.go:125)
+DRB_DEV uint64_t save_merge_start(uint64_t lo, uint64_t base) {
+  const uint64_t b0 = lo / LOGDB_BATCH;
+  return lo % LOGDB_BATCH ? umax64(b0 * LOGDB_BATCH, base) : lo;
+}
+
+template <int R>
+DRB_DEV void encode_save_records(const Lane &L, Rep<R> &r, uint64_t lo,
+                                 uint64_t hi, const uint32_t *crc_tab,
+                                 uint32_t &n_ent, uint32_t &n_bytes) {
+  const View &v = *L.v;
+  uint64_t base = over_ld(L, F_SAVE_BASE);
+  if (base == 0 || base > lo) {  // the record stream starts here
+    base = lo;
+    over_st(L, F_SAVE_BASE, base);
+  }
+  uint4 *buf = v.save_buf + ix(v, L.slot, L.g) * v.save_cap16;
+  uint32_t off16 = 0, nrec = 0;
+  for (uint64_t b = lo / LOGDB_BATCH; b <= hi / LOGDB_BATCH; ++b) {
+    const uint64_t start =
+        b == lo / LOGDB_BATCH ? save_merge_start(lo, base) : b * LOGDB_BATCH;
+    const uint64_t end = umin64(hi, b * LOGDB_BATCH + LOGDB_BATCH - 1);
+    // compactBatchFields: one term from the first entry to the last (the
+    // indices are contiguous by construction)
+    const bool compact =
+        end > start && ring_term<R>(L, L.slot, start) ==
+                           ring_term<R>(L, L.slot, end);
+    ByteOut o;
+    bo_init(o, buf + off16, off16 < v.save_cap16 ? v.save_cap16 - off16 : 0,
+            crc_tab);
+    for (uint64_t idx = start; idx <= end; ++idx)
+      encode_entry(o, L, idx, compact && idx > start);
+    const uint32_t crc = bo_finish(o);
+    if (o.overflow || nrec >= DRB_SAVE_RECS) {  // bounded by the pre-pass
+      set_error(r, DRB_FB_CAPACITY);
+      v.save_len[ix(v, L.slot, L.g)] = 0;
+      v.save_nrec[ix(v, L.slot, L.g)] = 0;
+      return;
+    }
+    v.save_rec[ix(v, L.slot, L.g) * DRB_SAVE_RECS + nrec] =
+        make_uint4((uint32_t)b, off16, o.total, crc);
+    nrec++;
+    off16 += (o.total + 15) / 16;
+    n_bytes += o.total;
+  }
+  n_ent += (uint32_t)(hi - lo + 1);
+  v.save_len[ix(v, L.slot, L.g)] = off16 * 16;
+  v.save_crc[ix(v, L.slot, L.g)] = 0;
+  v.save_nrec[ix(v, L.slot, L.g)] = nrec;
 }
 
 // ------------------------------------------------------------ served reads
@@ -1880,8 +1949,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       // EntriesToSave lie in [min(committed, saved_to) + 1, new last]
       const uint64_t top = umax64(r.last + nprops, max_app);
       const uint64_t base = umin64(r.committed, r.saved_to);
-      const uint64_t n_save = top > base ? top - base : 0;
-      if (n_save * entrybatch_elem_bound(v.C16 * 16) >
+      uint64_t n_save = top > base ? top - base : 0;
+      uint64_t slack = 0;
+      if (v.save_batched && n_save) {
+        // the records also hold the first batch's earlier entries, which
+        // must still be resident, and start 16 B aligned
+        uint64_t sb = over_ld(L, F_SAVE_BASE);
+        if (sb == 0 || sb > base + 1) sb = base + 1;
+        const uint64_t start = save_merge_start(base + 1, sb);
+        if (start < r.ring_lo ||
+            top / LOGDB_BATCH - (base + 1) / LOGDB_BATCH + 1 > DRB_SAVE_RECS)
+          fb = DRB_FB_CAPACITY;
+        n_save = top - start + 1;
+        slack = 16 * DRB_SAVE_RECS;
+      }
+      if (n_save * entrybatch_elem_bound(v.C16 * 16) + slack >
           (uint64_t)v.save_cap16 * 16)
         fb = DRB_FB_CAPACITY;
     }
@@ -2054,9 +2136,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         if (confirmed_index != r.applied_index)
           st_f(L, r, F_CONFIRMED_INDEX, r.applied_index);
         // SaveRaftState (engine.go:1343) of EntriesToSave
-        if (EXT && has_save && p.encode_saves)
-          encode_saves(L, r, save_lo, r.last, crc_tab, c_saved,
-                       c_saved_bytes);
+        if (EXT && has_save && p.encode_saves) {
+          if (v.save_batched)
+            encode_save_records(L, r, save_lo, r.last, crc_tab, c_saved,
+                                c_saved_bytes);
+          else
+            encode_saves(L, r, save_lo, r.last, crc_tab, c_saved,
+                         c_saved_bytes);
+        }
         // Peer.Commit -> entryLog.commitUpdate (logentry.go:351-371)
         if (has_save) r.saved_to = r.last;  // savedLogTo(last, term(last))
         if (has_apply) r.processed = apply_hi;

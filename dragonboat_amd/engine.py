@@ -43,6 +43,9 @@ SIGNATURES = {
                                  PU8, SZ]),
     "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
     "drb_host_slot": (C.c_int, [P, U32, C.c_int]),
+    "drb_export_save_records": (C.c_int, [P, U64, U32,
+                                          C.POINTER(abi.SaveRecord), SZ,
+                                          C.POINTER(SZ)]),
     "drb_role_slots": (C.c_int, [P, PU32, PU32]),
     "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8,
                                       SZ]),
@@ -132,7 +135,8 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 mailbox=16, kv_slots=512, kv_val_cap=4, election_rtt=10,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
-                kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0)
+                kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
+                save_batched=0)
 
 
 class Engine:
@@ -151,7 +155,7 @@ class Engine:
                    cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
                    cfg["entry_mbox"], cfg["kv_pool_blocks"],
                    cfg["flagged_cap"], cfg["quiesce"],
-                   cfg["durable_log"], 0)
+                   cfg["durable_log"], cfg["save_batched"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -379,6 +383,21 @@ class Engine:
         _ck(lib().drb_export_saved(self.h, g, slot, buf, cap, C.byref(ln),
                                    C.byref(crc)), "drb_export_saved")
         return bytes(buf[:ln.value]), crc.value
+
+    def export_save_records(self, g, slot):
+        """save_batched: [(batch id, record value, crc32)] of one replica's
+        last round, in Put order."""
+        recs = (abi.SaveRecord * 4)()
+        n = SZ()
+        _ck(lib().drb_export_save_records(self.h, g, slot, recs, 4,
+                                          C.byref(n)),
+            "drb_export_save_records")
+        if not n.value:
+            return []
+        data, _ = self.export_saved(g, slot)
+        return [(recs[i].batch, data[recs[i].offset:recs[i].offset +
+                                     recs[i].len], recs[i].crc)
+                for i in range(n.value)]
 
     # ---------------------------------------------------------- exchange
     def plane_counts(self):

@@ -307,7 +307,14 @@ typedef struct drb_config {
    * before the round's messages may be delivered: drb_step_round of round
    * t+1 and drb_encode_wire of round t require drb_commit_round(t) */
   uint32_t durable_log;
-  uint32_t reserved1;
+  /* 1: encode_saves writes the batched LogDB's records of EntriesToSave
+   * (internal/logdb/batch.go:288-346) instead of one EntryBatch: one
+   * EntryBatch record per 48-index batch the round touches (at most
+   * DRB_SAVE_RECS), the first merged with that batch's entries saved in
+   * earlier rounds (getMergedFirstBatch, from the resident window) and
+   * compactBatchFields applied; drb_export_save_records lists them.
+   * Needs window >= 64 and save_cap for a full batch. */
+  uint32_t save_batched;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -527,6 +534,23 @@ int drb_export_read_sums(drb_engine *e, uint64_t first_group,
  * *len = 0 when the replica saved nothing that round. */
 int drb_export_saved(drb_engine *e, uint64_t group, uint32_t slot,
                      uint8_t *buf, size_t cap, uint32_t *len, uint32_t *crc);
+/* save_batched: the round's LogDB records of one replica, in Put order.
+ * Record k is the value of key EntryBatchKey(shard, replica, batch)
+ * (batch.go:310-313): bytes [offset, offset + len) of the replica's
+ * drb_export_saved buffer, with its CRC32-IEEE.  The merge source of a
+ * batch is this engine's own earlier saves of that replica (its LogDB
+ * starts empty at drb_engine_create; an imported replica's record stream
+ * restarts at its next save). */
+#define DRB_SAVE_RECS 4
+typedef struct drb_save_record {
+  uint64_t batch;   /* index / 48 */
+  uint32_t offset;  /* bytes into the replica's save buffer */
+  uint32_t len;
+  uint32_t crc;
+  uint32_t reserved;
+} drb_save_record;
+int drb_export_save_records(drb_engine *e, uint64_t group, uint32_t slot,
+                            drb_save_record *out, size_t cap, size_t *n);
 /* The whole round's save output on the device, for a GPU-side writer or
  * one D2H copy: replica (slot, g) owns bytes[(slot * G + g) * save_cap ..]
  * with lens[slot * G + g] and crcs[slot * G + g]. */

@@ -62,6 +62,7 @@ STRUCTS = {
     "drb_wire_in": abi.WireIn,
     "drb_flagged": abi.Flagged,
     "drb_apply_result": abi.ApplyResult,
+    "drb_save_record": abi.SaveRecord,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}

@@ -179,6 +179,39 @@ def test_entries_to_save_entrybatch_crc(k):
 
 
 @pytest.mark.gpu
+def test_batched_logdb_records_match_oracle():
+    """save_batched (A26 -> F2): every round and replica, the GPU's batched
+    LogDB records (batchedEntries.record, logdb/batch.go:288-346: split at
+    index / 48, the first merged with the batch's earlier saves, then
+    compactBatchFields) equal the oracle's restatement fed the oracle's
+    EntriesToSave, byte for byte with their CRC32, across the batch
+    boundaries at 48 and 96 with 1-3 proposals a round."""
+    import zlib
+    from oracle import pyoracle as po
+    p = Pair(G=12, R=3, window=64, save_cap=8192, max_props=4,
+             save_batched=1)
+    db = po.BatchDB()
+    first = p.eng.cfg["first_shard_id"]
+    n_recs = merged = 0
+    for r in range(45):
+        o, e = p.round(k=1 + r % 3, tick=(r % 2 == 0),
+                       read_index=(r % 5 == 0), encode_saves=True)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        for g in range(p.G):
+            for s in range(p.R):
+                ob, _ = p.orc.export_saved(g, s)
+                ents = po.entrybatch_unmarshal(ob) if ob else []
+                want = [(b, v, zlib.crc32(v)) for b, v in
+                        db.record(first + g, s + 1, ents)] if ents else []
+                got = p.eng.export_save_records(g, s)
+                assert got == want, (r, g, s)
+                n_recs += len(got)
+                merged += sum(len(po.entrybatch_unmarshal(v)) > 1
+                              for _, v, _ in got)
+    assert n_recs and merged
+
+
+@pytest.mark.gpu
 def test_entries_to_save_capacity_falls_back():
     """A save buffer too small for the round's bound hands the replica to
     the CPU path before it mutates (DRB_FB_CAPACITY)."""
