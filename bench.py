@@ -122,6 +122,13 @@ def parse():
 
 
 C5_VAL = {128: 116, 1024: 1011}
+# C5 PBKV key space per group: half the KV slots a replica gets at that
+# payload (16 / 8 slots; values out of line at 1 KB, 4 pool blocks per
+# replica), so a long run upserts existing keys instead of overflowing the
+# table -- with the C3 key space (256) the Poisson tail of groups
+# proposing more than 16 times (1 %/round over ~650 rounds: ~650 groups)
+# fell back on a full table (DRB_FB_CAPACITY at apply)
+C5_KEYS = {128: 8, 1024: 4}
 
 
 def cpu_baseline(args, seconds):
@@ -147,7 +154,8 @@ def cpu_baseline(args, seconds):
         if args.workload == "c5":
             act = workload.active_groups(G, seed, rounds, args.active_ppm)
             counts, ents, pool = workload.build_batch(
-                G, args.k, seed, rounds, 256, C5_VAL[args.payload], act)
+                G, args.k, seed, rounds, C5_KEYS[args.payload],
+                C5_VAL[args.payload], act)
         else:
             counts, ents, pool = workload.build_batch(G, args.k, seed,
                                                       rounds)
@@ -276,7 +284,8 @@ def main():
         # ctx, served inside the round (drb_round_in.reads_per_ctx)
         fused = reads and args.reads_mode == "fused"
         if c5:  # this round's 1 % (an independent draw every round)
-            eng.gen_kv_proposals(i % NP, k, 256, C5_VAL[args.payload], seed,
+            eng.gen_kv_proposals(i % NP, k, C5_KEYS[args.payload],
+                                 C5_VAL[args.payload], seed,
                                  i, active_ppm=args.active_ppm)
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF,
@@ -450,11 +459,13 @@ def main():
                       "CRC32 of EntriesToSave; %%HBM BW" % (
                           G, args.payload, args.active_ppm / 1e4))
             wl = ("C5: %d groups x %d replicas per GPU, %d B PBKV writes "
-                  "(values out of line), %d ppm of the groups proposing per "
+                  "over %d keys per group (values out of line), %d ppm of "
+                  "the groups proposing per "
                   "round (independent seeded draw each round, generated "
                   "inside the timed loop), EntriesToSave encoded (EntryBatch + CRC32), tick "
                   "every %d round(s); Quiesce %s%s" % (
-                      G, R, args.payload, args.active_ppm, args.tick_every,
+                      G, R, args.payload, C5_KEYS[args.payload],
+                      args.active_ppm, args.tick_every,
                       "on" if args.quiesce else "off",
                       ", listed rounds" if args.listed else ""))
             par = "groups sharded, replicas co-resident"

@@ -327,10 +327,10 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   {
     const uint64_t nb = (G + 255) / 256;
     rc |= dalloc(e, &v.act_list, 2 * R * G);
-    rc |= dalloc(e, &v.act_total, 2 * R);
-    rc |= dalloc(e, &v.act_cnt, 2 * R * nb);
-    rc |= dalloc(e, &v.act_off, 2 * R * nb);
-    rc |= dalloc(e, &v.act_mask, 2 * R * nb * 4);
+    rc |= dalloc(e, &v.act_total, 4 * R);
+    rc |= dalloc(e, &v.act_cnt, 4 * R * nb);
+    rc |= dalloc(e, &v.act_off, 4 * R * nb);
+    rc |= dalloc(e, &v.act_mask, 4 * R * nb * 4);
   }
   rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
@@ -1249,6 +1249,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   // tag bytes: one u64 word per (receiver, group), a byte per sender
   std::unordered_map<uint64_t, uint32_t> tw;
   std::vector<uint64_t> tmask;  // sender bytes to set per word
+  std::vector<uint64_t> tbyte;  // their values (tag_byte, drb_msg.hpp)
   for (const InPlane &pl : planes) {
     if (!(mi_count(pl.cur.y) || (pl.cur.x & MQ_QUIESCE))) continue;
     const uint64_t w = ((uint64_t)buf * v.R + pl.to) * v.G + pl.g;
@@ -1257,17 +1258,18 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       it = tw.emplace(w, (uint32_t)tidx.size()).first;
       tidx.push_back(w);
       tmask.push_back(0);
+      tbyte.push_back(0);
     }
     tmask[it->second] |= 0xffull << (8 * pl.from);
+    tbyte[it->second] |= (uint64_t)tag_byte(tag, pl.cur.y) << (8 * pl.from);
   }
   std::vector<uint64_t> tv;
   if (scatter(e, v.ring, eidx, eval) || scatter(e, v.mbox, ridx, rval) ||
       scatter(e, v.mbox_meta, hidx, hval) ||
       scatter(e, v.mbox_maxapp, xidx, xval) || gather(e, v.inbox_tag, tidx, tv))
     return DRB_EDEVICE;
-  const uint64_t tb = tag & 0xffu;
   for (size_t w = 0; w < tidx.size(); ++w)
-    tv[w] = (tv[w] & ~tmask[w]) | (tmask[w] & (tb * 0x0101010101010101ull));
+    tv[w] = (tv[w] & ~tmask[w]) | (tmask[w] & tbyte[w]);
   if (scatter(e, v.inbox_tag, tidx, tv)) return DRB_EDEVICE;
   if (accepted) *accepted = acc;
   if (dropped) *dropped = drop;
@@ -1315,14 +1317,20 @@ static uint32_t slot_list(uint32_t mask, uint32_t *n) {
 // per-block counts into offsets, k_active_scatter writes the lanes.  The
 // step kernels then take 256 listed lanes per block, so a round where most
 // replicas are at rest (C5 with Quiesce) runs dense waves; group order
-// keeps neighbouring lanes' SoA accesses in the same lines.
+// keeps neighbouring lanes' SoA accesses in the same lines.  Each row's
+// list holds the "heavy" lanes first -- a leader with staged proposals, or
+// a replica whose inbox holds a Replicate / ReplicateResp (the tag byte's
+// heavy bit, drb_msg.hpp): it appends, commits, applies, saves -- then the
+// light ones (ticks, heartbeats), so the long paths of a round where 1 %
+// of the groups propose run in dense waves of their own instead of one
+// lane in sixty-four.  Count rows: [(role * R + slot) * 2 + heavy?0:1].
 template <int R>
 __global__ __launch_bounds__(256) void k_active_scan(const View v,
                                                      RoundParams p) {
   const uint32_t s = blockIdx.y;
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t nb = gridDim.x;
-  bool lead = false, run = false;
+  bool lead = false, run = false, heavy = false;
   if (g < v.G) {
     const uint32_t flags = v.u32[u32_ix(v, W_FLAGS, s, g)];
     lead = v.u32[u32_ix(v, W_ROLE, s, g)] == DRB_LEADER;
@@ -1334,21 +1342,41 @@ __global__ __launch_bounds__(256) void k_active_scan(const View v,
         run = !idle_round<R>(v, p, s, g, lead, flags);
       }
     }
+    if (run) {
+      const uint64_t tags =
+          v.inbox_tag[((uint64_t)((p.round - 1) & 1) * v.R + s) * v.G + g];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const uint32_t b = (uint32_t)(tags >> (8 * q)) & 0xffu;
+        if ((uint32_t)q != s && tag_current(b, p.round - 1) &&
+            (b & TAG_HEAVY))
+          heavy = true;
+      }
+      if (lead && stage_here(v, s, lead) && p.prop_slot != DRB_NONE &&
+          v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
+        heavy = true;
+    }
   }
-  const uint64_t bl = __ballot(run && lead), bf = __ballot(run && !lead);
-  __shared__ uint32_t c[2][4];
+  uint64_t bal[4];
+  bal[0] = __ballot(run && lead && heavy);
+  bal[1] = __ballot(run && lead && !heavy);
+  bal[2] = __ballot(run && !lead && heavy);
+  bal[3] = __ballot(run && !lead && !heavy);
+  __shared__ uint32_t c[4][4];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 0) {
-    v.act_mask[(((uint64_t)0 * v.R + s) * nb + blockIdx.x) * 4 + wave] = bl;
-    v.act_mask[(((uint64_t)1 * v.R + s) * nb + blockIdx.x) * 4 + wave] = bf;
-    c[0][wave] = (uint32_t)__popcll(bl);
-    c[1][wave] = (uint32_t)__popcll(bf);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint64_t row = ((uint64_t)(k >> 1) * v.R + s) * 2 + (k & 1);
+      v.act_mask[(row * nb + blockIdx.x) * 4 + wave] = bal[k];
+      c[k][wave] = (uint32_t)__popcll(bal[k]);
+    }
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    const uint32_t t = threadIdx.x;
-    v.act_cnt[((uint64_t)t * v.R + s) * nb + blockIdx.x] =
-        c[t][0] + c[t][1] + c[t][2] + c[t][3];
+  if (threadIdx.x < 4) {
+    const uint32_t k = threadIdx.x;
+    const uint64_t row = ((uint64_t)(k >> 1) * v.R + s) * 2 + (k & 1);
+    v.act_cnt[row * nb + blockIdx.x] = c[k][0] + c[k][1] + c[k][2] + c[k][3];
   }
 }
 
@@ -1385,16 +1413,18 @@ __global__ __launch_bounds__(256) void k_active_scatter(const View v) {
   const uint64_t nb = gridDim.x;
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint32_t t = 0; t < 2; ++t) {
-    const uint64_t row = (uint64_t)t * v.R + s;
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint64_t lrow = (uint64_t)(k >> 1) * v.R + s;  // the list's row
+    const uint64_t row = lrow * 2 + (k & 1);             // its count row
     const uint64_t *m = v.act_mask + (row * nb + blockIdx.x) * 4;
     const uint64_t mw = m[wave];
     if (!((mw >> lane) & 1ull)) continue;
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += (uint32_t)__popcll(m[w]);
-    const uint64_t pos = v.act_off[row * nb + blockIdx.x] + before +
+    const uint64_t base = (k & 1) ? v.act_total[lrow * 2] : 0;  // light
+    const uint64_t pos = base + v.act_off[row * nb + blockIdx.x] + before +
                          (uint32_t)__popcll(mw & ((1ull << lane) - 1ull));
-    v.act_list[row * v.G + pos] = (uint32_t)g;
+    v.act_list[lrow * v.G + pos] = (uint32_t)g;
   }
 }
 
@@ -1403,7 +1433,7 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const unsigned gx = (unsigned)((e->v.G + 255) / 256);
   if (p0.listed) {
     k_active_scan<R><<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v, p0);
-    k_active_prefix<<<2 * e->v.R, 1024, 0, e->stream>>>(e->v, gx);
+    k_active_prefix<<<4 * e->v.R, 1024, 0, e->stream>>>(e->v, gx);
     k_active_scatter<<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v);
   }
   RoundParams pl = p0, pf = p0;

@@ -330,9 +330,9 @@ struct View {
   // listed rounds (drb_round_in.listed): per (role, slot) row the lanes
   // with work this round in group order, and their count
   uint32_t *act_list;               // [2][R][G]
-  unsigned long long *act_total;    // [2][R]
-  uint32_t *act_cnt, *act_off;      // [2][R][blocks]
-  uint64_t *act_mask;               // [2][R][blocks][4] (one word a wave)
+  unsigned long long *act_total;    // [2][R][2 (heavy, light)]
+  uint32_t *act_cnt, *act_off;      // [2][R][2][blocks]
+  uint64_t *act_mask;               // [2][R][2][blocks][4] (a word a wave)
 };
 
 __host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,

@@ -84,6 +84,20 @@ __host__ __device__ inline bool tag_is(uint32_t word, uint64_t round) {
   return (word & MQ_TAG) == ((uint32_t)round & MQ_TAG);
 }
 
+// inbox round-tag byte, one per sender in the receiver's word: bits 0-6
+// the round (mod 128) of the sender's last records to this replica, bit 7
+// set when they include a Replicate or a ReplicateResp -- the receiver's
+// round then appends, commits or applies, and a listed round steps it in
+// the dense "heavy" part of its list (drb_engine.hip, k_active_scan)
+constexpr uint32_t TAG_HEAVY = 0x80u;
+__host__ __device__ inline uint8_t tag_byte(uint64_t round, uint32_t info) {
+  const bool heavy = mi_nrep(info) != 0 || ((info >> MI_NRR) & 0x1fu) != 0;
+  return (uint8_t)((round & 0x7fu) | (heavy ? TAG_HEAVY : 0u));
+}
+__host__ __device__ inline bool tag_current(uint32_t byte, uint64_t round) {
+  return (byte & 0x7fu) == (uint32_t)(round & 0x7fu);
+}
+
 struct Msg {
   uint32_t type, reject, n;
   uint64_t term, log_index, log_term, commit, hint, hint_high;

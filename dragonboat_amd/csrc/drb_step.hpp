@@ -1562,10 +1562,10 @@ DRB_DEV bool idle_round(const View &v, const RoundParams &p, uint32_t slot,
   if (p.tick && !(v.quiesce && (flags & F_QUIESCED))) return false;
   const uint32_t rbuf = (uint32_t)((p.round - 1) & 1);
   const uint64_t tags = v.inbox_tag[((uint64_t)rbuf * v.R + slot) * v.G + g];
-  const uint32_t want = (uint32_t)(p.round - 1) & 0xffu;
 #pragma unroll
   for (int s = 0; s < R; ++s)
-    if ((uint32_t)s != slot && ((tags >> (8 * s)) & 0xffu) == want)
+    if ((uint32_t)s != slot &&
+        tag_current((uint32_t)(tags >> (8 * s)) & 0xffu, p.round - 1))
       return false;
   if (stage_here(v, slot, lead) && p.prop_slot != DRB_NONE &&
       v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
@@ -1702,8 +1702,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   const uint64_t lrow = ((uint64_t)(LEAD ? 0 : 1) * v.R + slot);
   const uint64_t li = (uint64_t)bp.x * blockDim.x + threadIdx.x;
   uint64_t nlisted = 0;
-  if (p.listed) {
-    nlisted = v.act_total[lrow];
+  if (p.listed) {  // the heavy part of the row's list, then the light one
+    nlisted = v.act_total[2 * lrow] + v.act_total[2 * lrow + 1];
     if ((uint64_t)bp.x * blockDim.x >= nlisted) return;  // uniform
   }
   const uint64_t g = p.listed ? (li < nlisted ? v.act_list[lrow * v.G + li]
@@ -2250,7 +2250,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         // the receiver's round tag byte for this sender (a byte store: the
         // other senders own the other bytes of the word)
         ((uint8_t *)&v.inbox_tag[((uint64_t)L.wbuf * v.R + s) * v.G + g])
-            [slot] = (uint8_t)p.round;
+            [slot] = tag_byte(p.round, w);
       }
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
