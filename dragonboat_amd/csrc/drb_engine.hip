@@ -55,11 +55,13 @@ struct drb_engine {
   void *stage_buf = nullptr;  // drb_stage_proposals upload (grow-only)
   size_t stage_bytes = 0;
   struct WireState *wire = nullptr;          // drb_encode_wire (drb_wire.hpp)
+  struct IngestState *ingest = nullptr;      // drb_ingest_wire (drb_ingest.hpp)
   std::mutex ingest_mu;  // drb_ingest: concurrent transport threads
   bool crc_tab_ready = false;  // c_crc_tab uploaded on this engine's device
 };
 
 static void wire_free(drb_engine *e);
+static void ingest_free(struct IngestState *st);
 static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 static int refresh_roles(drb_engine *e);
 
@@ -358,6 +360,7 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   if (e->scratch) (void)hipFree(e->scratch);
   if (e->stage_buf) (void)hipFree(e->stage_buf);
   wire_free(e);
+  ingest_free(e->ingest);
   (void)hipEventDestroy(e->ev_fork);
   (void)hipEventDestroy(e->ev_join);
   (void)hipEventDestroy(e->ev_staged);
@@ -2381,3 +2384,4 @@ extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
 
 // ---------------------------------------------------------------- wire
 #include "drb_wire.hpp"
+#include "drb_ingest.hpp"

@@ -1,0 +1,787 @@
+// drb_ingest.hpp -- the inbound wire path on the GPU (SURVEY 8(f) F1,
+// receive half): the TCP byte stream a peer NodeHost wrote
+// (tcp.go:142-178, transport.go:443-508) taken into the engine's mailbox.
+//
+//   tcp.go readMessage (:180-237)      magic, requestHeader + its CRC
+//                                      (host: 20 B a frame), payload CRC32
+//                                      (GPU: 16 KB chunks, combined per
+//                                      frame with crc32_combine algebra)
+//   MessageBatch.Unmarshal             top-level field walk (host, one
+//     (raft_optimized.go:1056-1207)    thread per frame): where each
+//                                      Requests element starts
+//   Message.Unmarshal (:659-983),      GPU, one lane per message, two
+//     colfer Entry (:308-656)          passes (entry counts, then the
+//                                      decode into SoA records)
+//   Transport.handleRequest's          DeploymentId / BinVer per frame
+//     filter (transport.go:305-316)
+//   IMessageHandler.HandleMessageBatch GPU: messages sorted by (group,
+//     -> MessageQueue.Add (node.go,    sender, receiver) plane (a stable
+//     internal/server/message.go:      radix sort keeps stream order), one
+//     105-123), drb_ingest semantics   lane per plane placing its records,
+//                                      entries, header, max-append word
+//                                      and the receiver's round-tag byte
+//
+// Error behaviour follows the host transport: a frame whose header or
+// payload CRC fails, or whose batch does not decode, is ErrBadMessage --
+// the frames before it are delivered, it and the rest are not
+// (drb_wire_in.bad, .consumed); a snapshot chunk frame (method 200) and an
+// InstallSnapshot message are counted for the CPU path.
+#pragma once
+
+#include <hipcub/hipcub.hpp>
+
+#include <thread>
+
+namespace drb {
+
+// one decoded pb.Message (raftpb/message.go:6-20) of an ingested stream
+struct DecMsg {
+  uint64_t shard, from, to, term, log_term, log_index, commit, hint,
+      hint_high;
+  uint64_t ent0;   // its first entry in the decoded entry array
+  uint32_t type, reject, n_ent, err;  // err: ING_*
+};
+constexpr uint32_t ING_OK = 0, ING_BAD = 1, ING_SNAPSHOT = 2, ING_BIG = 3;
+
+__device__ inline bool d_varint(const uint8_t *d, uint32_t n, uint32_t &i,
+                                uint64_t &v) {
+  v = 0;
+  for (uint32_t s = 0; s < 70; s += 7) {
+    if (i >= n) return false;
+    const uint32_t b = d[i++];
+    v |= (uint64_t)(b & 0x7fu) << s;
+    if (b < 0x80u) return true;
+  }
+  return false;
+}
+
+// skipRaft (raft.pb.go): an unknown field
+__device__ inline bool d_skip(const uint8_t *d, uint32_t n, uint32_t &i,
+                              uint64_t wire) {
+  uint64_t x;
+  switch (wire & 7) {
+    case 0: return d_varint(d, n, i, x);
+    case 1: i += 8; return i <= n;
+    case 2:
+      if (!d_varint(d, n, i, x) || x > n - i) return false;
+      i += (uint32_t)x;
+      return true;
+    case 5: i += 4; return i <= n;
+    default: return false;  // groups are not used by raftpb
+  }
+}
+
+// colfer u64 field body (raft_optimized.go:316-350): varint whose 9th
+// byte is taken whole, or 8 bytes big endian after a 0x80-flagged tag
+__device__ inline bool d_colfer_u64(const uint8_t *d, uint32_t n, uint32_t &i,
+                                    bool flag, uint64_t &v) {
+  if (flag) {
+    if (i + 8 >= n) return false;
+    v = 0;
+    for (int k = 0; k < 8; ++k) v = (v << 8) | d[i + k];
+    i += 8;
+    return true;
+  }
+  v = 0;
+  for (uint32_t s = 0;; s += 7) {
+    if (i + 1 >= n) return false;
+    const uint64_t b = d[i++];
+    if (s == 56 || b < 0x80) {
+      v |= b << s;
+      return true;
+    }
+    v |= (b & 0x7f) << s;
+  }
+}
+
+// colfer Entry.Unmarshal (raft_optimized.go:308-656); cmd_off is the Cmd's
+// offset from d
+__device__ inline bool d_entry(const uint8_t *d, uint32_t n, drb_entry &e) {
+  e.term = e.index = e.key = e.client_id = e.series_id = e.responded_to = 0;
+  e.type = e.cmd_len = 0;
+  e.cmd_off = 0;
+  if (n == 0) return false;
+  uint32_t i = 1;
+  uint32_t h = d[0];
+  for (uint32_t tag = 0; tag < 7; ++tag) {
+    if ((h & 0x7fu) != tag || h == 0x7fu) continue;
+    if (tag == 2) {  // Type: uint32 varint, 0x80 flag = negated
+      uint64_t x = 0;
+      for (uint32_t s = 0;; s += 7) {
+        if (i + 1 >= n) return false;
+        const uint64_t b = d[i++];
+        x |= (b & 0x7f) << s;
+        if (b < 0x80) break;
+        if (s > 28) return false;
+      }
+      e.type = (h & 0x80u) ? (uint32_t)(~(uint32_t)x + 1) : (uint32_t)x;
+    } else {
+      uint64_t x;
+      if (!d_colfer_u64(d, n, i, (h & 0x80u) != 0, x)) return false;
+      switch (tag) {
+        case 0: e.term = x; break;
+        case 1: e.index = x; break;
+        case 3: e.key = x; break;
+        case 4: e.client_id = x; break;
+        case 5: e.series_id = x; break;
+        default: e.responded_to = x; break;
+      }
+    }
+    h = d[i++];
+  }
+  if (h == 7) {  // Cmd (raft_optimized.go:603-641)
+    uint64_t x = 0;
+    for (uint32_t s = 0;; s += 7) {
+      if (i >= n) return false;
+      const uint64_t b = d[i++];
+      x |= (b & 0x7f) << s;
+      if (b < 0x80) break;
+      if (s > 56) return false;
+    }
+    if (x > 16 * 1024 * 1024 || x >= n - i) return false;  // ColferSizeMax
+    e.cmd_off = i;
+    e.cmd_len = (uint32_t)x;
+    i += (uint32_t)x;
+    h = d[i++];
+  }
+  return h == 0x7fu && i == n;
+}
+
+__constant__ uint8_t c_empty_snapshot[24] = {
+    0x12, 0, 0x18, 0, 0x20, 0, 0x28, 0, 0x32, 2, 0x08, 0,
+    0x48, 0, 0x50, 0, 0x58, 0, 0x60, 0, 0x68, 0, 0x70, 0};
+
+// Message.Unmarshal (raft_optimized.go:659-983).  ents == nullptr: count
+// the entries only.  Returns ING_*; *big when a Cmd exceeds cmd_cap.
+__device__ inline uint32_t d_message(const uint8_t *d, uint32_t n, DecMsg &m,
+                                     drb_entry *ents, uint64_t base,
+                                     uint32_t cmd_cap, bool &big) {
+  m.shard = m.from = m.to = m.term = m.log_term = m.log_index = m.commit = 0;
+  m.hint = m.hint_high = 0;
+  m.type = m.reject = m.n_ent = 0;
+  uint32_t i = 0;
+  while (i < n) {
+    uint64_t wire, v;
+    if (!d_varint(d, n, i, wire)) return ING_BAD;
+    const uint64_t field = wire >> 3;
+    const uint32_t wt = (uint32_t)(wire & 7);
+    if (field == 0) return ING_BAD;
+    if ((field >= 1 && field <= 10) || field == 13) {
+      if (wt != 0 || !d_varint(d, n, i, v)) return ING_BAD;
+      switch (field) {
+        case 1: m.type = (uint32_t)v; break;
+        case 2: m.to = v; break;
+        case 3: m.from = v; break;
+        case 4: m.shard = v; break;
+        case 5: m.term = v; break;
+        case 6: m.log_term = v; break;
+        case 7: m.log_index = v; break;
+        case 8: m.commit = v; break;
+        case 9: m.reject = v != 0; break;
+        case 10: m.hint = v; break;
+        default: m.hint_high = v; break;
+      }
+    } else if (field == 11 || field == 12) {
+      uint64_t l;
+      if (wt != 2 || !d_varint(d, n, i, l) || l > n - i) return ING_BAD;
+      if (field == 11) {
+        drb_entry e;
+        if (!d_entry(d + i, (uint32_t)l, e)) return ING_BAD;
+        if (e.cmd_len > cmd_cap) big = true;
+        if (ents) {
+          e.cmd_off += base + i;  // the Cmd's offset in the stream
+          ents[m.n_ent] = e;
+        }
+        m.n_ent++;
+      } else {
+        bool empty = l == 24;
+        for (uint32_t k = 0; empty && k < 24; ++k)
+          empty = d[i + k] == c_empty_snapshot[k];
+        if (!empty) return ING_SNAPSHOT;  // InstallSnapshot: the CPU path
+      }
+      i += (uint32_t)l;
+    } else if (!d_skip(d, n, i, wire)) {
+      return ING_BAD;
+    }
+  }
+  return ING_OK;
+}
+
+// pass 1: entry counts and errors; the frame of a malformed message is
+// marked (the host stops the stream there)
+__global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
+                            const uint32_t *mlen, const uint32_t *mframe,
+                            uint32_t *n_ent, uint32_t *err,
+                            uint32_t *frame_bad, uint64_t n,
+                            uint32_t cmd_cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DecMsg m;
+  bool big = false;
+  uint32_t r = d_message(s + moff[i], mlen[i], m, nullptr, 0, cmd_cap, big);
+  if (r == ING_OK && big) r = ING_BIG;
+  n_ent[i] = r == ING_OK ? m.n_ent : 0;
+  err[i] = r;
+  if (r == ING_BAD) atomicOr(&frame_bad[mframe[i]], 1u);
+  if (r == ING_BIG) atomicOr(&frame_bad[mframe[i]], 2u);
+}
+
+// pass 2: the records and entries of the messages to deliver
+__global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
+                             const uint32_t *mlen, const uint32_t *err,
+                             const uint64_t *ent0, const uint8_t *deliver,
+                             DecMsg *out, drb_entry *ents, uint64_t n,
+                             uint32_t cmd_cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DecMsg m;
+  m.err = ING_BAD;
+  m.ent0 = ent0[i];
+  if (deliver[i] && err[i] == ING_OK) {
+    bool big = false;
+    m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
+                      cmd_cap, big);
+    m.ent0 = ent0[i];
+  }
+  out[i] = m;
+}
+
+// plane keys (group, sender slot, receiver slot); messages drb_ingest would
+// refuse on their shape, or not delivered, sort last (~0)
+__global__ void k_ing_keys(const View v, const DecMsg *dm, uint32_t *key,
+                           uint32_t *val, uint64_t n,
+                           unsigned long long *ctr) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DecMsg m = dm[i];
+  uint32_t k = ~0u;
+  if (m.err == ING_OK) {
+    const uint64_t g = m.shard - v.first_shard_id;
+    const bool ok = g < v.G && m.to >= 1 && m.to <= v.R && m.from >= 1 &&
+                    m.from <= v.R && m.from != m.to && m.n_ent <= v.W;
+    if (ok)
+      k = (uint32_t)((g * v.R + (m.from - 1)) * v.R + (m.to - 1));
+    else
+      atomicAdd(&ctr[1], 1ull);  // dropped
+  }
+  key[i] = k;
+  val[i] = (uint32_t)i;
+}
+
+// one lane per plane (the head of a run of equal keys): MessageQueue.Add of
+// its messages in stream order (drb_engine.hip drb_ingest, restated)
+__global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
+                            const drb_entry *ents, const uint32_t *key,
+                            const uint32_t *idx, uint64_t n, uint32_t buf,
+                            uint32_t tag, unsigned long long *ctr) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= n) return;
+  const uint32_t k = key[i0];
+  if (k == ~0u || (i0 > 0 && key[i0 - 1] == k)) return;
+  const uint32_t to = k % v.R, from = (k / v.R) % v.R;
+  const uint64_t g = (uint64_t)(k / v.R) / v.R;
+  uint64_t i1 = i0 + 1;
+  while (i1 < n && key[i1] == k) ++i1;
+  const uint32_t ft = v.u32[u32_ix(v, W_FLAGS, to, g)];
+  const uint32_t ff = v.u32[u32_ix(v, W_FLAGS, from, g)];
+  const bool live = (ft & DRB_F_HOSTED) && !(ft & (DRB_F_FALLBACK | DRB_F_ERROR));
+  const bool from_hosted =
+      (ff & DRB_F_HOSTED) && !(ff & (DRB_F_FALLBACK | DRB_F_ERROR));
+  if (!live || from_hosted) {  // the transport delivers remote senders only
+    atomicAdd(&ctr[1], (unsigned long long)(i1 - i0));
+    return;
+  }
+  uint4 cur = v.mbox_meta[mmeta_ix(v, buf, from, to, g)];
+  uint64_t maxapp = v.mbox_maxapp[mmeta_ix(v, buf, from, to, g)];
+  if (!tag_is(cur.x, tag)) {  // nothing there yet this round
+    cur = make_uint4(tag & MQ_TAG, 0, 0, 0);
+  }
+  bool maxapp_valid = mi_nrep(cur.y) > 0;
+  uint64_t acc = 0, drop = 0;
+  for (uint64_t j = i0; j < i1; ++j) {
+    const DecMsg m = dm[idx[j]];
+    if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
+      cur.x |= MQ_QUIESCE;
+      acc++;
+      continue;
+    }
+    if (mi_count(cur.y) >= v.MB) {  // MessageQueue full (message.go:105-123)
+      drop++;
+      continue;
+    }
+    const bool rep = m.type == DRB_MSG_REPLICATE;
+    const uint32_t kk =
+        rep ? mi_nrep(cur.y) : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (rep && m.n_ent) {
+      // the entries travel in the sender's (unhosted) window slot
+      for (uint32_t x = 0; x < m.n_ent; ++x) {
+        const drb_entry en = ents[m.ent0 + x];
+        const uint64_t index = m.log_index + 1 + x;
+        uint4 *row = v.ring;
+        row[ring_ix(v, from, index, 0, g)] =
+            make_uint4((uint32_t)en.term, (uint32_t)(en.term >> 32),
+                       (uint32_t)en.key, (uint32_t)(en.key >> 32));
+        row[ring_ix(v, from, index, 1, g)] = make_uint4(
+            (uint32_t)en.client_id, (uint32_t)(en.client_id >> 32),
+            (uint32_t)en.series_id, (uint32_t)(en.series_id >> 32));
+        row[ring_ix(v, from, index, 2, g)] =
+            make_uint4((uint32_t)en.responded_to,
+                       (uint32_t)(en.responded_to >> 32), en.type,
+                       en.cmd_len);
+        for (uint32_t c = 0; c < v.C16; ++c) {
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (uint32_t b = 0; b < 16 && c * 16 + b < en.cmd_len; ++b)
+            w[b >> 2] |= (uint32_t)s[en.cmd_off + c * 16 + b] << (8 * (b & 3));
+          row[ring_ix(v, from, index, ENT_META + c, g)] =
+              make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    }
+    Msg mm;
+    mm.type = m.type;
+    mm.reject = m.reject ? 1 : 0;
+    mm.n = m.n_ent;
+    mm.term = m.term;
+    mm.log_index = m.log_index;
+    mm.log_term = m.log_term;
+    mm.commit = m.commit;
+    mm.hint = m.hint;
+    mm.hint_high = m.hint_high;
+    uint4 c0, c1;
+    msg_encode(mm, to, nullptr, c0, c1);
+    // the sender's term is stored once per (sender, receiver, round) in the
+    // header; a record whose term differs makes the receiver fall back
+    const bool zero = (c0.x & MF_TERM_ZERO) != 0;
+    bool other = false;
+    if (!zero) {
+      if (!(cur.y & MI_TERM)) {
+        cur.z = (uint32_t)m.term;
+        cur.w = (uint32_t)(m.term >> 32);
+      } else if (q_hi(cur) != m.term) {
+        other = true;
+        c0.x |= MF_TERM_OTHER;
+      }
+    }
+    v.mbox[mbox_ix(v, buf, from, to, kk, 0, g)] = c0;
+    v.mbox[mbox_ix(v, buf, from, to, kk, 1, g)] = c1;
+    const uint32_t inf =
+        msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0u);
+    cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
+    if (rep) {
+      const uint64_t ma = m.log_index + m.n_ent;
+      maxapp = maxapp_valid ? umax64(maxapp, ma) : ma;
+      maxapp_valid = true;
+    }
+    acc++;
+  }
+  v.mbox_meta[mmeta_ix(v, buf, from, to, g)] = cur;
+  v.mbox_maxapp[mmeta_ix(v, buf, from, to, g)] = maxapp;
+  if (mi_count(cur.y) || (cur.x & MQ_QUIESCE))  // this sender's tag byte
+    ((uint8_t *)&v.inbox_tag[((uint64_t)buf * v.R + to) * v.G + g])[from] =
+        tag_byte(tag, cur.y);
+  if (acc) atomicAdd(&ctr[0], (unsigned long long)acc);
+  if (drop) atomicAdd(&ctr[1], (unsigned long long)drop);
+}
+
+}  // namespace drb
+
+// ------------------------------------------------------------ host side
+namespace wirehost {
+
+static uint32_t crc_tab[256];
+static uint32_t x2n[32];  // x^(2^k) mod P (zlib x2n_table)
+static std::once_flag crc_once;
+
+static void crc_build() {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k)
+      c = (c & 1) ? drb::CRC32_IEEE_POLY ^ (c >> 1) : c >> 1;
+    crc_tab[i] = c;
+  }
+  uint32_t p = 1u << 30;  // x^1
+  x2n[0] = p;
+  for (int n = 1; n < 32; ++n) x2n[n] = p = drb::gf2_multmodp(p, p);
+}
+// thread-safe: transport threads may call drb_ingest_wire concurrently
+static void crc_init() { std::call_once(crc_once, crc_build); }
+
+static uint32_t crc32_small(const uint8_t *p, size_t n) {
+  uint32_t c = 0xffffffffu;
+  while (n--) c = crc_tab[(c ^ *p++) & 0xff] ^ (c >> 8);
+  return c ^ 0xffffffffu;
+}
+
+// crc32_combine(a, b, len_b) (zlib): CRC(A|B) from CRC(A), CRC(B), |B|
+static uint32_t crc32_combine(uint32_t a, uint32_t b, uint64_t len_b) {
+  uint32_t p = 1u << 31;  // x^0
+  uint32_t k = 3;         // 8 * len_b = len_b * 2^3
+  for (uint64_t n = len_b; n; n >>= 1, ++k)
+    if (n & 1) p = drb::gf2_multmodp(x2n[k & 31], p);
+  return drb::gf2_multmodp(p, a) ^ b;
+}
+
+static uint64_t be(const uint8_t *p, int n) {
+  uint64_t x = 0;
+  for (int k = 0; k < n; ++k) x = (x << 8) | p[k];
+  return x;
+}
+
+static bool varint(const uint8_t *d, size_t n, size_t &i, uint64_t &v) {
+  v = 0;
+  for (unsigned s = 0; s < 70; s += 7) {
+    if (i >= n) return false;
+    const uint8_t b = d[i++];
+    v |= (uint64_t)(b & 0x7f) << s;
+    if (b < 0x80) return true;
+  }
+  return false;
+}
+
+static bool skip(const uint8_t *d, size_t n, size_t &i, uint64_t wire) {
+  uint64_t x;
+  switch (wire & 7) {
+    case 0: return varint(d, n, i, x);
+    case 1: i += 8; return i <= n;
+    case 2:
+      if (!varint(d, n, i, x) || x > n - i) return false;
+      i += (size_t)x;
+      return true;
+    case 5: i += 4; return i <= n;
+    default: return false;
+  }
+}
+
+struct Frame {
+  uint64_t off;   // payload offset in the stream
+  uint64_t size;  // payload bytes
+  uint32_t method, pcrc;
+  bool scan_ok = true;
+  uint64_t did = 0, bv = 0;
+  std::vector<uint64_t> moff;  // Requests elements: stream offset, length
+  std::vector<uint32_t> mlen;
+};
+
+// MessageBatch.Unmarshal's top-level walk (raft_optimized.go:1056-1207):
+// where each Requests element (field 1) lies; DeploymentId, BinVer
+static void scan_batch(const uint8_t *stream, Frame &f) {
+  const uint8_t *p = stream + f.off;
+  const size_t n = (size_t)f.size;
+  size_t j = 0;
+  while (j < n) {
+    uint64_t wire, v;
+    if (!varint(p, n, j, wire) || (wire >> 3) == 0) {
+      f.scan_ok = false;
+      return;
+    }
+    const uint64_t field = wire >> 3;
+    if (field == 1) {
+      uint64_t l;
+      if ((wire & 7) != 2 || !varint(p, n, j, l) || l > n - j) {
+        f.scan_ok = false;
+        return;
+      }
+      f.moff.push_back(f.off + j);
+      f.mlen.push_back((uint32_t)l);
+      j += (size_t)l;
+    } else if (field == 2 || field == 4) {
+      if ((wire & 7) != 0 || !varint(p, n, j, v)) {
+        f.scan_ok = false;
+        return;
+      }
+      (field == 2 ? f.did : f.bv) = v;
+    } else if (!skip(p, n, j, wire)) {
+      f.scan_ok = false;
+      return;
+    }
+  }
+}
+
+}  // namespace wirehost
+
+// device buffers of drb_ingest_wire (grow-only, under ingest_mu)
+struct IngestBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+static int ing_grow(IngestBuf &b, size_t need) {
+  if (need <= b.cap) return DRB_OK;
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = nullptr;
+  HIPCHK(hipMalloc(&b.p, need));
+  b.cap = need;
+  return DRB_OK;
+}
+struct IngestState {
+  IngestBuf stream, msgs, ents, sort, misc;
+};
+static void ingest_free(IngestState *st) {
+  if (!st) return;
+  for (IngestBuf *b : {&st->stream, &st->msgs, &st->ents, &st->sort,
+                       &st->misc})
+    if (b->p) (void)hipFree(b->p);
+  delete st;
+}
+
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
+                               size_t len, uint64_t deployment_id,
+                               drb_wire_in *out) {
+  using namespace drb;
+  if (!e || (!stream && len)) return DRB_EINVAL;
+  // replicas spread over ranks: planes move by drb_exchange_* (drb_ingest)
+  if (e->v.remote_mask) return DRB_ENOSYS;
+  wirehost::crc_init();
+  std::lock_guard<std::mutex> lock(e->ingest_mu);
+  if (!e->ingest) e->ingest = new IngestState();
+  IngestState &st = *e->ingest;
+  const View &v = e->v;
+  drb_wire_in res;
+  memset(&res, 0, sizeof(res));
+  // 1. frames: magic + requestHeader + its CRC (tcp.go:64-112, 180-237)
+  std::vector<wirehost::Frame> fr;
+  size_t i = 0;
+  bool bad_header = false;
+  while (i < len) {
+    if (len - i < 20 || stream[i] != 0xAE || stream[i + 1] != 0x7D) {
+      bad_header = true;
+      break;
+    }
+    uint8_t h[18];
+    memcpy(h, stream + i + 2, 18);
+    const uint32_t hcrc = (uint32_t)wirehost::be(h + 10, 4);
+    memset(h + 10, 0, 4);
+    const uint32_t method = (uint32_t)wirehost::be(h, 2);
+    const uint64_t size = wirehost::be(h + 2, 8);
+    if (wirehost::crc32_small(h, 18) != hcrc ||
+        (method != 100 && method != 200) || size == 0 ||
+        size > len - i - 20) {
+      bad_header = true;  // ErrBadMessage: the connection is closed
+      break;
+    }
+    wirehost::Frame f;
+    f.off = i + 20;
+    f.size = size;
+    f.method = method;
+    f.pcrc = (uint32_t)wirehost::be(h + 14, 4);
+    fr.push_back(std::move(f));
+    i += 20 + (size_t)size;
+  }
+  const size_t walked = i;  // bytes of whole frames
+  // 2. Requests boundaries, one host thread per frame (a frame holds up to
+  // 64 MiB of messages); at most 16 threads
+  {
+    const size_t nt = std::min<size_t>(16, fr.size());
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {
+        for (size_t f = t; f < fr.size(); f += nt)
+          if (fr[f].method == 100) wirehost::scan_batch(stream, fr[f]);
+      });
+    for (auto &x : th) x.join();
+  }
+  uint64_t nm = 0;
+  for (const auto &f : fr) nm += f.moff.size();
+  // 3. the stream up, the payload CRCs in 16 KB chunks
+  constexpr uint64_t CH = 16384;
+  std::vector<uint64_t> coff;
+  std::vector<uint32_t> clen;
+  std::vector<uint32_t> cfirst(fr.size() + 1, 0);
+  for (size_t f = 0; f < fr.size(); ++f) {
+    cfirst[f] = (uint32_t)coff.size();
+    for (uint64_t o = 0; o < fr[f].size; o += CH) {
+      coff.push_back(fr[f].off + o);
+      clen.push_back((uint32_t)std::min<uint64_t>(CH, fr[f].size - o));
+    }
+  }
+  cfirst[fr.size()] = (uint32_t)coff.size();
+  const size_t nc = coff.size();
+  const size_t sb = al256(walked + 16);
+  if (ing_grow(st.stream, sb)) return DRB_EDEVICE;
+  // misc: chunk offsets/lens/crcs, message offsets/lens/frames, counts,
+  // errors, entry bases, deliver flags, per-frame error, 2 counters
+  const size_t m1 = nm ? nm : 1;
+  const size_t mb =
+      al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) + al256(m1 * 4) * 4 +
+      al256(m1 * 8) + al256(m1) + al256((fr.size() + 1) * 4) + 256;
+  if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
+  uint8_t *ds = (uint8_t *)st.stream.p;
+  uint8_t *q = (uint8_t *)st.misc.p;
+  auto take = [&](size_t b) {
+    uint8_t *r = q;
+    q += al256(b);
+    return r;
+  };
+  uint64_t *d_coff = (uint64_t *)take(nc * 8);
+  uint32_t *d_clen = (uint32_t *)take(nc * 4);
+  uint32_t *d_ccrc = (uint32_t *)take(nc * 4);
+  uint64_t *d_moff = (uint64_t *)take(m1 * 8);
+  uint32_t *d_mlen = (uint32_t *)take(m1 * 4);
+  uint32_t *d_mframe = (uint32_t *)take(m1 * 4);
+  uint32_t *d_nent = (uint32_t *)take(m1 * 4);
+  uint32_t *d_err = (uint32_t *)take(m1 * 4);
+  uint64_t *d_ent0 = (uint64_t *)take(m1 * 8);
+  uint8_t *d_deliver = take(m1);
+  uint32_t *d_fbad = (uint32_t *)take((fr.size() + 1) * 4);
+  unsigned long long *d_ctr = (unsigned long long *)take(16);
+  if (!e->crc_tab_ready) {
+    uint32_t tab[8][256];
+    for (uint32_t a = 0; a < 256; ++a) tab[0][a] = wirehost::crc_tab[a];
+    for (uint32_t a = 0; a < 256; ++a)
+      for (int s = 1; s < 8; ++s)
+        tab[s][a] = tab[0][tab[s - 1][a] & 0xff] ^ (tab[s - 1][a] >> 8);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
+    e->crc_tab_ready = true;
+  }
+  std::vector<uint64_t> hmoff;
+  std::vector<uint32_t> hmlen, hmframe;
+  hmoff.reserve(nm);
+  hmlen.reserve(nm);
+  hmframe.reserve(nm);
+  for (size_t f = 0; f < fr.size(); ++f)
+    for (size_t k = 0; k < fr[f].moff.size(); ++k) {
+      hmoff.push_back(fr[f].moff[k]);
+      hmlen.push_back(fr[f].mlen[k]);
+      hmframe.push_back((uint32_t)f);
+    }
+  hipStream_t sm = e->stream;
+  if (walked) HIPCHK(hipMemcpyAsync(ds, stream, walked, hipMemcpyHostToDevice, sm));
+  if (nc) {
+    HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice, sm));
+    k_crc32<<<(unsigned)((nc + 255) / 256), 256, 0, sm>>>(ds, d_coff, d_clen,
+                                                          d_ccrc, nc);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipMemsetAsync(d_fbad, 0, (fr.size() + 1) * 4, sm));
+  HIPCHK(hipMemsetAsync(d_ctr, 0, 16, sm));
+  const uint32_t cmd_cap = v.C16 * 16;
+  if (nm) {
+    HIPCHK(hipMemcpyAsync(d_moff, hmoff.data(), nm * 8, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(d_mlen, hmlen.data(), nm * 4, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(d_mframe, hmframe.data(), nm * 4,
+                          hipMemcpyHostToDevice, sm));
+    k_ing_count<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+        ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad, nm, cmd_cap);
+    HIPCHK(hipGetLastError());
+  }
+  std::vector<uint32_t> ccrc(nc), fbad(fr.size() + 1);
+  if (nc)
+    HIPCHK(hipMemcpyAsync(ccrc.data(), d_ccrc, nc * 4, hipMemcpyDeviceToHost, sm));
+  HIPCHK(hipMemcpyAsync(fbad.data(), d_fbad, (fr.size() + 1) * 4,
+                        hipMemcpyDeviceToHost, sm));
+  HIPCHK(hipStreamSynchronize(sm));
+  // 4. the frames delivered: up to the first with a bad CRC or a batch that
+  // does not decode (ErrBadMessage closes the connection, tcp.go:528-530)
+  std::vector<uint8_t> deliver(m1, 0);
+  std::vector<uint32_t> err_h;
+  size_t consumed = 0;
+  bool big = false;
+  bool any_deliver = false;
+  {
+    size_t mi = 0;
+    for (size_t f = 0; f < fr.size(); ++f) {
+      uint32_t c = 0;
+      for (uint32_t k = cfirst[f]; k < cfirst[f + 1]; ++k)
+        c = k == cfirst[f] ? ccrc[k] : wirehost::crc32_combine(c, ccrc[k],
+                                                               clen[k]);
+      const size_t nmf = fr[f].moff.size();
+      if (c != fr[f].pcrc || !fr[f].scan_ok || (fbad[f] & 1u)) {
+        res.bad = 1;
+        break;
+      }
+      res.frames++;
+      consumed = fr[f].off + fr[f].size;
+      if (fr[f].method == 200) {  // a snapshot Chunk (tcp.go:532-540)
+        res.snapshots++;
+        mi += nmf;
+        continue;
+      }
+      const bool keep = fr[f].did == deployment_id && fr[f].bv == 210;
+      if (keep && (fbad[f] & 2u)) big = true;
+      for (size_t k = 0; k < nmf; ++k) deliver[mi + k] = keep;
+      any_deliver |= keep && nmf;
+      mi += nmf;
+    }
+  }
+  if (bad_header && !res.bad) res.bad = 1;
+  if (big) return DRB_ERANGE;  // a Cmd the window rows cannot hold
+  res.consumed = consumed;
+  // per-message outcomes of the delivered frames (snapshot / filtered)
+  if (nm) {
+    err_h.resize(nm);
+    std::vector<uint32_t> nent(nm);
+    HIPCHK(hipMemcpyAsync(err_h.data(), d_err, nm * 4, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(nent.data(), d_nent, nm * 4, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipStreamSynchronize(sm));
+    // the frames counted above, message by message
+    size_t mi = 0;
+    for (size_t f = 0; f < res.frames; ++f) {
+      const size_t nmf = fr[f].moff.size();
+      if (fr[f].method == 100) {
+        const bool keep = fr[f].did == deployment_id && fr[f].bv == 210;
+        for (size_t k = 0; k < nmf; ++k) {
+          const uint32_t r = err_h[mi + k];
+          if (r == ING_SNAPSHOT) {
+            res.snapshots++;
+          } else if (keep) {
+            res.messages++;
+          } else {
+            res.dropped++;
+          }
+        }
+      }
+      mi += nmf;
+    }
+    // entry bases
+    std::vector<uint64_t> ent0(nm);
+    uint64_t tot = 0;
+    for (size_t k = 0; k < nm; ++k) {
+      ent0[k] = tot;
+      if (deliver[k] && err_h[k] == ING_OK) tot += nent[k];
+    }
+    if (any_deliver) {
+      const size_t eb = al256((tot ? tot : 1) * sizeof(drb_entry));
+      if (ing_grow(st.ents, eb) || ing_grow(st.msgs, al256(nm * sizeof(DecMsg))))
+        return DRB_EDEVICE;
+      HIPCHK(hipMemcpyAsync(d_ent0, ent0.data(), nm * 8, hipMemcpyHostToDevice, sm));
+      HIPCHK(hipMemcpyAsync(d_deliver, deliver.data(), nm, hipMemcpyHostToDevice,
+                            sm));
+      DecMsg *dm = (DecMsg *)st.msgs.p;
+      drb_entry *de = (drb_entry *)st.ents.p;
+      k_ing_decode<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+          ds, d_moff, d_mlen, d_err, d_ent0, d_deliver, dm, de, nm, cmd_cap);
+      HIPCHK(hipGetLastError());
+      // 5. planes: keys, a stable radix sort, one lane per plane
+      size_t tb = 0;
+      uint32_t *kin = nullptr, *kout = nullptr, *vin = nullptr, *vout = nullptr;
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin,
+                                                vout, (int)nm, 0, 32, sm));
+      const size_t sbytes = al256(nm * 4) * 4 + al256(tb);
+      if (ing_grow(st.sort, sbytes)) return DRB_EDEVICE;
+      uint8_t *sp = (uint8_t *)st.sort.p;
+      kin = (uint32_t *)sp;
+      kout = (uint32_t *)(sp + al256(nm * 4));
+      vin = (uint32_t *)(sp + 2 * al256(nm * 4));
+      vout = (uint32_t *)(sp + 3 * al256(nm * 4));
+      void *tmp = sp + 4 * al256(nm * 4);
+      k_ing_keys<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+          v, dm, kin, vin, nm, d_ctr);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout,
+                                                (int)nm, 0, 32, sm));
+      k_ing_place<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+          v, ds, dm, de, kout, vout, nm, (uint32_t)(e->round & 1),
+          (uint32_t)e->round, d_ctr);
+      HIPCHK(hipGetLastError());
+      unsigned long long ctr[2];
+      HIPCHK(hipMemcpyAsync(ctr, d_ctr, 16, hipMemcpyDeviceToHost, sm));
+      HIPCHK(hipStreamSynchronize(sm));
+      res.accepted = ctr[0];
+      res.dropped += ctr[1];
+    }
+  }
+  if (out) *out = res;
+  return DRB_OK;
+}

@@ -859,313 +859,3 @@ extern "C" int drb_export_wire(drb_engine *e, uint8_t *out, size_t cap,
   HIPCHK(hipStreamSynchronize(e->stream));
   return DRB_OK;
 }
-
-// ------------------------------------------------------------ inbound
-// The receiving side of the same connection: tcp.go readMessage
-// (tcp.go:180-237: header decode + CRC, payload CRC), MessageBatch.Unmarshal
-// (raft_optimized.go:1056-1207), Message.Unmarshal (:659-983) with colfer
-// Entries (:308-656), Transport.handleRequest's DeploymentId / BinVer
-// filter (transport.go:305-316), then drb_ingest (HandleMessageBatch).
-// Host code: the bytes arrive in host memory from the socket.
-namespace wirehost {
-
-static uint32_t crc_tab[8][256];
-static std::once_flag crc_once;
-
-static void crc_build() {
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k)
-      c = (c & 1) ? drb::CRC32_IEEE_POLY ^ (c >> 1) : c >> 1;
-    crc_tab[0][i] = c;
-  }
-  for (uint32_t i = 0; i < 256; ++i)
-    for (int s = 1; s < 8; ++s)
-      crc_tab[s][i] = crc_tab[0][crc_tab[s - 1][i] & 0xff] ^
-                      (crc_tab[s - 1][i] >> 8);
-}
-// thread-safe: transport threads may call drb_ingest_wire concurrently
-static void crc_init() { std::call_once(crc_once, crc_build); }
-
-// slicing-by-8 CRC32-IEEE (Go crc32.ChecksumIEEE)
-static uint32_t crc32(const uint8_t *p, size_t n) {
-  uint32_t c = 0xffffffffu;
-  while (n >= 8) {
-    uint32_t lo, hi;
-    memcpy(&lo, p, 4);
-    memcpy(&hi, p + 4, 4);
-    lo ^= c;
-    c = crc_tab[7][lo & 0xff] ^ crc_tab[6][(lo >> 8) & 0xff] ^
-        crc_tab[5][(lo >> 16) & 0xff] ^ crc_tab[4][lo >> 24] ^
-        crc_tab[3][hi & 0xff] ^ crc_tab[2][(hi >> 8) & 0xff] ^
-        crc_tab[1][(hi >> 16) & 0xff] ^ crc_tab[0][hi >> 24];
-    p += 8;
-    n -= 8;
-  }
-  while (n--) c = crc_tab[0][(c ^ *p++) & 0xff] ^ (c >> 8);
-  return c ^ 0xffffffffu;
-}
-
-static uint64_t be(const uint8_t *p, int n) {
-  uint64_t x = 0;
-  for (int k = 0; k < n; ++k) x = (x << 8) | p[k];
-  return x;
-}
-
-// protobuf varint (gogo generated decoders: at most 10 bytes)
-static bool varint(const uint8_t *d, size_t n, size_t &i, uint64_t &v) {
-  v = 0;
-  for (unsigned s = 0; s < 70; s += 7) {
-    if (i >= n) return false;
-    const uint8_t b = d[i++];
-    v |= (uint64_t)(b & 0x7f) << s;
-    if (b < 0x80) return true;
-  }
-  return false;
-}
-
-// skipRaft (raft.pb.go): an unknown field
-static bool skip(const uint8_t *d, size_t n, size_t &i, uint64_t wire) {
-  uint64_t x;
-  switch (wire & 7) {
-    case 0: return varint(d, n, i, x);
-    case 1: i += 8; return i <= n;
-    case 2:
-      if (!varint(d, n, i, x) || x > n - i) return false;
-      i += (size_t)x;
-      return true;
-    case 5: i += 4; return i <= n;
-    default: return false;  // groups are not used by raftpb
-  }
-}
-
-// colfer u64 field body: varint whose 9th byte is taken whole, or 8 bytes
-// big endian after a 0x80-flagged tag (raft_optimized.go:316-350); the
-// entry's next header must follow
-static bool colfer_u64(const uint8_t *d, size_t n, size_t &i, bool flag,
-                       uint64_t &v) {
-  if (flag) {
-    if (i + 8 >= n) return false;
-    v = be(d + i, 8);
-    i += 8;
-    return true;
-  }
-  v = 0;
-  for (unsigned s = 0;; s += 7) {
-    if (i + 1 >= n) return false;
-    const uint64_t b = d[i++];
-    if (s == 56 || b < 0x80) {
-      v |= b << s;
-      return true;
-    }
-    v |= (b & 0x7f) << s;
-  }
-}
-
-static bool entry(const uint8_t *d, size_t n, drb_entry &e,
-                  std::vector<uint8_t> &pool) {
-  memset(&e, 0, sizeof(e));
-  if (n == 0) return false;
-  size_t i = 1;
-  uint8_t h = d[0];
-  uint64_t *u64s[7] = {&e.term, &e.index, nullptr, &e.key, &e.client_id,
-                       &e.series_id, &e.responded_to};
-  for (uint32_t tag = 0; tag < 7; ++tag) {
-    if ((h & 0x7f) != tag || h == 0x7f) continue;
-    if (tag == 2) {  // Type: uint32 varint, 0x80 flag = negated
-      uint64_t x = 0;
-      for (unsigned s = 0;; s += 7) {
-        if (i + 1 >= n) return false;
-        const uint64_t b = d[i++];
-        x |= (b & 0x7f) << s;
-        if (b < 0x80) break;
-        if (s > 28) return false;
-      }
-      e.type = (h & 0x80) ? (uint32_t)(~(uint32_t)x + 1) : (uint32_t)x;
-    } else if (!colfer_u64(d, n, i, (h & 0x80) != 0, *u64s[tag])) {
-      return false;
-    }
-    h = d[i++];
-  }
-  if (h == 7) {  // Cmd (raft_optimized.go:603-641)
-    uint64_t x = 0;
-    for (unsigned s = 0;; s += 7) {
-      if (i >= n) return false;
-      const uint64_t b = d[i++];
-      x |= (b & 0x7f) << s;
-      if (b < 0x80) break;
-      if (s > 56) return false;
-    }
-    if (x > 16 * 1024 * 1024 || x >= n - i) return false;  // ColferSizeMax
-    e.cmd_off = pool.size();
-    e.cmd_len = (uint32_t)x;
-    pool.insert(pool.end(), d + i, d + i + x);
-    i += (size_t)x;
-    h = d[i++];
-  }
-  return h == 0x7f && i == n;
-}
-
-static const uint8_t kEmptySnapshot[24] = {
-    0x12, 0, 0x18, 0, 0x20, 0, 0x28, 0, 0x32, 2, 0x08, 0,
-    0x48, 0, 0x50, 0, 0x58, 0, 0x60, 0, 0x68, 0, 0x70, 0};
-
-// 0: ok, -1: malformed, -2: carries a snapshot (not on this path)
-static int message(const uint8_t *d, size_t n, drb_message &m,
-                   std::vector<drb_entry> &ents, std::vector<uint8_t> &pool) {
-  memset(&m, 0, sizeof(m));
-  m.entries_off = ents.size();
-  size_t i = 0;
-  while (i < n) {
-    uint64_t wire, v;
-    if (!varint(d, n, i, wire)) return -1;
-    const uint64_t field = wire >> 3;
-    const uint32_t wt = (uint32_t)(wire & 7);
-    if (field == 0) return -1;
-    if ((field >= 1 && field <= 10) || field == 13) {
-      if (wt != 0 || !varint(d, n, i, v)) return -1;
-      switch (field) {
-        case 1: m.type = (uint32_t)v; break;
-        case 2: m.to = v; break;
-        case 3: m.from = v; break;
-        case 4: m.shard_id = v; break;
-        case 5: m.term = v; break;
-        case 6: m.log_term = v; break;
-        case 7: m.log_index = v; break;
-        case 8: m.commit = v; break;
-        case 9: m.reject = v != 0; break;
-        case 10: m.hint = v; break;
-        default: m.hint_high = v; break;
-      }
-    } else if (field == 11 || field == 12) {
-      uint64_t l;
-      if (wt != 2 || !varint(d, n, i, l) || l > n - i) return -1;
-      if (field == 11) {
-        drb_entry e;
-        if (!entry(d + i, (size_t)l, e, pool)) return -1;
-        ents.push_back(e);
-        m.n_entries++;
-      } else if (l != sizeof(kEmptySnapshot) ||
-                 memcmp(d + i, kEmptySnapshot, sizeof(kEmptySnapshot))) {
-        return -2;
-      }
-      i += (size_t)l;
-    } else if (!skip(d, n, i, wire)) {
-      return -1;
-    }
-  }
-  return 0;
-}
-
-}  // namespace wirehost
-
-extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
-                               size_t len, uint64_t deployment_id,
-                               drb_wire_in *out) {
-  if (!e || (!stream && len)) return DRB_EINVAL;
-  // replicas spread over ranks: planes move by drb_exchange_* (drb_ingest)
-  if (e->v.remote_mask) return DRB_ENOSYS;
-  wirehost::crc_init();
-  drb_wire_in res;
-  memset(&res, 0, sizeof(res));
-  std::vector<drb_message> msgs;
-  std::vector<drb_entry> ents;
-  std::vector<uint8_t> pool;
-  size_t i = 0;
-  while (i < len) {
-    // magic + requestHeader (tcp.go:64-112, readMagicNumber / readMessage)
-    if (len - i < 20 || stream[i] != 0xAE || stream[i + 1] != 0x7D) {
-      res.bad = 1;
-      break;
-    }
-    uint8_t h[18];
-    memcpy(h, stream + i + 2, 18);
-    const uint32_t hcrc = (uint32_t)wirehost::be(h + 10, 4);
-    memset(h + 10, 0, 4);
-    const uint32_t method = (uint32_t)wirehost::be(h, 2);
-    const uint64_t size = wirehost::be(h + 2, 8);
-    const uint32_t pcrc = (uint32_t)wirehost::be(h + 14, 4);
-    if (wirehost::crc32(h, 18) != hcrc || (method != 100 && method != 200) ||
-        size == 0 || size > len - i - 20) {
-      res.bad = 1;  // ErrBadMessage: the connection is closed
-      break;
-    }
-    const uint8_t *p = stream + i + 20;
-    if (wirehost::crc32(p, (size_t)size) != pcrc) {
-      res.bad = 1;
-      break;
-    }
-    i += 20 + (size_t)size;
-    res.frames++;
-    if (method == 200) {  // snapshotType: a Chunk (tcp.go:532-540), CPU path
-      res.snapshots++;
-      continue;
-    }
-    // MessageBatch.Unmarshal
-    const size_t m0 = msgs.size(), e0 = ents.size(), p0 = pool.size();
-    uint64_t did = 0, bv = 0;
-    size_t j = 0;
-    bool ok = true;
-    while (ok && j < size) {
-      uint64_t wire, v;
-      if (!wirehost::varint(p, size, j, wire) || (wire >> 3) == 0) {
-        ok = false;
-        break;
-      }
-      const uint64_t field = wire >> 3;
-      if (field == 1) {
-        uint64_t l;
-        if ((wire & 7) != 2 || !wirehost::varint(p, size, j, l) ||
-            l > size - j) {
-          ok = false;
-          break;
-        }
-        drb_message m;
-        const int rc = wirehost::message(p + j, (size_t)l, m, ents, pool);
-        if (rc == -1) {
-          ok = false;
-          break;
-        }
-        if (rc == -2)
-          res.snapshots++;  // InstallSnapshot: the CPU path's business
-        else
-          msgs.push_back(m);
-        j += (size_t)l;
-      } else if (field == 2 || field == 4) {
-        if ((wire & 7) != 0 || !wirehost::varint(p, size, j, v)) {
-          ok = false;
-          break;
-        }
-        (field == 2 ? did : bv) = v;
-      } else if (!wirehost::skip(p, size, j, wire)) {
-        ok = false;
-      }
-    }
-    if (!ok) {  // Unmarshal error: the connection is closed (tcp.go:528-530)
-      msgs.resize(m0);
-      ents.resize(e0);
-      pool.resize(p0);
-      res.bad = 1;
-      break;
-    }
-    if (did != deployment_id || bv != 210) {  // transport.go:305-316
-      res.dropped += msgs.size() - m0;
-      msgs.resize(m0);
-      ents.resize(e0);
-      pool.resize(p0);
-    }
-  }
-  res.consumed = i;
-  res.messages = msgs.size();
-  if (!msgs.empty()) {
-    uint64_t acc = 0, drop = 0;
-    const int rc = drb_ingest(e, msgs.data(), msgs.size(), ents.data(),
-                              pool.empty() ? nullptr : pool.data(), &acc,
-                              &drop);
-    if (rc) return rc;
-    res.accepted = acc;
-    res.dropped += drop;
-  }
-  if (out) *out = res;
-  return DRB_OK;
-}

@@ -726,8 +726,12 @@ typedef struct drb_wire_in {
  * CRC32), MessageBatch / Message / colfer Entry Unmarshal
  * (raft_optimized.go:308-656, 659-983, 1056-1207), the DeploymentId /
  * BinVer filter of Transport.handleRequest (transport.go:305-316), then
- * drb_ingest.  Frames are consumed in order; a bad frame stops the stream
- * as ErrBadMessage closes the connection. */
+ * drb_ingest's placement.  Frames are consumed in order; a bad frame stops
+ * the stream as ErrBadMessage closes the connection.  The stream is
+ * uploaded once: payload CRCs, message decode and placement run on the
+ * GPU (drb_ingest.hpp); the host reads the 20 B frame headers and walks
+ * each batch's top-level fields.  DRB_ERANGE (nothing placed) when a
+ * delivered entry's Cmd exceeds cmd_cap. */
 int drb_ingest_wire(drb_engine *e, const uint8_t *stream, size_t len,
                     uint64_t deployment_id, drb_wire_in *out);
 
