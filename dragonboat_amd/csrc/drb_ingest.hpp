@@ -226,18 +226,65 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   if (r == ING_BIG) atomicOr(&frame_bad[mframe[i]], 2u);
 }
 
+// the frame of each message: the last frame whose first message is <= i
+__global__ void k_ing_frames(const uint64_t *mbase, uint32_t nf,
+                             uint32_t *mframe, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t lo = 0, hi = nf;  // mbase[lo] <= i < mbase[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (mbase[mid] <= i) lo = mid; else hi = mid;
+  }
+  mframe[i] = lo;
+}
+
+// the outcome of each message once the host decided which frames are
+// delivered (fstate: 0 past the stream's end, 1 delivered, 2 filtered by
+// DeploymentId / BinVer): its entry count for the decode's scan, and the
+// drb_wire_in tallies (ctr[2] snapshots, [3] messages, [4] filtered,
+// [5] entries), one atomic per wave and counter
+__global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
+                            const uint32_t *err, const uint32_t *n_ent,
+                            uint32_t *nsc, uint8_t *deliver, uint64_t n,
+                            unsigned long long *ctr) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t st = 0, r = ING_BAD, ne = 0;
+  if (i < n) {
+    st = fstate[mframe[i]];
+    r = err[i];
+    ne = n_ent[i];
+  }
+  const bool dl = st == 1 && r == ING_OK;
+  if (i < n) {
+    nsc[i] = dl ? ne : 0u;
+    deliver[i] = dl ? 1 : 0;
+  }
+  const bool snap = st != 0 && r == ING_SNAPSHOT;
+  const bool msg = st == 1 && r != ING_SNAPSHOT;
+  const bool filt = st == 2 && r != ING_SNAPSHOT;
+  const uint64_t b0 = __ballot(snap), b1 = __ballot(msg), b2 = __ballot(filt);
+  uint32_t e = dl ? ne : 0u;
+  for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o);
+  if ((threadIdx.x & 63) == 0) {
+    if (b0) atomicAdd(&ctr[2], (unsigned long long)__popcll(b0));
+    if (b1) atomicAdd(&ctr[3], (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(&ctr[4], (unsigned long long)__popcll(b2));
+    if (e) atomicAdd(&ctr[5], (unsigned long long)e);
+  }
+}
+
 // pass 2: the records and entries of the messages to deliver
 __global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
-                             const uint32_t *mlen, const uint32_t *err,
-                             const uint64_t *ent0, const uint8_t *deliver,
-                             DecMsg *out, drb_entry *ents, uint64_t n,
-                             uint32_t cmd_cap) {
+                             const uint32_t *mlen, const uint32_t *ent0,
+                             const uint8_t *deliver, DecMsg *out,
+                             drb_entry *ents, uint64_t n, uint32_t cmd_cap) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   DecMsg m;
   m.err = ING_BAD;
   m.ent0 = ent0[i];
-  if (deliver[i] && err[i] == ING_OK) {
+  if (deliver[i]) {
     bool big = false;
     m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
                       cmd_cap, big);
@@ -602,9 +649,11 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // misc: chunk offsets/lens/crcs, message offsets/lens/frames, counts,
   // errors, entry bases, deliver flags, per-frame error, 2 counters
   const size_t m1 = nm ? nm : 1;
-  const size_t mb =
-      al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) + al256(m1 * 4) * 4 +
-      al256(m1 * 8) + al256(m1) + al256((fr.size() + 1) * 4) + 256;
+  const size_t nf = fr.size();
+  const size_t mb = al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) +
+                    al256(m1 * 4) * 6 + al256(m1) +
+                    al256((nf + 1) * 4) + al256((nf + 1) * 8) +
+                    al256(nf + 1) + 256;
   if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
   uint8_t *ds = (uint8_t *)st.stream.p;
   uint8_t *q = (uint8_t *)st.misc.p;
@@ -621,10 +670,13 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint32_t *d_mframe = (uint32_t *)take(m1 * 4);
   uint32_t *d_nent = (uint32_t *)take(m1 * 4);
   uint32_t *d_err = (uint32_t *)take(m1 * 4);
-  uint64_t *d_ent0 = (uint64_t *)take(m1 * 8);
+  uint32_t *d_nsc = (uint32_t *)take(m1 * 4);
+  uint32_t *d_ent0 = (uint32_t *)take(m1 * 4);
   uint8_t *d_deliver = take(m1);
-  uint32_t *d_fbad = (uint32_t *)take((fr.size() + 1) * 4);
-  unsigned long long *d_ctr = (unsigned long long *)take(16);
+  uint32_t *d_fbad = (uint32_t *)take((nf + 1) * 4);
+  uint64_t *d_mbase = (uint64_t *)take((nf + 1) * 8);
+  uint8_t *d_fstate = take(nf + 1);
+  unsigned long long *d_ctr = (unsigned long long *)take(64);
   if (!e->crc_tab_ready) {
     uint32_t tab[8][256];
     for (uint32_t a = 0; a < 256; ++a) tab[0][a] = wirehost::crc_tab[a];
@@ -634,17 +686,9 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
     e->crc_tab_ready = true;
   }
-  std::vector<uint64_t> hmoff;
-  std::vector<uint32_t> hmlen, hmframe;
-  hmoff.reserve(nm);
-  hmlen.reserve(nm);
-  hmframe.reserve(nm);
-  for (size_t f = 0; f < fr.size(); ++f)
-    for (size_t k = 0; k < fr[f].moff.size(); ++k) {
-      hmoff.push_back(fr[f].moff[k]);
-      hmlen.push_back(fr[f].mlen[k]);
-      hmframe.push_back((uint32_t)f);
-    }
+  // each frame's Requests go up straight from its scan vectors
+  std::vector<uint64_t> mbase(nf + 1, 0);
+  for (size_t f = 0; f < nf; ++f) mbase[f + 1] = mbase[f] + fr[f].moff.size();
   hipStream_t sm = e->stream;
   if (walked) HIPCHK(hipMemcpyAsync(ds, stream, walked, hipMemcpyHostToDevice, sm));
   if (nc) {
@@ -655,13 +699,21 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemsetAsync(d_fbad, 0, (fr.size() + 1) * 4, sm));
-  HIPCHK(hipMemsetAsync(d_ctr, 0, 16, sm));
+  HIPCHK(hipMemsetAsync(d_ctr, 0, 64, sm));
   const uint32_t cmd_cap = v.C16 * 16;
   if (nm) {
-    HIPCHK(hipMemcpyAsync(d_moff, hmoff.data(), nm * 8, hipMemcpyHostToDevice, sm));
-    HIPCHK(hipMemcpyAsync(d_mlen, hmlen.data(), nm * 4, hipMemcpyHostToDevice, sm));
-    HIPCHK(hipMemcpyAsync(d_mframe, hmframe.data(), nm * 4,
+    for (size_t f = 0; f < nf; ++f) {
+      const size_t k = fr[f].moff.size();
+      if (!k) continue;
+      HIPCHK(hipMemcpyAsync(d_moff + mbase[f], fr[f].moff.data(), k * 8,
+                            hipMemcpyHostToDevice, sm));
+      HIPCHK(hipMemcpyAsync(d_mlen + mbase[f], fr[f].mlen.data(), k * 4,
+                            hipMemcpyHostToDevice, sm));
+    }
+    HIPCHK(hipMemcpyAsync(d_mbase, mbase.data(), (nf + 1) * 8,
                           hipMemcpyHostToDevice, sm));
+    k_ing_frames<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+        d_mbase, (uint32_t)nf, d_mframe, nm);
     k_ing_count<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
         ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad, nm, cmd_cap);
     HIPCHK(hipGetLastError());
@@ -674,14 +726,13 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   HIPCHK(hipStreamSynchronize(sm));
   // 4. the frames delivered: up to the first with a bad CRC or a batch that
   // does not decode (ErrBadMessage closes the connection, tcp.go:528-530)
-  std::vector<uint8_t> deliver(m1, 0);
-  std::vector<uint32_t> err_h;
+  std::vector<uint8_t> fstate(nf + 1, 0);
   size_t consumed = 0;
   bool big = false;
   bool any_deliver = false;
   {
     size_t mi = 0;
-    for (size_t f = 0; f < fr.size(); ++f) {
+    for (size_t f = 0; f < nf; ++f) {
       uint32_t c = 0;
       for (uint32_t k = cfirst[f]; k < cfirst[f + 1]; ++k)
         c = k == cfirst[f] ? ccrc[k] : wirehost::crc32_combine(c, ccrc[k],
@@ -700,7 +751,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       }
       const bool keep = fr[f].did == deployment_id && fr[f].bv == 210;
       if (keep && (fbad[f] & 2u)) big = true;
-      for (size_t k = 0; k < nmf; ++k) deliver[mi + k] = keep;
+      fstate[f] = keep ? 1 : 2;
       any_deliver |= keep && nmf;
       mi += nmf;
     }
@@ -708,64 +759,47 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (bad_header && !res.bad) res.bad = 1;
   if (big) return DRB_ERANGE;  // a Cmd the window rows cannot hold
   res.consumed = consumed;
-  // per-message outcomes of the delivered frames (snapshot / filtered)
+  // per-message outcomes (snapshot / delivered / filtered), the entry bases
   if (nm) {
-    err_h.resize(nm);
-    std::vector<uint32_t> nent(nm);
-    HIPCHK(hipMemcpyAsync(err_h.data(), d_err, nm * 4, hipMemcpyDeviceToHost, sm));
-    HIPCHK(hipMemcpyAsync(nent.data(), d_nent, nm * 4, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(d_fstate, fstate.data(), nf + 1,
+                          hipMemcpyHostToDevice, sm));
+    k_ing_tally<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+        d_mframe, d_fstate, d_err, d_nent, d_nsc, d_deliver, nm, d_ctr);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0, tb2 = 0;
+    uint32_t *kin = nullptr, *kout = nullptr, *vin = nullptr, *vout = nullptr;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin,
+                                              vout, (int)nm, 0, 32, sm));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, d_nsc, d_ent0,
+                                            (int)nm, sm));
+    tb = std::max(tb, tb2);
+    const size_t sbytes = al256(nm * 4) * 4 + al256(tb);
+    if (ing_grow(st.sort, sbytes)) return DRB_EDEVICE;
+    uint8_t *sp = (uint8_t *)st.sort.p;
+    void *tmp = sp + 4 * al256(nm * 4);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_nsc, d_ent0, (int)nm,
+                                            sm));
+    unsigned long long c0[6];
+    HIPCHK(hipMemcpyAsync(c0, d_ctr, sizeof(c0), hipMemcpyDeviceToHost, sm));
     HIPCHK(hipStreamSynchronize(sm));
-    // the frames counted above, message by message
-    size_t mi = 0;
-    for (size_t f = 0; f < res.frames; ++f) {
-      const size_t nmf = fr[f].moff.size();
-      if (fr[f].method == 100) {
-        const bool keep = fr[f].did == deployment_id && fr[f].bv == 210;
-        for (size_t k = 0; k < nmf; ++k) {
-          const uint32_t r = err_h[mi + k];
-          if (r == ING_SNAPSHOT) {
-            res.snapshots++;
-          } else if (keep) {
-            res.messages++;
-          } else {
-            res.dropped++;
-          }
-        }
-      }
-      mi += nmf;
-    }
-    // entry bases
-    std::vector<uint64_t> ent0(nm);
-    uint64_t tot = 0;
-    for (size_t k = 0; k < nm; ++k) {
-      ent0[k] = tot;
-      if (deliver[k] && err_h[k] == ING_OK) tot += nent[k];
-    }
+    res.snapshots += c0[2];
+    res.messages = c0[3];
+    res.dropped += c0[4];
+    const uint64_t tot = c0[5];
     if (any_deliver) {
       const size_t eb = al256((tot ? tot : 1) * sizeof(drb_entry));
       if (ing_grow(st.ents, eb) || ing_grow(st.msgs, al256(nm * sizeof(DecMsg))))
         return DRB_EDEVICE;
-      HIPCHK(hipMemcpyAsync(d_ent0, ent0.data(), nm * 8, hipMemcpyHostToDevice, sm));
-      HIPCHK(hipMemcpyAsync(d_deliver, deliver.data(), nm, hipMemcpyHostToDevice,
-                            sm));
       DecMsg *dm = (DecMsg *)st.msgs.p;
       drb_entry *de = (drb_entry *)st.ents.p;
       k_ing_decode<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-          ds, d_moff, d_mlen, d_err, d_ent0, d_deliver, dm, de, nm, cmd_cap);
+          ds, d_moff, d_mlen, d_ent0, d_deliver, dm, de, nm, cmd_cap);
       HIPCHK(hipGetLastError());
       // 5. planes: keys, a stable radix sort, one lane per plane
-      size_t tb = 0;
-      uint32_t *kin = nullptr, *kout = nullptr, *vin = nullptr, *vout = nullptr;
-      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin,
-                                                vout, (int)nm, 0, 32, sm));
-      const size_t sbytes = al256(nm * 4) * 4 + al256(tb);
-      if (ing_grow(st.sort, sbytes)) return DRB_EDEVICE;
-      uint8_t *sp = (uint8_t *)st.sort.p;
       kin = (uint32_t *)sp;
       kout = (uint32_t *)(sp + al256(nm * 4));
       vin = (uint32_t *)(sp + 2 * al256(nm * 4));
       vout = (uint32_t *)(sp + 3 * al256(nm * 4));
-      void *tmp = sp + 4 * al256(nm * 4);
       k_ing_keys<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
           v, dm, kin, vin, nm, d_ctr);
       HIPCHK(hipGetLastError());
