@@ -383,10 +383,11 @@ def main():
                         device=local)
             rx.init_steady(term=2, leader_slot=0, seed=seed)
             rx.host_slot(0, False)
-            # a first call sizes the device buffers; the next round takes
-            # its messages in, then the timed call
+            # a first call sizes the device buffers; the replicas are reset
+            # (the mailbox keeps room for a second copy), then the timed call
             rx.ingest_wire(stream, deployment_id=1)
-            rx.step(tick=False, prop_slot=0xFFFFFFFF, ri_slot=0xFFFFFFFF)
+            rx.init_steady(term=2, leader_slot=0, seed=seed)
+            rx.host_slot(0, False)
             rx.sync()
             i0 = time.perf_counter()
             res = rx.ingest_wire(stream, deployment_id=1)
