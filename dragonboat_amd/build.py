@@ -12,15 +12,15 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libdrb_engine.so")
 SOURCES = ["drb_engine.hip"]
-HEADERS = ["drb_layout.hpp", "drb_msg.hpp", "drb_step.hpp", "drb_codec.hpp",
-           "drb_wire.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 
 def _deps():
+    """Every source and header the engine includes (all of csrc/)."""
     inc = os.path.join(os.path.dirname(HERE), "include", "drb_engine.h")
-    return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [inc]
+    return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))
+            if f.endswith((".hip", ".hpp"))] + [inc]
 
 
 def up_to_date():

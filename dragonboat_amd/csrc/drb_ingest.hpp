@@ -572,6 +572,28 @@ static void ingest_free(IngestState *st) {
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// DRB_INGEST_TRACE=1: per-phase wall times on stderr (each mark waits for
+// the engine stream, so a traced call is slower than an untraced one)
+#include <chrono>
+struct IngestTrace {
+  bool on;
+  hipStream_t s;
+  std::chrono::steady_clock::time_point t;
+  explicit IngestTrace(hipStream_t st) : s(st) {
+    const char *e = getenv("DRB_INGEST_TRACE");
+    on = e && e[0] == '1';
+    t = std::chrono::steady_clock::now();
+  }
+  void mark(const char *what) {
+    if (!on) return;
+    (void)hipStreamSynchronize(s);
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "ingest %-10s %8.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                size_t len, uint64_t deployment_id,
                                drb_wire_in *out) {
@@ -586,6 +608,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   const View &v = e->v;
   drb_wire_in res;
   memset(&res, 0, sizeof(res));
+  IngestTrace tr(e->stream);
   // 1. frames: magic + requestHeader + its CRC (tcp.go:64-112, 180-237)
   std::vector<wirehost::Frame> fr;
   size_t i = 0;
@@ -616,6 +639,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     i += 20 + (size_t)size;
   }
   const size_t walked = i;  // bytes of whole frames
+  tr.mark("headers");
   // 2. Requests boundaries, one host thread per frame (a frame holds up to
   // 64 MiB of messages); at most 16 threads
   {
@@ -630,6 +654,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   }
   uint64_t nm = 0;
   for (const auto &f : fr) nm += f.moff.size();
+  tr.mark("scan");
   // 3. the stream up, the payload CRCs in 16 KB chunks
   constexpr uint64_t CH = 16384;
   std::vector<uint64_t> coff;
@@ -724,6 +749,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   HIPCHK(hipMemcpyAsync(fbad.data(), d_fbad, (fr.size() + 1) * 4,
                         hipMemcpyDeviceToHost, sm));
   HIPCHK(hipStreamSynchronize(sm));
+  tr.mark("up+crc+cnt");
   // 4. the frames delivered: up to the first with a bad CRC or a batch that
   // does not decode (ErrBadMessage closes the connection, tcp.go:528-530)
   std::vector<uint8_t> fstate(nf + 1, 0);
@@ -795,6 +821,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       k_ing_decode<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
           ds, d_moff, d_mlen, d_ent0, d_deliver, dm, de, nm, cmd_cap);
       HIPCHK(hipGetLastError());
+      tr.mark("decode");
       // 5. planes: keys, a stable radix sort, one lane per plane
       kin = (uint32_t *)sp;
       kout = (uint32_t *)(sp + al256(nm * 4));
@@ -816,6 +843,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       res.dropped += ctr[1];
     }
   }
+  tr.mark("place");
   if (out) *out = res;
   return DRB_OK;
 }
