@@ -552,7 +552,11 @@ def main():
         if xch is not None:
             res["exchange"] = {"mode": args.exchange,
                                "bytes_sent_per_round_rank0":
-                               xch.bytes_sent / K}
+                               xch.bytes_sent / K,
+                               "note": "the tests run this exchange over "
+                                       "gloo with host staging (one-GPU "
+                                       "boxes); this line is its first "
+                                       "RCCL run"}
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(res))

@@ -114,3 +114,23 @@ def test_engine_without_gpu_fails_loudly():
         pytest.skip("a GPU is present")
     with pytest.raises(engine.DrbError):
         engine.Engine(num_groups=64, num_replicas=3)
+
+
+@pytest.mark.parametrize("kw", [
+    # the plane summary word carries E in 8 bits (DRB_PLANE_E)
+    dict(num_groups=64, num_replicas=3, place_world=2, place_rank=0,
+         entry_mbox=256, window=512),
+    dict(num_groups=64, num_replicas=3, place_world=2, place_rank=2,
+         entry_mbox=3),
+    # batched LogDB records merge from the window: window >= 64, save_cap
+    dict(num_groups=64, num_replicas=3, save_batched=1, save_cap=4096),
+    dict(num_groups=64, num_replicas=3, save_batched=1, window=64),
+    dict(num_groups=64, num_replicas=3, window=48),  # not a power of two
+    dict(num_groups=64, num_replicas=3, save_cap=1000),  # not 16 B aligned
+])
+def test_create_rejects_invalid_config(kw):
+    """drb_engine_create validates the configuration before it touches a
+    device: DRB_EINVAL, on a box with or without a GPU."""
+    with pytest.raises(engine.DrbError) as ei:
+        engine.Engine(**kw)
+    assert "status %d" % abi.DRB_EINVAL in str(ei.value)
