@@ -155,6 +155,8 @@ typedef struct orc_node {
   size_t nrtr, caprtr;
   orc_evec applyq; /* tasks pushed for the apply worker */
   orc_evec saved;  /* ud.EntriesToSave of the last round (SaveRaftState) */
+  int upd_have;    /* the last round produced a pb.Update for SaveRaftState */
+  uint64_t upd_st[3]; /* its State {Term, Vote, Commit}, zero when empty */
 } orc_node;
 
 struct orc_cluster {
@@ -686,6 +688,7 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
     mv_clear(&n->out);
     n->nrtr = 0;
     n->saved.n = 0;
+    n->upd_have = 0;
     n->quiesce_to = 0;
     if (!n->hosted) {
       mv_clear(&n->inbox);
@@ -750,6 +753,10 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
     orc_update *ud = &uds[s];
     db_append(n->db, ud->save.v, ud->save.n); /* LogReader.Append */
     ev_copy_range(&n->saved, ud->save.v, ud->save.n);
+    n->upd_have = 1;
+    n->upd_st[0] = ud->has_state ? ud->st_term : 0;
+    n->upd_st[1] = ud->has_state ? ud->st_vote : 0;
+    n->upd_st[2] = ud->has_state ? ud->st_commit : 0;
     for (size_t i = 0; i < ud->msgs.n; i++)
       if (ud->msgs.v[i].type != DRB_MSG_REPLICATE)
         deliver(c, g, s, &ud->msgs.v[i]);
@@ -1108,6 +1115,34 @@ long orc_cluster_export_saved(orc_cluster *c, uint64_t g, uint32_t slot,
     if (crc) *crc = orc_crc32_ieee(buf, sz);
     rc = (long)sz;
   }
+  free(de);
+  free(pool);
+  return rc;
+}
+
+/* SaveRaftState of the last round's pb.Update of replica (g, slot) into a
+ * regular tan db (internal/tan/logdb.go:306-340 -> db.write, db.go:97):
+ * 1 written, 0 no Update or nothing to write, -1 error */
+int orc_cluster_tan_write(orc_cluster *c, uint64_t g, uint32_t slot,
+                          orc_tandb *db, int *sync) {
+  orc_node *n = node_at(c, g, slot);
+  if (sync) *sync = 0;
+  if (!n->upd_have) return 0;
+  const size_t ne = n->saved.n;
+  drb_entry *de = (drb_entry *)calloc(ne ? ne : 1, sizeof(drb_entry));
+  size_t pool_n = 0;
+  for (size_t i = 0; i < ne; i++)
+    pool_n += n->saved.v[i].cmd ? n->saved.v[i].cmd->len : 0;
+  uint8_t *pool = (uint8_t *)malloc(pool_n + 1);
+  size_t used = 0;
+  int rc = 0;
+  for (size_t i = 0; i < ne && rc == 0; i++)
+    rc = entry_to_view(&n->saved.v[i], &de[i], pool, pool_n + 1, &used);
+  if (rc == 0)
+    rc = orc_tandb_write(db, n->r->shard_id, n->r->replica_id, n->upd_st[0],
+                         n->upd_st[1], n->upd_st[2], de, ne, pool, sync);
+  else
+    rc = -1;
   free(de);
   free(pool);
   return rc;

@@ -290,6 +290,43 @@ int orc_batch_compact(drb_entry *e, size_t n, int restore);
 long orc_batch_merged_first(const drb_entry *eb, size_t ne,
                             const drb_entry *lb, size_t nl, drb_entry *out);
 
+/* ---- tan LogDB write path (internal/tan: record.go, db.go, crc.go) ---- */
+/* xxhash.Sum64 (cespare/xxhash/v2 v2.1.2; tan getCRC = its low 32 bits) */
+uint64_t orc_xxh64(const uint8_t *p, size_t n);
+/* record writer (record.go:414-653) over an in-memory io.Writer */
+typedef struct orc_tanw orc_tanw;
+orc_tanw *orc_tanw_new(void);
+void orc_tanw_free(orc_tanw *w);
+int64_t orc_tanw_write_record(orc_tanw *w, const uint8_t *p, size_t n);
+int orc_tanw_flush(orc_tanw *w, int close);
+int64_t orc_tanw_size(const orc_tanw *w);
+int64_t orc_tanw_last_record_offset(const orc_tanw *w);
+long orc_tanw_bytes(const orc_tanw *w, uint8_t *buf, size_t cap);
+/* record reader (record.go:163-311) over a whole log */
+#define ORC_TAN_ZEROED (-2)         /* ErrZeroedChunk */
+#define ORC_TAN_INVALID (-3)        /* ErrInvalidChunk */
+#define ORC_TAN_CRC (-4)            /* ErrCRCMismatch */
+#define ORC_TAN_UNEXPECTED_EOF (-5) /* io.ErrUnexpectedEOF */
+long orc_tan_read(const uint8_t *file, size_t size, int64_t *offsets,
+                  size_t *lens, size_t max_recs, uint8_t *data,
+                  size_t data_cap);
+/* Update.MarshalTo (raftpb/update.go:128-169), empty Snapshot */
+size_t orc_update_size_bound(const drb_entry *ents, size_t n);
+size_t orc_update_marshal(uint64_t shard, uint64_t replica, uint64_t term,
+                          uint64_t vote, uint64_t commit,
+                          const drb_entry *ents, size_t n,
+                          const uint8_t *pool, uint8_t *buf);
+/* one replica's tan db (db.go:97-130; max_log_size 0: 64 MiB) */
+typedef struct orc_tandb orc_tandb;
+orc_tandb *orc_tandb_new(int64_t max_log_size);
+void orc_tandb_free(orc_tandb *db);
+int orc_tandb_write(orc_tandb *db, uint64_t shard, uint64_t replica,
+                    uint64_t term, uint64_t vote, uint64_t commit,
+                    const drb_entry *ents, size_t n, const uint8_t *pool,
+                    int *sync);
+void orc_tandb_last(const orc_tandb *db, int64_t *out6);
+long orc_tandb_file(const orc_tandb *db, size_t log, uint8_t *buf, size_t cap);
+
 /* ---- rsm (statemachine.go, encoded.go) : KAT hooks -------------------- */
 long orc_get_payload(uint32_t type, const uint8_t *cmd, size_t clen,
                      uint8_t *out, size_t cap);
@@ -356,6 +393,8 @@ long orc_cluster_export_ready(orc_cluster *c, uint64_t g, uint32_t slot,
                               drb_ready_to_read *out, size_t cap);
 long orc_cluster_export_saved(orc_cluster *c, uint64_t g, uint32_t slot,
                               uint8_t *buf, size_t cap, uint32_t *crc);
+int orc_cluster_tan_write(orc_cluster *c, uint64_t g, uint32_t slot,
+                          orc_tandb *db, int *sync);
 int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
                            int hosted);
 /* make an engine-importable image of replica (g,slot) */

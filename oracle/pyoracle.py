@@ -146,6 +146,28 @@ def _declare(L):
         "orc_batch_compact": (C.c_int, [PE, C.c_size_t, C.c_int]),
         "orc_batch_merged_first": (C.c_long, [PE, C.c_size_t, PE, C.c_size_t,
                                               PE]),
+        "orc_xxh64": (U64, [PU8, C.c_size_t]),
+        "orc_tanw_new": (P, []),
+        "orc_tanw_free": (None, [P]),
+        "orc_tanw_write_record": (C.c_int64, [P, PU8, C.c_size_t]),
+        "orc_tanw_flush": (C.c_int, [P, C.c_int]),
+        "orc_tanw_size": (C.c_int64, [P]),
+        "orc_tanw_last_record_offset": (C.c_int64, [P]),
+        "orc_tanw_bytes": (C.c_long, [P, PU8, C.c_size_t]),
+        "orc_tan_read": (C.c_long, [PU8, C.c_size_t, C.POINTER(C.c_int64),
+                                    C.POINTER(C.c_size_t), C.c_size_t, PU8,
+                                    C.c_size_t]),
+        "orc_update_size_bound": (C.c_size_t, [PE, C.c_size_t]),
+        "orc_update_marshal": (C.c_size_t, [U64, U64, U64, U64, U64, PE,
+                                            C.c_size_t, PU8, PU8]),
+        "orc_tandb_new": (P, [C.c_int64]),
+        "orc_tandb_free": (None, [P]),
+        "orc_tandb_write": (C.c_int, [P, U64, U64, U64, U64, U64, PE,
+                                      C.c_size_t, PU8, C.POINTER(C.c_int)]),
+        "orc_tandb_last": (None, [P, C.POINTER(C.c_int64)]),
+        "orc_tandb_file": (C.c_long, [P, C.c_size_t, PU8, C.c_size_t]),
+        "orc_cluster_tan_write": (C.c_int, [P, U64, U32, P,
+                                            C.POINTER(C.c_int)]),
         "orc_sm_new": (P, [U64, U64]),
         "orc_sm_free": (None, [P]),
         "orc_sm_handle": (C.c_long, [P, PE, C.c_size_t, PU8]),
@@ -710,6 +732,15 @@ class Cluster:
             raise RuntimeError("export_saved: buffer too small")
         return bytes(buf[:n]), crc.value
 
+    def tan_write(self, g, slot, db):
+        """SaveRaftState of replica (g, slot)'s last pb.Update into a
+        TanDB: None when there was nothing to write, else the write's
+        TanDB.last() record."""
+        sync = C.c_int()
+        rc = _check(lib().orc_cluster_tan_write(self.p, g, slot, db.p,
+                                                C.byref(sync)))
+        return db.last() if rc == 1 else None
+
     def serve_reads(self, reads_per_ctx=9, key_space=256):
         """Returns (sums[G*R] -- None where nothing was served, served,
         deferred)."""
@@ -1007,3 +1038,108 @@ def batch_merged_first(eb, lb):
     out = (Entry * max(1, len(eb) + len(lb)))()
     n = _check(lib().orc_batch_merged_first(a, len(eb), b, len(lb), out))
     return [(out[i].term, out[i].index) for i in range(n)]
+
+
+# ---------------------------------------------------------------- tan
+ORC_TAN_ERRORS = {-2: "zeroed chunk", -3: "invalid chunk", -4: "crc mismatch",
+                  -5: "unexpected EOF"}
+
+
+def xxh64(data):
+    """xxhash.Sum64 (cespare/xxhash/v2); tan getCRC is its low 32 bits."""
+    return lib().orc_xxh64(_u8(data), len(data))
+
+
+class TanWriter:
+    """The tan record writer (internal/tan/record.go:414-653) over an
+    in-memory io.Writer."""
+
+    def __init__(self):
+        self.p = lib().orc_tanw_new()
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_tanw_free(self.p)
+
+    def write_record(self, data):
+        return _check(lib().orc_tanw_write_record(self.p, _u8(data),
+                                                  len(data)))
+
+    def flush(self):
+        return _check(lib().orc_tanw_flush(self.p, 0))
+
+    def close(self):
+        return _check(lib().orc_tanw_flush(self.p, 1))
+
+    def size(self):
+        return lib().orc_tanw_size(self.p)
+
+    def last_record_offset(self):
+        return lib().orc_tanw_last_record_offset(self.p)
+
+    def bytes(self):
+        n = lib().orc_tanw_bytes(self.p, None, 0)
+        buf = (C.c_uint8 * max(1, n))()
+        lib().orc_tanw_bytes(self.p, buf, n)
+        return bytes(buf[:n])
+
+
+def tan_read(data, max_recs=1 << 20):
+    """The records of a tan log (record.go reader): [(offset, payload)];
+    raises on a format error."""
+    offs = (C.c_int64 * max_recs)()
+    lens = (C.c_size_t * max_recs)()
+    cap = max(1, len(data))
+    out = (C.c_uint8 * cap)()
+    n = lib().orc_tan_read(_u8(data), len(data), offs, lens, max_recs, out,
+                           cap)
+    if n < 0:
+        raise OracleError("tan read: " + ORC_TAN_ERRORS.get(n, str(n)))
+    recs, pos = [], 0
+    for i in range(n):
+        recs.append((offs[i], bytes(out[pos:pos + lens[i]])))
+        pos += lens[i]
+    return recs
+
+
+def update_marshal(shard, replica, state, entries):
+    """Update.MarshalTo (raftpb/update.go:128-169); state (term, vote,
+    commit) or None."""
+    arr, pool, n = EntryPool(entries).arrays()
+    buf = (C.c_uint8 * lib().orc_update_size_bound(arr, n))()
+    t, v, c = state or (0, 0, 0)
+    k = lib().orc_update_marshal(shard, replica, t, v, c, arr, n, pool, buf)
+    return bytes(buf[:k])
+
+
+class TanDB:
+    """One replica's regular tan db (internal/tan/db.go:97-130)."""
+
+    def __init__(self, max_log_size=0):
+        self.p = lib().orc_tandb_new(max_log_size)
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().orc_tandb_free(self.p)
+
+    def write(self, shard, replica, state, entries):
+        """db.write: None when nothing is written, else last()."""
+        arr, pool, n = EntryPool(entries).arrays()
+        t, v, c = state or (0, 0, 0)
+        sync = C.c_int()
+        rc = _check(lib().orc_tandb_write(self.p, shard, replica, t, v, c,
+                                          arr, n, pool, C.byref(sync)))
+        return self.last() if rc == 1 else None
+
+    def last(self):
+        """{off, len, sync, new_log, log, offset} of the last write."""
+        o = (C.c_int64 * 6)()
+        lib().orc_tandb_last(self.p, o)
+        return dict(off=o[0], len=o[1], sync=bool(o[2]), new_log=bool(o[3]),
+                    log=o[4], offset=o[5])
+
+    def file(self, log):
+        n = _check(lib().orc_tandb_file(self.p, log, None, 0))
+        buf = (C.c_uint8 * max(1, n))()
+        lib().orc_tandb_file(self.p, log, buf, n)
+        return bytes(buf[:n])
