@@ -129,7 +129,8 @@ class Config(C.Structure):
                 ("place_rank", C.c_uint32), ("entry_mbox", C.c_uint32),
                 ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
                 ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
-                ("save_batched", C.c_uint32)]
+                ("save_batched", C.c_uint32), ("save_tan", C.c_uint32),
+                ("reserved0", C.c_uint32), ("tan_max_log", C.c_uint64)]
 
 
 class ApplyResult(C.Structure):
@@ -153,6 +154,23 @@ class Flagged(C.Structure):
                 ("round", C.c_uint64), ("slot", C.c_uint32),
                 ("reason", C.c_uint32), ("flags", C.c_uint32),
                 ("pad", C.c_uint32)]
+
+
+TAN_WRITTEN, TAN_SYNC, TAN_NEW_LOG, TAN_OVERFLOW = 1, 2, 4, 8
+
+
+class TanRecord(C.Structure):
+    """drb_tan_record: what one replica's tan log grew by last round."""
+    _fields_ = [("offset", C.c_uint64), ("first_index", C.c_uint64),
+                ("last_index", C.c_uint64), ("commit", C.c_uint64),
+                ("len", C.c_uint32), ("flags", C.c_uint32),
+                ("log", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class TanState(C.Structure):
+    """drb_tan_state: a replica's tan writer position."""
+    _fields_ = [("offset", C.c_uint64), ("log", C.c_uint32),
+                ("state_stored", C.c_uint32)]
 
 
 class Region(C.Structure):
@@ -209,7 +227,9 @@ class RoundOut(C.Structure):
                 ("fallbacks", C.c_uint64), ("errors", C.c_uint64),
                 ("reads_served", C.c_uint64), ("reads_deferred", C.c_uint64),
                 ("saved_entries", C.c_uint64), ("saved_bytes", C.c_uint64),
-                ("replicas_stepped", C.c_uint64)]
+                ("replicas_stepped", C.c_uint64),
+                ("log_records", C.c_uint64), ("log_syncs", C.c_uint64),
+                ("log_new", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

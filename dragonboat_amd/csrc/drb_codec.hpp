@@ -78,8 +78,10 @@ __device__ __forceinline__ uint32_t bo_finish(ByteOut &o) {
   return o.crc ^ 0xffffffffu;
 }
 
-// protobuf / colfer varint (raftpb/common.go:11-19)
-__device__ __forceinline__ void bo_varint(ByteOut &o, uint64_t x) {
+// protobuf / colfer varint (raftpb/common.go:11-19); O is any byte sink
+// with a bo_byte(O &, uint32_t) overload (ByteOut, TanOut)
+template <class O>
+__device__ __forceinline__ void bo_varint(O &o, uint64_t x) {
   while (x >= 0x80) {
     bo_byte(o, (uint32_t)(x | 0x80));
     x >>= 7;
@@ -102,8 +104,8 @@ __device__ __forceinline__ uint32_t colfer_u64_size(uint64_t x) {
   if (x == 0) return 0;
   return 1 + varint_size(x);
 }
-__device__ __forceinline__ void colfer_u64(ByteOut &o, uint32_t tag,
-                                           uint64_t x) {
+template <class O>
+__device__ __forceinline__ void colfer_u64(O &o, uint32_t tag, uint64_t x) {
   if (x >= (1ull << 49)) {
     bo_byte(o, tag | 0x80);
 #pragma unroll

@@ -58,12 +58,17 @@ struct drb_engine {
   struct IngestState *ingest = nullptr;      // drb_ingest_wire (drb_ingest.hpp)
   std::mutex ingest_mu;  // drb_ingest: concurrent transport threads
   bool crc_tab_ready = false;  // c_crc_tab uploaded on this engine's device
+  uint64_t tan_blocks = 0;                   // k_tan_encode grid (save_tan)
+  unsigned long long *tan_total = nullptr;   // its counter rows summed
 };
 
 static void wire_free(drb_engine *e);
 static void ingest_free(struct IngestState *st);
 static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 static int refresh_roles(drb_engine *e);
+static int launch_tan(drb_engine *e, uint32_t round);  // drb_tan.hpp
+static int read_tan_counters(drb_engine *e, unsigned long long *t4,
+                             int reset);
 
 template <typename T>
 static int dalloc(drb_engine *e, T **p, uint64_t count) {
@@ -188,6 +193,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   // batched records merge from the window: a batch's 47 earlier entries
   // plus the round's must be resident
   if (cfg->save_batched && (cfg->save_cap == 0 || cfg->window < 64))
+    return DRB_EINVAL;
+  if (cfg->save_tan && (cfg->save_cap == 0 || cfg->save_batched))
     return DRB_EINVAL;
   // entry_mbox travels as the 8-bit E of the plane summary word
   // (block_plane_summary, DRB_PLANE_E)
@@ -319,6 +326,19 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   if (v.save_batched) {
     rc |= dalloc(e, &v.save_rec, R * G * DRB_SAVE_RECS);
     rc |= dalloc(e, &v.save_nrec, R * G);
+  }
+  v.save_tan = cfg->save_tan ? 1u : 0u;
+  if (v.save_tan) {
+    // beyond the entries' EntryBatch bound: the Update's shard, replica,
+    // State and counts (<= 63 B), zero padding (<= 6 B) and a 7-byte chunk
+    // header per block the record touches
+    v.save_slack = 63 + 6 + 7 * (cfg->save_cap / (32768 - 7) + 2);
+    e->tan_blocks = (R * G + 255) / 256;
+    rc |= dalloc(e, &v.tan_sum, 3 * R * G);
+    rc |= dalloc(e, &v.tan_st, R * G);
+    rc |= dalloc(e, &v.tan_rec, R * G);
+    rc |= dalloc(e, &v.tan_ctr, e->tan_blocks * 4);
+    rc |= dalloc(e, &e->tan_total, 4);
   }
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
@@ -1563,6 +1583,10 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
     default: return DRB_EINVAL;
   }
   HIPCHK(hipGetLastError());
+  if (p.encode_saves && e->v.save_tan) {
+    int rc = launch_tan(e, (uint32_t)p.round);
+    if (rc) return rc;
+  }
   e->round++;
   e->ticks += p.tick;
   return DRB_OK;
@@ -1610,6 +1634,18 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->saved_entries = c[C_SAVED_ENTRIES];
   out->saved_bytes = c[C_SAVED_BYTES];
   out->replicas_stepped = c[C_STEPPED];
+  out->log_records = 0;
+  out->log_syncs = 0;
+  out->log_new = 0;
+  if (e->v.save_tan) {  // the tan records' bytes stand for the saves'
+    unsigned long long t[4];
+    int rc = read_tan_counters(e, t, reset);
+    if (rc) return rc;
+    out->saved_bytes = t[0];
+    out->log_records = t[1];
+    out->log_syncs = t[2];
+    out->log_new = t[3];
+  }
   if (reset) {
     HIPCHK(hipMemsetAsync(e->v.counters, 0,
                           e->ctr_rows * NUM_COUNTERS * sizeof(c[0]),
@@ -1776,6 +1812,10 @@ extern "C" int drb_step_round(drb_engine *e, const drb_round_in *in,
   HIPCHK(hipMemsetAsync(e->v.counters, 0,
                         e->ctr_rows * NUM_COUNTERS * sizeof(unsigned long long),
                         e->stream));
+  if (e->v.save_tan)
+    HIPCHK(hipMemsetAsync(e->v.tan_ctr, 0,
+                          e->tan_blocks * 4 * sizeof(unsigned long long),
+                          e->stream));
   int rc = drb_step_round_async(e, in);
   if (rc) return rc;
   if (out) return drb_read_counters(e, out, 1);
@@ -2385,3 +2425,121 @@ extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
 // ---------------------------------------------------------------- wire
 #include "drb_wire.hpp"
 #include "drb_ingest.hpp"
+#include "drb_tan.hpp"
+
+// ---------------------------------------------------------------- tan
+static int launch_tan(drb_engine *e, uint32_t round) {
+  const uint64_t max_log = e->cfg.tan_max_log ? e->cfg.tan_max_log
+                                              : drb::TAN_MAX_LOG;
+  k_tan_encode<<<(unsigned)e->tan_blocks, 256, 0, e->stream>>>(e->v, round,
+                                                               max_log);
+  HIPCHK(hipGetLastError());
+  return DRB_OK;
+}
+
+__global__ void k_sum_tan(const unsigned long long *rows, uint64_t n,
+                          unsigned long long *total) {
+  __shared__ unsigned long long part[256];
+  for (int c = 0; c < 4; ++c) {
+    unsigned long long s = 0;
+    for (uint64_t r = threadIdx.x; r < n; r += blockDim.x) s += rows[r * 4 + c];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < (unsigned)o) part[threadIdx.x] += part[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) total[c] = part[0];
+    __syncthreads();
+  }
+}
+
+static int read_tan_counters(drb_engine *e, unsigned long long *t4,
+                             int reset) {
+  k_sum_tan<<<1, 256, 0, e->stream>>>(e->v.tan_ctr, e->tan_blocks,
+                                      e->tan_total);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(t4, e->tan_total, 4 * sizeof(t4[0]),
+                        hipMemcpyDeviceToHost, e->stream));
+  if (reset)
+    HIPCHK(hipMemsetAsync(e->v.tan_ctr, 0, e->tan_blocks * 4 * sizeof(t4[0]),
+                          e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+extern "C" int drb_export_tan(drb_engine *e, uint64_t group, uint32_t slot,
+                              drb_tan_record *rec, uint8_t *buf, size_t cap) {
+  if (!e || !rec || (cap && !buf)) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!v.save_tan) return DRB_EINVAL;
+  if (group >= v.G || slot >= v.R) return DRB_ERANGE;
+  uint4 r, s[3];
+  HIPCHK(hipMemcpyAsync(&r, v.tan_rec + ix(v, slot, group), sizeof(r),
+                        hipMemcpyDeviceToHost, e->stream));
+  for (uint32_t k = 0; k < 3; ++k)
+    HIPCHK(hipMemcpyAsync(&s[k], v.tan_sum + tan_sum_ix(v, k, slot, group),
+                          sizeof(uint4), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  memset(rec, 0, sizeof(*rec));
+  rec->offset = (uint64_t)r.x | ((uint64_t)r.y << 32);
+  rec->len = r.z;
+  rec->flags = r.w & 0xffu;
+  rec->log = r.w >> 8;
+  if (rec->flags & DRB_TAN_WRITTEN) {
+    const uint32_t n_save = s[2].x;
+    const uint64_t save_lo = (uint64_t)s[1].z | ((uint64_t)s[1].w << 32);
+    if (n_save) {
+      rec->first_index = save_lo;
+      rec->last_index = save_lo + n_save - 1;
+    }
+    if (s[2].y & TS_STATE)
+      rec->commit = (uint64_t)s[1].x | ((uint64_t)s[1].y << 32);
+  }
+  if (rec->len > cap) return rec->len && buf ? DRB_ERANGE : DRB_OK;
+  if (rec->len) {
+    HIPCHK(hipMemcpyAsync(buf, v.save_buf + ix(v, slot, group) * v.save_cap16,
+                          rec->len, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_tan_get(drb_engine *e, uint64_t group, uint32_t slot,
+                           drb_tan_state *out) {
+  if (!e || !out) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!v.save_tan) return DRB_EINVAL;
+  if (group >= v.G || slot >= v.R) return DRB_ERANGE;
+  uint4 st;
+  HIPCHK(hipMemcpyAsync(&st, v.tan_st + ix(v, slot, group), sizeof(st),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  out->offset = (uint64_t)st.x | ((uint64_t)st.y << 32);
+  out->log = st.z;
+  out->state_stored = st.w & TST_STATE;
+  return DRB_OK;
+}
+
+extern "C" int drb_tan_set(drb_engine *e, uint64_t group, uint32_t slot,
+                           const drb_tan_state *in) {
+  if (!e || !in) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!v.save_tan) return DRB_EINVAL;
+  if (group >= v.G || slot >= v.R || in->log > 0xffffffu) return DRB_ERANGE;
+  const uint4 st = make_uint4((uint32_t)in->offset,
+                              (uint32_t)(in->offset >> 32), in->log,
+                              in->state_stored ? TST_STATE : 0u);
+  HIPCHK(hipMemcpyAsync(v.tan_st + ix(v, slot, group), &st, sizeof(st),
+                        hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+extern "C" int drb_tan_buffers(drb_engine *e, void **bytes, void **recs) {
+  if (!e || !bytes || !recs) return DRB_EINVAL;
+  if (!e->v.save_tan) return DRB_EINVAL;
+  *bytes = e->v.save_buf;
+  *recs = e->v.tan_rec;
+  return DRB_OK;
+}

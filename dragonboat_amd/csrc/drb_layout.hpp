@@ -307,6 +307,15 @@ struct View {
   uint32_t save_batched;  // drb_config.save_batched
   uint4 *save_rec;        // [R][G][DRB_SAVE_RECS] {batch, off16, len, crc}
   uint32_t *save_nrec;    // [R][G] records of the round
+  // save_tan (drb_tan.hpp): the round's pb.Update per replica as the
+  // step kernel leaves it, the tan writer position, the round's record
+  uint32_t save_tan;
+  uint32_t save_slack;    // pre-pass bound: Update framing + chunk headers
+  uint4 *tan_sum;         // [3][R][G] {term, vote} {commit, save_lo}
+                          // {n_save, flags, round, 0}
+  uint4 *tan_st;          // [R][G] {offset lo, hi, log, TST_* flags}
+  uint4 *tan_rec;         // [R][G] {offset lo, hi, len, DRB_TAN_* | log << 8}
+  unsigned long long *tan_ctr;  // [blocks][4] bytes, records, syncs, logs
   // placement (drb_config) and the cross-rank planes (world >= 2)
   uint32_t place_world, place_rank;
   uint64_t total_groups;

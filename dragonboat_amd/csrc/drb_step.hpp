@@ -1157,49 +1157,62 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
 // inmemory.go:116-122) encoded as one EntryBatch (entrybatch.go:25-58) of
 // colfer Entries (raft_optimized.go:166-300) straight from the resident
 // window, with its CRC32-IEEE.
+// The fields of window entry idx of replica (slot, g) as the encoder sees
+// them; `compact` zeroes Term and Index (compactBatchFields).
+DRB_DEV EntryHdr ring_entry_hdr(const View &v, uint32_t slot, uint64_t g,
+                                uint64_t idx, bool compact) {
+  const uint4 m0 = v.ring[ring_ix(v, slot, idx, 0, g)];
+  const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
+  const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
+  EntryHdr e;
+  e.term = compact ? 0 : lo64(m0);
+  e.index = compact ? 0 : idx;
+  e.key = hi64(m0);
+  e.client_id = lo64(m1);
+  e.series_id = hi64(m1);
+  e.responded_to = lo64(m2);
+  e.type = m2.z;
+  e.cmd_len = m2.w;
+  return e;
+}
+
+// Entry.marshalTo (raft_optimized.go:166-300) of e, its Cmd read from the
+// window chunk by chunk, into any byte sink O
+template <class O>
+DRB_DEV void emit_entry(O &o, const View &v, uint32_t slot, uint64_t g,
+                        uint64_t idx, const EntryHdr &e) {
+  colfer_u64(o, 0, e.term);
+  colfer_u64(o, 1, e.index);
+  if (e.type != 0) {
+    bo_byte(o, 2);
+    bo_varint(o, e.type);
+  }
+  colfer_u64(o, 3, e.key);
+  colfer_u64(o, 4, e.client_id);
+  colfer_u64(o, 5, e.series_id);
+  colfer_u64(o, 6, e.responded_to);
+  if (e.cmd_len != 0) {
+    bo_byte(o, 7);
+    bo_varint(o, e.cmd_len);
+    for (uint32_t c = 0; c * 16 < e.cmd_len; ++c) {
+      const uint4 q = v.ring[ring_ix(v, slot, idx, ENT_META + c, g)];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (uint32_t b = 0; b < 16; ++b)
+        if (c * 16 + b < e.cmd_len) bo_byte(o, w[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+  bo_byte(o, 0x7f);
+}
+
 // One EntryBatch.Entries element of window entry idx; `compact` writes it
 // with Term and Index zero (compactBatchFields, logdb/batch.go:100-113).
 DRB_DEV void encode_entry(ByteOut &o, const Lane &L, uint64_t idx,
                           bool compact) {
-  const View &v = *L.v;
-  {
-    const uint4 m0 = v.ring[ring_ix(v, L.slot, idx, 0, L.g)];
-    const uint4 m1 = v.ring[ring_ix(v, L.slot, idx, 1, L.g)];
-    const uint4 m2 = v.ring[ring_ix(v, L.slot, idx, 2, L.g)];
-    EntryHdr e;
-    e.term = compact ? 0 : lo64(m0);
-    e.index = compact ? 0 : idx;
-    e.key = hi64(m0);
-    e.client_id = lo64(m1);
-    e.series_id = hi64(m1);
-    e.responded_to = lo64(m2);
-    e.type = m2.z;
-    e.cmd_len = m2.w;
-    bo_byte(o, 0x0a);  // EntryBatch.Entries, wire type 2
-    bo_varint(o, entry_size(e));
-    colfer_u64(o, 0, e.term);
-    colfer_u64(o, 1, e.index);
-    if (e.type != 0) {
-      bo_byte(o, 2);
-      bo_varint(o, e.type);
-    }
-    colfer_u64(o, 3, e.key);
-    colfer_u64(o, 4, e.client_id);
-    colfer_u64(o, 5, e.series_id);
-    colfer_u64(o, 6, e.responded_to);
-    if (e.cmd_len != 0) {
-      bo_byte(o, 7);
-      bo_varint(o, e.cmd_len);
-      for (uint32_t c = 0; c * 16 < e.cmd_len; ++c) {
-        const uint4 q = v.ring[ring_ix(v, L.slot, idx, ENT_META + c, L.g)];
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (uint32_t b = 0; b < 16; ++b)
-          if (c * 16 + b < e.cmd_len) bo_byte(o, w[b >> 2] >> (8 * (b & 3)));
-      }
-    }
-    bo_byte(o, 0x7f);
-  }
+  const EntryHdr e = ring_entry_hdr(*L.v, L.slot, L.g, idx, compact);
+  bo_byte(o, 0x0a);  // EntryBatch.Entries, wire type 2
+  bo_varint(o, entry_size(e));
+  emit_entry(o, *L.v, L.slot, L.g, idx, e);
 }
 
 template <int R>
@@ -1963,6 +1976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         n_save = top - start + 1;
         slack = 16 * DRB_SAVE_RECS;
       }
+      if (v.save_tan) slack = v.save_slack;
       if (n_save * entrybatch_elem_bound(v.C16 * 16) + slack >
           (uint64_t)v.save_cap16 * 16)
         fb = DRB_FB_CAPACITY;
@@ -2136,7 +2150,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         if (confirmed_index != r.applied_index)
           st_f(L, r, F_CONFIRMED_INDEX, r.applied_index);
         // SaveRaftState (engine.go:1343) of EntriesToSave
-        if (EXT && has_save && p.encode_saves) {
+        if (EXT && p.encode_saves && v.save_tan) {
+          // the Update a tan LogDB writes, for k_tan_encode (drb_tan.hpp)
+          const uint32_t n_save =
+              has_save ? (uint32_t)(r.last - save_lo + 1) : 0u;
+          const uint32_t tf =
+              1u /*TS_HAVE*/ | (state_changed && !state_empty ? 2u : 0u) |
+              (prev_term != r.term || prev_vote != vote ? 4u : 0u);
+          const uint64_t RG = (uint64_t)v.R * v.G, ti = ix(v, L.slot, L.g);
+          v.tan_sum[ti] = make_uint4((uint32_t)r.term,
+                                     (uint32_t)(r.term >> 32), (uint32_t)vote,
+                                     (uint32_t)(vote >> 32));
+          v.tan_sum[RG + ti] = make_uint4(
+              (uint32_t)r.committed, (uint32_t)(r.committed >> 32),
+              (uint32_t)save_lo, (uint32_t)(save_lo >> 32));
+          v.tan_sum[2 * RG + ti] = make_uint4(n_save, tf, (uint32_t)p.round, 0);
+          c_saved += n_save;
+        } else if (EXT && has_save && p.encode_saves) {
           if (v.save_batched)
             encode_save_records(L, r, save_lo, r.last, crc_tab, c_saved,
                                 c_saved_bytes);

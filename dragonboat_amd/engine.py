@@ -82,6 +82,11 @@ SIGNATURES = {
     "drb_export_saved": (C.c_int, [P, U64, U32, PU8, SZ, PU32, PU32]),
     "drb_saved_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(PU32),
                                     C.POINTER(PU32)]),
+    "drb_export_tan": (C.c_int, [P, U64, U32, C.POINTER(abi.TanRecord), PU8,
+                                 SZ]),
+    "drb_tan_get": (C.c_int, [P, U64, U32, C.POINTER(abi.TanState)]),
+    "drb_tan_set": (C.c_int, [P, U64, U32, C.POINTER(abi.TanState)]),
+    "drb_tan_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
     "drb_plane_counts": (C.c_int, [P, PU32]),
     "drb_plane_peer": (C.c_int, [P, U32, U32, C.c_int]),
     "drb_place_peer": (C.c_int, [U32, U32, U32, U32, C.c_int]),
@@ -136,7 +141,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
-                save_batched=0)
+                save_batched=0, save_tan=0, tan_max_log=0)
 
 
 class Engine:
@@ -155,7 +160,8 @@ class Engine:
                    cfg["total_groups"], cfg["place_world"], cfg["place_rank"],
                    cfg["entry_mbox"], cfg["kv_pool_blocks"],
                    cfg["flagged_cap"], cfg["quiesce"],
-                   cfg["durable_log"], cfg["save_batched"])
+                   cfg["durable_log"], cfg["save_batched"],
+                   cfg["save_tan"], 0, cfg["tan_max_log"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -383,6 +389,26 @@ class Engine:
         _ck(lib().drb_export_saved(self.h, g, slot, buf, cap, C.byref(ln),
                                    C.byref(crc)), "drb_export_saved")
         return bytes(buf[:ln.value]), crc.value
+
+    def export_tan(self, g, slot):
+        """save_tan: (drb_tan_record as a dict, the bytes appended) of one
+        replica's last round."""
+        rec = abi.TanRecord()
+        cap = self.cfg["save_cap"]
+        buf = (C.c_uint8 * max(1, cap))()
+        _ck(lib().drb_export_tan(self.h, g, slot, C.byref(rec), buf, cap),
+            "drb_export_tan")
+        d = {f: getattr(rec, f) for f, _ in rec._fields_ if f != "pad"}
+        return d, bytes(buf[:rec.len])
+
+    def tan_get(self, g, slot):
+        st = abi.TanState()
+        _ck(lib().drb_tan_get(self.h, g, slot, C.byref(st)), "drb_tan_get")
+        return st.offset, st.log, st.state_stored
+
+    def tan_set(self, g, slot, offset, log, state_stored):
+        st = abi.TanState(offset, log, int(bool(state_stored)))
+        _ck(lib().drb_tan_set(self.h, g, slot, C.byref(st)), "drb_tan_set")
 
     def export_save_records(self, g, slot):
         """save_batched: [(batch id, record value, crc32)] of one replica's

@@ -315,6 +315,17 @@ typedef struct drb_config {
    * compactBatchFields applied; drb_export_save_records lists them.
    * Needs window >= 64 and save_cap for a full batch. */
   uint32_t save_batched;
+  /* 1: encode_saves writes each replica's pb.Update as the record a
+   * regular tan LogDB appends to that replica's log (internal/tan/db.go:
+   * 97-130, record.go:548-591; drb_export_tan / drb_tan_buffers): the
+   * marshalled Update (raftpb/update.go:128-169) in 32 KiB-block chunks
+   * with XXH64 checksums, zero padding included, at the log offset the
+   * engine tracks per replica (drb_tan_get / drb_tan_set).  Needs
+   * save_cap; excludes save_batched. */
+  uint32_t save_tan;
+  uint32_t reserved0;
+  /* tan MaxLogFileSize (internal/tan/options.go:29); 0: 64 MiB */
+  uint64_t tan_max_log;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -360,6 +371,9 @@ typedef struct drb_round_out {
   uint64_t replicas_stepped;      /* replicas that ran the round; the others
                                    * were at rest with no input (or
                                    * quiesced at rest on a tick round) */
+  uint64_t log_records;           /* save_tan: records appended to tan logs */
+  uint64_t log_syncs;             /* ... of them with db.write's sync */
+  uint64_t log_new;               /* ... of them that started a new log */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;
@@ -551,6 +565,49 @@ typedef struct drb_save_record {
 } drb_save_record;
 int drb_export_save_records(drb_engine *e, uint64_t group, uint32_t slot,
                             drb_save_record *out, size_t cap, size_t *n);
+/* save_tan: the record replica (slot, group) appended to its tan log in
+ * the last round that ran with encode_saves -- what db.write
+ * (internal/tan/db.go:97-130) puts in the log file: the host pwrites `len`
+ * bytes at `offset` of log `log` (creating that log first when
+ * DRB_TAN_NEW_LOG: createNewLog, open.go:171-198), fsyncs when
+ * DRB_TAN_SYNC, and updates its index with {first_index, last_index}
+ * (EntriesToSave, 0 when none) and `commit` (the State's, 0 when the
+ * Update had none) at position `offset` (db.updateIndex, db.go:139-173). */
+#define DRB_TAN_WRITTEN 1u  /* a record was written (else len = 0) */
+#define DRB_TAN_SYNC 2u     /* db.write's sync result (db.go:113-114) */
+#define DRB_TAN_NEW_LOG 4u  /* makeRoomForWrite switched to a new log */
+#define DRB_TAN_OVERFLOW 8u /* save_cap too small (never with the pre-pass) */
+typedef struct drb_tan_record {
+  uint64_t offset;      /* log offset the bytes start at (d.mu.offset) */
+  uint64_t first_index; /* EntriesToSave[0].Index */
+  uint64_t last_index;  /* EntriesToSave[n-1].Index */
+  uint64_t commit;      /* State.Commit */
+  uint32_t len;         /* bytes appended, zero padding and chunk headers
+                         * included */
+  uint32_t flags;       /* DRB_TAN_* */
+  uint32_t log;         /* this replica's log number (0: the first) */
+  uint32_t pad;
+} drb_tan_record;
+int drb_export_tan(drb_engine *e, uint64_t group, uint32_t slot,
+                   drb_tan_record *rec, uint8_t *buf, size_t cap);
+/* the tan writer position of a replica: the offset in its current log,
+ * that log's number, and whether nodeStates holds a non-empty State (the
+ * next Update's skip / sync decision, db.go:108-114).  drb_tan_set hands a
+ * replica over from a CPU tan db (fallback return, node.go:1139-1159). */
+typedef struct drb_tan_state {
+  uint64_t offset;
+  uint32_t log;
+  uint32_t state_stored;
+} drb_tan_state;
+int drb_tan_get(drb_engine *e, uint64_t group, uint32_t slot,
+                drb_tan_state *out);
+int drb_tan_set(drb_engine *e, uint64_t group, uint32_t slot,
+                const drb_tan_state *in);
+/* The round's tan records on the device for a bulk writer: replica
+ * (slot, g)'s bytes at bytes + (slot * G + g) * save_cap, its record
+ * {offset lo, offset hi, len, flags | log << 8} at recs[slot * G + g]. */
+int drb_tan_buffers(drb_engine *e, void **bytes, void **recs);
+
 /* The whole round's save output on the device, for a GPU-side writer or
  * one D2H copy: replica (slot, g) owns bytes[(slot * G + g) * save_cap ..]
  * with lens[slot * G + g] and crcs[slot * G + g]. */

@@ -63,6 +63,8 @@ STRUCTS = {
     "drb_flagged": abi.Flagged,
     "drb_apply_result": abi.ApplyResult,
     "drb_save_record": abi.SaveRecord,
+    "drb_tan_record": abi.TanRecord,
+    "drb_tan_state": abi.TanState,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}
@@ -127,6 +129,10 @@ def test_engine_without_gpu_fails_loudly():
     dict(num_groups=64, num_replicas=3, save_batched=1, window=64),
     dict(num_groups=64, num_replicas=3, window=48),  # not a power of two
     dict(num_groups=64, num_replicas=3, save_cap=1000),  # not 16 B aligned
+    # tan records go to the save buffer; one persistence format at a time
+    dict(num_groups=64, num_replicas=3, save_tan=1),
+    dict(num_groups=64, num_replicas=3, save_tan=1, save_batched=1,
+         save_cap=4096, window=64),
 ])
 def test_create_rejects_invalid_config(kw):
     """drb_engine_create validates the configuration before it touches a
