@@ -103,6 +103,12 @@ def parse():
     ap.add_argument("--quiesce", type=int, default=-1,
                     help="Config.Quiesce (default: on for c5, SURVEY 8d)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--save", default="",
+                    choices=["", "none", "entrybatch", "tan"],
+                    help="persistence output of every round: none, "
+                         "EntryBatch + CRC32 per replica, or the regular "
+                         "tan LogDB's log record per replica (XXH64 "
+                         "chunks); default: entrybatch for c5, else none")
     ap.add_argument("--no-wire", action="store_true",
                     help="skip the off-GPU wire encode measurement (C3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -224,6 +230,9 @@ def main():
         args.no_read_index = True  # writes, no reads
         if args.groups == 1 << 20:
             args.groups = 4 << 20
+    if not args.save:
+        args.save = "entrybatch" if c5 else "none"
+    saves = args.save != "none"
     G, R, k = args.groups, args.replicas, args.k
     if c4:
         args.no_read_index = True  # 16 B writes, k_w = 1
@@ -259,14 +268,22 @@ def main():
                      max_props=max(1, k), prop_slots=NP, ri_slots=1,
                      mailbox=8, kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
                      kv_pool_blocks=ks * G * R if args.payload == 128
-                     else 4 * G * R, save_cap=(4 * bound + 15) // 16 * 16,
+                     else 4 * G * R, save_cap=(4 * bound + 15) // 16 * 16 +
+                     (128 if args.save == "tan" else 0),
+                     save_tan=int(args.save == "tan"),
                      quiesce=args.quiesce, first_shard_id=first_shard,
                      device=local)
     else:
         first_shard, seed = ddist.shard_plan(rank, G)
+        # with --save: room for the round's EntriesToSave (a follower may
+        # save the last round's entries with this round's)
+        bound = 73 + 32  # EntryBatch element bound at cmd_cap 32
         eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                      max_props=max(1, k), prop_slots=NP, ri_slots=NP,
                      mailbox=16, kv_slots=args.kv_slots or 512, kv_val_cap=4,
+                     save_cap=(((2 * k + 2) * bound + 15) // 16 * 16 + 128
+                               if saves else 0),
+                     save_tan=int(args.save == "tan"),
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
@@ -290,7 +307,7 @@ def main():
         eng.step_async(tick=tick, prop_slot=i % NP,
                        ri_slot=(i % NP) if reads else 0xFFFFFFFF,
                        reads_per_ctx=READS_PER_CTX if fused else 0,
-                       key_space=KEY_SPACE, encode_saves=c5,
+                       key_space=KEY_SPACE, encode_saves=saves,
                        ri_replica=2 if args.reads_at == "follower" else 0,
                        listed=bool(args.listed))
         if reads and not fused:
@@ -350,6 +367,8 @@ def main():
     else:
         alg = alg_bytes_per_group_round(R, k, 16, reads, c4 and world > 1) * \
             g_here
+        if saves:  # + the save bytes the round writes
+            alg += out.saved_bytes / K
     achieved = alg / (kern_ms * 1e-3) / 1e9
     wire = None
     if not (c4 or c5 or args.no_wire):
@@ -460,18 +479,20 @@ def main():
             out.fallbacks, out.errors, by_reason), file=sys.stderr)
     if rank == 0:
         if c5:
+            sv = ("EntryBatch + CRC32 of EntriesToSave" if args.save ==
+                  "entrybatch" else "tan log records (XXH64) of every "
+                  "Update" if args.save == "tan" else "no saves")
             metric = ("committed entries/sec (node) at %d 3-replica groups, "
-                      "%d B payload, %g %% active per round, EntryBatch + "
-                      "CRC32 of EntriesToSave; %%HBM BW" % (
-                          G, args.payload, args.active_ppm / 1e4))
+                      "%d B payload, %g %% active per round, %s; %%HBM BW" % (
+                          G, args.payload, args.active_ppm / 1e4, sv))
             wl = ("C5: %d groups x %d replicas per GPU, %d B PBKV writes "
                   "over %d keys per group (values out of line), %d ppm of "
                   "the groups proposing per "
                   "round (independent seeded draw each round, generated "
-                  "inside the timed loop), EntriesToSave encoded (EntryBatch + CRC32), tick "
+                  "inside the timed loop), %s, tick "
                   "every %d round(s); Quiesce %s%s" % (
                       G, R, args.payload, C5_KEYS[args.payload],
-                      args.active_ppm, args.tick_every,
+                      args.active_ppm, sv, args.tick_every,
                       "on" if args.quiesce else "off",
                       ", listed rounds" if args.listed else ""))
             par = "groups sharded, replicas co-resident"
@@ -545,6 +566,18 @@ def main():
                          "saved_entries": out.saved_entries,
                          "saved_bytes": out.saved_bytes},
         }
+        if args.save == "tan":
+            res["counters"].update(
+                log_records=out.log_records, log_syncs=out.log_syncs,
+                log_new=out.log_new)
+        if saves:
+            res["config"]["save"] = {
+                "entrybatch": "EntriesToSave as one EntryBatch + CRC32 per "
+                              "replica per round (encode_saves)",
+                "tan": "each replica's pb.Update as the regular tan LogDB's "
+                       "log record (Update.MarshalTo in 32 KiB-block chunks "
+                       "with XXH64 checksums, db.write skip / sync, "
+                       "k_tan_encode)"}[args.save]
         if wire is not None:
             res["wire"] = wire
         if host_staged is not None:

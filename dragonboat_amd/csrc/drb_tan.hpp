@@ -15,9 +15,9 @@
 // Update summary (tan_sum, written by step_kernel) and the resident
 // window.  Each lane writes the bytes its log file grows by -- zero padding
 // included -- into its save buffer, with {file offset, length, sync,
-// new-log} for the host's pwrite / fsync.  Chunk checksums are folded as
-// the bytes are produced (streaming XXH64 over 32-byte stripes in
-// registers) and patched into the chunk headers, so nothing is read back.
+// new-log} for the host's pwrite / fsync.  The payload goes out first
+// (16-byte stores), then each chunk's checksum is computed over the bytes
+// read back from L2 and written into its header.
 #pragma once
 #include "drb_codec.hpp"
 #include "drb_layout.hpp"
@@ -53,69 +53,57 @@ __device__ __forceinline__ uint64_t xx_merge(uint64_t acc, uint64_t v) {
   return (acc ^ xx_round(0, v)) * XP1 + XP4;
 }
 
-// streaming XXH64 with seed 0: the current 32-byte stripe in four words
-struct Xxh {
-  uint64_t v0, v1, v2, v3;
-  uint64_t b0, b1, b2, b3;
-  uint32_t n;      // bytes in the stripe
-  uint32_t total;  // bytes hashed
-};
-
-__device__ __forceinline__ void xx_init(Xxh &h) {
-  h.v0 = XP1 + XP2;
-  h.v1 = XP2;
-  h.v2 = 0;
-  h.v3 = 0 - XP1;
-  h.b0 = h.b1 = h.b2 = h.b3 = 0;
-  h.n = h.total = 0;
+// XXH64 (seed 0) of n bytes at byte position p of a lane's 8-byte aligned
+// output: 8-byte words read back with a funnel shift (the lane wrote them
+// just before; they are in L2)
+__device__ __forceinline__ uint64_t ld8(const uint64_t *w, uint32_t p,
+                                        uint32_t cap8) {
+  const uint32_t a = p >> 3, s = (p & 7) * 8;
+  const uint64_t w0 = w[a];
+  if (s == 0) return w0;
+  const uint64_t w1 = a + 1 < cap8 ? w[a + 1] : 0;
+  return (w0 >> s) | (w1 << (64 - s));
 }
 
-__device__ __forceinline__ void xx_byte(Xxh &h, uint32_t b) {
-  const uint64_t x = (uint64_t)(b & 0xffu) << (8 * (h.n & 7));
-  const uint32_t w = h.n >> 3;
-  h.b0 |= w == 0 ? x : 0;
-  h.b1 |= w == 1 ? x : 0;
-  h.b2 |= w == 2 ? x : 0;
-  h.b3 |= w == 3 ? x : 0;
-  h.total++;
-  if (++h.n == 32) {
-    h.v0 = xx_round(h.v0, h.b0);
-    h.v1 = xx_round(h.v1, h.b1);
-    h.v2 = xx_round(h.v2, h.b2);
-    h.v3 = xx_round(h.v3, h.b3);
-    h.b0 = h.b1 = h.b2 = h.b3 = 0;
-    h.n = 0;
-  }
-}
-
-// Sum64's tail and avalanche over the bytes left in the stripe
-__device__ __forceinline__ uint64_t xx_final(const Xxh &h) {
+__device__ uint64_t xxh64_at(const uint64_t *w, uint32_t p, uint32_t n,
+                             uint32_t cap8) {
   uint64_t acc;
-  if (h.total >= 32) {
-    acc = rotl64(h.v0, 1) + rotl64(h.v1, 7) + rotl64(h.v2, 12) +
-          rotl64(h.v3, 18);
-    acc = xx_merge(acc, h.v0);
-    acc = xx_merge(acc, h.v1);
-    acc = xx_merge(acc, h.v2);
-    acc = xx_merge(acc, h.v3);
+  uint32_t left = n;
+  if (n >= 32) {
+    uint64_t v0 = XP1 + XP2, v1 = XP2, v2 = 0, v3 = 0 - XP1;
+    while (left >= 32) {
+      v0 = xx_round(v0, ld8(w, p, cap8));
+      v1 = xx_round(v1, ld8(w, p + 8, cap8));
+      v2 = xx_round(v2, ld8(w, p + 16, cap8));
+      v3 = xx_round(v3, ld8(w, p + 24, cap8));
+      p += 32;
+      left -= 32;
+    }
+    acc = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
+    acc = xx_merge(acc, v0);
+    acc = xx_merge(acc, v1);
+    acc = xx_merge(acc, v2);
+    acc = xx_merge(acc, v3);
   } else {
     acc = XP5;
   }
-  acc += h.total;
-  const uint32_t words = h.n >> 3;
-  if (words > 0) acc = rotl64(acc ^ xx_round(0, h.b0), 27) * XP1 + XP4;
-  if (words > 1) acc = rotl64(acc ^ xx_round(0, h.b1), 27) * XP1 + XP4;
-  if (words > 2) acc = rotl64(acc ^ xx_round(0, h.b2), 27) * XP1 + XP4;
-  uint64_t t = words == 0 ? h.b0 : words == 1 ? h.b1 : words == 2 ? h.b2 : h.b3;
-  uint32_t r = h.n & 7;
-  if (r >= 4) {
-    acc = rotl64(acc ^ (t & 0xffffffffull) * XP1, 23) * XP2 + XP3;
-    t >>= 32;
-    r -= 4;
+  acc += n;
+  while (left >= 8) {
+    acc = rotl64(acc ^ xx_round(0, ld8(w, p, cap8)), 27) * XP1 + XP4;
+    p += 8;
+    left -= 8;
   }
-  for (uint32_t k = 0; k < r; ++k) {
-    acc = rotl64(acc ^ (t & 0xffull) * XP5, 11) * XP1;
-    t >>= 8;
+  if (left) {
+    uint64_t t = ld8(w, p, cap8);
+    if (left >= 4) {
+      acc = rotl64(acc ^ (t & 0xffffffffull) * XP1, 23) * XP2 + XP3;
+      t >>= 32;
+      left -= 4;
+    }
+    for (; left; --left) {
+      acc = rotl64(acc ^ (t & 0xffull) * XP5, 11) * XP1;
+      t >>= 8;
+    }
   }
   acc ^= acc >> 33;
   acc *= XP2;
@@ -126,11 +114,13 @@ __device__ __forceinline__ uint64_t xx_final(const Xxh &h) {
 }
 
 // ------------------------------------------------------------ record out
-// The bytes one record adds to its log file: zero padding when the chunk
-// header does not fit in the block (getNext, record.go:548-573), then the
-// chunks (singleWriter.Write, :628-653), headers filled by fillHeader
-// (:468-487).  Bytes leave as 16-byte stores from a register accumulator;
-// a finished chunk's checksum is patched into its header.
+// Pass 1 writes the bytes one record adds to its log file, chunk headers
+// left zero: zero padding when the header does not fit in the block
+// (getNext, record.go:548-573), a 7-byte header, the payload, and a new
+// header wherever the payload reaches a block's end with bytes left
+// (singleWriter.Write, :628-653).  Bytes leave as 16-byte stores from a
+// register accumulator.  Pass 2 (tan_headers) fills each header
+// (fillHeader, :468-487) from the bytes read back.
 struct TanOut {
   uint4 *dst;
   uint32_t cap16;
@@ -139,20 +129,12 @@ struct TanOut {
   uint32_t pos;     // 16 B chunks stored
   uint32_t total;   // bytes produced
   uint32_t bpos;    // position in the block of the next byte
-  uint32_t hdr;     // output position of the current chunk's header
-  uint32_t cleft;   // payload bytes left in the current chunk
-  uint32_t rleft;   // payload bytes of the record not yet in a chunk
-  bool first;       // the current chunk is the record's first
-  bool overflow;
-  Xxh h;
 };
 
 __device__ __forceinline__ void to_flush16(TanOut &o) {
   if (o.pos < o.cap16)
     o.dst[o.pos] = make_uint4((uint32_t)o.lo, (uint32_t)(o.lo >> 32),
                               (uint32_t)o.hi, (uint32_t)(o.hi >> 32));
-  else
-    o.overflow = true;
   o.pos++;
   o.lo = o.hi = 0;
   o.n = 0;
@@ -165,73 +147,36 @@ __device__ __forceinline__ void to_raw(TanOut &o, uint32_t b) {
   else
     o.hi |= (uint64_t)b << (8 * (o.n - 8));
   o.total++;
-  if (++o.bpos == TAN_BLOCK) o.bpos = 0;
+  o.bpos++;
   if (++o.n == 16) to_flush16(o);
 }
 
-// byte p of the output, already produced as 0: set it
-__device__ __forceinline__ void to_patch(TanOut &o, uint32_t p, uint32_t b) {
-  b &= 0xffu;
-  const uint32_t flushed = o.pos * 16;
-  if (p < flushed) {
-    if (p / 16 < o.cap16) reinterpret_cast<uint8_t *>(o.dst)[p] = (uint8_t)b;
-  } else {
-    const uint32_t k = p - flushed;
-    if (k < 8)
-      o.lo |= (uint64_t)b << (8 * k);
-    else
-      o.hi |= (uint64_t)b << (8 * (k - 8));
-  }
+__device__ __forceinline__ void to_zeros(TanOut &o, uint32_t k) {
+  for (uint32_t i = 0; i < k; ++i) to_raw(o, 0);
 }
 
-// a chunk header at the current position: checksum placeholder, length,
-// type; its checksum covers the type byte and the payload
-__device__ __forceinline__ void to_chunk(TanOut &o, bool first) {
-  const uint32_t room = TAN_BLOCK - o.bpos - TAN_HDR;
-  const uint32_t len = o.rleft < room ? o.rleft : room;
-  o.rleft -= len;
-  const bool last = o.rleft == 0;
-  // fullChunkType 1, firstChunkType 2, middleChunkType 3, lastChunkType 4
-  const uint32_t type = last ? (first ? 1u : 4u) : (first ? 2u : 3u);
-  o.hdr = o.total;
-  for (int k = 0; k < 4; ++k) to_raw(o, 0);
-  to_raw(o, len);
-  to_raw(o, len >> 8);
-  to_raw(o, type);
-  xx_init(o.h);
-  xx_byte(o.h, type);
-  o.cleft = len;
-}
-
-__device__ __forceinline__ void to_end_chunk(TanOut &o) {
-  const uint32_t c = (uint32_t)xx_final(o.h);
-  for (int k = 0; k < 4; ++k) to_patch(o, o.hdr + k, c >> (8 * k));
-}
-
-// begins a record of `len` payload bytes at block position bpos
+// begins a record at block position bpos: padding and the first header
 __device__ __forceinline__ void to_begin(TanOut &o, uint4 *dst, uint32_t cap16,
-                                         uint32_t bpos, uint32_t len) {
+                                         uint32_t bpos) {
   o.dst = dst;
   o.cap16 = cap16;
   o.lo = o.hi = 0;
   o.n = o.pos = o.total = 0;
   o.bpos = bpos;
-  o.overflow = false;
-  if (bpos + TAN_HDR > TAN_BLOCK)  // the rest of the block stays zero
-    while (o.bpos != 0) to_raw(o, 0);
-  o.rleft = len;
-  to_chunk(o, true);
+  if (bpos + TAN_HDR > TAN_BLOCK) {  // the rest of the block stays zero
+    to_zeros(o, TAN_BLOCK - bpos);
+    o.bpos = 0;
+  }
+  to_zeros(o, TAN_HDR);
 }
 
 // one payload byte (the colfer / Update encoders' sink)
 __device__ __forceinline__ void bo_byte(TanOut &o, uint32_t b) {
-  if (o.cleft == 0) {  // the block is full: the next chunk (record.go:639)
-    to_end_chunk(o);
-    to_chunk(o, false);
+  if (o.bpos == TAN_BLOCK) {  // the block is full: the next chunk's header
+    o.bpos = 0;
+    to_zeros(o, TAN_HDR);
   }
   to_raw(o, b);
-  xx_byte(o.h, b);
-  o.cleft--;
 }
 
 __device__ __forceinline__ void to_le32(TanOut &o, uint32_t x) {
@@ -239,8 +184,45 @@ __device__ __forceinline__ void to_le32(TanOut &o, uint32_t x) {
 }
 
 __device__ __forceinline__ void to_finish(TanOut &o) {
-  to_end_chunk(o);
   if (o.n) to_flush16(o);
+}
+
+// Pass 2: the chunk headers of a record of `len` payload bytes laid out by
+// pass 1 from block position bpos in the lane's buffer: checksum = low 32
+// bits of XXH64 over the type byte and the payload, length, type
+// (fullChunkType 1, first 2, middle 3, last 4)
+__device__ __forceinline__ void tan_headers(uint4 *dst, uint32_t cap16,
+                                            uint32_t bpos, uint32_t len) {
+  // pass 1's stores are visible to this lane's loads
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  uint8_t *b = reinterpret_cast<uint8_t *>(dst);
+  const uint64_t *w = reinterpret_cast<const uint64_t *>(dst);
+  uint32_t h = 0;
+  if (bpos + TAN_HDR > TAN_BLOCK) {
+    h = TAN_BLOCK - bpos;
+    bpos = 0;
+  }
+  bool first = true;
+  uint32_t left = len;
+  for (;;) {
+    const uint32_t room = TAN_BLOCK - bpos - TAN_HDR;
+    const uint32_t k = left < room ? left : room;
+    left -= k;
+    const uint32_t type = left == 0 ? (first ? 1u : 4u) : (first ? 2u : 3u);
+    b[h + 6] = (uint8_t)type;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    const uint32_t c = (uint32_t)xxh64_at(w, h + 6, k + 1, cap16 * 2);
+    b[h + 0] = (uint8_t)c;
+    b[h + 1] = (uint8_t)(c >> 8);
+    b[h + 2] = (uint8_t)(c >> 16);
+    b[h + 3] = (uint8_t)(c >> 24);
+    b[h + 4] = (uint8_t)k;
+    b[h + 5] = (uint8_t)(k >> 8);
+    if (left == 0) return;
+    h += TAN_HDR + k;
+    bpos = 0;
+    first = false;
+  }
 }
 
 // bytes a record of `len` payload bytes adds at block position bpos
@@ -328,7 +310,8 @@ __global__ __launch_bounds__(256) void k_tan_encode(View v, uint32_t round,
           rec.w = (st.z << 8) | DRB_TAN_OVERFLOW;
         } else {
           TanOut o;
-          to_begin(o, v.save_buf + i * v.save_cap16, v.save_cap16, bpos, len);
+          uint4 *dst = v.save_buf + i * v.save_cap16;
+          to_begin(o, dst, v.save_cap16, bpos);
           bo_varint(o, shard);
           bo_varint(o, slot + 1);
           if (u_state) {
@@ -351,6 +334,7 @@ __global__ __launch_bounds__(256) void k_tan_encode(View v, uint32_t round,
           }
           bo_byte(o, 0);  // IsEmptySnapshot
           to_finish(o);
+          tan_headers(dst, v.save_cap16, bpos, len);
           // writeRecord's offset (record.go:589) = the file's new size
           rec.x = (uint32_t)off;
           rec.y = (uint32_t)(off >> 32);
