@@ -70,19 +70,20 @@ _REPLICA_U64 = [
     "saved_to", "applied_to_index", "applied_to_term", "applied_index",
     "confirmed_index", "pushed_index", "prev_term", "prev_vote",
     "prev_commit", "sm_index", "sm_term", "kv_count", "qs_current_tick",
-    "qs_idle_since", "qs_quiesced_since", "qs_exit_quiesce_tick"]
+    "qs_idle_since", "qs_quiesced_since", "qs_exit_quiesce_tick", "rng"]
 
 
 class ReplicaState(C.Structure):
     _fields_ = ([(n, C.c_uint64) for n in _REPLICA_U64] +
                 [("role", C.c_uint32), ("flags", C.c_uint32),
                  ("fallback_reason", C.c_uint32), ("ri_count", C.c_uint32),
+                 ("votes", C.c_uint32), ("pad0", C.c_uint32),
                  ("remotes", RemoteState * DRB_MAX_REPLICAS),
                  ("ri", ReadStatus * DRB_RI_DEPTH)])
 
     def to_dict(self, num_replicas=None):
         d = {n: getattr(self, n) for n in _REPLICA_U64}
-        for n in ("role", "flags", "fallback_reason", "ri_count"):
+        for n in ("role", "flags", "fallback_reason", "ri_count", "votes"):
             d[n] = getattr(self, n)
         nr = num_replicas or DRB_MAX_REPLICAS
         d["remotes"] = [(r.match, r.next, r.state, r.active)
@@ -130,7 +131,7 @@ class Config(C.Structure):
                 ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
                 ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
                 ("save_batched", C.c_uint32), ("save_tan", C.c_uint32),
-                ("reserved0", C.c_uint32), ("tan_max_log", C.c_uint64)]
+                ("elections", C.c_uint32), ("tan_max_log", C.c_uint64)]
 
 
 class ApplyResult(C.Structure):
@@ -229,7 +230,9 @@ class RoundOut(C.Structure):
                 ("saved_entries", C.c_uint64), ("saved_bytes", C.c_uint64),
                 ("replicas_stepped", C.c_uint64),
                 ("log_records", C.c_uint64), ("log_syncs", C.c_uint64),
-                ("log_new", C.c_uint64)]
+                ("log_new", C.c_uint64),
+                ("elections_stepped", C.c_uint64),
+                ("role_changes", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

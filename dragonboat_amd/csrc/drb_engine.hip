@@ -196,6 +196,9 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (cfg->save_tan && (cfg->save_cap == 0 || cfg->save_batched))
     return DRB_EINVAL;
+  // elections: the raft launch steps co-resident replicas, Quiesce off
+  if (cfg->elections && (cfg->place_world > 1 || cfg->quiesce))
+    return DRB_EINVAL;
   // entry_mbox travels as the 8-bit E of the plane summary word
   // (block_plane_summary, DRB_PLANE_E)
   if (cfg->place_world > 1 &&
@@ -340,6 +343,16 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.tan_ctr, e->tan_blocks * 4);
     rc |= dalloc(e, &e->tan_total, 4);
   }
+  v.elections = cfg->elections ? 1u : 0u;
+  if (v.elections) {
+    // the raft launch's workgroups own counter rows 0.. (block_counters):
+    // at most 2 per group block
+    v.slow_cap = (uint32_t)std::min<uint64_t>(
+        R * G, 2ull * ((G + 255) / 256) * 256);
+    rc |= dalloc(e, &v.slow_list, v.slow_cap);
+    rc |= dalloc(e, &v.slow_n, 1);
+    rc |= dalloc(e, &v.rterm, 2ull * R * R * v.MB * G);
+  }
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
   rc |= dalloc(e, &e->ctr_total, NUM_COUNTERS);
@@ -418,7 +431,8 @@ static const int kU64Order[NUM_U64_EXPORTED] = {
     F_SAVED_TO,       F_APPLIED_TO_INDEX, F_APPLIED_TO_TERM, F_APPLIED_INDEX,
     F_CONFIRMED_INDEX, F_PUSHED_INDEX, F_PREV_TERM,       F_PREV_VOTE,
     F_PREV_COMMIT,    F_SM_INDEX,      F_SM_TERM,         F_KV_COUNT,
-    F_QS_TICK,        F_QS_IDLE,       F_QS_SINCE,        F_QS_EXIT};
+    F_QS_TICK,        F_QS_IDLE,       F_QS_SINCE,        F_QS_EXIT,
+    F_RNG};
 
 // drb_replica_state fields 2.. in kU64Order order (after shard/replica id)
 static uint64_t *st_u64(drb_replica_state *s, int k) {
@@ -519,6 +533,7 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
       for (int k = 0; k < NUM_U64; ++k) {
         const bool counter = k == F_TICK_COUNT || k == F_KV_COUNT ||
                              (k >= F_QS_TICK && k <= F_QS_EXIT) ||
+                             k == F_RNG ||
                              k == F_QS_BASE || k == F_SAVE_BASE;
         i64.push_back(u64_ix(v, k, s, g));
         d64.push_back(counter ? vals[k] : (over[k] ? over[k] : vals[k]));
@@ -526,7 +541,7 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
       const uint32_t quiesced =
           v.quiesce && c.qs_quiesced_since > 0 ? F_QUIESCED : 0u;
       const uint32_t w32[NUM_U32] = {c.role, (c.flags & F_PUBLIC) | quiesced,
-                                     c.fallback_reason, c.ri_count};
+                                     c.fallback_reason, c.ri_count, c.votes};
       for (int k = 0; k < NUM_U32; ++k) {
         i32.push_back(u32_ix(v, k, s, g));
         d32.push_back(w32[k]);
@@ -613,6 +628,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       o.flags = d32[b++] & F_PUBLIC;
       o.fallback_reason = d32[b++];
       o.ri_count = d32[b++];
+      o.votes = d32[b++];
       for (uint32_t p = 0; p < R; ++p, ++c2) {
         o.remotes[p].match = drm[c2];
         o.remotes[p].next = drn[c2];
@@ -811,11 +827,16 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   for (int f = F_QS_TICK; f <= F_QS_EXIT; ++f) v.u64[u64_ix(v, f, s, g)] = vals[f];
   v.u64[u64_ix(v, F_QS_BASE, s, g)] = 0;
   v.u64[u64_ix(v, F_SAVE_BASE, s, g)] = 0;
+  // raft.rand: restarted from a per-replica seed (the oracle's setup does
+  // the same), one splitmix64 draw per randomized timeout afterwards
+  v.u64[u64_ix(v, F_RNG, s, g)] =
+      mix64(seed ^ (0xE2ull << 56) ^ (gid(v, s, g) * R + s));
   v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
   v.u32[u32_ix(v, W_FLAGS, s, g)] =
       gid(v, s, g) < v.total_groups ? DRB_F_HOSTED : 0u;
   v.u32[u32_ix(v, W_FB_REASON, s, g)] = 0;
   v.u32[u32_ix(v, W_RI_COUNT, s, g)] = 0;
+  v.u32[u32_ix(v, W_VOTES, s, g)] = 0;
   for (uint32_t p = 0; p < v.R; ++p) {
     uint64_t m, n;
     uint32_t st, act;
@@ -1189,7 +1210,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     planes[p].maxapp_valid = mi_nrep(cur.y) > 0;
   }
   // 3. place every message in its plane, in order
-  std::vector<uint64_t> ridx, eidx;
+  std::vector<uint64_t> ridx, eidx, tridx, trval;
   std::vector<uint4> rval, eval;
   std::vector<uint4> ch(ENT_META + v.C16);
   for (size_t i = 0; i < n; ++i) {
@@ -1246,6 +1267,10 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       } else if (q_hi(cur) != m.term) {
         other = true;
         c0.x |= MF_TERM_OTHER;
+        if (v.rterm) {  // elections: the raft launch reads it
+          tridx.push_back(rterm_ix(v, buf, pl.from, pl.to, k, pl.g));
+          trval.push_back(m.term);
+        }
       }
     }
     ridx.push_back(mbox_ix(v, buf, pl.from, pl.to, k, 0, pl.g));
@@ -1287,7 +1312,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     tbyte[it->second] |= (uint64_t)tag_byte(tag, pl.cur.y) << (8 * pl.from);
   }
   std::vector<uint64_t> tv;
-  if (scatter(e, v.ring, eidx, eval) || scatter(e, v.mbox, ridx, rval) ||
+  if ((v.rterm && scatter(e, v.rterm, tridx, trval)) ||
+      scatter(e, v.ring, eidx, eval) || scatter(e, v.mbox, ridx, rval) ||
       scatter(e, v.mbox_meta, hidx, hval) ||
       scatter(e, v.mbox_maxapp, xidx, xval) || gather(e, v.inbox_tag, tidx, tv))
     return DRB_EDEVICE;
@@ -1502,6 +1528,13 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
   }
+  if (e->v.elections) {  // the replicas the two launches routed (F_SLOW)
+    RoundParams ps = p0;
+    ps.slots = 0;
+    ps.nrows = 1;
+    step_kernel<R, true, true, true>
+        <<<(e->v.slow_cap + 255) / 256, 256, 0, e->stream>>>(e->v, ps);
+  }
 }
 
 // role map: bit s of role_slots[0] when a hosted replica of slot s is a
@@ -1523,6 +1556,10 @@ __global__ void k_role_scan(View v, uint32_t *out) {
 }
 
 static int refresh_roles(drb_engine *e) {
+  if (e->v.elections) {  // roles change on the device: both launches span
+    e->role_slots[0] = e->role_slots[1] = (1u << e->v.R) - 1u;  // every slot
+    return DRB_OK;
+  }
   HIPCHK(hipMemsetAsync(e->role_dev, 0, 8, e->stream));
   dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
   k_role_scan<<<grid, 256, 0, e->stream>>>(e->v, e->role_dev);
@@ -1564,7 +1601,9 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
   p.ri_replica = in->ri_replica;
   p.listed = in->listed ? 1 : 0;
-  if (p.listed && e->v.remote_mask) return DRB_EINVAL;
+  if (p.listed && (e->v.remote_mask || e->v.elections)) return DRB_EINVAL;
+  if (e->v.elections)  // this round's slow list
+    HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
   if (p.ri_replica > e->v.R || (p.ri_replica && e->v.place_world > 1))
     return DRB_EINVAL;
   if (e->v.remote_mask)  // plane summaries of this round only
@@ -1634,6 +1673,8 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->saved_entries = c[C_SAVED_ENTRIES];
   out->saved_bytes = c[C_SAVED_BYTES];
   out->replicas_stepped = c[C_STEPPED];
+  out->elections_stepped = c[C_ELECT];
+  out->role_changes = c[C_ROLE];
   out->log_records = 0;
   out->log_syncs = 0;
   out->log_new = 0;
@@ -1858,7 +1899,13 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
   for (uint32_t q = 0; q < k; ++q) {
     if (*nm >= cap) return DRB_ERANGE;
     const uint4 *c = &val[q * MSG_CHUNKS];
-    Msg mm = msg_decode(c[0], c[1], q_hi(meta), prev_lo, prev_hi);
+    uint64_t rt = q_hi(meta);
+    if ((c[0].x & MF_TERM_OTHER) && v.rterm) {  // elections: its own term
+      std::vector<uint64_t> ti{rterm_ix(v, buf, from, to, pos[q], g)}, tv;
+      if (gather(e, v.rterm, ti, tv)) return DRB_EDEVICE;
+      rt = tv[0];
+    }
+    Msg mm = msg_decode(c[0], c[1], rt, prev_lo, prev_hi);
     drb_message &m = out[(*nm)++];
     memset(&m, 0, sizeof(m));
     m.shard_id = v.first_shard_id + gid(v, from, g);

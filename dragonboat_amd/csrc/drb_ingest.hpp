@@ -407,6 +407,7 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
       } else if (q_hi(cur) != m.term) {
         other = true;
         c0.x |= MF_TERM_OTHER;
+        if (v.rterm) v.rterm[rterm_ix(v, buf, from, to, kk, g)] = m.term;
       }
     }
     v.mbox[mbox_ix(v, buf, from, to, kk, 0, g)] = c0;

@@ -50,6 +50,7 @@ enum U64Field : int {
   F_QS_IDLE,     // .idleSince
   F_QS_SINCE,    // .quiescedSince (0: not quiesced)
   F_QS_EXIT,     // .exitQuiesceTick
+  F_RNG,         // raft.rand state (splitmix64): randomized timeouts
   // internal (not part of drb_replica_state)
   F_RING_LO,     // lowest index still resident in the window
   F_RING_GUARD,  // lowest index referenced by last round's Replicates
@@ -215,15 +216,25 @@ __host__ __device__ inline void pk_decode(const uint32_t *w,
   vals[F_TICK_COUNT] = over[F_TICK_COUNT];
   vals[F_KV_COUNT] = over[F_KV_COUNT];
   for (int f = F_QS_TICK; f <= F_QS_EXIT; ++f) vals[f] = over[f];
+  vals[F_RNG] = over[F_RNG];
   vals[F_QS_BASE] = over[F_QS_BASE];
 }
 
 // per-replica u32 fields, array [F][slot][g]
-enum U32Field : int { W_ROLE = 0, W_FLAGS, W_FB_REASON, W_RI_COUNT, NUM_U32 };
+enum U32Field : int {
+  W_ROLE = 0,
+  W_FLAGS,
+  W_FB_REASON,
+  W_RI_COUNT,
+  W_VOTES,  // candidate votes: answered | granted << 8, bit per slot
+  NUM_U32
+};
 
 // internal W_FLAGS bits (masked out of drb_replica_state.flags)
 constexpr uint32_t F_AT_REST = 1u << 16;  // a round without input is a no-op
 constexpr uint32_t F_QUIESCED = 1u << 17;  // node.qs.quiesced() (Quiesce on)
+// elections: the replica's round goes to the raft launch (slow list)
+constexpr uint32_t F_SLOW = 1u << 18;
 constexpr uint32_t F_PUBLIC = 0xffffu;
 
 // message record: 1-2 x uint4 (drb_msg.hpp)
@@ -316,6 +327,14 @@ struct View {
   uint4 *tan_st;          // [R][G] {offset lo, hi, log, TST_* flags}
   uint4 *tan_rec;         // [R][G] {offset lo, hi, len, DRB_TAN_* | log << 8}
   unsigned long long *tan_ctr;  // [blocks][4] bytes, records, syncs, logs
+  // elections (drb_config.elections): the replicas the raft launch steps
+  // this round {g lo, g hi, slot, 0}, their count, and the term of every
+  // record it wrote whose term differs from its header's (MF_TERM_OTHER)
+  uint32_t elections;
+  uint32_t slow_cap;
+  uint4 *slow_list;
+  unsigned long long *slow_n;
+  uint64_t *rterm;        // [2][R][R][MB][G]
   // placement (drb_config) and the cross-rank planes (world >= 2)
   uint32_t place_world, place_rank;
   uint64_t total_groups;
@@ -400,6 +419,11 @@ __host__ __device__ inline bool pair_remote(const View &v, uint32_t from,
   return (v.remote_mask >> (from * v.R + to)) & 1ull;
 }
 // the global group of replica slot s at lane g (include/drb_engine.h)
+__host__ __device__ inline uint64_t rterm_ix(const View &v, uint32_t buf,
+                                             uint32_t from, uint32_t to,
+                                             uint32_t k, uint64_t g) {
+  return ((((uint64_t)buf * v.R + from) * v.R + to) * v.MB + k) * v.G + g;
+}
 __host__ __device__ inline uint64_t gid(const View &v, uint32_t s,
                                         uint64_t g) {
   if (v.place_world <= 1) return g;

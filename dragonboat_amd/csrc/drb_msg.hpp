@@ -19,7 +19,11 @@
 //   HeartbeatResp  a=Hint x=HintHigh (hh32)  else c1={Hint, HintHigh}
 //   ReadIndex      a=Commit    c1={Hint, HintHigh}
 //   ReadIndexResp  a=LogIndex  c1={Hint, HintHigh}
+//   RequestVote    a=LogIndex  c1={LogTerm, Hint}      (elections)
+//   RequestVoteResp, NoOP      Reject in meta, nothing else
 //   other          a=LogIndex  c1={Hint, HintHigh}
+// term_other: the record's term is not its header's; it is in the rterm
+// side array (elections: a sender whose term changed within the round)
 // hint_prev: the ReadIndex ctx {Hint, HintHigh} equals the last ctx written
 // explicitly in this (sender, receiver) record sequence (a leader sends the
 // same ctx twice per round: with the ReadIndex broadcast and, as peepCtx,
@@ -226,6 +230,15 @@ __host__ __device__ inline bool msg_encode(const Msg &m, uint32_t dest,
       c = m.hint_high;
       has = !dedup;
       break;
+    case DRB_MSG_REQUEST_VOTE:
+      a = m.log_index;
+      b = m.log_term;
+      c = m.hint;
+      has = true;
+      break;
+    case DRB_MSG_REQUEST_VOTE_RESP:
+    case DRB_MSG_NOOP:
+      break;
     default:
       a = m.log_index;
       b = m.hint;
@@ -293,6 +306,14 @@ __host__ __device__ inline Msg msg_decode(uint4 c0, uint4 c1,
       m.commit = a;
       m.hint = b;
       m.hint_high = c;
+      break;
+    case DRB_MSG_REQUEST_VOTE:
+      m.log_index = a;
+      m.log_term = b;
+      m.hint = c;
+      break;
+    case DRB_MSG_REQUEST_VOTE_RESP:
+    case DRB_MSG_NOOP:
       break;
     default:
       m.log_index = a;

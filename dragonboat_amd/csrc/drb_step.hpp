@@ -82,6 +82,8 @@ enum : int {
   C_SAVED_ENTRIES,  // encode_saves
   C_SAVED_BYTES,
   C_STEPPED,  // replicas that ran the round (not skipped as idle)
+  C_ELECT,    // elections: replicas the raft launch stepped
+  C_ROLE,     // elections: role changes
   NUM_COUNTERS
 };
 
@@ -103,6 +105,7 @@ struct Rep {
   uint32_t kv_added;     // KVTest.Count increments this round
   bool applied_any, lid_dirty;
   uint32_t role, flags, fb, ri_count;
+  uint32_t votes;  // elections: answered | granted << 8, bit per slot
   // leader remotes live in LDS (RemLds), see rem_get/rem_put
   // leader: readIndex queue
   uint64_t ri_lo[DRB_RI_DEPTH], ri_hi[DRB_RI_DEPTH], ri_ix[DRB_RI_DEPTH],
@@ -144,6 +147,7 @@ struct Lane {
   uint64_t g;
   uint32_t rbuf, wbuf;
   uint64_t round;
+  bool slow;  // the raft launch (elections): records carry their own term
 };
 
 // ------------------------------------------------------------ helpers
@@ -363,6 +367,9 @@ DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   const uint32_t inf = msg_info(mm.type, mm.term == 0, m.reject != 0);
   w = (w + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
   v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] = c0;
+  // the raft launch may change its term after this record: keep the
+  // record's own (the header gets the final term, drb_msg.hpp)
+  if (L.slow) v.rterm[rterm_ix(v, L.wbuf, L.slot, to_slot, k, L.g)] = mm.term;
   if (has) {
     v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 1, L.g)] = c1;
     r.c1mask |= 1u << to_slot;
@@ -893,6 +900,275 @@ DRB_DEV void dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
       follower_heartbeat(L, r, s, m);
     else if (m.type == DRB_MSG_READ_INDEX_RESP)
       follower_read_index_resp(L, r, s, m);
+  }
+}
+
+// ------------------------------------------------------------ elections
+// The raft launch (drb_config.elections): the state changes
+// the step round leaves to the CPU path -- term changes, votes, the
+// candidate state, CheckQuorum step-down -- restated from raft.go for the
+// replicas the step kernels routed to it (F_SLOW).
+
+// raft.rand -> setRandomizedElectionTimeout (raft.go:658-661): one
+// splitmix64 draw from the replica's generator state
+template <int R>
+DRB_DEV void el_rand_timeout(const Lane &L, Rep<R> &r) {
+  const View &v = *L.v;
+  uint64_t s = over_ld(L, F_RNG) + 0x9E3779B97F4A7C15ull;
+  over_st(L, F_RNG, s);
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  st_f(L, r, F_RAND_TIMEOUT, v.election_rtt + z % v.election_rtt);
+}
+
+// a new term: the record's term-relative fields are re-coded against it,
+// and no log entry carries it yet (term_start, log_term)
+template <int R>
+DRB_DEV void el_set_term(const Lane &L, Rep<R> &r, uint64_t t) {
+  const uint64_t at = ld_f(L, r, F_APPLIED_TO_TERM);
+  const uint64_t pt = ld_f(L, r, F_PREV_TERM);
+  const uint64_t smt = r.applied_any ? r.sm_term : ld_f(L, r, F_SM_TERM);
+  r.term = t;
+  r.pw[2] = (uint32_t)t;
+  r.pw[3] = (uint32_t)(t >> 32);
+  st_f(L, r, F_APPLIED_TO_TERM, at);
+  st_f(L, r, F_PREV_TERM, pt);
+  if (!r.applied_any) st_f(L, r, F_SM_TERM, smt);
+  r.term_start = r.last + 1;
+}
+
+// reset (raft.go:1052-1073) with resetRemotes (raft.go:1088-1097)
+template <int R>
+DRB_DEV void el_reset(const Lane &L, Rep<R> &r, uint64_t term,
+                      bool reset_election) {
+  if (r.term != term) {
+    el_set_term(L, r, term);
+    st_f(L, r, F_VOTE, 0);
+  }
+  if (reset_election) {
+    r.election_tick = 0;
+    el_rand_timeout(L, r);
+  }
+  r.votes = 0;
+  r.heartbeat_tick = 0;
+  r.ri_count = 0;
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    rem_put<R>(L, s,
+               RemoteV{(uint32_t)s == L.slot ? r.last : 0, r.last + 1,
+                       DRB_REMOTE_RETRY, 0});
+}
+
+// becomeFollower / becomeFollowerKE (raft.go:961-999)
+template <int R>
+DRB_DEV void el_become_follower(const Lane &L, Rep<R> &r, uint64_t term,
+                                uint64_t leader, bool reset_election) {
+  r.role = DRB_FOLLOWER;
+  el_reset(L, r, term, reset_election);
+  set_leader(r, leader);
+  r.leader_update = true;
+}
+
+// becomeLeader (raft.go:1038-1050): the term-start no-op entry
+// (appendEntries, raft.go:944-955); config-change entries never reach the
+// GPU log, so preLeaderPromotionHandleConfigChange finds none
+template <int R>
+DRB_DEV void el_become_leader(const Lane &L, Rep<R> &r) {
+  const View &v = *L.v;
+  r.role = DRB_LEADER;
+  el_reset(L, r, r.term, true);
+  set_leader(r, (uint64_t)L.slot + 1);
+  r.leader_update = true;
+  const uint64_t idx = r.last + 1;
+  v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = mk4(r.term, 0);
+  v.ring[ring_ix(v, L.slot, idx, 1, L.g)] = mk4(0, 0);
+  v.ring[ring_ix(v, L.slot, idx, 2, L.g)] = make_uint4(0, 0, 0, 0);
+  r.last = idx;
+  if (r.last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, r.last + 1 - v.W);
+  if (r.term_start > idx) r.term_start = idx;
+  rem_try_update<R>(L, (int)L.slot, r.last);  // self remote
+  if (R == 1) try_commit(L, r);
+}
+
+// handleVoteResp (raft.go:1125-1147): granted votes so far
+template <int R>
+DRB_DEV uint32_t el_vote_resp(Rep<R> &r, uint32_t from_slot, bool rejected) {
+  if (!((r.votes >> from_slot) & 1u)) {
+    r.votes |= 1u << from_slot;
+    if (!rejected) r.votes |= 1u << (8 + from_slot);
+  }
+  return __builtin_popcount(r.votes >> 8);
+}
+
+// campaign (raft.go:1176-1217) after becomeCandidate (raft.go:1020-1036)
+template <int R>
+DRB_DEV void el_campaign(const Lane &L, Rep<R> &r) {
+  r.role = DRB_CANDIDATE;
+  el_reset(L, r, r.term + 1, true);
+  set_leader(r, 0);
+  r.leader_update = true;
+  st_f(L, r, F_VOTE, (uint64_t)L.slot + 1);
+  el_vote_resp(r, L.slot, false);
+  if (R == 1) {  // a single-node quorum
+    el_become_leader(L, r);
+    return;
+  }
+  Msg m = {};
+  m.type = DRB_MSG_REQUEST_VOTE;
+  m.log_index = r.last;
+  m.log_term = log_term(L, r, r.last);
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if ((uint32_t)s != L.slot) emit(L, r, (uint32_t)s, m);
+}
+
+// handleNodeElection (raft.go:1632-1668): not while a config change may be
+// waiting to be applied (hasConfigChangeToApply, raft.go:1611-1622)
+template <int R>
+DRB_DEV void el_election(const Lane &L, Rep<R> &r) {
+  if (r.role == DRB_LEADER) return;
+  if (r.committed > ld_f(L, r, F_APPLIED)) return;
+  el_campaign(L, r);
+}
+
+// upToDate (logentry.go:381-393)
+template <int R>
+DRB_DEV bool el_up_to_date(const Lane &L, Rep<R> &r, uint64_t index,
+                           uint64_t term) {
+  const uint64_t lt = log_term(L, r, r.last);
+  return term > lt || (term == lt && index >= r.last);
+}
+
+// handleNodeRequestVote (raft.go:1697-1722)
+template <int R>
+DRB_DEV void el_request_vote(const Lane &L, Rep<R> &r, int s, const Msg &m) {
+  const uint64_t vote = ld_f(L, r, F_VOTE);
+  const bool can = vote == 0 || vote == (uint64_t)s + 1 || m.term > r.term;
+  Msg resp = {};
+  resp.type = DRB_MSG_REQUEST_VOTE_RESP;
+  if (can && el_up_to_date(L, r, m.log_index, m.log_term)) {
+    r.election_tick = 0;
+    st_f(L, r, F_VOTE, (uint64_t)s + 1);
+  } else {
+    resp.reject = 1;
+  }
+  emit(L, r, (uint32_t)s, resp);
+}
+
+// handleCandidateRequestVoteResp (raft.go:2235-2253)
+template <int R>
+DRB_DEV void el_candidate_vote_resp(const Lane &L, Rep<R> &r, int s,
+                                    const Msg &m) {
+  constexpr uint32_t quorum = R / 2 + 1;
+  const uint32_t granted = el_vote_resp(r, (uint32_t)s, m.reject != 0);
+  const uint32_t answered = __builtin_popcount(r.votes & 0xffu);
+  if (granted == quorum) {
+    el_become_leader(L, r);
+    broadcast_replicate(L, r);
+  } else if (answered - granted == quorum) {
+    el_become_follower(L, r, r.term, 0, true);
+  }
+}
+
+DRB_DEV bool el_leader_message(uint32_t t) {  // isLeaderMessage
+  return t == DRB_MSG_REPLICATE || t == DRB_MSG_INSTALL_SNAPSHOT ||
+         t == DRB_MSG_HEARTBEAT || t == DRB_MSG_TIMEOUT_NOW ||
+         t == DRB_MSG_READ_INDEX_RESP;
+}
+
+// Handle's term gate (raft.go:1596-1609): onMessageTermNotMatched
+// (raft.go:1540-1590) with dropRequestVoteFromHighTermNode (1507-1529);
+// true: the message is dropped
+template <int R>
+DRB_DEV bool el_term_gate(const Lane &L, Rep<R> &r, int s, const Msg &m) {
+  const View &v = *L.v;
+  if (m.term == 0 || m.term == r.term) return false;
+  if (m.type == DRB_MSG_REQUEST_VOTE && v.check_quorum && m.term > r.term &&
+      m.hint != (uint64_t)s + 1 && r.leader_id != 0 &&
+      r.election_tick < v.election_rtt)
+    return true;
+  if (m.term > r.term) {
+    const uint64_t leader = el_leader_message(m.type) ? (uint64_t)s + 1 : 0;
+    el_become_follower(L, r, m.term, leader,
+                       m.type != DRB_MSG_REQUEST_VOTE);  // ...KE keeps ticks
+    return false;
+  }
+  if (el_leader_message(m.type) && v.check_quorum) {
+    Msg resp = {};
+    resp.type = DRB_MSG_NOOP;
+    emit(L, r, (uint32_t)s, resp);
+  }
+  return true;
+}
+
+// the handler table (raft.go:2332-2417) for the three states of the path
+template <int R>
+DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
+                         const EntSrc &src) {
+  if (el_term_gate(L, r, s, m)) return;
+  const uint32_t t = m.type;
+  if (r.role == DRB_LEADER) {
+    if (t == DRB_MSG_REQUEST_VOTE)
+      el_request_vote(L, r, s, m);
+    else
+      dispatch(L, r, s, m, src);
+  } else if (r.role == DRB_FOLLOWER) {
+    if (t == DRB_MSG_REQUEST_VOTE)
+      el_request_vote(L, r, s, m);
+    else if (t == DRB_MSG_READ_INDEX)  // handleFollowerReadIndex
+      follower_read_index(L, r, m.hint, m.hint_high);
+    else
+      dispatch(L, r, s, m, src);
+  } else {  // candidate
+    if (t == DRB_MSG_REPLICATE || t == DRB_MSG_HEARTBEAT) {
+      // handleCandidateReplicate / Heartbeat (raft.go:2205-2233)
+      el_become_follower(L, r, r.term, (uint64_t)s + 1, true);
+      dispatch(L, r, s, m, src);
+    } else if (t == DRB_MSG_REQUEST_VOTE_RESP) {
+      el_candidate_vote_resp(L, r, s, m);
+    } else if (t == DRB_MSG_REQUEST_VOTE) {
+      el_request_vote(L, r, s, m);
+    } else if (t == DRB_MSG_READ_INDEX) {  // handleCandidateReadIndex
+      r.ndropped_ri++;
+    }
+  }
+}
+
+// LocalTick (raft.go:571-648) for any role; CheckQuorum (raft.go:1785-1792)
+// may step the leader down
+template <int R>
+DRB_DEV void el_tick(const Lane &L, Rep<R> &r) {
+  const View &v = *L.v;
+  over_st(L, F_TICK_COUNT, over_ld(L, F_TICK_COUNT) + 1);
+  if (r.role == DRB_LEADER) {
+    r.election_tick++;
+    if (r.election_tick >= v.election_rtt) {
+      r.election_tick = 0;
+      if (v.check_quorum) {  // leaderHasQuorum (raft.go:395-405)
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          RemoteV x = rem_get<R>(L, s);
+          if ((uint32_t)s == L.slot || x.a) c++;
+          x.a = 0;
+          rem_put<R>(L, s, x);
+        }
+        if (c < R / 2 + 1) el_become_follower(L, r, r.term, 0, true);
+      }
+    }
+    r.heartbeat_tick++;
+    if (r.heartbeat_tick >= v.heartbeat_rtt) {
+      r.heartbeat_tick = 0;
+      if (r.role == DRB_LEADER) broadcast_heartbeat(L, r);
+    }
+    return;
+  }
+  r.election_tick++;
+  if (r.election_tick >= ld_f(L, r, F_RAND_TIMEOUT)) {
+    r.election_tick = 0;
+    el_election(L, r);
   }
 }
 
@@ -1698,7 +1974,10 @@ DRB_DEV void block_plane_summary(const View &v, BlockPos bp, uint32_t from,
 // to what its own handlers need.
 // EXT: the instantiation for Cmds longer than 64 B, out-of-line values or
 // encode_saves (C5); the other one keeps the common path lean
-template <int R, bool LEAD, bool EXT>
+// SLOW: the raft launch of an elections engine (LEAD = EXT = true): it
+// steps the replicas on the slow list (F_SLOW) with the election state
+// machine (el_*, above) as well, whatever their role.
+template <int R, bool LEAD, bool EXT, bool SLOW = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT ? DRB_EXT_LEAD_WAVES : DRB_LEAD_WAVES) : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
@@ -1707,8 +1986,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   const View *vp = &v;
   const BlockPos bp = block_pos(p);
   // the slots this launch steps (4 bits each): a role's launch covers only
-  // the slots where that role occurs (drb_engine.hip role map)
-  const uint32_t slot = (p.slots >> (4 * bp.y)) & 0xfu;
+  // the slots where that role occurs (drb_engine.hip role map); the raft
+  // launch takes (group, slot) from the slow list
+  uint4 slow_e = make_uint4(0, 0, 0, 0);
+  if (SLOW) {
+    const uint64_t slow_n = umin64(*v.slow_n, v.slow_cap);
+    if ((uint64_t)blockIdx.x * blockDim.x >= slow_n) return;  // uniform
+    const uint64_t si = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    slow_e = si < slow_n ? v.slow_list[si]
+                         : make_uint4(0xffffffffu, 0xffffffffu, 0, 0);
+  }
+  const uint32_t slot = SLOW ? slow_e.z : (p.slots >> (4 * bp.y)) & 0xfu;
   // Listed rounds step only the replicas k_active_scan found with work,
   // packed in group order into dense waves (drb_engine.hip); the blocks
   // past the list's end have nothing to do.
@@ -1719,7 +2007,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     nlisted = v.act_total[2 * lrow] + v.act_total[2 * lrow + 1];
     if ((uint64_t)bp.x * blockDim.x >= nlisted) return;  // uniform
   }
-  const uint64_t g = p.listed ? (li < nlisted ? v.act_list[lrow * v.G + li]
+  const uint64_t g = SLOW ? lo64(slow_e)
+                   : p.listed ? (li < nlisted ? v.act_list[lrow * v.G + li]
                                               : v.G)
                               : li;
   __shared__ RemLds<R> rl;
@@ -1741,31 +2030,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   L.round = p.round;
   L.rbuf = (uint32_t)((p.round - 1) & 1);
   L.wbuf = (uint32_t)(p.round & 1);
+  L.slow = SLOW;
   uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint64_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
-  uint32_t c_stepped = 0;
+  uint32_t c_stepped = 0, c_elect = 0, c_role = 0;
   uint32_t sent_c1 = 0;     // remote planes: destinations given a c1 chunk
   uint32_t qz_out = 0;      // destinations sent a Quiesce message
   uint64_t last_final = 0;  // leader: last index at the end of the round
   bool active = g < v.G;
   uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
   uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
-  if (!(flags & DRB_F_HOSTED) || ((role == DRB_LEADER) != LEAD))
+  if (SLOW) {
+    if (!(flags & DRB_F_HOSTED) || !(flags & F_SLOW)) active = false;
+  } else if (!(flags & DRB_F_HOSTED) || ((role == DRB_LEADER) != LEAD)) {
+    // an unhosted replica (stopped, or on another NodeHost) has no round
+    // output; the launch of its role clears what an earlier round left
+    if (active && !(flags & DRB_F_HOSTED) && (role == DRB_LEADER) == LEAD) {
+      v.rtr_count[ix(v, slot, g)] = 0;
+      if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
+    }
     active = false;
+  }
   if (active && (flags & (DRB_F_FALLBACK | DRB_F_ERROR))) {
     // left the fast path in an earlier round: no round output
     v.rtr_count[ix(v, slot, g)] = 0;
     if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
     active = false;
   }
-  if (active && !p.listed && idle_round<R>(v, p, slot, g, LEAD, flags))
+  if (!SLOW && active && !p.listed &&
+      idle_round<R>(v, p, slot, g, LEAD, flags))
     active = false;
   if (active) {
     c_stepped = 1;
     Rep<R> r;
     load_rep<R, LEAD>(L, r);
-    r.role = LEAD ? DRB_LEADER : DRB_FOLLOWER;
+    r.role = SLOW ? role : LEAD ? DRB_LEADER : DRB_FOLLOWER;
+    r.votes = SLOW ? v.u32[u32_ix(v, W_VOTES, slot, g)] : 0u;
+    if (SLOW) {  // off the slow list
+      r.flags &= ~F_SLOW;
+      v.u32[u32_ix(v, W_FLAGS, slot, g)] = r.flags;
+      c_elect = 1;
+    }
+    const uint64_t term0 = r.term;
+    const uint32_t role0 = r.role, votes0 = r.votes;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       oinfo[s * 256 + threadIdx.x] = 0;
@@ -1798,8 +2106,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 
     // ---------------------------------------------- pre-pass (read only)
     uint32_t fb = DRB_FB_NONE;
-    constexpr bool is_leader = LEAD;
-    if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) fb = DRB_FB_ROLE;
+    const bool is_leader = SLOW ? r.role == DRB_LEADER : LEAD;
+    if (SLOW) {
+      if (role != DRB_LEADER && role != DRB_FOLLOWER && role != DRB_CANDIDATE)
+        fb = DRB_FB_ROLE;
+    } else if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) {
+      fb = DRB_FB_ROLE;
+    }
+    bool higher_in = false;  // raft launch: a message may raise the term
     // the inbox, from the per-sender headers alone (drb_msg.hpp)
     uint64_t nin_packed = 0;  // 5-bit inbox record count per sender
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
@@ -1818,19 +2132,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       const uint32_t ns = mi_count(info);
       nin_packed |= (uint64_t)ns << (5 * s);
       if (cur && (meta.x & MQ_QUIESCE)) qz_from |= 1u << s;
-      if ((info & (LEAD ? MI_OFF_LEADER : MI_OFF_FOLLOWER)) &&
-          fb == DRB_FB_NONE)
-        fb = DRB_FB_MESSAGE_TYPE;
-      if (((info & MI_TERM_OTHER) ||
-           ((info & MI_TERM) && hi64(meta) != r.term)) &&
-          fb == DRB_FB_NONE)
-        fb = DRB_FB_TERM_MISMATCH;
+      if (SLOW) {
+        // the types the raft launch handles (el_dispatch); anything else
+        // (snapshots, leader transfer, ...) is the CPU path's
+        if (info & (MI_OFF_LEADER | MI_OFF_FOLLOWER)) {
+          const uint4 *mb = rm ? v.mbox_in : v.mbox;
+          const uint32_t nrp = mi_nrep(info);
+          for (uint32_t j = 0; j < ns; ++j) {
+            const uint32_t k = rec_pos(j < nrp, j < nrp ? j : j - nrp, v.MB);
+            const uint32_t t =
+                mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)].x & 0xffu;
+            const bool ok =
+                t == DRB_MSG_REPLICATE || t == DRB_MSG_REPLICATE_RESP ||
+                t == DRB_MSG_HEARTBEAT || t == DRB_MSG_HEARTBEAT_RESP ||
+                t == DRB_MSG_READ_INDEX || t == DRB_MSG_READ_INDEX_RESP ||
+                t == DRB_MSG_REQUEST_VOTE || t == DRB_MSG_REQUEST_VOTE_RESP ||
+                t == DRB_MSG_NOOP;
+            if (!ok && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
+          }
+        }
+        if ((info & MI_TERM) && hi64(meta) > r.term) higher_in = true;
+        if (info & MI_TERM_OTHER) {  // the records with a term of their own
+          const uint4 *mb = rm ? v.mbox_in : v.mbox;
+          const uint32_t nrp = mi_nrep(info);
+          for (uint32_t j = 0; j < ns; ++j) {
+            const uint32_t k = rec_pos(j < nrp, j < nrp ? j : j - nrp, v.MB);
+            if ((mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)].x & MF_TERM_OTHER) &&
+                v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)] > r.term)
+              higher_in = true;
+          }
+        }
+      } else {
+        if ((info & (LEAD ? MI_OFF_LEADER : MI_OFF_FOLLOWER)) &&
+            fb == DRB_FB_NONE)
+          fb = DRB_FB_MESSAGE_TYPE;
+        if (((info & MI_TERM_OTHER) ||
+             ((info & MI_TERM) && hi64(meta) != r.term)) &&
+            fb == DRB_FB_NONE)
+          fb = DRB_FB_TERM_MISMATCH;
+      }
       n_ri_msgs += (info >> MI_NRI) & 0x1fu;
       nri_packed |= (uint64_t)((info >> MI_NRI) & 0x1fu) << (5 * s);
       n_rr += (info >> MI_NRR) & 0x1fu;
       if (info & MI_RESP) resp_from |= 1u << s;
       if (info & MI_REJECT) rej_from |= 1u << s;
-      if (!LEAD && mi_nrep(info))
+      if (!is_leader && mi_nrep(info))
         max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
                                       v, L.rbuf, s, slot, g)]);
       total_in += ns;
@@ -1843,14 +2189,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         umin64(umin64(r.processed + 1, r.committed), r.sm_index);
     // staged inputs are per lane: with replicas spread over ranks a lane
     // holds R different groups, and they go to the stage slot's leader
-    if (ri_here(v, p, slot, LEAD)) {
+    if (ri_here(v, p, slot, is_leader)) {
       uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
       in_lo = lo64(c);
       in_hi = hi64(c);
     }
+    bool cq_fail = false;  // raft launch: CheckQuorum steps down at the tick
     if (is_leader) {
-      if (p.prop_slot != DRB_NONE && stage_here(v, slot, LEAD))
+      if (p.prop_slot != DRB_NONE && stage_here(v, slot, is_leader))
         nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
+      // with elections a group can hold two leaders (a stale one and the
+      // new one): its entry queue goes to the hosted leader in the highest
+      // slot (the NodeHost the client reaches; tests/gpu_harness.py)
+      if (v.elections && nprops) {
+#pragma unroll
+        for (int s = 0; s < R; ++s)
+          if ((uint32_t)s > slot &&
+              (v.u32[u32_ix(v, W_FLAGS, s, g)] & DRB_F_HOSTED) &&
+              v.u32[u32_ix(v, W_ROLE, s, g)] == DRB_LEADER)
+            nprops = 0;
+      }
       if (r.ri_count + (in_lo != 0) + n_ri_msgs > DRB_RI_DEPTH &&
           fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
@@ -1914,7 +2272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         uint64_t adv = r.last > r.committed ? r.last - r.committed : 0;
         uint32_t nb = (uint32_t)umin64((uint64_t)n_rr, adv);
         uint32_t base = (in_lo != 0) + (p.tick ? 1 : 0) + (nprops ? 1 : 0) +
-                        n_ri_msgs * 2 + r.ri_count + nb;
+                        n_ri_msgs * 2 + r.ri_count + nb + (SLOW ? 1 : 0);
 #pragma unroll
         for (int s = 0; s < R; ++s) {
           if ((uint32_t)s == slot) continue;
@@ -1936,8 +2294,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           if ((uint32_t)s != slot &&
               (rem_get<R>(L, s).a || ((resp_from >> s) & 1)))
             c++;
-        if (c < R / 2 + 1 && fb == DRB_FB_NONE) fb = DRB_FB_CHECK_QUORUM;
+        if (c < R / 2 + 1) {
+          if (SLOW)
+            cq_fail = true;
+          else if (fb == DRB_FB_NONE)
+            fb = DRB_FB_CHECK_QUORUM;
+        }
       }
+      // a leader that may step down before handleProposals would forward
+      // or drop its proposals (handleFollowerPropose, raft.go:2103-2116):
+      // the CPU path's
+      if (SLOW && nprops && (higher_in || cq_fail) && fb == DRB_FB_NONE)
+        fb = higher_in ? DRB_FB_TERM_MISMATCH : DRB_FB_CHECK_QUORUM;
     } else {
       if (max_app && max_app >= keep_common + v.W &&
           fb == DRB_FB_NONE)
@@ -1947,12 +2315,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 #pragma unroll
       for (int s = 0; s < R; ++s)
         if ((uint32_t)s != slot &&
-            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) > v.MB &&
+            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) + (SLOW ? 1 : 0) >
+                v.MB &&
             fb == DRB_FB_NONE)
           fb = DRB_FB_CAPACITY;
       const bool qtick =
           qon && p.tick && total_in == 0 && qs_quiet_tick(v, r, qz_from);
-      if (p.tick && !qtick) {
+      if (!SLOW && p.tick && !qtick) {
         uint64_t et = (total_in ? 0 : r.election_tick) + 1;
         if (et >= ld_f(L, r, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
           fb = DRB_FB_ELECTION;
@@ -1981,7 +2350,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           (uint64_t)v.save_cap16 * 16)
         fb = DRB_FB_CAPACITY;
     }
-    if (fb != DRB_FB_NONE) {
+    // elections: what the raft launch handles goes there, untouched
+    bool to_slow = false;
+    if (!SLOW && v.elections &&
+        (fb == DRB_FB_TERM_MISMATCH || fb == DRB_FB_MESSAGE_TYPE ||
+         fb == DRB_FB_ELECTION || fb == DRB_FB_CHECK_QUORUM ||
+         fb == DRB_FB_ROLE)) {
+      const unsigned long long i = atomicAdd(v.slow_n, 1ull);
+      if (i < v.slow_cap) {
+        v.slow_list[i] = make_uint4((uint32_t)g, (uint32_t)(g >> 32), slot, 0);
+        v.u32[u32_ix(v, W_FLAGS, slot, g)] = r.flags | F_SLOW;
+        to_slow = true;
+        c_stepped = 0;
+      }
+    }
+    if (to_slow) {
+      // the raft launch runs this replica's round after this launch
+    } else if (fb != DRB_FB_NONE) {
       r.flags |= DRB_F_FALLBACK;
       r.fb = fb;
       v.u32[u32_ix(v, W_FLAGS, slot, g)] = r.flags;
@@ -2037,14 +2422,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
             const uint4 c0 = mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
             uint4 c1 = make_uint4(0, 0, 0, 0);
             if (c0.x & MF_HAS_C1) c1 = mb[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
-            const Msg m = msg_decode(c0, c1, sterm, prev_lo, prev_hi);
+            // the raft launch: a record whose sender changed terms
+            // within its round carries its own term (rterm)
+            const uint64_t rt =
+                (SLOW && (c0.x & MF_TERM_OTHER))
+                    ? v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)]
+                    : sterm;
+            const Msg m = msg_decode(c0, c1, rt, prev_lo, prev_hi);
             if (qon)  // node.recordMessage (node.go:1339-1345)
               qs_record(v, r,
                         (m.type == DRB_MSG_HEARTBEAT ||
                          m.type == DRB_MSG_HEARTBEAT_RESP) && m.hint > 0
                             ? (uint32_t)DRB_MSG_READ_INDEX
                             : m.type);
-            dispatch(L, r, s, m, src);
+            if (SLOW)
+              el_dispatch(L, r, s, m, src);
+            else
+              dispatch(L, r, s, m, src);
           }
         }
       }
@@ -2056,6 +2450,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       }
       if (p.tick && quiet) {
         r.election_tick++;  // raft.quiescedTick (raft.go:650-656)
+      } else if (SLOW && p.tick) {
+        el_tick(L, r);  // any role; may campaign or step down
       } else if (p.tick) {
         over_st(L, F_TICK_COUNT, over_ld(L, F_TICK_COUNT) + 1);
         if (is_leader) {
@@ -2212,7 +2608,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
             break;
           }
           c_applied++;
-          if (rc == 1 && is_leader) c_commit++;
+          if (rc == 1 && (SLOW ? r.role == DRB_LEADER : is_leader))
+            c_commit++;
         }
       }
       // the entry rows of remote followers' planes: [lowest sent, last]
@@ -2261,6 +2658,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         over_st(L, F_QS_BASE, p.tick_no);
       }
       store_rep<R, LEAD>(L, r, flags0, fb0);
+      if (SLOW) {  // what only the raft launch changes
+        if (r.role != role0) {
+          v.u32[u32_ix(v, W_ROLE, slot, g)] = r.role;
+          c_role = 1;
+        }
+        if (r.votes != votes0) v.u32[u32_ix(v, W_VOTES, slot, g)] = r.votes;
+      }
       c_msgs = r.nmsgs;
       c_rtr = r.nrtr;
       c_drop = r.ndropped_ri;
@@ -2270,8 +2674,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     // that got records: a receiver reads a stale tag as an empty inbox
 #pragma unroll
     for (int s = 0; s < R; ++s) {
-      const uint32_t w = oinfo[s * 256 + threadIdx.x];
+      uint32_t w = oinfo[s * 256 + threadIdx.x];
       const bool qz = (qz_out >> s) & 1u;
+      if (SLOW && r.term != term0 && mi_count(w)) {
+        // the records sent before the term changed keep theirs (rterm)
+        const uint32_t nrp = mi_nrep(w), nt = mi_count(w);
+        for (uint32_t j = 0; j < nt; ++j) {
+          const uint32_t k = rec_pos(j < nrp, j < nrp ? j : j - nrp, v.MB);
+          const uint64_t ci = mbox_ix(v, L.wbuf, slot, (uint32_t)s, k, 0, g);
+          uint4 c0 = v.mbox[ci];
+          if (!(c0.x & MF_TERM_ZERO) &&
+              v.rterm[rterm_ix(v, L.wbuf, slot, (uint32_t)s, k, g)] !=
+                  r.term) {
+            c0.x |= MF_TERM_OTHER;
+            v.mbox[ci] = c0;
+            w |= MI_TERM_OTHER;
+          }
+        }
+      }
       if (mi_count(w) || qz) {
         uint4 meta = mk4(0, r.term);
         meta.x = ((uint32_t)p.round & MQ_TAG) | (qz ? MQ_QUIESCE : 0u);
@@ -2314,8 +2734,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       (uint32_t)c_commit, (uint32_t)c_applied, (uint32_t)c_msgs,
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
       (uint32_t)c_err,    c_served,            c_deferred,
-      c_saved,            c_saved_bytes,       c_stepped};
-  block_counters<LEAD, 0, NUM_COUNTERS>(v, slot, bp, cnt);
+      c_saved,            c_saved_bytes,       c_stepped,
+      c_elect,            c_role};
+  block_counters<LEAD, 0, NUM_COUNTERS>(v, SLOW ? 0u : slot, bp, cnt);
 }
 
 }  // namespace drb

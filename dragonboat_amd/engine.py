@@ -141,7 +141,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
-                save_batched=0, save_tan=0, tan_max_log=0)
+                save_batched=0, save_tan=0, tan_max_log=0, elections=0)
 
 
 class Engine:
@@ -161,7 +161,7 @@ class Engine:
                    cfg["entry_mbox"], cfg["kv_pool_blocks"],
                    cfg["flagged_cap"], cfg["quiesce"],
                    cfg["durable_log"], cfg["save_batched"],
-                   cfg["save_tan"], 0, cfg["tan_max_log"])
+                   cfg["save_tan"], cfg["elections"], cfg["tan_max_log"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")

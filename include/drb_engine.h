@@ -208,10 +208,17 @@ typedef struct drb_replica_state {
   uint64_t qs_idle_since;
   uint64_t qs_quiesced_since;          /* 0: not quiesced */
   uint64_t qs_exit_quiesce_tick;
+  /* the state of raft.rand, the randomized election timeout's source
+   * (raft.go:658-661): splitmix64, one draw per reset (elections) */
+  uint64_t rng;
   uint32_t role;                       /* drb_role */
   uint32_t flags;                      /* DRB_F_* */
   uint32_t fallback_reason;            /* drb_fallback_reason */
   uint32_t ri_count;                   /* valid entries in ri[] */
+  /* a candidate's votes (raft.votes, raft.go:1125-1147): bit s of the low
+   * byte = replica slot s answered, of the next byte = it granted */
+  uint32_t votes;
+  uint32_t pad0;
   drb_remote_state remotes[DRB_MAX_REPLICAS];
   drb_read_status ri[DRB_RI_DEPTH];
 } drb_replica_state;
@@ -323,7 +330,15 @@ typedef struct drb_config {
    * engine tracks per replica (drb_tan_get / drb_tan_set).  Needs
    * save_cap; excludes save_batched. */
   uint32_t save_tan;
-  uint32_t reserved0;
+  /* 1: elections on the GPU.  The replicas a step round
+   * would hand to the CPU for an election timeout, CheckQuorum, a term
+   * change, a vote message or the candidate role are stepped by a second
+   * launch with the whole raft state machine instead (campaign,
+   * RequestVote / RequestVoteResp, becomeFollower / Candidate / Leader,
+   * the term gate, raft.go:1052-1217, 1507-1590, 1670-1722, 2235-2253);
+   * only capacity and off-path entries still fall back.  Co-resident
+   * placement, Quiesce off. */
+  uint32_t elections;
   /* tan MaxLogFileSize (internal/tan/options.go:29); 0: 64 MiB */
   uint64_t tan_max_log;
 } drb_config;
@@ -374,6 +389,9 @@ typedef struct drb_round_out {
   uint64_t log_records;           /* save_tan: records appended to tan logs */
   uint64_t log_syncs;             /* ... of them with db.write's sync */
   uint64_t log_new;               /* ... of them that started a new log */
+  uint64_t elections_stepped;     /* elections: replicas the raft launch
+                                   * stepped (term gate, votes, campaign) */
+  uint64_t role_changes;          /* elections: replicas whose role changed */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;

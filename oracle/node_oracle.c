@@ -896,6 +896,9 @@ int orc_cluster_setup_steady(orc_cluster *c, uint32_t leader_slot) {
       uint64_t e = c->cfg.election_rtt;
       r->randomized_election_timeout =
           e + mix64(c->cfg.seed ^ (0xE1ull << 56) ^ (c->gids[g] * R + s)) % e;
+      /* raft.rand restarts from a per-replica seed the engine derives the
+       * same way (k_init_steady), so later resets draw the same timeouts */
+      r->rng = mix64(c->cfg.seed ^ (0xE2ull << 56) ^ (c->gids[g] * R + s));
     }
   return 0;
 }
@@ -1006,6 +1009,14 @@ int orc_cluster_export(orc_cluster *c, uint64_t g, uint32_t slot,
   st->qs_idle_since = n->qs.idle_since;
   st->qs_quiesced_since = n->qs.quiesced_since;
   st->qs_exit_quiesce_tick = n->qs.exit_quiesce_tick;
+  st->rng = n->r->rng;
+  st->votes = 0;
+  for (int i = 0; i < n->r->nvotes; i++) {
+    const uint64_t id = n->r->vote_id[i];
+    if (id < 1 || id > 8) continue;
+    st->votes |= 1u << (id - 1);
+    if (n->r->vote_ok[i]) st->votes |= 1u << (8 + id - 1);
+  }
   st->flags = n->hosted ? DRB_F_HOSTED : 0;
   return 0;
 }

@@ -20,7 +20,8 @@ STATE_FIELDS = [
     "applied_to_index", "applied_to_term", "applied_index",
     "confirmed_index", "pushed_index", "prev_term", "prev_vote",
     "prev_commit", "sm_index", "sm_term", "kv_count", "qs_current_tick",
-    "qs_idle_since", "qs_quiesced_since", "qs_exit_quiesce_tick", "role"]
+    "qs_idle_since", "qs_quiesced_since", "qs_exit_quiesce_tick", "rng",
+    "role"]
 
 
 def state_diff(a, b, R):
@@ -35,6 +36,8 @@ def state_diff(a, b, R):
                     (y.match, y.next, y.state, y.active):
                 d["remote%d" % s] = ((x.match, x.next, x.state, x.active),
                                      (y.match, y.next, y.state, y.active))
+    if a.votes != b.votes:
+        d["votes"] = (a.votes, b.votes)
     if a.ri_count != b.ri_count:
         d["ri_count"] = (a.ri_count, b.ri_count)
     else:

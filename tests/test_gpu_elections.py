@@ -1,0 +1,130 @@
+"""GPU: elections on the device (drb_config.elections).
+
+The replicas a step round would hand to the CPU path for an election
+timeout, a CheckQuorum loss, a term change, a vote message or the candidate
+role are stepped by the raft launch instead: campaign (raft.go:1176-1217),
+RequestVote / RequestVoteResp (raft.go:1697-1722, 2235-2253), becomeFollower
+/ Candidate / Leader (raft.go:961-1050), the term gate with
+dropRequestVoteFromHighTermNode and the NoOP answer to a stale leader
+(raft.go:1507-1590), CheckQuorum step-down (raft.go:1785-1792).  Every
+round is compared with the oracle cluster (the reference step loop) over
+every field -- term, vote, role, votes, the randomized timeout and its
+generator state included -- the log, the KV, the outboxes and the
+ReadyToReads; no replica leaves the GPU.
+"""
+import pytest
+
+from dragonboat_amd import abi
+from tests.gpu_harness import Pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _unhost(p, groups, slot):
+    for g in groups:
+        p.orc.set_hosted(g, slot, False)
+        sts = p.eng.export_replicas(g, 1)
+        sts[slot].flags &= ~abi.F_HOSTED
+        p.eng.import_replicas(g, sts)
+
+
+def _rehost(p, groups, slot):
+    for g in groups:
+        p.orc.set_hosted(g, slot, True)
+        sts = p.eng.export_replicas(g, 1)
+        sts[slot].flags |= abi.F_HOSTED
+        p.eng.import_replicas(g, sts)
+
+
+def _rounds(p, n, stats, k=1, tick=True, ri_every=3, groups=None):
+    for _ in range(n):
+        o, e = p.round(k=k, tick=tick, read_index=(p.rounds % ri_every == 0),
+                       groups=groups)
+        assert e.fallbacks == 0 and e.errors == 0, (p.rounds, e.to_dict(),
+                                                     p.why())
+        assert (e.committed_entries, e.messages) == (o.committed_entries,
+                                                     o.messages), \
+            (p.rounds, e.to_dict(), o.to_dict())
+        errs = p.check()
+        assert not errs, (p.rounds, errs[:2])
+        stats["slow"] += e.elections_stepped
+        stats["roles"] += e.role_changes
+
+
+def _roles(p, g):
+    return [(st.role, st.term) for st in p.eng.export_replicas(g, 1)]
+
+
+@pytest.mark.parametrize("R", [3, 5])
+def test_leader_loss_elects_on_gpu(R):
+    """The leader replica of some groups stops (unhosted): its followers
+    time out, campaign at term 3, vote, and a new leader takes over --
+    appending its term-start no-op and replicating -- all on the GPU,
+    bit-exact with the oracle every round.  The old leader then returns at
+    term 2: the new leader's heartbeats make it answer with NoOP or step
+    down to follower at term 3 (raft.go:1540-1590)."""
+    p = Pair(G=24, R=R, elections=1)
+    st = {"slow": 0, "roles": 0}
+    _rounds(p, 3, st)
+    E = [1, 6, 11, 20]
+    _unhost(p, E, 0)
+    for _ in range(60):
+        _rounds(p, 1, st)
+        if all(abi.LEADER in [r for r, _ in _roles(p, g)[1:]] for g in E):
+            break
+    for g in E:
+        roles = _roles(p, g)
+        assert roles[0] == (abi.LEADER, 2), roles  # the stopped one
+        lead = [s for s in range(1, R) if roles[s][0] == abi.LEADER]
+        assert len(lead) == 1 and roles[lead[0]][1] >= 3, roles
+    assert st["slow"] > 0 and st["roles"] >= len(E)
+    _rounds(p, 8, st)  # writes and reads under the new leaders
+    _rehost(p, E, 0)
+    _rounds(p, 12, st)
+    for g in E:
+        roles = _roles(p, g)
+        assert roles[0][0] == abi.FOLLOWER and roles[0][1] >= 3, roles
+        assert sum(r == abi.LEADER for r, _ in roles) == 1, roles
+    _rounds(p, 6, st)
+
+
+def test_check_quorum_step_down_and_reelection():
+    """A leader whose followers stopped answering loses quorum at the
+    CheckQuorum tick and steps down (becomeFollower at its term); when the
+    followers return the group elects again -- possibly several rounds of
+    split or rejected votes -- and settles with one leader."""
+    p = Pair(G=16, R=3, elections=1)
+    st = {"slow": 0, "roles": 0}
+    _rounds(p, 2, st)
+    E = [3, 9]
+    _unhost(p, E, 1)
+    _unhost(p, E, 2)
+    # no client writes to the cut-off leader: its window would fill with
+    # entries nobody acknowledges (the CPU path's, DRB_FB_CAPACITY)
+    rest = [g for g in range(p.G) if g not in E]
+    for _ in range(30):
+        _rounds(p, 1, st, groups=rest)
+        if all(_roles(p, g)[0][0] == abi.FOLLOWER for g in E):
+            break
+    for g in E:
+        assert _roles(p, g)[0] == (abi.FOLLOWER, 2), _roles(p, g)
+    _rehost(p, E, 1)
+    _rehost(p, E, 2)
+    for _ in range(80):
+        _rounds(p, 1, st, groups=rest)
+        if all(sum(r == abi.LEADER for r, _ in _roles(p, g)) == 1
+               for g in E):
+            break
+    for g in E:
+        assert sum(r == abi.LEADER for r, _ in _roles(p, g)) == 1
+    _rounds(p, 8, st)
+    assert st["roles"] > 0
+
+
+def test_elections_engine_steady_state_matches_plain_engine():
+    """With nothing to elect, an elections engine runs the same rounds as a
+    plain one: no replica goes to the raft launch."""
+    p = Pair(G=32, R=3, elections=1)
+    st = {"slow": 0, "roles": 0}
+    _rounds(p, 10, st)
+    assert st == {"slow": 0, "roles": 0}
