@@ -1010,13 +1010,6 @@ int orc_cluster_export(orc_cluster *c, uint64_t g, uint32_t slot,
   st->qs_quiesced_since = n->qs.quiesced_since;
   st->qs_exit_quiesce_tick = n->qs.exit_quiesce_tick;
   st->rng = n->r->rng;
-  st->votes = 0;
-  for (int i = 0; i < n->r->nvotes; i++) {
-    const uint64_t id = n->r->vote_id[i];
-    if (id < 1 || id > 8) continue;
-    st->votes |= 1u << (id - 1);
-    if (n->r->vote_ok[i]) st->votes |= 1u << (8 + id - 1);
-  }
   st->flags = n->hosted ? DRB_F_HOSTED : 0;
   return 0;
 }

@@ -215,6 +215,7 @@ int orc_raft_broadcast_heartbeat(orc_raft *r);
 int orc_raft_try_commit(orc_raft *r);
 int orc_raft_tick(orc_raft *r);
 int orc_raft_campaign(orc_raft *r);
+void orc_raft_set_check_quorum(orc_raft *r, int on);
 void orc_raft_set_randomized_election_timeout(orc_raft *r, uint64_t v);
 int orc_raft_network_reset(orc_raft *r, uint64_t id, const uint64_t *ids,
                            int n);

@@ -99,6 +99,7 @@ def _declare(L):
         "orc_raft_tick": (C.c_int, [P]),
         "orc_raft_campaign": (C.c_int, [P]),
         "orc_raft_set_randomized_election_timeout": (None, [P, U64]),
+        "orc_raft_set_check_quorum": (None, [P, C.c_int]),
         "orc_raft_network_reset": (C.c_int, [P, U64, PU64, C.c_int]),
         "orc_raft_read_messages": (C.c_long, [P, PM, C.c_size_t, PE,
                                               C.c_size_t, PU8, C.c_size_t]),
@@ -454,6 +455,9 @@ class TestRaft:
 
     def campaign(self):
         _check(lib().orc_raft_campaign(self.p))
+
+    def set_check_quorum(self, on):
+        lib().orc_raft_set_check_quorum(self.p, int(bool(on)))
 
     def set_randomized_election_timeout(self, v):
         lib().orc_raft_set_randomized_election_timeout(self.p, v)

@@ -1953,6 +1953,9 @@ int orc_raft_campaign(orc_raft *r) {
   return 0;
 }
 
+/* the test harness's r.checkQuorum = ... (raft_etcd_test.go) */
+void orc_raft_set_check_quorum(orc_raft *r, int on) { r->check_quorum = on; }
+
 void orc_raft_set_randomized_election_timeout(orc_raft *r, uint64_t v) {
   r->randomized_election_timeout = v;
 }
@@ -2034,6 +2037,14 @@ void orc_raft_info(orc_raft *r, drb_replica_state *st) {
   st->applied_to_index = r->log.im.applied_to_index;
   st->applied_to_term = r->log.im.applied_to_term;
   st->role = r->state;
+  st->rng = r->rng;
+  /* raft.votes as answered | granted << 8, bit (ID - 1) */
+  for (int i = 0; i < r->nvotes; i++) {
+    const uint64_t id = r->vote_id[i];
+    if (id < 1 || id > 8) continue;
+    st->votes |= 1u << (id - 1);
+    if (r->vote_ok[i]) st->votes |= 1u << (8 + id - 1);
+  }
   for (int i = 0; i < r->nrem && i < DRB_MAX_REPLICAS; i++) {
     uint64_t id = r->rem_id[i];
     if (id == 0 || id > DRB_MAX_REPLICAS) continue;

@@ -494,3 +494,94 @@ def test_handle_leader_read_index():
 # raft_test.go:3039-3063 (TestWitnessReadIndex) is not restated: witness
 # members are outside the GPU fast path, which only steps
 # voting members.
+
+
+# ---------------------------------------------------------------- elections
+# The election state machine the GPU's raft launch restates (el_*,
+# drb_step.hpp) is checked against the oracle; these pin the oracle.
+REQUEST_VOTE = MSG["RequestVote"]
+REQUEST_VOTE_RESP = MSG["RequestVoteResp"]
+
+
+def _granted(st, rid):
+    return bool((st.votes >> (8 + rid - 1)) & 1)
+
+
+@pytest.mark.parametrize("state", ["follower", "candidate"])
+def test_nonleader_start_election(state):
+    # raft_etcd_paper_test.go:141-193 (testNonleaderStartElection)
+    et = 10
+    r = po.TestRaft(1, [1, 2, 3], et, 1)
+    if state == "follower":
+        r.become_follower(1, 2)
+    else:
+        r.become_candidate()
+    for _ in range(1, 2 * et):
+        r.tick()
+    st = r.info()
+    assert st.term == 2 and st.role == CANDIDATE
+    assert _granted(st, 1)
+    msgs = sorted(r.read_messages(), key=lambda m: m["to"])
+    assert [(m["from_"], m["to"], m["term"], m["type"]) for m in msgs] == [
+        (1, 2, 2, REQUEST_VOTE), (1, 3, 2, REQUEST_VOTE)]
+
+
+@pytest.mark.parametrize("size,votes,state", [
+    # raft_etcd_paper_test.go:199-242 (TestLeaderElectionInOneRoundRPC)
+    (1, {}, LEADER), (3, {2: True, 3: True}, LEADER), (3, {2: True}, LEADER),
+    (5, {2: True, 3: True, 4: True, 5: True}, LEADER),
+    (5, {2: True, 3: True, 4: True}, LEADER), (5, {2: True, 3: True}, LEADER),
+    (3, {2: False, 3: False}, FOLLOWER),
+    (5, {2: False, 3: False, 4: False, 5: False}, FOLLOWER),
+    (5, {2: True, 3: False, 4: False, 5: False}, FOLLOWER),
+    (3, {}, CANDIDATE), (5, {2: True}, CANDIDATE),
+    (5, {2: False, 3: False}, CANDIDATE), (5, {}, CANDIDATE)])
+def test_leader_election_in_one_round_rpc(size, votes, state):
+    r = po.TestRaft(1, ids_by_size(size), 10, 1)
+    r.handle(msg(MSG["Election"], from_=1, to=1))
+    for rid, vote in votes.items():
+        r.handle(msg(REQUEST_VOTE_RESP, from_=rid, to=1, term=r.info().term,
+                     reject=not vote))
+    st = r.info()
+    assert st.role == state
+    assert st.term == 1
+
+
+@pytest.mark.parametrize("vote,nvote,wreject", [
+    # raft_etcd_paper_test.go:244-276 (TestFollowerVote)
+    (0, 1, False), (0, 2, False), (1, 1, False), (2, 2, False),
+    (1, 2, True), (2, 1, True)])
+def test_follower_vote(vote, nvote, wreject):
+    r = po.TestRaft(1, [1, 2, 3], 10, 1)
+    r.load_state(term=1, vote=vote)
+    r.handle(msg(REQUEST_VOTE, from_=nvote, to=1, term=1))
+    msgs = r.read_messages()
+    assert [(m["from_"], m["to"], m["term"], m["type"], bool(m["reject"]))
+            for m in msgs] == [(1, nvote, 1, REQUEST_VOTE_RESP, wreject)]
+
+
+@pytest.mark.parametrize("term", [1, 2])
+def test_candidate_fallback(term):
+    # raft_etcd_paper_test.go:278-303 (TestCandidateFallback)
+    r = po.TestRaft(1, [1, 2, 3], 10, 1)
+    r.handle(msg(MSG["Election"], from_=1, to=1))
+    assert r.info().role == CANDIDATE
+    r.handle(msg(REPLICATE, from_=2, to=1, term=term))
+    st = r.info()
+    assert st.role == FOLLOWER and st.term == term
+
+
+@pytest.mark.parametrize("active", [True, False])
+def test_leader_stepdown_check_quorum(active):
+    # raft_etcd_test.go:1656-1688 (TestLeaderStepdownWhenQuorumActive /
+    # ...QuorumLost)
+    r = po.TestRaft(1, [1, 2, 3], 5, 1)
+    r.set_check_quorum(True)
+    r.become_candidate()
+    r.become_leader()
+    for _ in range(5 + 1):
+        if active:
+            r.handle(msg(MSG["HeartbeatResp"], from_=2, to=1,
+                         term=r.info().term))
+        r.tick()
+    assert r.info().role == (LEADER if active else FOLLOWER)
