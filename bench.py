@@ -109,6 +109,14 @@ def parse():
                          "EntryBatch + CRC32 per replica, or the regular "
                          "tan LogDB's log record per replica (XXH64 "
                          "chunks); default: entrybatch for c5, else none")
+    ap.add_argument("--elections", type=int, default=0,
+                    help="1: the engine runs elections on the GPU "
+                         "(drb_config.elections); the timed rounds show its "
+                         "steady-state cost")
+    ap.add_argument("--failover", action="store_true",
+                    help="with --elections, after the timed region: stop "
+                         "every group's leader replica and time the rounds "
+                         "until every group elected a new one on the GPU")
     ap.add_argument("--no-wire", action="store_true",
                     help="skip the off-GPU wire encode measurement (C3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -284,6 +292,7 @@ def main():
                      save_cap=(((2 * k + 2) * bound + 15) // 16 * 16 + 128
                                if saves else 0),
                      save_tan=int(args.save == "tan"),
+                     elections=args.elections,
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     for b in range(NP):
@@ -424,10 +433,43 @@ def main():
                         "outside the timed region"}
             rx.close()
             del stream
+    failover = None
+    if args.failover and args.elections and not (c4 or c5):
+        # every group loses its leader replica (slot 0 stops); the
+        # followers time out, campaign, vote and elect on the GPU (the
+        # raft launch); ticks every round, no client traffic meanwhile
+        eng.read_counters(reset=True)
+        eng.host_slot(0, False)
+        eng.sync()
+        f0 = time.perf_counter()
+        nr, elected, stepped = 0, 0, 0
+        while nr < 12 * 10:
+            for _ in range(5):
+                eng.step_async(tick=True)
+            nr += 5
+            cen = eng.role_census()
+            elected = sum(cen[s][3] for s in range(1, R))
+            if elected >= G:
+                break
+        eng.sync()
+        fms = (time.perf_counter() - f0) * 1e3
+        fo = eng.read_counters(reset=True)
+        failover = {
+            "groups": G, "elected": elected, "rounds": nr, "ms": fms,
+            "ms_per_round": fms / nr,
+            "raft_launch_replicas": fo.elections_stepped,
+            "role_changes": fo.role_changes,
+            "fallbacks": fo.fallbacks, "errors": fo.errors,
+            "note": "drb_host_slot(0, off) then LocalTick rounds until every "
+                    "group has a leader among the other slots (census every "
+                    "5 rounds, included in the time); election timeouts "
+                    "are randomized in [10, 20) ticks (ElectionRTT 10)"}
+        eng.host_slot(0, True)
     from dragonboat_amd import abi as _abi
     host_staged = None
     if args.host_staged < 0:
-        args.host_staged = int(world == 1 and not (c4 or c5) and k == 1)
+        args.host_staged = int(world == 1 and not (c4 or c5) and k == 1 and
+                               not args.failover)
     if args.host_staged:
         # the same rounds with this round's proposals staged from host
         # memory (the entryQueue as the host holds it: drb_entry rows and a
@@ -582,6 +624,10 @@ def main():
             res["wire"] = wire
         if host_staged is not None:
             res["host_staged"] = host_staged
+        if failover is not None:
+            res["failover"] = failover
+        if args.elections:
+            res["config"]["elections"] = "on the GPU (drb_config.elections)"
         if xch is not None:
             res["exchange"] = {"mode": args.exchange,
                                "bytes_sent_per_round_rank0":

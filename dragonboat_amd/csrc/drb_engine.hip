@@ -1570,6 +1570,37 @@ static int refresh_roles(drb_engine *e) {
   return DRB_OK;
 }
 
+__global__ void k_role_census(View v, unsigned long long *out) {
+  __shared__ unsigned long long part[8];
+  if (threadIdx.x < 8) part[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t s = blockIdx.y;
+  if (g < v.G) {
+    const uint32_t fl = v.u32[u32_ix(v, W_FLAGS, s, g)];
+    if ((fl & DRB_F_HOSTED) && !(fl & (DRB_F_FALLBACK | DRB_F_ERROR)))
+      atomicAdd(&part[v.u32[u32_ix(v, W_ROLE, s, g)] & 7u], 1ull);
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && part[threadIdx.x])
+    atomicAdd(&out[s * 8 + threadIdx.x], part[threadIdx.x]);
+}
+
+extern "C" int drb_role_census(drb_engine *e, uint64_t *counts) {
+  if (!e || !counts) return DRB_EINVAL;
+  void *d;
+  const size_t bytes = (size_t)e->v.R * 8 * sizeof(uint64_t);
+  if (scratch(e, bytes, &d)) return DRB_EDEVICE;
+  HIPCHK(hipMemsetAsync(d, 0, bytes, e->stream));
+  dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
+  k_role_census<<<grid, 256, 0, e->stream>>>(e->v,
+                                             (unsigned long long *)d);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(counts, d, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
 extern "C" int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
                               uint32_t *follower_slots) {
   if (!e) return DRB_EINVAL;

@@ -43,6 +43,7 @@ SIGNATURES = {
                                  PU8, SZ]),
     "drb_init_steady": (C.c_int, [P, U64, U32, U64]),
     "drb_host_slot": (C.c_int, [P, U32, C.c_int]),
+    "drb_role_census": (C.c_int, [P, PU64]),
     "drb_export_save_records": (C.c_int, [P, U64, U32,
                                           C.POINTER(abi.SaveRecord), SZ,
                                           C.POINTER(SZ)]),
@@ -389,6 +390,12 @@ class Engine:
         _ck(lib().drb_export_saved(self.h, g, slot, buf, cap, C.byref(ln),
                                    C.byref(crc)), "drb_export_saved")
         return bytes(buf[:ln.value]), crc.value
+
+    def role_census(self):
+        """[slot][role] counts of the hosted fast-path replicas."""
+        c = (C.c_uint64 * (8 * self.R))()
+        _ck(lib().drb_role_census(self.h, c), "drb_role_census")
+        return [[c[s * 8 + k] for k in range(8)] for s in range(self.R)]
 
     def export_tan(self, g, slot):
         """save_tan: (drb_tan_record as a dict, the bytes appended) of one

@@ -432,6 +432,11 @@ int drb_export_log(drb_engine *e, uint64_t group, uint32_t slot, uint64_t lo,
  * through drb_ingest / drb_ingest_wire (NodeHost.StartReplica /
  * StopReplica for one replica of every shard, nodehost.go). */
 int drb_host_slot(drb_engine *e, uint32_t slot, int hosted);
+/* Role census of the hosted replicas that are on the fast path (not
+ * FALLBACK / ERROR): counts[slot * 8 + role] for slots 0..R-1, roles
+ * drb_role -- how many groups have a leader after a failover, without
+ * exporting every replica. */
+int drb_role_census(drb_engine *e, uint64_t *counts);
 
 /* Device-side initialisation of every group to the post-election steady
  * state: bootstrap (peer.go:404-428) with R config-change entries at term

@@ -128,3 +128,15 @@ def test_elections_engine_steady_state_matches_plain_engine():
     st = {"slow": 0, "roles": 0}
     _rounds(p, 10, st)
     assert st == {"slow": 0, "roles": 0}
+
+
+def test_role_census_counts_leaders():
+    """drb_role_census: per slot, the hosted fast-path replicas by role."""
+    p = Pair(G=40, R=3, elections=1)
+    st = {"slow": 0, "roles": 0}
+    _rounds(p, 2, st)
+    c = p.eng.role_census()
+    assert c[0][abi.LEADER] == 40 and c[1][abi.FOLLOWER] == 40
+    _unhost(p, [5, 7], 0)
+    c = p.eng.role_census()
+    assert c[0][abi.LEADER] == 38
