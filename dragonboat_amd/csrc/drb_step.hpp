@@ -2235,6 +2235,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         const RemoteV x = rem_get<R>(L, s);
         if (x.st == DRB_REMOTE_SNAPSHOT && fb == DRB_FB_NONE)
           fb = DRB_FB_SNAPSHOT;
+        // a paused remote (Wait) that sent nothing this round is sent no
+        // Replicate (isPaused, remote.go:200-213; only its own responses
+        // unpause it): it holds no rows of the window this round -- a
+        // stopped follower does not hold the leader back.  When it answers
+        // again below the window, that round falls back.
+        if (x.st == DRB_REMOTE_WAIT && !((nin_packed >> (5 * s)) & 31u))
+          continue;
         const uint64_t lowest = ((rej_from >> s) & 1) ? umin64(x.m, x.n) : x.n;
         const uint64_t need = lowest > 0 ? lowest - 1 : 0;  // LogTerm index
         keep = umin64(keep, need);
@@ -2254,6 +2261,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         for (int s = 0; s < R; ++s)
           if ((uint32_t)s != slot && pair_remote(v, slot, s)) {
             const RemoteV x = rem_get<R>(L, s);
+            if (x.st == DRB_REMOTE_WAIT && !((nin_packed >> (5 * s)) & 31u))
+              continue;  // paused and silent: nothing is sent to it
             const bool lowers = ((rej_from >> s) & 1) ||
                                 (((resp_from >> s) & 1) &&
                                  x.st != DRB_REMOTE_REPLICATE);

@@ -161,3 +161,112 @@ def test_fullsize_c5_sampled(payload, rounds):
              for i in range(n) for s in range(R))
     if rounds > 220:
         assert qs > 0  # some sampled groups went quiet past the threshold
+
+
+def test_fullsize_failover_sampled():
+    """Elections on the GPU at the C3 size: 1,048,576 groups x 3 with
+    writes and reads, then every group's leader replica (slot 0) stops; the
+    followers elect new leaders through the raft launch while the client
+    queue keeps proposing (dropped while a group has no leader), and the
+    sampled groups match the oracle bit-exactly throughout -- terms, votes,
+    roles, randomized timeouts and their generator state, logs, KV,
+    outboxes."""
+    G, R, NP = 1 << 20, 3, 8
+    eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                 max_props=1, prop_slots=NP, ri_slots=NP, mailbox=16,
+                 kv_slots=512, kv_val_cap=4, elections=1)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    for b in range(NP):
+        eng.gen_kv_proposals(b, 1, 256, 4, SEED, b)
+        eng.gen_read_index(b, SEED, b + 30)
+    gids = _sample(G, 800)
+    n = len(gids)
+    orc = po.Cluster(n, R, seed=SEED, gids=gids)
+    orc.setup_steady(0)
+    slow = 0
+    for r in range(200):
+        if r == 6:  # the leaders stop
+            eng.host_slot(0, False)
+            for i in range(n):
+                orc.set_hosted(i, 0, False)
+        b = r % NP
+        counts, ents, pool = workload.build_batch(n, 1, SEED, b, gids=gids)
+        orc.stage_proposals(counts, 1, ents, pool)
+        lo, hi = workload.build_read_index(n, SEED, 1, b + 30, gids=gids)
+        orc.stage_read_index(lo, hi)
+        o = orc.round(tick=True)
+        e = eng.step(tick=True, prop_slot=b, ri_slot=b)
+        if e.fallbacks or e.errors:
+            recs, _ = eng.take_flagged(cap=4096)
+            hist = {}
+            for (g, s, reason, flags, _r, _sh) in recs:
+                hist[(s, reason, flags)] = hist.get((s, reason, flags), 0) + 1
+            st = [eng.export_replicas(g, 1)[s].to_dict(R)
+                  for (g, s, *_x) in recs[:2]]
+            raise AssertionError((r, e.to_dict(), hist, st))
+        slow += e.elections_stepped
+        if r % 15 == 14:
+            errs = _compare(eng, orc, gids, R)
+            assert not errs, (r, errs[:3])
+        if r >= 40 and r % 10 == 9:
+            cen = eng.role_census()
+            if sum(cen[s][3] for s in (1, 2)) == G:  # every group re-elected
+                break
+    assert sum(cen[s][3] for s in (1, 2)) == G, cen
+    errs = _compare(eng, orc, gids, R)
+    assert not errs, errs[:3]
+    assert slow > 0
+
+
+def test_fullsize_c5_tan_sampled():
+    """C5 at 128 B with the tan LogDB records (save_tan): 4,194,304 groups,
+    1 % proposing per round, Quiesce, listed rounds.  The oracle's tan db of
+    every sampled replica takes that replica's Update every round; at the
+    check rounds the GPU's record of the round -- bytes, offset, sync, log
+    -- and its writer position equal the oracle's."""
+    G, R = 4 << 20, 3
+    vlen = 116
+    cmd_cap = ((12 + 1 + vlen) + 15) // 16 * 16
+    bound = 73 + cmd_cap
+    eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
+                 max_props=1, prop_slots=2, ri_slots=1, mailbox=8,
+                 kv_slots=16, kv_val_cap=vlen + 13 & ~15,
+                 kv_pool_blocks=16 * G * R,
+                 save_cap=(4 * bound + 15) // 16 * 16 + 128, save_tan=1,
+                 quiesce=1)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    gids = _sample(G, 500)
+    n = len(gids)
+    orc = po.Cluster(n, R, seed=SEED, gids=gids, quiesce=True)
+    orc.setup_steady(0)
+    dbs = [[po.TanDB() for _ in range(R)] for _ in range(n)]
+    checked = 0
+    for r in range(48):
+        act = workload.active_groups(n, SEED, r, 10000, gids=gids)
+        counts, ents, pool = workload.build_batch(n, 1, SEED, r, 256, vlen,
+                                                  groups=act, gids=gids)
+        orc.stage_proposals(counts, 1, ents, pool)
+        eng.gen_kv_proposals(r % 2, 1, 256, vlen, SEED, r, active_ppm=10000)
+        o = orc.round(tick=True)
+        e = eng.step(tick=True, prop_slot=r % 2, encode_saves=True,
+                     listed=True)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        check = r % 12 == 11
+        for i, g in enumerate(gids):
+            for s in range(R):
+                want = orc.tan_write(i, s, dbs[i][s])
+                if not check:
+                    continue
+                rec, data = eng.export_tan(g, s)
+                where = (r, g, s, rec, want)
+                if want is None:
+                    assert not rec["flags"] & 1, where
+                    continue
+                assert (rec["offset"], rec["len"], rec["log"],
+                        bool(rec["flags"] & 2)) == \
+                    (want["off"], want["len"], want["log"], want["sync"]), where
+                f = dbs[i][s].file(want["log"])
+                assert data == f[want["off"]:want["off"] + want["len"]], where
+                assert eng.tan_get(g, s)[0] == want["offset"], where
+                checked += 1
+    assert checked > 0
