@@ -562,9 +562,12 @@ static int ing_grow(IngestBuf &b, size_t need) {
 }
 struct IngestState {
   IngestBuf stream, msgs, ents, sort, misc;
+  uint8_t *pinned = nullptr;  // drb_ingest_buffer (hipHostMalloc)
+  size_t pinned_cap = 0;
 };
 static void ingest_free(IngestState *st) {
   if (!st) return;
+  if (st->pinned) (void)hipHostFree(st->pinned);
   for (IngestBuf *b : {&st->stream, &st->msgs, &st->ents, &st->sort,
                        &st->misc})
     if (b->p) (void)hipFree(b->p);
@@ -594,6 +597,22 @@ struct IngestTrace {
     t = n;
   }
 };
+
+extern "C" int drb_ingest_buffer(drb_engine *e, size_t cap, uint8_t **buf) {
+  if (!e || !buf) return DRB_EINVAL;
+  std::lock_guard<std::mutex> lock(e->ingest_mu);
+  if (!e->ingest) e->ingest = new IngestState();
+  IngestState &st = *e->ingest;
+  if (cap > st.pinned_cap) {
+    if (st.pinned) HIPCHK(hipHostFree(st.pinned));
+    st.pinned = nullptr;
+    st.pinned_cap = 0;
+    HIPCHK(hipHostMalloc((void **)&st.pinned, cap, hipHostMallocDefault));
+    st.pinned_cap = cap;
+  }
+  *buf = st.pinned;
+  return DRB_OK;
+}
 
 extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                size_t len, uint64_t deployment_id,

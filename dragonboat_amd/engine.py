@@ -99,6 +99,7 @@ SIGNATURES = {
     "drb_wire_buffer": (C.c_int, [P, C.POINTER(P), PU64]),
     "drb_export_wire": (C.c_int, [P, PU8, SZ, C.POINTER(SZ)]),
     "drb_ingest_wire": (C.c_int, [P, PU8, SZ, U64, C.POINTER(WireIn)]),
+    "drb_ingest_buffer": (C.c_int, [P, SZ, C.POINTER(PU8)]),
 }
 
 
@@ -497,6 +498,23 @@ class Engine:
         # the bytes object's own buffer (no copy: a C3 plane is ~400 MB)
         buf = C.cast(C.c_char_p(bytes(data)), PU8) if data else _u8(b"")
         _ck(lib().drb_ingest_wire(self.h, buf, len(data), deployment_id,
+                                  C.byref(res)), "drb_ingest_wire")
+        return {f: getattr(res, f) for f, _ in WireIn._fields_}
+
+    def ingest_buffer(self, data):
+        """Copies data into the engine's pinned receive buffer
+        (drb_ingest_buffer), as a transport reading its connection into it
+        would; returns the buffer pointer for ingest_wire_pinned."""
+        ptr = PU8()
+        _ck(lib().drb_ingest_buffer(self.h, max(1, len(data)), C.byref(ptr)),
+            "drb_ingest_buffer")
+        C.memmove(ptr, bytes(data), len(data))
+        return ptr
+
+    def ingest_wire_pinned(self, ptr, n, deployment_id=0):
+        """drb_ingest_wire of n bytes already in the pinned buffer."""
+        res = WireIn()
+        _ck(lib().drb_ingest_wire(self.h, ptr, n, deployment_id,
                                   C.byref(res)), "drb_ingest_wire")
         return {f: getattr(res, f) for f, _ in WireIn._fields_}
 

@@ -814,6 +814,13 @@ typedef struct drb_wire_in {
  * delivered entry's Cmd exceeds cmd_cap. */
 int drb_ingest_wire(drb_engine *e, const uint8_t *stream, size_t len,
                     uint64_t deployment_id, drb_wire_in *out);
+/* A receive buffer of at least `cap` bytes in pinned (page-locked) host
+ * memory, owned by the engine (grow-only; valid until the next call or
+ * drb_engine_destroy).  A transport that reads its connection into it
+ * (conn.Read in tcp.go:180-237's readMessage) and passes it to
+ * drb_ingest_wire has the stream uploaded by DMA at the link's rate
+ * instead of through the driver's pageable staging. */
+int drb_ingest_buffer(drb_engine *e, size_t cap, uint8_t **buf);
 
 #ifdef __cplusplus
 }

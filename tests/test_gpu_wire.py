@@ -180,7 +180,12 @@ class TwoNodes:
     def _cross(self, src, dst, frm, to):
         res, data = src.encode_wire(frm, to, self.did, SRC)
         self.wire_bytes += len(data)
-        got = dst.ingest_wire(data, self.did)
+        if self.rounds % 2:  # every other round through the pinned
+            # receive buffer a transport reads its connection into
+            ptr = dst.ingest_buffer(data)
+            got = dst.ingest_wire_pinned(ptr, len(data), self.did)
+        else:
+            got = dst.ingest_wire(data, self.did)
         assert got["bad"] == 0 and got["consumed"] == len(data), got
         assert got["messages"] == res["n_msgs"] == got["accepted"], got
 
