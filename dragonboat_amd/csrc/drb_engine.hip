@@ -58,7 +58,11 @@ struct drb_engine {
   struct IngestState *ingest = nullptr;      // drb_ingest_wire (drb_ingest.hpp)
   std::mutex ingest_mu;  // drb_ingest: concurrent transport threads
   bool crc_tab_ready = false;  // c_crc_tab uploaded on this engine's device
-  uint64_t tan_blocks = 0;                   // k_tan_encode grid (save_tan)
+  uint64_t tan_blocks = 0;                   // k_tan_select grid (save_tan)
+  uint64_t tan_wblocks = 0;                  // k_tan_write grid
+  uint32_t *tan_list = nullptr;              // replicas with a record
+  uint32_t *tan_n = nullptr;                 // their counts, 256 B apart
+  uint32_t tan_per_list = 0;
   unsigned long long *tan_total = nullptr;   // its counter rows summed
 };
 
@@ -196,6 +200,9 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (cfg->save_tan && (cfg->save_cap == 0 || cfg->save_batched))
     return DRB_EINVAL;
+  // (the tan write pass lists replicas by 32-bit lane number)
+  if (cfg->save_tan && (uint64_t)cfg->num_replicas * cfg->num_groups > 0xffffffffull)
+    return DRB_ERANGE;
   // elections: the raft launch steps co-resident replicas, Quiesce off
   if (cfg->elections && (cfg->place_world > 1 || cfg->quiesce))
     return DRB_EINVAL;
@@ -340,7 +347,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.tan_sum, 3 * R * G);
     rc |= dalloc(e, &v.tan_st, R * G);
     rc |= dalloc(e, &v.tan_rec, R * G);
+    e->tan_wblocks = std::min<uint64_t>(e->tan_blocks, 4096);
+    e->tan_per_list =
+        (uint32_t)(((e->tan_blocks + drb::TAN_LISTS - 1) / drb::TAN_LISTS) * 256);
     rc |= dalloc(e, &v.tan_ctr, e->tan_blocks * 4);
+    rc |= dalloc(e, &e->tan_list, (uint64_t)e->tan_per_list * drb::TAN_LISTS);
+    rc |= dalloc(e, &e->tan_n, 64 * drb::TAN_LISTS);
     rc |= dalloc(e, &e->tan_total, 4);
   }
   v.elections = cfg->elections ? 1u : 0u;
@@ -2509,8 +2521,13 @@ extern "C" int drb_crc32_ieee_batch(drb_engine *e, const uint8_t *data,
 static int launch_tan(drb_engine *e, uint32_t round) {
   const uint64_t max_log = e->cfg.tan_max_log ? e->cfg.tan_max_log
                                               : drb::TAN_MAX_LOG;
-  k_tan_encode<<<(unsigned)e->tan_blocks, 256, 0, e->stream>>>(e->v, round,
-                                                               max_log);
+  HIPCHK(hipMemsetAsync(e->tan_n, 0, 64 * drb::TAN_LISTS * sizeof(uint32_t),
+                        e->stream));
+  k_tan_select<<<(unsigned)e->tan_blocks, 256, 0, e->stream>>>(
+      e->v, round, max_log, e->tan_list, e->tan_per_list, e->tan_n);
+  HIPCHK(hipGetLastError());
+  k_tan_write<<<(unsigned)e->tan_wblocks, 256, 0, e->stream>>>(
+      e->v, round, max_log, e->tan_list, e->tan_per_list, e->tan_n);
   HIPCHK(hipGetLastError());
   return DRB_OK;
 }

@@ -12,6 +12,9 @@
 
 namespace drb {
 
+// the tan select pass's replica lists (drb_tan.hpp)
+constexpr uint32_t TAN_LISTS = 64;
+
 // splitmix64 finaliser: seeded synthetic inputs and the served-read keys
 __host__ __device__ inline uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;

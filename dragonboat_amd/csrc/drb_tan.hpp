@@ -255,116 +255,211 @@ __device__ __forceinline__ uint32_t state_size(uint64_t t, uint64_t vo,
   return 3 + varint_size(t) + varint_size(vo) + varint_size(c);
 }
 
-// per block: {bytes, records, syncs, new logs} added to tan_ctr rows
-__global__ __launch_bounds__(256) void k_tan_encode(View v, uint32_t round,
-                                                    uint64_t max_log) {
-  __shared__ unsigned long long part[4];
-  if (threadIdx.x < 4) part[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t slot = (uint32_t)(t / v.G);
-  const uint64_t g = t - (uint64_t)slot * v.G;
-  uint32_t c_bytes = 0, c_rec = 0, c_sync = 0, c_new = 0;
-  if (slot < v.R) {
-    const uint64_t i = ix(v, slot, g);
-    const uint4 s2 = v.tan_sum[tan_sum_ix(v, 2, slot, g)];
-    const uint32_t fl = v.u32[u32_ix(v, W_FLAGS, slot, g)];
-    uint4 rec = make_uint4(0, 0, 0, 0);
-    // an Update of this round from a replica that stayed on the fast path
-    if (s2.z == round && (s2.y & TS_HAVE) && (fl & DRB_F_HOSTED) &&
-        !(fl & (DRB_F_FALLBACK | DRB_F_ERROR))) {
-      const uint4 s0 = v.tan_sum[tan_sum_ix(v, 0, slot, g)];
-      const uint4 s1 = v.tan_sum[tan_sum_ix(v, 1, slot, g)];
-      uint4 st = v.tan_st[i];
-      uint64_t off = (uint64_t)st.x | ((uint64_t)st.y << 32);
-      const uint32_t n_save = s2.x;
-      const bool u_state = (s2.y & TS_STATE) != 0;
-      const bool st_state = (st.w & TST_STATE) != 0;
-      rec.x = st.x;
-      rec.y = st.y;
-      rec.w = st.z << 8;
-      // db.write (db.go:97-116): IsStateEqual(u.State, st) with no entries
-      // (the stored state is the empty one or Peer.prevState, see DESIGN)
-      if (u_state || st_state || n_save > 0) {
-        const uint64_t term = lo64(s0), vote = hi64(s0), commit = lo64(s1);
-        const uint64_t save_lo = hi64(s1);
-        // stateSyncChange (db.go:88-90)
-        const bool sync =
-            n_save > 0 ||
-            (u_state ? (!st_state || (s2.y & TS_TV)) : st_state);
-        // makeRoomForWrite (db.go:175-180) -> createNewLog (open.go:171)
-        const bool new_log = off >= max_log;
-        if (new_log) {
-          off = 0;
-          st.z++;
-        }
-        // the marshalled Update's size (update.go:128-169)
-        const uint64_t shard = v.first_shard_id + gid(v, slot, g);
-        uint32_t len = varint_size(shard) + varint_size(slot + 1) + 1 + 4 + 1;
-        if (u_state) len += 4 + state_size(term, vote, commit);
-        for (uint32_t k = 0; k < n_save; ++k)
-          len += 4 + entry_size(ring_entry_hdr(v, slot, g, save_lo + k, false));
-        const uint32_t bpos = (uint32_t)(off % TAN_BLOCK);
-        const uint32_t add = tan_appended(bpos, len);
-        if (add > v.save_cap16 * 16) {  // bounded by the pre-pass
-          rec.w = (st.z << 8) | DRB_TAN_OVERFLOW;
-        } else {
-          TanOut o;
-          uint4 *dst = v.save_buf + i * v.save_cap16;
-          to_begin(o, dst, v.save_cap16, bpos);
-          bo_varint(o, shard);
-          bo_varint(o, slot + 1);
-          if (u_state) {
-            bo_byte(o, 1);
-            to_le32(o, state_size(term, vote, commit));
-            bo_byte(o, 0x08);
-            bo_varint(o, term);
-            bo_byte(o, 0x10);
-            bo_varint(o, vote);
-            bo_byte(o, 0x18);
-            bo_varint(o, commit);
-          } else {
-            bo_byte(o, 0);
-          }
-          to_le32(o, n_save);
-          for (uint32_t k = 0; k < n_save; ++k) {
-            const EntryHdr e = ring_entry_hdr(v, slot, g, save_lo + k, false);
-            to_le32(o, entry_size(e));
-            emit_entry(o, v, slot, g, save_lo + k, e);
-          }
-          bo_byte(o, 0);  // IsEmptySnapshot
-          to_finish(o);
-          tan_headers(dst, v.save_cap16, bpos, len);
-          // writeRecord's offset (record.go:589) = the file's new size
-          rec.x = (uint32_t)off;
-          rec.y = (uint32_t)(off >> 32);
-          rec.z = o.total;
-          rec.w = (st.z << 8) | DRB_TAN_WRITTEN | (sync ? DRB_TAN_SYNC : 0) |
-                  (new_log ? DRB_TAN_NEW_LOG : 0);
-          off += o.total;
-          st.x = (uint32_t)off;
-          st.y = (uint32_t)(off >> 32);
-          st.w = u_state ? TST_STATE : 0;  // nodeStates.setState(u.State)
-          v.tan_st[i] = st;
-          c_bytes = o.total;
-          c_rec = 1;
-          c_sync = sync;
-          c_new = new_log;
-        }
-      }
-    }
-    v.tan_rec[i] = rec;
-    v.save_len[i] = rec.z;
+// The records of a round can be sparse (C5: 3 % of the replicas) and long
+// (a 1 KB entry is 64 window chunks): a lane-per-replica pass would run
+// waves with one or two busy lanes.  So the select pass writes the records
+// of dense workgroups in place (C3: every replica has one) and lists the
+// replicas of sparse ones -- wave-aggregated appends spread over TAN_LISTS
+// counters (TAN_LISTS, drb_layout.hpp) -- for the write pass: one listed record per lane, full waves.
+constexpr uint32_t TAN_DENSE = 64;  // of a 256-lane workgroup
+
+// the Update of this round that db.write does not skip (db.go:97-116)
+__device__ __forceinline__ bool tan_pending(const View &v, uint32_t round,
+                                            uint32_t slot, uint64_t g,
+                                            uint4 &s2, uint4 &st, bool &have) {
+  const uint64_t i = ix(v, slot, g);
+  s2 = v.tan_sum[tan_sum_ix(v, 2, slot, g)];
+  const uint32_t fl = v.u32[u32_ix(v, W_FLAGS, slot, g)];
+  // an Update of this round from a replica that stayed on the fast path
+  have = s2.z == round && (s2.y & TS_HAVE) && (fl & DRB_F_HOSTED) &&
+         !(fl & (DRB_F_FALLBACK | DRB_F_ERROR));
+  st = have ? v.tan_st[i] : make_uint4(0, 0, 0, 0);
+  if (!have) return false;
+  // IsStateEqual(u.State, st) with no entries (the stored state is the
+  // empty one or Peer.prevState, see DESIGN)
+  return (s2.y & TS_STATE) || (st.w & TST_STATE) || s2.x > 0;
+}
+
+struct TanCount {
+  uint32_t bytes = 0, rec = 0, sync = 0, fresh = 0;
+};
+
+// db.write of replica (slot, g)'s pending Update: its record into the
+// replica's save buffer, {offset, length, flags} into tan_rec
+__device__ __forceinline__ void tan_write_one(const View &v, uint32_t slot, uint64_t g,
+                              uint4 s2, uint4 st, uint64_t max_log,
+                              TanCount &c) {
+  const uint64_t i = ix(v, slot, g);
+  const uint4 s0 = v.tan_sum[tan_sum_ix(v, 0, slot, g)];
+  const uint4 s1 = v.tan_sum[tan_sum_ix(v, 1, slot, g)];
+  uint64_t off = (uint64_t)st.x | ((uint64_t)st.y << 32);
+  const uint32_t n_save = s2.x;
+  const bool u_state = (s2.y & TS_STATE) != 0;
+  const bool st_state = (st.w & TST_STATE) != 0;
+  uint4 rec = make_uint4(st.x, st.y, 0, st.z << 8);
+  const uint64_t term = lo64(s0), vote = hi64(s0), commit = lo64(s1);
+  const uint64_t save_lo = hi64(s1);
+  // stateSyncChange (db.go:88-90)
+  const bool sync =
+      n_save > 0 || (u_state ? (!st_state || (s2.y & TS_TV)) : st_state);
+  // makeRoomForWrite (db.go:175-180) -> createNewLog (open.go:171)
+  const bool new_log = off >= max_log;
+  if (new_log) {
+    off = 0;
+    st.z++;
   }
-  if (c_rec) {
-    atomicAdd(&part[0], (unsigned long long)c_bytes);
-    atomicAdd(&part[1], 1ull);
-    if (c_sync) atomicAdd(&part[2], 1ull);
-    if (c_new) atomicAdd(&part[3], 1ull);
+  // the marshalled Update's size (update.go:128-169)
+  const uint64_t shard = v.first_shard_id + gid(v, slot, g);
+  uint32_t len = varint_size(shard) + varint_size(slot + 1) + 1 + 4 + 1;
+  if (u_state) len += 4 + state_size(term, vote, commit);
+  for (uint32_t k = 0; k < n_save; ++k)
+    len += 4 + entry_size(ring_entry_hdr(v, slot, g, save_lo + k, false));
+  const uint32_t bpos = (uint32_t)(off % TAN_BLOCK);
+  const uint32_t add = tan_appended(bpos, len);
+  if (add > v.save_cap16 * 16) {  // bounded by the pre-pass
+    rec.w = (st.z << 8) | DRB_TAN_OVERFLOW;
+  } else {
+    TanOut o;
+    uint4 *dst = v.save_buf + i * v.save_cap16;
+    to_begin(o, dst, v.save_cap16, bpos);
+    bo_varint(o, shard);
+    bo_varint(o, slot + 1);
+    if (u_state) {
+      bo_byte(o, 1);
+      to_le32(o, state_size(term, vote, commit));
+      bo_byte(o, 0x08);
+      bo_varint(o, term);
+      bo_byte(o, 0x10);
+      bo_varint(o, vote);
+      bo_byte(o, 0x18);
+      bo_varint(o, commit);
+    } else {
+      bo_byte(o, 0);
+    }
+    to_le32(o, n_save);
+    for (uint32_t k = 0; k < n_save; ++k) {
+      const EntryHdr e = ring_entry_hdr(v, slot, g, save_lo + k, false);
+      to_le32(o, entry_size(e));
+      emit_entry(o, v, slot, g, save_lo + k, e);
+    }
+    bo_byte(o, 0);  // IsEmptySnapshot
+    to_finish(o);
+    tan_headers(dst, v.save_cap16, bpos, len);
+    // writeRecord's offset (record.go:589) = the file's new size
+    rec.x = (uint32_t)off;
+    rec.y = (uint32_t)(off >> 32);
+    rec.z = o.total;
+    rec.w = (st.z << 8) | DRB_TAN_WRITTEN | (sync ? DRB_TAN_SYNC : 0) |
+            (new_log ? DRB_TAN_NEW_LOG : 0);
+    off += o.total;
+    st.x = (uint32_t)off;
+    st.y = (uint32_t)(off >> 32);
+    st.w = u_state ? TST_STATE : 0;  // nodeStates.setState(u.State)
+    v.tan_st[i] = st;
+    c.bytes += o.total;
+    c.rec++;
+    c.sync += sync;
+    c.fresh += new_log;
+  }
+  v.tan_rec[i] = rec;
+  v.save_len[i] = rec.z;
+}
+
+// a workgroup's {bytes, records, syncs, new logs} added to its tan_ctr row
+__device__ __forceinline__ void tan_count_row(const View &v, const TanCount &c,
+                                              unsigned long long *part) {
+  if (c.rec) {
+    atomicAdd(&part[0], (unsigned long long)c.bytes);
+    atomicAdd(&part[1], (unsigned long long)c.rec);
+    if (c.sync) atomicAdd(&part[2], (unsigned long long)c.sync);
+    if (c.fresh) atomicAdd(&part[3], (unsigned long long)c.fresh);
   }
   __syncthreads();
   if (threadIdx.x < 4)
     v.tan_ctr[(uint64_t)blockIdx.x * 4 + threadIdx.x] += part[threadIdx.x];
+}
+
+// list r of the select pass holds the replicas of workgroups b = r mod
+// TAN_LISTS, at most per_list of them; its count is n[r * 64]
+__global__ __launch_bounds__(256) void k_tan_select(View v, uint32_t round,
+                                                    uint64_t max_log,
+                                                    uint32_t *list,
+                                                    uint32_t per_list,
+                                                    uint32_t *n) {
+  __shared__ unsigned long long part[4];
+  if (threadIdx.x < 4) part[threadIdx.x] = 0;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t slot = (uint32_t)(t / v.G);
+  const uint64_t g = t - (uint64_t)slot * v.G;
+  bool pend = false;
+  uint4 s2 = make_uint4(0, 0, 0, 0), st = s2;
+  if (slot < v.R) {
+    bool have = false;
+    pend = tan_pending(v, round, slot, g, s2, st, have);
+    if (!pend) {
+      const uint64_t i = ix(v, slot, g);
+      v.tan_rec[i] = make_uint4(st.x, st.y, 0, have ? st.z << 8 : 0);
+      v.save_len[i] = 0;
+    }
+  }
+  TanCount c;
+  if (__syncthreads_count(pend) >= (int)TAN_DENSE) {
+    if (pend) tan_write_one(v, slot, g, s2, st, max_log, c);
+  } else {
+    const uint64_t m = __ballot(pend);
+    if (m) {
+      const uint32_t r = blockIdx.x % TAN_LISTS;
+      const uint32_t lane = __lane_id();
+      const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == first) base = atomicAdd(&n[r * 64], (uint32_t)__popcll(m));
+      base = __shfl(base, first);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pend) list[(uint64_t)r * per_list + base + below] = (uint32_t)t;
+    }
+  }
+  tan_count_row(v, c, part);
+}
+
+// the listed records, one per lane (grid-stride over the lists' total);
+// its workgroups add into tan_ctr rows 0.. as well (the launches run in
+// stream order)
+__global__ __launch_bounds__(256) void k_tan_write(View v, uint32_t round,
+                                                   uint64_t max_log,
+                                                   const uint32_t *list,
+                                                   uint32_t per_list,
+                                                   const uint32_t *n) {
+  __shared__ unsigned long long part[4];
+  __shared__ uint32_t pre[TAN_LISTS + 1];
+  if (threadIdx.x < 4) part[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (uint32_t r = 0; r < TAN_LISTS; ++r) {
+      pre[r] = a;
+      a += n[r * 64];
+    }
+    pre[TAN_LISTS] = a;
+  }
+  __syncthreads();
+  const uint32_t cnt = pre[TAN_LISTS];
+  TanCount c;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt;
+       j += gridDim.x * blockDim.x) {
+    uint32_t lo = 0, hi = TAN_LISTS;  // the list r with pre[r] <= j < pre[r+1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (pre[mid] <= j) lo = mid; else hi = mid;
+    }
+    const uint64_t t = list[(uint64_t)lo * per_list + (j - pre[lo])];
+    const uint32_t slot = (uint32_t)(t / v.G);
+    const uint64_t g = t - (uint64_t)slot * v.G;
+    uint4 s2, st;
+    bool have;
+    if (slot < v.R && tan_pending(v, round, slot, g, s2, st, have))
+      tan_write_one(v, slot, g, s2, st, max_log, c);
+  }
+  tan_count_row(v, c, part);
 }
 
 }  // namespace drb
