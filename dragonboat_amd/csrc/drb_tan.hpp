@@ -10,14 +10,13 @@
 // github.com/cespare/xxhash/v2) -- and the node's state is remembered for
 // the next Update's skip / sync decision.
 //
-// Here one lane is one replica: every replica's log is independent, so the
+// Here one lane is one record: every replica's log is independent, so the
 // round's records are built in parallel straight from the step round's
 // Update summary (tan_sum, written by step_kernel) and the resident
 // window.  Each lane writes the bytes its log file grows by -- zero padding
 // included -- into its save buffer, with {file offset, length, sync,
-// new-log} for the host's pwrite / fsync.  The payload goes out first
-// (16-byte stores), then each chunk's checksum is computed over the bytes
-// read back from L2 and written into its header.
+// new-log} for the host's pwrite / fsync, in one pass: 16-byte stores, the
+// chunk checksums hashed on the way out.
 #pragma once
 #include "drb_codec.hpp"
 #include "drb_layout.hpp"
@@ -53,74 +52,16 @@ __device__ __forceinline__ uint64_t xx_merge(uint64_t acc, uint64_t v) {
   return (acc ^ xx_round(0, v)) * XP1 + XP4;
 }
 
-// XXH64 (seed 0) of n bytes at byte position p of a lane's 8-byte aligned
-// output: 8-byte words read back with a funnel shift (the lane wrote them
-// just before; they are in L2)
-__device__ __forceinline__ uint64_t ld8(const uint64_t *w, uint32_t p,
-                                        uint32_t cap8) {
-  const uint32_t a = p >> 3, s = (p & 7) * 8;
-  const uint64_t w0 = w[a];
-  if (s == 0) return w0;
-  const uint64_t w1 = a + 1 < cap8 ? w[a + 1] : 0;
-  return (w0 >> s) | (w1 << (64 - s));
-}
-
-__device__ uint64_t xxh64_at(const uint64_t *w, uint32_t p, uint32_t n,
-                             uint32_t cap8) {
-  uint64_t acc;
-  uint32_t left = n;
-  if (n >= 32) {
-    uint64_t v0 = XP1 + XP2, v1 = XP2, v2 = 0, v3 = 0 - XP1;
-    while (left >= 32) {
-      v0 = xx_round(v0, ld8(w, p, cap8));
-      v1 = xx_round(v1, ld8(w, p + 8, cap8));
-      v2 = xx_round(v2, ld8(w, p + 16, cap8));
-      v3 = xx_round(v3, ld8(w, p + 24, cap8));
-      p += 32;
-      left -= 32;
-    }
-    acc = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
-    acc = xx_merge(acc, v0);
-    acc = xx_merge(acc, v1);
-    acc = xx_merge(acc, v2);
-    acc = xx_merge(acc, v3);
-  } else {
-    acc = XP5;
-  }
-  acc += n;
-  while (left >= 8) {
-    acc = rotl64(acc ^ xx_round(0, ld8(w, p, cap8)), 27) * XP1 + XP4;
-    p += 8;
-    left -= 8;
-  }
-  if (left) {
-    uint64_t t = ld8(w, p, cap8);
-    if (left >= 4) {
-      acc = rotl64(acc ^ (t & 0xffffffffull) * XP1, 23) * XP2 + XP3;
-      t >>= 32;
-      left -= 4;
-    }
-    for (; left; --left) {
-      acc = rotl64(acc ^ (t & 0xffull) * XP5, 11) * XP1;
-      t >>= 8;
-    }
-  }
-  acc ^= acc >> 33;
-  acc *= XP2;
-  acc ^= acc >> 29;
-  acc *= XP3;
-  acc ^= acc >> 32;
-  return acc;
-}
-
 // ------------------------------------------------------------ record out
-// Pass 1 writes the bytes one record adds to its log file, chunk headers
-// left zero: zero padding when the header does not fit in the block
-// (getNext, record.go:548-573), a 7-byte header, the payload, and a new
-// header wherever the payload reaches a block's end with bytes left
-// (singleWriter.Write, :628-653).  Bytes leave as 16-byte stores from a
-// register accumulator.  Pass 2 (tan_headers) fills each header
-// (fillHeader, :468-487) from the bytes read back.
+// The bytes one record adds to its log file go out as 16-byte stores from a
+// register accumulator: zero padding when the header does not fit in the
+// block (getNext, record.go:548-573), a 7-byte header, the payload, and a
+// new header wherever the payload reaches a block's end with bytes left
+// (singleWriter.Write, :628-653).  Each chunk's checksum -- the low 32 bits
+// of XXH64 (seed 0) over its type byte and payload (fillHeader, :468-487)
+// -- is computed as the bytes go out, by a streaming XXH64 kept in
+// registers, and patched into the chunk's header when the chunk ends
+// (into the accumulator if that header has not been stored yet).
 struct TanOut {
   uint4 *dst;
   uint32_t cap16;
@@ -129,6 +70,13 @@ struct TanOut {
   uint32_t pos;     // 16 B chunks stored
   uint32_t total;   // bytes produced
   uint32_t bpos;    // position in the block of the next byte
+  uint32_t left;    // payload bytes still to come
+  uint32_t hdr;     // byte position of the open chunk's header
+  bool first;       // no chunk opened yet
+  // XXH64 of the open chunk: stripe accumulators, the partial stripe
+  uint64_t v0, v1, v2, v3, h0, h1, h2, h3;
+  uint32_t hn;    // bytes in the partial stripe
+  uint32_t hlen;  // bytes hashed
 };
 
 __device__ __forceinline__ void to_flush16(TanOut &o) {
@@ -155,28 +103,139 @@ __device__ __forceinline__ void to_zeros(TanOut &o, uint32_t k) {
   for (uint32_t i = 0; i < k; ++i) to_raw(o, 0);
 }
 
-// begins a record at block position bpos: padding and the first header
+// byte p of the output (a zero placeholder) becomes b: in the accumulator
+// when p has not been stored yet, else a byte store behind the lane's own
+// 16-byte store of that word (same address, program order)
+__device__ __forceinline__ void to_patch(TanOut &o, uint32_t p, uint32_t b) {
+  const uint32_t base = o.pos * 16;
+  b &= 0xffu;
+  if (p >= base) {
+    const uint32_t q = p - base;
+    if (q < 8)
+      o.lo |= (uint64_t)b << (8 * q);
+    else
+      o.hi |= (uint64_t)b << (8 * (q - 8));
+  } else if (p < o.cap16 * 16) {
+    reinterpret_cast<uint8_t *>(o.dst)[p] = (uint8_t)b;
+  }
+}
+
+__device__ __forceinline__ void xs_byte(TanOut &o, uint32_t b) {
+  const uint64_t x = (uint64_t)(b & 0xffu) << ((o.hn & 7) * 8);
+  const uint32_t w = o.hn >> 3;
+  o.h0 |= w == 0 ? x : 0;
+  o.h1 |= w == 1 ? x : 0;
+  o.h2 |= w == 2 ? x : 0;
+  o.h3 |= w == 3 ? x : 0;
+  o.hlen++;
+  if (++o.hn == 32) {
+    o.v0 = xx_round(o.v0, o.h0);
+    o.v1 = xx_round(o.v1, o.h1);
+    o.v2 = xx_round(o.v2, o.h2);
+    o.v3 = xx_round(o.v3, o.h3);
+    o.h0 = o.h1 = o.h2 = o.h3 = 0;
+    o.hn = 0;
+  }
+}
+
+// XXH64_digest of the open chunk (xxhash.go Sum64 / Digest.Sum64)
+__device__ __forceinline__ uint64_t xs_final(const TanOut &o) {
+  uint64_t acc;
+  if (o.hlen >= 32) {
+    acc = rotl64(o.v0, 1) + rotl64(o.v1, 7) + rotl64(o.v2, 12) +
+          rotl64(o.v3, 18);
+    acc = xx_merge(acc, o.v0);
+    acc = xx_merge(acc, o.v1);
+    acc = xx_merge(acc, o.v2);
+    acc = xx_merge(acc, o.v3);
+  } else {
+    acc = XP5;
+  }
+  acc += o.hlen;
+  const uint64_t hw[4] = {o.h0, o.h1, o.h2, o.h3};
+  uint32_t left = o.hn;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (left >= 8 * (k + 1))
+      acc = rotl64(acc ^ xx_round(0, hw[k]), 27) * XP1 + XP4;
+  const uint32_t w = left >> 3;
+  uint64_t t = w == 0 ? o.h0 : w == 1 ? o.h1 : w == 2 ? o.h2 : o.h3;
+  left &= 7;
+  if (left >= 4) {
+    acc = rotl64(acc ^ (t & 0xffffffffull) * XP1, 23) * XP2 + XP3;
+    t >>= 32;
+    left -= 4;
+  }
+  for (; left; --left) {
+    acc = rotl64(acc ^ (t & 0xffull) * XP5, 11) * XP1;
+    t >>= 8;
+  }
+  acc ^= acc >> 33;
+  acc *= XP2;
+  acc ^= acc >> 29;
+  acc *= XP3;
+  acc ^= acc >> 32;
+  return acc;
+}
+
+// the open chunk is complete: its checksum into its header
+__device__ __forceinline__ void to_close(TanOut &o) {
+  const uint32_t c = (uint32_t)xs_final(o);
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) to_patch(o, o.hdr + k, c >> (8 * k));
+}
+
+// a chunk header at the current block position: checksum placeholder,
+// length, type (fullChunkType 1, first 2, middle 3, last 4); the hash
+// starts over with the type byte
+__device__ __forceinline__ void to_open(TanOut &o) {
+  const uint32_t room = TAN_BLOCK - o.bpos - TAN_HDR;
+  const uint32_t k = o.left < room ? o.left : room;
+  const bool last = k == o.left;
+  const uint32_t type = last ? (o.first ? 1u : 4u) : (o.first ? 2u : 3u);
+  o.first = false;
+  o.hdr = o.total;
+  to_zeros(o, 4);
+  to_raw(o, k);
+  to_raw(o, k >> 8);
+  to_raw(o, type);
+  o.v0 = XP1 + XP2;
+  o.v1 = XP2;
+  o.v2 = 0;
+  o.v3 = 0 - XP1;
+  o.h0 = o.h1 = o.h2 = o.h3 = 0;
+  o.hn = o.hlen = 0;
+  xs_byte(o, type);
+}
+
+// begins a record of `len` payload bytes at block position bpos: padding
+// and the first header
 __device__ __forceinline__ void to_begin(TanOut &o, uint4 *dst, uint32_t cap16,
-                                         uint32_t bpos) {
+                                         uint32_t bpos, uint32_t len) {
   o.dst = dst;
   o.cap16 = cap16;
   o.lo = o.hi = 0;
   o.n = o.pos = o.total = 0;
   o.bpos = bpos;
+  o.left = len;
+  o.first = true;
   if (bpos + TAN_HDR > TAN_BLOCK) {  // the rest of the block stays zero
     to_zeros(o, TAN_BLOCK - bpos);
     o.bpos = 0;
   }
-  to_zeros(o, TAN_HDR);
+  to_open(o);
 }
 
 // one payload byte (the colfer / Update encoders' sink)
 __device__ __forceinline__ void bo_byte(TanOut &o, uint32_t b) {
-  if (o.bpos == TAN_BLOCK) {  // the block is full: the next chunk's header
+  if (o.bpos == TAN_BLOCK) {  // the block is full: the next chunk
+    to_close(o);
     o.bpos = 0;
-    to_zeros(o, TAN_HDR);
+    to_open(o);
   }
   to_raw(o, b);
+  xs_byte(o, b);
+  o.left--;
 }
 
 __device__ __forceinline__ void to_le32(TanOut &o, uint32_t x) {
@@ -184,45 +243,8 @@ __device__ __forceinline__ void to_le32(TanOut &o, uint32_t x) {
 }
 
 __device__ __forceinline__ void to_finish(TanOut &o) {
+  to_close(o);
   if (o.n) to_flush16(o);
-}
-
-// Pass 2: the chunk headers of a record of `len` payload bytes laid out by
-// pass 1 from block position bpos in the lane's buffer: checksum = low 32
-// bits of XXH64 over the type byte and the payload, length, type
-// (fullChunkType 1, first 2, middle 3, last 4)
-__device__ __forceinline__ void tan_headers(uint4 *dst, uint32_t cap16,
-                                            uint32_t bpos, uint32_t len) {
-  // pass 1's stores are visible to this lane's loads
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  uint8_t *b = reinterpret_cast<uint8_t *>(dst);
-  const uint64_t *w = reinterpret_cast<const uint64_t *>(dst);
-  uint32_t h = 0;
-  if (bpos + TAN_HDR > TAN_BLOCK) {
-    h = TAN_BLOCK - bpos;
-    bpos = 0;
-  }
-  bool first = true;
-  uint32_t left = len;
-  for (;;) {
-    const uint32_t room = TAN_BLOCK - bpos - TAN_HDR;
-    const uint32_t k = left < room ? left : room;
-    left -= k;
-    const uint32_t type = left == 0 ? (first ? 1u : 4u) : (first ? 2u : 3u);
-    b[h + 6] = (uint8_t)type;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    const uint32_t c = (uint32_t)xxh64_at(w, h + 6, k + 1, cap16 * 2);
-    b[h + 0] = (uint8_t)c;
-    b[h + 1] = (uint8_t)(c >> 8);
-    b[h + 2] = (uint8_t)(c >> 16);
-    b[h + 3] = (uint8_t)(c >> 24);
-    b[h + 4] = (uint8_t)k;
-    b[h + 5] = (uint8_t)(k >> 8);
-    if (left == 0) return;
-    h += TAN_HDR + k;
-    bpos = 0;
-    first = false;
-  }
 }
 
 // bytes a record of `len` payload bytes adds at block position bpos
@@ -321,7 +343,7 @@ __device__ __forceinline__ void tan_write_one(const View &v, uint32_t slot, uint
   } else {
     TanOut o;
     uint4 *dst = v.save_buf + i * v.save_cap16;
-    to_begin(o, dst, v.save_cap16, bpos);
+    to_begin(o, dst, v.save_cap16, bpos, len);
     bo_varint(o, shard);
     bo_varint(o, slot + 1);
     if (u_state) {
@@ -344,7 +366,6 @@ __device__ __forceinline__ void tan_write_one(const View &v, uint32_t slot, uint
     }
     bo_byte(o, 0);  // IsEmptySnapshot
     to_finish(o);
-    tan_headers(dst, v.save_cap16, bpos, len);
     // writeRecord's offset (record.go:589) = the file's new size
     rec.x = (uint32_t)off;
     rec.y = (uint32_t)(off >> 32);
