@@ -516,8 +516,25 @@ static void scan_batch(const uint8_t *stream, Frame &f) {
   const uint8_t *p = stream + f.off;
   const size_t n = (size_t)f.size;
   size_t j = 0;
+  f.moff.reserve(n / 32);
+  f.mlen.reserve(n / 32);
   while (j < n) {
     uint64_t wire, v;
+    // the common element: tag 0x0a and a one- or two-byte length
+    if (p[j] == 0x0a && j + 3 <= n) {
+      uint32_t l = p[j + 1];
+      size_t h = 2;
+      if (l >= 0x80) {
+        l = (l & 0x7f) | ((uint32_t)p[j + 2] << 7);
+        h = 3;
+      }
+      if (l < (1u << 14) && l <= n - j - h) {
+        f.moff.push_back(f.off + j + h);
+        f.mlen.push_back(l);
+        j += h + l;
+        continue;
+      }
+    }
     if (!varint(p, n, j, wire) || (wire >> 3) == 0) {
       f.scan_ok = false;
       return;
@@ -564,6 +581,9 @@ struct IngestState {
   IngestBuf stream, msgs, ents, sort, misc;
   uint8_t *pinned = nullptr;  // drb_ingest_buffer (hipHostMalloc)
   size_t pinned_cap = 0;
+  // the frames of the last call; their Requests vectors keep their
+  // capacity, so a warm call neither faults nor unmaps ~12 B per message
+  std::vector<wirehost::Frame> frames;
 };
 static void ingest_free(IngestState *st) {
   if (!st) return;
@@ -588,6 +608,7 @@ struct IngestTrace {
     on = e && e[0] == '1';
     t = std::chrono::steady_clock::now();
   }
+  ~IngestTrace() { mark("return"); }
   void mark(const char *what) {
     if (!on) return;
     (void)hipStreamSynchronize(s);
@@ -630,7 +651,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   memset(&res, 0, sizeof(res));
   IngestTrace tr(e->stream);
   // 1. frames: magic + requestHeader + its CRC (tcp.go:64-112, 180-237)
-  std::vector<wirehost::Frame> fr;
+  std::vector<wirehost::Frame> &fr = st.frames;
+  size_t nfr = 0;
   size_t i = 0;
   bool bad_header = false;
   while (i < len) {
@@ -650,19 +672,34 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       bad_header = true;  // ErrBadMessage: the connection is closed
       break;
     }
-    wirehost::Frame f;
+    if (nfr == fr.size()) fr.emplace_back();
+    wirehost::Frame &f = fr[nfr++];
     f.off = i + 20;
     f.size = size;
     f.method = method;
     f.pcrc = (uint32_t)wirehost::be(h + 14, 4);
-    fr.push_back(std::move(f));
+    f.scan_ok = true;
+    f.did = f.bv = 0;
+    f.moff.clear();
+    f.mlen.clear();
     i += 20 + (size_t)size;
   }
+  fr.resize(nfr);
   const size_t walked = i;  // bytes of whole frames
   tr.mark("headers");
-  // 2. Requests boundaries, one host thread per frame (a frame holds up to
-  // 64 MiB of messages); at most 16 threads
+  const size_t sb = al256(walked + 16);
+  if (ing_grow(st.stream, sb)) return DRB_EDEVICE;
+  uint8_t *ds = (uint8_t *)st.stream.p;
+  hipStream_t sm = e->stream;
+  // 2. the stream goes up (its own host thread: a pageable source makes
+  // the copy synchronous) while Requests boundaries are found, one host
+  // thread per frame (a frame holds up to 64 MiB of messages), at most 16
   {
+    hipError_t up_err = hipSuccess;
+    std::thread up([&]() {
+      if (walked)
+        up_err = hipMemcpyAsync(ds, stream, walked, hipMemcpyHostToDevice, sm);
+    });
     const size_t nt = std::min<size_t>(16, fr.size());
     std::vector<std::thread> th;
     for (size_t t = 0; t < nt; ++t)
@@ -671,10 +708,12 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
           if (fr[f].method == 100) wirehost::scan_batch(stream, fr[f]);
       });
     for (auto &x : th) x.join();
+    up.join();
+    HIPCHK(up_err);
   }
   uint64_t nm = 0;
   for (const auto &f : fr) nm += f.moff.size();
-  tr.mark("scan");
+  tr.mark("up+scan");
   // 3. the stream up, the payload CRCs in 16 KB chunks
   constexpr uint64_t CH = 16384;
   std::vector<uint64_t> coff;
@@ -689,8 +728,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   }
   cfirst[fr.size()] = (uint32_t)coff.size();
   const size_t nc = coff.size();
-  const size_t sb = al256(walked + 16);
-  if (ing_grow(st.stream, sb)) return DRB_EDEVICE;
   // misc: chunk offsets/lens/crcs, message offsets/lens/frames, counts,
   // errors, entry bases, deliver flags, per-frame error, 2 counters
   const size_t m1 = nm ? nm : 1;
@@ -700,7 +737,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                     al256((nf + 1) * 4) + al256((nf + 1) * 8) +
                     al256(nf + 1) + 256;
   if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
-  uint8_t *ds = (uint8_t *)st.stream.p;
   uint8_t *q = (uint8_t *)st.misc.p;
   auto take = [&](size_t b) {
     uint8_t *r = q;
@@ -734,8 +770,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // each frame's Requests go up straight from its scan vectors
   std::vector<uint64_t> mbase(nf + 1, 0);
   for (size_t f = 0; f < nf; ++f) mbase[f + 1] = mbase[f] + fr[f].moff.size();
-  hipStream_t sm = e->stream;
-  if (walked) HIPCHK(hipMemcpyAsync(ds, stream, walked, hipMemcpyHostToDevice, sm));
   if (nc) {
     HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice, sm));
@@ -769,7 +803,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   HIPCHK(hipMemcpyAsync(fbad.data(), d_fbad, (fr.size() + 1) * 4,
                         hipMemcpyDeviceToHost, sm));
   HIPCHK(hipStreamSynchronize(sm));
-  tr.mark("up+crc+cnt");
+  tr.mark("crc+cnt");
   // 4. the frames delivered: up to the first with a bad CRC or a batch that
   // does not decode (ErrBadMessage closes the connection, tcp.go:528-530)
   std::vector<uint8_t> fstate(nf + 1, 0);
