@@ -104,11 +104,13 @@ def parse():
                     help="Config.Quiesce (default: on for c5, SURVEY 8d)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--save", default="",
-                    choices=["", "none", "entrybatch", "tan"],
+                    choices=["", "none", "entrybatch", "tan", "tanmux"],
                     help="persistence output of every round: none, "
-                         "EntryBatch + CRC32 per replica, or the regular "
+                         "EntryBatch + CRC32 per replica, the regular "
                          "tan LogDB's log record per replica (XXH64 "
-                         "chunks); default: entrybatch for c5, else none")
+                         "chunks), or the multiplexed tan's (16 logs per "
+                         "slot, records back to back); default: entrybatch "
+                         "for c5, else none")
     ap.add_argument("--elections", type=int, default=0,
                     help="1: the engine runs elections on the GPU "
                          "(drb_config.elections); the timed rounds show its "
@@ -287,8 +289,9 @@ def main():
                      mailbox=8, kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
                      kv_pool_blocks=ks * G * R if args.payload == 128
                      else 4 * G * R, save_cap=(4 * bound + 15) // 16 * 16 +
-                     (128 if args.save == "tan" else 0),
-                     save_tan=int(args.save == "tan"),
+                     (128 if args.save in ("tan", "tanmux") else 0),
+                     save_tan=int(args.save in ("tan", "tanmux")),
+                     tan_multiplexed=int(args.save == "tanmux"),
                      quiesce=args.quiesce, first_shard_id=first_shard,
                      device=local)
     else:
@@ -301,7 +304,8 @@ def main():
                      mailbox=16, kv_slots=args.kv_slots or 512, kv_val_cap=4,
                      save_cap=(((2 * k + 2) * bound + 15) // 16 * 16 + 128
                                if saves else 0),
-                     save_tan=int(args.save == "tan"),
+                     save_tan=int(args.save in ("tan", "tanmux")),
+                     tan_multiplexed=int(args.save == "tanmux"),
                      elections=args.elections,
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
@@ -558,7 +562,9 @@ def main():
         if c5:
             sv = ("EntryBatch + CRC32 of EntriesToSave" if args.save ==
                   "entrybatch" else "tan log records (XXH64) of every "
-                  "Update" if args.save == "tan" else "no saves")
+                  "Update" if args.save == "tan" else "multiplexed tan log "
+                  "records (XXH64) of every Update" if args.save == "tanmux"
+                  else "no saves")
             metric = ("committed entries/sec (node) at %d 3-replica groups, "
                       "%d B payload, %g %% active per round, %s; %%HBM BW" % (
                           G, args.payload, args.active_ppm / 1e4, sv))
@@ -643,7 +649,7 @@ def main():
                          "saved_entries": out.saved_entries,
                          "saved_bytes": out.saved_bytes},
         }
-        if args.save == "tan":
+        if args.save in ("tan", "tanmux"):
             res["counters"].update(
                 log_records=out.log_records, log_syncs=out.log_syncs,
                 log_new=out.log_new)
@@ -654,7 +660,11 @@ def main():
                 "tan": "each replica's pb.Update as the regular tan LogDB's "
                        "log record (Update.MarshalTo in 32 KiB-block chunks "
                        "with XXH64 checksums, db.write skip / sync, "
-                       "k_tan_encode)"}[args.save]
+                       "k_tan_select / k_tan_write)",
+                "tanmux": "each replica's pb.Update as a record of the "
+                          "multiplexed tan LogDB (16 logs per slot, key = "
+                          "ShardID % 16, records back to back in group "
+                          "order, k_tanm_chain)"}[args.save]
         if wire is not None:
             res["wire"] = wire
         if host_staged is not None:

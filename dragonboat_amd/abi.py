@@ -131,7 +131,8 @@ class Config(C.Structure):
                 ("kv_pool_blocks", C.c_uint32), ("flagged_cap", C.c_uint32),
                 ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
                 ("save_batched", C.c_uint32), ("save_tan", C.c_uint32),
-                ("elections", C.c_uint32), ("tan_max_log", C.c_uint64)]
+                ("elections", C.c_uint32), ("tan_max_log", C.c_uint64),
+                ("tan_multiplexed", C.c_uint32), ("tan_pad", C.c_uint32)]
 
 
 class ApplyResult(C.Structure):
@@ -172,6 +173,14 @@ class TanState(C.Structure):
     """drb_tan_state: a replica's tan writer position."""
     _fields_ = [("offset", C.c_uint64), ("log", C.c_uint32),
                 ("state_stored", C.c_uint32)]
+
+
+class TanLog(C.Structure):
+    """drb_tan_log: a multiplexed tan log's part of the last round."""
+    _fields_ = [("start_offset", C.c_uint64), ("end_offset", C.c_uint64),
+                ("bytes", C.c_uint64), ("start_log", C.c_uint32),
+                ("end_log", C.c_uint32), ("flags", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 class Region(C.Structure):

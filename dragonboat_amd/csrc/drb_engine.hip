@@ -200,6 +200,9 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (cfg->save_tan && (cfg->save_cap == 0 || cfg->save_batched))
     return DRB_EINVAL;
+  // the multiplexed tan: a tan option, ShardIDs of this rank's groups
+  if (cfg->tan_multiplexed && (!cfg->save_tan || cfg->place_world > 1))
+    return DRB_EINVAL;
   // (the tan write pass lists replicas by 32-bit lane number)
   if (cfg->save_tan && (uint64_t)cfg->num_replicas * cfg->num_groups > 0xffffffffull)
     return DRB_ERANGE;
@@ -328,7 +331,15 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   }
   v.save_cap16 = cfg->save_cap / 16;
   if (v.save_cap16) {
-    rc |= dalloc(e, &v.save_buf, R * G * v.save_cap16);
+    // the multiplexed tan stages each log's round in save_buf: 16 logs per
+    // slot of at most tanm_J records each
+    v.tan_mux = cfg->save_tan && cfg->tan_multiplexed ? 1u : 0u;
+    v.tanm_J = (uint32_t)((((G + 15) / 16) + 255) & ~255ull);
+    v.tanm_cap16 = (uint64_t)v.tanm_J * v.save_cap16;
+    if (v.tan_mux && v.tanm_cap16 * 16 > 0xffffffffull) return DRB_ERANGE;
+    rc |= dalloc(e, &v.save_buf,
+                 std::max<uint64_t>(R * G, v.tan_mux ? R * 16 * v.tanm_J : 0) *
+                     v.save_cap16);
     rc |= dalloc(e, &v.save_len, R * G);
     rc |= dalloc(e, &v.save_crc, R * G);
   }
@@ -353,6 +364,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.tan_ctr, e->tan_blocks * 4);
     rc |= dalloc(e, &e->tan_list, (uint64_t)e->tan_per_list * drb::TAN_LISTS);
     rc |= dalloc(e, &e->tan_n, 64 * drb::TAN_LISTS);
+    if (v.tan_mux) {
+      rc |= dalloc(e, &v.tanm_len, R * 16 * v.tanm_J);
+      rc |= dalloc(e, &v.tanm_pos, R * 16 * v.tanm_J);
+      rc |= dalloc(e, &v.tanm_cur, R * 16);
+      rc |= dalloc(e, &v.tanm_log, R * 16 * 2);
+    }
     rc |= dalloc(e, &e->tan_total, 4);
   }
   v.elections = cfg->elections ? 1u : 0u;
@@ -2526,6 +2543,10 @@ static int launch_tan(drb_engine *e, uint32_t round) {
   k_tan_select<<<(unsigned)e->tan_blocks, 256, 0, e->stream>>>(
       e->v, round, max_log, e->tan_list, e->tan_per_list, e->tan_n);
   HIPCHK(hipGetLastError());
+  if (e->v.tan_mux) {
+    k_tanm_chain<<<e->v.R * 16, 64, 0, e->stream>>>(e->v, max_log);
+    HIPCHK(hipGetLastError());
+  }
   k_tan_write<<<(unsigned)e->tan_wblocks, 256, 0, e->stream>>>(
       e->v, round, max_log, e->tan_list, e->tan_per_list, e->tan_n);
   HIPCHK(hipGetLastError());
@@ -2593,8 +2614,48 @@ extern "C" int drb_export_tan(drb_engine *e, uint64_t group, uint32_t slot,
   }
   if (rec->len > cap) return rec->len && buf ? DRB_ERANGE : DRB_OK;
   if (rec->len) {
-    HIPCHK(hipMemcpyAsync(buf, v.save_buf + ix(v, slot, group) * v.save_cap16,
-                          rec->len, hipMemcpyDeviceToHost, e->stream));
+    const uint8_t *src =
+        reinterpret_cast<const uint8_t *>(v.save_buf + ix(v, slot, group) *
+                                                           v.save_cap16);
+    if (v.tan_mux) {  // its place in its log's staging
+      uint4 p;
+      HIPCHK(hipMemcpyAsync(&p, v.tanm_pos + tanm_ix(v, slot, group),
+                            sizeof(p), hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
+      src = reinterpret_cast<const uint8_t *>(
+                v.save_buf + ((uint64_t)slot * 16 + tanm_key(v, group)) *
+                                 v.tanm_cap16) + p.z;
+    }
+    HIPCHK(hipMemcpyAsync(buf, src, rec->len, hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  return DRB_OK;
+}
+
+extern "C" int drb_export_tan_log(drb_engine *e, uint32_t slot, uint32_t key,
+                                  drb_tan_log *out, uint8_t *buf, size_t cap) {
+  if (!e || !out || (cap && !buf)) return DRB_EINVAL;
+  const View &v = e->v;
+  if (!v.tan_mux) return DRB_EINVAL;
+  if (slot >= v.R || key >= 16) return DRB_ERANGE;
+  uint4 lg[2];
+  const uint64_t L = (uint64_t)slot * 16 + key;
+  HIPCHK(hipMemcpyAsync(lg, v.tanm_log + 2 * L, sizeof(lg),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  memset(out, 0, sizeof(*out));
+  out->start_offset = (uint64_t)lg[0].x | ((uint64_t)lg[0].y << 32);
+  out->start_log = lg[0].z;
+  out->flags = lg[0].w;
+  out->bytes = lg[1].x;
+  out->end_log = lg[1].y;
+  out->end_offset = (uint64_t)lg[1].z | ((uint64_t)lg[1].w << 32);
+  if (!buf) return DRB_OK;
+  if (out->bytes > cap) return DRB_ERANGE;
+  if (out->bytes) {
+    HIPCHK(hipMemcpyAsync(buf, v.save_buf + L * v.tanm_cap16, out->bytes,
+                          hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
   }
   return DRB_OK;
@@ -2606,10 +2667,18 @@ extern "C" int drb_tan_get(drb_engine *e, uint64_t group, uint32_t slot,
   const View &v = e->v;
   if (!v.save_tan) return DRB_EINVAL;
   if (group >= v.G || slot >= v.R) return DRB_ERANGE;
-  uint4 st;
+  uint4 st, cur;
   HIPCHK(hipMemcpyAsync(&st, v.tan_st + ix(v, slot, group), sizeof(st),
                         hipMemcpyDeviceToHost, e->stream));
+  if (v.tan_mux)  // the writer of the replica's multiplexed log
+    HIPCHK(hipMemcpyAsync(&cur, v.tanm_cur + slot * 16 + tanm_key(v, group),
+                          sizeof(cur), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (v.tan_mux) {
+    st.x = cur.x;
+    st.y = cur.y;
+    st.z = cur.z;
+  }
   out->offset = (uint64_t)st.x | ((uint64_t)st.y << 32);
   out->log = st.z;
   out->state_stored = st.w & TST_STATE;
@@ -2627,6 +2696,11 @@ extern "C" int drb_tan_set(drb_engine *e, uint64_t group, uint32_t slot,
                               in->state_stored ? TST_STATE : 0u);
   HIPCHK(hipMemcpyAsync(v.tan_st + ix(v, slot, group), &st, sizeof(st),
                         hipMemcpyHostToDevice, e->stream));
+  if (v.tan_mux) {  // (the log's writer, shared by the slot's replicas)
+    const uint4 cur = make_uint4(st.x, st.y, st.z, 0);
+    HIPCHK(hipMemcpyAsync(v.tanm_cur + slot * 16 + tanm_key(v, group), &cur,
+                          sizeof(cur), hipMemcpyHostToDevice, e->stream));
+  }
   HIPCHK(hipStreamSynchronize(e->stream));
   return DRB_OK;
 }

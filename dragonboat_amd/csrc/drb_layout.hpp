@@ -330,6 +330,17 @@ struct View {
   uint4 *tan_st;          // [R][G] {offset lo, hi, log, TST_* flags}
   uint4 *tan_rec;         // [R][G] {offset lo, hi, len, DRB_TAN_* | log << 8}
   unsigned long long *tan_ctr;  // [blocks][4] bytes, records, syncs, logs
+  // multiplexed tan (CreateLogMultiplexedTan): 16 logs per replica slot,
+  // key = ShardID % 16 (db_keeper.go:84-123), records in group order
+  uint32_t tan_mux;
+  uint32_t tanm_J;        // records per log row: >= ceil(G / 16), 256 | J
+  uint32_t *tanm_len;     // [R][16][J] payload bytes | sync << 31, 0: none
+  uint4 *tanm_pos;        // [R][16][J] {offset lo, hi, staging byte,
+                          //  log << 1 | new log}
+  uint4 *tanm_cur;        // [R][16] the log writer {offset lo, hi, log, 0}
+  uint4 *tanm_log;        // [R][16][2] the round: {start offset lo, hi,
+                          //  start log, flags} {bytes, end log, end lo, hi}
+  uint64_t tanm_cap16;    // staging chunks per log (in save_buf)
   // elections (drb_config.elections): the replicas the raft launch steps
   // this round {g lo, g hi, slot, 0}, their count, and the term of every
   // record it wrote whose term differs from its header's (MF_TERM_OTHER)

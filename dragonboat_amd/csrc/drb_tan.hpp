@@ -65,6 +65,9 @@ __device__ __forceinline__ uint64_t xx_merge(uint64_t acc, uint64_t v) {
 struct TanOut {
   uint4 *dst;
   uint32_t cap16;
+  uint32_t start;   // byte position of the record in dst
+  uint32_t skip;    // bytes of the first 16 B word that precede the record
+  bool shared;      // dst is a log's staging: the last word is shared too
   uint64_t lo, hi;  // pending bytes
   uint32_t n;       // pending byte count
   uint32_t pos;     // 16 B chunks stored
@@ -79,10 +82,24 @@ struct TanOut {
   uint32_t hlen;  // bytes hashed
 };
 
+// bytes [from, to) of the pending word, one byte store each (a word the
+// record shares with its neighbour in a log's staging)
+__device__ __forceinline__ void to_store_bytes(TanOut &o, uint32_t from,
+                                               uint32_t to) {
+  if (o.pos >= o.cap16) return;
+  uint8_t *b = reinterpret_cast<uint8_t *>(o.dst + o.pos);
+  for (uint32_t k = from; k < to; ++k)
+    b[k] = (uint8_t)(k < 8 ? o.lo >> (8 * k) : o.hi >> (8 * (k - 8)));
+}
+
 __device__ __forceinline__ void to_flush16(TanOut &o) {
-  if (o.pos < o.cap16)
+  if (o.skip) {
+    to_store_bytes(o, o.skip, 16);
+    o.skip = 0;
+  } else if (o.pos < o.cap16) {
     o.dst[o.pos] = make_uint4((uint32_t)o.lo, (uint32_t)(o.lo >> 32),
                               (uint32_t)o.hi, (uint32_t)(o.hi >> 32));
+  }
   o.pos++;
   o.lo = o.hi = 0;
   o.n = 0;
@@ -194,7 +211,7 @@ __device__ __forceinline__ void to_open(TanOut &o) {
   const bool last = k == o.left;
   const uint32_t type = last ? (o.first ? 1u : 4u) : (o.first ? 2u : 3u);
   o.first = false;
-  o.hdr = o.total;
+  o.hdr = o.start + o.total;
   to_zeros(o, 4);
   to_raw(o, k);
   to_raw(o, k >> 8);
@@ -208,14 +225,20 @@ __device__ __forceinline__ void to_open(TanOut &o) {
   xs_byte(o, type);
 }
 
-// begins a record of `len` payload bytes at block position bpos: padding
-// and the first header
+// begins a record of `len` payload bytes at block position bpos, byte
+// `start` of dst: padding and the first header
 __device__ __forceinline__ void to_begin(TanOut &o, uint4 *dst, uint32_t cap16,
-                                         uint32_t bpos, uint32_t len) {
+                                         uint32_t bpos, uint32_t len,
+                                         uint32_t start = 0,
+                                         bool shared = false) {
   o.dst = dst;
   o.cap16 = cap16;
+  o.start = start;
+  o.shared = shared;
   o.lo = o.hi = 0;
-  o.n = o.pos = o.total = 0;
+  o.pos = start / 16;
+  o.n = o.skip = start % 16;
+  o.total = 0;
   o.bpos = bpos;
   o.left = len;
   o.first = true;
@@ -244,7 +267,14 @@ __device__ __forceinline__ void to_le32(TanOut &o, uint32_t x) {
 
 __device__ __forceinline__ void to_finish(TanOut &o) {
   to_close(o);
-  if (o.n) to_flush16(o);
+  if (o.n > o.skip) {
+    if (o.shared || o.skip) {
+      to_store_bytes(o, o.skip, o.n);
+      o.pos++;
+    } else {
+      to_flush16(o);
+    }
+  }
 }
 
 // bytes a record of `len` payload bytes adds at block position bpos
@@ -306,44 +336,85 @@ struct TanCount {
   uint32_t bytes = 0, rec = 0, sync = 0, fresh = 0;
 };
 
-// db.write of replica (slot, g)'s pending Update: its record into the
-// replica's save buffer, {offset, length, flags} into tan_rec
-__device__ __forceinline__ void tan_write_one(const View &v, uint32_t slot, uint64_t g,
-                              uint4 s2, uint4 st, uint64_t max_log,
-                              TanCount &c) {
-  const uint64_t i = ix(v, slot, g);
+// the multiplexed logs: log (slot, key) holds the groups g with
+// (first_shard_id + g) % 16 == key, record j of the round being the j-th
+// such group (place_world 1: ShardID = first_shard_id + g)
+__host__ __device__ inline uint32_t tanm_key(const View &v, uint64_t g) {
+  return (uint32_t)((v.first_shard_id + g) % 16);
+}
+__host__ __device__ inline uint64_t tanm_ix(const View &v, uint32_t slot,
+                                            uint64_t g) {
+  return ((uint64_t)slot * 16 + tanm_key(v, g)) * v.tanm_J + g / 16;
+}
+
+// the marshalled Update's size (update.go:128-169) and stateSyncChange
+// (db.go:88-90) of replica (slot, g)'s pending Update
+__device__ __forceinline__ uint32_t tan_len(const View &v, uint32_t slot,
+                                            uint64_t g, uint4 s2, uint4 st,
+                                            bool &sync) {
   const uint4 s0 = v.tan_sum[tan_sum_ix(v, 0, slot, g)];
   const uint4 s1 = v.tan_sum[tan_sum_ix(v, 1, slot, g)];
-  uint64_t off = (uint64_t)st.x | ((uint64_t)st.y << 32);
   const uint32_t n_save = s2.x;
   const bool u_state = (s2.y & TS_STATE) != 0;
   const bool st_state = (st.w & TST_STATE) != 0;
-  uint4 rec = make_uint4(st.x, st.y, 0, st.z << 8);
-  const uint64_t term = lo64(s0), vote = hi64(s0), commit = lo64(s1);
-  const uint64_t save_lo = hi64(s1);
-  // stateSyncChange (db.go:88-90)
-  const bool sync =
-      n_save > 0 || (u_state ? (!st_state || (s2.y & TS_TV)) : st_state);
-  // makeRoomForWrite (db.go:175-180) -> createNewLog (open.go:171)
-  const bool new_log = off >= max_log;
-  if (new_log) {
-    off = 0;
-    st.z++;
-  }
-  // the marshalled Update's size (update.go:128-169)
+  sync = n_save > 0 || (u_state ? (!st_state || (s2.y & TS_TV)) : st_state);
   const uint64_t shard = v.first_shard_id + gid(v, slot, g);
   uint32_t len = varint_size(shard) + varint_size(slot + 1) + 1 + 4 + 1;
-  if (u_state) len += 4 + state_size(term, vote, commit);
+  if (u_state) len += 4 + state_size(lo64(s0), hi64(s0), lo64(s1));
   for (uint32_t k = 0; k < n_save; ++k)
-    len += 4 + entry_size(ring_entry_hdr(v, slot, g, save_lo + k, false));
+    len += 4 + entry_size(ring_entry_hdr(v, slot, g, hi64(s1) + k, false));
+  return len;
+}
+
+// db.write of replica (slot, g)'s pending Update: its record into the
+// replica's save buffer (multiplexed: at its place in its log's staging,
+// laid out by k_tanm_chain), {offset, length, flags} into tan_rec
+__device__ __forceinline__ void tan_write_one(const View &v, uint32_t slot,
+                                              uint64_t g, uint4 s2, uint4 st,
+                                              uint64_t max_log, TanCount &c) {
+  const uint64_t i = ix(v, slot, g);
+  const uint4 s0 = v.tan_sum[tan_sum_ix(v, 0, slot, g)];
+  const uint4 s1 = v.tan_sum[tan_sum_ix(v, 1, slot, g)];
+  const uint32_t n_save = s2.x;
+  const bool u_state = (s2.y & TS_STATE) != 0;
+  const uint64_t term = lo64(s0), vote = hi64(s0), commit = lo64(s1);
+  const uint64_t save_lo = hi64(s1);
+  bool sync;
+  const uint32_t len = tan_len(v, slot, g, s2, st, sync);
+  uint64_t off;
+  uint32_t logn, start = 0;
+  bool new_log;
+  uint4 *dst;
+  uint32_t cap16;
+  if (v.tan_mux) {
+    const uint4 p = v.tanm_pos[tanm_ix(v, slot, g)];
+    off = (uint64_t)p.x | ((uint64_t)p.y << 32);
+    start = p.z;
+    logn = p.w >> 1;
+    new_log = p.w & 1;
+    dst = v.save_buf + ((uint64_t)slot * 16 + tanm_key(v, g)) * v.tanm_cap16;
+    cap16 = (uint32_t)v.tanm_cap16;
+  } else {
+    off = (uint64_t)st.x | ((uint64_t)st.y << 32);
+    logn = st.z;
+    // makeRoomForWrite (db.go:175-180) -> createNewLog (open.go:171)
+    new_log = off >= max_log;
+    if (new_log) {
+      off = 0;
+      logn++;
+    }
+    dst = v.save_buf + i * v.save_cap16;
+    cap16 = v.save_cap16;
+  }
+  uint4 rec = make_uint4(st.x, st.y, 0, st.z << 8);
   const uint32_t bpos = (uint32_t)(off % TAN_BLOCK);
   const uint32_t add = tan_appended(bpos, len);
   if (add > v.save_cap16 * 16) {  // bounded by the pre-pass
     rec.w = (st.z << 8) | DRB_TAN_OVERFLOW;
   } else {
+    const uint64_t shard = v.first_shard_id + gid(v, slot, g);
     TanOut o;
-    uint4 *dst = v.save_buf + i * v.save_cap16;
-    to_begin(o, dst, v.save_cap16, bpos, len);
+    to_begin(o, dst, cap16, bpos, len, start, v.tan_mux != 0);
     bo_varint(o, shard);
     bo_varint(o, slot + 1);
     if (u_state) {
@@ -370,11 +441,14 @@ __device__ __forceinline__ void tan_write_one(const View &v, uint32_t slot, uint
     rec.x = (uint32_t)off;
     rec.y = (uint32_t)(off >> 32);
     rec.z = o.total;
-    rec.w = (st.z << 8) | DRB_TAN_WRITTEN | (sync ? DRB_TAN_SYNC : 0) |
+    rec.w = (logn << 8) | DRB_TAN_WRITTEN | (sync ? DRB_TAN_SYNC : 0) |
             (new_log ? DRB_TAN_NEW_LOG : 0);
-    off += o.total;
-    st.x = (uint32_t)off;
-    st.y = (uint32_t)(off >> 32);
+    if (!v.tan_mux) {  // (a multiplexed log's writer: k_tanm_chain)
+      off += o.total;
+      st.x = (uint32_t)off;
+      st.y = (uint32_t)(off >> 32);
+      st.z = logn;
+    }
     st.w = u_state ? TST_STATE : 0;  // nodeStates.setState(u.State)
     v.tan_st[i] = st;
     c.bytes += o.total;
@@ -419,12 +493,19 @@ __global__ __launch_bounds__(256) void k_tan_select(View v, uint32_t round,
     pend = tan_pending(v, round, slot, g, s2, st, have);
     if (!pend) {
       const uint64_t i = ix(v, slot, g);
-      v.tan_rec[i] = make_uint4(st.x, st.y, 0, have ? st.z << 8 : 0);
+      v.tan_rec[i] = v.tan_mux ? make_uint4(0, 0, 0, 0)
+                               : make_uint4(st.x, st.y, 0, have ? st.z << 8 : 0);
       v.save_len[i] = 0;
+    }
+    if (v.tan_mux) {  // the record sizes k_tanm_chain lays out
+      bool sync = false;
+      const uint32_t len = pend ? tan_len(v, slot, g, s2, st, sync) : 0;
+      v.tanm_len[tanm_ix(v, slot, g)] = len | (sync ? 1u << 31 : 0u);
     }
   }
   TanCount c;
-  if (__syncthreads_count(pend) >= (int)TAN_DENSE) {
+  // (multiplexed: every record waits for the chain, so all are listed)
+  if (!v.tan_mux && __syncthreads_count(pend) >= (int)TAN_DENSE) {
     if (pend) tan_write_one(v, slot, g, s2, st, max_log, c);
   } else {
     const uint64_t m = __ballot(pend);
@@ -441,6 +522,140 @@ __global__ __launch_bounds__(256) void k_tan_select(View v, uint32_t round,
     }
   }
   tan_count_row(v, c, part);
+}
+
+// wave-wide exclusive prefix sum
+__device__ __forceinline__ uint32_t wave_excl(uint32_t x, uint32_t lane) {
+  uint32_t incl = x;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d);
+    if (lane >= d) incl += y;
+  }
+  return incl - x;
+}
+
+// One wave per multiplexed log (slot, key): the offsets of the round's
+// records in group order (concurrentSaveState, logdb.go:265-304; each
+// db.write's makeRoomForWrite and writeRecord, db.go:97-130), 256 records
+// per step, 4 per lane.  A record of len bytes takes len + 7 unless it
+// starts too close to a block's end for its header (padding), runs past
+// the block (more chunks), or finds the log full (a new log at offset 0):
+// the first such record of a step is placed exactly (tan_appended) and
+// the step continues after it.  Each record gets {offset, staging byte,
+// log, new log}; the log's staging is the round's bytes back to back.
+__global__ __launch_bounds__(64) void k_tanm_chain(View v, uint64_t max_log) {
+  const uint32_t L = blockIdx.x;  // slot * 16 + key
+  const uint32_t lane = threadIdx.x;
+  const uint4 cur = v.tanm_cur[L];
+  uint64_t off = (uint64_t)cur.x | ((uint64_t)cur.y << 32);
+  uint32_t logn = cur.z;
+  const uint64_t off0 = off;
+  const uint32_t log0 = logn;
+  uint32_t spos = 0;
+  bool any_sync = false, switched = false;
+  const uint32_t J = v.tanm_J;
+  const uint4 *lens4 = reinterpret_cast<const uint4 *>(v.tanm_len + (uint64_t)L * J);
+  uint4 *pos = v.tanm_pos + (uint64_t)L * J;
+  uint4 nxt = lens4[lane];
+  for (uint32_t base = 0; base < J; base += 256) {
+    const uint4 cl = nxt;
+    if (base + 256 < J) nxt = lens4[(base + 256) / 4 + lane];
+    const uint32_t raw[4] = {cl.x, cl.y, cl.z, cl.w};
+    uint32_t len[4];
+    uint32_t todo = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      len[k] = raw[k] & 0x7fffffffu;
+      any_sync |= (raw[k] >> 31) != 0;
+      todo |= (raw[k] ? 1u : 0u) << k;
+    }
+    any_sync = __ballot(any_sync) != 0;
+    if (__ballot(todo != 0) == 0) continue;
+    uint4 out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = make_uint4(0, 0, 0, 0);
+    for (;;) {
+      uint32_t sz[4], lp[4], sum = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sz[k] = (todo >> k & 1u) ? len[k] + TAN_HDR : 0;
+        lp[k] = sum;
+        sum += sz[k];
+      }
+      const uint32_t ex = wave_excl(sum, lane);
+      // the first record of this lane whose naive size is not exact
+      uint32_t kk = 4;
+#pragma unroll
+      for (int k = 3; k >= 0; --k) {
+        const uint64_t st = off + ex + lp[k];
+        const uint32_t b = (uint32_t)(st % TAN_BLOCK);
+        if ((todo >> k & 1u) && (st >= max_log || b + TAN_HDR + len[k] > TAN_BLOCK))
+          kk = k;
+      }
+      const uint64_t m = __ballot(kk < 4);
+      const uint32_t fl = m ? (uint32_t)__ffsll((unsigned long long)m) - 1 : 64;
+      const uint32_t fk = __shfl(kk, fl < 64 ? fl : 0);
+      // the records before it are placed at their naive offsets
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((todo >> k & 1u) && (lane < fl || (lane == fl && (uint32_t)k < fk))) {
+          const uint64_t st = off + ex + lp[k];
+          out[k] = make_uint4((uint32_t)st, (uint32_t)(st >> 32),
+                              spos + ex + lp[k], logn << 1);
+          todo &= ~(1u << k);
+        }
+      }
+      if (fl == 64) {
+        const uint32_t tot = __shfl(ex + sum, 63);
+        off += tot;
+        spos += tot;
+        break;
+      }
+      // the record that is not: placed exactly
+      uint32_t rel = 0, flen = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((uint32_t)k == kk) {
+          rel = ex + lp[k];
+          flen = len[k];
+        }
+      rel = __shfl(rel, fl);
+      flen = __shfl(flen, fl);
+      off += rel;
+      spos += rel;
+      bool fresh = false;
+      if (off >= max_log) {  // makeRoomForWrite (db.go:175-180)
+        off = 0;
+        logn++;
+        fresh = switched = true;
+      }
+      if (lane == fl) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((uint32_t)k == fk) {
+            out[k] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), spos,
+                                (logn << 1) | (fresh ? 1u : 0u));
+            todo &= ~(1u << k);
+          }
+      }
+      const uint32_t add = tan_appended((uint32_t)(off % TAN_BLOCK), flen);
+      off += add;
+      spos += add;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (raw[k]) pos[base + lane * 4 + k] = out[k];
+  }
+  if (lane == 0) {
+    v.tanm_cur[L] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), logn, 0);
+    v.tanm_log[2 * (uint64_t)L] =
+        make_uint4((uint32_t)off0, (uint32_t)(off0 >> 32), log0,
+                   (any_sync ? DRB_TAN_SYNC : 0u) |
+                       (switched ? DRB_TAN_NEW_LOG : 0u));
+    v.tanm_log[2 * (uint64_t)L + 1] =
+        make_uint4(spos, logn, (uint32_t)off, (uint32_t)(off >> 32));
+  }
 }
 
 // the listed records, one per lane (grid-stride over the lists' total);

@@ -86,6 +86,8 @@ SIGNATURES = {
     "drb_export_tan": (C.c_int, [P, U64, U32, C.POINTER(abi.TanRecord), PU8,
                                  SZ]),
     "drb_tan_get": (C.c_int, [P, U64, U32, C.POINTER(abi.TanState)]),
+    "drb_export_tan_log": (C.c_int, [P, U32, U32, C.POINTER(abi.TanLog), PU8,
+                                     C.c_size_t]),
     "drb_tan_set": (C.c_int, [P, U64, U32, C.POINTER(abi.TanState)]),
     "drb_tan_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
     "drb_plane_counts": (C.c_int, [P, PU32]),
@@ -143,7 +145,8 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 heartbeat_rtt=1, check_quorum=1, device=0, save_cap=0,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
-                save_batched=0, save_tan=0, tan_max_log=0, elections=0)
+                save_batched=0, save_tan=0, tan_max_log=0, elections=0,
+                tan_multiplexed=0)
 
 
 class Engine:
@@ -163,7 +166,8 @@ class Engine:
                    cfg["entry_mbox"], cfg["kv_pool_blocks"],
                    cfg["flagged_cap"], cfg["quiesce"],
                    cfg["durable_log"], cfg["save_batched"],
-                   cfg["save_tan"], cfg["elections"], cfg["tan_max_log"])
+                   cfg["save_tan"], cfg["elections"], cfg["tan_max_log"],
+                   cfg["tan_multiplexed"], 0)
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -408,6 +412,18 @@ class Engine:
             "drb_export_tan")
         d = {f: getattr(rec, f) for f, _ in rec._fields_ if f != "pad"}
         return d, bytes(buf[:rec.len])
+
+    def export_tan_log(self, slot, key):
+        """tan_multiplexed: (drb_tan_log as a dict, the round's bytes) of
+        log (slot, key)."""
+        lg = abi.TanLog()
+        _ck(lib().drb_export_tan_log(self.h, slot, key, C.byref(lg), None, 0),
+            "drb_export_tan_log")
+        buf = (C.c_uint8 * max(1, lg.bytes))()
+        _ck(lib().drb_export_tan_log(self.h, slot, key, C.byref(lg), buf,
+                                     lg.bytes), "drb_export_tan_log")
+        d = {f: getattr(lg, f) for f, _ in lg._fields_ if f != "pad"}
+        return d, bytes(buf[:lg.bytes])
 
     def tan_get(self, g, slot):
         st = abi.TanState()

@@ -341,6 +341,15 @@ typedef struct drb_config {
   uint32_t elections;
   /* tan MaxLogFileSize (internal/tan/options.go:29); 0: 64 MiB */
   uint64_t tan_max_log;
+  /* with save_tan, 1: the multiplexed tan (CreateLogMultiplexedTan,
+   * internal/tan/logdb.go:110-118, db_keeper.go:84-123): each replica slot
+   * (one NodeHost) keeps 16 logs, key = ShardID % 16, shared by its
+   * replicas; a round's records of one log follow in group order (the
+   * step worker's order, engine.go:1316, is a Go map's) and are laid out
+   * back to back in that log's staging (drb_export_tan_log).  place_world
+   * 1 only. */
+  uint32_t tan_multiplexed;
+  uint32_t tan_pad;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -626,6 +635,24 @@ int drb_tan_get(drb_engine *e, uint64_t group, uint32_t slot,
                 drb_tan_state *out);
 int drb_tan_set(drb_engine *e, uint64_t group, uint32_t slot,
                 const drb_tan_state *in);
+/* tan_multiplexed: log (slot, key)'s part of the last encode_saves round
+ * -- what concurrentSaveState (internal/tan/logdb.go:265-304) appended to
+ * it: `bytes` bytes starting at offset start_offset of log start_log, the
+ * records back to back; when DRB_TAN_NEW_LOG a makeRoomForWrite switch
+ * happened inside (each record's drb_export_tan says where, the new log
+ * starts at offset 0); one fsync of the log when DRB_TAN_SYNC.  buf
+ * (cap >= bytes) receives the bytes. */
+typedef struct drb_tan_log {
+  uint64_t start_offset;
+  uint64_t end_offset;  /* the log writer's offset after the round */
+  uint64_t bytes;
+  uint32_t start_log;
+  uint32_t end_log;
+  uint32_t flags;       /* DRB_TAN_SYNC | DRB_TAN_NEW_LOG */
+  uint32_t pad;
+} drb_tan_log;
+int drb_export_tan_log(drb_engine *e, uint32_t slot, uint32_t key,
+                       drb_tan_log *out, uint8_t *buf, size_t cap);
 /* The round's tan records on the device for a bulk writer: replica
  * (slot, g)'s bytes at bytes + (slot * G + g) * save_cap, its record
  * {offset lo, offset hi, len, flags | log << 8} at recs[slot * G + g]. */

@@ -417,14 +417,20 @@ size_t orc_update_marshal(uint64_t shard, uint64_t replica, uint64_t term,
   return off;
 }
 
-/* ---- db (db.go) for one replica --------------------------------------- */
+/* ---- db (db.go): one replica's (regular) or many shards' (multiplexed) */
 struct orc_tandb {
   orc_tanw w;
   tan_file *files; /* one per log created, in order */
   size_t nfiles;
   int64_t offset;      /* db.mu.offset */
   int64_t max_log;     /* MaxLogFileSize */
-  uint64_t st_term, st_vote, st_commit; /* nodeStates state */
+  /* nodeStates (db.go:108, 128): the last stored State per (shard,
+   * replica) -- one node in the regular tan, the nodes of every shard
+   * with the same key in the multiplexed one (db_keeper.go:84-123) */
+  struct tan_node {
+    uint64_t shard, replica, term, vote, commit;
+  } *nodes;
+  size_t nnodes;
   /* the last orc_tandb_write */
   int64_t last_off;   /* file offset its bytes start at */
   size_t last_len;    /* bytes it appended (zero padding included) */
@@ -453,6 +459,7 @@ void orc_tandb_free(orc_tandb *db) {
   if (!db) return;
   for (size_t i = 0; i < db->nfiles; i++) free(db->files[i].p);
   free(db->files);
+  free(db->nodes);
   free(db);
 }
 
@@ -467,11 +474,22 @@ int orc_tandb_write(orc_tandb *db, uint64_t shard, uint64_t replica,
   db->last_new_log = 0;
   db->last_off = db->offset;
   if (sync) *sync = 0;
-  if (term == db->st_term && vote == db->st_vote && commit == db->st_commit &&
-      n == 0)
+  struct tan_node *nd = NULL;
+  for (size_t k = 0; k < db->nnodes && !nd; k++)
+    if (db->nodes[k].shard == shard && db->nodes[k].replica == replica)
+      nd = &db->nodes[k];
+  if (!nd) { /* getState of a node never written: the empty State */
+    db->nodes = (struct tan_node *)realloc(
+        db->nodes, (db->nnodes + 1) * sizeof(struct tan_node));
+    nd = &db->nodes[db->nnodes++];
+    memset(nd, 0, sizeof(*nd));
+    nd->shard = shard;
+    nd->replica = replica;
+  }
+  if (term == nd->term && vote == nd->vote && commit == nd->commit && n == 0)
     return 0;
   /* stateSyncChange (db.go:88-90) */
-  const int s = n > 0 || term != db->st_term || vote != db->st_vote;
+  const int s = n > 0 || term != nd->term || vote != nd->vote;
   uint8_t *buf = (uint8_t *)malloc(orc_update_size_bound(ents, n));
   const size_t len =
       orc_update_marshal(shard, replica, term, vote, commit, ents, n, pool, buf);
@@ -487,9 +505,9 @@ int orc_tandb_write(orc_tandb *db, uint64_t shard, uint64_t replica,
   free(buf);
   db->last_off = (int64_t)before;
   db->last_len = db->files[db->nfiles - 1].n - before;
-  db->st_term = term;
-  db->st_vote = vote;
-  db->st_commit = commit;
+  nd->term = term;
+  nd->vote = vote;
+  nd->commit = commit;
   db->last_sync = s;
   if (sync) *sync = s;
   return 1;

@@ -65,6 +65,7 @@ STRUCTS = {
     "drb_save_record": abi.SaveRecord,
     "drb_tan_record": abi.TanRecord,
     "drb_tan_state": abi.TanState,
+    "drb_tan_log": abi.TanLog,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}
@@ -133,6 +134,10 @@ def test_engine_without_gpu_fails_loudly():
     dict(num_groups=64, num_replicas=3, save_tan=1),
     dict(num_groups=64, num_replicas=3, save_tan=1, save_batched=1,
          save_cap=4096, window=64),
+    # the multiplexed tan: a tan option; keys are ShardIDs of one rank
+    dict(num_groups=64, num_replicas=3, tan_multiplexed=1, save_cap=4096),
+    dict(num_groups=64, num_replicas=3, save_tan=1, tan_multiplexed=1,
+         save_cap=4096, place_world=2, place_rank=0, entry_mbox=64),
 ])
 def test_create_rejects_invalid_config(kw):
     """drb_engine_create validates the configuration before it touches a

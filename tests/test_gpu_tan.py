@@ -126,3 +126,80 @@ def test_tan_writer_position_roundtrip():
     _read_back(logs, dbs)
     rec, _ = p.eng.export_tan(2, 1)
     assert rec["offset"] > off
+
+
+def _mux_round(p, dbs, r):
+    """One round of the multiplexed tan: every log (slot, key) takes its
+    groups' Updates in group order; each record and each log's staged
+    bytes equal the oracle db's."""
+    first = p.eng.cfg["first_shard_id"]
+    n = 0
+    for s in range(p.R):
+        for c in range(16):
+            db = dbs[s][c]
+            before = db.last()["offset"]  # the writer's, before the round
+            pieces, syncs, fresh = [], False, False
+            for g in range(p.G):
+                if (first + g) % 16 != c:
+                    continue
+                want = p.orc.tan_write(g, s, db)
+                rec, data = p.eng.export_tan(g, s)
+                where = (r, s, c, g, rec, want)
+                if want is None:
+                    assert not rec["flags"] & abi.TAN_WRITTEN, where
+                    continue
+                assert rec["flags"] & abi.TAN_WRITTEN, where
+                assert (rec["offset"], rec["len"], rec["log"]) == \
+                    (want["off"], want["len"], want["log"]), where
+                assert bool(rec["flags"] & abi.TAN_SYNC) == want["sync"]
+                assert bool(rec["flags"] & abi.TAN_NEW_LOG) == \
+                    want["new_log"], where
+                f = db.file(want["log"])
+                assert data == f[want["off"]:want["off"] + want["len"]], where
+                pieces.append(data)
+                syncs |= want["sync"]
+                fresh |= want["new_log"]
+                n += 1
+            lg, staged = p.eng.export_tan_log(s, c)
+            where = (r, s, c, lg)
+            assert staged == b"".join(pieces), where
+            assert lg["start_offset"] == before, where
+            end = db.last()["offset"]
+            assert lg["end_offset"] == end, where
+            assert bool(lg["flags"] & abi.TAN_SYNC) == syncs, where
+            assert bool(lg["flags"] & abi.TAN_NEW_LOG) == fresh, where
+            if pieces:
+                assert p.eng.tan_get(next(
+                    g for g in range(p.G) if (first + g) % 16 == c), s)[0] \
+                    == end, where
+    return n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("val_len,cmd_cap,val_cap,max_log", [
+    (4, 32, 4, 2048), (1011, 1040, 1024, 1 << 16)])
+def test_tan_multiplexed_matches_oracle(val_len, cmd_cap, val_cap, max_log):
+    """tan_multiplexed (CreateLogMultiplexedTan): 16 logs per slot shared by
+    the shards with the same ShardID % 16, each replica's skip / sync from
+    its own stored State; a round's records of one log back to back in
+    group order at the offsets the oracle's shared db gives them -- block
+    padding, FIRST / MIDDLE / LAST chunks (1 KB payloads in 64 KiB logs)
+    and log switches inside a round (2 KiB logs) included."""
+    kw = dict(cmd_cap=cmd_cap, kv_val_cap=val_cap) if val_len > 4 else {}
+    if val_len > 4:
+        kw.update(kv_slots=64)
+    p = Pair(G=40, R=3, save_cap=8192, max_props=4, save_tan=1,
+             tan_multiplexed=1, tan_max_log=max_log, **kw)
+    dbs = [[po.TanDB(max_log) for _ in range(16)] for _ in range(p.R)]
+    written = 0
+    for r in range(30):
+        k = (0, 1, 3, 0, 2)[r % 5]
+        rkw = dict(val_len=val_len) if val_len > 4 else {}
+        o, e = p.round(k=k, tick=(r % 2 == 0), read_index=(r % 3 == 0),
+                       encode_saves=True, **rkw)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+        n = _mux_round(p, dbs, r)
+        assert e.log_records == n, (r, e.to_dict())
+        written += n
+    assert written > 0
+    assert any(db.last()["log"] > 0 for row in dbs for db in row)

@@ -264,3 +264,21 @@ def test_db_switches_log_at_max_size():
     for lg in range(3):
         recs = po.tan_read(db.file(lg))
         assert len(recs) == logs.count(lg)
+
+
+def test_multiplexed_db_keeps_state_per_node():
+    """A multiplexed log (db_keeper.go:84-123) holds the records of many
+    shards; db.write's skip and sync (db.go:108-114) use each node's own
+    stored State (nodeStates.getState(ShardID, ReplicaID)): the same State
+    from another shard is still written and synced, a repeat from the same
+    node is skipped."""
+    db = po.TanDB()
+    a = db.write(1, 1, (2, 1, 5), [])
+    assert a and a["sync"] and a["off"] == 0
+    b = db.write(17, 1, (2, 1, 5), [])  # same key 1, another shard
+    assert b and b["sync"] and b["off"] == a["off"] + a["len"]
+    assert db.write(1, 1, (2, 1, 5), []) is None
+    c = db.write(17, 1, (2, 1, 6), [])  # commit only: written, no sync
+    assert c and not c["sync"]
+    recs = po.tan_read(db.file(0))
+    assert [r[0] for r in recs] == [0, a["len"], a["len"] + b["len"]]

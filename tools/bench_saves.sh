@@ -7,12 +7,12 @@ o=gpurun_out/${1:-saves}
 mkdir -p "$o"
 export TMPDIR=/tmp
 B="--steps 30 --warmup 5 --no-cpu-baseline --no-wire --host-staged 0"
-for s in none entrybatch tan; do
+for s in none entrybatch tan tanmux; do
   tools/gpu_step.sh 300 "$o/c3_$s.log" python bench.py $B --save $s || exit 1
   tail -1 "$o/c3_$s.log" > "$o/c3_$s.json"
 done
 for p in 128 1024; do
-  for s in entrybatch tan; do
+  for s in entrybatch tan tanmux; do
     tools/gpu_step.sh 400 "$o/c5_${p}_$s.log" python bench.py $B --workload c5 --payload $p --save $s || exit 1
     tail -1 "$o/c5_${p}_$s.log" > "$o/c5_${p}_$s.json"
   done
