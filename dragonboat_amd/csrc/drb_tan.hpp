@@ -524,15 +524,18 @@ __global__ __launch_bounds__(256) void k_tan_select(View v, uint32_t round,
   tan_count_row(v, c, part);
 }
 
-// wave-wide exclusive prefix sum
-__device__ __forceinline__ uint32_t wave_excl(uint32_t x, uint32_t lane) {
-  uint32_t incl = x;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d);
-    if (lane >= d) incl += y;
-  }
-  return incl - x;
+// wave-wide exclusive prefix sum with DPP lane moves (no LDS round trips):
+// row_shr 1, 2, 4, 8 scan each row of 16 lanes, row_bcast 15 / 31 carry
+// the row totals into the rows above
+__device__ __forceinline__ uint32_t wave_excl(uint32_t x, uint32_t) {
+  int v = (int)x;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+  return (uint32_t)v - x;
 }
 
 // One wave per multiplexed log (slot, key): the offsets of the round's
