@@ -817,6 +817,7 @@ orc_cluster *orc_cluster_new(const orc_cluster_cfg *cfg) {
       n->r = raft_new(cfg->first_shard_id + gid, s + 1, cfg->election_rtt,
                       cfg->heartbeat_rtt, (int)cfg->check_quorum, n->db,
                       mix64(cfg->seed ^ (gid * R + s)));
+      n->r->pre_vote = cfg->pre_vote != 0;
       n->hosted = 1;
       /* quiesceState{electionTick: ElectionRTT * 2} (node.go:195-200) */
       n->qs.election_tick = 2ull * cfg->election_rtt;

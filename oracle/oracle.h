@@ -216,6 +216,7 @@ int orc_raft_try_commit(orc_raft *r);
 int orc_raft_tick(orc_raft *r);
 int orc_raft_campaign(orc_raft *r);
 void orc_raft_set_check_quorum(orc_raft *r, int on);
+void orc_raft_set_pre_vote(orc_raft *r, int on);
 void orc_raft_set_randomized_election_timeout(orc_raft *r, uint64_t v);
 int orc_raft_network_reset(orc_raft *r, uint64_t id, const uint64_t *ids,
                            int n);
@@ -351,7 +352,7 @@ typedef struct orc_cluster_cfg {
   uint64_t seed;
   uint64_t logdb_keep; /* 0: keep every saved entry; else compact behind */
   uint32_t quiesce;    /* Config.Quiesce (config.go:195) */
-  uint32_t pad;
+  uint32_t pre_vote;   /* Config.PreVote (config.go:178-183) */
   /* NULL: group g is global group g.  Else group g of this cluster is
    * global group gids[g] (ShardID, seeds): a sample of a large engine's
    * groups, simulated alone (groups are independent) */

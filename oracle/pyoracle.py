@@ -42,7 +42,7 @@ class ClusterCfg(C.Structure):
                 ("num_replicas", C.c_uint32), ("election_rtt", C.c_uint32),
                 ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
                 ("seed", C.c_uint64), ("logdb_keep", C.c_uint64),
-                ("quiesce", C.c_uint32), ("pad", C.c_uint32),
+                ("quiesce", C.c_uint32), ("pre_vote", C.c_uint32),
                 ("gids", C.POINTER(C.c_uint64))]
 
 
@@ -100,6 +100,7 @@ def _declare(L):
         "orc_raft_campaign": (C.c_int, [P]),
         "orc_raft_set_randomized_election_timeout": (None, [P, U64]),
         "orc_raft_set_check_quorum": (None, [P, C.c_int]),
+        "orc_raft_set_pre_vote": (None, [P, C.c_int]),
         "orc_raft_network_reset": (C.c_int, [P, U64, PU64, C.c_int]),
         "orc_raft_read_messages": (C.c_long, [P, PM, C.c_size_t, PE,
                                               C.c_size_t, PU8, C.c_size_t]),
@@ -459,6 +460,9 @@ class TestRaft:
     def set_check_quorum(self, on):
         lib().orc_raft_set_check_quorum(self.p, int(bool(on)))
 
+    def set_pre_vote(self, on):
+        lib().orc_raft_set_pre_vote(self.p, int(bool(on)))
+
     def set_randomized_election_timeout(self, v):
         lib().orc_raft_set_randomized_election_timeout(self.p, v)
 
@@ -633,7 +637,8 @@ class Cluster:
 
     def __init__(self, num_groups, num_replicas=3, election_rtt=10,
                  heartbeat_rtt=1, check_quorum=1, seed=0x5EEDD8B0,
-                 first_shard_id=1, logdb_keep=0, quiesce=0, gids=None):
+                 first_shard_id=1, logdb_keep=0, quiesce=0, gids=None,
+                 pre_vote=0):
         """gids: simulate only these global group ids (group i of the
         cluster is global group gids[i]; None: 0..num_groups-1)."""
         self.gids = None if gids is None else \
@@ -642,7 +647,8 @@ class Cluster:
             num_groups = len(gids)
         cfg = ClusterCfg(num_groups, first_shard_id, num_replicas,
                          election_rtt, heartbeat_rtt, check_quorum, seed,
-                         logdb_keep, int(bool(quiesce)), 0, self.gids)
+                         logdb_keep, int(bool(quiesce)), int(bool(pre_vote)),
+                         self.gids)
         self.cfg = cfg
         self.G = num_groups
         self.R = num_replicas

@@ -1251,6 +1251,39 @@ static void raft_campaign(orc_raft *r) {
   }
 }
 
+/* becomePreVoteCandidate (raft.go:1001-1018) */
+static void raft_become_pre_vote_candidate(orc_raft *r) {
+  if (!r->pre_vote) orc_panic("becomePreVoteCandidate: preVote not enabled");
+  if (r->state == DRB_LEADER)
+    orc_panic("transitioning to candidate state from leader");
+  r->state = DRB_PREVOTE_CANDIDATE;
+  raft_reset(r, r->term, 1);
+  raft_set_leader_id(r, 0);
+}
+
+/* preVoteCampaign (raft.go:1149-1174): RequestPreVote at term + 1, the
+ * term itself unchanged */
+static void raft_pre_vote_campaign(orc_raft *r) {
+  raft_become_pre_vote_candidate(r);
+  raft_handle_vote_resp(r, r->replica_id, 0);
+  if (raft_single_node_quorum(r)) {
+    raft_campaign(r);
+    return;
+  }
+  uint64_t index = log_last(&r->log);
+  uint64_t last_term;
+  if (log_term(&r->log, index, &last_term))
+    orc_panic("preVoteCampaign: log error");
+  for (int i = 0; i < r->nrem; i++) {
+    if (r->rem_id[i] == r->replica_id) continue;
+    orc_msg m = new_msg(DRB_MSG_REQUEST_PREVOTE, r->rem_id[i]);
+    m.term = r->term + 1;
+    m.log_index = index;
+    m.log_term = last_term;
+    raft_send(r, &m);
+  }
+}
+
 /* handleHeartbeatMessage (raft.go:1400-1409) */
 static void raft_handle_heartbeat_message(orc_raft *r, const orc_msg *m) {
   log_commit_to(&r->log, m->commit);
@@ -1519,6 +1552,32 @@ static void handle_node_request_vote(orc_raft *r, const orc_msg *m) {
   raft_send(r, &resp);
 }
 
+/* handleNodeRequestPreVote (raft.go:1670-1695) */
+static void handle_node_request_pre_vote(orc_raft *r, const orc_msg *m) {
+  orc_msg resp = new_msg(DRB_MSG_REQUEST_PREVOTE_RESP, m->from);
+  int utd;
+  if (log_up_to_date(&r->log, m->log_index, m->log_term, &utd))
+    orc_panic("upToDate: log error");
+  if (m->term < r->term) orc_panic("m.term < r.term");
+  if (m->term > r->term && utd) {
+    resp.term = m->term;
+  } else {
+    resp.term = r->term;
+    resp.reject = 1;
+  }
+  raft_send(r, &resp);
+}
+
+/* handlePreVoteCandidateRequestPreVoteResp (raft.go:2259-2276) */
+static void handle_pre_vote_candidate_resp(orc_raft *r, const orc_msg *m) {
+  int count = raft_handle_vote_resp(r, m->from, m->reject);
+  if (count == raft_quorum(r)) {
+    raft_campaign(r);
+  } else if (r->nvotes - count == raft_quorum(r)) {
+    raft_to_follower(r, r->term, 0, 1);
+  }
+}
+
 /* handleCandidateRequestVoteResp (raft.go:2235-2253) */
 static void handle_candidate_vote_resp(orc_raft *r, const orc_msg *m) {
   int count = raft_handle_vote_resp(r, m->from, m->reject);
@@ -1535,6 +1594,10 @@ static void handle_node_election(orc_raft *r) {
   if (r->state != DRB_LEADER) {
     if (!r->test_has_config_change_hook && r->log.committed > r->applied)
       return; /* hasConfigChangeToApply (raft.go:1611-1622) */
+    if (r->pre_vote && !r->is_leader_transfer_target) {
+      raft_pre_vote_campaign(r);
+      return;
+    }
     raft_campaign(r);
   }
 }
@@ -1574,6 +1637,9 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
           return;
         case DRB_MSG_REQUEST_VOTE:
           handle_node_request_vote(r, m);
+          return;
+        case DRB_MSG_REQUEST_PREVOTE:
+          handle_node_request_pre_vote(r, m);
           return;
         case DRB_MSG_LOCAL_TICK:
           if (m->reject)
@@ -1635,6 +1701,9 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
         case DRB_MSG_REQUEST_VOTE:
           handle_node_request_vote(r, m);
           return;
+        case DRB_MSG_REQUEST_PREVOTE:
+          handle_node_request_pre_vote(r, m);
+          return;
         case DRB_MSG_LOCAL_TICK:
           if (m->reject)
             raft_quiesced_tick(r);
@@ -1660,6 +1729,9 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
         case DRB_MSG_REQUEST_VOTE:
           handle_node_request_vote(r, m);
           return;
+        case DRB_MSG_REQUEST_PREVOTE:
+          handle_node_request_pre_vote(r, m);
+          return;
         case DRB_MSG_ELECTION:
           handle_node_election(r);
           return;
@@ -1678,6 +1750,43 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
         default:
           return;
       }
+    case DRB_PREVOTE_CANDIDATE: /* raft.go:2348-2360 */
+      switch (t) {
+        case DRB_MSG_REPLICATE:
+          raft_to_follower(r, r->term, m->from, 1);
+          raft_handle_replicate_message(r, m);
+          return;
+        case DRB_MSG_HEARTBEAT:
+          raft_to_follower(r, r->term, m->from, 1);
+          raft_handle_heartbeat_message(r, m);
+          return;
+        case DRB_MSG_REQUEST_PREVOTE_RESP:
+          handle_pre_vote_candidate_resp(r, m);
+          return;
+        case DRB_MSG_REQUEST_VOTE:
+          handle_node_request_vote(r, m);
+          return;
+        case DRB_MSG_REQUEST_PREVOTE:
+          handle_node_request_pre_vote(r, m);
+          return;
+        case DRB_MSG_ELECTION:
+          handle_node_election(r);
+          return;
+        case DRB_MSG_READ_INDEX:
+          raft_report_dropped_ri(r, m);
+          return;
+        case DRB_MSG_PROPOSE:
+          r->ndropped_entries += m->ents.n;
+          return;
+        case DRB_MSG_LOCAL_TICK:
+          if (m->reject)
+            raft_quiesced_tick(r);
+          else
+            raft_tick(r);
+          return;
+        default:
+          return;
+      }
     default:
       orc_panic("raft state %u not on this path", r->state);
   }
@@ -1685,11 +1794,13 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
 
 /* Handle (raft.go:1596-1609) */
 static int raft_handle(orc_raft *r, orc_msg *m) {
-  if (m->type == DRB_MSG_REQUEST_PREVOTE ||
-      m->type == DRB_MSG_REQUEST_PREVOTE_RESP)
+  const int pv = m->type == DRB_MSG_REQUEST_PREVOTE ||
+                 m->type == DRB_MSG_REQUEST_PREVOTE_RESP;
+  if (pv && !r->pre_vote) /* inconsistentRaftConfig (raft.go:1592-1594) */
     orc_panic("received preVote message when preVote is not enabled");
   if (!raft_term_not_matched(r, m)) {
-    if (m->term != 0 && r->term != m->term) orc_panic("mismatched term found");
+    if (!pv && m->term != 0 && r->term != m->term)
+      orc_panic("mismatched term found");
     raft_dispatch(r, m);
   }
   return 0;
@@ -1955,6 +2066,7 @@ int orc_raft_campaign(orc_raft *r) {
 
 /* the test harness's r.checkQuorum = ... (raft_etcd_test.go) */
 void orc_raft_set_check_quorum(orc_raft *r, int on) { r->check_quorum = on; }
+void orc_raft_set_pre_vote(orc_raft *r, int on) { r->pre_vote = on; }
 
 void orc_raft_set_randomized_election_timeout(orc_raft *r, uint64_t v) {
   r->randomized_election_timeout = v;

@@ -585,3 +585,78 @@ def test_leader_stepdown_check_quorum(active):
                          term=r.info().term))
         r.tick()
     assert r.info().role == (LEADER if active else FOLLOWER)
+
+
+# ------------------------------------------------------------ PreVote
+PREVOTE_CANDIDATE = 2
+
+
+def test_become_pre_vote_candidate():
+    # raft_test.go:269-287 (TestBecomePreVoteCandidate)
+    r = po.TestRaft(1, [1, 2, 3], 10, 1)
+    r.set_pre_vote(True)
+    r.become_follower(2, 3)
+    r.handle(msg(MSG["Election"], from_=1, to=1))
+    st = r.info()
+    assert st.term == 2 and st.role == PREVOTE_CANDIDATE
+    assert st.leader_id == 0
+    msgs = sorted(r.read_messages(), key=lambda m: m["to"])
+    assert [(m["to"], m["term"], m["type"]) for m in msgs] == [
+        (2, 3, MSG["RequestPreVote"]), (3, 3, MSG["RequestPreVote"])]
+
+
+def test_no_op_sent_on_small_term_rejected_request_pre_vote():
+    # raft_test.go:1420-1432
+    r = po.TestRaft(1, [1, 2], 5, 1)
+    r.set_pre_vote(True)
+    r.become_follower(10, 2)
+    r.handle(msg(MSG["RequestPreVote"], from_=2, to=1, term=9))
+    msgs = r.read_messages()
+    assert [(m["type"], m["to"], m["from_"], m["term"]) for m in msgs] == [
+        (MSG["NoOP"], 2, 1, 10)]
+
+
+def test_pre_vote_resp_with_higher_term():
+    # raft_test.go:1434-1446
+    r = po.TestRaft(1, [1, 2], 5, 1)
+    r.set_pre_vote(True)
+    r.become_follower(10, 2)
+    r.handle(msg(MSG["RequestPreVoteResp"], from_=2, to=1, term=11))
+    assert r.info().term == 10
+    r.handle(msg(MSG["RequestPreVoteResp"], from_=2, to=1, term=20,
+                 reject=True))
+    assert r.info().term == 20
+
+
+def test_election_with_pre_vote():
+    # raft_test.go:3278-3296 (TestElectionWithPreVote)
+    peers = [po.TestRaft(i, [1, 2, 3], 10, 1) for i in (1, 2, 3)]
+    for p in peers:
+        p.set_pre_vote(True)
+    nt = po.Network(*peers)
+    nt.send(msg(MSG["Election"], from_=1, to=1))
+    assert [p.info().role for p in peers] == [LEADER, FOLLOWER, FOLLOWER]
+    assert peers[0].info().term == 1  # one campaign after the PreVote round
+
+
+@pytest.mark.parametrize("utd,higher,reject", [
+    (True, True, False), (False, True, True), (True, False, True)])
+def test_handle_node_request_pre_vote(utd, higher, reject):
+    # handleNodeRequestPreVote (raft.go:1670-1695): granted at m.Term only
+    # for a higher term and an up-to-date log, else rejected at r.term
+    r = po.TestRaft(1, [1, 2, 3], 10, 1)
+    r.set_pre_vote(True)
+    r.become_follower(5, 3)
+    # the follower's log: one entry at term 5
+    r.handle(msg(REPLICATE, from_=3, to=1, term=5,
+                 entries=[ent(term=5, index=1)]))
+    r.read_messages()
+    t = 6 if higher else 5
+    r.handle(msg(MSG["RequestPreVote"], from_=2, to=1, term=t, log_index=1,
+                 log_term=5 if utd else 4))
+    msgs = r.read_messages()
+    assert len(msgs) == 1
+    m = msgs[0]
+    assert m["type"] == MSG["RequestPreVoteResp"] and bool(m["reject"]) == reject
+    assert m["term"] == (t if not reject else 5)
+    assert r.info().term == 5  # a PreVote never changes the term
