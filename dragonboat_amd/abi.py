@@ -132,7 +132,7 @@ class Config(C.Structure):
                 ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
                 ("save_batched", C.c_uint32), ("save_tan", C.c_uint32),
                 ("elections", C.c_uint32), ("tan_max_log", C.c_uint64),
-                ("tan_multiplexed", C.c_uint32), ("tan_pad", C.c_uint32)]
+                ("tan_multiplexed", C.c_uint32), ("pre_vote", C.c_uint32)]
 
 
 class ApplyResult(C.Structure):

@@ -200,6 +200,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     return DRB_EINVAL;
   if (cfg->save_tan && (cfg->save_cap == 0 || cfg->save_batched))
     return DRB_EINVAL;
+  // PreVote runs in the raft launch
+  if (cfg->pre_vote && !cfg->elections) return DRB_EINVAL;
   // the multiplexed tan: a tan option, ShardIDs of this rank's groups
   if (cfg->tan_multiplexed && (!cfg->save_tan || cfg->place_world > 1))
     return DRB_EINVAL;
@@ -373,6 +375,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &e->tan_total, 4);
   }
   v.elections = cfg->elections ? 1u : 0u;
+  v.pre_vote = cfg->pre_vote ? 1u : 0u;
   if (v.elections) {
     // the raft launch's workgroups own counter rows 0.. (block_counters):
     // at most 2 per group block

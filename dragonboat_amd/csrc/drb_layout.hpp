@@ -332,6 +332,7 @@ struct View {
   unsigned long long *tan_ctr;  // [blocks][4] bytes, records, syncs, logs
   // multiplexed tan (CreateLogMultiplexedTan): 16 logs per replica slot,
   // key = ShardID % 16 (db_keeper.go:84-123), records in group order
+  uint32_t pre_vote;      // Config.PreVote (elections)
   uint32_t tan_mux;
   uint32_t tanm_J;        // records per log row: >= ceil(G / 16), 256 | J
   uint32_t *tanm_len;     // [R][16][J] payload bytes | sync << 31, 0: none

@@ -128,6 +128,11 @@ __host__ __device__ inline uint64_t q_hi(uint4 q) {
   return (uint64_t)q.z | ((uint64_t)q.w << 32);
 }
 
+// PreVote messages carry a term of their own (r.term + 1, or the one a
+// pre-vote is granted at), not the sender's
+__host__ __device__ inline bool is_prevote_type(uint32_t t) {
+  return t == DRB_MSG_REQUEST_PREVOTE || t == DRB_MSG_REQUEST_PREVOTE_RESP;
+}
 __host__ __device__ inline bool is_request_type(uint32_t t) {
   return t == DRB_MSG_PROPOSE || t == DRB_MSG_READ_INDEX ||
          t == DRB_MSG_LEADER_TRANSFER;
@@ -231,12 +236,14 @@ __host__ __device__ inline bool msg_encode(const Msg &m, uint32_t dest,
       has = !dedup;
       break;
     case DRB_MSG_REQUEST_VOTE:
+    case DRB_MSG_REQUEST_PREVOTE:
       a = m.log_index;
       b = m.log_term;
       c = m.hint;
       has = true;
       break;
     case DRB_MSG_REQUEST_VOTE_RESP:
+    case DRB_MSG_REQUEST_PREVOTE_RESP:
     case DRB_MSG_NOOP:
       break;
     default:
@@ -308,11 +315,13 @@ __host__ __device__ inline Msg msg_decode(uint4 c0, uint4 c1,
       m.hint_high = c;
       break;
     case DRB_MSG_REQUEST_VOTE:
+    case DRB_MSG_REQUEST_PREVOTE:
       m.log_index = a;
       m.log_term = b;
       m.hint = c;
       break;
     case DRB_MSG_REQUEST_VOTE_RESP:
+    case DRB_MSG_REQUEST_PREVOTE_RESP:
     case DRB_MSG_NOOP:
       break;
     default:

@@ -119,6 +119,7 @@ struct Rep {
   uint32_t ndropped_ri;
   uint64_t guard_new;
   bool leader_update;
+  bool oterm;  // raft launch: a record went out with a term not r.term
   bool err;
   // node.qs (Quiesce on, EXT instantiation): quiesce.go:23-33
   uint64_t qs_tick, qs_idle, qs_since, qs_exit;
@@ -361,7 +362,10 @@ DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   const uint32_t k = rep ? mi_nrep(w) : rec_pos(false, mi_noth(w), v.MB);
   r.nmsgs++;
   Msg mm = m;
-  mm.term = is_request_type(m.type) ? 0 : r.term;
+  mm.term = is_request_type(m.type) ? 0
+            : is_prevote_type(m.type) ? m.term
+                                      : r.term;
+  if (mm.term != r.term && mm.term != 0) r.oterm = true;
   uint4 c0, c1;
   const bool has = msg_encode(mm, to_slot, &r.hc, c0, c1);
   const uint32_t inf = msg_info(mm.type, mm.term == 0, m.reject != 0);
@@ -1024,13 +1028,40 @@ DRB_DEV void el_campaign(const Lane &L, Rep<R> &r) {
     if ((uint32_t)s != L.slot) emit(L, r, (uint32_t)s, m);
 }
 
+// preVoteCampaign (raft.go:1149-1174) after becomePreVoteCandidate
+// (raft.go:1001-1018): RequestPreVote at term + 1, the term unchanged
+template <int R>
+DRB_DEV void el_pre_vote_campaign(const Lane &L, Rep<R> &r) {
+  r.role = DRB_PREVOTE_CANDIDATE;
+  el_reset(L, r, r.term, true);
+  set_leader(r, 0);
+  r.leader_update = true;
+  el_vote_resp(r, L.slot, false);
+  if (R == 1) {  // a single-node quorum
+    el_campaign(L, r);
+    return;
+  }
+  Msg m = {};
+  m.type = DRB_MSG_REQUEST_PREVOTE;
+  m.term = r.term + 1;
+  m.log_index = r.last;
+  m.log_term = log_term(L, r, r.last);
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if ((uint32_t)s != L.slot) emit(L, r, (uint32_t)s, m);
+}
+
 // handleNodeElection (raft.go:1632-1668): not while a config change may be
-// waiting to be applied (hasConfigChangeToApply, raft.go:1611-1622)
+// waiting to be applied (hasConfigChangeToApply, raft.go:1611-1622); with
+// PreVote the pre-vote round first (no leader transfer on this path)
 template <int R>
 DRB_DEV void el_election(const Lane &L, Rep<R> &r) {
   if (r.role == DRB_LEADER) return;
   if (r.committed > ld_f(L, r, F_APPLIED)) return;
-  el_campaign(L, r);
+  if (L.v->pre_vote)
+    el_pre_vote_campaign(L, r);
+  else
+    el_campaign(L, r);
 }
 
 // upToDate (logentry.go:381-393)
@@ -1055,6 +1086,34 @@ DRB_DEV void el_request_vote(const Lane &L, Rep<R> &r, int s, const Msg &m) {
     resp.reject = 1;
   }
   emit(L, r, (uint32_t)s, resp);
+}
+
+// handleNodeRequestPreVote (raft.go:1670-1695): granted at the asked term
+// for an up-to-date log, else rejected at r.term
+template <int R>
+DRB_DEV void el_request_pre_vote(const Lane &L, Rep<R> &r, int s,
+                                 const Msg &m) {
+  Msg resp = {};
+  resp.type = DRB_MSG_REQUEST_PREVOTE_RESP;
+  if (m.term > r.term && el_up_to_date(L, r, m.log_index, m.log_term)) {
+    resp.term = m.term;
+  } else {
+    resp.term = r.term;
+    resp.reject = 1;
+  }
+  emit(L, r, (uint32_t)s, resp);
+}
+
+// handlePreVoteCandidateRequestPreVoteResp (raft.go:2259-2276)
+template <int R>
+DRB_DEV void el_pre_vote_resp(const Lane &L, Rep<R> &r, int s, const Msg &m) {
+  constexpr uint32_t quorum = R / 2 + 1;
+  const uint32_t granted = el_vote_resp(r, (uint32_t)s, m.reject != 0);
+  const uint32_t answered = __builtin_popcount(r.votes & 0xffu);
+  if (granted == quorum)
+    el_campaign(L, r);
+  else if (answered - granted == quorum)
+    el_become_follower(L, r, r.term, 0, true);
 }
 
 // handleCandidateRequestVoteResp (raft.go:2235-2253)
@@ -1085,17 +1144,22 @@ template <int R>
 DRB_DEV bool el_term_gate(const Lane &L, Rep<R> &r, int s, const Msg &m) {
   const View &v = *L.v;
   if (m.term == 0 || m.term == r.term) return false;
-  if (m.type == DRB_MSG_REQUEST_VOTE && v.check_quorum && m.term > r.term &&
-      m.hint != (uint64_t)s + 1 && r.leader_id != 0 &&
-      r.election_tick < v.election_rtt)
+  if ((m.type == DRB_MSG_REQUEST_VOTE || m.type == DRB_MSG_REQUEST_PREVOTE) &&
+      v.check_quorum && m.term > r.term && m.hint != (uint64_t)s + 1 &&
+      r.leader_id != 0 && r.election_tick < v.election_rtt)
     return true;
   if (m.term > r.term) {
+    // isPreVoteMessageWithExpectedHigherTerm (raft.go:1531-1534)
+    if (m.type == DRB_MSG_REQUEST_PREVOTE ||
+        (m.type == DRB_MSG_REQUEST_PREVOTE_RESP && !m.reject))
+      return false;
     const uint64_t leader = el_leader_message(m.type) ? (uint64_t)s + 1 : 0;
     el_become_follower(L, r, m.term, leader,
                        m.type != DRB_MSG_REQUEST_VOTE);  // ...KE keeps ticks
     return false;
   }
-  if (el_leader_message(m.type) && v.check_quorum) {
+  if (m.type == DRB_MSG_REQUEST_PREVOTE ||
+      (el_leader_message(m.type) && (v.check_quorum || v.pre_vote))) {
     Msg resp = {};
     resp.type = DRB_MSG_NOOP;
     emit(L, r, (uint32_t)s, resp);
@@ -1109,25 +1173,31 @@ DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
                          const EntSrc &src) {
   if (el_term_gate(L, r, s, m)) return;
   const uint32_t t = m.type;
+  if (t == DRB_MSG_REQUEST_PREVOTE) {  // any state (raft.go:2342-2413)
+    el_request_pre_vote(L, r, s, m);
+    return;
+  }
   if (r.role == DRB_LEADER) {
     if (t == DRB_MSG_REQUEST_VOTE)
       el_request_vote(L, r, s, m);
-    else
+    else if (t != DRB_MSG_REQUEST_PREVOTE_RESP)
       dispatch(L, r, s, m, src);
   } else if (r.role == DRB_FOLLOWER) {
     if (t == DRB_MSG_REQUEST_VOTE)
       el_request_vote(L, r, s, m);
     else if (t == DRB_MSG_READ_INDEX)  // handleFollowerReadIndex
       follower_read_index(L, r, m.hint, m.hint_high);
-    else
+    else if (t != DRB_MSG_REQUEST_PREVOTE_RESP)
       dispatch(L, r, s, m, src);
-  } else {  // candidate
+  } else {  // candidate, preVoteCandidate
     if (t == DRB_MSG_REPLICATE || t == DRB_MSG_HEARTBEAT) {
       // handleCandidateReplicate / Heartbeat (raft.go:2205-2233)
       el_become_follower(L, r, r.term, (uint64_t)s + 1, true);
       dispatch(L, r, s, m, src);
     } else if (t == DRB_MSG_REQUEST_VOTE_RESP) {
-      el_candidate_vote_resp(L, r, s, m);
+      if (r.role == DRB_CANDIDATE) el_candidate_vote_resp(L, r, s, m);
+    } else if (t == DRB_MSG_REQUEST_PREVOTE_RESP) {
+      if (r.role == DRB_PREVOTE_CANDIDATE) el_pre_vote_resp(L, r, s, m);
     } else if (t == DRB_MSG_REQUEST_VOTE) {
       el_request_vote(L, r, s, m);
     } else if (t == DRB_MSG_READ_INDEX) {  // handleCandidateReadIndex
@@ -2087,6 +2157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     r.ndropped_ri = 0;
     r.guard_new = ~0ull;
     r.leader_update = false;
+    r.oterm = false;
     r.err = false;
     r.qs_new = false;
     const uint32_t flags0 = r.flags, fb0 = r.fb;
@@ -2108,7 +2179,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     uint32_t fb = DRB_FB_NONE;
     const bool is_leader = SLOW ? r.role == DRB_LEADER : LEAD;
     if (SLOW) {
-      if (role != DRB_LEADER && role != DRB_FOLLOWER && role != DRB_CANDIDATE)
+      if (role != DRB_LEADER && role != DRB_FOLLOWER && role != DRB_CANDIDATE &&
+          role != DRB_PREVOTE_CANDIDATE)
         fb = DRB_FB_ROLE;
     } else if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) {
       fb = DRB_FB_ROLE;
@@ -2147,7 +2219,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
                 t == DRB_MSG_HEARTBEAT || t == DRB_MSG_HEARTBEAT_RESP ||
                 t == DRB_MSG_READ_INDEX || t == DRB_MSG_READ_INDEX_RESP ||
                 t == DRB_MSG_REQUEST_VOTE || t == DRB_MSG_REQUEST_VOTE_RESP ||
-                t == DRB_MSG_NOOP;
+                t == DRB_MSG_NOOP ||
+                (v.pre_vote && is_prevote_type(t));
             if (!ok && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
           }
         }
@@ -2157,7 +2230,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           const uint32_t nrp = mi_nrep(info);
           for (uint32_t j = 0; j < ns; ++j) {
             const uint32_t k = rec_pos(j < nrp, j < nrp ? j : j - nrp, v.MB);
-            if ((mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)].x & MF_TERM_OTHER) &&
+            const uint32_t x = mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)].x;
+            // (a RequestPreVote or a granted pre-vote raises no term,
+            // isPreVoteMessageWithExpectedHigherTerm, raft.go:1531-1534)
+            const bool pv = (x & 0xffu) == DRB_MSG_REQUEST_PREVOTE ||
+                            ((x & 0xffu) == DRB_MSG_REQUEST_PREVOTE_RESP &&
+                             !(x & MF_REJECT));
+            if ((x & MF_TERM_OTHER) && !pv &&
                 v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)] > r.term)
               higher_in = true;
           }
@@ -2685,7 +2764,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
     for (int s = 0; s < R; ++s) {
       uint32_t w = oinfo[s * 256 + threadIdx.x];
       const bool qz = (qz_out >> s) & 1u;
-      if (SLOW && r.term != term0 && mi_count(w)) {
+      if (SLOW && (r.term != term0 || r.oterm) && mi_count(w)) {
         // the records sent before the term changed keep theirs (rterm)
         const uint32_t nrp = mi_nrep(w), nt = mi_count(w);
         for (uint32_t j = 0; j < nt; ++j) {

@@ -146,7 +146,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
-                tan_multiplexed=0)
+                tan_multiplexed=0, pre_vote=0)
 
 
 class Engine:
@@ -167,7 +167,7 @@ class Engine:
                    cfg["flagged_cap"], cfg["quiesce"],
                    cfg["durable_log"], cfg["save_batched"],
                    cfg["save_tan"], cfg["elections"], cfg["tan_max_log"],
-                   cfg["tan_multiplexed"], 0)
+                   cfg["tan_multiplexed"], cfg["pre_vote"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")

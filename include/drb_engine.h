@@ -349,7 +349,11 @@ typedef struct drb_config {
    * back to back in that log's staging (drb_export_tan_log).  place_world
    * 1 only. */
   uint32_t tan_multiplexed;
-  uint32_t tan_pad;
+  /* with elections, 1: Config.PreVote (config.go): a timed-out replica
+   * first asks for pre-votes at term + 1 without changing its term
+   * (preVoteCampaign, raft.go:1149-1174; handleNodeRequestPreVote,
+   * :1670-1695; the preVoteCandidate handlers, :2256-2276) */
+  uint32_t pre_vote;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */

@@ -1153,6 +1153,13 @@ int orc_cluster_tan_write(orc_cluster *c, uint64_t g, uint32_t slot,
   return rc;
 }
 
+/* Config.PreVote of every replica (set after setup_steady's election) */
+void orc_cluster_set_pre_vote(orc_cluster *c, int on) {
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++)
+    for (uint32_t s = 0; s < c->cfg.num_replicas; s++)
+      node_at(c, g, s)->r->pre_vote = on;
+}
+
 int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
                            int hosted) {
   node_at(c, g, slot)->hosted = hosted;

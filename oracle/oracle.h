@@ -397,6 +397,7 @@ long orc_cluster_export_saved(orc_cluster *c, uint64_t g, uint32_t slot,
                               uint8_t *buf, size_t cap, uint32_t *crc);
 int orc_cluster_tan_write(orc_cluster *c, uint64_t g, uint32_t slot,
                           orc_tandb *db, int *sync);
+void orc_cluster_set_pre_vote(orc_cluster *c, int on);
 int orc_cluster_set_hosted(orc_cluster *c, uint64_t g, uint32_t slot,
                            int hosted);
 /* make an engine-importable image of replica (g,slot) */

@@ -201,6 +201,7 @@ def _declare(L):
                                                 C.POINTER(ReadyToRead),
                                                 C.c_size_t]),
         "orc_cluster_set_hosted": (C.c_int, [P, U64, U32, C.c_int]),
+        "orc_cluster_set_pre_vote": (None, [P, C.c_int]),
         "orc_cluster_export_saved": (C.c_long, [P, U64, U32, PU8,
                                                 C.c_size_t, PU32]),
         "orc_cluster_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32,
@@ -766,6 +767,9 @@ class Cluster:
 
     def set_hosted(self, g, slot, hosted):
         lib().orc_cluster_set_hosted(self.p, g, slot, int(bool(hosted)))
+
+    def set_pre_vote(self, on):
+        lib().orc_cluster_set_pre_vote(self.p, int(bool(on)))
 
 
 # ---------------------------------------------------------------- codecs

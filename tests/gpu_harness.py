@@ -69,6 +69,8 @@ class Pair:
         self.orc = po.Cluster(G, R, seed=seed, election_rtt=election_rtt,
                               quiesce=quiesce)
         self.orc.setup_steady(leader_slot)
+        if engine_kw.get("pre_vote"):
+            self.orc.set_pre_vote(True)
         self.eng.init_steady(term=2, leader_slot=leader_slot, seed=seed)
         self.rounds = 0
         self.cpu = set()  # groups handed to the CPU path (the oracle)

@@ -55,15 +55,15 @@ def _roles(p, g):
     return [(st.role, st.term) for st in p.eng.export_replicas(g, 1)]
 
 
-@pytest.mark.parametrize("R", [3, 5])
-def test_leader_loss_elects_on_gpu(R):
+@pytest.mark.parametrize("R,pre_vote", [(3, 0), (5, 0), (3, 1), (5, 1)])
+def test_leader_loss_elects_on_gpu(R, pre_vote):
     """The leader replica of some groups stops (unhosted): its followers
     time out, campaign at term 3, vote, and a new leader takes over --
     appending its term-start no-op and replicating -- all on the GPU,
     bit-exact with the oracle every round.  The old leader then returns at
     term 2: the new leader's heartbeats make it answer with NoOP or step
     down to follower at term 3 (raft.go:1540-1590)."""
-    p = Pair(G=24, R=R, elections=1)
+    p = Pair(G=24, R=R, elections=1, pre_vote=pre_vote)
     st = {"slow": 0, "roles": 0}
     _rounds(p, 3, st)
     E = [1, 6, 11, 20]
@@ -88,12 +88,15 @@ def test_leader_loss_elects_on_gpu(R):
     _rounds(p, 6, st)
 
 
-def test_check_quorum_step_down_and_reelection():
+@pytest.mark.parametrize("pre_vote", [0, 1])
+def test_check_quorum_step_down_and_reelection(pre_vote):
     """A leader whose followers stopped answering loses quorum at the
     CheckQuorum tick and steps down (becomeFollower at its term); when the
     followers return the group elects again -- possibly several rounds of
-    split or rejected votes -- and settles with one leader."""
-    p = Pair(G=16, R=3, elections=1)
+    split or rejected votes, with PreVote a pre-vote round before each
+    campaign (RequestPreVote at term + 1, the term unchanged until a
+    quorum granted it) -- and settles with one leader."""
+    p = Pair(G=16, R=3, elections=1, pre_vote=pre_vote)
     st = {"slow": 0, "roles": 0}
     _rounds(p, 2, st)
     E = [3, 9]
