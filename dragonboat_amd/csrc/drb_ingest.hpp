@@ -244,6 +244,7 @@ __global__ void k_ing_frames(const uint64_t *mbase, uint32_t nf,
 // DeploymentId / BinVer): its entry count for the decode's scan, and the
 // drb_wire_in tallies (ctr[2] snapshots, [3] messages, [4] filtered,
 // [5] entries), one atomic per wave and counter
+constexpr uint32_t ING_TALLY_ROWS = 64;
 __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
                             const uint32_t *err, const uint32_t *n_ent,
                             uint32_t *nsc, uint8_t *deliver, uint64_t n,
@@ -266,12 +267,21 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
   const uint64_t b0 = __ballot(snap), b1 = __ballot(msg), b2 = __ballot(filt);
   uint32_t e = dl ? ne : 0u;
   for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o);
+  // per workgroup, then one of ING_TALLY_ROWS counter rows (64 B apart):
+  // ~25k workgroups adding to one line serialised at its L2 channel
+  __shared__ unsigned long long part[4];
+  if (threadIdx.x < 4) part[threadIdx.x] = 0;
+  __syncthreads();
   if ((threadIdx.x & 63) == 0) {
-    if (b0) atomicAdd(&ctr[2], (unsigned long long)__popcll(b0));
-    if (b1) atomicAdd(&ctr[3], (unsigned long long)__popcll(b1));
-    if (b2) atomicAdd(&ctr[4], (unsigned long long)__popcll(b2));
-    if (e) atomicAdd(&ctr[5], (unsigned long long)e);
+    if (b0) atomicAdd(&part[0], (unsigned long long)__popcll(b0));
+    if (b1) atomicAdd(&part[1], (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(&part[2], (unsigned long long)__popcll(b2));
+    if (e) atomicAdd(&part[3], (unsigned long long)e);
   }
+  __syncthreads();
+  if (threadIdx.x < 4 && part[threadIdx.x])
+    atomicAdd(&ctr[(blockIdx.x % ING_TALLY_ROWS) * 8 + 2 + threadIdx.x],
+              part[threadIdx.x]);
 }
 
 // pass 2: the records and entries of the messages to deliver
@@ -427,8 +437,10 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
   if (mi_count(cur.y) || (cur.x & MQ_QUIESCE))  // this sender's tag byte
     ((uint8_t *)&v.inbox_tag[((uint64_t)buf * v.R + to) * v.G + g])[from] =
         tag_byte(tag, cur.y);
-  if (acc) atomicAdd(&ctr[0], (unsigned long long)acc);
-  if (drop) atomicAdd(&ctr[1], (unsigned long long)drop);
+  // (a lane per plane: the adds spread over the counter rows)
+  unsigned long long *row = ctr + (blockIdx.x % ING_TALLY_ROWS) * 8;
+  if (acc) atomicAdd(&row[0], (unsigned long long)acc);
+  if (drop) atomicAdd(&row[1], (unsigned long long)drop);
 }
 
 }  // namespace drb
@@ -735,7 +747,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   const size_t mb = al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) +
                     al256(m1 * 4) * 6 + al256(m1) +
                     al256((nf + 1) * 4) + al256((nf + 1) * 8) +
-                    al256(nf + 1) + 256;
+                    al256(nf + 1) + ING_TALLY_ROWS * 64;
   if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
   uint8_t *q = (uint8_t *)st.misc.p;
   auto take = [&](size_t b) {
@@ -757,7 +769,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint32_t *d_fbad = (uint32_t *)take((nf + 1) * 4);
   uint64_t *d_mbase = (uint64_t *)take((nf + 1) * 8);
   uint8_t *d_fstate = take(nf + 1);
-  unsigned long long *d_ctr = (unsigned long long *)take(64);
+  unsigned long long *d_ctr =
+      (unsigned long long *)take(ING_TALLY_ROWS * 8 * 8);
   if (!e->crc_tab_ready) {
     uint32_t tab[8][256];
     for (uint32_t a = 0; a < 256; ++a) tab[0][a] = wirehost::crc_tab[a];
@@ -778,7 +791,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemsetAsync(d_fbad, 0, (fr.size() + 1) * 4, sm));
-  HIPCHK(hipMemsetAsync(d_ctr, 0, 64, sm));
+  HIPCHK(hipMemsetAsync(d_ctr, 0, ING_TALLY_ROWS * 8 * 8, sm));
   const uint32_t cmd_cap = v.C16 * 16;
   if (nm) {
     for (size_t f = 0; f < nf; ++f) {
@@ -859,9 +872,12 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     void *tmp = sp + 4 * al256(nm * 4);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_nsc, d_ent0, (int)nm,
                                             sm));
-    unsigned long long c0[6];
-    HIPCHK(hipMemcpyAsync(c0, d_ctr, sizeof(c0), hipMemcpyDeviceToHost, sm));
+    unsigned long long rows[ING_TALLY_ROWS * 8], c0[6] = {0, 0, 0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(rows, d_ctr, sizeof(rows), hipMemcpyDeviceToHost,
+                          sm));
     HIPCHK(hipStreamSynchronize(sm));
+    for (uint32_t q = 0; q < ING_TALLY_ROWS; ++q)
+      for (int k = 2; k < 6; ++k) c0[k] += rows[q * 8 + k];
     res.snapshots += c0[2];
     res.messages = c0[3];
     res.dropped += c0[4];
@@ -890,11 +906,13 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
           v, ds, dm, de, kout, vout, nm, (uint32_t)(e->round & 1),
           (uint32_t)e->round, d_ctr);
       HIPCHK(hipGetLastError());
-      unsigned long long ctr[2];
-      HIPCHK(hipMemcpyAsync(ctr, d_ctr, 16, hipMemcpyDeviceToHost, sm));
+      HIPCHK(hipMemcpyAsync(rows, d_ctr, sizeof(rows), hipMemcpyDeviceToHost,
+                            sm));
       HIPCHK(hipStreamSynchronize(sm));
-      res.accepted = ctr[0];
-      res.dropped += ctr[1];
+      for (uint32_t q = 0; q < ING_TALLY_ROWS; ++q) {
+        res.accepted += rows[q * 8];
+        res.dropped += rows[q * 8 + 1];
+      }
     }
   }
   tr.mark("place");
