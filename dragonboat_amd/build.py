@@ -2,25 +2,66 @@
 
 hipcc cross-compiles for gfx950 without a GPU; the .so is built in-tree so
 it travels to the GPU box with the repository snapshot.
+
+The step kernel has 40 instantiations (R = 1..8 replicas per group x five
+kinds, drb_launch.hpp).  Each is its own translation unit
+(drb_step_inst.hip compiled with -DDRB_INST_R / -DDRB_INST_KIND), so the
+objects build in parallel and only the ones whose sources changed rebuild;
+the engine's host code and auxiliary kernels are drb_engine.hip.
 """
+import hashlib
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libdrb_engine.so")
-SOURCES = ["drb_engine.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
+         "-Wno-pass-failed"]
+NUM_KINDS = 5
+# the headers a step-kernel instantiation includes
+STEP_DEPS = ["drb_step_inst.hip", "drb_step.hpp", "drb_launch.hpp",
+             "drb_layout.hpp", "drb_msg.hpp", "drb_codec.hpp"]
+
+
+def _inc():
+    return os.path.join(os.path.dirname(HERE), "include", "drb_engine.h")
 
 
 def _deps():
     """Every source and header the engine includes (all of csrc/)."""
-    inc = os.path.join(os.path.dirname(HERE), "include", "drb_engine.h")
     return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))
-            if f.endswith((".hip", ".hpp"))] + [inc]
+            if f.endswith((".hip", ".hpp"))] + [_inc()]
+
+
+def _units(defines):
+    """(object name, source, extra defines, dependencies) of every TU."""
+    step_deps = [os.path.join(CSRC, f) for f in STEP_DEPS] + [_inc()]
+    tan_deps = step_deps + [os.path.join(CSRC, f)
+                            for f in ("drb_tan_inst.hip", "drb_tan.hpp")]
+    units = [("drb_engine.o", "drb_engine.hip", [], _deps()),
+             ("tan_write.o", "drb_tan_inst.hip", ["DRB_TAN_KERNELS=2"],
+              tan_deps),
+             ("tan_select.o", "drb_tan_inst.hip", ["DRB_TAN_KERNELS=1"],
+              tan_deps)]
+    for r in range(1, 9):
+        for k in range(NUM_KINDS):
+            units.append(("step_r%d_k%d.o" % (r, k), "drb_step_inst.hip",
+                          ["DRB_INST_R=%d" % r, "DRB_INST_KIND=%d" % k],
+                          step_deps))
+    return units
+
+
+def _stale(obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
 
 
 def up_to_date():
@@ -30,28 +71,50 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in _deps())
 
 
-def build(force=False, verbose=False, out=None, defines=()):
-    """Builds the engine; `out`/`defines` build a tuning variant elsewhere."""
-    if out is not None:
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
-               "-shared", "-Wno-pass-failed", "-o", out] + \
-            ["-D" + d for d in defines] + \
-            [os.path.join(CSRC, f) for f in SOURCES]
-        subprocess.check_call(cmd)
-        return out
-    if not force and up_to_date():
-        return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
-           "-shared", "-Wno-pass-failed", "-o", tmp] + \
-        [os.path.join(CSRC, f) for f in SOURCES]
+def _compile(args):
+    obj, src, defs, verbose = args
+    tmp = obj + ".tmp"
+    cmd = [HIPCC] + FLAGS + ["-c", "-o", tmp] + ["-D" + d for d in defs] + \
+        [os.path.join(CSRC, src)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, obj)
+    return obj
+
+
+def build(force=False, verbose=False, out=None, defines=(), jobs=None):
+    """Builds the engine; `out`/`defines` build a tuning variant elsewhere
+    (its objects live in a directory of their own, keyed by the defines)."""
+    target = LIB if out is None else out
+    if out is None and not force and up_to_date():
+        return LIB
+    key = hashlib.sha1(" ".join(sorted(defines)).encode()).hexdigest()[:10]
+    objdir = os.path.join(LIBDIR, "obj" if not defines else "obj_" + key)
+    os.makedirs(objdir, exist_ok=True)
+    todo, objs = [], []
+    for name, src, defs, deps in _units(defines):
+        obj = os.path.join(objdir, name)
+        objs.append(obj)
+        if force or _stale(obj, deps):
+            todo.append((obj, src, list(defines) + defs, verbose))
+    jobs = jobs or int(os.environ.get("DRB_BUILD_JOBS", 0)) or \
+        max(1, min(16, os.cpu_count() or 1))
+    # the longest translation units first
+    first = ("tan_write.o", "tan_select.o", "drb_engine.o")
+    todo.sort(key=lambda t: (not t[0].endswith(first), t[0]))
+    if todo:
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(_compile, todo))
+    tmp = target + ".tmp"
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", tmp] + \
+        objs
+    if verbose:
+        print(" ".join(cmd[:6]) + " <%d objects>" % len(objs), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

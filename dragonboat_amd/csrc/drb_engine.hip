@@ -17,6 +17,7 @@
 #include "drb_layout.hpp"
 #include "drb_msg.hpp"
 #include "drb_step.hpp"
+#include "drb_launch.hpp"
 
 using namespace drb;
 
@@ -1534,24 +1535,15 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   pl.nrows = nl;
   pf.nrows = nf;
   // one-dimensional grids, rows interleaved per XCD (block_pos)
-  if (nl) {
-    if (ext)
-      step_kernel<R, true, true><<<gx * nl, 256, 0, e->stream>>>(e->v, pl);
-    else
-      step_kernel<R, true, false><<<gx * nl, 256, 0, e->stream>>>(e->v, pl);
-  }
+  const StepLaunchFn *launch = kStepLaunch[R - 1];
+  if (nl) launch[ext ? SK_LEAD_EXT : SK_LEAD](e->v, pl, gx * nl, e->stream);
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
     k_serve_reads<<<dim3(gx, nl), 256, 0, e->stream2>>>(
         e->v, p0.n_reads, p0.key_space, pl.slots);
   }
-  if (nf) {
-    if (ext)
-      step_kernel<R, false, true><<<gx * nf, 256, 0, sf>>>(e->v, pf);
-    else
-      step_kernel<R, false, false><<<gx * nf, 256, 0, sf>>>(e->v, pf);
-  }
+  if (nf) launch[ext ? SK_FOLLOW_EXT : SK_FOLLOW](e->v, pf, gx * nf, sf);
   if (split) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
@@ -1564,8 +1556,7 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
     RoundParams ps = p0;
     ps.slots = 0;
     ps.nrows = 1;
-    step_kernel<R, true, true, true>
-        <<<(e->v.slow_cap + 255) / 256, 256, 0, e->stream>>>(e->v, ps);
+    launch[SK_SLOW](e->v, ps, (e->v.slow_cap + 255) / 256, e->stream);
   }
 }
 
@@ -2543,15 +2534,15 @@ static int launch_tan(drb_engine *e, uint32_t round) {
                                               : drb::TAN_MAX_LOG;
   HIPCHK(hipMemsetAsync(e->tan_n, 0, 64 * drb::TAN_LISTS * sizeof(uint32_t),
                         e->stream));
-  k_tan_select<<<(unsigned)e->tan_blocks, 256, 0, e->stream>>>(
-      e->v, round, max_log, e->tan_list, e->tan_per_list, e->tan_n);
+  tan_launch_select(e->v, round, max_log, e->tan_list, e->tan_per_list,
+                    e->tan_n, (unsigned)e->tan_blocks, e->stream);
   HIPCHK(hipGetLastError());
   if (e->v.tan_mux) {
-    k_tanm_chain<<<e->v.R * 16, 64, 0, e->stream>>>(e->v, max_log);
+    tan_launch_chain(e->v, max_log, e->v.R * 16, e->stream);
     HIPCHK(hipGetLastError());
   }
-  k_tan_write<<<(unsigned)e->tan_wblocks, 256, 0, e->stream>>>(
-      e->v, round, max_log, e->tan_list, e->tan_per_list, e->tan_n);
+  tan_launch_write(e->v, round, max_log, e->tan_list, e->tan_per_list,
+                   e->tan_n, (unsigned)e->tan_wblocks, e->stream);
   HIPCHK(hipGetLastError());
   return DRB_OK;
 }

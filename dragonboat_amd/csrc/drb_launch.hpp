@@ -1,0 +1,68 @@
+// drb_launch.hpp -- the step kernel's instantiations as separately compiled
+// launchers (drb_step_inst.hip), one per (replicas per group, kind).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "drb_layout.hpp"
+
+namespace drb {
+
+struct RoundParams;  // drb_step.hpp
+
+enum StepKind : int {
+  SK_LEAD = 0,        // step_kernel<R, true, false>: leaders, C3 paths
+  SK_LEAD_EXT = 1,    // step_kernel<R, true, true>: + long Cmds, out-of-line
+                      //   values, EntryBatch / tan encoding, Quiesce
+  SK_FOLLOW = 2,      // step_kernel<R, false, false>
+  SK_FOLLOW_EXT = 3,  // step_kernel<R, false, true>
+  SK_SLOW = 4,        // step_kernel<R, true, true, true>: the raft launch
+  NUM_STEP_KINDS
+};
+
+typedef void (*StepLaunchFn)(const View &v, const RoundParams &p,
+                             unsigned grid, hipStream_t s);
+
+#define DRB_STEP_LAUNCH_NAME2(R, K) step_launch_r##R##_k##K
+#define DRB_STEP_LAUNCH_NAME(R, K) DRB_STEP_LAUNCH_NAME2(R, K)
+
+#define DRB_DECLARE_STEP_LAUNCH(R, K)                                      \
+  void DRB_STEP_LAUNCH_NAME(R, K)(const View &v, const RoundParams &p,     \
+                                  unsigned grid, hipStream_t s);
+#define DRB_DECLARE_STEP_LAUNCH_R(R)                                      \
+  DRB_DECLARE_STEP_LAUNCH(R, 0)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 1)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 2)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 3)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 4)
+DRB_DECLARE_STEP_LAUNCH_R(1)
+DRB_DECLARE_STEP_LAUNCH_R(2)
+DRB_DECLARE_STEP_LAUNCH_R(3)
+DRB_DECLARE_STEP_LAUNCH_R(4)
+DRB_DECLARE_STEP_LAUNCH_R(5)
+DRB_DECLARE_STEP_LAUNCH_R(6)
+DRB_DECLARE_STEP_LAUNCH_R(7)
+DRB_DECLARE_STEP_LAUNCH_R(8)
+
+// the tan record kernels (drb_tan.hpp), compiled in drb_tan_inst.hip
+void tan_launch_select(const View &v, uint32_t round, uint64_t max_log,
+                       uint32_t *list, uint32_t per_list, uint32_t *n,
+                       unsigned blocks, hipStream_t s);
+void tan_launch_chain(const View &v, uint64_t max_log, unsigned blocks,
+                      hipStream_t s);
+void tan_launch_write(const View &v, uint32_t round, uint64_t max_log,
+                      const uint32_t *list, uint32_t per_list,
+                      const uint32_t *n, unsigned blocks, hipStream_t s);
+
+#ifndef DRB_INST_R
+// kStepLaunch[R - 1][kind]
+#define DRB_STEP_LAUNCH_ROW(R)                                            \
+  {DRB_STEP_LAUNCH_NAME(R, 0), DRB_STEP_LAUNCH_NAME(R, 1),                \
+   DRB_STEP_LAUNCH_NAME(R, 2), DRB_STEP_LAUNCH_NAME(R, 3),                \
+   DRB_STEP_LAUNCH_NAME(R, 4)}
+static const StepLaunchFn kStepLaunch[8][NUM_STEP_KINDS] = {
+    DRB_STEP_LAUNCH_ROW(1), DRB_STEP_LAUNCH_ROW(2), DRB_STEP_LAUNCH_ROW(3),
+    DRB_STEP_LAUNCH_ROW(4), DRB_STEP_LAUNCH_ROW(5), DRB_STEP_LAUNCH_ROW(6),
+    DRB_STEP_LAUNCH_ROW(7), DRB_STEP_LAUNCH_ROW(8)};
+#endif
+
+}  // namespace drb

@@ -1,0 +1,33 @@
+// drb_step_inst.hip -- one instantiation of the step kernel (drb_step.hpp)
+// and its launcher, compiled once per (R, kind) with -DDRB_INST_R and
+// -DDRB_INST_KIND (dragonboat_amd/build.py).  The 40 instantiations are
+// independent translation units so the build runs them in parallel; the
+// engine (drb_engine.hip) calls them through kStepLaunch (drb_launch.hpp).
+//
+// Written for gfx950 (MI355X) only.
+#include <hip/hip_runtime.h>
+
+#include "drb_launch.hpp"
+#include "drb_step.hpp"
+
+#ifndef DRB_INST_R
+#error "DRB_INST_R (replicas per group) is required"
+#endif
+#ifndef DRB_INST_KIND
+#error "DRB_INST_KIND (drb_launch.hpp StepKind) is required"
+#endif
+
+namespace drb {
+
+void DRB_STEP_LAUNCH_NAME(DRB_INST_R, DRB_INST_KIND)(const View &v,
+                                                     const RoundParams &p,
+                                                     unsigned grid,
+                                                     hipStream_t s) {
+  constexpr int K = DRB_INST_KIND;
+  constexpr bool LEAD = K == SK_LEAD || K == SK_LEAD_EXT || K == SK_SLOW;
+  constexpr bool EXT = K == SK_LEAD_EXT || K == SK_FOLLOW_EXT || K == SK_SLOW;
+  constexpr bool SLOW = K == SK_SLOW;
+  step_kernel<DRB_INST_R, LEAD, EXT, SLOW><<<grid, 256, 0, s>>>(v, p);
+}
+
+}  // namespace drb

@@ -474,6 +474,11 @@ __device__ __forceinline__ void tan_count_row(const View &v, const TanCount &c,
     v.tan_ctr[(uint64_t)blockIdx.x * 4 + threadIdx.x] += part[threadIdx.x];
 }
 
+// The kernels are compiled in their own translation units
+// (drb_tan_inst.hip: DRB_TAN_KERNELS 1 = select + chain, 2 = write; the
+// engine launches them through drb_launch.hpp), so the engine's other code
+// does not wait on their long register allocation.
+#if DRB_TAN_KERNELS == 1
 // list r of the select pass holds the replicas of workgroups b = r mod
 // TAN_LISTS, at most per_list of them; its count is n[r * 64]
 __global__ __launch_bounds__(256) void k_tan_select(View v, uint32_t round,
@@ -661,6 +666,9 @@ __global__ __launch_bounds__(64) void k_tanm_chain(View v, uint64_t max_log) {
   }
 }
 
+#endif  // DRB_TAN_KERNELS == 1
+
+#if DRB_TAN_KERNELS == 2
 // the listed records, one per lane (grid-stride over the lists' total);
 // its workgroups add into tan_ctr rows 0.. as well (the launches run in
 // stream order)
@@ -700,5 +708,6 @@ __global__ __launch_bounds__(256) void k_tan_write(View v, uint32_t round,
   }
   tan_count_row(v, c, part);
 }
+#endif  // DRB_TAN_KERNELS == 2
 
 }  // namespace drb

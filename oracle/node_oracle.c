@@ -1015,6 +1015,97 @@ int orc_cluster_export(orc_cluster *c, uint64_t g, uint32_t slot,
   return 0;
 }
 
+/* The inverse of orc_cluster_export plus the log: replica (g, slot) takes
+ * the given state, as the engine's drb_import_replicas + drb_import_log do
+ * -- raft.loadState over a LogDB (raft.go:1099-1117) and the inMemory
+ * window (newEntryLog, logentry.go:86-95, with the markers the state
+ * names).  ents hold [ents[0].index, st->last_index] contiguously: those
+ * <= saved_to are the LogDB's (LogReader), those >= marker_index
+ * inMemory's.  The KV keeps its contents (KVTest.Count is taken from st);
+ * the inbox and the apply queue are emptied.  0 ok, -1 bad input. */
+int orc_cluster_import(orc_cluster *c, uint64_t g, uint32_t slot,
+                       const drb_replica_state *st, const drb_entry *ents,
+                       size_t n, const uint8_t *pool) {
+  if (g >= c->cfg.num_groups || slot >= c->cfg.num_replicas) return -1;
+  if (st->ri_count) return -1; /* a readIndex queue is not imported */
+  const uint64_t first = n ? ents[0].index : st->last_index + 1;
+  if (first == 0 || first - 1 + n != st->last_index) return -1;
+  if (st->marker_index < first || st->marker_index > st->last_index + 1 ||
+      st->saved_to + 1 < first || st->saved_to > st->last_index)
+    return -1;
+  orc_node *nd = node_at(c, g, slot);
+  orc_raft *r = nd->r;
+  ORC_TRY(-1);
+  orc_logdb *db = nd->db;
+  ev_truncate(&db->ents, 0);
+  db->marker_index = first - 1;
+  db->marker_term = 0; /* first == 1 on this path: term(0) == 0 */
+  orc_log *l = &r->log;
+  ev_truncate(&l->im.ents, 0);
+  for (size_t i = 0; i < n; i++) {
+    orc_entry e = entry_from_view(&ents[i], pool);
+    e.index = first + i;
+    if (e.index <= st->saved_to) ev_push(&db->ents, &e);
+    if (e.index >= st->marker_index) ev_push(&l->im.ents, &e);
+    blob_unref(e.cmd);
+  }
+  l->im.marker_index = st->marker_index;
+  l->im.saved_to = st->saved_to;
+  l->im.applied_to_index = st->applied_to_index;
+  l->im.applied_to_term = st->applied_to_term;
+  l->im.shrunk = 0;
+  l->committed = st->committed;
+  l->processed = st->processed;
+  r->term = st->term;
+  r->vote = st->vote;
+  r->leader_id = st->leader_id;
+  r->applied = st->applied;
+  r->election_tick = st->election_tick;
+  r->heartbeat_tick = st->heartbeat_tick;
+  r->randomized_election_timeout = st->randomized_election_timeout;
+  r->tick_count = st->tick_count;
+  r->state = st->role;
+  r->rng = st->rng;
+  r->leader_transfer_target = 0;
+  r->is_leader_transfer_target = 0;
+  r->nvotes = 0;
+  for (uint32_t s = 0; s < DRB_MAX_REPLICAS; s++)
+    if ((st->votes >> s) & 1u) {
+      r->vote_id[r->nvotes] = s + 1;
+      r->vote_ok[r->nvotes] = (int)((st->votes >> (8 + s)) & 1u);
+      r->nvotes++;
+    }
+  for (int i = 0; i < r->nrem; i++) {
+    const uint64_t id = r->rem_id[i];
+    if (id < 1 || id > DRB_MAX_REPLICAS) continue;
+    const drb_remote_state *d = &st->remotes[id - 1];
+    r->rem[i].match = d->match;
+    r->rem[i].next = d->next;
+    r->rem[i].state = d->state;
+    r->rem[i].active = (int)d->active;
+  }
+  r->ri.n = 0;
+  raft_clear_msgs(r);
+  nd->applied_index = st->applied_index;
+  nd->confirmed_index = st->confirmed_index;
+  nd->pushed_index = st->pushed_index;
+  nd->prev_term = st->prev_term;
+  nd->prev_vote = st->prev_vote;
+  nd->prev_commit = st->prev_commit;
+  nd->sm_index = nd->la_index = st->sm_index;
+  nd->sm_term = nd->la_term = st->sm_term;
+  nd->kv.count = st->kv_count;
+  nd->qs.current_tick = st->qs_current_tick;
+  nd->qs.idle_since = st->qs_idle_since;
+  nd->qs.quiesced_since = st->qs_quiesced_since;
+  nd->qs.exit_quiesce_tick = st->qs_exit_quiesce_tick;
+  nd->hosted = (st->flags & DRB_F_HOSTED) != 0;
+  mv_clear(&nd->inbox);
+  ev_truncate(&nd->applyq, 0);
+  ORC_END;
+  return 0;
+}
+
 long orc_cluster_export_log(orc_cluster *c, uint64_t g, uint32_t slot,
                             uint64_t lo, uint64_t hi, drb_entry *out,
                             uint8_t *pool, size_t pool_cap) {

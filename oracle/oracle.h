@@ -237,6 +237,24 @@ int orc_raft_set_remote(orc_raft *r, uint64_t id, const orc_remote *in);
 size_t orc_raft_ready_to_read(orc_raft *r, uint64_t *index, uint64_t *low,
                               uint64_t *high, size_t cap);
 size_t orc_raft_dropped_read_indexes(orc_raft *r);
+/* election KAT hooks: fields the reference's tests assign directly */
+enum {
+  ORC_POKE_STATE = 0,
+  ORC_POKE_TERM,
+  ORC_POKE_VOTE,
+  ORC_POKE_ELECTION_TICK,
+  ORC_POKE_ELECTION_TIMEOUT,
+  ORC_POKE_COMMITTED,
+  ORC_POKE_APPLIED,
+  ORC_POKE_CONFIG_CHANGE_HOOK /* 1: hasNotAppliedConfigChange = test hook */
+};
+int orc_raft_poke(orc_raft *r, int field, uint64_t v);
+uint64_t orc_raft_peek(orc_raft *r, int field);
+int orc_raft_reset(orc_raft *r, uint64_t term);
+int orc_raft_become_pre_vote_candidate(orc_raft *r);
+int orc_raft_draw_timeout_time_for_election(orc_raft *r);
+int orc_raft_term_not_matched(orc_raft *r, const drb_message *m,
+                              const drb_entry *ents, const uint8_t *pool);
 /* entryLog KAT hooks */
 int orc_log_commit_to(orc_raft *r, uint64_t index);
 int orc_log_try_commit(orc_raft *r, uint64_t index, uint64_t term);
@@ -381,6 +399,11 @@ int orc_cluster_round_range(orc_cluster *c, int tick, uint64_t g0, uint64_t g1,
 int orc_cluster_end_round(orc_cluster *c);
 int orc_cluster_export(orc_cluster *c, uint64_t g, uint32_t slot,
                        drb_replica_state *st);
+/* replica (g, slot) takes state st and the log ents (drb_import_replicas +
+ * drb_import_log on the engine side); see node_oracle.c */
+int orc_cluster_import(orc_cluster *c, uint64_t g, uint32_t slot,
+                       const drb_replica_state *st, const drb_entry *ents,
+                       size_t n, const uint8_t *pool);
 long orc_cluster_export_log(orc_cluster *c, uint64_t g, uint32_t slot,
                             uint64_t lo, uint64_t hi, drb_entry *out,
                             uint8_t *pool, size_t pool_cap);

@@ -102,6 +102,12 @@ def _declare(L):
         "orc_raft_set_check_quorum": (None, [P, C.c_int]),
         "orc_raft_set_pre_vote": (None, [P, C.c_int]),
         "orc_raft_network_reset": (C.c_int, [P, U64, PU64, C.c_int]),
+        "orc_raft_poke": (C.c_int, [P, C.c_int, U64]),
+        "orc_raft_peek": (U64, [P, C.c_int]),
+        "orc_raft_reset": (C.c_int, [P, U64]),
+        "orc_raft_become_pre_vote_candidate": (C.c_int, [P]),
+        "orc_raft_draw_timeout_time_for_election": (C.c_int, [P]),
+        "orc_raft_term_not_matched": (C.c_int, [P, PM, PE, PU8]),
         "orc_raft_read_messages": (C.c_long, [P, PM, C.c_size_t, PE,
                                               C.c_size_t, PU8, C.c_size_t]),
         "orc_raft_log_entries": (C.c_long, [P, C.c_int, PE, C.c_size_t, PU8,
@@ -189,6 +195,9 @@ def _declare(L):
         "orc_cluster_end_round": (C.c_int, [P]),
         "orc_cluster_export": (C.c_int, [P, U64, U32,
                                          C.POINTER(ReplicaState)]),
+        "orc_cluster_import": (C.c_int, [P, U64, U32,
+                                         C.POINTER(ReplicaState), PE,
+                                         C.c_size_t, PU8]),
         "orc_cluster_export_log": (C.c_long, [P, U64, U32, U64, U64, PE, PU8,
                                               C.c_size_t]),
         "orc_cluster_export_outbox": (C.c_long, [P, U64, U32, PM, C.c_size_t,
@@ -467,6 +476,36 @@ class TestRaft:
     def set_randomized_election_timeout(self, v):
         lib().orc_raft_set_randomized_election_timeout(self.p, v)
 
+    # fields the reference's tests assign directly (orc_raft_poke)
+    POKE = dict(state=0, term=1, vote=2, election_tick=3,
+                election_timeout=4, committed=5, applied=6,
+                config_change_hook=7)
+
+    def poke(self, **kw):
+        for k, v in kw.items():
+            if lib().orc_raft_poke(self.p, self.POKE[k], int(v)):
+                raise KeyError(k)
+
+    def peek(self, field):
+        return lib().orc_raft_peek(self.p, self.POKE[field])
+
+    def reset(self, term):
+        """reset(term, true) (raft.go:1052-1073)."""
+        _check(lib().orc_raft_reset(self.p, term))
+
+    def become_pre_vote_candidate(self):
+        _check(lib().orc_raft_become_pre_vote_candidate(self.p))
+
+    def draw_timeout_time_for_election(self):
+        """setRandomizedElectionTimeout(); timeForElection()."""
+        return bool(lib().orc_raft_draw_timeout_time_for_election(self.p))
+
+    def term_not_matched(self, m):
+        """onMessageTermNotMatched (raft.go:1540-1590): True = dropped."""
+        marr, n, earr, pool = build_messages([m])
+        return bool(_check(lib().orc_raft_term_not_matched(self.p, marr, earr,
+                                                           pool)))
+
     def network_reset(self, id, ids):
         arr = (U64 * len(ids))(*ids)
         _check(lib().orc_raft_network_reset(self.p, id, arr, len(ids)))
@@ -611,17 +650,25 @@ class BlackHole:
 
 
 class Network:
-    """network (raft_etcd_test.go:2896-3030): synchronous delivery."""
+    """network (raft_etcd_test.go:2896-3030): synchronous delivery, with the
+    drop / cut / isolate / ignore / recover filters (:2980-3026; drop rates
+    are 0 or 1 in every test restated here, so the filter is exact)."""
 
-    def __init__(self, *peers):
+    def __init__(self, *peers, pre_vote=False, check_quorum=False):
         ids = list(range(1, len(peers) + 1))
         self.peers = {}
         for i, p in zip(ids, peers):
             if p is None:
                 p = TestRaft(i, ids, 10, 1)
+                if pre_vote:
+                    p.set_pre_vote(True)
+                if check_quorum:
+                    p.set_check_quorum(True)
             elif isinstance(p, TestRaft):
                 p.network_reset(i, ids)
             self.peers[i] = p
+        self.dropm = {}
+        self.ignorem = set()
 
     def send(self, *msgs):
         q = list(msgs)
@@ -629,7 +676,67 @@ class Network:
             m = q.pop(0)
             p = self.peers[m["to"]]
             p.handle(m)
-            q.extend(p.read_messages())
+            q.extend(self.filter(p.read_messages()))
+
+    def drop(self, frm, to, perc):
+        self.dropm[(frm, to)] = perc
+
+    def cut(self, one, other):
+        self.drop(one, other, 1.0)
+        self.drop(other, one, 1.0)
+
+    def isolate(self, id):
+        for nid in self.peers:
+            if nid != id:
+                self.drop(id, nid, 1.0)
+                self.drop(nid, id, 1.0)
+
+    def ignore(self, t):
+        self.ignorem.add(t)
+
+    def recover(self):
+        self.dropm = {}
+        self.ignorem = set()
+
+    def filter(self, msgs):
+        out = []
+        for m in msgs:
+            if m["type"] in self.ignorem:
+                continue
+            if m["type"] == MSG_ELECTION:
+                raise OracleError("unexpected msgHup")
+            if self.dropm.get((m["from_"], m["to"]), 0.0) >= 1.0:
+                continue
+            out.append(m)
+        return out
+
+
+MSG_ELECTION = 1
+
+
+def ents_with_config(*terms, pre_vote=False):
+    """entsWithConfig (raft_etcd_test.go:2865-2878): a raft (election 5)
+    whose LogDB holds one entry per term given, reset to the last term."""
+    db = LogDB([ent(term=t, index=i + 1) for i, t in enumerate(terms)])
+    r = TestRaft(1, [], 5, 1, db)
+    r.poke(config_change_hook=0)  # newRaft, not newTestRaft
+    if pre_vote:
+        r.set_pre_vote(True)
+    r.reset(terms[-1])
+    return r
+
+
+def voted_with_config(vote, term, pre_vote=False):
+    """votedWithConfig (raft_etcd_test.go:2880-2893): Vote and Term set in
+    the LogDB's state, no entries."""
+    db = LogDB()
+    db.set_state(term=term, vote=vote)
+    r = TestRaft(1, [], 5, 1, db)
+    r.poke(config_change_hook=0)  # newRaft, not newTestRaft
+    if pre_vote:
+        r.set_pre_vote(True)
+    r.reset(term)
+    return r
 
 
 # ---------------------------------------------------------------- cluster
@@ -689,6 +796,16 @@ class Cluster:
         if lib().orc_cluster_export(self.p, g, slot, st):
             raise IndexError((g, slot))
         return st
+
+    def import_replica(self, g, slot, st, entries):
+        """Replica (g, slot) takes state `st` (a ReplicaState) and the log
+        `entries` (entry dicts, indices from 1 up to st.last_index);
+        drb_import_replicas + drb_import_log on the engine side."""
+        arr, pool, n = EntryPool(entries).arrays()
+        for i in range(n):
+            arr[i].index = i + 1
+        _check(lib().orc_cluster_import(self.p, g, slot, C.byref(st), arr, n,
+                                        pool))
 
     def export_log(self, g, slot, lo, hi):
         cap = hi - lo + 1

@@ -2493,3 +2493,72 @@ int orc_raft_network_reset(orc_raft *r, uint64_t id, const uint64_t *ids,
   ORC_END;
   return 0;
 }
+
+/* ---- election KAT hooks (raft_etcd_test.go, raft_test.go) ------------- */
+/* the raft fields the reference's tests assign directly (sm.state = ...,
+ * r.term = ..., r.electionTick = ..., r.log.committed = ...,
+ * r.hasNotAppliedConfigChange = nil) */
+int orc_raft_poke(orc_raft *r, int field, uint64_t v) {
+  switch (field) {
+    case ORC_POKE_STATE: r->state = (uint32_t)v; break;
+    case ORC_POKE_TERM: r->term = v; break;
+    case ORC_POKE_VOTE: r->vote = v; break;
+    case ORC_POKE_ELECTION_TICK: r->election_tick = v; break;
+    case ORC_POKE_ELECTION_TIMEOUT: r->election_timeout = v; break;
+    case ORC_POKE_COMMITTED: r->log.committed = v; break;
+    case ORC_POKE_APPLIED: r->applied = v; break;
+    case ORC_POKE_CONFIG_CHANGE_HOOK: r->test_has_config_change_hook = (int)v;
+      break;
+    default: return -1;
+  }
+  return 0;
+}
+
+uint64_t orc_raft_peek(orc_raft *r, int field) {
+  switch (field) {
+    case ORC_POKE_STATE: return r->state;
+    case ORC_POKE_TERM: return r->term;
+    case ORC_POKE_VOTE: return r->vote;
+    case ORC_POKE_ELECTION_TICK: return r->election_tick;
+    case ORC_POKE_ELECTION_TIMEOUT: return r->election_timeout;
+    case ORC_POKE_COMMITTED: return r->log.committed;
+    case ORC_POKE_APPLIED: return r->applied;
+    case ORC_POKE_CONFIG_CHANGE_HOOK: return (uint64_t)r->test_has_config_change_hook;
+    default: return ~0ull;
+  }
+}
+
+/* reset(term, true) (raft.go:1052-1073), as entsWithConfig /
+ * votedWithConfig call it (raft_etcd_test.go:2865-2893) */
+int orc_raft_reset(orc_raft *r, uint64_t term) {
+  ORC_TRY(-1);
+  raft_reset(r, term, 1);
+  ORC_END;
+  return 0;
+}
+
+int orc_raft_become_pre_vote_candidate(orc_raft *r) {
+  ORC_TRY(-1);
+  raft_become_pre_vote_candidate(r);
+  ORC_END;
+  return 0;
+}
+
+/* setRandomizedElectionTimeout (raft.go:658-661) + timeForElection
+ * (raft.go:602-604): TestPastElectionTimeout draws the timeout and asks */
+int orc_raft_draw_timeout_time_for_election(orc_raft *r) {
+  raft_set_rand_timeout(r);
+  return r->election_tick >= r->randomized_election_timeout;
+}
+
+/* onMessageTermNotMatched (raft.go:1540-1590) alone: 1 when the message is
+ * dropped there */
+int orc_raft_term_not_matched(orc_raft *r, const drb_message *m,
+                              const drb_entry *ents, const uint8_t *pool) {
+  orc_msg mm = msg_from_view(m, ents, pool);
+  ORC_TRY(-1);
+  int rc = raft_term_not_matched(r, &mm);
+  ORC_END;
+  msg_free(&mm);
+  return rc;
+}

@@ -197,6 +197,30 @@ class Pair:
         self.eng.import_replicas(g, sts)
         self.cpu.discard(g)
 
+    def import_group(self, g, reps):
+        """Every replica of group g takes reps[slot] = (ReplicaState, log
+        entry dicts from index 1) on both sides: orc_cluster_import and
+        drb_import_log + drb_kv_import (empty) + drb_import_replicas."""
+        sts = []
+        for s, (st, log) in enumerate(reps):
+            self.orc.import_replica(g, s, st, log)
+            if log:
+                ep = po.EntryPool(log)
+                arr, pool, n = ep.arrays()
+                for i in range(n):
+                    arr[i].index = i + 1
+                self.eng.import_log(g, s, arr, pool)
+            self.eng.kv_import(g, s, {})
+            sts.append(st)
+        self.eng.import_replicas(g, sts)
+
+    def ingest(self, msgs):
+        """The same messages from unhosted senders into both sides
+        (drb_ingest / orc_cluster_ingest)."""
+        self.orc.ingest(msgs)
+        marr, n, earr, pool = po.build_messages(msgs)
+        return self.eng.ingest(marr, n, earr, pool)
+
     def live_groups(self):
         return [g for g in range(self.G) if g not in self.cpu]
 

@@ -232,3 +232,38 @@ def test_sampled_cluster_matches_full_cluster():
                 assert a.to_dict(3) == b.to_dict(3), (r, g, s)
                 assert full.export_outbox(g, s) == samp.export_outbox(i, s)
                 assert full.export_kv(g, s) == samp.export_kv(i, s)
+
+
+# ------------------------------------------------ divergent logs (import)
+@pytest.mark.parametrize("case", range(6))
+def test_leader_sync_follower_log_in_cluster(case):
+    """LeaderSyncFollowerLog (raft_etcd_paper_test.go:690-770) through the
+    cluster's step loop: the states are imported (orc_cluster_import, the
+    oracle side of drb_import_replicas / drb_import_log), the leader-to-be
+    times out, the hole's vote is ingested, and after the rounds the
+    follower's log equals the leader's -- LEAD_ENTS plus the term-9 no-op
+    -- with every entry committed and applied on both."""
+    from tests import scenarios as sc
+    c = po.Cluster(1, 3, seed=SEED, election_rtt=10)
+    c.setup_steady(0)
+    reps = sc.sync_follower_group(lambda s: c.export(0, s),
+                                  sc.SYNC_CASES[case])
+    for s, (st, log) in enumerate(reps):
+        c.import_replica(0, s, st, log)
+        assert c.export(0, s).last_index == len(log)
+    c.round(tick=True)
+    assert (c.export(0, 0).role, c.export(0, 0).term) == \
+        (abi.CANDIDATE, sc.LEAD_TERM + 1)
+    c.ingest([sc.vote_from_hole(c.export(0, 0).shard_id)])
+    for _ in range(30):  # the probe walks back one index a Replicate
+        c.round(tick=True)
+    lead, fol = c.export(0, 0), c.export(0, 1)
+    assert lead.role == abi.LEADER and fol.role == abi.FOLLOWER
+    assert lead.last_index == fol.last_index == len(sc.LEAD_ENTS) + 1
+    assert lead.committed == fol.committed == lead.last_index
+    assert fol.sm_index == fol.committed
+    want = [(e["term"], i + 1) for i, e in enumerate(sc.LEAD_ENTS)] + \
+        [(sc.LEAD_TERM + 1, len(sc.LEAD_ENTS) + 1)]
+    for s in (0, 1):
+        got = [(e[0], e[1]) for e in c.export_log(0, s, 1, lead.last_index)]
+        assert got == want, (s, got)
