@@ -84,6 +84,11 @@ def parse():
     ap.add_argument("--kv-slots", type=int, default=0,
                     help="KV table slots per replica (0: the workload's)")
     ap.add_argument("--no-read-index", action="store_true")
+    ap.add_argument("--kv-fill", type=int, default=-1,
+                    help="c2/c3: rounds of fresh-key writes before the "
+                         "timed region, so each replica's KV holds its "
+                         "group's K = 256 keys (SURVEY 8d steady state); "
+                         "default 1536 (255 of 256 keys expected)")
     ap.add_argument("--tick-every", type=int, default=0,
                     help="LocalTick every N rounds (0: derive from --tick-ms)")
     ap.add_argument("--tick-ms", type=float, default=1.0,
@@ -257,7 +262,11 @@ def main():
     if c4:
         args.no_read_index = True  # 16 B writes, k_w = 1
     reads = not args.no_read_index
-    NP = 8  # staged input batches (resident in HBM before timing)
+    # staged input batches: one per timed round, every one with fresh keys,
+    # all resident in HBM before the timed region
+    NP = max(8, args.steps)
+    if args.kv_fill < 0:
+        args.kv_fill = 0 if (c4 or c5) else 1536
     xch = None
     if c4:  # one global set of G groups spread over the world
         lanes = (G + world - 1) // world
@@ -309,16 +318,20 @@ def main():
                      elections=args.elections,
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
-    for b in range(NP):
-        if c5:
-            continue  # generated per round inside step()
-        eng.gen_kv_proposals(b, k, 256, 4, seed, b)
-        eng.gen_read_index(b, seed, b + 30)
     stream = torch.cuda.ExternalStream(eng.stream)
 
     tick_every = [max(1, args.tick_every)]
+    # input salts: the KV fill, the warmup and the timed rounds each draw
+    # batches no earlier round used (workload.py: key = f(seed, g, salt))
+    FILL_SALT, WARM_SALT, TIMED_SALT = 1 << 20, 1 << 21, 1 << 22
 
-    def step(i):
+    def stage(b, salt):
+        """batch b := the seeded inputs of salt (SURVEY 8d generators)"""
+        eng.gen_kv_proposals(b, k, KEY_SPACE, 4, seed, salt)
+        if reads:
+            eng.gen_read_index(b, seed, salt + 30)
+
+    def step(i, b=None):
         tick = i % tick_every[0] == 0
         # with reads: ReadLocalNode for the 9 reads behind every released
         # ctx, served inside the round (drb_round_in.reads_per_ctx)
@@ -327,8 +340,10 @@ def main():
             eng.gen_kv_proposals(i % NP, k, C5_KEYS[args.payload],
                                  C5_VAL[args.payload], seed,
                                  i, active_ppm=args.active_ppm)
-        eng.step_async(tick=tick, prop_slot=i % NP,
-                       ri_slot=(i % NP) if reads else 0xFFFFFFFF,
+        if b is None:
+            b = i % NP
+        eng.step_async(tick=tick, prop_slot=b,
+                       ri_slot=b if reads else 0xFFFFFFFF,
                        reads_per_ctx=READS_PER_CTX if fused else 0,
                        key_space=KEY_SPACE, encode_saves=saves,
                        ri_replica=2 if args.reads_at == "follower" else 0,
@@ -338,20 +353,52 @@ def main():
         if xch is not None:  # C4: this round's cross-GPU planes
             xch.step()
 
+    # the KV's steady state (writes uniform over K = 256 keys
+    # per group): fresh-key writes through the engine's own rounds until
+    # each replica's table holds (nearly) all of its group's keys
+    for i in range(args.kv_fill):
+        eng.gen_kv_proposals(0, k, KEY_SPACE, 4, seed, FILL_SALT + i)
+        eng.step_async(tick=True, prop_slot=0)
+        if i % 256 == 255:
+            eng.sync()
     # warmup (ticking every round); the tick cadence then follows the
     # reference's wall-clock tick worker: one LocalTick per RTTMillisecond
+    def warm_step(i):
+        if not c5:
+            stage(0, WARM_SALT + i)
+        step(i, 0 if not c5 else None)
+
     tw0 = time.perf_counter()
     for i in range(args.warmup):
-        step(i)
+        warm_step(i)
     eng.sync()
     warm_ms = (time.perf_counter() - tw0) * 1e3 / max(1, args.warmup)
     if args.tick_every <= 0:
         te = max(1, int(round(args.tick_ms / max(warm_ms, 1e-6))))
         tick_every[0] = ddist.agree_min(te, red)
         for i in range(args.warmup, 2 * args.warmup):
-            step(i)
+            warm_step(i)
         eng.sync()
     args.tick_every = tick_every[0]
+    if not c5:  # the timed rounds' inputs, resident before timing starts
+        for b in range(args.steps):
+            stage(b, TIMED_SALT + b)
+        eng.sync()
+    kv_load = None
+    if not (c4 or c5):
+        # the KV occupancy the timed rounds run at: distinct keys per
+        # replica over a sample of groups (drb_kv_export)
+        smp = [g * (G // 64) for g in range(64)]
+        nk = [len(eng.kv_export(g, s)) for g in smp for s in range(R)]
+        kv_slots = args.kv_slots or 512
+        kv_load = {"keys_per_replica": sum(nk) / len(nk),
+                   "kv_slots": kv_slots,
+                   "load": sum(nk) / len(nk) / kv_slots,
+                   "fill_rounds": args.kv_fill,
+                   "note": "distinct keys per replica table after the fill "
+                           "and warmup rounds, 64 sampled groups x %d "
+                           "replicas; the timed rounds write fresh keys "
+                           "and read uniformly over the %d" % (R, KEY_SPACE)}
     eng.read_counters(reset=True)
     warm_flagged = len(eng.take_flagged(reset=True)[0])
     if xch is not None:
@@ -365,7 +412,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(K):
         ev[i][0].record(stream)
-        step(2 * args.warmup + i)
+        step(2 * args.warmup + i, None if c5 else i)
         ev[i][1].record(stream)
     eng.sync()
     torch.cuda.synchronize()
@@ -517,9 +564,10 @@ def main():
         from dragonboat_amd import workload
         # the host arrays in pinned memory, so the upload overlaps the
         # previous round (drb_stage_proposals copies on its own stream)
+        HB = 8  # host batches, cycled
         hb = [tuple(torch.from_numpy(x.view("u1")).pin_memory()
                     for x in workload.build_batch_np(G, seed, b))
-              for b in range(NP)]
+              for b in range(HB)]
         hp = [(C.cast(c.data_ptr(), C.POINTER(C.c_uint32)),
                C.cast(e.data_ptr(), C.POINTER(_abi.Entry)),
                C.cast(p.data_ptr(), C.POINTER(C.c_uint8))) for c, e, p in hb]
@@ -528,9 +576,9 @@ def main():
         eng.sync()
         h0 = time.perf_counter()
         for i in range(KH):
-            b = i % NP
+            b = i % HB
             eng.stage_proposals(b, *hp[b], pool_len=hb[b][2].numel())
-            step(2 * args.warmup + K + i)
+            step(2 * args.warmup + K + i, b)
         eng.sync()
         hms = (time.perf_counter() - h0) * 1e3 / KH
         hout = eng.read_counters(reset=True)
@@ -673,6 +721,8 @@ def main():
             res["failover"] = failover
         if args.elections:
             res["config"]["elections"] = "on the GPU (drb_config.elections)"
+        if kv_load is not None:
+            res["kv_load"] = kv_load
         if xch is not None:
             res["exchange"] = {"mode": args.exchange,
                                "bytes_sent_per_round_rank0":

@@ -132,7 +132,18 @@ class Config(C.Structure):
                 ("quiesce", C.c_uint32), ("durable_log", C.c_uint32),
                 ("save_batched", C.c_uint32), ("save_tan", C.c_uint32),
                 ("elections", C.c_uint32), ("tan_max_log", C.c_uint64),
-                ("tan_multiplexed", C.c_uint32), ("pre_vote", C.c_uint32)]
+                ("tan_multiplexed", C.c_uint32), ("pre_vote", C.c_uint32),
+                ("max_reads_per_ctx", C.c_uint32)]
+
+
+class ReadResult(C.Structure):
+    """drb_read_result: one served ReadLocalNode read of the last round."""
+    _fields_ = [("shard_id", C.c_uint64), ("index", C.c_uint64),
+                ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64),
+                ("key", C.c_uint64), ("replica_id", C.c_uint32),
+                ("read", C.c_uint32), ("found", C.c_uint32),
+                ("vlen", C.c_uint32), ("value", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 class ApplyResult(C.Structure):

@@ -13,6 +13,7 @@ import hashlib
 import os
 import subprocess
 import sys
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -26,7 +27,10 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
 NUM_KINDS = 5
 # the headers a step-kernel instantiation includes
 STEP_DEPS = ["drb_step_inst.hip", "drb_step.hpp", "drb_launch.hpp",
-             "drb_layout.hpp", "drb_msg.hpp", "drb_codec.hpp"]
+             "drb_layout.hpp", "drb_msg.hpp", "drb_codec.hpp", "drb_ring.hpp"]
+# the tan record kernels' (drb_tan_inst.hip)
+TAN_DEPS = ["drb_tan_inst.hip", "drb_tan.hpp", "drb_launch.hpp",
+            "drb_layout.hpp", "drb_codec.hpp", "drb_ring.hpp"]
 
 
 def _inc():
@@ -42,8 +46,7 @@ def _deps():
 def _units(defines):
     """(object name, source, extra defines, dependencies) of every TU."""
     step_deps = [os.path.join(CSRC, f) for f in STEP_DEPS] + [_inc()]
-    tan_deps = step_deps + [os.path.join(CSRC, f)
-                            for f in ("drb_tan_inst.hip", "drb_tan.hpp")]
+    tan_deps = [os.path.join(CSRC, f) for f in TAN_DEPS] + [_inc()]
     units = [("drb_engine.o", "drb_engine.hip", [], _deps()),
              ("tan_write.o", "drb_tan_inst.hip", ["DRB_TAN_KERNELS=2"],
               tan_deps),
@@ -76,10 +79,12 @@ def _compile(args):
     tmp = obj + ".tmp"
     cmd = [HIPCC] + FLAGS + ["-c", "-o", tmp] + ["-D" + d for d in defs] + \
         [os.path.join(CSRC, src)]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+    t0 = time.time()
     subprocess.check_call(cmd)
     os.replace(tmp, obj)
+    if verbose:
+        print("%6.1f s  %s" % (time.time() - t0, os.path.basename(obj)),
+              file=sys.stderr)
     return obj
 
 

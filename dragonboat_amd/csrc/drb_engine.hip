@@ -13,6 +13,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "../../include/drb_engine.h"
 #include "drb_layout.hpp"
 #include "drb_msg.hpp"
@@ -65,6 +67,12 @@ struct drb_engine {
   uint32_t *tan_n = nullptr;                 // their counts, 256 B apart
   uint32_t tan_per_list = 0;
   unsigned long long *tan_total = nullptr;   // its counter rows summed
+  // the last round whose reads were served (in-round or drb_serve_reads),
+  // their count per ctx and key space (drb_export_read_results)
+  uint64_t reads_round = ~0ull;
+  uint32_t reads_n = 0, reads_ks = 0;
+  void *xout = nullptr;  // batch exports' device output (grow-only)
+  size_t xout_bytes = 0;
 };
 
 static void wire_free(drb_engine *e);
@@ -319,6 +327,11 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
   rc |= dalloc(e, &v.rtr_count, R * G);
   rc |= dalloc(e, &v.read_sum, R * G);
+  v.max_reads = cfg->max_reads_per_ctx;
+  if (v.max_reads) {
+    rc |= dalloc(e, &v.read_res, R * RTR_CAP * (uint64_t)v.max_reads * G);
+    rc |= dalloc(e, &v.read_served, R * G);
+  }
   if (v.remote_mask) {  // inbound copies of the remote planes
     rc |= dalloc(e, &v.mbox_in, 2 * R * R * v.MB * MSG_CHUNKS * G);
     rc |= dalloc(e, &v.meta_in, 2 * R * R * G);
@@ -425,6 +438,7 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   for (void *p : e->allocs) (void)hipFree(p);
   if (e->scratch) (void)hipFree(e->scratch);
   if (e->stage_buf) (void)hipFree(e->stage_buf);
+  if (e->xout) (void)hipFree(e->xout);
   wire_free(e);
   ingest_free(e->ingest);
   (void)hipEventDestroy(e->ev_fork);
@@ -1025,6 +1039,135 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
   return DRB_OK;
 }
 
+// The packed form of a NoOP-session batch (drb_stage_proposals_packed):
+// counts u8 per group, Key / ClientID / Cmd length per entry, the Cmd bytes
+// back to back.  ent0[g] / coff[i]: exclusive scans of counts / lengths.
+__global__ void k_widen_u8(const uint8_t *in, uint32_t *out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+__global__ void k_widen_u16(const uint16_t *in, uint32_t *out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+
+__global__ void k_stage_packed(View v, uint32_t slot, uint32_t type,
+                               const uint32_t *counts, const uint32_t *ent0,
+                               const uint64_t *keys, const uint64_t *clients,
+                               const uint32_t *lens, const uint32_t *coff,
+                               const uint8_t *pool, uint64_t pool_len) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  const uint32_t n = counts[g];
+  v.prop_count[(uint64_t)slot * v.G + g] = n;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t i = (uint64_t)ent0[g] + j;
+    const uint64_t key = keys[i], cid = clients[i];
+    const uint32_t len = lens[i];
+    const uint64_t off = coff[i];
+    v.props[prop_ix(v, slot, j, 0, g)] = mk4h(key, cid);
+    v.props[prop_ix(v, slot, j, 1, g)] = make_uint4(0, 0, 0, 0);
+    if (len > v.C16 * 16 || off + len > pool_len) {  // CAPACITY (pre-pass)
+      v.props[prop_ix(v, slot, j, 2, g)] = make_uint4(type, ~0u, 1, 0);
+      continue;
+    }
+    const uint8_t *cmd = pool + off;
+    v.props[prop_ix(v, slot, j, 2, g)] = make_uint4(
+        type, len, prop_fast(type, cid, 0, len, len ? cmd[0] : 0u), 0);
+    for (uint32_t c = 0; c < v.C16; ++c) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t b = 0; b < 16 && c * 16 + b < len; ++b)
+        w[b >> 2] |= (uint32_t)cmd[c * 16 + b] << (8 * (b & 3));
+      v.props[prop_ix(v, slot, j, PROP_META + c, g)] =
+          make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+extern "C" int drb_stage_proposals_packed(
+    drb_engine *e, uint32_t slot, uint32_t type, const uint8_t *counts,
+    uint64_t n_entries, const uint64_t *keys, const uint64_t *client_ids,
+    const uint16_t *cmd_lens, const uint8_t *pool, size_t pool_len) {
+  if (!e || slot >= e->cfg.prop_slots) return DRB_ERANGE;
+  if (!counts || (n_entries && (!keys || !client_ids || !cmd_lens)) ||
+      (pool_len && !pool))
+    return DRB_EINVAL;
+  const View &v = e->v;
+  const uint64_t G = v.G, n = n_entries;
+  uint64_t tot = 0, bytes = 0;
+  for (uint64_t g = 0; g < G; ++g) {
+    if (counts[g] > v.max_props) return DRB_ERANGE;
+    tot += counts[g];
+  }
+  if (tot != n) return DRB_EINVAL;
+  for (uint64_t i = 0; i < n; ++i) bytes += cmd_lens[i];
+  if (bytes != pool_len) return DRB_EINVAL;
+  // upload: counts | keys | client ids | lengths | pool, then device-side
+  // u32 counts, lengths, their scans and the scans' temp storage
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const uint64_t n1 = n ? n : 1;
+  size_t tb1 = 0, tb2 = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, (uint32_t *)nullptr,
+                                          (uint32_t *)nullptr, (int)G,
+                                          e->stream));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (uint32_t *)nullptr,
+                                          (uint32_t *)nullptr, (int)n1,
+                                          e->stream));
+  const size_t o_cnt = 0, o_key = al(G), o_cid = o_key + al(8 * n1),
+               o_len = o_cid + al(8 * n1), o_pool = o_len + al(2 * n1),
+               up = o_pool + std::max<size_t>(pool_len, 16);
+  const size_t o_c32 = al(up), o_e0 = o_c32 + al(4 * G),
+               o_l32 = o_e0 + al(4 * G), o_off = o_l32 + al(4 * n1),
+               o_tmp = o_off + al(4 * n1),
+               need = o_tmp + al(std::max(tb1, tb2));
+  if (need > e->stage_bytes) {
+    HIPCHK(hipStreamSynchronize(e->stream));  // the buffer may be in use
+    if (e->stage_buf) HIPCHK(hipFree(e->stage_buf));
+    e->stage_buf = nullptr;
+    HIPCHK(hipMalloc(&e->stage_buf, need));
+    e->stage_bytes = need;
+  }
+  uint8_t *d = (uint8_t *)e->stage_buf;
+  // the upload on the copy stream (overlapping the running round), the
+  // layout on the engine stream, as drb_stage_proposals
+  HIPCHK(hipStreamWaitEvent(e->stream_h2d, e->ev_stage_free, 0));
+  HIPCHK(hipMemcpyAsync(d + o_cnt, counts, G, hipMemcpyHostToDevice,
+                        e->stream_h2d));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(d + o_key, keys, 8 * n, hipMemcpyHostToDevice,
+                          e->stream_h2d));
+    HIPCHK(hipMemcpyAsync(d + o_cid, client_ids, 8 * n,
+                          hipMemcpyHostToDevice, e->stream_h2d));
+    HIPCHK(hipMemcpyAsync(d + o_len, cmd_lens, 2 * n, hipMemcpyHostToDevice,
+                          e->stream_h2d));
+  }
+  if (pool_len)
+    HIPCHK(hipMemcpyAsync(d + o_pool, pool, pool_len, hipMemcpyHostToDevice,
+                          e->stream_h2d));
+  HIPCHK(hipEventRecord(e->ev_staged, e->stream_h2d));
+  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_staged, 0));
+  uint32_t *c32 = (uint32_t *)(d + o_c32), *e0 = (uint32_t *)(d + o_e0);
+  uint32_t *l32 = (uint32_t *)(d + o_l32), *off = (uint32_t *)(d + o_off);
+  k_widen_u8<<<(unsigned)((G + 255) / 256), 256, 0, e->stream>>>(d + o_cnt,
+                                                                  c32, G);
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(d + o_tmp, tb1, c32, e0, (int)G,
+                                          e->stream));
+  if (n) {
+    k_widen_u16<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(
+        (const uint16_t *)(d + o_len), l32, n);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(d + o_tmp, tb2, l32, off, (int)n,
+                                            e->stream));
+  }
+  k_stage_packed<<<(unsigned)((G + 255) / 256), 256, 0, e->stream>>>(
+      v, slot, type, c32, e0, (const uint64_t *)(d + o_key),
+      (const uint64_t *)(d + o_cid), l32, off, d + o_pool,
+      (uint64_t)pool_len);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e->ev_stage_free, e->stream));
+  HIPCHK(hipEventSynchronize(e->ev_staged));
+  return DRB_OK;
+}
+
 // SURVEY 8(d) synthetic writes; bit-identical to dragonboat_amd/workload.py
 constexpr uint64_t ACTIVE_SALT = 0xAC71BE5EAC71BE5Eull;
 
@@ -1134,8 +1277,11 @@ __global__ void k_gen_ri(View v, uint32_t rs, uint64_t seed, uint64_t salt,
 extern "C" int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
                                   uint64_t high) {
   if (!e || slot >= e->cfg.ri_slots) return DRB_ERANGE;
+  // the ctx of batch `high` (ctx.High = the round + 30 of the reference's
+  // genCtx, request.go:864-875): Low drawn from (seed, group, high), so
+  // every batch staged ahead of its round has its own ctx and read keys
   k_gen_ri<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
-      e->v, slot, seed, e->round + 1, high);
+      e->v, slot, seed, high, high);
   HIPCHK(hipGetLastError());  // stream-ordered before the next round
   return DRB_OK;
 }
@@ -1294,10 +1440,14 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     const bool zero = (c0.x & MF_TERM_ZERO) != 0;
     bool other = false;
     if (!zero) {
-      if (!(cur.y & MI_TERM)) {
+      // a pre-vote record carries a term of its own (r.term + 1 or the
+      // granted one): it never seeds the header's term (drb_ingest_wire
+      // and the GPU's emit do the same)
+      const bool pv = is_prevote_type(m.type);
+      if (!pv && !(cur.y & MI_TERM)) {
         cur.z = (uint32_t)m.term;
         cur.w = (uint32_t)(m.term >> 32);
-      } else if (q_hi(cur) != m.term) {
+      } else if (pv || q_hi(cur) != m.term) {
         other = true;
         c0.x |= MF_TERM_OTHER;
         if (v.rterm) {  // elections: the raft launch reads it
@@ -1634,6 +1784,9 @@ extern "C" int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
 
 extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (!e || !in) return DRB_EINVAL;
+  // transport threads stage the next round's inbox under this lock: a
+  // round launches and advances e->round atomically with respect to them
+  std::lock_guard<std::mutex> ingest_lock(e->ingest_mu);
   // a durable LogDB: the last round's messages wait for its persistence
   if (e->cfg.durable_log && e->committed_round < e->round) return DRB_EINVAL;
   if (in->prop_slot != DRB_NONE && in->prop_slot >= e->cfg.prop_slots)
@@ -1651,6 +1804,8 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.n_reads = in->reads_per_ctx;
   p.key_space = in->read_key_space;
   if (p.n_reads && !p.key_space) return DRB_EINVAL;
+  if (p.n_reads && e->v.max_reads && p.n_reads > e->v.max_reads)
+    return DRB_ERANGE;
   p.encode_saves = in->encode_saves ? 1 : 0;
   if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
   p.ri_replica = in->ri_replica;
@@ -1682,6 +1837,11 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   }
   e->round++;
   e->ticks += p.tick;
+  if (p.n_reads) {
+    e->reads_round = e->round;
+    e->reads_n = p.n_reads;
+    e->reads_ks = p.key_space;
+  }
   return DRB_OK;
 }
 
@@ -2425,12 +2585,16 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
 extern "C" int drb_serve_reads(drb_engine *e, uint32_t reads_per_ctx,
                                uint32_t key_space) {
   if (!e || key_space == 0) return DRB_EINVAL;
+  if (e->v.max_reads && reads_per_ctx > e->v.max_reads) return DRB_ERANGE;
   dim3 grid((unsigned)((e->v.G + 255) / 256), e->v.R);
   uint32_t all = 0;
   for (uint32_t s = 0; s < e->v.R; ++s) all |= s << (4 * s);
   k_serve_reads<<<grid, 256, 0, e->stream>>>(e->v, reads_per_ctx, key_space,
                                              all);
   HIPCHK(hipGetLastError());
+  e->reads_round = e->round;
+  e->reads_n = reads_per_ctx;
+  e->reads_ks = key_space;
   return DRB_OK;
 }
 
@@ -2705,4 +2869,174 @@ extern "C" int drb_tan_buffers(drb_engine *e, void **bytes, void **recs) {
   *bytes = e->v.save_buf;
   *recs = e->v.tan_rec;
   return DRB_OK;
+}
+
+// ------------------------------------------------ batched round outputs
+// The round's ReadyToReads and served-read results of one replica slot
+// over a range of groups, compacted on the device: a per-lane record count,
+// an exclusive scan (hipCUB), then each lane writes its records at its
+// offset -- node.processReadyToRead (node.go:1081) and the clients'
+// ReadLocalNode results (nodehost.go:849) for a whole step worker's groups
+// without a device round trip per group.
+namespace {
+enum BatchKind : uint32_t { BK_RTR = 0, BK_READS = 1 };
+}
+
+// records of lane g of the range: ReadyToReads, or served reads (bit k of
+// read_served for ctx k < rtr_count, n_reads each)
+__global__ void k_batch_count(const View v, uint32_t slot, uint64_t g0,
+                              uint64_t n, uint32_t kind, uint32_t n_reads,
+                              uint32_t *cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  uint32_t c = 0;
+  if (i < n) {
+    const uint64_t g = g0 + i;
+    const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+    if (kind == BK_RTR) {
+      c = nr;
+    } else if (nr) {
+      const uint32_t m = v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u);
+      c = (uint32_t)__popc(m) * n_reads;
+    }
+  }
+  cnt[i] = c;  // cnt[n] = 0: the scan's last element is the total
+}
+
+__global__ void k_batch_rtr(const View v, uint32_t slot, uint64_t g0,
+                            uint64_t n, const uint32_t *off,
+                            drb_ready_to_read *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t g = g0 + i;
+  const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+  uint64_t o = off[i];
+  for (uint32_t k = 0; k < nr; ++k, ++o) {
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    const uint4 c1 = v.rtr[rtr_ix(v, slot, k, 1, g)];
+    drb_ready_to_read r;
+    r.shard_id = v.first_shard_id + gid(v, slot, g);
+    r.replica_id = slot + 1;
+    r.index = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+    r.ctx_low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
+    r.ctx_high = (uint64_t)c1.x | ((uint64_t)c1.y << 32);
+    out[o] = r;
+  }
+}
+
+__global__ void k_batch_reads(const View v, uint32_t slot, uint64_t g0,
+                              uint64_t n, uint32_t n_reads,
+                              uint32_t key_space, const uint32_t *off,
+                              drb_read_result *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t g = g0 + i;
+  const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+  if (!nr) return;
+  const uint32_t m = v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u);
+  uint64_t o = off[i];
+  for (uint32_t k = 0; k < nr; ++k) {
+    if (!((m >> k) & 1u)) continue;
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    const uint4 c1 = v.rtr[rtr_ix(v, slot, k, 1, g)];
+    const uint64_t low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
+    for (uint32_t j = 0; j < n_reads; ++j, ++o) {
+      const uint2 w = v.read_res[rres_ix(v, slot, k, j, g)];
+      const uint64_t x =
+          mix64(low ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
+      drb_read_result r;
+      r.shard_id = v.first_shard_id + gid(v, slot, g);
+      r.index = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+      r.ctx_low = low;
+      r.ctx_high = (uint64_t)c1.x | ((uint64_t)c1.y << 32);
+      r.key = x % key_space;  // serve_reads_lane's key (drb_step.hpp)
+      r.replica_id = slot + 1;
+      r.read = j;
+      r.found = w.y >> 31;
+      r.vlen = w.y & 0x7fffffffu;
+      r.value = w.x;
+      r.pad = 0;
+      out[o] = r;
+    }
+  }
+}
+
+static int xout(drb_engine *e, size_t bytes, void **p) {
+  if (bytes > e->xout_bytes) {
+    if (e->xout) HIPCHK(hipFree(e->xout));
+    e->xout = nullptr;
+    e->xout_bytes = 0;
+    HIPCHK(hipMalloc(&e->xout, bytes));
+    e->xout_bytes = bytes;
+  }
+  *p = e->xout;
+  return DRB_OK;
+}
+
+static int batch_export(drb_engine *e, uint32_t slot, uint64_t first,
+                        uint64_t n, uint32_t kind, void *out, size_t rec,
+                        size_t cap, size_t *n_out) {
+  if (!e || !n_out || (cap && !out)) return DRB_EINVAL;
+  if (slot >= e->v.R || check_range(e, first, n)) return DRB_ERANGE;
+  *n_out = 0;
+  const uint32_t n_reads = kind == BK_READS ? e->reads_n : 0;
+  // reads: only the last round's, and only if that round served them
+  if (kind == BK_READS && (!e->v.read_res || e->reads_round != e->round))
+    return e->v.read_res ? DRB_OK : DRB_EINVAL;
+  const View &v = e->v;
+  // scratch: counts and offsets [n + 1] each, then the scan's temp storage
+  size_t tb = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr,
+                                          (uint32_t *)nullptr, (int)(n + 1),
+                                          e->stream));
+  const size_t a = ((n + 1) * 4 + 255) & ~(size_t)255;
+  void *s;
+  if (scratch(e, 2 * a + tb + 256, &s)) return DRB_EDEVICE;
+  uint32_t *cnt = (uint32_t *)s;
+  uint32_t *off = (uint32_t *)((char *)s + a);
+  void *tmp = (char *)s + 2 * a;
+  const unsigned blocks = (unsigned)((n + 1 + 255) / 256);
+  k_batch_count<<<blocks, 256, 0, e->stream>>>(v, slot, first, n, kind,
+                                               n_reads, cnt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)(n + 1),
+                                          e->stream));
+  uint32_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, off + n, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *n_out = total;
+  if (total > cap) return DRB_ERANGE;
+  if (!total) return DRB_OK;
+  void *d;
+  if (xout(e, (size_t)total * rec, &d)) return DRB_EDEVICE;
+  const unsigned wb = (unsigned)((n + 255) / 256);
+  if (kind == BK_RTR)
+    k_batch_rtr<<<wb, 256, 0, e->stream>>>(v, slot, first, n, off,
+                                           (drb_ready_to_read *)d);
+  else
+    k_batch_reads<<<wb, 256, 0, e->stream>>>(v, slot, first, n, n_reads,
+                                             e->reads_ks, off,
+                                             (drb_read_result *)d);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, d, (size_t)total * rec, hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
+}
+
+extern "C" int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
+                                               uint64_t first_group,
+                                               uint64_t n_groups,
+                                               drb_ready_to_read *out,
+                                               size_t cap, size_t *n_out) {
+  return batch_export(e, slot, first_group, n_groups, BK_RTR, out,
+                      sizeof(drb_ready_to_read), cap, n_out);
+}
+
+extern "C" int drb_export_read_results(drb_engine *e, uint32_t slot,
+                                       uint64_t first_group, uint64_t n_groups,
+                                       drb_read_result *out, size_t cap,
+                                       size_t *n_out) {
+  return batch_export(e, slot, first_group, n_groups, BK_READS, out,
+                      sizeof(drb_read_result), cap, n_out);
 }

@@ -411,10 +411,14 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
     const bool zero = (c0.x & MF_TERM_ZERO) != 0;
     bool other = false;
     if (!zero) {
-      if (!(cur.y & MI_TERM)) {
+      // a pre-vote record carries a term of its own (r.term + 1 or the
+      // granted one, not the sender's): it never seeds the header's term
+      // and always travels with its own (as the GPU's emit writes them)
+      const bool pv = is_prevote_type(m.type);
+      if (!pv && !(cur.y & MI_TERM)) {
         cur.z = (uint32_t)m.term;
         cur.w = (uint32_t)(m.term >> 32);
-      } else if (q_hi(cur) != m.term) {
+      } else if (pv || q_hi(cur) != m.term) {
         other = true;
         c0.x |= MF_TERM_OTHER;
         if (v.rterm) v.rterm[rterm_ix(v, buf, from, to, kk, g)] = m.term;
@@ -631,6 +635,27 @@ struct IngestTrace {
   }
 };
 
+// A transport's own pinned receive buffer (one per connection / thread):
+// drb_ingest_wire reads it while the caller holds it, and no other caller
+// can grow or free it.
+extern "C" int drb_ingest_buffer_alloc(drb_engine *e, size_t cap,
+                                       uint8_t **buf) {
+  if (!e || !buf || !cap) return DRB_EINVAL;
+  *buf = nullptr;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(hipHostMalloc((void **)buf, cap, hipHostMallocDefault));
+  return DRB_OK;
+}
+
+extern "C" int drb_ingest_buffer_free(drb_engine *e, uint8_t *buf) {
+  if (!e) return DRB_EINVAL;
+  if (buf) {
+    // a drb_ingest_wire of this buffer has synchronised before returning
+    HIPCHK(hipHostFree(buf));
+  }
+  return DRB_OK;
+}
+
 extern "C" int drb_ingest_buffer(drb_engine *e, size_t cap, uint8_t **buf) {
   if (!e || !buf) return DRB_EINVAL;
   std::lock_guard<std::mutex> lock(e->ingest_mu);
@@ -703,6 +728,13 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (ing_grow(st.stream, sb)) return DRB_EDEVICE;
   uint8_t *ds = (uint8_t *)st.stream.p;
   hipStream_t sm = e->stream;
+  // once the upload is enqueued, every return waits for the engine stream
+  // first: the caller may reuse or refill `stream` (a pinned buffer is
+  // read by the DMA engine asynchronously) as soon as this call returns
+  struct SyncOnReturn {
+    hipStream_t s;
+    ~SyncOnReturn() { (void)hipStreamSynchronize(s); }
+  } sync_on_return{e->stream};
   // 2. the stream goes up (its own host thread: a pageable source makes
   // the copy synchronous) while Requests boundaries are found, one host
   // thread per frame (a frame holds up to 64 MiB of messages), at most 16

@@ -15,6 +15,13 @@ namespace drb {
 // the tan select pass's replica lists (drb_tan.hpp)
 constexpr uint32_t TAN_LISTS = 64;
 
+__host__ __device__ inline uint64_t lo64(uint4 q) {
+  return (uint64_t)q.x | ((uint64_t)q.y << 32);
+}
+__host__ __device__ inline uint64_t hi64(uint4 q) {
+  return (uint64_t)q.z | ((uint64_t)q.w << 32);
+}
+
 // splitmix64 finaliser: seeded synthetic inputs and the served-read keys
 __host__ __device__ inline uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -314,6 +321,12 @@ struct View {
   uint4 *rtr;             // [R][RTR_CAP][G] x 2 chunks {index, low},{high,0}
   uint32_t *rtr_count;    // [R][G]
   uint64_t *read_sum;     // [R][G] served-read checksum (drb_serve_reads)
+  // served-read results (drb_config.max_reads_per_ctx > 0): [R][RTR_CAP]
+  // [max_reads][G] {LE32 value, vlen | found << 31}, and per replica the
+  // ReadyToReads whose reads were served (bit k)
+  uint2 *read_res;
+  uint32_t *read_served;  // [R][G]
+  uint32_t max_reads;
   uint4 *save_buf;        // [R][G][save_cap16] EntryBatch of EntriesToSave
   uint32_t *save_len;     // [R][G] bytes (0: nothing saved)
   uint32_t *save_crc;     // [R][G] CRC32-IEEE of those bytes
@@ -477,6 +490,11 @@ __host__ __device__ inline uint64_t prop_ix(const View &v, uint32_t ps,
                                             uint64_t g) {
   return (((uint64_t)ps * v.max_props + j) * (PROP_META + v.C16) + chunk) *
              v.G + g;
+}
+__host__ __device__ inline uint64_t rres_ix(const View &v, uint32_t slot,
+                                            uint32_t k, uint32_t j,
+                                            uint64_t g) {
+  return (((uint64_t)slot * RTR_CAP + k) * v.max_reads + j) * v.G + g;
 }
 __host__ __device__ inline uint64_t rtr_ix(const View &v, uint32_t slot,
                                            uint32_t k, uint32_t chunk,

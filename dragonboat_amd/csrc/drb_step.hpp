@@ -19,6 +19,7 @@
 #include "drb_codec.hpp"
 #include "drb_layout.hpp"
 #include "drb_msg.hpp"
+#include "drb_ring.hpp"
 
 namespace drb {
 
@@ -107,10 +108,9 @@ struct Rep {
   uint32_t role, flags, fb, ri_count;
   uint32_t votes;  // elections: answered | granted << 8, bit per slot
   // leader remotes live in LDS (RemLds), see rem_get/rem_put
-  // leader: readIndex queue
-  uint64_t ri_lo[DRB_RI_DEPTH], ri_hi[DRB_RI_DEPTH], ri_ix[DRB_RI_DEPTH],
-      ri_fr[DRB_RI_DEPTH];
-  uint32_t ri_cf[DRB_RI_DEPTH];
+  // leader: readIndex queue (the ctx of each entry in LDS, Lane.rq)
+  uint64_t ri_ix[DRB_RI_DEPTH];
+  uint32_t ri_fr[DRB_RI_DEPTH], ri_cf[DRB_RI_DEPTH];
   // round-local
   HintCtx hc;          // ctx dedup state of this sender (drb_msg.hpp)
   uint32_t nmsgs;
@@ -141,7 +141,9 @@ struct Lane {
   void *rl;       // RemLds<R> of this workgroup
   uint32_t *oi;   // [R][256] outbox header info per destination (LDS)
   uint64_t *elo;  // [R][256] leader: lowest entry index sent to a remote
-                  // follower this round (~0: none), LDS
+                  // follower this round (~0: none), LDS (placement C4)
+  uint64_t *rq;   // [2][DRB_RI_DEPTH][256] leader: the readIndex queue's
+                  // ctx {low, high} per entry, LDS
   uint32_t tid;   // lane within the workgroup
   const View *v;
   uint32_t slot;
@@ -152,11 +154,16 @@ struct Lane {
 };
 
 // ------------------------------------------------------------ helpers
+// the ctx of readIndex queue entry d (d a compile-time index)
+DRB_DEV uint64_t &rq_lo(const Lane &L, int d) {
+  return L.rq[(uint32_t)d * 256 + L.tid];
+}
+DRB_DEV uint64_t &rq_hi(const Lane &L, int d) {
+  return L.rq[(uint32_t)(DRB_RI_DEPTH + d) * 256 + L.tid];
+}
 DRB_DEV uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 DRB_DEV uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
-DRB_DEV uint64_t lo64(uint4 q) { return (uint64_t)q.x | ((uint64_t)q.y << 32); }
-DRB_DEV uint64_t hi64(uint4 q) { return (uint64_t)q.z | ((uint64_t)q.w << 32); }
 
 template <int R>
 DRB_DEV void set_error(Rep<R> &r, uint32_t reason) {
@@ -520,8 +527,8 @@ DRB_DEV void broadcast_heartbeat(const Lane &L, Rep<R> &r) {
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d)
     if ((uint32_t)d + 1 == r.ri_count) {  // peepCtx: last queued
-      lo = r.ri_lo[d];
-      hi = r.ri_hi[d];
+      lo = rq_lo(L, d);
+      hi = rq_hi(L, d);
     }
   broadcast_heartbeat_hint(L, r, lo, hi);
 }
@@ -569,12 +576,12 @@ DRB_DEV void add_ready(const Lane &L, Rep<R> &r, uint64_t index, uint64_t lo,
 
 // readIndex.addRequest (readindex.go:43-66)
 template <int R>
-DRB_DEV void ri_add_request(Rep<R> &r, uint64_t index, uint64_t lo,
-                            uint64_t hi, uint64_t from) {
+DRB_DEV void ri_add_request(const Lane &L, Rep<R> &r, uint64_t index,
+                            uint64_t lo, uint64_t hi, uint64_t from) {
   bool found = false;
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d)
-    if ((uint32_t)d < r.ri_count && r.ri_lo[d] == lo && r.ri_hi[d] == hi)
+    if ((uint32_t)d < r.ri_count && rq_lo(L, d) == lo && rq_hi(L, d) == hi)
       found = true;
   if (found) return;
   uint64_t tail_index = 0;
@@ -592,10 +599,10 @@ DRB_DEV void ri_add_request(Rep<R> &r, uint64_t index, uint64_t lo,
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d)
     if ((uint32_t)d == r.ri_count) {
-      r.ri_lo[d] = lo;
-      r.ri_hi[d] = hi;
+      rq_lo(L, d) = lo;
+      rq_hi(L, d) = hi;
       r.ri_ix[d] = index;
-      r.ri_fr[d] = from;
+      r.ri_fr[d] = (uint32_t)from;
       r.ri_cf[d] = 0;
     }
   r.ri_count++;
@@ -609,8 +616,8 @@ DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
   int pos = -1;
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d)
-    if (pos < 0 && (uint32_t)d < r.ri_count && r.ri_lo[d] == lo &&
-        r.ri_hi[d] == hi)
+    if (pos < 0 && (uint32_t)d < r.ri_count && rq_lo(L, d) == lo &&
+        rq_hi(L, d) == hi)
       pos = d;
   if (pos < 0) return;
   uint32_t cf = 0;
@@ -633,7 +640,7 @@ DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
     if (r.ri_ix[d] > sidx) set_error(r, DRB_ERR_READINDEX);
     uint64_t fr = r.ri_fr[d];
     if (fr == 0 || fr == (uint64_t)L.slot + 1) {
-      add_ready(L, r, sidx, r.ri_lo[d], r.ri_hi[d]);
+      add_ready(L, r, sidx, rq_lo(L, d), rq_hi(L, d));
     } else {
       Msg m = {};
       m.type = DRB_MSG_READ_INDEX_RESP;
@@ -647,19 +654,19 @@ DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
   uint32_t done = (uint32_t)pos + 1;
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d) {
-    uint64_t nl = 0, nh = 0, ni = 0, nf = 0;
-    uint32_t nc = 0;
+    uint64_t nl = 0, nh = 0, ni = 0;
+    uint32_t nf = 0, nc = 0;
 #pragma unroll
     for (int e = 0; e < DRB_RI_DEPTH; ++e)
       if ((uint32_t)e == (uint32_t)d + done) {
-        nl = r.ri_lo[e];
-        nh = r.ri_hi[e];
+        nl = rq_lo(L, e);
+        nh = rq_hi(L, e);
         ni = r.ri_ix[e];
         nf = r.ri_fr[e];
         nc = r.ri_cf[e];
       }
-    r.ri_lo[d] = nl;
-    r.ri_hi[d] = nh;
+    rq_lo(L, d) = nl;
+    rq_hi(L, d) = nh;
     r.ri_ix[d] = ni;
     r.ri_fr[d] = nf;
     r.ri_cf[d] = nc;
@@ -738,7 +745,7 @@ DRB_DEV void leader_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
       r.ndropped_ri++;  // reportDroppedReadIndex
       return;
     }
-    ri_add_request(r, r.committed, lo, hi, from);
+    ri_add_request(L, r, r.committed, lo, hi, from);
     broadcast_heartbeat_hint(L, r, lo, hi);
   } else {
     add_ready(L, r, r.committed, lo, hi);
@@ -1503,54 +1510,6 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
 // inmemory.go:116-122) encoded as one EntryBatch (entrybatch.go:25-58) of
 // colfer Entries (raft_optimized.go:166-300) straight from the resident
 // window, with its CRC32-IEEE.
-// The fields of window entry idx of replica (slot, g) as the encoder sees
-// them; `compact` zeroes Term and Index (compactBatchFields).
-DRB_DEV EntryHdr ring_entry_hdr(const View &v, uint32_t slot, uint64_t g,
-                                uint64_t idx, bool compact) {
-  const uint4 m0 = v.ring[ring_ix(v, slot, idx, 0, g)];
-  const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
-  const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
-  EntryHdr e;
-  e.term = compact ? 0 : lo64(m0);
-  e.index = compact ? 0 : idx;
-  e.key = hi64(m0);
-  e.client_id = lo64(m1);
-  e.series_id = hi64(m1);
-  e.responded_to = lo64(m2);
-  e.type = m2.z;
-  e.cmd_len = m2.w;
-  return e;
-}
-
-// Entry.marshalTo (raft_optimized.go:166-300) of e, its Cmd read from the
-// window chunk by chunk, into any byte sink O
-template <class O>
-DRB_DEV void emit_entry(O &o, const View &v, uint32_t slot, uint64_t g,
-                        uint64_t idx, const EntryHdr &e) {
-  colfer_u64(o, 0, e.term);
-  colfer_u64(o, 1, e.index);
-  if (e.type != 0) {
-    bo_byte(o, 2);
-    bo_varint(o, e.type);
-  }
-  colfer_u64(o, 3, e.key);
-  colfer_u64(o, 4, e.client_id);
-  colfer_u64(o, 5, e.series_id);
-  colfer_u64(o, 6, e.responded_to);
-  if (e.cmd_len != 0) {
-    bo_byte(o, 7);
-    bo_varint(o, e.cmd_len);
-    for (uint32_t c = 0; c * 16 < e.cmd_len; ++c) {
-      const uint4 q = v.ring[ring_ix(v, slot, idx, ENT_META + c, g)];
-      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (uint32_t b = 0; b < 16; ++b)
-        if (c * 16 + b < e.cmd_len) bo_byte(o, w[b >> 2] >> (8 * (b & 3)));
-    }
-  }
-  bo_byte(o, 0x7f);
-}
-
 // One EntryBatch.Entries element of window entry idx; `compact` writes it
 // with Term and Index zero (compactBatchFields, logdb/batch.go:100-113).
 DRB_DEV void encode_entry(ByteOut &o, const Lane &L, uint64_t idx,
@@ -1693,12 +1652,14 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
   const uint4 *tbl = v.kv + kv_ix(v, slot, g, 0);
   const bool ks_pow2 = (key_space & (key_space - 1)) == 0;
   uint64_t sum = 0;
+  uint32_t served_mask = 0;
   for (uint32_t k = 0; k < nrtr; ++k) {
     const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
     if (lo64(c0) > sm_index) {  // pendingReadIndex: index not applied yet
       deferred += n_reads;
       continue;
     }
+    served_mask |= 1u << k;
     const uint64_t low = hi64(c0);
     for (uint32_t j0 = 0; j0 < n_reads; j0 += READ_BATCH) {
       uint64_t key[READ_BATCH];
@@ -1735,10 +1696,16 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
           w = kv_probe_word(v, tbl, ks[t], 2, key[t], 8);
         sum += mix64(w ^ key[t] ^ ((uint64_t)j << 56));
         served++;
+        if (v.read_res)  // ReadLocalNode's result for the client
+          v.read_res[rres_ix(v, slot, k, j, g)] =
+              w == ~0ull ? make_uint2(0, 0)
+                         : make_uint2((uint32_t)w,
+                                      (uint32_t)(w >> 32) | 0x80000000u);
       }
     }
   }
   v.read_sum[ix(v, slot, g)] = sum;
+  if (v.read_res) v.read_served[ix(v, slot, g)] = served_mask;
 }
 
 // ------------------------------------------------------------ load/store
@@ -1789,13 +1756,15 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
     if (LEAD && (uint32_t)d < r.ri_count) {
       uint4 c = v.ri_ctx[ri_ix(v, L.slot, d, L.g)];
       uint4 i = v.ri_idx[ri_ix(v, L.slot, d, L.g)];
-      r.ri_lo[d] = lo64(c);
-      r.ri_hi[d] = hi64(c);
+      rq_lo(L, d) = lo64(c);
+      rq_hi(L, d) = hi64(c);
       r.ri_ix[d] = lo64(i);
-      r.ri_fr[d] = hi64(i);
+      r.ri_fr[d] = (uint32_t)hi64(i);
       r.ri_cf[d] = v.ri_conf[ri_ix(v, L.slot, d, L.g)];
     } else {
-      r.ri_lo[d] = r.ri_hi[d] = r.ri_ix[d] = r.ri_fr[d] = 0;
+      if (LEAD) rq_lo(L, d) = rq_hi(L, d) = 0;
+      r.ri_ix[d] = 0;
+      r.ri_fr[d] = 0;
       r.ri_cf[d] = 0;
     }
   }
@@ -1855,7 +1824,7 @@ DRB_DEV void store_rep(const Lane &L, Rep<R> &r, uint32_t flags0,
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d) {
     if ((uint32_t)d >= r.ri_count) continue;
-    v.ri_ctx[ri_ix(v, L.slot, d, L.g)] = mk4(r.ri_lo[d], r.ri_hi[d]);
+    v.ri_ctx[ri_ix(v, L.slot, d, L.g)] = mk4(rq_lo(L, d), rq_hi(L, d));
     v.ri_idx[ri_ix(v, L.slot, d, L.g)] = mk4(r.ri_ix[d], r.ri_fr[d]);
     v.ri_conf[ri_ix(v, L.slot, d, L.g)] = r.ri_cf[d];
   }
@@ -2084,7 +2053,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
-  __shared__ uint64_t elo_lds[LEAD ? R : 1][256];
+  __shared__ uint64_t rq_lds[LEAD ? 2 * DRB_RI_DEPTH : 1][256];
+  // placement C4 only: [R][256] (the launch sizes it, drb_step_inst.hip)
+  extern __shared__ uint64_t elo_dyn[];
+  uint64_t(*elo_lds)[256] = reinterpret_cast<uint64_t(*)[256]>(elo_dyn);
   if (EXT && p.encode_saves) {  // uniform: every thread reaches the barrier
     crc32_table_init(crc_tab, threadIdx.x);
     __syncthreads();
@@ -2092,7 +2064,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   Lane L;
   L.rl = &rl;
   L.oi = oinfo;
-  L.elo = &elo_lds[0][0];
+  L.elo = elo_dyn;
+  L.rq = &rq_lds[0][0];
   L.tid = threadIdx.x;
   L.v = vp;
   L.slot = slot;
@@ -2147,7 +2120,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       oinfo[s * 256 + threadIdx.x] = 0;
-      if (LEAD) elo_lds[LEAD ? s : 0][threadIdx.x] = ~0ull;
+      if (LEAD && v.remote_mask) elo_lds[s][threadIdx.x] = ~0ull;
     }
     r.c1mask = 0;
     r.hc.lo = r.hc.hi = 0;

@@ -27,7 +27,9 @@ void DRB_STEP_LAUNCH_NAME(DRB_INST_R, DRB_INST_KIND)(const View &v,
   constexpr bool LEAD = K == SK_LEAD || K == SK_LEAD_EXT || K == SK_SLOW;
   constexpr bool EXT = K == SK_LEAD_EXT || K == SK_FOLLOW_EXT || K == SK_SLOW;
   constexpr bool SLOW = K == SK_SLOW;
-  step_kernel<DRB_INST_R, LEAD, EXT, SLOW><<<grid, 256, 0, s>>>(v, p);
+  // the leader's per-remote entry-row floors (LDS) exist with placement C4
+  const size_t dyn = LEAD && v.remote_mask ? DRB_INST_R * 256 * 8 : 0;
+  step_kernel<DRB_INST_R, LEAD, EXT, SLOW><<<grid, 256, dyn, s>>>(v, p);
 }
 
 }  // namespace drb

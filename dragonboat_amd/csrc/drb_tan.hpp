@@ -20,7 +20,8 @@
 #pragma once
 #include "drb_codec.hpp"
 #include "drb_layout.hpp"
-#include "drb_step.hpp"  // ring_entry_hdr, emit_entry
+#include "../../include/drb_engine.h"
+#include "drb_ring.hpp"  // ring_entry_hdr, emit_entry
 
 namespace drb {
 

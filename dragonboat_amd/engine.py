@@ -50,6 +50,9 @@ SIGNATURES = {
     "drb_role_slots": (C.c_int, [P, PU32, PU32]),
     "drb_stage_proposals": (C.c_int, [P, U32, PU32, C.POINTER(Entry), PU8,
                                       SZ]),
+    "drb_stage_proposals_packed": (C.c_int, [P, U32, U32, PU8, U64, PU64,
+                                             PU64, C.POINTER(C.c_uint16),
+                                             PU8, SZ]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
     "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
                                               U64, U32]),
@@ -73,6 +76,12 @@ SIGNATURES = {
     "drb_export_ready_to_reads": (C.c_int, [P, U64, U32,
                                             C.POINTER(ReadyToRead), SZ,
                                             C.POINTER(SZ)]),
+    "drb_export_ready_to_reads_batch": (C.c_int, [P, U32, U64, U64,
+                                                  C.POINTER(ReadyToRead), SZ,
+                                                  C.POINTER(SZ)]),
+    "drb_export_read_results": (C.c_int, [P, U32, U64, U64,
+                                          C.POINTER(abi.ReadResult), SZ,
+                                          C.POINTER(SZ)]),
     "drb_serve_reads": (C.c_int, [P, U32, U32]),
     "drb_export_read_sums": (C.c_int, [P, U64, U64, PU64]),
     "drb_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32, PU32]),
@@ -102,6 +111,8 @@ SIGNATURES = {
     "drb_export_wire": (C.c_int, [P, PU8, SZ, C.POINTER(SZ)]),
     "drb_ingest_wire": (C.c_int, [P, PU8, SZ, U64, C.POINTER(WireIn)]),
     "drb_ingest_buffer": (C.c_int, [P, SZ, C.POINTER(PU8)]),
+    "drb_ingest_buffer_alloc": (C.c_int, [P, SZ, C.POINTER(PU8)]),
+    "drb_ingest_buffer_free": (C.c_int, [P, PU8]),
 }
 
 
@@ -146,7 +157,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
-                tan_multiplexed=0, pre_vote=0)
+                tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0)
 
 
 class Engine:
@@ -167,7 +178,8 @@ class Engine:
                    cfg["flagged_cap"], cfg["quiesce"],
                    cfg["durable_log"], cfg["save_batched"],
                    cfg["save_tan"], cfg["elections"], cfg["tan_max_log"],
-                   cfg["tan_multiplexed"], cfg["pre_vote"])
+                   cfg["tan_multiplexed"], cfg["pre_vote"],
+                   cfg["max_reads_per_ctx"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -253,6 +265,15 @@ class Engine:
             pool_len = C.sizeof(pool)
         _ck(lib().drb_stage_proposals(self.h, slot, counts, ents, pool,
                                       pool_len), "drb_stage_proposals")
+
+    def stage_proposals_packed(self, slot, type, counts, n, keys, clients,
+                               lens, pool, pool_len):
+        """drb_stage_proposals_packed; the arrays are ctypes pointers (or
+        arrays): counts u8[G], keys / clients u64[n], lens u16[n]."""
+        _ck(lib().drb_stage_proposals_packed(self.h, slot, type, counts, n,
+                                             keys, clients, lens, pool,
+                                             pool_len),
+            "drb_stage_proposals_packed")
 
     def gen_kv_proposals(self, slot, k, key_space, val_len, seed, salt,
                          active_ppm=1000000):
@@ -358,6 +379,43 @@ class Engine:
             "drb_export_ready_to_reads")
         return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high)
                 for i in range(min(n.value, cap))]
+
+    def _batch(self, fn, typ, slot, first_group, n_groups, cap):
+        n_groups = self.G - first_group if n_groups is None else n_groups
+        n = SZ()
+        arr = (typ * max(1, cap))()
+        rc = fn(self.h, slot, first_group, n_groups, arr, cap, C.byref(n))
+        if rc == abi.DRB_ERANGE and n.value > cap:  # sized by the count
+            arr = (typ * n.value)()
+            rc = fn(self.h, slot, first_group, n_groups, arr, n.value,
+                    C.byref(n))
+        _ck(rc, fn.__name__)
+        return arr, n.value
+
+    def export_ready_batch(self, slot, first_group=0, n_groups=None,
+                           cap=1 << 16):
+        """{group: [(index, ctx_low, ctx_high)]} of replica slot's
+        ReadyToReads of the last round (drb_export_ready_to_reads_batch)."""
+        arr, n = self._batch(lib().drb_export_ready_to_reads_batch,
+                             ReadyToRead, slot, first_group, n_groups, cap)
+        out = {}
+        base = self.cfg["first_shard_id"]
+        for i in range(n):
+            r = arr[i]
+            out.setdefault(r.shard_id - base, []).append(
+                (r.index, r.ctx_low, r.ctx_high))
+        return out
+
+    def export_read_results(self, slot, first_group=0, n_groups=None,
+                            cap=1 << 16):
+        """[(group, index, ctx_low, read j, key, found, vlen, value)] of the
+        reads replica slot served in the last round (drb_export_read_
+        results)."""
+        arr, n = self._batch(lib().drb_export_read_results, abi.ReadResult,
+                             slot, first_group, n_groups, cap)
+        base = self.cfg["first_shard_id"]
+        return [(r.shard_id - base, r.index, r.ctx_low, r.read, r.key,
+                 r.found, r.vlen, r.value) for r in arr[:n]]
 
     def kv_export(self, g, slot):
         cap = self.cfg["kv_slots"]
@@ -526,6 +584,18 @@ class Engine:
             "drb_ingest_buffer")
         C.memmove(ptr, bytes(data), len(data))
         return ptr
+
+    def ingest_buffer_alloc(self, cap):
+        """A pinned receive buffer of this caller's own
+        (drb_ingest_buffer_alloc); free it with ingest_buffer_free."""
+        ptr = PU8()
+        _ck(lib().drb_ingest_buffer_alloc(self.h, max(1, cap), C.byref(ptr)),
+            "drb_ingest_buffer_alloc")
+        return ptr
+
+    def ingest_buffer_free(self, ptr):
+        _ck(lib().drb_ingest_buffer_free(self.h, ptr),
+            "drb_ingest_buffer_free")
 
     def ingest_wire_pinned(self, ptr, n, deployment_id=0):
         """drb_ingest_wire of n bytes already in the pinned buffer."""

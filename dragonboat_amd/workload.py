@@ -154,3 +154,35 @@ def active_groups(num_groups, seed, salt, active_ppm, gids=None):
             if mix64(seed ^ ACTIVE_SALT ^
                      (((g if gids is None else gids[g]) * GOLDEN) & MASK) ^
                      ((salt << 24) & MASK)) % 1000000 < active_ppm]
+
+
+def pack_batch(num_groups, k, counts, ents, pool):
+    """A build_batch batch (NoOP-session entries) in the packed form of
+    drb_stage_proposals_packed: (counts u8[G], keys u64[n], clients u64[n],
+    lens u16[n], pool bytes), entries group by group."""
+    cnt = (C.c_uint8 * max(1, num_groups))()
+    keys, cids, lens, out = [], [], [], bytearray()
+    pb = bytes(pool)
+    for g in range(num_groups):
+        cnt[g] = counts[g]
+        for j in range(counts[g]):
+            e = ents[g * k + j]
+            keys.append(e.key)
+            cids.append(e.client_id)
+            lens.append(e.cmd_len)
+            out += pb[e.cmd_off:e.cmd_off + e.cmd_len]
+    n = len(keys)
+    return (cnt, n, (C.c_uint64 * max(1, n))(*keys),
+            (C.c_uint64 * max(1, n))(*cids), (C.c_uint16 * max(1, n))(*lens),
+            (C.c_uint8 * max(1, len(out))).from_buffer_copy(bytes(out) or
+                                                            b"\0"), len(out))
+
+
+def build_packed_np(num_groups, seed, salt, key_space=256):
+    """build_batch_np's batch in the packed form (numpy arrays): what a
+    host uploads per round with drb_stage_proposals_packed."""
+    import numpy as np
+    counts, ents, pool = build_batch_np(num_groups, seed, salt, key_space)
+    return (counts.astype(np.uint8), np.ascontiguousarray(ents["key"]),
+            np.ascontiguousarray(ents["client_id"]),
+            ents["cmd_len"].astype(np.uint16), pool)

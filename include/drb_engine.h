@@ -36,9 +36,13 @@
  *
  * Threading: drb_ingest / drb_ingest_wire may be called from several
  * transport threads at once (each call stages under the engine's ingest
- * lock); every other entry point is driven by one host thread, which is
- * not re-entrant (the reference holds node.raftMu across stepNode,
- * node.go:1140).
+ * lock, which drb_step_round* also takes while it launches a round and
+ * advances the round number, so a message lands either before a round's
+ * launch -- read by that round -- or after it, read by the next); each
+ * such thread reads its connection into a buffer of its own
+ * (drb_ingest_buffer_alloc).  Every other entry point is driven by one
+ * host thread, which is not re-entrant (the reference holds node.raftMu
+ * across stepNode, node.go:1140).
  */
 #ifndef DRB_ENGINE_H
 #define DRB_ENGINE_H
@@ -354,6 +358,12 @@ typedef struct drb_config {
    * (preVoteCampaign, raft.go:1149-1174; handleNodeRequestPreVote,
    * :1670-1695; the preVoteCandidate handlers, :2256-2276) */
   uint32_t pre_vote;
+  /* > 0: the reads served behind each ReadyToRead (drb_round_in.
+   * reads_per_ctx <= this, drb_serve_reads) also leave one result per read
+   * -- found, value length, value -- that drb_export_read_results hands to
+   * the clients' ReadLocalNode calls; 0: only the per-replica checksum
+   * (drb_export_read_sums) */
+  uint32_t max_reads_per_ctx;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -478,6 +488,23 @@ int drb_init_steady(drb_engine *e, uint64_t term, uint32_t leader_slot,
 int drb_stage_proposals(drb_engine *e, uint32_t slot, const uint32_t *counts,
                         const drb_entry *ents, const uint8_t *pool,
                         size_t pool_len);
+/* The same for a batch of NoOP-session entries (SeriesID = RespondedTo = 0,
+ * every entry of Type `type`: client.go NoOPSession, request.go:1085-1096)
+ * in the packed form a host builds its per-round upload in: counts[g]
+ * entries for group g (g ascending, counts[g] <= max_props), and per entry
+ * -- group by group, in queue order -- its Key, ClientID and Cmd length,
+ * the Cmd bytes back to back in pool (pool_len = the sum of the lengths).
+ * 1 + n x 18 + pool bytes cross the host link instead of drb_entry rows:
+ * 36 B per group at C3 (16 B PBKV writes) against 85 B.  Offsets are
+ * scanned and the entries laid out on the device, ordered and overlapped
+ * as drb_stage_proposals; DRB_EINVAL when the counts or lengths do not add
+ * up. */
+int drb_stage_proposals_packed(drb_engine *e, uint32_t slot, uint32_t type,
+                               const uint8_t *counts, uint64_t n_entries,
+                               const uint64_t *keys,
+                               const uint64_t *client_ids,
+                               const uint16_t *cmd_lens, const uint8_t *pool,
+                               size_t pool_len);
 /* Device-side synthetic proposal generator (bench / SURVEY 8d inputs):
  * k KVTest PBKV writes per group, NoOP session, EncodedEntry v0. */
 int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,
@@ -495,6 +522,9 @@ int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot, uint32_t k,
  * node.go:1296). */
 int drb_stage_read_index(drb_engine *e, uint32_t slot, const uint64_t *ctx_low,
                          const uint64_t *ctx_high);
+/* Device-side synthetic ReadIndex ctx per group (bench / SURVEY 8d):
+ * ctx = {mix64(seed ^ RI ^ g * GOLDEN ^ high << 40) | 1, high}
+ * (dragonboat_amd/workload.py read_index_ctx with salt = high). */
 int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
                        uint64_t high);
 
@@ -556,6 +586,46 @@ int drb_export_outbox(drb_engine *e, uint64_t group, uint32_t from_slot,
 int drb_export_ready_to_reads(drb_engine *e, uint64_t group, uint32_t slot,
                               drb_ready_to_read *out, size_t cap,
                               size_t *n_out);
+
+/* pb.Update.ReadyToReads of the last round for replica slot `slot` of
+ * groups [first_group, first_group + n_groups), compacted on the device:
+ * the records of node.processReadyToRead (node.go:1081 ->
+ * pendingReadIndex.addReady, request.go:883) for a whole step worker's
+ * groups in one call -- in group order, each replica's in release order.
+ * *n_out is the count (DRB_ERANGE with nothing copied if more than cap).
+ * Two device-to-host copies (the count, then the records). */
+int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
+                                    uint64_t first_group, uint64_t n_groups,
+                                    drb_ready_to_read *out, size_t cap,
+                                    size_t *n_out);
+
+/* One ReadLocalNode result (nodehost.go:849 -> KVTest.Lookup,
+ * kvtest.go:164-175) of the reads served behind a ReadyToRead: the read's
+ * ctx and position, its key and what the lookup found.  value holds the
+ * value's first 4 bytes little-endian (all of it when vlen <= 4, as at
+ * C3's 16 B writes); a longer value is read with drb_kv_lookup, valid until
+ * the next round. */
+typedef struct drb_read_result {
+  uint64_t shard_id;
+  uint64_t index;       /* the ReadyToRead's index (pendingReadIndex.applied) */
+  uint64_t ctx_low;
+  uint64_t ctx_high;
+  uint64_t key;         /* LE64 key looked up */
+  uint32_t replica_id;
+  uint32_t read;        /* j: the read's position in its ctx */
+  uint32_t found;       /* 1: the key is in the replica's KV */
+  uint32_t vlen;
+  uint32_t value;
+  uint32_t pad;
+} drb_read_result;
+/* The results of the reads served by replica slot `slot` of groups
+ * [first_group, first_group + n_groups) in the last round that served
+ * reads (its reads_per_ctx per released ctx; deferred ctx have none), in
+ * group order, then ctx order, then read order; compacted on the device.
+ * Needs drb_config.max_reads_per_ctx.  *n_out / DRB_ERANGE as above. */
+int drb_export_read_results(drb_engine *e, uint32_t slot, uint64_t first_group,
+                            uint64_t n_groups, drb_read_result *out,
+                            size_t cap, size_t *n_out);
 
 /*
  * Serves the linearizable reads behind the ReadyToReads of the last round:
@@ -852,6 +922,13 @@ int drb_ingest_wire(drb_engine *e, const uint8_t *stream, size_t len,
  * drb_ingest_wire has the stream uploaded by DMA at the link's rate
  * instead of through the driver's pageable staging. */
 int drb_ingest_buffer(drb_engine *e, size_t cap, uint8_t **buf);
+/* drb_ingest_buffer is the engine's one buffer, for a single transport
+ * thread (a later call with a larger cap replaces it).  Several transport
+ * threads each take a buffer of their own, pinned, and free it when their
+ * connection closes; drb_ingest_wire waits for its upload before
+ * returning, so a buffer may be refilled as soon as the call returns. */
+int drb_ingest_buffer_alloc(drb_engine *e, size_t cap, uint8_t **buf);
+int drb_ingest_buffer_free(drb_engine *e, uint8_t *buf);
 
 #ifdef __cplusplus
 }

@@ -62,25 +62,45 @@ def _compare(eng, orc, gids, R, logs=True, saves=False):
 
 
 def test_fullsize_c3_sampled():
-    """C3 as bench.py runs it (8 staged batches from the device
-    generators, a LocalTick every round, 9 served reads per ctx)."""
-    G, R, NP = 1 << 20, 3, 8
+    """C3 as bench.py runs it: first rounds of fresh-key writes until each
+    replica's KV holds most of its group's 256 keys (SURVEY 8d's steady
+    state; bench.py --kv-fill), then rounds whose inputs -- a write with
+    fresh keys and a ReadIndex ctx per group -- come from the device
+    generators, a LocalTick every round, 9 served reads per ctx, which now
+    mostly find their key."""
+    G, R, NP, FILL = 1 << 20, 3, 8, 400
     eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                  max_props=1, prop_slots=NP, ri_slots=NP, mailbox=16,
                  kv_slots=512, kv_val_cap=4)
     eng.init_steady(term=2, leader_slot=0, seed=SEED)
-    for b in range(NP):
-        eng.gen_kv_proposals(b, 1, 256, 4, SEED, b)
-        eng.gen_read_index(b, SEED, b + 30)  # ctx salt: the round (1)
     gids = _sample(G)
     n = len(gids)
     orc = po.Cluster(n, R, seed=SEED, gids=gids)
     orc.setup_steady(0)
-    for r in range(24):
-        b = r % NP
-        counts, ents, pool = workload.build_batch(n, 1, SEED, b, gids=gids)
+    for r in range(FILL):
+        salt = (1 << 20) + r
+        counts, ents, pool = workload.build_batch(n, 1, SEED, salt,
+                                                  gids=gids)
         orc.stage_proposals(counts, 1, ents, pool)
-        lo, hi = workload.build_read_index(n, SEED, 1, b + 30, gids=gids)
+        eng.gen_kv_proposals(0, 1, 256, 4, SEED, salt)
+        orc.round(tick=True)
+        e = eng.step(tick=True, prop_slot=0)
+        assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
+    errs = _compare(eng, orc, gids, R)
+    assert not errs, ("fill", errs[:3])
+    keys = [len(orc.export_kv(i, s)) for i in range(0, n, 50)
+            for s in range(R)]
+    assert sum(keys) / len(keys) > 200  # ~ 256 (1 - e^(-400/256)) = 202
+    found = total = 0
+    for r in range(24):
+        b, salt = r % NP, (1 << 22) + r
+        eng.gen_kv_proposals(b, 1, 256, 4, SEED, salt)
+        eng.gen_read_index(b, SEED, salt + 30)
+        counts, ents, pool = workload.build_batch(n, 1, SEED, salt,
+                                                  gids=gids)
+        orc.stage_proposals(counts, 1, ents, pool)
+        lo, hi = workload.build_read_index(n, SEED, salt + 30, salt + 30,
+                                           gids=gids)
         orc.stage_read_index(lo, hi)
         o = orc.round(tick=True)
         e = eng.step(tick=True, prop_slot=b, ri_slot=b, reads_per_ctx=9,
@@ -98,6 +118,17 @@ def test_fullsize_c3_sampled():
         if r % 8 == 7:
             errs = _compare(eng, orc, gids, R)
             assert not errs, (r, errs[:3])
+    # the reads of a ctx look up keys that are (nearly always) present
+    for i in range(0, n, 97):
+        kv = orc.export_kv(i, 0)
+        for rr in range(4):
+            lo, _ = workload.read_index_ctx(SEED, gids[i], rr, rr)
+            for j in range(9):
+                key = workload.mix64(lo ^ ((j + 1) * workload.GOLDEN &
+                                           workload.MASK)) % 256
+                total += 1
+                found += key.to_bytes(8, "little") in kv
+    assert found > 0.7 * total
 
 
 def test_fullsize_five_replicas_sampled():
@@ -192,7 +223,8 @@ def test_fullsize_failover_sampled():
         b = r % NP
         counts, ents, pool = workload.build_batch(n, 1, SEED, b, gids=gids)
         orc.stage_proposals(counts, 1, ents, pool)
-        lo, hi = workload.build_read_index(n, SEED, 1, b + 30, gids=gids)
+        lo, hi = workload.build_read_index(n, SEED, b + 30, b + 30,
+                                           gids=gids)
         orc.stage_read_index(lo, hi)
         o = orc.round(tick=True)
         e = eng.step(tick=True, prop_slot=b, ri_slot=b)

@@ -75,7 +75,7 @@ def test_leader_sync_follower_log():
         assert fol.committed == fol.sm_index == lead.last_index
     # the cases that needed an overwrite (entries not in the leader's log)
     cut = [g for g in range(G) if any(x not in want for x in before[g])]
-    assert cut == [2, 3, 5]
+    assert cut == [2, 3, 4, 5]
 
 
 def _unhost(p, groups, slot, hosted=False):
@@ -129,7 +129,7 @@ def test_deposed_leader_log_overwritten(pre_vote):
     _unhost(p, E, 0, hosted=True)
     _rounds(p, 3, tick=False, ri=False)
     old = {g: p.eng.export(g, 0) for g in E}
-    old_log = {g: _log(p, g, 0) for g in E}
+    old_log = {g: _log(p, g, 0, 12) for g in E}
     for g in E:
         assert old[g].role == abi.LEADER and old[g].term == 2
         assert old[g].last_index == old[g].committed + (5 if g in E1 else 3)
@@ -142,30 +142,47 @@ def test_deposed_leader_log_overwritten(pre_vote):
         if all(any(p.eng.export(g, s).role == abi.LEADER for s in (1, 2))
                for g in E):
             break
-    _rounds(p, 4)  # writes under the new leaders
-    # the old leader returns
+    _rounds(p, 2)  # writes under the new leaders
+    # the old leader returns; no client writes meanwhile, so its log's
+    # changed region stays resident while it is compared
     _unhost(p, E, 0, hosted=True)
+    ci, new_t = {}, {}
     for _ in range(40):
-        _rounds(p, 1)
-        done = True
+        _rounds(p, 1, k=0)
         for g in E:
-            lead = [s for s in (1, 2) if p.eng.export(g, s).role == abi.LEADER]
-            if _log(p, g, 0) != _log(p, g, lead[0]):
-                done = False
-        if done:
+            if g in ci:
+                continue
+            ot = dict((i, t) for t, i in old_log[g])
+            st = p.eng.export(g, 0)
+            lo, hi = min(ot), min(max(ot), st.last_index)
+            cur = dict((i, t) for t, i in (
+                (e[0], e[1]) for e in p.eng.export_log(g, 0, lo, hi)))
+            changed = [i for i in cur if cur[i] != ot[i]]
+            if changed:
+                ci[g] = min(changed)
+                new_t[g] = cur[ci[g]]
+        if len(ci) == len(E) and all(
+                _log(p, g, 0, 8) == _log(p, g, _leader(p, g), 8) for g in E):
             break
     _rounds(p, 3)
     for g in E:
         st = p.eng.export(g, 0)
         assert st.role == abi.FOLLOWER and st.term >= 3
-        new_log = _log(p, g, 0)
-        # the first index whose entry changed: the conflict index
-        ot, nt = dict((i, t) for t, i in old_log[g]), \
-            dict((i, t) for t, i in new_log)
-        ci = min(i for i in ot if i in nt and ot[i] != nt[i])
-        assert nt[ci] >= 3 and ot[ci] == 2
+        # (writes go on: the follower may be a round behind the leader)
+        lo = st.last_index - 7
+        assert p.eng.export_log(g, 0, lo, st.last_index) == \
+            p.eng.export_log(g, _leader(p, g), lo, st.last_index)
+        # the conflict index: the first entry of the old leader's log that
+        # changed, a term-2 entry replaced by a term >= 3 one
+        assert new_t[g] >= 3 and dict(
+            (i, t) for t, i in old_log[g])[ci[g]] == 2
         m = old[g].marker_index
         if g in E1:
-            assert ci > m, (g, ci, m)   # keep [marker, ci), then append
+            assert ci[g] > m, (g, ci[g], m)   # keep [marker, ci), append
         else:
-            assert ci == m, (g, ci, m)  # replace from the marker
+            assert ci[g] == m, (g, ci[g], m)  # replace from the marker
+
+
+def _leader(p, g):
+    lead = [s for s in range(p.R) if p.eng.export(g, s).role == abi.LEADER]
+    return lead[-1]
