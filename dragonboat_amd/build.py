@@ -88,21 +88,29 @@ def _compile(args):
     return obj
 
 
-def build(force=False, verbose=False, out=None, defines=(), jobs=None):
-    """Builds the engine; `out`/`defines` build a tuning variant elsewhere
-    (its objects live in a directory of their own, keyed by the defines)."""
+def build(force=False, verbose=False, out=None, defines=(), jobs=None,
+          variant_r=(3,)):
+    """Builds the engine; `out`/`defines` build a tuning variant elsewhere:
+    the step kernels of R in variant_r with the defines (their objects in a
+    directory of their own, keyed by the defines), everything else from the
+    in-tree build."""
     target = LIB if out is None else out
     if out is None and not force and up_to_date():
         return LIB
     key = hashlib.sha1(" ".join(sorted(defines)).encode()).hexdigest()[:10]
-    objdir = os.path.join(LIBDIR, "obj" if not defines else "obj_" + key)
-    os.makedirs(objdir, exist_ok=True)
+    main_dir = os.path.join(LIBDIR, "obj")
+    var_dir = os.path.join(LIBDIR, "obj_" + key)
+    for d in (main_dir, var_dir if defines else main_dir):
+        os.makedirs(d, exist_ok=True)
     todo, objs = [], []
     for name, src, defs, deps in _units(defines):
-        obj = os.path.join(objdir, name)
+        var = bool(defines) and any(name.startswith("step_r%d_" % r)
+                                    for r in variant_r)
+        obj = os.path.join(var_dir if var else main_dir, name)
         objs.append(obj)
         if force or _stale(obj, deps):
-            todo.append((obj, src, list(defines) + defs, verbose))
+            todo.append((obj, src, (list(defines) if var else []) + defs,
+                         verbose))
     jobs = jobs or int(os.environ.get("DRB_BUILD_JOBS", 0)) or \
         max(1, min(16, os.cpu_count() or 1))
     # the longest translation units first
@@ -122,4 +130,16 @@ def build(force=False, verbose=False, out=None, defines=(), jobs=None):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))
+    # python build.py [--force] [-v] [--variant NAME -DX=1 ...]: a variant
+    # goes to tools/_bin/NAME.so (bench.py loads it with DRB_ENGINE_LIB)
+    args = sys.argv[1:]
+    if "--variant" in args:
+        i = args.index("--variant")
+        name, defs = args[i + 1], [a[2:] for a in args[i + 2:]
+                                   if a.startswith("-D")]
+        out = os.path.join(os.path.dirname(HERE), "tools", "_bin",
+                           name + ".so")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        print(build(verbose="-v" in args, out=out, defines=defs))
+    else:
+        print(build(force="--force" in args, verbose="-v" in args))

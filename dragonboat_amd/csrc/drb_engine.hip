@@ -217,9 +217,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   // (the tan write pass lists replicas by 32-bit lane number)
   if (cfg->save_tan && (uint64_t)cfg->num_replicas * cfg->num_groups > 0xffffffffull)
     return DRB_ERANGE;
-  // elections: the raft launch steps co-resident replicas, Quiesce off
-  if (cfg->elections && (cfg->place_world > 1 || cfg->quiesce))
-    return DRB_EINVAL;
+  // elections: the raft launch steps co-resident replicas
+  if (cfg->elections && cfg->place_world > 1) return DRB_EINVAL;
   // entry_mbox travels as the 8-bit E of the plane summary word
   // (block_plane_summary, DRB_PLANE_E)
   if (cfg->place_world > 1 &&
@@ -1810,7 +1809,7 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if (p.encode_saves && !e->v.save_cap16) return DRB_EINVAL;
   p.ri_replica = in->ri_replica;
   p.listed = in->listed ? 1 : 0;
-  if (p.listed && (e->v.remote_mask || e->v.elections)) return DRB_EINVAL;
+  if (p.listed && e->v.remote_mask) return DRB_EINVAL;
   if (e->v.elections)  // this round's slow list
     HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
   if (p.ri_replica > e->v.R || (p.ri_replica && e->v.place_world > 1))

@@ -468,22 +468,24 @@ __host__ __device__ inline uint64_t kv_ix(const View &v, uint32_t slot,
   return (((uint64_t)slot * v.G + g) * v.KS + ks) * v.KVW;
 }
 // KV probe sequence: the slot of probe t (0 <= t < KS) for home slot h.
-// The probes walk the home slot's 128 B line first, wrapping inside it,
-// then the following lines, so a lookup at load <= 1/2 nearly always
-// touches one line (with plain linear probing, 1 in 8 home slots is the
-// last of its line and the second probe lands on the next).  Tables are
-// 128 B aligned (KS * KVW * 16 B per replica).
+// The probes walk the home slot's 64 B group first, wrapping inside it,
+// then the following groups: one 64 B fetch -- HBM's access granule for a
+// random read (MI355X_MICROARCH.md; profiles/r02_kvline/calib.log) --
+// holds a lookup's first spl probes, and a lookup loads the whole group at
+// once (serve_reads_lane, apply_entry), so at the steady state's load of
+// about 1/2 it nearly always resolves in one memory round trip.  Tables
+// are 64 B aligned (KS * KVW * 16 B per replica).
 __host__ __device__ inline uint32_t kv_spl(const View &v) {
-  // slots per 128 B line: 8 / KVW when KVW is a power of two, else 1
-  return (v.KVW <= 8 && (v.KVW & (v.KVW - 1)) == 0 && v.KS >= 8 / v.KVW)
-             ? 8u / v.KVW
+  // slots per 64 B group: 4 / KVW when KVW is a power of two <= 4, else 1
+  return (v.KVW <= 4 && (v.KVW & (v.KVW - 1)) == 0 && v.KS >= 4 / v.KVW)
+             ? 4u / v.KVW
              : 1u;
 }
 __host__ __device__ inline uint32_t kv_probe(const View &v, uint32_t h,
                                              uint32_t t) {
   const uint32_t spl = kv_spl(v);
-  const uint32_t line = ((h / spl) + (t / spl)) & (v.KS / spl - 1);
-  return line * spl + ((h + t) & (spl - 1));
+  const uint32_t grp = ((h / spl) + (t / spl)) & (v.KS / spl - 1);
+  return grp * spl + ((h + t) & (spl - 1));
 }
 __host__ __device__ inline uint64_t prop_ix(const View &v, uint32_t ps,
                                             uint32_t j, uint32_t chunk,

@@ -51,11 +51,19 @@ namespace drb {
 // Measured at C3 (same box): W=1 1.016, 2 1.033, 4 1.063, 8 1.240 ms/round,
 // and kv_slots 1024 no faster than 512: the probe chains are not what the
 // KV accesses wait on (the random line fetches are)
+// (round 2, near-empty tables: W=1 1.016, 2 1.033, 4 1.063 ms/round.  At
+// the steady state's load of 1/2 a lookup's first probe often misses, and
+// the whole 64 B probe group -- one HBM fetch, see kv_probe -- is loaded at
+// once: DRB_PROBE_W = 4 for the upserts, DRB_READ_W = 4 for the served
+// reads' first group and DRB_PROBE_WR = 4 for their later groups.)
 #ifndef DRB_PROBE_W
-#define DRB_PROBE_W 1
+#define DRB_PROBE_W 4
 #endif
 #ifndef DRB_PROBE_WR
 #define DRB_PROBE_WR DRB_PROBE_W
+#endif
+#ifndef DRB_READ_W
+#define DRB_READ_W 4
 #endif
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
@@ -1629,17 +1637,30 @@ DRB_DEV uint64_t kv_probe_word(const View &v, const uint4 *tbl, uint32_t home,
     for (uint32_t t = 0; t < DRB_PROBE_WR; ++t)
       hs[t] = p0 + t < v.KS ? tbl[(uint64_t)kv_probe(v, home, p0 + t) * v.KVW]
                             : make_uint4(0, 0, 0, 0);
+    // resolved in probe order without leaving the unrolled loop (an early
+    // return from it put hs[] in scratch memory)
+    uint32_t res = 0;  // 0: go on, 1: an empty slot, 2: found
+    uint64_t w = ~0ull;
 #pragma unroll
     for (uint32_t t = 0; t < DRB_PROBE_WR; ++t) {
-      if (!kv_used(hs[t])) return ~0ull;  // also the padding past KS
-      if (kv_match(hs[t], key8, klen)) return kv_word(hs[t]);
+      if (res) continue;
+      if (!kv_used(hs[t])) {
+        res = 1;  // also the padding past KS
+      } else if (kv_match(hs[t], key8, klen)) {
+        res = 2;
+        w = kv_word(hs[t]);
+      }
     }
+    if (res) return w;
   }
   return ~0ull;
 }
 
+// lookups issued together (each loads its whole first probe group): at the
+// steady state's 1/2 load, C3 ran 1.131 ms/round with 3, 1.139 with 5
+// (profiles/r03_kvw); 9 spills
 #ifndef DRB_READ_BATCH
-#define DRB_READ_BATCH 5
+#define DRB_READ_BATCH 3
 #endif
 constexpr uint32_t READ_BATCH = DRB_READ_BATCH;
 
@@ -1664,36 +1685,40 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
     for (uint32_t j0 = 0; j0 < n_reads; j0 += READ_BATCH) {
       uint64_t key[READ_BATCH];
       uint32_t ks[READ_BATCH];
-      uint4 h0[READ_BATCH], h1[READ_BATCH];
+      uint4 h[READ_BATCH][DRB_READ_W];
 #pragma unroll
       for (uint32_t t = 0; t < READ_BATCH; ++t) {
         const uint64_t x =
             mix64(low ^ ((uint64_t)(j0 + t + 1) * 0x9E3779B97F4A7C15ull));
         key[t] = ks_pow2 ? (x & (key_space - 1)) : x % key_space;
         ks[t] = (uint32_t)kv_hash(key[t], 8) & mask;
-        h0[t] = h1[t] = make_uint4(0, 0, 0, 0);
-        if (j0 + t < n_reads) {
-          // (plain loads: with the nontemporal hint the step kernel fetched
-          // 7 % more bytes, profiles/r02_kvline)
-          h0[t] = tbl[(uint64_t)ks[t] * v.KVW];
-          h1[t] = tbl[(uint64_t)kv_probe(v, ks[t], 1) * v.KVW];
-        }
+        // the first DRB_READ_W probes (one 64 B group): independent loads
+        // (plain: with the nontemporal hint the step kernel fetched 7 %
+        // more bytes, profiles/r02_kvline)
+#pragma unroll
+        for (uint32_t q = 0; q < DRB_READ_W; ++q)
+          h[t][q] = j0 + t < n_reads && q < v.KS
+                        ? tbl[(uint64_t)kv_probe(v, ks[t], q) * v.KVW]
+                        : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (uint32_t t = 0; t < READ_BATCH; ++t) {
         const uint32_t j = j0 + t;
         if (j >= n_reads) continue;
-        uint64_t w;
-        if (!kv_used(h0[t]))
-          w = ~0ull;
-        else if (kv_match(h0[t], key[t], 8))
-          w = kv_word(h0[t]);
-        else if (v.KS < 2 || !kv_used(h1[t]))
-          w = ~0ull;
-        else if (kv_match(h1[t], key[t], 8))
-          w = kv_word(h1[t]);
-        else
-          w = kv_probe_word(v, tbl, ks[t], 2, key[t], 8);
+        uint64_t w = ~0ull;
+        bool done = false;
+#pragma unroll
+        for (uint32_t q = 0; q < DRB_READ_W; ++q) {
+          if (done) continue;
+          if (!kv_used(h[t][q])) {
+            done = true;  // an empty slot ends the probe sequence
+          } else if (kv_match(h[t][q], key[t], 8)) {
+            w = kv_word(h[t][q]);
+            done = true;
+          }
+        }
+        if (!done && v.KS > DRB_READ_W)
+          w = kv_probe_word(v, tbl, ks[t], DRB_READ_W, key[t], 8);
         sum += mix64(w ^ key[t] ^ ((uint64_t)j << 56));
         served++;
         if (v.read_res)  // ReadLocalNode's result for the client
@@ -2380,8 +2405,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
                 v.MB &&
             fb == DRB_FB_NONE)
           fb = DRB_FB_CAPACITY;
-      const bool qtick =
-          qon && p.tick && total_in == 0 && qs_quiet_tick(v, r, qz_from);
+      // (a staged ReadIndex ends the quiesce before the tick: node.
+      // handleReadIndex -> qs.record, node.go:1296-1298)
+      const bool qtick = qon && p.tick && total_in == 0 && in_lo == 0 &&
+                         qs_quiet_tick(v, r, qz_from);
       if (!SLOW && p.tick && !qtick) {
         uint64_t et = (total_in ? 0 : r.election_tick) + 1;
         if (et >= ld_f(L, r, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)

@@ -341,7 +341,9 @@ typedef struct drb_config {
    * RequestVote / RequestVoteResp, becomeFollower / Candidate / Leader,
    * the term gate, raft.go:1052-1217, 1507-1590, 1670-1722, 2235-2253);
    * only capacity and off-path entries still fall back.  Co-resident
-   * placement, Quiesce off. */
+   * placement; with Quiesce a quiesced replica ticks with quiescedTick
+   * (raft.go:650-656: no election) until input ends its quiesce
+   * (node.go:1296-1345, quiesce.go:56-74); listed rounds allowed. */
   uint32_t elections;
   /* tan MaxLogFileSize (internal/tan/options.go:29); 0: 64 MiB */
   uint64_t tan_max_log;

@@ -143,3 +143,54 @@ def test_role_census_counts_leaders():
     _unhost(p, [5, 7], 0)
     c = p.eng.role_census()
     assert c[0][abi.LEADER] == 38
+
+
+@pytest.mark.parametrize("pre_vote,listed", [(0, 0), (1, 0), (0, 1)])
+def test_quiesced_groups_fail_over(pre_vote, listed):
+    """Elections with Quiesce (SURVEY 8d C5's mostly idle groups, F3 + F4):
+    every group goes quiet (20 x ElectionRTT idle ticks, quiesce.go:80-82)
+    and then loses its leader.  A quiesced follower ticks with
+    quiescedTick (raft.go:650-656): it never times out while quiet, so the
+    groups stay leaderless -- until a ReadIndex at a follower ends its
+    quiesce (node.handleReadIndex -> qs.record, node.go:1296-1298); its
+    next tick then campaigns at once (the quiesced ticks counted), on the
+    GPU, and the group elects.  Bit-exact with the oracle every checked
+    round, listed rounds (C5) included."""
+    p = Pair(G=16, R=3, elections=1, quiesce=True, pre_vote=pre_vote)
+    st = {"slow": 0, "roles": 0}
+
+    def rounds(n, check_every=1, **kw):
+        for _ in range(n):
+            o, e = p.round(k=0, tick=True, listed=bool(listed), **kw)
+            assert e.fallbacks == 0 and e.errors == 0, (p.rounds, e.to_dict(),
+                                                         p.why())
+            assert (e.committed_entries, e.messages) == \
+                (o.committed_entries, o.messages), (p.rounds, e.to_dict(),
+                                                    o.to_dict())
+            if p.rounds % check_every == 0:
+                errs = p.check()
+                assert not errs, (p.rounds, errs[:2])
+            st["slow"] += e.elections_stepped
+            st["roles"] += e.role_changes
+
+    rounds(230, check_every=23)
+    assert all(p.eng.export(g, s).qs_quiesced_since > 0
+               for g in range(p.G) for s in range(p.R))
+    E = [2, 5, 11]
+    _unhost(p, E, 0)
+    rounds(40, check_every=4)  # quiet: nobody notices
+    for g in E:
+        assert [r for r, _ in _roles(p, g)[1:]] == [abi.FOLLOWER] * 2
+    assert st["slow"] == 0
+    # a read at replica 3 of the leaderless groups wakes that follower
+    rounds(1, read_index=True, groups=E, ri_replica=3)
+    for _ in range(60):
+        rounds(1)
+        if all(abi.LEADER in [r for r, _ in _roles(p, g)[1:]] for g in E):
+            break
+    for g in E:
+        roles = _roles(p, g)
+        lead = [s for s in (1, 2) if roles[s][0] == abi.LEADER]
+        assert len(lead) == 1 and roles[lead[0]][1] >= 3, roles
+    assert st["slow"] > 0 and st["roles"] >= len(E)
+    rounds(10)
