@@ -48,7 +48,7 @@ F_APPLY_STOPPED = 8
 FB = dict(NONE=0, TERM_MISMATCH=1, MESSAGE_TYPE=2, ELECTION=3,
           CHECK_QUORUM=4, ENTRY_TYPE=5, CAPACITY=6, ROLE=7, SNAPSHOT=9,
           ERR_LOG_RANGE=100, ERR_COMMIT=101, ERR_APPEND=103, ERR_APPLY=104,
-          ERR_READINDEX=105)
+          ERR_READINDEX=105, ERR_TRANSFER=106)
 FB_NAME = {v: k for k, v in FB.items()}
 
 
@@ -77,13 +77,14 @@ class ReplicaState(C.Structure):
     _fields_ = ([(n, C.c_uint64) for n in _REPLICA_U64] +
                 [("role", C.c_uint32), ("flags", C.c_uint32),
                  ("fallback_reason", C.c_uint32), ("ri_count", C.c_uint32),
-                 ("votes", C.c_uint32), ("pad0", C.c_uint32),
+                 ("votes", C.c_uint32), ("transfer", C.c_uint32),
                  ("remotes", RemoteState * DRB_MAX_REPLICAS),
                  ("ri", ReadStatus * DRB_RI_DEPTH)])
 
     def to_dict(self, num_replicas=None):
         d = {n: getattr(self, n) for n in _REPLICA_U64}
-        for n in ("role", "flags", "fallback_reason", "ri_count", "votes"):
+        for n in ("role", "flags", "fallback_reason", "ri_count", "votes",
+                  "transfer"):
             d[n] = getattr(self, n)
         nr = num_replicas or DRB_MAX_REPLICAS
         d["remotes"] = [(r.match, r.next, r.state, r.active)
@@ -252,7 +253,8 @@ class RoundOut(C.Structure):
                 ("log_records", C.c_uint64), ("log_syncs", C.c_uint64),
                 ("log_new", C.c_uint64),
                 ("elections_stepped", C.c_uint64),
-                ("role_changes", C.c_uint64)]
+                ("role_changes", C.c_uint64),
+                ("dropped_proposals", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

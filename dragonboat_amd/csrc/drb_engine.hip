@@ -397,6 +397,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.slow_list, v.slow_cap);
     rc |= dalloc(e, &v.slow_n, 1);
     rc |= dalloc(e, &v.rterm, 2ull * R * R * v.MB * G);
+    rc |= dalloc(e, &v.xfer_in, (uint64_t)R * G);
   }
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
@@ -586,7 +587,13 @@ extern "C" int drb_import_replicas(drb_engine *e, uint64_t first_group,
       }
       const uint32_t quiesced =
           v.quiesce && c.qs_quiesced_since > 0 ? F_QUIESCED : 0u;
-      const uint32_t w32[NUM_U32] = {c.role, (c.flags & F_PUBLIC) | quiesced,
+      // a leader's transfer target (a pending request is not imported)
+      const uint32_t xfer = c.role == DRB_LEADER && c.transfer >= 1 &&
+                                    c.transfer <= R && c.transfer != s + 1
+                                ? c.transfer << F_XFER_SHIFT
+                                : 0u;
+      const uint32_t w32[NUM_U32] = {c.role,
+                                     (c.flags & F_PUBLIC) | quiesced | xfer,
                                      c.fallback_reason, c.ri_count, c.votes};
       for (int k = 0; k < NUM_U32; ++k) {
         i32.push_back(u32_ix(v, k, s, g));
@@ -675,6 +682,7 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       o.fallback_reason = d32[b++];
       o.ri_count = d32[b++];
       o.votes = d32[b++];
+      o.transfer = (fl & F_XFER) >> F_XFER_SHIFT;
       for (uint32_t p = 0; p < R; ++p, ++c2) {
         o.remotes[p].match = drm[c2];
         o.remotes[p].next = drn[c2];
@@ -1285,6 +1293,60 @@ extern "C" int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
   return DRB_OK;
 }
 
+// ------------------------------------------------------- leader transfer
+// pendingLeaderTransfer.request (node.go:474-482, request.go): one pending
+// target per replica -- a replica that still holds one refuses (busy)
+__global__ void k_stage_xfer(View v, uint32_t slot, const uint32_t *targets,
+                             unsigned long long *busy) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  const uint32_t t = targets[g];
+  if (t == 0) return;
+  const uint64_t fi = u32_ix(v, W_FLAGS, slot, g);
+  const uint32_t f = v.u32[fi];
+  if (!(f & DRB_F_HOSTED)) return;  // ErrShardNotFound at this NodeHost
+  if (f & (F_XFER_REQ | DRB_F_FALLBACK | DRB_F_ERROR)) {
+    atomicAdd(busy, 1ull);
+    return;
+  }
+  v.xfer_in[ix(v, slot, g)] = (uint8_t)t;
+  // the round takes it even when the replica is at rest (setStepReady,
+  // nodehost.go:1249)
+  v.u32[fi] = (f | F_XFER_REQ) & ~F_AT_REST;
+}
+
+extern "C" int drb_request_leader_transfer(drb_engine *e, uint32_t slot,
+                                           const uint32_t *targets,
+                                           uint64_t *busy) {
+  if (!e || !targets) return DRB_EINVAL;
+  if (slot >= e->cfg.num_replicas) return DRB_ERANGE;
+  if (!e->v.elections || e->v.place_world > 1) return DRB_EINVAL;
+  const uint64_t G = e->v.G;
+  const uint32_t R = e->cfg.num_replicas;
+  for (uint64_t g = 0; g < G; ++g)
+    if (targets[g] > R) return DRB_EINVAL;
+  std::lock_guard<std::mutex> lock(e->ingest_mu);  // ordered with rounds
+  uint32_t *dt = nullptr;
+  unsigned long long *db = nullptr;
+  void *sc = nullptr;
+  const size_t tb = (G * sizeof(uint32_t) + 15) & ~(size_t)15;
+  if (scratch(e, tb + 16, &sc)) return DRB_EDEVICE;
+  dt = (uint32_t *)sc;
+  db = (unsigned long long *)((char *)sc + tb);
+  HIPCHK(hipMemcpyAsync(dt, targets, G * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemsetAsync(db, 0, sizeof(*db), e->stream));
+  k_stage_xfer<<<(unsigned)((G + 255) / 256), 256, 0, e->stream>>>(e->v, slot,
+                                                                   dt, db);
+  HIPCHK(hipGetLastError());
+  unsigned long long nb = 0;
+  HIPCHK(hipMemcpyAsync(&nb, db, sizeof(nb), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (busy) *busy = nb;
+  return DRB_OK;
+}
+
 // ---------------------------------------------------------------- ingest
 // drb_ingest: the whole batch in a fixed number of device transfers.  The
 // host decides every message's fate from one gather of the replicas'
@@ -1888,6 +1950,7 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->replicas_stepped = c[C_STEPPED];
   out->elections_stepped = c[C_ELECT];
   out->role_changes = c[C_ROLE];
+  out->dropped_proposals = c[C_DPROP];
   out->log_records = 0;
   out->log_syncs = 0;
   out->log_new = 0;

@@ -245,6 +245,14 @@ constexpr uint32_t F_AT_REST = 1u << 16;  // a round without input is a no-op
 constexpr uint32_t F_QUIESCED = 1u << 17;  // node.qs.quiesced() (Quiesce on)
 // elections: the replica's round goes to the raft launch (slow list)
 constexpr uint32_t F_SLOW = 1u << 18;
+// elections: a staged NodeHost.RequestLeaderTransfer (target in v.xfer_in)
+// that this replica's next round takes (node.handleLeaderTransfer,
+// node.go:1249-1257); the round goes to the raft launch
+constexpr uint32_t F_XFER_REQ = 1u << 19;
+// a leader's raft.leaderTransferTarget (raft.go:375-381), a replica ID;
+// a leader with one steps in the raft launch until it is cleared
+constexpr int F_XFER_SHIFT = 20;
+constexpr uint32_t F_XFER = 0xfu << F_XFER_SHIFT;
 constexpr uint32_t F_PUBLIC = 0xffffu;
 
 // message record: 1-2 x uint4 (drb_msg.hpp)
@@ -363,6 +371,8 @@ struct View {
   uint4 *slow_list;
   unsigned long long *slow_n;
   uint64_t *rterm;        // [2][R][R][MB][G]
+  uint8_t *xfer_in;       // [R][G] a staged leader transfer's target (the
+                          // replica's F_XFER_REQ; drb_request_leader_transfer)
   // placement (drb_config) and the cross-rank planes (world >= 2)
   uint32_t place_world, place_rank;
   uint64_t total_groups;

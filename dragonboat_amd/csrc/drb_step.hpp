@@ -93,6 +93,7 @@ enum : int {
   C_STEPPED,  // replicas that ran the round (not skipped as idle)
   C_ELECT,    // elections: replicas the raft launch stepped
   C_ROLE,     // elections: role changes
+  C_DPROP,    // elections: proposals a transferring leader dropped
   NUM_COUNTERS
 };
 
@@ -685,13 +686,14 @@ DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
 // ------------------------------------------------------------ handlers
 // handleLeaderReplicateResp (raft.go:1878-1908), via lw (2309-2323)
 template <int R>
-DRB_DEV void leader_replicate_resp(const Lane &L, Rep<R> &r, int s,
+DRB_DEV bool leader_replicate_resp(const Lane &L, Rep<R> &r, int s,
                                    const Msg &m) {
   RemoteV x = rem_get<R>(L, s);
   x.a = 1;  // setActive
+  bool upd = false;
   if (!m.reject) {
     bool paused = rv_is_paused(x);
-    bool upd = rv_try_update(x, m.log_index);
+    upd = rv_try_update(x, m.log_index);
     if (upd && x.st == DRB_REMOTE_RETRY) {  // respondedTo (remote.go:170)
       x.n = x.m + 1;                        // becomeReplicate
       x.st = DRB_REMOTE_REPLICATE;
@@ -724,6 +726,7 @@ DRB_DEV void leader_replicate_resp(const Lane &L, Rep<R> &r, int s,
     rem_put<R>(L, s, x);
     if (dec) send_replicate(L, r, s);
   }
+  return upd;
 }
 
 // handleLeaderHeartbeatResp (raft.go:1910-1923)
@@ -973,6 +976,7 @@ DRB_DEV void el_reset(const Lane &L, Rep<R> &r, uint64_t term,
   r.votes = 0;
   r.heartbeat_tick = 0;
   r.ri_count = 0;
+  r.flags &= ~F_XFER;  // abortLeaderTransfer (raft.go:1068)
 #pragma unroll
   for (int s = 0; s < R; ++s)
     rem_put<R>(L, s,
@@ -1021,9 +1025,11 @@ DRB_DEV uint32_t el_vote_resp(Rep<R> &r, uint32_t from_slot, bool rejected) {
   return __builtin_popcount(r.votes >> 8);
 }
 
-// campaign (raft.go:1176-1217) after becomeCandidate (raft.go:1020-1036)
+// campaign (raft.go:1176-1217) after becomeCandidate (raft.go:1020-1036);
+// xfer: isLeaderTransferTarget -- the RequestVotes name the candidate in
+// Hint, which passes the voters' leader lease (raft.go:1192-1196, 1518)
 template <int R>
-DRB_DEV void el_campaign(const Lane &L, Rep<R> &r) {
+DRB_DEV void el_campaign(const Lane &L, Rep<R> &r, bool xfer = false) {
   r.role = DRB_CANDIDATE;
   el_reset(L, r, r.term + 1, true);
   set_leader(r, 0);
@@ -1038,6 +1044,7 @@ DRB_DEV void el_campaign(const Lane &L, Rep<R> &r) {
   m.type = DRB_MSG_REQUEST_VOTE;
   m.log_index = r.last;
   m.log_term = log_term(L, r, r.last);
+  m.hint = xfer ? (uint64_t)L.slot + 1 : 0;
 #pragma unroll
   for (int s = 0; s < R; ++s)
     if ((uint32_t)s != L.slot) emit(L, r, (uint32_t)s, m);
@@ -1068,15 +1075,45 @@ DRB_DEV void el_pre_vote_campaign(const Lane &L, Rep<R> &r) {
 
 // handleNodeElection (raft.go:1632-1668): not while a config change may be
 // waiting to be applied (hasConfigChangeToApply, raft.go:1611-1622); with
-// PreVote the pre-vote round first (no leader transfer on this path)
+// PreVote the pre-vote round first, unless this replica is a leader
+// transfer's target (xfer, raft.go:1659)
 template <int R>
-DRB_DEV void el_election(const Lane &L, Rep<R> &r) {
+DRB_DEV void el_election(const Lane &L, Rep<R> &r, bool xfer = false) {
   if (r.role == DRB_LEADER) return;
   if (r.committed > ld_f(L, r, F_APPLIED)) return;
-  if (L.v->pre_vote)
+  if (L.v->pre_vote && !xfer)
     el_pre_vote_campaign(L, r);
   else
-    el_campaign(L, r);
+    el_campaign(L, r, xfer);
+}
+
+// sendTimeoutNowMessage (raft.go:873-878)
+template <int R>
+DRB_DEV void el_send_timeout_now(const Lane &L, Rep<R> &r, uint32_t to_slot) {
+  Msg m = {};
+  m.type = DRB_MSG_TIMEOUT_NOW;
+  emit(L, r, to_slot, m);
+}
+
+DRB_DEV uint32_t xfer_target(uint32_t flags) {
+  return (flags & F_XFER) >> F_XFER_SHIFT;
+}
+
+// handleLeaderTransfer (raft.go:1925-1953): the target (a replica ID) is
+// recorded and, when it already holds the whole log, told to campaign now
+template <int R>
+DRB_DEV void el_leader_transfer(const Lane &L, Rep<R> &r, uint64_t target) {
+  if (target == 0) {  // plog.Panicf: target not set
+    set_error(r, DRB_ERR_TRANSFER);
+    return;
+  }
+  if (r.flags & F_XFER) return;                // a transfer is ongoing
+  if (target == (uint64_t)L.slot + 1) return;  // pointing to itself
+  if (target > (uint64_t)R) return;            // unknown target
+  r.flags = (r.flags & ~F_XFER) | ((uint32_t)target << F_XFER_SHIFT);
+  r.election_tick = 0;
+  if (rem_get<R>(L, (int)target - 1).m == r.last)
+    el_send_timeout_now(L, r, (uint32_t)target - 1);
 }
 
 // upToDate (logentry.go:381-393)
@@ -1193,15 +1230,28 @@ DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
     return;
   }
   if (r.role == DRB_LEADER) {
-    if (t == DRB_MSG_REQUEST_VOTE)
+    if (t == DRB_MSG_REQUEST_VOTE) {
       el_request_vote(L, r, s, m);
-    else if (t != DRB_MSG_REQUEST_PREVOTE_RESP)
+    } else if (t == DRB_MSG_LEADER_TRANSFER) {
+      el_leader_transfer(L, r, m.hint);
+    } else if (t == DRB_MSG_REPLICATE_RESP) {
+      // the transfer target caught up: TimeoutNow (raft.go:1890-1895)
+      if (leader_replicate_resp(L, r, s, m) &&
+          xfer_target(r.flags) == (uint32_t)s + 1 &&
+          rem_get<R>(L, s).m == r.last)
+        el_send_timeout_now(L, r, (uint32_t)s);
+    } else if (t != DRB_MSG_REQUEST_PREVOTE_RESP) {
       dispatch(L, r, s, m, src);
+    }
   } else if (r.role == DRB_FOLLOWER) {
     if (t == DRB_MSG_REQUEST_VOTE)
       el_request_vote(L, r, s, m);
     else if (t == DRB_MSG_READ_INDEX)  // handleFollowerReadIndex
       follower_read_index(L, r, m.hint, m.hint_high);
+    else if (t == DRB_MSG_LEADER_TRANSFER)
+      el_forward_transfer(L, r, m.hint);
+    else if (t == DRB_MSG_TIMEOUT_NOW)
+      el_timeout_now(L, r);
     else if (t != DRB_MSG_REQUEST_PREVOTE_RESP)
       dispatch(L, r, s, m, src);
   } else {  // candidate, preVoteCandidate
@@ -1222,13 +1272,16 @@ DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
 }
 
 // LocalTick (raft.go:571-648) for any role; CheckQuorum (raft.go:1785-1792)
-// may step the leader down
+// may step the leader down, and a transfer not done within an election
+// timeout is abandoned (timeToAbortLeaderTransfer, raft.go:622-636)
 template <int R>
-DRB_DEV void el_tick(const Lane &L, Rep<R> &r) {
+DRB_DEV void el_tick(const Lane &L, Rep<R> &r, bool xfer = false) {
   const View &v = *L.v;
   over_st(L, F_TICK_COUNT, over_ld(L, F_TICK_COUNT) + 1);
   if (r.role == DRB_LEADER) {
     r.election_tick++;
+    const bool abort_xfer =
+        (r.flags & F_XFER) && r.election_tick >= v.election_rtt;
     if (r.election_tick >= v.election_rtt) {
       r.election_tick = 0;
       if (v.check_quorum) {  // leaderHasQuorum (raft.go:395-405)
@@ -1243,6 +1296,7 @@ DRB_DEV void el_tick(const Lane &L, Rep<R> &r) {
         if (c < R / 2 + 1) el_become_follower(L, r, r.term, 0, true);
       }
     }
+    if (abort_xfer) r.flags &= ~F_XFER;
     r.heartbeat_tick++;
     if (r.heartbeat_tick >= v.heartbeat_rtt) {
       r.heartbeat_tick = 0;
@@ -1253,8 +1307,26 @@ DRB_DEV void el_tick(const Lane &L, Rep<R> &r) {
   r.election_tick++;
   if (r.election_tick >= ld_f(L, r, F_RAND_TIMEOUT)) {
     r.election_tick = 0;
-    el_election(L, r);
+    el_election(L, r, xfer);
   }
+}
+
+// handleFollowerTimeoutNow (raft.go:2172-2185): the clock moving forward
+// quickly -- a tick at the election timeout, campaigning without PreVote
+template <int R>
+DRB_DEV void el_timeout_now(const Lane &L, Rep<R> &r) {
+  r.election_tick = ld_f(L, r, F_RAND_TIMEOUT);
+  el_tick(L, r, true);
+}
+
+// handleFollowerLeaderTransfer (raft.go:2145-2153): to the leader, if known
+template <int R>
+DRB_DEV void el_forward_transfer(const Lane &L, Rep<R> &r, uint64_t target) {
+  if (r.leader_id == 0 || r.leader_id > (uint64_t)R) return;
+  Msg m = {};
+  m.type = DRB_MSG_LEADER_TRANSFER;
+  m.hint = target;
+  emit(L, r, (uint32_t)r.leader_id - 1, m);
 }
 
 // ------------------------------------------------------------ apply
@@ -2102,7 +2174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint64_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
-  uint32_t c_stepped = 0, c_elect = 0, c_role = 0;
+  uint32_t c_stepped = 0, c_elect = 0, c_role = 0, c_dprop = 0;
   uint32_t sent_c1 = 0;     // remote planes: destinations given a c1 chunk
   uint32_t qz_out = 0;      // destinations sent a Quiesce message
   uint64_t last_final = 0;  // leader: last index at the end of the round
@@ -2182,8 +2254,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         fb = DRB_FB_ROLE;
     } else if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) {
       fb = DRB_FB_ROLE;
+    } else if (flags & (F_XFER | F_XFER_REQ)) {
+      fb = DRB_FB_ROLE;  // a leader transfer: the raft launch's
     }
     bool higher_in = false;  // raft launch: a message may raise the term
+    uint32_t n_lt = 0;       // raft launch: LeaderTransfer records
     // the inbox, from the per-sender headers alone (drb_msg.hpp)
     uint64_t nin_packed = 0;  // 5-bit inbox record count per sender
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
@@ -2217,9 +2292,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
                 t == DRB_MSG_HEARTBEAT || t == DRB_MSG_HEARTBEAT_RESP ||
                 t == DRB_MSG_READ_INDEX || t == DRB_MSG_READ_INDEX_RESP ||
                 t == DRB_MSG_REQUEST_VOTE || t == DRB_MSG_REQUEST_VOTE_RESP ||
-                t == DRB_MSG_NOOP ||
+                t == DRB_MSG_NOOP || t == DRB_MSG_LEADER_TRANSFER ||
+                t == DRB_MSG_TIMEOUT_NOW ||
                 (v.pre_vote && is_prevote_type(t));
             if (!ok && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
+            n_lt += t == DRB_MSG_LEADER_TRANSFER;
           }
         }
         if ((info & MI_TERM) && hi64(meta) > r.term) higher_in = true;
@@ -2364,8 +2441,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           if ((uint32_t)s == slot) continue;
           // a ReadIndex from s is answered by the broadcast and the
           // release counted in base, not by a send of its own
-          uint32_t bound = base + (uint32_t)((nin_packed >> (5 * s)) & 31u) -
+          const uint32_t ns = (uint32_t)((nin_packed >> (5 * s)) & 31u);
+          uint32_t bound = base + ns -
                            (uint32_t)((nri_packed >> (5 * s)) & 31u);
+          // a transfer: TimeoutNow once, or after each ReplicateResp
+          if (SLOW && (n_lt || (flags & (F_XFER | F_XFER_REQ))))
+            bound += 1 + ns;
           if (bound > v.MB && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
         }
       }
@@ -2401,7 +2482,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
 #pragma unroll
       for (int s = 0; s < R; ++s)
         if ((uint32_t)s != slot &&
-            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) + (SLOW ? 1 : 0) >
+            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) + (SLOW ? 1 : 0) +
+                    (SLOW ? n_lt + ((flags & F_XFER_REQ) ? 1u : 0u) : 0u) >
                 v.MB &&
             fb == DRB_FB_NONE)
           fb = DRB_FB_CAPACITY;
@@ -2562,8 +2644,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         }
       }
       // handleProposals (node.go:1275) -> handleLeaderPropose
-      // (raft.go:1794-1815) -> appendEntries (raft.go:944-955)
-      if (nprops) {
+      // (raft.go:1794-1815) -> appendEntries (raft.go:944-955); a leader
+      // transferring its leadership drops them (raft.go:1796-1800)
+      if (SLOW && nprops && (r.flags & F_XFER)) {
+        c_dprop = nprops;
+      } else if (nprops) {
         const uint32_t chunks = PROP_META + v.C16;
         for (uint32_t j = 0; j < nprops; ++j) {
           uint64_t idx = r.last + 1 + j;
@@ -2583,6 +2668,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
         rem_try_update<R>(L, (int)slot, r.last);  // self remote
         if (R == 1) try_commit(L, r);
         broadcast_replicate(L, r);
+      }
+      // handleLeaderTransfer (node.go:1249-1257) -> Peer.RequestLeader-
+      // Transfer (peer.go:106-113): a LeaderTransfer to itself, term 0
+      if (SLOW && (r.flags & F_XFER_REQ)) {
+        r.flags &= ~F_XFER_REQ;
+        const uint64_t target = v.xfer_in[ix(v, slot, g)];
+        if (r.role == DRB_LEADER)
+          el_leader_transfer(L, r, target);
+        else if (r.role == DRB_FOLLOWER)
+          el_forward_transfer(L, r, target);
       }
       // stepNode: newQuiesceState -> sendEnterQuiesceMessages to every
       // other member (node.go:993-1005, 1148-1150), sent ahead of the
@@ -2608,7 +2703,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       bool state_empty = r.term == 0 && vote == 0 && r.committed == 0;
       bool has_update = has_save || r.leader_update || r.nmsgs > 0 ||
                         has_apply || (!state_empty && state_changed) ||
-                        r.nrtr > 0 || r.ndropped_ri > 0;
+                        r.nrtr > 0 || r.ndropped_ri > 0 || c_dprop > 0;
       uint64_t apply_lo = 0, apply_hi = 0;
       if (has_update || confirmed_index != r.applied_index) {
         // validateUpdate / pushEntries (node.go:1100) / Peer.Commit
@@ -2823,7 +2918,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       (uint32_t)c_rtr,    (uint32_t)c_drop,    (uint32_t)c_fb,
       (uint32_t)c_err,    c_served,            c_deferred,
       c_saved,            c_saved_bytes,       c_stepped,
-      c_elect,            c_role};
+      c_elect,            c_role,              c_dprop};
   block_counters<LEAD, 0, NUM_COUNTERS>(v, SLOW ? 0u : slot, bp, cnt);
 }
 

@@ -58,6 +58,7 @@ SIGNATURES = {
                                               U64, U32]),
     "drb_stage_read_index": (C.c_int, [P, U32, PU64, PU64]),
     "drb_gen_read_index": (C.c_int, [P, U32, U64, U64]),
+    "drb_request_leader_transfer": (C.c_int, [P, U32, PU32, PU64]),
     "drb_ingest": (C.c_int, [P, C.POINTER(Message), SZ, C.POINTER(Entry),
                              PU8, PU64, PU64]),
     "drb_step_round": (C.c_int, [P, C.POINTER(RoundIn),
@@ -289,6 +290,17 @@ class Engine:
     def gen_read_index(self, slot, seed, high):
         _ck(lib().drb_gen_read_index(self.h, slot, seed, high),
             "drb_gen_read_index")
+
+    def request_leader_transfer(self, slot, targets):
+        """NodeHost.RequestLeaderTransfer at replica slot `slot` of every
+        group g with targets[g] (a replica ID) != 0; returns how many were
+        refused as busy (drb_request_leader_transfer)."""
+        arr = (C.c_uint32 * self.G)(*targets)
+        busy = U64()
+        _ck(lib().drb_request_leader_transfer(self.h, slot, arr,
+                                              C.byref(busy)),
+            "drb_request_leader_transfer")
+        return busy.value
 
     def ingest(self, marr, n, earr, pool):
         acc, drop = U64(), U64()

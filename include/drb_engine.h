@@ -151,7 +151,9 @@ enum drb_fallback_reason {
                                  * logentry.go:296-321 committed entry
                                  * changed */
   DRB_ERR_APPLY = 104,          /* statemachine.go:935-969 malformed entry */
-  DRB_ERR_READINDEX = 105       /* readindex.go:43-115 invariant */
+  DRB_ERR_READINDEX = 105,      /* readindex.go:43-115 invariant */
+  DRB_ERR_TRANSFER = 106        /* raft.go:1929-1931 LeaderTransfer without
+                                 * a target */
 };
 
 /* remote (internal/raft/remote.go:72-80); remotes[] is indexed by slot. */
@@ -222,7 +224,9 @@ typedef struct drb_replica_state {
   /* a candidate's votes (raft.votes, raft.go:1125-1147): bit s of the low
    * byte = replica slot s answered, of the next byte = it granted */
   uint32_t votes;
-  uint32_t pad0;
+  /* a leader's raft.leaderTransferTarget (raft.go:375-381): the replica ID
+   * leadership is being handed to, 0 none (elections) */
+  uint32_t transfer;
   drb_remote_state remotes[DRB_MAX_REPLICAS];
   drb_read_status ri[DRB_RI_DEPTH];
 } drb_replica_state;
@@ -417,6 +421,9 @@ typedef struct drb_round_out {
   uint64_t elections_stepped;     /* elections: replicas the raft launch
                                    * stepped (term gate, votes, campaign) */
   uint64_t role_changes;          /* elections: replicas whose role changed */
+  uint64_t dropped_proposals;     /* entries a leader transferring its
+                                   * leadership dropped (raft.go:1796-1800;
+                                   * the clients' requests complete Dropped) */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;
@@ -529,6 +536,23 @@ int drb_stage_read_index(drb_engine *e, uint32_t slot, const uint64_t *ctx_low,
  * (dragonboat_amd/workload.py read_index_ctx with salt = high). */
 int drb_gen_read_index(drb_engine *e, uint32_t slot, uint64_t seed,
                        uint64_t high);
+/* NodeHost.RequestLeaderTransfer (nodehost.go:1238-1251) at replica slot
+ * `slot` (that NodeHost) of every group g with targets[g] != 0, a replica
+ * ID <= num_replicas: node.requestLeaderTransfer ->
+ * pendingLeaderTransfer.request (node.go:474-482).  The replica's next
+ * round takes it after its proposals (node.handleLeaderTransfer,
+ * node.go:1198, 1249-1257 -> Peer.RequestLeaderTransfer, peer.go:106-113):
+ * a leader starts the transfer (raft.go:1925-1953), a follower forwards it
+ * to its leader (raft.go:2145-2153), a candidate ignores it.  The leader
+ * then drops proposals (drb_round_out.dropped_proposals) until the target
+ * holds its whole log and is sent TimeoutNow, which makes it campaign at
+ * once without PreVote (raft.go:1890-1895, 2172-2185); an election timeout
+ * without a new leader abandons the transfer (raft.go:622-636).  Needs
+ * elections (co-resident placement).  A replica still holding an earlier
+ * request, or off the fast path, refuses (ErrSystemBusy): *busy (may be
+ * NULL) counts those; unhosted replicas are skipped.  Synchronous. */
+int drb_request_leader_transfer(drb_engine *e, uint32_t slot,
+                                const uint32_t *targets, uint64_t *busy);
 
 /* Inbound boundary: IMessageHandler.HandleMessageBatch
  * (internal/transport/transport.go:86-91, nodehost.go:2072-2122).  Places

@@ -149,6 +149,7 @@ typedef struct orc_node {
   orc_evec props; /* incomingProposals */
   int has_ri;
   orc_ctx ri;
+  uint64_t xfer; /* pendingLeaderTransfer: a requested target, 0 none */
   int hosted;
   orc_mvec out;   /* ud.Messages of the last round */
   orc_rtr *rtr;   /* ud.ReadyToReads of the last round */
@@ -564,6 +565,18 @@ static int node_handle_events(orc_node *n, int tick) {
     msg_free(&m);
     has_event = 1;
   }
+  /* handleLeaderTransfer (node.go:1249-1257) -> Peer.RequestLeaderTransfer
+   * (peer.go:106-113) */
+  if (n->xfer) {
+    orc_msg m;
+    memset(&m, 0, sizeof(m));
+    m.type = DRB_MSG_LEADER_TRANSFER;
+    m.to = r->replica_id;
+    m.hint = n->xfer;
+    n->xfer = 0;
+    raft_handle_msg(r, &m);
+    has_event = 1;
+  }
   return has_event;
 }
 
@@ -744,6 +757,7 @@ static void group_round(orc_cluster *c, uint64_t g, int tick,
     if (out) {
       out->messages += ud->msgs.n;
       out->dropped_read_indexes += r->ndropped_ri;
+      out->dropped_proposals += r->ndropped_entries;
     }
   }
   /* SaveRaftState, processRaftUpdate, commitRaftUpdate, sm.Handle */
@@ -954,6 +968,27 @@ int orc_cluster_stage_read_index_at(orc_cluster *c, const uint64_t *low,
   return 0;
 }
 
+/* NodeHost.RequestLeaderTransfer (nodehost.go:1238-1251) ->
+ * node.requestLeaderTransfer -> pendingLeaderTransfer.request (a channel of
+ * one: a second request before the node takes the first is ErrSystemBusy)
+ * at replica slot `slot` of every group with targets[g] != 0.  Returns the
+ * number of busy refusals. */
+int64_t orc_cluster_request_leader_transfer(orc_cluster *c, uint32_t slot,
+                                            const uint32_t *targets) {
+  if (slot >= c->cfg.num_replicas) return -1;
+  int64_t busy = 0;
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++) {
+    if (!targets[g]) continue;
+    orc_node *n = node_at(c, g, slot);
+    if (!n->hosted) continue;
+    if (n->xfer)
+      busy++;
+    else
+      n->xfer = targets[g];
+  }
+  return busy;
+}
+
 int orc_cluster_ingest(orc_cluster *c, const drb_message *m, size_t n,
                        const drb_entry *ents, const uint8_t *pool) {
   for (size_t i = 0; i < n; i++) {
@@ -1066,7 +1101,7 @@ int orc_cluster_import(orc_cluster *c, uint64_t g, uint32_t slot,
   r->tick_count = st->tick_count;
   r->state = st->role;
   r->rng = st->rng;
-  r->leader_transfer_target = 0;
+  r->leader_transfer_target = st->role == DRB_LEADER ? st->transfer : 0;
   r->is_leader_transfer_target = 0;
   r->nvotes = 0;
   for (uint32_t s = 0; s < DRB_MAX_REPLICAS; s++)

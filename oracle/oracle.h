@@ -246,7 +246,9 @@ enum {
   ORC_POKE_ELECTION_TIMEOUT,
   ORC_POKE_COMMITTED,
   ORC_POKE_APPLIED,
-  ORC_POKE_CONFIG_CHANGE_HOOK /* 1: hasNotAppliedConfigChange = test hook */
+  ORC_POKE_CONFIG_CHANGE_HOOK, /* 1: hasNotAppliedConfigChange = test hook */
+  ORC_POKE_LEADER_TRANSFER_TARGET,
+  ORC_POKE_IS_LEADER_TRANSFER_TARGET
 };
 int orc_raft_poke(orc_raft *r, int field, uint64_t v);
 uint64_t orc_raft_peek(orc_raft *r, int field);
@@ -388,6 +390,8 @@ int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
 /* stage one ReadIndex ctx per group (low==0: none) for next round */
 int orc_cluster_stage_read_index(orc_cluster *c, const uint64_t *low,
                                  const uint64_t *high);
+int64_t orc_cluster_request_leader_transfer(orc_cluster *c, uint32_t slot,
+                                            const uint32_t *targets);
 int orc_cluster_stage_read_index_at(orc_cluster *c, const uint64_t *low,
                                     const uint64_t *high, uint32_t replica);
 int orc_cluster_ingest(orc_cluster *c, const drb_message *m, size_t n,

@@ -188,6 +188,7 @@ def _declare(L):
         "orc_cluster_stage_proposals": (C.c_int, [P, PU32, U32, PE, PU8]),
         "orc_cluster_stage_read_index": (C.c_int, [P, PU64, PU64]),
         "orc_cluster_stage_read_index_at": (C.c_int, [P, PU64, PU64, U32]),
+        "orc_cluster_request_leader_transfer": (C.c_int64, [P, U32, PU32]),
         "orc_cluster_ingest": (C.c_int, [P, PM, C.c_size_t, PE, PU8]),
         "orc_cluster_round": (C.c_int, [P, C.c_int, C.POINTER(RoundOut)]),
         "orc_cluster_round_range": (C.c_int, [P, C.c_int, U64, U64,
@@ -479,7 +480,8 @@ class TestRaft:
     # fields the reference's tests assign directly (orc_raft_poke)
     POKE = dict(state=0, term=1, vote=2, election_tick=3,
                 election_timeout=4, committed=5, applied=6,
-                config_change_hook=7)
+                config_change_hook=7, leader_transfer_target=8,
+                is_leader_transfer_target=9)
 
     def poke(self, **kw):
         for k, v in kw.items():
@@ -781,6 +783,17 @@ class Cluster:
         `replica` (which forwards it when it is a follower)."""
         _check(lib().orc_cluster_stage_read_index_at(self.p, low, high,
                                                      replica))
+
+    def request_leader_transfer(self, slot, targets):
+        """NodeHost.RequestLeaderTransfer at replica slot `slot` of every
+        group g with targets[g] (a replica ID) != 0, taken by that node's
+        next round (node.handleLeaderTransfer, node.go:1249).  Returns the
+        number refused as busy (a request still pending)."""
+        arr = (C.c_uint32 * self.G)(*targets)
+        n = lib().orc_cluster_request_leader_transfer(self.p, slot, arr)
+        if n < 0:
+            raise OracleError("request_leader_transfer: bad slot")
+        return n
 
     def ingest(self, msgs):
         marr, n, earr, pool = build_messages(msgs)

@@ -1238,6 +1238,11 @@ static void raft_campaign(orc_raft *r) {
     raft_become_leader(r);
     return;
   }
+  uint64_t hint = 0; /* the transfer target names itself (raft.go:1192) */
+  if (r->is_leader_transfer_target) {
+    hint = r->replica_id;
+    r->is_leader_transfer_target = 0;
+  }
   uint64_t index = log_last(&r->log);
   uint64_t last_term;
   if (log_term(&r->log, index, &last_term)) orc_panic("campaign: log error");
@@ -1247,6 +1252,7 @@ static void raft_campaign(orc_raft *r) {
     m.term = term;
     m.log_index = index;
     m.log_term = last_term;
+    m.hint = hint;
     raft_send(r, &m);
   }
 }
@@ -1447,6 +1453,17 @@ static void raft_quiesced_tick(orc_raft *r) {
   r->election_tick++;
 }
 
+/* leaderTransfering / abortLeaderTransfer (raft.go:375-381) */
+static int raft_leader_transfering(const orc_raft *r) {
+  return r->leader_transfer_target != 0 && r->state == DRB_LEADER;
+}
+
+/* sendTimeoutNowMessage (raft.go:873-878) */
+static void raft_send_timeout_now(orc_raft *r, uint64_t to) {
+  orc_msg m = new_msg(DRB_MSG_TIMEOUT_NOW, to);
+  raft_send(r, &m);
+}
+
 /* handleLeaderReplicateResp (raft.go:1878-1908) */
 static void handle_leader_replicate_resp(orc_raft *r, const orc_msg *m,
                                          orc_remote *rp) {
@@ -1459,7 +1476,11 @@ static void handle_leader_replicate_resp(orc_raft *r, const orc_msg *m,
         raft_broadcast_replicate(r);
       else if (paused)
         raft_send_replicate(r, m->from);
-      /* leader transfer (raft.go:1892-1895) is not on this path */
+      /* the leadership transfer protocol, p29 of the raft thesis
+       * (raft.go:1890-1895): the target caught up */
+      if (raft_leader_transfering(r) && m->from == r->leader_transfer_target &&
+          log_last(&r->log) == rp->match)
+        raft_send_timeout_now(r, r->leader_transfer_target);
     }
   } else {
     if (orc_remote_decrease_to(rp, m->log_index, m->hint)) {
@@ -1515,7 +1536,10 @@ static void handle_leader_read_index(orc_raft *r, const orc_msg *m) {
 
 /* handleLeaderPropose (raft.go:1794-1815) */
 static void handle_leader_propose(orc_raft *r, orc_msg *m) {
-  /* leader transfer is not on this path (leaderTransfering() false) */
+  if (raft_leader_transfering(r)) { /* raft.go:1796-1800 */
+    r->ndropped_entries += m->ents.n;
+    return;
+  }
   for (size_t i = 0; i < m->ents.n; i++)
     if (m->ents.v[i].type == DRB_ENTRY_CONFIG_CHANGE) {
       if (r->pending_config_change) {
@@ -1529,6 +1553,30 @@ static void handle_leader_propose(orc_raft *r, orc_msg *m) {
     }
   raft_append_entries(r, m->ents.v, m->ents.n);
   raft_broadcast_replicate(r);
+}
+
+/* handleLeaderTransfer (raft.go:1925-1953) */
+static void handle_leader_transfer(orc_raft *r, const orc_msg *m) {
+  uint64_t target = m->hint;
+  if (target == 0) orc_panic("leader transfer target not set");
+  if (raft_leader_transfering(r)) return; /* a transfer is ongoing */
+  if (r->replica_id == target) return;    /* pointing to itself */
+  int i = raft_rem_idx(r, target);
+  if (i < 0) return; /* unknown target */
+  r->leader_transfer_target = target;
+  r->election_tick = 0;
+  /* fast path, or wait for the target to catch up (p29, raft thesis) */
+  if (r->rem[i].match == log_last(&r->log))
+    raft_send_timeout_now(r, target);
+}
+
+/* handleFollowerTimeoutNow (raft.go:2172-2185): the clock moving forward
+ * quickly, campaigning without a pre-vote round */
+static void handle_follower_timeout_now(orc_raft *r) {
+  r->election_tick = r->randomized_election_timeout;
+  r->is_leader_transfer_target = 1;
+  raft_tick(r);
+  r->is_leader_transfer_target = 0;
 }
 
 /* handleLeaderCheckQuorum (raft.go:1785-1792) */
@@ -1641,6 +1689,9 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
         case DRB_MSG_REQUEST_PREVOTE:
           handle_node_request_pre_vote(r, m);
           return;
+        case DRB_MSG_LEADER_TRANSFER:
+          handle_leader_transfer(r, m);
+          return;
         case DRB_MSG_LOCAL_TICK:
           if (m->reject)
             raft_quiesced_tick(r);
@@ -1703,6 +1754,17 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
           return;
         case DRB_MSG_REQUEST_PREVOTE:
           handle_node_request_pre_vote(r, m);
+          return;
+        case DRB_MSG_LEADER_TRANSFER: /* handleFollowerLeaderTransfer */
+          if (r->leader_id == 0) return; /* raft.go:2145-2153 */
+          {
+            orc_msg fwd = new_msg(DRB_MSG_LEADER_TRANSFER, r->leader_id);
+            fwd.hint = m->hint;
+            raft_send(r, &fwd);
+          }
+          return;
+        case DRB_MSG_TIMEOUT_NOW:
+          handle_follower_timeout_now(r);
           return;
         case DRB_MSG_LOCAL_TICK:
           if (m->reject)
@@ -2150,6 +2212,7 @@ void orc_raft_info(orc_raft *r, drb_replica_state *st) {
   st->applied_to_term = r->log.im.applied_to_term;
   st->role = r->state;
   st->rng = r->rng;
+  st->transfer = (uint32_t)r->leader_transfer_target;
   /* raft.votes as answered | granted << 8, bit (ID - 1) */
   for (int i = 0; i < r->nvotes; i++) {
     const uint64_t id = r->vote_id[i];
@@ -2509,6 +2572,11 @@ int orc_raft_poke(orc_raft *r, int field, uint64_t v) {
     case ORC_POKE_APPLIED: r->applied = v; break;
     case ORC_POKE_CONFIG_CHANGE_HOOK: r->test_has_config_change_hook = (int)v;
       break;
+    /* abortLeaderTransfer (raft.go:379-381) is a poke of 0 */
+    case ORC_POKE_LEADER_TRANSFER_TARGET: r->leader_transfer_target = v; break;
+    case ORC_POKE_IS_LEADER_TRANSFER_TARGET:
+      r->is_leader_transfer_target = (int)v;
+      break;
     default: return -1;
   }
   return 0;
@@ -2524,6 +2592,9 @@ uint64_t orc_raft_peek(orc_raft *r, int field) {
     case ORC_POKE_COMMITTED: return r->log.committed;
     case ORC_POKE_APPLIED: return r->applied;
     case ORC_POKE_CONFIG_CHANGE_HOOK: return (uint64_t)r->test_has_config_change_hook;
+    case ORC_POKE_LEADER_TRANSFER_TARGET: return r->leader_transfer_target;
+    case ORC_POKE_IS_LEADER_TRANSFER_TARGET:
+      return (uint64_t)r->is_leader_transfer_target;
     default: return ~0ull;
   }
 }

@@ -38,6 +38,8 @@ def state_diff(a, b, R):
                                      (y.match, y.next, y.state, y.active))
     if a.votes != b.votes:
         d["votes"] = (a.votes, b.votes)
+    if a.transfer != b.transfer:
+        d["transfer"] = (a.transfer, b.transfer)
     if a.ri_count != b.ri_count:
         d["ri_count"] = (a.ri_count, b.ri_count)
     else:
