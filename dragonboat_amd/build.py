@@ -140,6 +140,8 @@ if __name__ == "__main__":
         out = os.path.join(os.path.dirname(HERE), "tools", "_bin",
                            name + ".so")
         os.makedirs(os.path.dirname(out), exist_ok=True)
-        print(build(verbose="-v" in args, out=out, defines=defs))
+        vr = tuple(int(a[4:]) for a in args if a.startswith("--r="))
+        print(build(verbose="-v" in args, out=out, defines=defs,
+                    variant_r=vr or (3,)))
     else:
         print(build(force="--force" in args, verbose="-v" in args))

@@ -42,6 +42,12 @@ namespace drb {
 #ifndef DRB_EXT_LEAD_WAVES
 #define DRB_EXT_LEAD_WAVES 3
 #endif
+// the raft launch steps only the replicas routed to it: its register
+// budget matters more than its occupancy (at 3 waves it spilled ~400 VGPRs
+// and ~330 SGPRs into VGPR lanes)
+#ifndef DRB_SLOW_WAVES
+#define DRB_SLOW_WAVES 1
+#endif
 #ifndef DRB_FOLLOW_WAVES
 #define DRB_FOLLOW_WAVES 4
 #endif
@@ -2114,7 +2120,7 @@ DRB_DEV void block_plane_summary(const View &v, BlockPos bp, uint32_t from,
 // steps the replicas on the slow list (F_SLOW) with the election state
 // machine (el_*, above) as well, whatever their role.
 template <int R, bool LEAD, bool EXT, bool SLOW = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT ? DRB_EXT_LEAD_WAVES : DRB_LEAD_WAVES) : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_SLOW_WAVES : LEAD ? (EXT ? DRB_EXT_LEAD_WAVES : DRB_LEAD_WAVES) : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
   // kernarg loads, and the pointers loaded from it are known to address
@@ -2139,7 +2145,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
   const uint64_t lrow = ((uint64_t)(LEAD ? 0 : 1) * v.R + slot);
   const uint64_t li = (uint64_t)bp.x * blockDim.x + threadIdx.x;
   uint64_t nlisted = 0;
-  if (p.listed) {  // the heavy part of the row's list, then the light one
+  // (the raft launch takes its lanes from the slow list, listed or not)
+  if (!SLOW && p.listed) {  // the heavy part of the row's list, then light
     nlisted = v.act_total[2 * lrow] + v.act_total[2 * lrow + 1];
     if ((uint64_t)bp.x * blockDim.x >= nlisted) return;  // uniform
   }
@@ -2258,6 +2265,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       fb = DRB_FB_ROLE;  // a leader transfer: the raft launch's
     }
     bool higher_in = false;  // raft launch: a message may raise the term
+    bool higher_lead = false;  // ... and one of them is a leader message
     uint32_t n_lt = 0;       // raft launch: LeaderTransfer records
     // the inbox, from the per-sender headers alone (drb_msg.hpp)
     uint64_t nin_packed = 0;  // 5-bit inbox record count per sender
@@ -2299,8 +2307,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
             n_lt += t == DRB_MSG_LEADER_TRANSFER;
           }
         }
-        if ((info & MI_TERM) && hi64(meta) > r.term) higher_in = true;
-        if (info & MI_TERM_OTHER) {  // the records with a term of their own
+        const bool hterm = (info & MI_TERM) && hi64(meta) > r.term;
+        if (hterm) higher_in = true;
+        if (hterm || (info & MI_TERM_OTHER)) {
+          // the records above this replica's term: records with a term of
+          // their own (rterm), and the leader messages among them -- a
+          // leader that steps down for one learns the new leader, and would
+          // forward its queued proposals to it (handleFollowerPropose,
+          // raft.go:2103-2116); without one it drops them
           const uint4 *mb = rm ? v.mbox_in : v.mbox;
           const uint32_t nrp = mi_nrep(info);
           for (uint32_t j = 0; j < ns; ++j) {
@@ -2311,9 +2325,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
             const bool pv = (x & 0xffu) == DRB_MSG_REQUEST_PREVOTE ||
                             ((x & 0xffu) == DRB_MSG_REQUEST_PREVOTE_RESP &&
                              !(x & MF_REJECT));
-            if ((x & MF_TERM_OTHER) && !pv &&
-                v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)] > r.term)
-              higher_in = true;
+            const uint64_t rt =
+                (x & MF_TERM_OTHER)
+                    ? v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)]
+                    : (x & MF_TERM_ZERO) ? 0 : hi64(meta);
+            if ((x & MF_TERM_OTHER) && !pv && rt > r.term) higher_in = true;
+            if (rt > r.term && el_leader_message(x & 0xffu))
+              higher_lead = true;
           }
         }
       } else {
@@ -2348,7 +2366,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       in_lo = lo64(c);
       in_hi = hi64(c);
     }
-    bool cq_fail = false;  // raft launch: CheckQuorum steps down at the tick
     if (is_leader) {
       if (p.prop_slot != DRB_NONE && stage_here(v, slot, is_leader))
         nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
@@ -2444,9 +2461,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           const uint32_t ns = (uint32_t)((nin_packed >> (5 * s)) & 31u);
           uint32_t bound = base + ns -
                            (uint32_t)((nri_packed >> (5 * s)) & 31u);
-          // a transfer: TimeoutNow once, or after each ReplicateResp
+          // a transfer: one TimeoutNow from the ReplicateResps (it needs
+          // match == lastIndex after a successful tryUpdate, and match only
+          // grows while lastIndex stands: raft.go:1883-1895), plus a
+          // TimeoutNow or Replicate per LeaderTransfer handled
+          // (handleLeaderTransfer, raft.go:1925-1953)
           if (SLOW && (n_lt || (flags & (F_XFER | F_XFER_REQ))))
-            bound += 1 + ns;
+            bound += 1 + n_lt + ((flags & F_XFER_REQ) ? 1u : 0u);
           if (bound > v.MB && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
         }
       }
@@ -2461,18 +2482,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
           if ((uint32_t)s != slot &&
               (rem_get<R>(L, s).a || ((resp_from >> s) & 1)))
             c++;
-        if (c < R / 2 + 1) {
-          if (SLOW)
-            cq_fail = true;
-          else if (fb == DRB_FB_NONE)
-            fb = DRB_FB_CHECK_QUORUM;
-        }
+        // (the raft launch steps the leader down at the tick, el_tick)
+        if (c < R / 2 + 1 && !SLOW && fb == DRB_FB_NONE)
+          fb = DRB_FB_CHECK_QUORUM;
       }
-      // a leader that may step down before handleProposals would forward
-      // or drop its proposals (handleFollowerPropose, raft.go:2103-2116):
-      // the CPU path's
-      if (SLOW && nprops && (higher_in || cq_fail) && fb == DRB_FB_NONE)
-        fb = higher_in ? DRB_FB_TERM_MISMATCH : DRB_FB_CHECK_QUORUM;
+      // a leader that may step down before handleProposals and learn the
+      // new leader in the same round would forward its proposals to it
+      // (handleFollowerPropose, raft.go:2103-2116): the CPU path's.  One
+      // that steps down for a vote, a NoOP or CheckQuorum knows no leader
+      // and drops them (below).
+      if (SLOW && nprops && higher_lead && fb == DRB_FB_NONE)
+        fb = DRB_FB_TERM_MISMATCH;
     } else {
       if (max_app && max_app >= keep_common + v.W &&
           fb == DRB_FB_NONE)
@@ -2648,6 +2668,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       // transferring its leadership drops them (raft.go:1796-1800)
       if (SLOW && nprops && (r.flags & F_XFER)) {
         c_dprop = nprops;
+      } else if (SLOW && nprops && r.role != DRB_LEADER) {
+        // stepped down this round: handleCandidatePropose, or
+        // handleFollowerPropose with no leader known (raft.go:2197-2201,
+        // 2103-2108) -- reportDroppedProposal
+        if (r.role == DRB_FOLLOWER && r.leader_id != 0)
+          set_error(r, DRB_FB_TERM_MISMATCH);  // excluded by the pre-pass
+        else
+          c_dprop = nprops;
       } else if (nprops) {
         const uint32_t chunks = PROP_META + v.C16;
         for (uint32_t j = 0; j < nprops; ++j) {
@@ -2671,6 +2699,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAD ? (EXT
       }
       // handleLeaderTransfer (node.go:1249-1257) -> Peer.RequestLeader-
       // Transfer (peer.go:106-113): a LeaderTransfer to itself, term 0
+#ifdef DRB_DBG_XFER
+      if (SLOW)
+        printf("xfer g %lu s %u flags %x role %u lid %lu tgt %u fb %u\n",
+               (unsigned long)g, slot, r.flags, r.role,
+               (unsigned long)r.leader_id, (unsigned)v.xfer_in[ix(v, slot, g)],
+               fb);
+#endif
       if (SLOW && (r.flags & F_XFER_REQ)) {
         r.flags &= ~F_XFER_REQ;
         const uint64_t target = v.xfer_in[ix(v, slot, g)];

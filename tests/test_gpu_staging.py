@@ -29,7 +29,7 @@ def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4):
 @pytest.mark.parametrize("k,val_len", [(1, 4), (3, 4), (2, 16)])
 def test_packed_staging_matches_oracle(k, val_len):
     G = 96
-    p = Pair(G=G, R=3, max_props=4, cmd_cap=32)
+    p = Pair(G=G, R=3, max_props=4, cmd_cap=32, kv_val_cap=16)
     for rnd in range(10):
         groups = None if rnd % 3 else [g for g in range(G) if g % 4]
         _stage_packed(p, k, rnd, groups, val_len=val_len)
