@@ -147,13 +147,21 @@ def parse():
 
 
 C5_VAL = {128: 116, 1024: 1011}
-# C5 PBKV key space per group: half the KV slots a replica gets at that
-# payload (16 / 8 slots; values out of line at 1 KB, 4 pool blocks per
-# replica), so a long run upserts existing keys instead of overflowing the
-# table -- with the C3 key space (256) the Poisson tail of groups
-# proposing more than 16 times (1 %/round over ~650 rounds: ~650 groups)
-# fell back on a full table (DRB_FB_CAPACITY at apply)
-C5_KEYS = {128: 8, 1024: 4}
+# C5 KV: writes uniform over the K = 256 keys of SURVEY 8d, as C3.  A
+# replica's table holds C5_SLOTS keys -- a group proposes Poisson(1 % x
+# rounds) times in a run, ~0.7 in the default one, so no table fills (a full
+# one would stop that replica's apply: DRB_F_APPLY_STOPPED, counted in the
+# JSON) -- and the values live in one shared block pool sized for the keys
+# the run can write (put_value_long: a block per distinct key, bump-allocated)
+C5_KEYS = KEY_SPACE
+C5_SLOTS = 32
+
+
+def c5_pool_blocks(G, R, rounds, active_ppm):
+    """Value blocks for every distinct key a C5 run of `rounds` rounds can
+    write: R replicas of each proposing group, mean + 8 sigma + slack."""
+    mean = G * R * active_ppm / 1e6 * rounds
+    return int(mean + 8 * mean ** 0.5) + R * 65536
 
 
 def cpu_baseline(args, seconds):
@@ -179,7 +187,7 @@ def cpu_baseline(args, seconds):
         if args.workload == "c5":
             act = workload.active_groups(G, seed, rounds, args.active_ppm)
             counts, ents, pool = workload.build_batch(
-                G, args.k, seed, rounds, C5_KEYS[args.payload],
+                G, args.k, seed, rounds, C5_KEYS,
                 C5_VAL[args.payload], act)
         else:
             counts, ents, pool = workload.build_batch(G, args.k, seed,
@@ -288,16 +296,16 @@ def main():
         # salt = round) into two alternating staged batches
         NP = 2
         bound = 73 + cmd_cap  # EntryBatch element bound (drb_codec.hpp)
-        # the KV keeps up to kv_slots keys per replica, their values in a
-        # block pool: a block per slot at 128 B (26 GB); 4 per replica at
-        # 1 KB (52 GB) -- a run writing more new keys per replica than
-        # that shows CAPACITY/apply fallbacks in the histogram
-        ks = 16 if args.payload == 128 else 8
+        # the KV: C5_SLOTS keys per replica, the values in one shared pool
+        # sized for the keys the run writes (c5_pool_blocks)
+        ks = C5_SLOTS
+        c5_rounds = 2 * args.warmup + args.steps + 8
         eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
                      max_props=max(1, k), prop_slots=NP, ri_slots=1,
                      mailbox=8, kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
-                     kv_pool_blocks=ks * G * R if args.payload == 128
-                     else 4 * G * R, save_cap=(4 * bound + 15) // 16 * 16 +
+                     kv_pool_blocks=c5_pool_blocks(G, R, c5_rounds * k,
+                                                   args.active_ppm),
+                     save_cap=(4 * bound + 15) // 16 * 16 +
                      (128 if args.save in ("tan", "tanmux") else 0),
                      save_tan=int(args.save in ("tan", "tanmux")),
                      tan_multiplexed=int(args.save == "tanmux"),
@@ -337,7 +345,7 @@ def main():
         # ctx, served inside the round (drb_round_in.reads_per_ctx)
         fused = reads and args.reads_mode == "fused"
         if c5:  # this round's 1 % (an independent draw every round)
-            eng.gen_kv_proposals(i % NP, k, C5_KEYS[args.payload],
+            eng.gen_kv_proposals(i % NP, k, C5_KEYS,
                                  C5_VAL[args.payload], seed,
                                  i, active_ppm=args.active_ppm)
         if b is None:
@@ -558,26 +566,31 @@ def main():
                                not args.failover)
     if args.host_staged:
         # the same rounds with this round's proposals staged from host
-        # memory (the entryQueue as the host holds it: drb_entry rows and a
-        # Cmd pool, uploaded and laid out on the device, one call a round)
+        # memory: the entryQueue as a host builds its per-round upload
+        # (drb_stage_proposals_packed: per group a count, per entry Key /
+        # ClientID / Cmd length, the Cmd bytes back to back), uploaded and
+        # laid out on the device, one call a round
         import ctypes as C
         from dragonboat_amd import workload
         # the host arrays in pinned memory, so the upload overlaps the
-        # previous round (drb_stage_proposals copies on its own stream)
+        # previous round (the staging copies run on their own stream)
         HB = 8  # host batches, cycled
         hb = [tuple(torch.from_numpy(x.view("u1")).pin_memory()
-                    for x in workload.build_batch_np(G, seed, b))
+                    for x in workload.build_packed_np(G, seed, b))
               for b in range(HB)]
-        hp = [(C.cast(c.data_ptr(), C.POINTER(C.c_uint32)),
-               C.cast(e.data_ptr(), C.POINTER(_abi.Entry)),
-               C.cast(p.data_ptr(), C.POINTER(C.c_uint8))) for c, e, p in hb]
+        u8p, u64p, u16p = (C.POINTER(C.c_uint8), C.POINTER(C.c_uint64),
+                           C.POINTER(C.c_uint16))
+        hp = [(C.cast(c.data_ptr(), u8p), kk.numel() // 8,
+               C.cast(kk.data_ptr(), u64p), C.cast(ci.data_ptr(), u64p),
+               C.cast(ln.data_ptr(), u16p), C.cast(pl.data_ptr(), u8p),
+               pl.numel()) for c, kk, ci, ln, pl in hb]
         KH = max(5, min(K, 20))
         eng.read_counters(reset=True)
         eng.sync()
         h0 = time.perf_counter()
         for i in range(KH):
             b = i % HB
-            eng.stage_proposals(b, *hp[b], pool_len=hb[b][2].numel())
+            eng.stage_proposals_packed(b, _abi.ENTRY_ENCODED, *hp[b])
             step(2 * args.warmup + K + i, b)
         eng.sync()
         hms = (time.perf_counter() - h0) * 1e3 / KH
@@ -588,9 +601,11 @@ def main():
                                                                  1e-3),
             "upload_bytes_per_round": int(sum(x.numel() for x in hb[0])),
             "note": "proposals staged from pinned host memory every round "
-                    "(drb_stage_proposals: one H2D per array on a copy "
-                    "stream, overlapping the previous round, + a layout "
-                    "kernel), timed around the whole loop; not `value`"}
+                    "in the packed form (drb_stage_proposals_packed: Key, "
+                    "ClientID, Cmd length and bytes per entry, one H2D per "
+                    "array on a copy stream overlapping the previous round, "
+                    "+ scans and a layout kernel), timed around the whole "
+                    "loop; not `value`"}
         del hb, hp
     # the replicas that left the fast path during the run, by reason
     # (drb_take_flagged): a run with any is not a pure fast-path number
@@ -622,7 +637,7 @@ def main():
                   "round (independent seeded draw each round, generated "
                   "inside the timed loop), %s, tick "
                   "every %d round(s); Quiesce %s%s" % (
-                      G, R, args.payload, C5_KEYS[args.payload],
+                      G, R, args.payload, C5_KEYS,
                       args.active_ppm, sv, args.tick_every,
                       "on" if args.quiesce else "off",
                       ", listed rounds" if args.listed else ""))

@@ -55,10 +55,11 @@ def _request(p, slot, targets):
 
 
 def _leader(p, g):
+    """The group's one leader (replica ID), 0 while it has none or two (a
+    campaign in flight, a deposed leader not yet told)."""
     ls = [s for s, st in enumerate(p.eng.export_replicas(g, 1))
           if st.role == abi.LEADER]
-    assert len(ls) == 1, (g, ls)
-    return ls[0] + 1
+    return ls[0] + 1 if len(ls) == 1 else 0
 
 
 @pytest.mark.parametrize("R,pre_vote,at", [(3, 0, "leader"),

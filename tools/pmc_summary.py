@@ -38,8 +38,15 @@ def main():
     ap.add_argument("--groups", type=int, default=1 << 20)
     ap.add_argument("--replicas", type=int, default=3)
     ap.add_argument("--workload", default="")
+    ap.add_argument("--last", type=int, default=0,
+                    help="average only the last N launches of each kernel "
+                         "(the timed rounds, after a KV fill's rounds)")
     a = ap.parse_args()
     fetch, write = load(a.fetch), load(a.write)
+    if a.last:
+        for per in (fetch, write):
+            for key in per:
+                per[key] = per[key][-a.last:]
     kernels = {}
     for (name, ctr), vals in list(fetch.items()) + list(write.items()):
         k = kernels.setdefault(name, {})
