@@ -199,7 +199,7 @@ class Region(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
 
 
-PLANE_REGIONS = 8
+PLANE_REGIONS = 10
 PLANE_C1 = 1 << 18
 
 

@@ -130,15 +130,15 @@ def build(force=False, verbose=False, out=None, defines=(), jobs=None,
 
 
 if __name__ == "__main__":
-    # python build.py [--force] [-v] [--variant NAME -DX=1 ...]: a variant
-    # goes to tools/_bin/NAME.so (bench.py loads it with DRB_ENGINE_LIB)
+    # python build.py [--force] [-v] [--variant NAME [--r=R] -DX=1 ...]: a
+    # variant goes to _lib/variants/NAME.so (bench.py loads it with
+    # DRB_ENGINE_LIB; in-tree, so it travels to the GPU box)
     args = sys.argv[1:]
     if "--variant" in args:
         i = args.index("--variant")
         name, defs = args[i + 1], [a[2:] for a in args[i + 2:]
                                    if a.startswith("-D")]
-        out = os.path.join(os.path.dirname(HERE), "tools", "_bin",
-                           name + ".so")
+        out = os.path.join(LIBDIR, "variants", name + ".so")
         os.makedirs(os.path.dirname(out), exist_ok=True)
         vr = tuple(int(a[4:]) for a in args if a.startswith("--r="))
         print(build(verbose="-v" in args, out=out, defines=defs,

@@ -217,8 +217,6 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   // (the tan write pass lists replicas by 32-bit lane number)
   if (cfg->save_tan && (uint64_t)cfg->num_replicas * cfg->num_groups > 0xffffffffull)
     return DRB_ERANGE;
-  // elections: the raft launch steps co-resident replicas
-  if (cfg->elections && cfg->place_world > 1) return DRB_EINVAL;
   // entry_mbox travels as the 8-bit E of the plane summary word
   // (block_plane_summary, DRB_PLANE_E)
   if (cfg->place_world > 1 &&
@@ -398,6 +396,10 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.slow_n, 1);
     rc |= dalloc(e, &v.rterm, 2ull * R * R * v.MB * G);
     rc |= dalloc(e, &v.xfer_in, (uint64_t)R * G);
+    if (v.remote_mask) {
+      rc |= dalloc(e, &v.rterm_in, 2ull * R * R * v.MB * G);
+      rc |= dalloc(e, &v.xslow, 4ull * R * R * ((G + 255) / 256));
+    }
   }
   e->ctr_rows = 2ull * R * ((G + 255) / 256);  // see block_counters
   rc |= dalloc(e, &v.counters, e->ctr_rows * NUM_COUNTERS);
@@ -1880,6 +1882,10 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
     HIPCHK(hipMemsetAsync(e->v.xrows, 0,
                           2ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
                           e->stream));
+  if (e->v.xslow)
+    HIPCHK(hipMemsetAsync(e->v.xslow, 0,
+                          4ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
+                          e->stream));
   switch (e->v.R) {
     case 1: launch_step<1>(e, p); break;
     case 2: launch_step<2>(e, p); break;
@@ -2273,8 +2279,8 @@ extern "C" int drb_export_ready_to_reads(drb_engine *e, uint64_t group,
 // ---------------------------------------------------------------- exchange
 // the plane words (include/drb_engine.h DRB_PLANE_*) reduced over the
 // per-block rows of both roles: max counts, OR of the flags
-__global__ void k_plane_sum(const uint32_t *rows, uint32_t RR,
-                            uint32_t blocks, uint32_t *out) {
+__global__ void k_plane_sum(const uint32_t *rows, const uint32_t *slow,
+                            uint32_t RR, uint32_t blocks, uint32_t *out) {
   __shared__ uint32_t red[4][256];
   const uint32_t pair = blockIdx.x;
   uint32_t kr = 0, ko = 0, en = 0, f = 0;
@@ -2285,6 +2291,14 @@ __global__ void k_plane_sum(const uint32_t *rows, uint32_t RR,
       ko = max(ko, DRB_PLANE_KOTH(w));
       en = max(en, DRB_PLANE_E(w));
       f |= w & (DRB_PLANE_C1 | DRB_PLANE_HDR);
+    }
+  if (slow)  // the raft launch's lanes (elections)
+    for (uint32_t b = threadIdx.x; b < blocks; b += blockDim.x) {
+      const uint32_t *q = slow + ((uint64_t)pair * blocks + b) * 4;
+      kr = max(kr, q[0]);
+      ko = max(ko, q[1]);
+      en = max(en, q[2]);
+      f |= q[3] << 18;
     }
   red[0][threadIdx.x] = kr;
   red[1][threadIdx.x] = ko;
@@ -2312,7 +2326,8 @@ extern "C" int drb_plane_counts(drb_engine *e, uint32_t *words) {
     return DRB_OK;
   }
   const uint32_t blocks = (uint32_t)((v.G + 255) / 256);
-  k_plane_sum<<<RR, 256, 0, e->stream>>>(v.xrows, RR, blocks, e->xcount);
+  k_plane_sum<<<RR, 256, 0, e->stream>>>(v.xrows, v.xslow, RR, blocks,
+                                         e->xcount);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(words, e->xcount, RR * sizeof(uint32_t),
                         hipMemcpyDeviceToHost, e->stream));
@@ -2359,6 +2374,13 @@ extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
     if (Ko)
       out[n++] = {mb + mbox_ix(v, buf, from, to, v.MB - Ko, c, 0),
                   Ko * G * 16};
+  }
+  if ((word & DRB_PLANE_TOTHER) && v.rterm_in) {
+    // records with a term of their own (the raft launch): their rterm rows
+    uint64_t *rt = dir ? v.rterm_in : v.rterm;
+    if (Kr) out[n++] = {rt + rterm_ix(v, buf, from, to, 0, 0), Kr * G * 8};
+    if (Ko)
+      out[n++] = {rt + rterm_ix(v, buf, from, to, v.MB - Ko, 0), Ko * G * 8};
   }
   if (Kr || Ko || (word & DRB_PLANE_HDR))
     out[n++] = {meta + mmeta_ix(v, buf, from, to, 0), G * 16};

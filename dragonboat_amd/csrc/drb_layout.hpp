@@ -387,6 +387,13 @@ struct View {
   uint4 *embox;           // [2][R][R][E][ENT_META + C16][G] entries
   uint4 *embox_in;
   uint32_t *xrows;        // [2 roles][R][R][blocks] per-block plane summary
+  // elections with placement: the raft launch's lanes are not a block of
+  // one slot, so it adds its planes' summaries per lane to [R][R][blocks][4]
+  // {max K rep, max K other, max E, flags} (atomics), and the records with
+  // a term of their own bring their rterm rows along (rterm_in, shaped as
+  // rterm)
+  uint32_t *xslow;
+  uint64_t *rterm_in;
   unsigned long long *counters;  // [8] (drb_round_out order from index 1)
   // flagged-replica list (drb_take_flagged): {g lo, g hi, slot | reason
   // << 8 | flags << 16, round}, appended with one atomic per marked lane

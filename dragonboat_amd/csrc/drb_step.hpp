@@ -71,6 +71,12 @@ namespace drb {
 #ifndef DRB_READ_W
 #define DRB_READ_W 4
 #endif
+// follower inbox prefetch: the first DRB_FPF records from the (one)
+// sender with records, loaded to LDS at once by LDS-DMA (global_load_lds:
+// no VGPRs) instead of one dependent load per record in the dispatch loop
+#ifndef DRB_FPF
+#define DRB_FPF 8
+#endif
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
@@ -470,6 +476,40 @@ DRB_DEV bool rem_try_update(const Lane &L, int s, uint64_t index) {
 
 // ------------------------------------------------------------ log
 // commitTo (logentry.go:336-349)
+// The lowest next the round's ReplicateResps from remote s can leave it
+// at (pre-pass): a reject goes back to match + 1 in Replicate state, else
+// to max(1, min(LogIndex, Hint + 1)) (decreaseTo, remote.go:182-198); an
+// accepted one to max(match, LogIndex) + 1 (tryUpdate + respondedTo,
+// remote.go:143-176) -- a fresh leader's remotes (match 0) get their
+// floors from the answers, not from 1.
+template <int R>
+DRB_DEV uint64_t resp_floor(const Lane &L, const RemoteV &x, int s,
+                            uint32_t ns) {
+  const View &v = *L.v;
+  const bool rm = pair_remote(v, s, L.slot);
+  const uint4 *mb = rm ? v.mbox_in : v.mbox;
+  const uint32_t nrp = mi_nrep(
+      (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(v, L.rbuf, s, L.slot, L.g)].y);
+  uint64_t f = x.n;
+  for (uint32_t j = nrp; j < ns; ++j) {
+    const uint32_t k = rec_pos(false, j - nrp, v.MB);
+    const uint4 c0 = mb[mbox_ix(v, L.rbuf, s, L.slot, k, 0, L.g)];
+    if ((c0.x & 0xffu) != DRB_MSG_REPLICATE_RESP) continue;
+    const uint64_t idx = hi64(c0);
+    uint64_t c;
+    if (c0.x & MF_REJECT) {
+      const uint64_t hint =
+          (c0.x & MF_HAS_C1) ? lo64(mb[mbox_ix(v, L.rbuf, s, L.slot, k, 1, L.g)])
+                             : 0;
+      c = umin64(x.m + 1, umax64(1, umin64(idx, hint + 1)));
+    } else {
+      c = umax64(x.m, idx) + 1;
+    }
+    f = umin64(f, c);
+  }
+  return f;
+}
+
 template <int R>
 DRB_DEV void commit_to(Rep<R> &r, uint64_t index) {
   if (index <= r.committed) return;
@@ -2158,6 +2198,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[256];
   __shared__ uint64_t rq_lds[LEAD ? 2 * DRB_RI_DEPTH : 1][256];
+  constexpr bool FPF = !LEAD && !SLOW && DRB_FPF > 0;
+  __shared__ uint4 pf_lds[FPF ? DRB_FPF : 1][256];
   // placement C4 only: [R][256] (the launch sizes it, drb_step_inst.hip)
   extern __shared__ uint64_t elo_dyn[];
   uint64_t(*elo_lds)[256] = reinterpret_cast<uint64_t(*)[256]>(elo_dyn);
@@ -2274,6 +2316,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     uint32_t qz_from = 0;   // senders whose Quiesce message arrived
     uint64_t nri_packed = 0;  // 5-bit ReadIndex record count per sender
     uint64_t max_app = 0;
+    int pf_s = -1;         // follower: the sender whose records are in pf_lds
+    uint32_t pf_nrp = 0;   // ... and its Replicate count
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot) continue;
@@ -2327,7 +2371,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                              !(x & MF_REJECT));
             const uint64_t rt =
                 (x & MF_TERM_OTHER)
-                    ? v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)]
+                    ? (rm ? v.rterm_in : v.rterm)[rterm_ix(v, L.rbuf, s, slot,
+                                                           k, g)]
                     : (x & MF_TERM_ZERO) ? 0 : hi64(meta);
             if ((x & MF_TERM_OTHER) && !pv && rt > r.term) higher_in = true;
             if (rt > r.term && el_leader_message(x & 0xffu))
@@ -2351,6 +2396,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       if (!is_leader && mi_nrep(info))
         max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
                                       v, L.rbuf, s, slot, g)]);
+      if (FPF && ns && pf_s < 0) {
+        // the records go to LDS in one batch; the dispatch loop reads them
+        // there (after the wait below)
+        pf_s = s;
+        pf_nrp = mi_nrep(info);
+        const uint4 *mb = rm ? v.mbox_in : v.mbox;
+#pragma unroll
+        for (int j = 0; j < (FPF ? DRB_FPF : 1); ++j)
+          if ((uint32_t)j < ns) {
+            const uint32_t jj = (uint32_t)j;
+            const uint32_t k =
+                rec_pos(jj < pf_nrp, jj < pf_nrp ? jj : jj - pf_nrp, v.MB);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(
+                    mb + mbox_ix(v, L.rbuf, s, slot, k, 0, g)),
+                (__attribute__((address_space(3))) void *)&pf_lds[j][
+                    threadIdx.x & ~63u],
+                16, 0, 0);
+          }
+      }
       total_in += ns;
     }
     uint32_t nprops = 0;
@@ -2372,7 +2437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       // with elections a group can hold two leaders (a stale one and the
       // new one): its entry queue goes to the hosted leader in the highest
       // slot (the NodeHost the client reaches; tests/gpu_harness.py)
-      if (v.elections && nprops) {
+      if (v.elections && nprops && v.place_world <= 1) {
 #pragma unroll
         for (int s = 0; s < R; ++s)
           if ((uint32_t)s > slot &&
@@ -2413,7 +2478,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         // again below the window, that round falls back.
         if (x.st == DRB_REMOTE_WAIT && !((nin_packed >> (5 * s)) & 31u))
           continue;
-        const uint64_t lowest = ((rej_from >> s) & 1) ? umin64(x.m, x.n) : x.n;
+        uint64_t lowest = ((rej_from >> s) & 1) ? umin64(x.m, x.n) : x.n;
+        // an accepting answer outside Replicate state may lower next to
+        // the answer's match + 1 (respondedTo: a fresh leader's remotes)
+        if (!((rej_from >> s) & 1) && ((resp_from >> s) & 1) &&
+            x.st != DRB_REMOTE_REPLICATE)
+          lowest = umin64(lowest, resp_floor<R>(L, x, s,
+                                                (uint32_t)((nin_packed >>
+                                                            (5 * s)) & 31u)));
         const uint64_t need = lowest > 0 ? lowest - 1 : 0;  // LogTerm index
         keep = umin64(keep, need);
         const bool ents_below = need < r.last && need + 1 < r.ring_lo;
@@ -2437,7 +2509,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
             const bool lowers = ((rej_from >> s) & 1) ||
                                 (((resp_from >> s) & 1) &&
                                  x.st != DRB_REMOTE_REPLICATE);
-            const uint64_t floor = lowers ? x.m + 1 : x.n;
+            const uint64_t floor =
+                lowers ? resp_floor<R>(L, x, s,
+                                       (uint32_t)((nin_packed >> (5 * s)) & 31u))
+                       : x.n;
             if (r.last + nprops + 1 > floor + v.E && fb == DRB_FB_NONE)
               fb = DRB_FB_CAPACITY;
           }
@@ -2583,6 +2658,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           follower_read_index(L, r, in_lo, in_hi);
       }
       // handleReceivedMessages: Replicates by sender, then the rest
+      if (FPF && pf_s >= 0)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): pf_lds landed
 #pragma unroll 1
       for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll 1
@@ -2609,14 +2686,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           // spills more, profiles/r02_kvline/README.md)
           for (uint32_t j = 0; j < cnt; ++j) {
             const uint32_t k = rec_pos(pass == 0, j, v.MB);
-            const uint4 c0 = mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
+            const uint32_t ord = pass == 0 ? j : pf_nrp + j;
+            const uint4 c0 = (FPF && s == pf_s && ord < (uint32_t)DRB_FPF)
+                                 ? pf_lds[FPF ? ord : 0][threadIdx.x]
+                                 : mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
             uint4 c1 = make_uint4(0, 0, 0, 0);
             if (c0.x & MF_HAS_C1) c1 = mb[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
             // the raft launch: a record whose sender changed terms
             // within its round carries its own term (rterm)
             const uint64_t rt =
                 (SLOW && (c0.x & MF_TERM_OTHER))
-                    ? v.rterm[rterm_ix(v, L.rbuf, s, slot, k, g)]
+                    ? (rm ? v.rterm_in : v.rterm)[rterm_ix(v, L.rbuf, s, slot,
+                                                           k, g)]
                     : sterm;
             const Msg m = msg_decode(c0, c1, rt, prev_lo, prev_hi);
             if (qon)  // node.recordMessage (node.go:1339-1345)
@@ -2909,6 +2990,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
             w |= MI_TERM_OTHER;
           }
         }
+        oinfo[s * 256 + threadIdx.x] = w;  // (the plane summary's flag)
       }
       if (mi_count(w) || qz) {
         uint4 meta = mk4(0, r.term);
@@ -2929,8 +3011,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                        p.key_space, c_served, c_deferred);
   }
   // per-block summary of this rank's remote planes (drb_exchange_*): max
-  // records, max entry rows, c1 / Replicate flags
-  if (v.remote_mask) {  // uniform
+  // records, max entry rows, c1 / Replicate flags; the raft launch adds its
+  // lanes' to the slow rows, lane by lane (its lanes are no slot's block)
+  if (SLOW && v.remote_mask && active) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if ((uint32_t)s == slot || !pair_remote(v, slot, s)) continue;
+      const uint32_t w = oinfo[s * 256 + threadIdx.x];
+      uint32_t E = 0;
+      const uint64_t lo = elo_lds[s][threadIdx.x];
+      if (lo != ~0ull) E = (uint32_t)(last_final + 1 - lo);
+      const uint32_t fl = ((sent_c1 >> s) & 1u) | (((qz_out >> s) & 1u) << 1) |
+                          ((w & MI_TERM_OTHER) ? 4u : 0u);
+      if (!(mi_count(w) | E | fl)) continue;
+      uint32_t *q = v.xslow + (((uint64_t)slot * v.R + s) * ((v.G + 255) / 256) +
+                               g / 256) * 4;
+      atomicMax(&q[0], mi_nrep(w));
+      atomicMax(&q[1], mi_noth(w));
+      atomicMax(&q[2], E);
+      atomicOr(&q[3], fl);
+    }
+  }
+  if (!SLOW && v.remote_mask) {  // uniform
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot || !pair_remote(v, slot, s)) continue;

@@ -61,27 +61,36 @@ def place_peer(world, rank, a, b, direction):
     return _engine.lib().drb_place_peer(world, rank, a, b, direction)
 
 
-def full_word(mailbox, entry_mbox, leader_sender=True):
+PLANE_TOTHER = 1 << 20  # include/drb_engine.h DRB_PLANE_TOTHER
+
+
+def full_word(mailbox, entry_mbox, leader_sender=True, elections=False):
     """The summary word of a plane at full capacity (drb_plane_regions):
     every record position, both chunks, the header, and -- when the sender
     slot may hold leaders -- the max LogIndex word and every entry row.  A
-    follower-only sender slot sends responses (other records) only."""
-    if leader_sender:
-        return (mailbox & 0x1f) | ((entry_mbox & 0xff) << 10) | (1 << 18) | \
+    follower-only sender slot sends responses (other records) only.  With
+    elections every plane can carry both kinds, and the rterm rows of the
+    records the raft launch wrote with a term of their own."""
+    if leader_sender or elections:
+        w = (mailbox & 0x1f) | ((entry_mbox & 0xff) << 10) | (1 << 18) | \
             (1 << 19)
+        # (positions [0, mailbox) hold both kinds: Replicates from the
+        # bottom, the others from the top)
+        return w | (PLANE_TOTHER if elections else 0)
     return ((mailbox & 0x1f) << 5) | (1 << 18) | (1 << 19)
 
 
-def fixed_words(R, world, leader_mask, mailbox, entry_mbox):
+def fixed_words(R, world, leader_mask, mailbox, entry_mbox, elections=False):
     """Per-rank plane words of the fixed mode: plane (a, b) moves when a or
     b is a leader slot on some rank (leader_mask: the OR over the ranks of
-    drb_role_slots), at full capacity."""
+    drb_role_slots), at full capacity.  With elections roles change on the
+    device, so every plane moves."""
     row = []
     for a in range(R):
         for b in range(R):
             la, lb = (leader_mask >> a) & 1, (leader_mask >> b) & 1
-            row.append(0 if a == b or not (la or lb) else
-                       full_word(mailbox, entry_mbox, bool(la)))
+            row.append(0 if a == b or not (la or lb or elections) else
+                       full_word(mailbox, entry_mbox, bool(la), elections))
     return [row for _ in range(world)]
 
 
@@ -183,7 +192,8 @@ class PlaneExchange:
         if self.fixed:
             return fixed_words(R, self.world, self.leader_mask,
                                self.eng.cfg["mailbox"],
-                               self.eng.cfg["entry_mbox"])
+                               self.eng.cfg["entry_mbox"],
+                               bool(self.eng.cfg["elections"]))
         mine = self.eng.plane_counts()  # synchronises the engine stream
         dev = "cpu" if self.staged else self.device
         t = torch.tensor(mine, dtype=torch.int64, device=dev)

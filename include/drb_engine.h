@@ -344,10 +344,14 @@ typedef struct drb_config {
    * launch with the whole raft state machine instead (campaign,
    * RequestVote / RequestVoteResp, becomeFollower / Candidate / Leader,
    * the term gate, raft.go:1052-1217, 1507-1590, 1670-1722, 2235-2253);
-   * only capacity and off-path entries still fall back.  Co-resident
-   * placement; with Quiesce a quiesced replica ticks with quiescedTick
-   * (raft.go:650-656: no election) until input ends its quiesce
-   * (node.go:1296-1345, quiesce.go:56-74); listed rounds allowed. */
+   * only capacity and off-path entries still fall back.  With Quiesce a
+   * quiesced replica ticks with quiescedTick (raft.go:650-656: no
+   * election) until input ends its quiesce (node.go:1296-1345,
+   * quiesce.go:56-74); listed rounds allowed.  With placement (place_world
+   * > 1) the votes and the new leaders' messages cross ranks in the planes
+   * (drb_plane_regions ships the rterm rows of records whose term is not
+   * their header's, DRB_PLANE_TOTHER); staged input reaches a group only
+   * while its leader is at the stage slot. */
   uint32_t elections;
   /* tan MaxLogFileSize (internal/tan/options.go:29); 0: 64 MiB */
   uint64_t tan_max_log;
@@ -778,7 +782,7 @@ typedef struct drb_region {
   uint64_t bytes;
 } drb_region;
 
-#define DRB_PLANE_REGIONS 8
+#define DRB_PLANE_REGIONS 10
 /* per lane (max): Replicate records (positions 0..), other records
  * (positions mailbox-1 downwards), entry rows; a record's 2nd chunk */
 #define DRB_PLANE_KREP(w) ((w) & 0x1fu)
@@ -786,6 +790,9 @@ typedef struct drb_region {
 #define DRB_PLANE_E(w) (((w) >> 10) & 0xffu)
 #define DRB_PLANE_C1 (1u << 18)
 #define DRB_PLANE_HDR (1u << 19)  /* a header without records (Quiesce) */
+/* records with a term of their own (elections: the raft launch's
+ * MF_TERM_OTHER records): their rterm rows travel with the plane */
+#define DRB_PLANE_TOTHER (1u << 20)
 
 /* words[from * R + to] for this rank's remote planes of the last round
  * (0 for local or empty ones).  Synchronises the engine stream. */
@@ -795,12 +802,15 @@ int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to, int dir);
 /* The same routing as a pure function of the placement (no device). */
 int drb_place_peer(uint32_t world, uint32_t rank, uint32_t from, uint32_t to,
                    int dir);
-/* The engine's role map, kept on the host (roles change only by init and
- * import; a replica whose role would change in a round falls back): bit s
- * of *leader_slots when a hosted replica at slot s is a leader, of
- * *follower_slots when one is not.  No device work.  With fixed-capacity
- * exchange, plane (from, to) can carry fast-path messages only when `from`
- * or `to` is a leader slot on some rank (followers send only to leaders). */
+/* The engine's role map, kept on the host (without elections roles change
+ * only by init and import; a replica whose role would change in a round
+ * falls back): bit s of *leader_slots when a hosted replica at slot s is a
+ * leader, of *follower_slots when one is not.  No device work.  With
+ * fixed-capacity exchange, plane (from, to) can carry fast-path messages
+ * only when `from` or `to` is a leader slot on some rank (followers send
+ * only to leaders).  With drb_config.elections roles change on the device
+ * (the raft launch), so a fixed exchange moves every remote plane, with
+ * DRB_PLANE_TOTHER (dragonboat_amd/exchange.py fixed_words). */
 int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
                    uint32_t *follower_slots);
 /* The device regions of plane (from, to) for the last round, sized by the

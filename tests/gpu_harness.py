@@ -283,9 +283,37 @@ class DistPair:
                      for r in range(N)]
         self.orc = po.Cluster(G, R, seed=seed)
         self.orc.setup_steady(0)
+        if engine_kw.get("pre_vote"):
+            self.orc.set_pre_vote(True)
         for e in self.engs:
             e.init_steady(term=2, leader_slot=0, seed=seed)
         self.rounds = 0
+
+    def set_hosted(self, g, s, hosted):
+        """Replica slot s of group g stops (or returns) on both sides."""
+        self.orc.set_hosted(g, s, hosted)
+        r, j = self.where(g, s)
+        sts = self.engs[r].export_replicas(j, 1)
+        if hosted:
+            sts[s].flags |= abi.F_HOSTED
+        else:
+            sts[s].flags &= ~abi.F_HOSTED
+        self.engs[r].import_replicas(j, sts)
+
+    def why(self):
+        """The replicas flagged since the last call on every rank:
+        (global group, slot, reason, flags, round)."""
+        out = []
+        for r, e in enumerate(self.engs):
+            recs, _ = e.take_flagged()
+            for (j, s, reason, flags, rnd, _) in recs:
+                out.append((self.lane_group(r, s, j), s,
+                            abi.FB_NAME.get(reason, reason), flags, rnd))
+        return out
+
+    def replica(self, g, s):
+        r, j = self.where(g, s)
+        return self.engs[r].export_replicas(j, 1)[s]
 
     def where(self, g, s):
         """(rank, lane) of replica slot s of group g."""
@@ -334,7 +362,8 @@ class DistPair:
         self.rounds += 1
         tot = {}
         for f in ("committed_entries", "applied_entries", "messages",
-                  "ready_to_reads", "fallbacks", "errors"):
+                  "ready_to_reads", "fallbacks", "errors",
+                  "elections_stepped", "role_changes"):
             tot[f] = sum(getattr(x, f) for x in outs)
         return o, tot
 

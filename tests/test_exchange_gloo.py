@@ -169,3 +169,19 @@ def test_full_word_layout():
         for b in range(R):
             w = ws[0][a * R + b]
             assert bool(w) == (a != b and 0 in (a, b)), (a, b)
+
+
+def test_fixed_words_with_elections():
+    """With elections roles change on the device (the raft launch), so the
+    fixed mode moves every remote plane at full capacity -- Replicates and
+    responses alike -- with the rterm rows of the records that carry a term
+    of their own (DRB_PLANE_TOTHER, drb_plane_regions)."""
+    from dragonboat_amd import exchange as X
+    ws = X.fixed_words(R, 2, 1, 13, 3, elections=True)
+    for a in range(R):
+        for b in range(R):
+            w = ws[0][a * R + b]
+            assert bool(w) == (a != b), (a, b)
+            if w:
+                assert w == X.full_word(13, 3) | X.PLANE_TOTHER
+                assert (w & 0x1f) == 13 and ((w >> 5) & 0x1f) == 0

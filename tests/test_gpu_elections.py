@@ -194,3 +194,57 @@ def test_quiesced_groups_fail_over(pre_vote, listed):
         assert len(lead) == 1 and roles[lead[0]][1] >= 3, roles
     assert st["slow"] > 0 and st["roles"] >= len(E)
     rounds(10)
+
+
+@pytest.mark.parametrize("N,R,G,pre_vote", [(2, 3, 24, 0), (3, 5, 30, 1),
+                                            (4, 3, 24, 0), (8, 5, 40, 0)])
+def test_failover_with_replicas_spread_over_ranks(N, R, G, pre_vote):
+    """Elections under C4 placement (replica slot s of group g on rank
+    (g + s) mod N, drb_exchange_local moving the planes between the ranks'
+    engines -- what RCCL moves between GPUs): the leader replica of some
+    groups stops, its followers on other ranks time out, campaign and elect
+    in their raft launches, the votes and the new leader's Replicates and
+    entry rows crossing ranks (with the rterm rows of records whose term is
+    not their header's).  The old leader then returns and steps down.
+    Bit-exact with one oracle cluster of all G groups every round.  Client
+    input goes to the groups whose leader stayed at the stage slot
+    (drb_stage_proposals stages a lane's batch at slot 0's replica)."""
+    from tests.gpu_harness import DistPair
+    p = DistPair(G=G, R=R, N=N, max_props=2, elections=1, pre_vote=pre_vote)
+    st = {"slow": 0, "roles": 0}
+    E = [g for g in range(G) if g % 5 == 2]
+    rest = [g for g in range(G) if g not in E]
+
+    def rounds(n, groups=None, k=1):
+        for _ in range(n):
+            o, e = p.round(k=k, tick=True, read_index=(p.rounds % 3 == 0),
+                           groups=groups)
+            assert e["fallbacks"] == 0 and e["errors"] == 0, (p.rounds, e,
+                                                              p.why())
+            assert (e["committed_entries"], e["messages"]) == \
+                (o.committed_entries, o.messages), (p.rounds, e, o.to_dict())
+            errs = p.check()
+            assert not errs, (p.rounds, errs[:2])
+            st["slow"] += e["elections_stepped"]
+            st["roles"] += e["role_changes"]
+
+    rounds(3)
+    for g in E:
+        p.set_hosted(g, 0, False)
+    for _ in range(60):
+        rounds(1, groups=rest)
+        if all(any(p.replica(g, s).role == abi.LEADER for s in range(1, R))
+               for g in E):
+            break
+    for g in E:
+        lead = [s for s in range(1, R) if p.replica(g, s).role == abi.LEADER]
+        assert len(lead) == 1 and p.replica(g, lead[0]).term >= 3, g
+    assert st["slow"] > 0 and st["roles"] >= len(E)
+    rounds(4, groups=rest)
+    for g in E:
+        p.set_hosted(g, 0, True)
+    rounds(12, groups=rest)
+    for g in E:
+        roles = [p.replica(g, s).role for s in range(R)]
+        assert roles[0] == abi.FOLLOWER and roles.count(abi.LEADER) == 1, \
+            (g, roles)

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 o=gpurun_out/abl; mkdir -p $o
 B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --tick-every 1"
 for n in "$@"; do
-  if [ "${n:0:4}" = base ]; then lib=""; else lib=tools/_bin/$n.so; fi
+  if [ "${n:0:4}" = base ]; then lib=""; else lib=dragonboat_amd/_lib/variants/$n.so; fi
   export DRB_ENGINE_LIB=$lib
   tools/gpu_step.sh 200 $o/${n}_bench.log python bench.py --steps 40 --warmup 8 --no-cpu-baseline || exit 1
   tools/gpu_step.sh 200 $o/${n}_fetch.log rocprofv3 --pmc FETCH_SIZE -d $o/${n}_fetch -o run --output-format csv -- $B || exit 1
