@@ -46,15 +46,19 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
 
 def pmc_traffic(G, R):
     """HBM bytes per round from the committed rocprofv3 PMC passes of this
-    workload (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE over the
-    round's kernels), or None when none matches this configuration."""
+    workload (tools/pmc_summary.py over the timed rounds' step kernels):
+    (FETCH_SIZE x2 + WRITE_SIZE, FETCH_SIZE + WRITE_SIZE).  The first is an
+    upper bound -- the x2 correction is for coalesced 16 B/lane reads, and
+    the KV's random 16 B reads are already tallied at 64 B each -- the
+    second the matching lower bound.  (None, None) when no summary matches
+    this configuration."""
     try:
         s = json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
-        return None
+        return None, None
     if s.get("groups") != G or s.get("replicas") != R:
-        return None
-    return s.get("round_hbm_bytes")
+        return None, None
+    return s.get("round_hbm_bytes"), s.get("round_hbm_bytes_lower")
 
 
 def parse():
@@ -448,6 +452,8 @@ def main():
         if saves:  # + the save bytes the round writes
             alg += out.saved_bytes / K
     achieved = alg / (kern_ms * 1e-3) / 1e9
+    traffic = (None, None) if (c2 or c4 or c5 or args.kv_fill == 0) else \
+        pmc_traffic(G, R)
     wire = None
     if not (c4 or c5 or args.no_wire):
         # after the timed region: the last round's leader -> follower-slot-1
@@ -691,10 +697,15 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None if (c2 or c4 or c5) else pmc_traffic(G, R),
-                "traffic_source": "profiles/pmc_current.json (rocprofv3 "
-                                  "FETCH_SIZE x2 + WRITE_SIZE, bytes per "
-                                  "round)",
+                "traffic": traffic[0],
+                "traffic_lower": traffic[1],
+                "traffic_source": "profiles/pmc_current.json (rocprofv3, "
+                                  "the timed rounds' step kernels, bytes per "
+                                  "round): traffic = FETCH_SIZE x2 + "
+                                  "WRITE_SIZE, an upper bound (the x2 is for "
+                                  "coalesced reads; a random 16 B KV read is "
+                                  "tallied at 64 B already), traffic_lower = "
+                                  "FETCH_SIZE + WRITE_SIZE",
                 "alg_bytes_per_launch": alg,
                 "kernel_ms": kern_ms},
             "counters": {"committed_per_round": committed / K / world,

@@ -1103,14 +1103,17 @@ extern "C" int drb_stage_proposals_packed(
     return DRB_EINVAL;
   const View &v = e->v;
   const uint64_t G = v.G, n = n_entries;
-  uint64_t tot = 0, bytes = 0;
+  // the sums (vectorised loops; on 8 host threads the call measured slower:
+  // thread start-up costs more than the 3 MB these read)
+  uint64_t tsum = 0, bsum = 0;
+  uint32_t cmax = 0;
   for (uint64_t g = 0; g < G; ++g) {
-    if (counts[g] > v.max_props) return DRB_ERANGE;
-    tot += counts[g];
+    cmax = std::max<uint32_t>(cmax, counts[g]);
+    tsum += counts[g];
   }
-  if (tot != n) return DRB_EINVAL;
-  for (uint64_t i = 0; i < n; ++i) bytes += cmd_lens[i];
-  if (bytes != pool_len) return DRB_EINVAL;
+  if (cmax > v.max_props) return DRB_ERANGE;
+  for (uint64_t i = 0; i < n; ++i) bsum += cmd_lens[i];
+  if (tsum != n || bsum != pool_len) return DRB_EINVAL;
   // upload: counts | keys | client ids | lengths | pool, then device-side
   // u32 counts, lengths, their scans and the scans' temp storage
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };

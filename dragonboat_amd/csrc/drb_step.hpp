@@ -77,6 +77,9 @@ namespace drb {
 #ifndef DRB_FPF
 #define DRB_FPF 8
 #endif
+#ifndef DRB_REM_DIRTY
+#define DRB_REM_DIRTY 1
+#endif
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
@@ -156,6 +159,10 @@ struct RemLds {
   uint64_t n[R][256];
   uint32_t st[R][256];
   uint32_t a[R][256];
+  // fields changed this round, bit 4 * peer + {m, n, st, a}: the end of
+  // the round stores only those (a heartbeat round, C5's common one,
+  // changes none)
+  uint32_t dirty[256];
 };
 
 struct Lane {
@@ -172,6 +179,10 @@ struct Lane {
   uint32_t rbuf, wbuf;
   uint64_t round;
   bool slow;  // the raft launch (elections): records carry their own term
+  // the remotes' fields are stored back only where they changed (the EXT
+  // instantiation: C5's heartbeat rounds change none; the C3 path keeps
+  // its registers for the unconditional stores)
+  bool dirty;
 };
 
 // ------------------------------------------------------------ helpers
@@ -443,6 +454,13 @@ DRB_DEV RemoteV rem_get(const Lane &L, int s) {
 template <int R>
 DRB_DEV void rem_put(const Lane &L, int s, const RemoteV &x) {
   RemLds<R> &t = rl_of<R>(L);
+  if (L.dirty) {  // EXT (C5): only changed fields go back to HBM
+    const uint32_t d = (t.m[s][L.tid] != x.m ? 1u : 0u) |
+                       (t.n[s][L.tid] != x.n ? 2u : 0u) |
+                       (t.st[s][L.tid] != x.st ? 4u : 0u) |
+                       (t.a[s][L.tid] != x.a ? 8u : 0u);
+    if (d) t.dirty[L.tid] |= d << (4 * s);
+  }
   t.m[s][L.tid] = x.m;
   t.n[s][L.tid] = x.n;
   t.st[s][L.tid] = x.st;
@@ -1893,6 +1911,7 @@ DRB_DEV void load_rep(const Lane &L, Rep<R> &r) {
                          v.rem_next[rem_ix(v, L.slot, s, L.g)],
                          v.rem_state[rem_ix(v, L.slot, s, L.g)],
                          v.rem_active[rem_ix(v, L.slot, s, L.g)]});
+    if (L.dirty) rl_of<R>(L).dirty[L.tid] = 0;
   }
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d) {
@@ -1955,13 +1974,16 @@ DRB_DEV void store_rep(const Lane &L, Rep<R> &r, uint32_t flags0,
   if (!LEAD) return;  // followers keep no remotes and no readIndex queue
   v.u32[u32_ix(v, W_RI_COUNT, L.slot, L.g)] = r.ri_count;
   {
+    const uint32_t dm = L.dirty ? rl_of<R>(L).dirty[L.tid] : 0xffffffffu;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
+      const uint32_t d = dm >> (4 * s);
+      if (!(d & 15u)) continue;
       RemoteV x = rem_get<R>(L, s);
-      v.rem_match[rem_ix(v, L.slot, s, L.g)] = x.m;
-      v.rem_next[rem_ix(v, L.slot, s, L.g)] = x.n;
-      v.rem_state[rem_ix(v, L.slot, s, L.g)] = x.st;
-      v.rem_active[rem_ix(v, L.slot, s, L.g)] = x.a;
+      if (d & 1u) v.rem_match[rem_ix(v, L.slot, s, L.g)] = x.m;
+      if (d & 2u) v.rem_next[rem_ix(v, L.slot, s, L.g)] = x.n;
+      if (d & 4u) v.rem_state[rem_ix(v, L.slot, s, L.g)] = x.st;
+      if (d & 8u) v.rem_active[rem_ix(v, L.slot, s, L.g)] = x.a;
     }
   }
 #pragma unroll
@@ -2220,8 +2242,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   L.rbuf = (uint32_t)((p.round - 1) & 1);
   L.wbuf = (uint32_t)(p.round & 1);
   L.slow = SLOW;
-  uint64_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
-  uint64_t c_rtr = 0, c_drop = 0;
+  L.dirty = EXT && DRB_REM_DIRTY;
+  uint32_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
+  uint32_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
   uint32_t c_stepped = 0, c_elect = 0, c_role = 0, c_dprop = 0;
   uint32_t sent_c1 = 0;     // remote planes: destinations given a c1 chunk
@@ -2733,6 +2756,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
               // leaderHasQuorum (raft.go:395-405): quorum held (pre-pass)
 #pragma unroll
               for (int s = 0; s < R; ++s) rl_of<R>(L).a[s][L.tid] = 0;
+              if (L.dirty) rl_of<R>(L).dirty[L.tid] |= 0x88888888u;
             }
           }
           r.heartbeat_tick++;
