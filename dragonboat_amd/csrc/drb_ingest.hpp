@@ -207,6 +207,58 @@ __device__ inline uint32_t d_message(const uint8_t *d, uint32_t n, DecMsg &m,
   return ING_OK;
 }
 
+// The payload CRC of a frame in 16 KB chunks, a workgroup per chunk:
+// thread t takes the 64 bytes that end 64 * (255 - t) bytes before the
+// chunk's end (a shorter chunk is right-aligned: the pieces before its
+// start are empty), runs the register-only CRC over them (init 0, no final
+// xor: f(piece), linear over GF(2)) and shifts it past the bytes after it,
+// f * x^(8 * 64 * (255 - t)) mod P (c_crc_k64, zlib's multmodp); the
+// chunk's f is the XOR of the 256 pieces' (f is blind to leading zeros).
+// The host combines the chunks of a frame with crc32_combine and applies
+// the CRC's ~0 conditioning once per frame.  Coalesced (a wave reads 4 KB
+// contiguous) with one chunk per workgroup, where the one-lane-per-chunk
+// kernel ran a handful of waves each walking 16 KB alone.
+__constant__ uint32_t c_crc_k64[256];
+__global__ __launch_bounds__(256) void k_crc_chunks(const uint8_t *data,
+                                                     const uint64_t *off,
+                                                     const uint32_t *len,
+                                                     uint32_t *fraw) {
+  __shared__ uint32_t t[8][256];
+  __shared__ uint32_t red[4];
+  for (uint32_t i = threadIdx.x; i < 8 * 256; i += blockDim.x)
+    t[i >> 8][i & 255] = c_crc_tab[i >> 8][i & 255];
+  __syncthreads();
+  const uint64_t b = blockIdx.x;
+  const int64_t L = len[b];
+  const int64_t e = L - 64 * (int64_t)(255 - threadIdx.x);
+  const int64_t s0 = e > 64 ? e - 64 : 0;
+  uint32_t c = 0;
+  if (e > 0) {
+    const uint8_t *p = data + off[b] + s0;
+    uint32_t l = (uint32_t)(e - s0);
+    while (l && ((uintptr_t)p & 7)) {
+      c = t[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+      l--;
+    }
+    while (l >= 8) {
+      const uint64_t w = *(const uint64_t *)p;
+      const uint32_t lo = (uint32_t)w ^ c, hi = (uint32_t)(w >> 32);
+      c = t[7][lo & 0xff] ^ t[6][(lo >> 8) & 0xff] ^ t[5][(lo >> 16) & 0xff] ^
+          t[4][lo >> 24] ^ t[3][hi & 0xff] ^ t[2][(hi >> 8) & 0xff] ^
+          t[1][(hi >> 16) & 0xff] ^ t[0][hi >> 24];
+      p += 8;
+      l -= 8;
+    }
+    while (l--) c = t[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+    if (c) c = gf2_multmodp(c_crc_k64[threadIdx.x], c);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) fraw[b] = red[0] ^ red[1] ^ red[2] ^ red[3];
+}
+
 // pass 1: entry counts and errors; the frame of a malformed message is
 // marked (the host stops the stream there)
 __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
@@ -224,6 +276,35 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   err[i] = r;
   if (r == ING_BAD) atomicOr(&frame_bad[mframe[i]], 1u);
   if (r == ING_BIG) atomicOr(&frame_bad[mframe[i]], 2u);
+}
+
+__global__ void k_widen_step(const uint32_t *in, uint64_t *out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+
+// Requests element i: its tag at the frame's payload offset plus the
+// in-frame inclusive sum of the steps (scan minus the frame's start), then
+// its tag and length varints (the host walk validated both)
+__global__ void k_ing_elems(const uint8_t *s, const uint64_t *scan,
+                            const uint64_t *mbase, const uint64_t *foff,
+                            const uint32_t *mframe, uint64_t *moff,
+                            uint32_t *mlen, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = mframe[i];
+  const uint64_t first = mbase[f];
+  uint64_t at = foff[f] + scan[i] - (first ? scan[first - 1] : 0);
+  uint32_t sh = 0;
+  while (s[at++] & 0x80u) {}  // the tag (field 1, wire type 2)
+  uint64_t l = 0;
+  for (;; sh += 7) {
+    const uint32_t b = s[at++];
+    l |= (uint64_t)(b & 0x7fu) << sh;
+    if (b < 0x80u) break;
+  }
+  moff[i] = at;
+  mlen[i] = (uint32_t)l;
 }
 
 // the frame of each message: the last frame whose first message is <= i
@@ -522,8 +603,11 @@ struct Frame {
   uint32_t method, pcrc;
   bool scan_ok = true;
   uint64_t did = 0, bv = 0;
-  std::vector<uint64_t> moff;  // Requests elements: stream offset, length
-  std::vector<uint32_t> mlen;
+  // Requests elements: where each element's tag starts, as the distance
+  // from the previous element's tag (the first: from the payload start);
+  // the GPU rebuilds offsets and lengths from these (k_ing_elems), so 4 B
+  // per message cross the link instead of a u64 offset and a u32 length
+  std::vector<uint32_t> step;
 };
 
 // MessageBatch.Unmarshal's top-level walk (raft_optimized.go:1056-1207):
@@ -531,9 +615,8 @@ struct Frame {
 static void scan_batch(const uint8_t *stream, Frame &f) {
   const uint8_t *p = stream + f.off;
   const size_t n = (size_t)f.size;
-  size_t j = 0;
-  f.moff.reserve(n / 32);
-  f.mlen.reserve(n / 32);
+  size_t j = 0, prev = 0;
+  f.step.reserve(n / 32);
   while (j < n) {
     uint64_t wire, v;
     // the common element: tag 0x0a and a one- or two-byte length
@@ -545,12 +628,13 @@ static void scan_batch(const uint8_t *stream, Frame &f) {
         h = 3;
       }
       if (l < (1u << 14) && l <= n - j - h) {
-        f.moff.push_back(f.off + j + h);
-        f.mlen.push_back(l);
+        f.step.push_back((uint32_t)(j - prev));
+        prev = j;
         j += h + l;
         continue;
       }
     }
+    const size_t tag_at = j;
     if (!varint(p, n, j, wire) || (wire >> 3) == 0) {
       f.scan_ok = false;
       return;
@@ -562,8 +646,12 @@ static void scan_batch(const uint8_t *stream, Frame &f) {
         f.scan_ok = false;
         return;
       }
-      f.moff.push_back(f.off + j);
-      f.mlen.push_back((uint32_t)l);
+      if (l > 0xffffffffull || tag_at - prev > 0xffffffffull) {
+        f.scan_ok = false;
+        return;
+      }
+      f.step.push_back((uint32_t)(tag_at - prev));
+      prev = tag_at;
       j += (size_t)l;
     } else if (field == 2 || field == 4) {
       if ((wire & 7) != 0 || !varint(p, n, j, v)) {
@@ -595,6 +683,7 @@ static int ing_grow(IngestBuf &b, size_t need) {
 }
 struct IngestState {
   IngestBuf stream, msgs, ents, sort, misc;
+  bool k64_ready = false;     // c_crc_k64 uploaded
   uint8_t *pinned = nullptr;  // drb_ingest_buffer (hipHostMalloc)
   size_t pinned_cap = 0;
   // the frames of the last call; their Requests vectors keep their
@@ -717,8 +806,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     f.pcrc = (uint32_t)wirehost::be(h + 14, 4);
     f.scan_ok = true;
     f.did = f.bv = 0;
-    f.moff.clear();
-    f.mlen.clear();
+    f.step.clear();
     i += 20 + (size_t)size;
   }
   fr.resize(nfr);
@@ -756,7 +844,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(up_err);
   }
   uint64_t nm = 0;
-  for (const auto &f : fr) nm += f.moff.size();
+  for (const auto &f : fr) nm += f.step.size();
   tr.mark("up+scan");
   // 3. the stream up, the payload CRCs in 16 KB chunks
   constexpr uint64_t CH = 16384;
@@ -776,10 +864,13 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // errors, entry bases, deliver flags, per-frame error, 2 counters
   const size_t m1 = nm ? nm : 1;
   const size_t nf = fr.size();
-  const size_t mb = al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) +
-                    al256(m1 * 4) * 6 + al256(m1) +
-                    al256((nf + 1) * 4) + al256((nf + 1) * 8) +
-                    al256(nf + 1) + ING_TALLY_ROWS * 64;
+  size_t scan_tb = 0;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, scan_tb, (uint64_t *)nullptr,
+                                          (uint64_t *)nullptr, (int)m1, sm));
+  const size_t mb = al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) * 3 +
+                    al256(m1 * 4) * 7 + al256(m1) +
+                    al256((nf + 1) * 4) + al256((nf + 1) * 8) * 2 +
+                    al256(nf + 1) + ING_TALLY_ROWS * 64 + al256(scan_tb);
   if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
   uint8_t *q = (uint8_t *)st.misc.p;
   auto take = [&](size_t b) {
@@ -800,6 +891,11 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint8_t *d_deliver = take(m1);
   uint32_t *d_fbad = (uint32_t *)take((nf + 1) * 4);
   uint64_t *d_mbase = (uint64_t *)take((nf + 1) * 8);
+  uint64_t *d_foff = (uint64_t *)take((nf + 1) * 8);
+  uint32_t *d_step = (uint32_t *)take(m1 * 4);
+  uint64_t *d_step64 = (uint64_t *)take(m1 * 8);
+  uint64_t *d_scan = (uint64_t *)take(m1 * 8);
+  void *d_scan_tmp = take(scan_tb);
   uint8_t *d_fstate = take(nf + 1);
   unsigned long long *d_ctr =
       (unsigned long long *)take(ING_TALLY_ROWS * 8 * 8);
@@ -812,32 +908,48 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
     e->crc_tab_ready = true;
   }
+  if (!st.k64_ready) {  // x^(8 * 64 * (255 - t)) mod P
+    uint32_t k64[256];
+    for (int t = 0; t < 256; ++t)
+      k64[t] = wirehost::crc32_combine(1u << 31, 0, 64ull * (255 - t));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_k64), k64, sizeof(k64)));
+    st.k64_ready = true;
+  }
   // each frame's Requests go up straight from its scan vectors
   std::vector<uint64_t> mbase(nf + 1, 0);
-  for (size_t f = 0; f < nf; ++f) mbase[f + 1] = mbase[f] + fr[f].moff.size();
+  for (size_t f = 0; f < nf; ++f) mbase[f + 1] = mbase[f] + fr[f].step.size();
   if (nc) {
     HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice, sm));
-    k_crc32<<<(unsigned)((nc + 255) / 256), 256, 0, sm>>>(ds, d_coff, d_clen,
-                                                          d_ccrc, nc);
+    k_crc_chunks<<<(unsigned)nc, 256, 0, sm>>>(ds, d_coff, d_clen, d_ccrc);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemsetAsync(d_fbad, 0, (fr.size() + 1) * 4, sm));
   HIPCHK(hipMemsetAsync(d_ctr, 0, ING_TALLY_ROWS * 8 * 8, sm));
   const uint32_t cmd_cap = v.C16 * 16;
   if (nm) {
+    std::vector<uint64_t> foff(nf + 1, 0);
     for (size_t f = 0; f < nf; ++f) {
-      const size_t k = fr[f].moff.size();
+      foff[f] = fr[f].off;
+      const size_t k = fr[f].step.size();
       if (!k) continue;
-      HIPCHK(hipMemcpyAsync(d_moff + mbase[f], fr[f].moff.data(), k * 8,
-                            hipMemcpyHostToDevice, sm));
-      HIPCHK(hipMemcpyAsync(d_mlen + mbase[f], fr[f].mlen.data(), k * 4,
+      HIPCHK(hipMemcpyAsync(d_step + mbase[f], fr[f].step.data(), k * 4,
                             hipMemcpyHostToDevice, sm));
     }
     HIPCHK(hipMemcpyAsync(d_mbase, mbase.data(), (nf + 1) * 8,
                           hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(d_foff, foff.data(), (nf + 1) * 8,
+                          hipMemcpyHostToDevice, sm));
     k_ing_frames<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
         d_mbase, (uint32_t)nf, d_mframe, nm);
+    // offsets and lengths from the elements' steps: a scan, then each
+    // element's tag and length varints read from the uploaded stream
+    k_widen_step<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(d_step,
+                                                                d_step64, nm);
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(d_scan_tmp, scan_tb, d_step64,
+                                            d_scan, (int)nm, sm));
+    k_ing_elems<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+        ds, d_scan, d_mbase, d_foff, d_mframe, d_moff, d_mlen, nm);
     k_ing_count<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
         ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad, nm, cmd_cap);
     HIPCHK(hipGetLastError());
@@ -858,11 +970,13 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   {
     size_t mi = 0;
     for (size_t f = 0; f < nf; ++f) {
+      // the chunks' register-only CRCs combined, then the ~0 conditioning:
+      // CRC(M) = f(M) ^ (~0 * x^(8|M|) mod P) ^ ~0
       uint32_t c = 0;
       for (uint32_t k = cfirst[f]; k < cfirst[f + 1]; ++k)
-        c = k == cfirst[f] ? ccrc[k] : wirehost::crc32_combine(c, ccrc[k],
-                                                               clen[k]);
-      const size_t nmf = fr[f].moff.size();
+        c = wirehost::crc32_combine(c, ccrc[k], clen[k]);
+      c ^= wirehost::crc32_combine(0xffffffffu, 0, fr[f].size) ^ 0xffffffffu;
+      const size_t nmf = fr[f].step.size();
       if (c != fr[f].pcrc || !fr[f].scan_ok || (fbad[f] & 1u)) {
         res.bad = 1;
         break;
