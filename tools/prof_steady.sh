@@ -1,6 +1,7 @@
 #!/bin/bash
-# HEAD profile at the KV steady state: bench JSON, the kernel trace and the
-# two HBM PMC passes over the timed rounds (last 20 launches of each kernel)
+# HEAD profile at the KV steady state: the bench JSON, the kernel trace and
+# the two HBM PMC passes over the timed rounds (last 20 launches of each
+# kernel).  usage: tools/prof_steady.sh <tag> [bench args]
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 o=gpurun_out/${1:-r03_head}; shift
