@@ -1367,6 +1367,8 @@ struct InPlane {  // one (group, from, to) plane of this call
   uint4 cur;      // header: tag | quiesce, info, sender term
   uint64_t maxapp;
   bool maxapp_valid;
+  bool remote;    // placement C4: the sender slot lives on another rank
+  uint64_t elo;   // remote: the first entry index of the entry rows
 };
 }  // namespace
 
@@ -1375,8 +1377,6 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                           uint64_t *accepted, uint64_t *dropped) {
   if (!e || (n && !msgs)) return DRB_EINVAL;
   const View &v = e->v;
-  // replicas spread over ranks exchange whole mailbox planes instead
-  if (v.remote_mask) return DRB_ENOSYS;
   std::lock_guard<std::mutex> lock(e->ingest_mu);
   const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
   const uint32_t tag = (uint32_t)e->round;
@@ -1385,12 +1385,14 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   std::vector<uint8_t> ok(n, 0);
   std::vector<uint64_t> fidx;
   fidx.reserve(2 * n);
+  std::vector<uint64_t> lane(n, 0);  // the receiver's lane (ing_target)
   for (size_t i = 0; i < n; ++i) {
     const drb_message &m = msgs[i];
-    const uint64_t g = m.shard_id - v.first_shard_id;
-    ok[i] = g < v.G && m.to >= 1 && m.to <= v.R && m.from >= 1 &&
-            m.from <= v.R && m.from != m.to && m.n_entries <= v.W;
+    uint64_t g = 0;
+    ok[i] = ing_target(v, m.shard_id, m.from, m.to, &g) &&
+            m.n_entries <= v.W;
     if (!ok[i]) continue;
+    lane[i] = g;
     fidx.push_back(u32_ix(v, W_FLAGS, (uint32_t)(m.to - 1), g));
     fidx.push_back(u32_ix(v, W_FLAGS, (uint32_t)(m.from - 1), g));
   }
@@ -1412,15 +1414,17 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     const uint32_t ft = fl[q++], ff = fl[q++];
     const bool live = (ft & DRB_F_HOSTED) &&
                       !(ft & (DRB_F_FALLBACK | DRB_F_ERROR));
-    const bool from_hosted = (ff & DRB_F_HOSTED) &&
+    const uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
+    // (a sender slot on another rank: this lane's is another group)
+    const bool from_hosted = !pair_remote(v, from, to) &&
+                             (ff & DRB_F_HOSTED) &&
                              !(ff & (DRB_F_FALLBACK | DRB_F_ERROR));
     if (!live || from_hosted) {  // the transport delivers remote senders only
       drop++;
       ok[i] = 0;
       continue;
     }
-    const uint64_t g = m.shard_id - v.first_shard_id;
-    const uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
+    const uint64_t g = lane[i];
     const uint64_t key = (g * v.R + from) * v.R + to;
     if (key == last_key) {  // a transport batch keeps a group's messages
       mplane[i] = last_plane;  // together
@@ -1429,34 +1433,53 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     auto it = pid.find(key);
     if (it == pid.end()) {
       it = pid.emplace(key, (uint32_t)planes.size()).first;
-      planes.push_back(InPlane{g, from, to, make_uint4(0, 0, 0, 0), 0, false});
+      planes.push_back(
+          InPlane{g, from, to, make_uint4(0, 0, 0, 0), 0, false, false, 0});
     }
     mplane[i] = it->second;
     last_key = key;
     last_plane = it->second;
   }
-  std::vector<uint64_t> hidx, xidx;
-  for (const InPlane &pl : planes) {
-    hidx.push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
-    xidx.push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
-  }
-  std::vector<uint4> hdr;
-  std::vector<uint64_t> mx;
-  if (gather(e, v.mbox_meta, hidx, hdr) || gather(e, v.mbox_maxapp, xidx, mx))
-    return DRB_EDEVICE;
+  // co-resident planes (local) and, with placement C4, planes whose sender
+  // slot lives on another rank (remote: the inbound copies, entries in the
+  // plane's entry rows)
+  std::vector<uint64_t> hidx[2], xidx[2], lidx;
+  std::vector<size_t> pidx[2];
   for (size_t p = 0; p < planes.size(); ++p) {
-    uint4 cur = hdr[p];
-    if (!tag_is(cur.x, tag)) {  // nothing there yet this round
-      cur = pack2(0, 0);
-      cur.x = tag & MQ_TAG;
-    }
-    planes[p].cur = cur;
-    planes[p].maxapp = mx[p];
-    planes[p].maxapp_valid = mi_nrep(cur.y) > 0;
+    const InPlane &pl = planes[p];
+    const int r = pair_remote(v, pl.from, pl.to) ? 1 : 0;
+    hidx[r].push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
+    xidx[r].push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
+    pidx[r].push_back(p);
+    if (r) lidx.push_back(mmeta_ix(v, buf, pl.from, pl.to, pl.g));
   }
+  std::vector<uint4> hdr[2];
+  std::vector<uint64_t> mx[2], lo;
+  if (gather(e, v.mbox_meta, hidx[0], hdr[0]) ||
+      gather(e, v.mbox_maxapp, xidx[0], mx[0]))
+    return DRB_EDEVICE;
+  if (!lidx.empty() &&
+      (gather(e, v.meta_in, hidx[1], hdr[1]) ||
+       gather(e, v.maxapp_in, xidx[1], mx[1]) || gather(e, v.elo_in, lidx, lo)))
+    return DRB_EDEVICE;
+  for (int r = 0; r < 2; ++r)
+    for (size_t q = 0; q < pidx[r].size(); ++q) {
+      InPlane &pl = planes[pidx[r][q]];
+      uint4 cur = hdr[r][q];
+      if (!tag_is(cur.x, tag)) {  // nothing there yet this round
+        cur = pack2(0, 0);
+        cur.x = tag & MQ_TAG;
+      }
+      pl.cur = cur;
+      pl.maxapp = mx[r][q];
+      pl.maxapp_valid = mi_nrep(cur.y) > 0;
+      pl.remote = r == 1;
+      pl.elo = r && pl.maxapp_valid ? lo[q] : 0;
+    }
   // 3. place every message in its plane, in order
-  std::vector<uint64_t> ridx, eidx, tridx, trval;
-  std::vector<uint4> rval, eval;
+  // [0] local arrays, [1] the inbound (remote) ones
+  std::vector<uint64_t> ridx[2], eidx[2], tridx[2], trval[2];
+  std::vector<uint4> rval[2], eval[2];
   std::vector<uint4> ch(ENT_META + v.C16);
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
@@ -1473,18 +1496,33 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       continue;
     }
     const bool rep = m.type == DRB_MSG_REPLICATE;
+    const int r = pl.remote ? 1 : 0;
     const uint32_t k = rep ? mi_nrep(cur.y)
                            : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (rep && pl.remote) {
+      // entry rows [elo, elo + E): a Replicate outside them is dropped (the
+      // sender retries, as after any transport loss)
+      if (!pl.maxapp_valid) pl.elo = m.log_index + 1;
+      if (m.n_entries && (m.log_index + 1 < pl.elo ||
+                          m.log_index + m.n_entries - pl.elo >= v.E)) {
+        drop++;
+        continue;
+      }
+    }
     if (rep && m.n_entries) {
-      // the entries travel in the sender's (unhosted) window slot
+      // the entries travel in the sender's (unhosted) window slot, or in the
+      // plane's entry rows when the plane is remote
       for (uint64_t x = 0; x < m.n_entries; ++x) {
         drb_entry en = ents[m.entries_off + x];
         if (en.cmd_len > v.C16 * 16) return DRB_ERANGE;
         en.index = m.log_index + 1 + x;
         entry_to_chunks(v, en, pool, ch.data());
         for (uint32_t c = 0; c < ENT_META + v.C16; ++c) {
-          eidx.push_back(ring_ix(v, pl.from, en.index, c, pl.g));
-          eval.push_back(ch[c]);
+          eidx[r].push_back(
+              pl.remote ? embox_ix(v, buf, pl.from, pl.to,
+                                   (uint32_t)(en.index - pl.elo), c, pl.g)
+                        : ring_ix(v, pl.from, en.index, c, pl.g));
+          eval[r].push_back(ch[c]);
         }
       }
     }
@@ -1517,15 +1555,15 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
         other = true;
         c0.x |= MF_TERM_OTHER;
         if (v.rterm) {  // elections: the raft launch reads it
-          tridx.push_back(rterm_ix(v, buf, pl.from, pl.to, k, pl.g));
-          trval.push_back(m.term);
+          tridx[r].push_back(rterm_ix(v, buf, pl.from, pl.to, k, pl.g));
+          trval[r].push_back(m.term);
         }
       }
     }
-    ridx.push_back(mbox_ix(v, buf, pl.from, pl.to, k, 0, pl.g));
-    rval.push_back(c0);
-    ridx.push_back(mbox_ix(v, buf, pl.from, pl.to, k, 1, pl.g));
-    rval.push_back(c1);
+    ridx[r].push_back(mbox_ix(v, buf, pl.from, pl.to, k, 0, pl.g));
+    rval[r].push_back(c0);
+    ridx[r].push_back(mbox_ix(v, buf, pl.from, pl.to, k, 1, pl.g));
+    rval[r].push_back(c1);
     const uint32_t inf =
         msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0);
     cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
@@ -1537,17 +1575,20 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     acc++;
   }
   // 4. down: entries, records, headers, max-append, the round tag bytes
-  std::vector<uint4> hval;
-  std::vector<uint64_t> xval, tidx;
-  for (const InPlane &pl : planes) {
-    hval.push_back(pl.cur);
-    xval.push_back(pl.maxapp);
-  }
+  std::vector<uint4> hval[2];
+  std::vector<uint64_t> xval[2], tidx, lval;
+  for (int r = 0; r < 2; ++r)
+    for (size_t p : pidx[r]) {
+      hval[r].push_back(planes[p].cur);
+      xval[r].push_back(planes[p].maxapp);
+      if (r) lval.push_back(planes[p].elo);
+    }
   // tag bytes: one u64 word per (receiver, group), a byte per sender
   std::unordered_map<uint64_t, uint32_t> tw;
   std::vector<uint64_t> tmask;  // sender bytes to set per word
   std::vector<uint64_t> tbyte;  // their values (tag_byte, drb_msg.hpp)
   for (const InPlane &pl : planes) {
+    if (pl.remote) continue;  // (remote planes: the header's tag alone)
     if (!(mi_count(pl.cur.y) || (pl.cur.x & MQ_QUIESCE))) continue;
     const uint64_t w = ((uint64_t)buf * v.R + pl.to) * v.G + pl.g;
     auto it = tw.find(w);
@@ -1561,10 +1602,20 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     tbyte[it->second] |= (uint64_t)tag_byte(tag, pl.cur.y) << (8 * pl.from);
   }
   std::vector<uint64_t> tv;
-  if ((v.rterm && scatter(e, v.rterm, tridx, trval)) ||
-      scatter(e, v.ring, eidx, eval) || scatter(e, v.mbox, ridx, rval) ||
-      scatter(e, v.mbox_meta, hidx, hval) ||
-      scatter(e, v.mbox_maxapp, xidx, xval) || gather(e, v.inbox_tag, tidx, tv))
+  if ((v.rterm && scatter(e, v.rterm, tridx[0], trval[0])) ||
+      scatter(e, v.ring, eidx[0], eval[0]) ||
+      scatter(e, v.mbox, ridx[0], rval[0]) ||
+      scatter(e, v.mbox_meta, hidx[0], hval[0]) ||
+      scatter(e, v.mbox_maxapp, xidx[0], xval[0]) ||
+      gather(e, v.inbox_tag, tidx, tv))
+    return DRB_EDEVICE;
+  if (!pidx[1].empty() &&
+      ((v.rterm_in && scatter(e, v.rterm_in, tridx[1], trval[1])) ||
+       scatter(e, v.embox_in, eidx[1], eval[1]) ||
+       scatter(e, v.mbox_in, ridx[1], rval[1]) ||
+       scatter(e, v.meta_in, hidx[1], hval[1]) ||
+       scatter(e, v.maxapp_in, xidx[1], xval[1]) ||
+       scatter(e, v.elo_in, lidx, lval)))
     return DRB_EDEVICE;
   for (size_t w = 0; w < tidx.size(); ++w)
     tv[w] = (tv[w] & ~tmask[w]) | (tmask[w] & tbyte[w]);

@@ -394,9 +394,8 @@ __global__ void k_ing_keys(const View v, const DecMsg *dm, uint32_t *key,
   const DecMsg m = dm[i];
   uint32_t k = ~0u;
   if (m.err == ING_OK) {
-    const uint64_t g = m.shard - v.first_shard_id;
-    const bool ok = g < v.G && m.to >= 1 && m.to <= v.R && m.from >= 1 &&
-                    m.from <= v.R && m.from != m.to && m.n_ent <= v.W;
+    uint64_t g;
+    bool ok = ing_target(v, m.shard, m.from, m.to, &g) && m.n_ent <= v.W;
     if (ok)
       k = (uint32_t)((g * v.R + (m.from - 1)) * v.R + (m.to - 1));
     else
@@ -420,21 +419,33 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
   const uint64_t g = (uint64_t)(k / v.R) / v.R;
   uint64_t i1 = i0 + 1;
   while (i1 < n && key[i1] == k) ++i1;
+  // placement C4: a plane whose sender slot lives on another rank is read
+  // from the inbound copies (mbox_in, ...), entries from its entry rows
+  const bool rm = pair_remote(v, from, to);
+  uint4 *const mbox = rm ? v.mbox_in : v.mbox;
+  uint4 *const mmeta = rm ? v.meta_in : v.mbox_meta;
+  uint64_t *const mmax = rm ? v.maxapp_in : v.mbox_maxapp;
+  uint64_t *const rterm = rm ? v.rterm_in : v.rterm;
   const uint32_t ft = v.u32[u32_ix(v, W_FLAGS, to, g)];
-  const uint32_t ff = v.u32[u32_ix(v, W_FLAGS, from, g)];
   const bool live = (ft & DRB_F_HOSTED) && !(ft & (DRB_F_FALLBACK | DRB_F_ERROR));
+  // (co-resident senders step here; another rank's lane holds another group)
+  const uint32_t ff = rm ? 0u : v.u32[u32_ix(v, W_FLAGS, from, g)];
   const bool from_hosted =
       (ff & DRB_F_HOSTED) && !(ff & (DRB_F_FALLBACK | DRB_F_ERROR));
   if (!live || from_hosted) {  // the transport delivers remote senders only
     atomicAdd(&ctr[1], (unsigned long long)(i1 - i0));
     return;
   }
-  uint4 cur = v.mbox_meta[mmeta_ix(v, buf, from, to, g)];
-  uint64_t maxapp = v.mbox_maxapp[mmeta_ix(v, buf, from, to, g)];
+  uint4 cur = mmeta[mmeta_ix(v, buf, from, to, g)];
+  uint64_t maxapp = mmax[mmeta_ix(v, buf, from, to, g)];
   if (!tag_is(cur.x, tag)) {  // nothing there yet this round
     cur = make_uint4(tag & MQ_TAG, 0, 0, 0);
   }
   bool maxapp_valid = mi_nrep(cur.y) > 0;
+  // remote planes: the first entry index of the plane's entry rows (set by
+  // the round's first Replicate placed here)
+  uint64_t elo = maxapp_valid && rm ? v.elo_in[mmeta_ix(v, buf, from, to, g)]
+                                    : 0;
   uint64_t acc = 0, drop = 0;
   for (uint64_t j = i0; j < i1; ++j) {
     const DecMsg m = dm[idx[j]];
@@ -450,28 +461,48 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
     const bool rep = m.type == DRB_MSG_REPLICATE;
     const uint32_t kk =
         rep ? mi_nrep(cur.y) : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (rep && rm) {
+      // entry rows [elo, elo + E): a Replicate outside them is dropped (the
+      // sender retries, as after any transport loss)
+      if (!maxapp_valid) elo = m.log_index + 1;
+      if (m.n_ent && (m.log_index + 1 < elo ||
+                      m.log_index + m.n_ent - elo >= v.E)) {
+        drop++;
+        continue;
+      }
+    }
     if (rep && m.n_ent) {
-      // the entries travel in the sender's (unhosted) window slot
+      // the entries travel in the sender's (unhosted) window slot, or in the
+      // plane's entry rows when the plane is remote
       for (uint32_t x = 0; x < m.n_ent; ++x) {
         const drb_entry en = ents[m.ent0 + x];
         const uint64_t index = m.log_index + 1 + x;
-        uint4 *row = v.ring;
-        row[ring_ix(v, from, index, 0, g)] =
-            make_uint4((uint32_t)en.term, (uint32_t)(en.term >> 32),
-                       (uint32_t)en.key, (uint32_t)(en.key >> 32));
-        row[ring_ix(v, from, index, 1, g)] = make_uint4(
+        uint4 ch[ENT_META];
+        ch[0] = make_uint4((uint32_t)en.term, (uint32_t)(en.term >> 32),
+                           (uint32_t)en.key, (uint32_t)(en.key >> 32));
+        ch[1] = make_uint4(
             (uint32_t)en.client_id, (uint32_t)(en.client_id >> 32),
             (uint32_t)en.series_id, (uint32_t)(en.series_id >> 32));
-        row[ring_ix(v, from, index, 2, g)] =
-            make_uint4((uint32_t)en.responded_to,
-                       (uint32_t)(en.responded_to >> 32), en.type,
-                       en.cmd_len);
-        for (uint32_t c = 0; c < v.C16; ++c) {
-          uint32_t w[4] = {0, 0, 0, 0};
-          for (uint32_t b = 0; b < 16 && c * 16 + b < en.cmd_len; ++b)
-            w[b >> 2] |= (uint32_t)s[en.cmd_off + c * 16 + b] << (8 * (b & 3));
-          row[ring_ix(v, from, index, ENT_META + c, g)] =
-              make_uint4(w[0], w[1], w[2], w[3]);
+        ch[2] = make_uint4((uint32_t)en.responded_to,
+                           (uint32_t)(en.responded_to >> 32), en.type,
+                           en.cmd_len);
+        for (uint32_t c = 0; c < ENT_META + v.C16; ++c) {
+          uint4 q;
+          if (c < ENT_META) {
+            q = ch[c];
+          } else {
+            const uint32_t cc = c - ENT_META;
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint32_t b = 0; b < 16 && cc * 16 + b < en.cmd_len; ++b)
+              w[b >> 2] |= (uint32_t)s[en.cmd_off + cc * 16 + b]
+                           << (8 * (b & 3));
+            q = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+          if (rm)
+            v.embox_in[embox_ix(v, buf, from, to, (uint32_t)(index - elo), c,
+                                g)] = q;
+          else
+            v.ring[ring_ix(v, from, index, c, g)] = q;
         }
       }
     }
@@ -502,11 +533,11 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
       } else if (pv || q_hi(cur) != m.term) {
         other = true;
         c0.x |= MF_TERM_OTHER;
-        if (v.rterm) v.rterm[rterm_ix(v, buf, from, to, kk, g)] = m.term;
+        if (rterm) rterm[rterm_ix(v, buf, from, to, kk, g)] = m.term;
       }
     }
-    v.mbox[mbox_ix(v, buf, from, to, kk, 0, g)] = c0;
-    v.mbox[mbox_ix(v, buf, from, to, kk, 1, g)] = c1;
+    mbox[mbox_ix(v, buf, from, to, kk, 0, g)] = c0;
+    mbox[mbox_ix(v, buf, from, to, kk, 1, g)] = c1;
     const uint32_t inf =
         msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0u);
     cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
@@ -517,9 +548,10 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
     }
     acc++;
   }
-  v.mbox_meta[mmeta_ix(v, buf, from, to, g)] = cur;
-  v.mbox_maxapp[mmeta_ix(v, buf, from, to, g)] = maxapp;
-  if (mi_count(cur.y) || (cur.x & MQ_QUIESCE))  // this sender's tag byte
+  mmeta[mmeta_ix(v, buf, from, to, g)] = cur;
+  mmax[mmeta_ix(v, buf, from, to, g)] = maxapp;
+  if (rm && maxapp_valid) v.elo_in[mmeta_ix(v, buf, from, to, g)] = elo;
+  if (!rm && (mi_count(cur.y) || (cur.x & MQ_QUIESCE)))  // its tag byte
     ((uint8_t *)&v.inbox_tag[((uint64_t)buf * v.R + to) * v.G + g])[from] =
         tag_byte(tag, cur.y);
   // (a lane per plane: the adds spread over the counter rows)
@@ -766,8 +798,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                drb_wire_in *out) {
   using namespace drb;
   if (!e || (!stream && len)) return DRB_EINVAL;
-  // replicas spread over ranks: planes move by drb_exchange_* (drb_ingest)
-  if (e->v.remote_mask) return DRB_ENOSYS;
   wirehost::crc_init();
   std::lock_guard<std::mutex> lock(e->ingest_mu);
   if (!e->ingest) e->ingest = new IngestState();

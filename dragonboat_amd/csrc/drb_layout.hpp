@@ -475,6 +475,28 @@ __host__ __device__ inline uint64_t gid(const View &v, uint32_t s,
   const uint32_t N = v.place_world;
   return (uint64_t)N * g + (v.place_rank + N - (s % N)) % N;
 }
+// The lane of a message's receiver on this engine (drb_ingest's shape
+// checks): co-resident, the group; with replicas spread over ranks
+// (drb_config.place_world), replica slot s of global group g lives on rank
+// (g + s) mod N at lane g / N -- a message for another rank's replica is
+// not this NodeHost's (ErrShardNotFound, nodehost.go:2072-2122).
+__host__ __device__ inline bool ing_target(const View &v, uint64_t shard,
+                                           uint64_t from, uint64_t to,
+                                           uint64_t *lane) {
+  const uint64_t gid = shard - v.first_shard_id;
+  if (!(to >= 1 && to <= v.R && from >= 1 && from <= v.R && from != to))
+    return false;
+  uint64_t g = gid;
+  if (v.place_world > 1) {
+    if (gid >= v.total_groups ||
+        (gid + (to - 1)) % v.place_world != v.place_rank)
+      return false;
+    g = gid / v.place_world;
+  }
+  *lane = g;
+  return g < v.G;
+}
+
 __host__ __device__ inline uint64_t mmeta_ix(const View &v, uint32_t buf,
                                              uint32_t from, uint32_t to,
                                              uint64_t g) {

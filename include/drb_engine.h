@@ -562,7 +562,14 @@ int drb_request_leader_transfer(drb_engine *e, uint32_t slot,
  * (internal/transport/transport.go:86-91, nodehost.go:2072-2122).  Places
  * messages from replicas NOT hosted by this engine into the inbox of the
  * next round.  Messages for unknown shards / unhosted targets, or beyond
- * the mailbox capacity, are dropped (nodehost.go:2112-2114). */
+ * the mailbox capacity, are dropped (nodehost.go:2112-2114).  With
+ * placement (place_world > 1) shard_id names the global group: a message
+ * reaches the rank that hosts its receiver ((group + slot) mod N, lane
+ * group / N), others are dropped; a sender slot that belongs to another
+ * rank is written into the inbound planes, its Replicates' entries into the
+ * plane's entry_mbox rows (a Replicate beyond them is dropped: the sender
+ * retries).  Call it after the round's plane exchange.  The same holds for
+ * drb_ingest_wire. */
 int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                const drb_entry *ents, const uint8_t *pool, uint64_t *accepted,
                uint64_t *dropped);

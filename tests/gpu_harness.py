@@ -367,10 +367,10 @@ class DistPair:
             tot[f] = sum(getattr(x, f) for x in outs)
         return o, tot
 
-    def check(self, groups=None, logs=True, kv=True, msgs=True):
+    def check(self, groups=None, logs=True, kv=True, msgs=True, slots=None):
         errs = []
         for g in (range(self.G) if groups is None else groups):
-            for s in range(self.R):
+            for s in (range(self.R) if slots is None else slots):
                 r, j = self.where(g, s)
                 e = self.engs[r]
                 a, b = e.export_replicas(j, 1)[s], self.orc.export(g, s)
