@@ -77,6 +77,9 @@ namespace drb {
 #ifndef DRB_FPF
 #define DRB_FPF 8
 #endif
+#ifndef DRB_QS_DIRTY
+#define DRB_QS_DIRTY 1
+#endif
 #ifndef DRB_REM_DIRTY
 #define DRB_REM_DIRTY 1
 #endif
@@ -147,6 +150,7 @@ struct Rep {
   bool err;
   // node.qs (Quiesce on, EXT instantiation): quiesce.go:23-33
   uint64_t qs_tick, qs_idle, qs_since, qs_exit;
+  uint32_t qs_dirty;  // idle 1, since 2, exit 4: stored at the round's end
   bool qs_new;  // newQuiesceStateFlag: send Quiesce to the peers
 };
 
@@ -245,12 +249,14 @@ template <int R>
 DRB_DEV void qs_enter(Rep<R> &r) {  // enterQuiesce (quiesce.go:104-109)
   r.qs_since = r.qs_tick;
   r.qs_idle = r.qs_tick;
+  r.qs_dirty |= 3u;
   r.qs_new = true;
 }
 template <int R>
 DRB_DEV void qs_exit(Rep<R> &r) {  // exitQuiesce (quiesce.go:111-114)
   r.qs_since = 0;
   r.qs_exit = r.qs_tick;
+  r.qs_dirty |= 6u;
 }
 // record (quiesce.go:56-74); heartbeats carrying a ReadIndex ctx count as
 // ReadIndex (node.recordMessage, node.go:1339-1345)
@@ -261,6 +267,7 @@ DRB_DEV void qs_record(const View &v, Rep<R> &r, uint32_t type) {
     if (r.qs_tick - r.qs_since < 2ull * v.election_rtt) return;  // newToQuiesce
   }
   r.qs_idle = r.qs_tick;
+  r.qs_dirty |= 1u;
   if (qs_quiesced(r)) qs_exit(r);
 }
 // tryEnterQuiesce (quiesce.go:91-102): a Quiesce message
@@ -2311,6 +2318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       r.qs_idle = over_ld(L, F_QS_IDLE);
       r.qs_since = over_ld(L, F_QS_SINCE);
       r.qs_exit = over_ld(L, F_QS_EXIT);
+      r.qs_dirty = 0;
       // the quiesced ticks this replica skipped (only ever while quiesced)
       qs_owed = p.tick_no - p.tick - over_ld(L, F_QS_BASE);
       r.election_tick += qs_owed;
@@ -2974,10 +2982,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       if (qon) {
         r.flags = qs_quiesced(r) ? (r.flags | F_QUIESCED)
                                  : (r.flags & ~F_QUIESCED);
+        // (a heartbeat round moves only the tick and the base)
         over_st(L, F_QS_TICK, r.qs_tick);
-        over_st(L, F_QS_IDLE, r.qs_idle);
-        over_st(L, F_QS_SINCE, r.qs_since);
-        over_st(L, F_QS_EXIT, r.qs_exit);
+        const uint32_t qd = DRB_QS_DIRTY ? r.qs_dirty : 7u;
+        if (qd & 1u) over_st(L, F_QS_IDLE, r.qs_idle);
+        if (qd & 2u) over_st(L, F_QS_SINCE, r.qs_since);
+        if (qd & 4u) over_st(L, F_QS_EXIT, r.qs_exit);
         over_st(L, F_QS_BASE, p.tick_no);
       }
       store_rep<R, LEAD>(L, r, flags0, fb0);
