@@ -757,7 +757,8 @@ def main():
                                        "gloo with host staging (one-GPU "
                                        "boxes); this line is its first "
                                        "RCCL run"}
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
+            # (rank 0 at N = 1 only: the scaling runs keep their ranks' time)
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(res))
     if world > 1:
