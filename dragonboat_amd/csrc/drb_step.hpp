@@ -77,6 +77,11 @@ namespace drb {
 #ifndef DRB_FPF
 #define DRB_FPF 8
 #endif
+// the leader's: the first DRB_LPF records of each of its first two senders
+// with records (LDS: 2 x DRB_LPF x 4 KB a workgroup; 0: off)
+#ifndef DRB_LPF
+#define DRB_LPF 0
+#endif
 #ifndef DRB_QS_DIRTY
 #define DRB_QS_DIRTY 1
 #endif
@@ -2225,10 +2230,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                               : li;
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
-  __shared__ uint32_t crc_tab[256];
+  __shared__ uint32_t crc_tab[EXT ? 256 : 1];
   __shared__ uint64_t rq_lds[LEAD ? 2 * DRB_RI_DEPTH : 1][256];
-  constexpr bool FPF = !LEAD && !SLOW && DRB_FPF > 0;
-  __shared__ uint4 pf_lds[FPF ? DRB_FPF : 1][256];
+  // inbox prefetch (LDS-DMA): PFS senders x PFN records
+  constexpr int PFN = SLOW ? 0 : LEAD ? DRB_LPF : DRB_FPF;
+  constexpr bool FPF = PFN > 0;
+  constexpr int PFS = LEAD ? 2 : 1;
+  __shared__ uint4 pf_lds[FPF ? PFS : 1][FPF ? PFN : 1][FPF ? 256 : 1];
   // placement C4 only: [R][256] (the launch sizes it, drb_step_inst.hip)
   extern __shared__ uint64_t elo_dyn[];
   uint64_t(*elo_lds)[256] = reinterpret_cast<uint64_t(*)[256]>(elo_dyn);
@@ -2347,8 +2355,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     uint32_t qz_from = 0;   // senders whose Quiesce message arrived
     uint64_t nri_packed = 0;  // 5-bit ReadIndex record count per sender
     uint64_t max_app = 0;
-    int pf_s = -1;         // follower: the sender whose records are in pf_lds
-    uint32_t pf_nrp = 0;   // ... and its Replicate count
+    int pf_s[2] = {-1, -1};    // the senders whose records are in pf_lds
+    uint32_t pf_nrp[2] = {0, 0};  // ... and their Replicate counts
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot) continue;
@@ -2427,23 +2435,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       if (!is_leader && mi_nrep(info))
         max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
                                       v, L.rbuf, s, slot, g)]);
-      if (FPF && ns && pf_s < 0) {
+      if (FPF && ns && (pf_s[0] < 0 || (PFS > 1 && pf_s[1] < 0))) {
         // the records go to LDS in one batch; the dispatch loop reads them
         // there (after the wait below)
-        pf_s = s;
-        pf_nrp = mi_nrep(info);
+        const int q = pf_s[0] < 0 ? 0 : 1;
+        pf_s[q] = s;
+        pf_nrp[q] = mi_nrep(info);
         const uint4 *mb = rm ? v.mbox_in : v.mbox;
 #pragma unroll
-        for (int j = 0; j < (FPF ? DRB_FPF : 1); ++j)
+        for (int j = 0; j < (FPF ? PFN : 1); ++j)
           if ((uint32_t)j < ns) {
-            const uint32_t jj = (uint32_t)j;
-            const uint32_t k =
-                rec_pos(jj < pf_nrp, jj < pf_nrp ? jj : jj - pf_nrp, v.MB);
+            const uint32_t jj = (uint32_t)j, nr = pf_nrp[q];
+            const uint32_t k = rec_pos(jj < nr, jj < nr ? jj : jj - nr, v.MB);
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(
                     mb + mbox_ix(v, L.rbuf, s, slot, k, 0, g)),
-                (__attribute__((address_space(3))) void *)&pf_lds[j][
-                    threadIdx.x & ~63u],
+                (__attribute__((address_space(3))) void *)&pf_lds[FPF ? q : 0][
+                    FPF ? j : 0][FPF ? threadIdx.x & ~63u : 0],
                 16, 0, 0);
           }
       }
@@ -2689,7 +2697,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           follower_read_index(L, r, in_lo, in_hi);
       }
       // handleReceivedMessages: Replicates by sender, then the rest
-      if (FPF && pf_s >= 0)
+      if (FPF && pf_s[0] >= 0)
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): pf_lds landed
 #pragma unroll 1
       for (int pass = 0; pass < 2; ++pass) {
@@ -2717,9 +2725,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           // spills more, profiles/r02_kvline/README.md)
           for (uint32_t j = 0; j < cnt; ++j) {
             const uint32_t k = rec_pos(pass == 0, j, v.MB);
-            const uint32_t ord = pass == 0 ? j : pf_nrp + j;
-            const uint4 c0 = (FPF && s == pf_s && ord < (uint32_t)DRB_FPF)
-                                 ? pf_lds[FPF ? ord : 0][threadIdx.x]
+            const int q = s == pf_s[0] ? 0 : (PFS > 1 && s == pf_s[1]) ? 1 : -1;
+            const uint32_t ord = pass == 0 ? j : pf_nrp[q > 0 ? 1 : 0] + j;
+            const uint4 c0 = (FPF && q >= 0 && ord < (uint32_t)PFN)
+                                 ? pf_lds[FPF ? q : 0][FPF ? ord : 0]
+                                         [FPF ? threadIdx.x : 0]
                                  : mb[mbox_ix(v, L.rbuf, s, slot, k, 0, g)];
             uint4 c1 = make_uint4(0, 0, 0, 0);
             if (c0.x & MF_HAS_C1) c1 = mb[mbox_ix(v, L.rbuf, s, slot, k, 1, g)];
