@@ -153,12 +153,14 @@ def parse():
 C5_VAL = {128: 116, 1024: 1011}
 # C5 KV: writes uniform over the K = 256 keys of SURVEY 8d, as C3.  A
 # replica's table holds C5_SLOTS keys -- a group proposes Poisson(1 % x
-# rounds) times in a run, ~0.7 in the default one, so no table fills (a full
-# one would stop that replica's apply: DRB_F_APPLY_STOPPED, counted in the
-# JSON) -- and the values live in one shared block pool sized for the keys
-# the run can write (put_value_long: a block per distinct key, bump-allocated)
+# rounds) times in a run, ~0.7 in the default one -- and a full table grows
+# into overflow buckets (drb_config.kv_overflow_buckets, C5_OVF_PER buckets
+# per replica on average, the K = 256 keys of a long run); the values live
+# in one shared block pool sized for the keys the run can write
+# (put_value_long: a block per distinct key, bump-allocated)
 C5_KEYS = KEY_SPACE
 C5_SLOTS = 32
+C5_OVF_PER = 1 / 64
 
 
 def c5_pool_blocks(G, R, rounds, active_ppm):
@@ -309,6 +311,7 @@ def main():
                      mailbox=8, kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
                      kv_pool_blocks=c5_pool_blocks(G, R, c5_rounds * k,
                                                    args.active_ppm),
+                     kv_overflow_buckets=int(G * R * C5_OVF_PER) + 1024,
                      save_cap=(4 * bound + 15) // 16 * 16 +
                      (128 if args.save in ("tan", "tanmux") else 0),
                      save_tan=int(args.save in ("tan", "tanmux")),

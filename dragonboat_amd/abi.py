@@ -134,7 +134,8 @@ class Config(C.Structure):
                 ("save_batched", C.c_uint32), ("save_tan", C.c_uint32),
                 ("elections", C.c_uint32), ("tan_max_log", C.c_uint64),
                 ("tan_multiplexed", C.c_uint32), ("pre_vote", C.c_uint32),
-                ("max_reads_per_ctx", C.c_uint32)]
+                ("max_reads_per_ctx", C.c_uint32),
+                ("kv_overflow_buckets", C.c_uint64)]
 
 
 class ReadResult(C.Structure):

@@ -267,12 +267,15 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
                    : 1 + (cfg->kv_val_cap > 4 ? (cfg->kv_val_cap - 4 + 15) / 16
                                               : 0);
   v.VB = v.kv_ool ? (cfg->kv_val_cap + 15) / 16 : 0;
-  // default: a block for every slot (the pool never runs out before the
-  // table does); large configurations size it to their key count
+  // default: a block for every slot, overflow slots included (the pool
+  // never runs out before the table does); large configurations size it
+  // to their key count
   v.kv_pool_blocks =
-      v.kv_ool ? (cfg->kv_pool_blocks ? cfg->kv_pool_blocks
-                                      : std::min<uint64_t>(G * R * v.KS,
-                                                           0xffffffffull))
+      v.kv_ool ? (cfg->kv_pool_blocks
+                      ? cfg->kv_pool_blocks
+                      : std::min<uint64_t>(G * R * v.KS +
+                                               4 * cfg->kv_overflow_buckets,
+                                           0xffffffffull))
                : 0;
   v.max_props = cfg->max_props;
   v.election_rtt = cfg->election_rtt;
@@ -315,6 +318,17 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   if (v.kv_ool) {
     rc |= dalloc(e, &v.kv_pool, v.kv_pool_blocks * v.VB);
     rc |= dalloc(e, &v.kv_pool_next, 1);
+  }
+  v.kv_ovf_cap = cfg->kv_overflow_buckets;
+  if (v.kv_ovf_cap) {
+    if (v.kv_ovf_cap >= 0xffffffffull) {
+      delete e;
+      return DRB_ERANGE;
+    }
+    rc |= dalloc(e, &v.kv_ovf, v.kv_ovf_cap * 4 * v.KVW);
+    rc |= dalloc(e, &v.kv_ovf_next, v.kv_ovf_cap);
+    rc |= dalloc(e, &v.kv_ovf_head, R * G);
+    rc |= dalloc(e, &v.kv_ovf_used, 1);
   }
   rc |= dalloc(e, &v.props,
                (uint64_t)cfg->prop_slots * v.max_props * (PROP_META + v.C16) *
@@ -1798,7 +1812,8 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   if (split) pl.n_reads = 0;
   // the EXT instantiation only where its paths can run (drb_step.hpp)
   const bool ext =
-      e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves || e->v.quiesce;
+      e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves || e->v.quiesce ||
+      e->v.kv_ovf_cap;
   pl.nrows = nl;
   pf.nrows = nf;
   // one-dimensional grids, rows interleaved per XCD (block_pos)
@@ -2546,6 +2561,33 @@ static int read_kv_table(drb_engine *e, uint64_t group, uint32_t slot,
   return DRB_OK;
 }
 
+// the replica's overflow chain (drb_config.kv_overflow_buckets), its
+// buckets' slots in chain order (4 x KVW chunks a bucket)
+static int read_ovf_chain(drb_engine *e, uint64_t group, uint32_t slot,
+                          std::vector<uint4> &out) {
+  const View &v = e->v;
+  out.clear();
+  if (!v.kv_ovf_head) return DRB_OK;
+  uint32_t b = 0;
+  HIPCHK(hipMemcpyAsync(&b, v.kv_ovf_head + ix(v, slot, group), 4,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  std::vector<uint4> bk(4 * v.KVW);
+  for (uint64_t guard = 0; b && guard <= v.kv_ovf_cap; ++guard) {
+    if (b - 1 >= v.kv_ovf_cap) return DRB_EDEVICE;
+    uint32_t next = 0;
+    HIPCHK(hipMemcpyAsync(bk.data(), v.kv_ovf + (uint64_t)(b - 1) * 4 * v.KVW,
+                          bk.size() * sizeof(uint4), hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipMemcpyAsync(&next, v.kv_ovf_next + (b - 1), 4,
+                          hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    out.insert(out.end(), bk.begin(), bk.end());
+    b = next;
+  }
+  return DRB_OK;
+}
+
 static int slot_value(drb_engine *e, const uint4 *sl, uint8_t *val,
                       uint32_t vlen) {
   const View &v = e->v;
@@ -2591,6 +2633,19 @@ extern "C" int drb_kv_lookup(drb_engine *e, uint64_t group, uint32_t slot,
       return slot_value(e, sl, val, vlen);
     }
   }
+  // a full table: the overflow chain
+  std::vector<uint4> ch;
+  if (read_ovf_chain(e, group, slot, ch)) return DRB_EDEVICE;
+  for (size_t q = 0; q + v.KVW <= ch.size(); q += v.KVW) {
+    const uint4 *sl = &ch[q];
+    if (!((sl[0].z >> 31) & 1u)) continue;
+    uint32_t klen = sl[0].z & 0xffu, vlen = (sl[0].z >> 8) & 0xfffu;
+    if (klen == key_len && lo64h(sl[0]) == k8) {
+      if (val_len) *val_len = vlen;
+      if (vlen > val_cap) return DRB_ERANGE;
+      return slot_value(e, sl, val, vlen);
+    }
+  }
   return 1;
 }
 
@@ -2602,15 +2657,36 @@ extern "C" int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
     return DRB_ERANGE;
   if (n && (!keys || !key_lens || !vals || !val_lens)) return DRB_EINVAL;
   const View &v = e->v;
-  if (n > v.KS) return DRB_ERANGE;
+  if (n > v.KS && !v.kv_ovf_head) return DRB_ERANGE;
   std::vector<uint4> tbl((uint64_t)v.KS * v.KVW, make_uint4(0, 0, 0, 0));
-  std::vector<std::pair<uint32_t, size_t>> ool;  // (slot index, pair)
+  std::vector<size_t> spill;  // the pairs a full table sends to the chain
   const uint32_t mask = v.KS - 1;
+  // one pair into its slot (the device's slot format, drb_step.hpp
+  // apply_entry); an out-of-line value's block index is filled in below
+  auto fill = [&](uint4 *sl, size_t i, uint64_t k8) {
+    const uint32_t kl = key_lens[i], vl = val_lens[i];
+    const uint8_t *val = vals + i * val_stride;
+    uint32_t w0 = 0;
+    for (uint32_t b = 0; b < 4 && b < vl; ++b) w0 |= (uint32_t)val[b] << (8 * b);
+    sl[0] = make_uint4((uint32_t)k8, (uint32_t)(k8 >> 32),
+                       (1u << 31) | (vl << 8) | kl, w0);
+    if (!v.kv_ool) {
+      uint8_t tmp[16 * 9] = {0};
+      if (vl > 4) memcpy(tmp, val + 4, vl - 4);
+      for (uint32_t c = 1; c < v.KVW; ++c) memcpy(&sl[c], tmp + 16 * (c - 1), 16);
+    }
+  };
+  auto key8 = [&](size_t i) {
+    uint64_t k8 = 0;
+    for (uint32_t b = 0; b < key_lens[i]; ++b)
+      k8 |= (uint64_t)keys[i * 8 + b] << (8 * b);
+    return k8;
+  };
+  std::vector<std::pair<uint4 *, size_t>> ool;  // (slot, pair)
   for (size_t i = 0; i < n; ++i) {
     const uint32_t kl = key_lens[i], vl = val_lens[i];
     if (kl > 8 || vl > v.kv_val_cap) return DRB_ERANGE;
-    uint64_t k8 = 0;
-    for (uint32_t b = 0; b < kl; ++b) k8 |= (uint64_t)keys[i * 8 + b] << (8 * b);
+    const uint64_t k8 = key8(i);
     // the device's slot hash (drb_step.hpp kv_hash)
     uint64_t h = 0xcbf29ce484222325ull;
     for (uint32_t b = 0; b < kl; ++b)
@@ -2622,20 +2698,30 @@ extern "C" int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
       ++p;
       ks = kv_probe(v, home, p);
     }
-    if (p == v.KS) return DRB_ERANGE;
-    const uint8_t *val = vals + i * val_stride;
-    uint32_t w0 = 0;
-    for (uint32_t b = 0; b < 4 && b < vl; ++b) w0 |= (uint32_t)val[b] << (8 * b);
-    uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
-    sl[0] = make_uint4((uint32_t)k8, (uint32_t)(k8 >> 32),
-                       (1u << 31) | (vl << 8) | kl, w0);
-    if (v.kv_ool) {
-      ool.push_back({ks, i});
-    } else {
-      uint8_t tmp[16 * 9] = {0};
-      if (vl > 4) memcpy(tmp, val + 4, vl - 4);
-      for (uint32_t c = 1; c < v.KVW; ++c) memcpy(&sl[c], tmp + 16 * (c - 1), 16);
+    if (p == v.KS) {
+      spill.push_back(i);
+      continue;
     }
+    uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
+    fill(sl, i, k8);
+    if (v.kv_ool) ool.push_back({sl, i});
+  }
+  // the chain: fresh buckets from the overflow pool (4 slots a bucket);
+  // the replica's old chain, if any, is left behind like its old value
+  // blocks (both pools are bump-allocated, drb_config.kv_overflow_buckets)
+  const uint64_t nb = (spill.size() + 3) / 4;
+  std::vector<uint4> ovf(nb * 4 * v.KVW, make_uint4(0, 0, 0, 0));
+  unsigned long long obase = 0;
+  if (v.kv_ovf_head) {
+    HIPCHK(hipMemcpyAsync(&obase, v.kv_ovf_used, 8, hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (nb && obase + nb > v.kv_ovf_cap) return DRB_ERANGE;
+  }
+  for (size_t q = 0; q < spill.size(); ++q) {
+    uint4 *sl = &ovf[q * v.KVW];
+    fill(sl, spill[q], key8(spill[q]));
+    if (v.kv_ool) ool.push_back({sl, spill[q]});
   }
   if (!ool.empty()) {  // fresh value blocks from the bump allocator
     unsigned long long next = 0;
@@ -2646,8 +2732,7 @@ extern "C" int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
     std::vector<uint4> blocks(ool.size() * v.VB, make_uint4(0, 0, 0, 0));
     for (size_t q = 0; q < ool.size(); ++q) {
       const size_t i = ool[q].second;
-      tbl[(uint64_t)ool[q].first * v.KVW + 1] =
-          make_uint4((uint32_t)(next + q), 0, 0, 0);
+      ool[q].first[1] = make_uint4((uint32_t)(next + q), 0, 0, 0);
       memcpy(&blocks[q * v.VB], vals + i * val_stride, val_lens[i]);
     }
     HIPCHK(hipMemcpyAsync(v.kv_pool + next * v.VB, blocks.data(),
@@ -2656,6 +2741,24 @@ extern "C" int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
     const unsigned long long nn = next + ool.size();
     HIPCHK(hipMemcpyAsync(v.kv_pool_next, &nn, 8, hipMemcpyHostToDevice,
                           e->stream));
+  }
+  if (v.kv_ovf_head) {
+    std::vector<uint32_t> links(nb);
+    for (uint64_t q = 0; q < nb; ++q)
+      links[q] = q + 1 < nb ? (uint32_t)(obase + q + 2) : 0u;
+    const uint32_t head = nb ? (uint32_t)(obase + 1) : 0u;
+    if (nb) {
+      HIPCHK(hipMemcpyAsync(v.kv_ovf + obase * 4 * v.KVW, ovf.data(),
+                            ovf.size() * sizeof(uint4), hipMemcpyHostToDevice,
+                            e->stream));
+      HIPCHK(hipMemcpyAsync(v.kv_ovf_next + obase, links.data(), nb * 4,
+                            hipMemcpyHostToDevice, e->stream));
+      const unsigned long long nu = obase + nb;
+      HIPCHK(hipMemcpyAsync(v.kv_ovf_used, &nu, 8, hipMemcpyHostToDevice,
+                            e->stream));
+    }
+    HIPCHK(hipMemcpyAsync(v.kv_ovf_head + ix(v, slot, group), &head, 4,
+                          hipMemcpyHostToDevice, e->stream));
   }
   HIPCHK(hipMemcpyAsync(v.kv + kv_ix(v, slot, group, 0), tbl.data(),
                         tbl.size() * sizeof(uint4), hipMemcpyHostToDevice,
@@ -2672,8 +2775,12 @@ extern "C" int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot,
   const View &v = e->v;
   std::vector<uint4> tbl;
   if (read_kv_table(e, group, slot, tbl)) return DRB_EDEVICE;
+  std::vector<uint4> ch;  // the overflow chain's slots after the table's
+  if (read_ovf_chain(e, group, slot, ch)) return DRB_EDEVICE;
+  tbl.insert(tbl.end(), ch.begin(), ch.end());
+  const uint64_t nslots = tbl.size() / v.KVW;
   size_t n = 0;
-  for (uint32_t ks = 0; ks < v.KS; ++ks) {
+  for (uint64_t ks = 0; ks < nslots; ++ks) {
     const uint4 *sl = &tbl[(uint64_t)ks * v.KVW];
     if (!((sl[0].z >> 31) & 1u)) continue;
     if (n < cap) {
@@ -2711,8 +2818,8 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
       const uint64_t sm = code == PK_ESC16
                               ? v.u64[u64_ix(v, F_SM_INDEX, slot, g)]
                               : pk_idx_value(code, last, false);
-      serve_reads_lane(v, slot, g, n, sm, n_reads, key_space, served,
-                       deferred);
+      serve_reads_lane<true>(v, slot, g, n, sm, n_reads, key_space, served,
+                             deferred);
     }
   }
   const uint32_t cnt[2] = {served, deferred};

@@ -323,6 +323,14 @@ struct View {
   unsigned long long *kv_pool_next;  // bump allocator
   uint64_t kv_pool_blocks;
   uint32_t kv_ool, VB;
+  // KV overflow (drb_config.kv_overflow_buckets): buckets of 4 slots
+  // [bucket][4][KVW], per bucket the next one (+1, 0: end), per replica its
+  // chain's head (+1), the bump counter and the pool's size
+  uint4 *kv_ovf;
+  uint32_t *kv_ovf_next;
+  uint32_t *kv_ovf_head;  // [R][G]
+  unsigned long long *kv_ovf_used;
+  uint64_t kv_ovf_cap;
   uint4 *props;           // [P][max_props][PROP_META + C16][G]
   uint32_t *prop_count;   // [P][G]
   uint4 *ri_in;           // [RS][G] {low, high}

@@ -1515,6 +1515,39 @@ DRB_DEV bool put_value_long(const View &v, uint32_t slot,
   return true;
 }
 
+// The KV's overflow chain (drb_config.kv_overflow_buckets): a replica
+// whose table is full keeps further keys in buckets of 4 slots, newest
+// first.  Returns the key's slot (hit) or, with `insert`, a free one -- the
+// head bucket's next free slot, or slot 0 of a bucket taken from the pool
+// and linked in front -- else null (absent, or the pool is used up).
+DRB_DEV uint4 *kv_ovf_walk(const View &v, uint32_t slot, uint64_t g,
+                           uint64_t key8, uint32_t klen, bool insert,
+                           bool &hit) {
+  hit = false;
+  uint32_t *const headp = v.kv_ovf_head + ix(v, slot, g);
+  uint4 *free_sl = nullptr;
+  for (uint32_t b = *headp; b;) {
+    uint4 *bk = v.kv_ovf + (uint64_t)(b - 1) * 4 * v.KVW;
+    for (uint32_t t = 0; t < 4; ++t) {
+      uint4 *sl = bk + (uint64_t)t * v.KVW;
+      const uint4 h = sl[0];
+      if (!((h.z >> 31) & 1u)) {
+        if (!free_sl) free_sl = sl;
+      } else if ((h.z & 0xffu) == klen && lo64(h) == key8) {
+        hit = true;
+        return sl;
+      }
+    }
+    b = v.kv_ovf_next[b - 1];
+  }
+  if (!insert || free_sl) return free_sl;
+  const unsigned long long nb = atomicAdd(v.kv_ovf_used, 1ull);
+  if (nb >= v.kv_ovf_cap) return nullptr;
+  v.kv_ovf_next[nb] = *headp;
+  *headp = (uint32_t)nb + 1;
+  return v.kv_ovf + (uint64_t)nb * 4 * v.KVW;
+}
+
 // handleEntry (statemachine.go:935-969) -> update (1057-1103) ->
 // GetPayload (encoded.go:55-65) -> KVTest.Update (kvtest.go:145-162).
 // Returns: 0 noop applied, 1 KV updated, -1 not on the fast path, -2 the
@@ -1657,6 +1690,19 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       return 1;
     }
   }
+  if (EXT && v.kv_ovf_head) {  // the table is full: the overflow chain
+    bool hit = false;
+    uint4 *sl = kv_ovf_walk(v, L.slot, L.g, key8, klen, true, hit);
+    if (sl && put_value_long(v, L.slot, L.g, index, sl, hit, voff, vlen)) {
+      sl[0] = make_uint4((uint32_t)key8, (uint32_t)(key8 >> 32),
+                         (1u << 31) | (vlen << 8) | klen, w0);
+      r.kv_added++;
+      r.sm_index = index;
+      r.sm_term = term;
+      r.applied_any = true;
+      return 1;
+    }
+  }
   return -2;  // table full
 }
 
@@ -1777,8 +1823,10 @@ DRB_DEV uint64_t kv_word(uint4 h) {
 }
 // probes t0 .. KS-1 of home slot `home` (kv_probe), DRB_PROBE_WR slots
 // per memory round trip
+template <bool OVF>
 DRB_DEV uint64_t kv_probe_word(const View &v, const uint4 *tbl, uint32_t home,
-                               uint32_t t0, uint64_t key8, uint32_t klen) {
+                               uint32_t t0, uint64_t key8, uint32_t klen,
+                               uint32_t slot, uint64_t g) {
   for (uint32_t p0 = t0; p0 < v.KS; p0 += DRB_PROBE_WR) {
     uint4 hs[DRB_PROBE_WR];
 #pragma unroll
@@ -1801,6 +1849,11 @@ DRB_DEV uint64_t kv_probe_word(const View &v, const uint4 *tbl, uint32_t home,
     }
     if (res) return w;
   }
+  if (OVF && v.kv_ovf_head) {  // a full table: the overflow chain
+    bool hit = false;
+    const uint4 *sl = kv_ovf_walk(v, slot, g, key8, klen, false, hit);
+    if (hit) return kv_word(sl[0]);
+  }
   return ~0ull;
 }
 
@@ -1812,6 +1865,7 @@ DRB_DEV uint64_t kv_probe_word(const View &v, const uint4 *tbl, uint32_t home,
 #endif
 constexpr uint32_t READ_BATCH = DRB_READ_BATCH;
 
+template <bool OVF>
 DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
                               uint32_t nrtr, uint64_t sm_index,
                               uint32_t n_reads, uint32_t key_space,
@@ -1865,8 +1919,9 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
             done = true;
           }
         }
-        if (!done && v.KS > DRB_READ_W)
-          w = kv_probe_word(v, tbl, ks[t], DRB_READ_W, key[t], 8);
+        if (!done && (v.KS > DRB_READ_W || (OVF && v.kv_ovf_head)))
+          w = kv_probe_word<OVF>(v, tbl, ks[t], DRB_READ_W, key[t], 8, slot,
+                                 g);
         sum += mix64(w ^ key[t] ^ ((uint64_t)j << 56));
         served++;
         if (v.read_res)  // ReadLocalNode's result for the client
@@ -3051,7 +3106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     if (p.encode_saves && c_saved == 0) v.save_len[ix(v, slot, g)] = 0;
     // ReadLocalNode of the released reads, against the state just applied
     if (p.n_reads && !(DRB_ABLATE & 2))
-      serve_reads_lane(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
+      serve_reads_lane<EXT>(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
                        p.key_space, c_served, c_deferred);
   }
   // per-block summary of this rank's remote planes (drb_exchange_*): max

@@ -158,7 +158,8 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 total_groups=0, place_world=1, place_rank=0, entry_mbox=0,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
-                tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0)
+                tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0,
+                kv_overflow_buckets=0)
 
 
 class Engine:
@@ -180,7 +181,7 @@ class Engine:
                    cfg["durable_log"], cfg["save_batched"],
                    cfg["save_tan"], cfg["elections"], cfg["tan_max_log"],
                    cfg["tan_multiplexed"], cfg["pre_vote"],
-                   cfg["max_reads_per_ctx"])
+                   cfg["max_reads_per_ctx"], cfg["kv_overflow_buckets"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -432,12 +433,18 @@ class Engine:
     def kv_export(self, g, slot):
         cap = self.cfg["kv_slots"]
         vcap = self.cfg["kv_val_cap"]
-        keys = (C.c_uint8 * (8 * cap))()
-        vals = (C.c_uint8 * (vcap * cap))()
-        kl, vl = (U32 * cap)(), (U32 * cap)()
-        n = SZ()
-        _ck(lib().drb_kv_export(self.h, g, slot, keys, kl, vals, vl, cap,
-                                C.byref(n)), "drb_kv_export")
+        while True:  # (a KV with overflow buckets may hold more)
+            keys = (C.c_uint8 * (8 * cap))()
+            vals = (C.c_uint8 * (vcap * cap))()
+            kl, vl = (U32 * cap)(), (U32 * cap)()
+            n = SZ()
+            rc = lib().drb_kv_export(self.h, g, slot, keys, kl, vals, vl, cap,
+                                     C.byref(n))
+            if rc == -5 and n.value > cap:  # DRB_ERANGE: the full count
+                cap = n.value
+                continue
+            _ck(rc, "drb_kv_export")
+            break
         kb, vb = bytes(keys), bytes(vals)
         return {kb[i * 8:i * 8 + kl[i]]: vb[i * vcap:i * vcap + vl[i]]
                 for i in range(n.value)}

@@ -374,6 +374,16 @@ typedef struct drb_config {
    * the clients' ReadLocalNode calls; 0: only the per-replica checksum
    * (drb_export_read_sums) */
   uint32_t max_reads_per_ctx;
+  /* > 0: the KV grows past kv_slots.  A replica whose table is full puts
+   * further keys in overflow buckets of 4 slots, chained per replica and
+   * bump-allocated from a pool of this many buckets shared by the engine
+   * (KVTest's map grows, kvtest.go:145-162); a lookup that finds a full
+   * table walks the chain.  Rounds run the EXT step kernels.  An
+   * exhausted pool stops the apply as a full table does; drb_kv_import
+   * lays a replica's keys past kv_slots into fresh buckets (its old chain
+   * is not reclaimed).  0: a full table stops the replica's apply
+   * (DRB_F_APPLY_STOPPED). */
+  uint64_t kv_overflow_buckets;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -882,7 +892,9 @@ int drb_kv_import(drb_engine *e, uint64_t group, uint32_t slot,
                   const uint8_t *vals, const uint32_t *val_lens,
                   size_t val_stride, size_t n);
 /* Dumps every KV pair of one replica: keys[i*8..], key_lens[i],
- * vals[i*kv_val_cap..], val_lens[i]; returns the count in *n_out. */
+ * vals[i*kv_val_cap..], val_lens[i]; returns the count in *n_out (the
+ * table's slots, then the overflow chain's); DRB_ERANGE, with the full
+ * count in *n_out, when it exceeds cap. */
 int drb_kv_export(drb_engine *e, uint64_t group, uint32_t slot, uint8_t *keys,
                   uint32_t *key_lens, uint8_t *vals, uint32_t *val_lens,
                   size_t cap, size_t *n_out);
