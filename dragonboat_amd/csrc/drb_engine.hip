@@ -43,6 +43,12 @@ struct drb_engine {
   hipStream_t stream_h2d;         // drb_stage_proposals uploads
   hipEvent_t ev_staged;           // upload done -> layout kernel
   hipEvent_t ev_stage_free;       // layout kernel done -> next upload
+  hipEvent_t ev_uploaded;         // packed upload done -> host arrays free
+  // per proposal slot: the engine-stream work that last read or wrote it
+  // (drb_step_round_async, the generators, drb_stage_proposals), so that
+  // drb_stage_proposals_packed lays a slot out on the copy stream while
+  // rounds on other slots run
+  std::vector<hipEvent_t> ev_prop;
   uint64_t round;
   uint64_t ticks;  // LocalTicks delivered so far (RoundParams.tick_no)
   uint64_t committed_round = 0;  // drb_commit_round (durable_log)
@@ -248,10 +254,18 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
       hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) !=
           hipSuccess ||
       hipEventCreateWithFlags(&e->ev_stage_free, hipEventDisableTiming) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_uploaded, hipEventDisableTiming) !=
           hipSuccess) {
     delete e;
     return DRB_EDEVICE;
   }
+  e->ev_prop.resize(cfg->prop_slots);
+  for (auto &ev : e->ev_prop)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      delete e;
+      return DRB_EDEVICE;
+    }
   View &v = e->v;
   memset(&v, 0, sizeof(v));
   const uint64_t G = cfg->num_groups, R = cfg->num_replicas;
@@ -461,6 +475,8 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   (void)hipEventDestroy(e->ev_join);
   (void)hipEventDestroy(e->ev_staged);
   (void)hipEventDestroy(e->ev_stage_free);
+  (void)hipEventDestroy(e->ev_uploaded);
+  for (auto &ev : e->ev_prop) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream_h2d);
   (void)hipStreamDestroy(e->stream2);
   (void)hipStreamDestroy(e->stream);
@@ -1031,6 +1047,7 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
   const size_t need = pool_off + std::max<uint64_t>(pool_len, 16);
   if (need > e->stage_bytes) {
     HIPCHK(hipStreamSynchronize(e->stream));  // the buffer may be in use
+    HIPCHK(hipStreamSynchronize(e->stream_h2d));
     if (e->stage_buf) HIPCHK(hipFree(e->stage_buf));
     e->stage_buf = nullptr;
     HIPCHK(hipMalloc(&e->stage_buf, need));
@@ -1058,6 +1075,7 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
       d + pool_off, (uint64_t)pool_len);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e->ev_stage_free, e->stream));
+  HIPCHK(hipEventRecord(e->ev_prop[slot], e->stream));
   HIPCHK(hipEventSynchronize(e->ev_staged));
   return DRB_OK;
 }
@@ -1117,17 +1135,18 @@ extern "C" int drb_stage_proposals_packed(
     return DRB_EINVAL;
   const View &v = e->v;
   const uint64_t G = v.G, n = n_entries;
-  // the sums (vectorised loops; on 8 host threads the call measured slower:
-  // thread start-up costs more than the 3 MB these read)
-  uint64_t tsum = 0, bsum = 0;
+  // the counts before anything reads the entry arrays (they bound n); the
+  // lengths' sum below, beside the upload (vectorised loops; on 8 host
+  // threads the call measured slower: thread start-up costs more than the
+  // 3 MB these read)
+  uint64_t tsum = 0;
   uint32_t cmax = 0;
   for (uint64_t g = 0; g < G; ++g) {
     cmax = std::max<uint32_t>(cmax, counts[g]);
     tsum += counts[g];
   }
   if (cmax > v.max_props) return DRB_ERANGE;
-  for (uint64_t i = 0; i < n; ++i) bsum += cmd_lens[i];
-  if (tsum != n || bsum != pool_len) return DRB_EINVAL;
+  if (tsum != n) return DRB_EINVAL;
   // upload: counts | keys | client ids | lengths | pool, then device-side
   // u32 counts, lengths, their scans and the scans' temp storage
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1148,14 +1167,17 @@ extern "C" int drb_stage_proposals_packed(
                need = o_tmp + al(std::max(tb1, tb2));
   if (need > e->stage_bytes) {
     HIPCHK(hipStreamSynchronize(e->stream));  // the buffer may be in use
+    HIPCHK(hipStreamSynchronize(e->stream_h2d));
     if (e->stage_buf) HIPCHK(hipFree(e->stage_buf));
     e->stage_buf = nullptr;
     HIPCHK(hipMalloc(&e->stage_buf, need));
     e->stage_bytes = need;
   }
   uint8_t *d = (uint8_t *)e->stage_buf;
-  // the upload on the copy stream (overlapping the running round), the
-  // layout on the engine stream, as drb_stage_proposals
+  // the upload and the layout on the copy stream: the upload overlaps the
+  // running round; the layout waits only for the engine-stream work on
+  // this slot (ev_prop), so it runs beside a round that reads another
+  // slot, and the engine stream waits for it before its next round
   HIPCHK(hipStreamWaitEvent(e->stream_h2d, e->ev_stage_free, 0));
   HIPCHK(hipMemcpyAsync(d + o_cnt, counts, G, hipMemcpyHostToDevice,
                         e->stream_h2d));
@@ -1170,27 +1192,38 @@ extern "C" int drb_stage_proposals_packed(
   if (pool_len)
     HIPCHK(hipMemcpyAsync(d + o_pool, pool, pool_len, hipMemcpyHostToDevice,
                           e->stream_h2d));
-  HIPCHK(hipEventRecord(e->ev_staged, e->stream_h2d));
-  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_staged, 0));
+  HIPCHK(hipEventRecord(e->ev_uploaded, e->stream_h2d));
+  // the lengths' sum while the upload runs; a batch that fails it is not
+  // laid out, the slot stays as it was
+  uint64_t bsum = 0;
+  for (uint64_t i = 0; i < n; ++i) bsum += cmd_lens[i];
+  if (bsum != pool_len) {
+    HIPCHK(hipEventRecord(e->ev_stage_free, e->stream_h2d));
+    HIPCHK(hipEventSynchronize(e->ev_uploaded));
+    return DRB_EINVAL;
+  }
+  HIPCHK(hipStreamWaitEvent(e->stream_h2d, e->ev_prop[slot], 0));
+  hipStream_t ls = e->stream_h2d;
   uint32_t *c32 = (uint32_t *)(d + o_c32), *e0 = (uint32_t *)(d + o_e0);
   uint32_t *l32 = (uint32_t *)(d + o_l32), *off = (uint32_t *)(d + o_off);
-  k_widen_u8<<<(unsigned)((G + 255) / 256), 256, 0, e->stream>>>(d + o_cnt,
-                                                                  c32, G);
+  k_widen_u8<<<(unsigned)((G + 255) / 256), 256, 0, ls>>>(d + o_cnt, c32, G);
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(d + o_tmp, tb1, c32, e0, (int)G,
-                                          e->stream));
+                                          ls));
   if (n) {
-    k_widen_u16<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(
+    k_widen_u16<<<(unsigned)((n + 255) / 256), 256, 0, ls>>>(
         (const uint16_t *)(d + o_len), l32, n);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(d + o_tmp, tb2, l32, off, (int)n,
-                                            e->stream));
+                                            ls));
   }
-  k_stage_packed<<<(unsigned)((G + 255) / 256), 256, 0, e->stream>>>(
+  k_stage_packed<<<(unsigned)((G + 255) / 256), 256, 0, ls>>>(
       v, slot, type, c32, e0, (const uint64_t *)(d + o_key),
       (const uint64_t *)(d + o_cid), l32, off, d + o_pool,
       (uint64_t)pool_len);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(e->ev_stage_free, e->stream));
-  HIPCHK(hipEventSynchronize(e->ev_staged));
+  HIPCHK(hipEventRecord(e->ev_staged, ls));
+  HIPCHK(hipEventRecord(e->ev_stage_free, ls));
+  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_staged, 0));
+  HIPCHK(hipEventSynchronize(e->ev_uploaded));
   return DRB_OK;
 }
 
@@ -1266,6 +1299,7 @@ extern "C" int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot,
   k_gen_kv<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
       e->v, slot, k, key_space, val_len, seed, salt, active_ppm);
   HIPCHK(hipGetLastError());  // stream-ordered before the next round
+  HIPCHK(hipEventRecord(e->ev_prop[slot], e->stream));
   return DRB_OK;
 }
 
@@ -1971,6 +2005,8 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
     int rc = launch_tan(e, (uint32_t)p.round);
     if (rc) return rc;
   }
+  if (p.prop_slot != DRB_NONE)
+    HIPCHK(hipEventRecord(e->ev_prop[p.prop_slot], e->stream));
   e->round++;
   e->ticks += p.tick;
   if (p.n_reads) {
