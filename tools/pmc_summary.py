@@ -52,17 +52,27 @@ def main():
         k = kernels.setdefault(name, {})
         k[ctr] = sum(vals) / len(vals) * 1024.0
         k["launches_" + ctr] = len(vals)
-    round_bytes = 0.0
+    round_bytes = round_lower = 0.0
     for name, k in kernels.items():
         k["hbm_bytes"] = 2.0 * k.get("FETCH_SIZE", 0.0) + k.get("WRITE_SIZE",
                                                                  0.0)
         if any(t in name for t in ROUND_KERNELS):
             round_bytes += k["hbm_bytes"]
+            round_lower += k.get("FETCH_SIZE", 0.0) + k.get("WRITE_SIZE", 0.0)
     out = {"groups": a.groups, "replicas": a.replicas,
            "workload": a.workload,
            "round_hbm_bytes": round_bytes,
            "bytes_per_group_round": round_bytes / a.groups,
+           "round_hbm_bytes_lower": round_lower,
+           "bytes_per_group_round_lower": round_lower / a.groups,
            "correction": "FETCH_SIZE x2 + WRITE_SIZE (KiB -> B)",
+           "bound_note": "round_hbm_bytes = FETCH_SIZE x2 + WRITE_SIZE is an "
+                         "upper bound: the x2 correction is calibrated for "
+                         "coalesced 16 B/lane reads (MI355X_MICROARCH.md), "
+                         "while a random 16 B read (the KV probes) is tallied "
+                         "at its full 64 B already (profiles/r02_kvline/"
+                         "calib.log); FETCH_SIZE + WRITE_SIZE "
+                         "(round_hbm_bytes_lower) is the matching lower bound",
            "kernels": kernels}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)

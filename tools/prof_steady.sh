@@ -14,4 +14,4 @@ python tools/trace_summary.py $o/trace 20 $o/kernels_last20.csv > $o/kernels_las
 tools/gpu_step.sh 300 $o/fetch.log timeout -s KILL 280 rocprofv3 --pmc FETCH_SIZE -d $o/fetch -o run --output-format csv -- $B || exit 1
 tools/gpu_step.sh 300 $o/write.log timeout -s KILL 280 rocprofv3 --pmc WRITE_SIZE -d $o/write -o run --output-format csv -- $B || exit 1
 python tools/pmc_summary.py "$(dirname $(find $o/fetch -name '*counter_collection.csv' | head -1))" \
-  "$(dirname $(find $o/write -name '*counter_collection.csv' | head -1))" $o/pmc_summary.json --workload C3 --last 20
+  "$(dirname $(find $o/write -name '*counter_collection.csv' | head -1))" $o/pmc_summary.json --workload "C3 at the KV steady state (bench.py --kv-fill 1536), timed rounds only (--last 20)" --last 20
