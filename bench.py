@@ -415,6 +415,9 @@ def main():
                            "replicas; the timed rounds write fresh keys "
                            "and read uniformly over the %d" % (R, KEY_SPACE)}
     eng.read_counters(reset=True)
+    phase_dbg = os.environ.get("DRB_PHASE") == "1"  # timing variants only
+    if phase_dbg:
+        eng.debug_phase(reset=True)
     warm_flagged = len(eng.take_flagged(reset=True)[0])
     if xch is not None:
         xch.bytes_sent = 0
@@ -434,6 +437,13 @@ def main():
     ddist.barrier()
     t1 = time.perf_counter()
     out = eng.read_counters(reset=True)
+    if phase_dbg:  # cycles per stepped lane of each round phase
+        for role, x in eng.debug_phase(reset=True).items():
+            if x[0]:
+                print("phase %s lanes %d: %s" % (
+                    role, x[0] // K, " ".join("%.0f" % (c / x[0])
+                                              for c in x[1:])),
+                      file=sys.stderr)
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
     elapsed = t1 - t0
     committed = out.committed_entries

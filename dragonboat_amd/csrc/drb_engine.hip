@@ -333,6 +333,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.kv_pool, v.kv_pool_blocks * v.VB);
     rc |= dalloc(e, &v.kv_pool_next, 1);
   }
+  if (const char *ph = getenv("DRB_PHASE"))  // timing builds only
+    if (ph[0] == '1') rc |= dalloc(e, &v.phase, 16);
   v.kv_ovf_cap = cfg->kv_overflow_buckets;
   if (v.kv_ovf_cap) {
     if (v.kv_ovf_cap >= 0xffffffffull) {
@@ -2034,6 +2036,22 @@ __global__ void k_sum_counters(const unsigned long long *rows, uint64_t n,
     if (threadIdx.x == 0) total[c] = part[0];
     __syncthreads();
   }
+}
+
+// per-phase cycle sums of the step kernels' lanes ([follower, leader] x
+// {lanes, load + pre-pass, dispatch, tick + proposals, getUpdate, apply,
+// store, reads}); zeros unless the engine was created with DRB_PHASE=1 and
+// the step kernels built with DRB_PHASE_PROF=1 (a timing variant)
+extern "C" int drb_debug_phase(drb_engine *e, uint64_t *out, int reset) {
+  if (!e || !out) return DRB_EINVAL;
+  memset(out, 0, 16 * sizeof(uint64_t));
+  if (!e->v.phase) return DRB_OK;
+  HIPCHK(hipMemcpyAsync(out, e->v.phase, 16 * sizeof(uint64_t),
+                        hipMemcpyDeviceToHost, e->stream));
+  if (reset)
+    HIPCHK(hipMemsetAsync(e->v.phase, 0, 16 * sizeof(uint64_t), e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
 }
 
 extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,

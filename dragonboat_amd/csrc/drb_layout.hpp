@@ -331,6 +331,9 @@ struct View {
   uint32_t *kv_ovf_head;  // [R][G]
   unsigned long long *kv_ovf_used;
   uint64_t kv_ovf_cap;
+  // DRB_PHASE_PROF step builds: [2 roles][8] cycle sums per round phase
+  // (drb_debug_phase; allocated when DRB_PHASE=1 at drb_engine_create)
+  unsigned long long *phase;
   uint4 *props;           // [P][max_props][PROP_META + C16][G]
   uint32_t *prop_count;   // [P][G]
   uint4 *ri_in;           // [RS][G] {low, high}

@@ -91,6 +91,11 @@ namespace drb {
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
+// timing only: per-phase cycle sums of the leader / follower lanes
+// (View.phase, drb_debug_phase); 0 in shipped builds
+#ifndef DRB_PHASE_PROF
+#define DRB_PHASE_PROF 0
+#endif
 // interleave a launch's slot rows per XCD (block_pos); 0: row-major.
 // Measured (profiles/r01_pair_xcd, r01_c4_pair): neutral at C3, 7 % slower
 // at C4 N=1 (four follower rows), so off by default
@@ -2292,6 +2297,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   constexpr bool FPF = PFN > 0;
   constexpr int PFS = LEAD ? 2 : 1;
   __shared__ uint4 pf_lds[FPF ? PFS : 1][FPF ? PFN : 1][FPF ? 256 : 1];
+  constexpr int NPH = (DRB_PHASE_PROF && !SLOW) ? 8 : 1;
+  __shared__ uint32_t ph_lds[NPH][NPH > 1 ? 256 : 1];
+  uint32_t ph_t = 0;
+  if (NPH > 1)
+#pragma unroll
+    for (int i = 0; i < NPH; ++i) ph_lds[i][threadIdx.x] = 0;
+#define DRB_PH(i)                                                   \
+  do {                                                              \
+    if (NPH > 1) {                                                  \
+      const uint32_t now = (uint32_t)__builtin_readcyclecounter();  \
+      ph_lds[(i) < NPH ? (i) : 0][NPH > 1 ? threadIdx.x : 0] = now - ph_t; \
+      ph_t = now;                                                   \
+    }                                                               \
+  } while (0)
   // placement C4 only: [R][256] (the launch sizes it, drb_step_inst.hip)
   extern __shared__ uint64_t elo_dyn[];
   uint64_t(*elo_lds)[256] = reinterpret_cast<uint64_t(*)[256]>(elo_dyn);
@@ -2345,6 +2364,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     active = false;
   if (active) {
     c_stepped = 1;
+    if (NPH > 1) ph_t = (uint32_t)__builtin_readcyclecounter();
     Rep<R> r;
     load_rep<R, LEAD>(L, r);
     r.role = SLOW ? role : LEAD ? DRB_LEADER : DRB_FOLLOWER;
@@ -2709,6 +2729,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           (uint64_t)v.save_cap16 * 16)
         fb = DRB_FB_CAPACITY;
     }
+    DRB_PH(1);  // load + pre-pass
     // elections: what the raft launch handles goes there, untouched
     bool to_slow = false;
     if (!SLOW && v.elections &&
@@ -2809,6 +2830,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           }
         }
       }
+      DRB_PH(2);  // handleEvents: the inbox dispatch
       // LocalTick (node.tick node.go:1562 -> raft.tick raft.go:571-648)
       bool quiet = false;
       if (p.tick && qon) {
@@ -2900,6 +2922,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         r.nmsgs += R - 1;
       }
 
+      DRB_PH(3);  // tick + proposals
       // ---------------------------------------- getUpdate (node.go:1025)
       bool inmem_nonempty = r.last >= r.marker;
       uint64_t save_lo = r.saved_to + 1;
@@ -2982,6 +3005,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         }
         // clearReadyToRead: records stay in the round output buffer
       }
+      DRB_PH(4);  // getUpdate
       // ---------------------------------------- StateMachine.Handle
       if (apply_hi >= apply_lo && apply_lo != 0) {
         uint64_t from = umax64(apply_lo, r.sm_index + 1);
@@ -3008,6 +3032,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
             c_commit++;
         }
       }
+      DRB_PH(5);  // apply
       // the entry rows of remote followers' planes: [lowest sent, last]
       if (LEAD && v.remote_mask) {
         const uint32_t chunks = ENT_META + v.C16;
@@ -3104,11 +3129,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     }
     v.rtr_count[ix(v, slot, g)] = r.nrtr;
     if (p.encode_saves && c_saved == 0) v.save_len[ix(v, slot, g)] = 0;
+    DRB_PH(6);  // state store + outbox headers
     // ReadLocalNode of the released reads, against the state just applied
     if (p.n_reads && !(DRB_ABLATE & 2))
       serve_reads_lane<EXT>(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
                        p.key_space, c_served, c_deferred);
+    DRB_PH(7);  // served reads
   }
+  if (NPH > 1 && v.phase) {  // uniform: the lanes' phase sums, one atomic
+    // per wave and phase (lane 0: stepped lanes)
+#pragma unroll
+    for (int i = 0; i < NPH; ++i) {
+      uint64_t x =
+          i ? (c_stepped ? ph_lds[i][NPH > 1 ? threadIdx.x : 0] : 0u) : c_stepped;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+        x += (uint64_t)__shfl_xor((long long)x, o, 64);
+      if ((threadIdx.x & 63) == 0 && x)
+        atomicAdd(&v.phase[(LEAD ? 8 : 0) + i], (unsigned long long)x);
+    }
+  }
+#undef DRB_PH
   // per-block summary of this rank's remote planes (drb_exchange_*): max
   // records, max entry rows, c1 / Replicate flags; the raft launch adds its
   // lanes' to the slow rows, lane by lane (its lanes are no slot's block)

@@ -65,6 +65,7 @@ SIGNATURES = {
                                  C.POINTER(RoundOut)]),
     "drb_step_round_async": (C.c_int, [P, C.POINTER(RoundIn)]),
     "drb_read_counters": (C.c_int, [P, C.POINTER(RoundOut), C.c_int]),
+    "drb_debug_phase": (C.c_int, [P, C.POINTER(U64), C.c_int]),
     "drb_take_flagged": (C.c_int, [P, C.POINTER(Flagged), SZ, C.POINTER(SZ),
                                    PU64, C.c_int]),
     "drb_apply_results": (C.c_int, [P, U32, U64, U64, C.POINTER(ApplyResult),
@@ -338,6 +339,13 @@ class Engine:
         _ck(lib().drb_read_counters(self.h, C.byref(out), int(reset)),
             "drb_read_counters")
         return out
+
+    def debug_phase(self, reset=True):
+        """drb_debug_phase: {role: [lanes, cycles of each round phase]}
+        (timing builds only; zeros otherwise)."""
+        out = (U64 * 16)()
+        _ck(lib().drb_debug_phase(self.h, out, int(reset)), "drb_debug_phase")
+        return {"follower": list(out[:8]), "leader": list(out[8:])}
 
     def take_flagged(self, cap=65536, reset=True):
         """[(group, slot, reason, flags, round, shard_id)] of the replicas

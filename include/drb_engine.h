@@ -596,6 +596,12 @@ int drb_step_round(drb_engine *e, const drb_round_in *in, drb_round_out *out);
  * and are read by drb_read_counters(). */
 int drb_step_round_async(drb_engine *e, const drb_round_in *in);
 int drb_read_counters(drb_engine *e, drb_round_out *out, int reset);
+/* Timing builds only: per-phase cycle sums of the step kernels' lanes,
+ * out[16] = [follower, leader] x {lanes stepped, load + pre-pass, inbox
+ * dispatch, tick + proposals, getUpdate, apply, state store, served reads};
+ * zeros unless the engine was created with DRB_PHASE=1 in the environment
+ * and the step kernels were built with DRB_PHASE_PROF=1. */
+int drb_debug_phase(drb_engine *e, uint64_t *out, int reset);
 
 /*
  * The replicas that left the fast path (DRB_F_FALLBACK / DRB_F_ERROR),
