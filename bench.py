@@ -63,7 +63,11 @@ def pmc_traffic(G, R):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; without an external "
+                         "launcher, N > 1 starts N ranks itself "
+                         "(torch.distributed.run); under one it must equal "
+                         "WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3",
@@ -147,6 +151,12 @@ def parse():
                     help="after the timed region, also time rounds whose "
                          "proposals come from host memory through "
                          "drb_stage_proposals (default: on for c2/c3, N=1)")
+    ap.add_argument("--step-worker", type=int, default=-1,
+                    help="after the timed region, also time whole step-"
+                         "worker rounds: host-staged proposals, the round, "
+                         "and its ReadyToReads, read results and applied "
+                         "entries back in pinned host memory "
+                         "(drb_worker_export; default: on for c3, N=1)")
     return ap.parse_args()
 
 
@@ -236,8 +246,33 @@ def cpu_baseline(args, seconds):
                            else "writes only"))
 
 
+def self_launch(args):
+    """bench.py --gpus N with no launcher around it: start N ranks, one
+    process per GPU, as the driver's own torch.distributed.run line would,
+    and exit with their status.  This process touches no GPU before the
+    ranks start (nothing here imports torch.cuda state), so the ranks are
+    fresh children, not an exec of a GPU-initialised process."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" in os.environ:
+        if args.gpus is not None and args.gpus != int(os.environ["WORLD_SIZE"]):
+            sys.exit("bench.py: --gpus %d under a launcher with WORLD_SIZE=%s"
+                     % (args.gpus, os.environ["WORLD_SIZE"]))
+    elif args.gpus is not None and args.gpus > 1:
+        sys.exit(self_launch(args))
     import torch
     import torch.distributed as dist
     from dragonboat_amd import dist as ddist
@@ -331,6 +366,9 @@ def main():
                      save_tan=int(args.save in ("tan", "tanmux")),
                      tan_multiplexed=int(args.save == "tanmux"),
                      elections=args.elections,
+                     # the timed reads leave each client's ReadLocalNode
+                     # result (drb_export_read_results / the step worker)
+                     max_reads_per_ctx=READS_PER_CTX if reads else 0,
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     stream = torch.cuda.ExternalStream(eng.stream)
@@ -580,6 +618,7 @@ def main():
         eng.host_slot(0, True)
     from dragonboat_amd import abi as _abi
     host_staged = None
+    step_worker = None
     if args.host_staged < 0:
         args.host_staged = int(world == 1 and not (c4 or c5) and k == 1 and
                                not args.failover)
@@ -625,6 +664,60 @@ def main():
                     "array on a copy stream overlapping the previous round, "
                     "+ scans and a layout kernel), timed around the whole "
                     "loop; not `value`"}
+        if args.step_worker < 0:
+            args.step_worker = int(reads and not c2)
+        if args.step_worker:
+            # engine.processSteps as a whole (engine.go:1304-1364): the
+            # entry queue up, the round, and every output a step worker
+            # hands to its nodes down -- processReadyToRead, the served
+            # reads' results, pendingProposals.applied -- exported behind
+            # each round and drained on a copy stream into pinned host
+            # buffers while the next round runs (two buffer sets)
+            wb = [eng.worker_bufs(2 * G, 2 * G * READS_PER_CTX, 4 * G * k)
+                  for _ in range(2)]
+            KW = max(5, K)
+            down = [0, 0, 0]
+            eng.read_counters(reset=True)
+            eng.sync()
+            w0 = time.perf_counter()
+            for i in range(KW):
+                b = i % HB
+                bw = wb[i % 2]
+                if i >= 2:  # the worker consumed export i - 2's buffers
+                    n3 = eng.worker_wait(bw)
+                    down = [d + x for d, x in zip(down, n3)]
+                eng.stage_proposals_packed(b, _abi.ENTRY_ENCODED, *hp[b])
+                step(2 * args.warmup + K + KH + i, b)
+                eng.worker_export(0, bw)
+            for i in range(max(0, KW - 2), KW):
+                n3 = eng.worker_wait(wb[i % 2])
+                down = [d + x for d, x in zip(down, n3)]
+            wms = (time.perf_counter() - w0) * 1e3 / KW
+            wout = eng.read_counters(reset=True)
+            for bw in wb:
+                eng.free_worker_bufs(bw)
+            import ctypes as _C
+            dbytes = (down[0] * _C.sizeof(_abi.WorkerRead) + down[1] * 8 +
+                      down[2] * _C.sizeof(_abi.WorkerApplied)) / KW
+            step_worker = {
+                "ms_per_step": wms, "steps": KW,
+                "committed_entries_per_s": wout.committed_entries /
+                (wms * KW * 1e-3),
+                "upload_bytes_per_round": int(sum(x.numel()
+                                                  for x in hb[0])),
+                "download_bytes_per_round": int(dbytes),
+                "ready_to_reads_per_round": down[0] / KW,
+                "read_results_per_round": down[1] / KW,
+                "applied_per_round": down[2] / KW,
+                "note": "whole step-worker rounds timed around the loop: "
+                        "packed proposals from pinned host memory, the "
+                        "round with its 9 reads per released ctx, then "
+                        "drb_worker_export of slot 0's ReadyToReads, "
+                        "read results and applied entries into pinned "
+                        "host buffers (compaction behind the round, the "
+                        "transfer on a copy stream overlapping the next "
+                        "round; drb_worker_wait before a buffer set is "
+                        "reused); not `value`"}
         del hb, hp
     # the replicas that left the fast path during the run, by reason
     # (drb_take_flagged): a run with any is not a pure fast-path number
@@ -769,6 +862,8 @@ def main():
             res["wire"] = wire
         if host_staged is not None:
             res["host_staged"] = host_staged
+        if step_worker is not None:
+            res["step_worker"] = step_worker
         if failover is not None:
             res["failover"] = failover
         if args.elections:

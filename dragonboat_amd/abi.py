@@ -16,6 +16,7 @@ DRB_EDEVICE = -2
 DRB_ENOMEM = -3
 DRB_ENOSYS = -4
 DRB_ERANGE = -5
+DRB_EAGAIN = -6  # retry: ingest between a round and its exchange
 
 # raftpb.MessageType (raftpb/types.go:8-37)
 MSG = dict(
@@ -48,7 +49,7 @@ F_APPLY_STOPPED = 8
 FB = dict(NONE=0, TERM_MISMATCH=1, MESSAGE_TYPE=2, ELECTION=3,
           CHECK_QUORUM=4, ENTRY_TYPE=5, CAPACITY=6, ROLE=7, SNAPSHOT=9,
           ERR_LOG_RANGE=100, ERR_COMMIT=101, ERR_APPEND=103, ERR_APPLY=104,
-          ERR_READINDEX=105, ERR_TRANSFER=106)
+          ERR_READINDEX=105, ERR_TRANSFER=106, ERR_PROPOSE=107)
 FB_NAME = {v: k for k, v in FB.items()}
 
 
@@ -135,7 +136,8 @@ class Config(C.Structure):
                 ("elections", C.c_uint32), ("tan_max_log", C.c_uint64),
                 ("tan_multiplexed", C.c_uint32), ("pre_vote", C.c_uint32),
                 ("max_reads_per_ctx", C.c_uint32),
-                ("kv_overflow_buckets", C.c_uint64)]
+                ("kv_overflow_buckets", C.c_uint64),
+                ("forward_proposals", C.c_uint32)]
 
 
 class ReadResult(C.Structure):
@@ -154,6 +156,31 @@ class ApplyResult(C.Structure):
                 ("key", C.c_uint64), ("client_id", C.c_uint64),
                 ("series_id", C.c_uint64), ("value", C.c_uint64),
                 ("slot", C.c_uint32), ("ignored", C.c_uint32)]
+
+
+class WorkerRead(C.Structure):
+    """drb_worker_read: a ReadyToRead and where its served reads are."""
+    _fields_ = [("group", C.c_uint64), ("index", C.c_uint64),
+                ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64),
+                ("n_values", C.c_uint32), ("first", C.c_uint32)]
+
+
+class WorkerApplied(C.Structure):
+    """drb_worker_applied: one applied entry (pendingProposals.applied)."""
+    _fields_ = [("group", C.c_uint64), ("index", C.c_uint64),
+                ("key", C.c_uint64), ("value", C.c_uint64),
+                ("ignored", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class WorkerBufs(C.Structure):
+    """drb_worker_bufs: pinned host buffers of one step-worker export."""
+    _fields_ = [("reads", C.POINTER(WorkerRead)), ("reads_cap", C.c_uint64),
+                ("values", C.POINTER(C.c_uint64)),
+                ("values_cap", C.c_uint64),
+                ("applied", C.POINTER(WorkerApplied)),
+                ("applied_cap", C.c_uint64),
+                ("n_reads", C.c_uint64), ("n_values", C.c_uint64),
+                ("n_applied", C.c_uint64)]
 
 
 class SaveRecord(C.Structure):
@@ -239,7 +266,7 @@ class RoundIn(C.Structure):
                 ("ri_slot", C.c_uint32), ("reads_per_ctx", C.c_uint32),
                 ("read_key_space", C.c_uint32),
                 ("encode_saves", C.c_uint32), ("ri_replica", C.c_uint32),
-                ("listed", C.c_uint32)]
+                ("listed", C.c_uint32), ("prop_replica", C.c_uint32)]
 
 
 class RoundOut(C.Structure):

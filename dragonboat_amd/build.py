@@ -3,7 +3,7 @@
 hipcc cross-compiles for gfx950 without a GPU; the .so is built in-tree so
 it travels to the GPU box with the repository snapshot.
 
-The step kernel has 40 instantiations (R = 1..8 replicas per group x five
+The step kernel has 56 instantiations (R = 1..8 replicas per group x seven
 kinds, drb_launch.hpp).  Each is its own translation unit
 (drb_step_inst.hip compiled with -DDRB_INST_R / -DDRB_INST_KIND), so the
 objects build in parallel and only the ones whose sources changed rebuild;
@@ -24,7 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
          "-Wno-pass-failed"]
-NUM_KINDS = 5
+NUM_KINDS = 7
 # the headers a step-kernel instantiation includes
 STEP_DEPS = ["drb_step_inst.hip", "drb_step.hpp", "drb_launch.hpp",
              "drb_layout.hpp", "drb_msg.hpp", "drb_codec.hpp", "drb_ring.hpp"]

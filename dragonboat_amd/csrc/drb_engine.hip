@@ -44,6 +44,13 @@ struct drb_engine {
   hipEvent_t ev_staged;           // upload done -> layout kernel
   hipEvent_t ev_stage_free;       // layout kernel done -> next upload
   hipEvent_t ev_uploaded;         // packed upload done -> host arrays free
+  // drb_exchange_local: this engine's round done (its outbox planes may be
+  // copied), and the copies into its inbound planes done (its senders'
+  // next rounds may overwrite their outbox planes)
+  hipEvent_t ev_xsend = nullptr, ev_xrecv = nullptr;
+  // the last round whose remote planes were exchanged (or enqueued, drb_
+  // exchange_mark): ingest into remote planes waits for it (DRB_EAGAIN)
+  uint64_t exchanged_round = 0;
   // per proposal slot: the engine-stream work that last read or wrote it
   // (drb_step_round_async, the generators, drb_stage_proposals), so that
   // drb_stage_proposals_packed lays a slot out on the copy stream while
@@ -65,6 +72,7 @@ struct drb_engine {
   size_t stage_bytes = 0;
   struct WireState *wire = nullptr;          // drb_encode_wire (drb_wire.hpp)
   struct IngestState *ingest = nullptr;      // drb_ingest_wire (drb_ingest.hpp)
+  struct WorkerState *worker = nullptr;      // drb_worker_export (drb_worker.hpp)
   std::mutex ingest_mu;  // drb_ingest: concurrent transport threads
   bool crc_tab_ready = false;  // c_crc_tab uploaded on this engine's device
   uint64_t tan_blocks = 0;                   // k_tan_select grid (save_tan)
@@ -83,6 +91,7 @@ struct drb_engine {
 
 static void wire_free(drb_engine *e);
 static void ingest_free(struct IngestState *st);
+static void worker_free(drb_engine *e);
 static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 static int refresh_roles(drb_engine *e);
 static int launch_tan(drb_engine *e, uint32_t round);  // drb_tan.hpp
@@ -230,6 +239,11 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
        cfg->entry_mbox > cfg->window || cfg->entry_mbox > 255))
     return DRB_EINVAL;
   if (cfg->election_rtt == 0 || cfg->heartbeat_rtt == 0) return DRB_EINVAL;
+  // forwarded proposals: a Propose's entry count travels in 4 header bits
+  // (MI_NPROP); co-resident planes only
+  if (cfg->forward_proposals &&
+      (cfg->max_props > MAX_FWD_PROPS || cfg->place_world > 1))
+    return DRB_EINVAL;
   // limitSize never binds inside the window (entryutils.go:50-63)
   if ((uint64_t)cfg->window * (128 + cfg->cmd_cap) > MAX_ENTRY_SIZE)
     return DRB_EINVAL;
@@ -256,6 +270,10 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
       hipEventCreateWithFlags(&e->ev_stage_free, hipEventDisableTiming) !=
           hipSuccess ||
       hipEventCreateWithFlags(&e->ev_uploaded, hipEventDisableTiming) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_xsend, hipEventDisableTiming) !=
+          hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_xrecv, hipEventDisableTiming) !=
           hipSuccess) {
     delete e;
     return DRB_EDEVICE;
@@ -346,9 +364,11 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.kv_ovf_head, R * G);
     rc |= dalloc(e, &v.kv_ovf_used, 1);
   }
+  v.P = cfg->prop_slots;
+  v.fwd_props = cfg->forward_proposals ? 1u : 0u;
   rc |= dalloc(e, &v.props,
-               (uint64_t)cfg->prop_slots * v.max_props * (PROP_META + v.C16) *
-                   G);
+               ((uint64_t)cfg->prop_slots + (v.fwd_props ? 2 * R : 0)) *
+                   v.max_props * (PROP_META + v.C16) * G);
   rc |= dalloc(e, &v.prop_count, (uint64_t)cfg->prop_slots * G);
   rc |= dalloc(e, &v.ri_in, (uint64_t)cfg->ri_slots * G);
   rc |= dalloc(e, &v.rtr, R * RTR_CAP * 2 * G);
@@ -473,11 +493,14 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   if (e->xout) (void)hipFree(e->xout);
   wire_free(e);
   ingest_free(e->ingest);
+  worker_free(e);
   (void)hipEventDestroy(e->ev_fork);
   (void)hipEventDestroy(e->ev_join);
   (void)hipEventDestroy(e->ev_staged);
   (void)hipEventDestroy(e->ev_stage_free);
   (void)hipEventDestroy(e->ev_uploaded);
+  if (e->ev_xsend) (void)hipEventDestroy(e->ev_xsend);
+  if (e->ev_xrecv) (void)hipEventDestroy(e->ev_xrecv);
   for (auto &ev : e->ev_prop) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream_h2d);
   (void)hipStreamDestroy(e->stream2);
@@ -1428,6 +1451,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   if (!e || (n && !msgs)) return DRB_EINVAL;
   const View &v = e->v;
   std::lock_guard<std::mutex> lock(e->ingest_mu);
+  // replicas spread over ranks: not between a round and its exchange
+  if (v.remote_mask && e->exchanged_round != e->round) return DRB_EAGAIN;
   const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
   const uint32_t tag = (uint32_t)e->round;
   uint64_t acc = 0, drop = 0;
@@ -1528,8 +1553,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     }
   // 3. place every message in its plane, in order
   // [0] local arrays, [1] the inbound (remote) ones
-  std::vector<uint64_t> ridx[2], eidx[2], tridx[2], trval[2];
-  std::vector<uint4> rval[2], eval[2];
+  std::vector<uint64_t> ridx[2], eidx[2], tridx[2], trval[2], fwidx;
+  std::vector<uint4> rval[2], eval[2], fwval;
   std::vector<uint4> ch(ENT_META + v.C16);
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
@@ -1549,10 +1574,43 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     const int r = pl.remote ? 1 : 0;
     const uint32_t k = rep ? mi_nrep(cur.y)
                            : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (m.type == DRB_MSG_PROPOSE) {
+      // handleFollowerPropose's message from another NodeHost: its entries
+      // go to the sender's forward rows, one Propose per plane and round
+      // (a second one, or one the rows cannot hold, is dropped as by a full
+      // queue; so is any without forward rows, drb_config.forward_proposals)
+      bool fit = v.fwd_props && !pl.remote && !(cur.y & MI_PROP) &&
+                 m.n_entries <= v.max_props;
+      for (uint64_t x = 0; fit && x < m.n_entries; ++x)
+        fit = ents[m.entries_off + x].cmd_len <= v.C16 * 16;
+      if (!fit) {
+        drop++;
+        continue;
+      }
+      const uint32_t fw = fwd_ps(v, buf, pl.from);
+      for (uint64_t x = 0; x < m.n_entries; ++x) {
+        const drb_entry &en = ents[m.entries_off + x];
+        const uint8_t *cmd = pool + en.cmd_off;
+        std::vector<uint4> pc(PROP_META + v.C16, make_uint4(0, 0, 0, 0));
+        pc[0] = mk4h(en.key, en.client_id);
+        pc[1] = mk4h(en.series_id, en.responded_to);
+        pc[2] = make_uint4(en.type, en.cmd_len,
+                           prop_fast(en.type, en.client_id, en.series_id,
+                                     en.cmd_len, en.cmd_len ? cmd[0] : 0u),
+                           0);
+        if (en.cmd_len) memcpy(&pc[PROP_META], cmd, en.cmd_len);
+        for (uint32_t c = 0; c < PROP_META + v.C16; ++c) {
+          fwidx.push_back(prop_ix(v, fw, (uint32_t)x, c, pl.g));
+          fwval.push_back(pc[c]);
+        }
+      }
+    }
     if (rep && pl.remote) {
-      // entry rows [elo, elo + E): a Replicate outside them is dropped (the
-      // sender retries, as after any transport loss)
-      if (!pl.maxapp_valid) pl.elo = m.log_index + 1;
+      // entry rows [elo, elo + E), elo set by the round's first Replicate
+      // that carries entries (0: none yet; a commit-only Replicate needs no
+      // rows): a Replicate outside them is dropped (the sender retries, as
+      // after any transport loss)
+      if (m.n_entries && pl.elo == 0) pl.elo = m.log_index + 1;
       if (m.n_entries && (m.log_index + 1 < pl.elo ||
                           m.log_index + m.n_entries - pl.elo >= v.E)) {
         drop++;
@@ -1615,7 +1673,8 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
     ridx[r].push_back(mbox_ix(v, buf, pl.from, pl.to, k, 1, pl.g));
     rval[r].push_back(c1);
     const uint32_t inf =
-        msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0);
+        msg_info(m.type, zero, m.reject != 0, (uint32_t)m.n_entries) |
+        (other ? MI_TERM_OTHER : 0);
     cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
     if (rep) {
       const uint64_t ma = m.log_index + m.n_entries;
@@ -1654,6 +1713,7 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   std::vector<uint64_t> tv;
   if ((v.rterm && scatter(e, v.rterm, tridx[0], trval[0])) ||
       scatter(e, v.ring, eidx[0], eval[0]) ||
+      scatter(e, v.props, fwidx, fwval) ||
       scatter(e, v.mbox, ridx[0], rval[0]) ||
       scatter(e, v.mbox_meta, hidx[0], hval[0]) ||
       scatter(e, v.mbox_maxapp, xidx[0], xval[0]) ||
@@ -1751,7 +1811,7 @@ __global__ __launch_bounds__(256) void k_active_scan(const View v,
             (b & TAG_HEAVY))
           heavy = true;
       }
-      if (lead && stage_here(v, s, lead) && p.prop_slot != DRB_NONE &&
+      if (prop_here(v, p, s, lead) &&
           v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
         heavy = true;
     }
@@ -1854,14 +1914,18 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   pf.nrows = nf;
   // one-dimensional grids, rows interleaved per XCD (block_pos)
   const StepLaunchFn *launch = kStepLaunch[R - 1];
-  if (nl) launch[ext ? SK_LEAD_EXT : SK_LEAD](e->v, pl, gx * nl, e->stream);
+  // forwarded proposals: the EXT kernels with the Propose paths
+  const int kl = e->v.fwd_props ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
+  const int kf = e->v.fwd_props ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT
+                                                     : SK_FOLLOW;
+  if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
     k_serve_reads<<<dim3(gx, nl), 256, 0, e->stream2>>>(
         e->v, p0.n_reads, p0.key_space, pl.slots);
   }
-  if (nf) launch[ext ? SK_FOLLOW_EXT : SK_FOLLOW](e->v, pf, gx * nf, sf);
+  if (nf) launch[kf](e->v, pf, gx * nf, sf);
   if (split) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
@@ -1979,6 +2043,9 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.ri_replica = in->ri_replica;
   p.listed = in->listed ? 1 : 0;
   if (p.listed && e->v.remote_mask) return DRB_EINVAL;
+  p.prop_replica = in->prop_replica;
+  if (p.prop_replica > e->v.R || (p.prop_replica && !e->v.fwd_props))
+    return DRB_EINVAL;
   if (e->v.elections)  // this round's slow list
     HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
   if (p.ri_replica > e->v.R || (p.ri_replica && e->v.place_world > 1))
@@ -2339,6 +2406,35 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
       }
       *ne += ne_;
       *np += used;
+    } else if (m.type == DRB_MSG_PROPOSE && ne_) {
+      // the entries as proposed (no Term, no Index), from the sender's
+      // forward rows of this round
+      if (!v.fwd_props || ne_ > v.max_props) return DRB_EINVAL;
+      if (*ne + ne_ > ecap) return DRB_ERANGE;
+      const uint32_t chunks = PROP_META + v.C16, fw = fwd_ps(v, buf, from);
+      std::vector<uint64_t> pi;
+      for (uint64_t j = 0; j < ne_; ++j)
+        for (uint32_t c = 0; c < chunks; ++c)
+          pi.push_back(prop_ix(v, fw, (uint32_t)j, c, g));
+      std::vector<uint4> pv;
+      if (gather(e, v.props, pi, pv)) return DRB_EDEVICE;
+      for (uint64_t j = 0; j < ne_; ++j) {
+        const uint4 *q4 = &pv[j * chunks];
+        drb_entry &en = ents[*ne + j];
+        memset(&en, 0, sizeof(en));
+        en.key = lo64h(q4[0]);
+        en.client_id = hi64h(q4[0]);
+        en.series_id = lo64h(q4[1]);
+        en.responded_to = hi64h(q4[1]);
+        en.type = q4[2].x;
+        en.cmd_len = q4[2].y;
+        if (en.cmd_len > v.C16 * 16) return DRB_EINVAL;
+        if (*np + en.cmd_len > pcap) return DRB_ERANGE;
+        en.cmd_off = *np;
+        memcpy(pool + *np, &q4[PROP_META], en.cmd_len);
+        *np += en.cmd_len;
+      }
+      *ne += ne_;
     }
   }
   return DRB_OK;
@@ -2516,17 +2612,32 @@ extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
   return n;
 }
 
-extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
-  if (!engines || n == 0) return DRB_EINVAL;
+// every engine of one process at the same round, in placement order
+static int exchange_check(drb_engine *const *engines, uint32_t n) {
+  if (!engines || n == 0 || !engines[0]) return DRB_EINVAL;
   const uint32_t R = engines[0]->v.R;
-  std::vector<std::vector<uint32_t>> words(n, std::vector<uint32_t>(R * R));
   for (uint32_t r = 0; r < n; ++r) {
     const drb_engine *e = engines[r];
     if (!e || e->v.R != R || e->v.place_world != n || e->v.place_rank != r ||
         e->round != engines[0]->round || e->v.G != engines[0]->v.G)
       return DRB_EINVAL;
-    if (int rc = drb_plane_counts(engines[r], words[r].data())) return rc;
   }
+  return DRB_OK;
+}
+
+// the ingest locks of every engine, in rank order (drb_exchange_*: no
+// transport thread writes an inbound plane while the exchange runs)
+struct ExchangeLocks {
+  std::vector<std::unique_lock<std::mutex>> l;
+  ExchangeLocks(drb_engine *const *engines, uint32_t n) {
+    for (uint32_t r = 0; r < n; ++r) l.emplace_back(engines[r]->ingest_mu);
+  }
+};
+
+static int exchange_copy(drb_engine *const *engines, uint32_t n,
+                         const std::vector<std::vector<uint32_t>> &words,
+                         std::vector<uint32_t> *sent_to) {
+  const uint32_t R = engines[0]->v.R;
   for (uint32_t r = 0; r < n; ++r)
     for (uint32_t a = 0; a < R; ++a)
       for (uint32_t b = 0; b < R; ++b) {
@@ -2534,6 +2645,11 @@ extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
         const int peer = drb_plane_peer(engines[r], a, b, 0);
         if (peer < 0 || !w) continue;
         drb_engine *dst = engines[peer];
+        if (sent_to) {  // the receiver waits for this sender's round once
+          if (!(((*sent_to)[r] >> peer) & 1u))
+            HIPCHK(hipStreamWaitEvent(dst->stream, engines[r]->ev_xsend, 0));
+          (*sent_to)[r] |= 1u << peer;
+        }
         drb_region src[DRB_PLANE_REGIONS], dreg[DRB_PLANE_REGIONS];
         const int ns = drb_plane_regions(engines[r], a, b, w, 0, src);
         const int nd = drb_plane_regions(dst, a, b, w, 1, dreg);
@@ -2542,7 +2658,75 @@ extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
           HIPCHK(hipMemcpyAsync(dreg[q].ptr, src[q].ptr, src[q].bytes,
                                 hipMemcpyDefault, dst->stream));
       }
+  return DRB_OK;
+}
+
+// the summary word of a plane at full capacity (drb_plane_regions): every
+// record position, both chunks, the header; for a sender slot that may
+// hold leaders the max-append word and every entry row too; with
+// elections the rterm rows (dragonboat_amd/exchange.py full_word)
+static uint32_t full_word(const View &v, bool leader_sender) {
+  const uint32_t f = DRB_PLANE_C1 | DRB_PLANE_HDR;
+  if (leader_sender || v.elections)
+    return (v.MB & 0x1fu) | ((v.E & 0xffu) << 10) | f |
+           (v.elections ? DRB_PLANE_TOTHER : 0u);
+  return ((v.MB & 0x1fu) << 5) | f;
+}
+
+extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
+  if (int rc = exchange_check(engines, n)) return rc;
+  const View &v = engines[0]->v;
+  const uint32_t R = v.R;
+  ExchangeLocks locks(engines, n);
+  // plane (a, b) can carry fast-path messages when a or b holds a leader on
+  // some engine (followers send only to leaders); every plane when roles
+  // change on the device
+  uint32_t lead = 0;
+  for (uint32_t r = 0; r < n; ++r) lead |= engines[r]->role_slots[0];
+  std::vector<uint32_t> row(R * R, 0);
+  for (uint32_t a = 0; a < R; ++a)
+    for (uint32_t b = 0; b < R; ++b)
+      if (a != b && (((lead >> a) | (lead >> b)) & 1u || v.elections))
+        row[a * R + b] = full_word(v, (lead >> a) & 1u);
+  std::vector<std::vector<uint32_t>> words(n, row);
+  if (engines[0]->round == 0) return DRB_OK;
+  for (uint32_t r = 0; r < n; ++r)
+    HIPCHK(hipEventRecord(engines[r]->ev_xsend, engines[r]->stream));
+  std::vector<uint32_t> sent_to(n, 0);
+  if (int rc = exchange_copy(engines, n, words, &sent_to)) return rc;
+  for (uint32_t d = 0; d < n; ++d)
+    HIPCHK(hipEventRecord(engines[d]->ev_xrecv, engines[d]->stream));
+  // a sender's next round overwrites the other outbox buffer, the one
+  // after it this one: its stream waits for the copies that read it
+  for (uint32_t r = 0; r < n; ++r)
+    for (uint32_t d = 0; d < n; ++d)
+      if ((sent_to[r] >> d) & 1u)
+        HIPCHK(hipStreamWaitEvent(engines[r]->stream, engines[d]->ev_xrecv,
+                                  0));
+  for (uint32_t r = 0; r < n; ++r)
+    engines[r]->exchanged_round = engines[r]->round;
+  return DRB_OK;
+}
+
+extern "C" int drb_exchange_local_counted(drb_engine *const *engines,
+                                          uint32_t n) {
+  if (int rc = exchange_check(engines, n)) return rc;
+  const uint32_t R = engines[0]->v.R;
+  ExchangeLocks locks(engines, n);
+  std::vector<std::vector<uint32_t>> words(n, std::vector<uint32_t>(R * R));
+  for (uint32_t r = 0; r < n; ++r)
+    if (int rc = drb_plane_counts(engines[r], words[r].data())) return rc;
+  if (int rc = exchange_copy(engines, n, words, nullptr)) return rc;
   for (uint32_t r = 0; r < n; ++r) HIPCHK(hipStreamSynchronize(engines[r]->stream));
+  for (uint32_t r = 0; r < n; ++r)
+    engines[r]->exchanged_round = engines[r]->round;
+  return DRB_OK;
+}
+
+extern "C" int drb_exchange_mark(drb_engine *e) {
+  if (!e) return DRB_EINVAL;
+  std::lock_guard<std::mutex> lock(e->ingest_mu);
+  e->exchanged_round = e->round;
   return DRB_OK;
 }
 
@@ -3339,3 +3523,6 @@ extern "C" int drb_export_read_results(drb_engine *e, uint32_t slot,
   return batch_export(e, slot, first_group, n_groups, BK_READS, out,
                       sizeof(drb_read_result), cap, n_out);
 }
+
+// ---------------------------------------------------------------- worker
+#include "drb_worker.hpp"

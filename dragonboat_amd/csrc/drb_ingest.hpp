@@ -259,12 +259,13 @@ __global__ __launch_bounds__(256) void k_crc_chunks(const uint8_t *data,
   if (threadIdx.x == 0) fraw[b] = red[0] ^ red[1] ^ red[2] ^ red[3];
 }
 
-// pass 1: entry counts and errors; the frame of a malformed message is
-// marked (the host stops the stream there)
+// pass 1: entry counts and errors, and the record of every message (the
+// decode pass parses again only the messages with entries); the frame of a
+// malformed message is marked (the host stops the stream there)
 __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
                             const uint32_t *mlen, const uint32_t *mframe,
                             uint32_t *n_ent, uint32_t *err,
-                            uint32_t *frame_bad, uint64_t n,
+                            uint32_t *frame_bad, DecMsg *out, uint64_t n,
                             uint32_t cmd_cap) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -274,6 +275,9 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   if (r == ING_OK && big) r = ING_BIG;
   n_ent[i] = r == ING_OK ? m.n_ent : 0;
   err[i] = r;
+  m.err = r;
+  m.ent0 = 0;
+  out[i] = m;
   if (r == ING_BAD) atomicOr(&frame_bad[mframe[i]], 1u);
   if (r == ING_BIG) atomicOr(&frame_bad[mframe[i]], 2u);
 }
@@ -365,22 +369,25 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
               part[threadIdx.x]);
 }
 
-// pass 2: the records and entries of the messages to deliver
+// pass 2: the entries of the messages to deliver (their records are pass
+// 1's); a message not delivered is marked so that it sorts last
 __global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
                              const uint32_t *mlen, const uint32_t *ent0,
-                             const uint8_t *deliver, DecMsg *out,
-                             drb_entry *ents, uint64_t n, uint32_t cmd_cap) {
+                             const uint32_t *n_ent, const uint8_t *deliver,
+                             DecMsg *out, drb_entry *ents, uint64_t n,
+                             uint32_t cmd_cap) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  DecMsg m;
-  m.err = ING_BAD;
-  m.ent0 = ent0[i];
-  if (deliver[i]) {
-    bool big = false;
-    m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
-                      cmd_cap, big);
-    m.ent0 = ent0[i];
+  if (!deliver[i]) {
+    out[i].err = ING_BAD;
+    return;
   }
+  if (n_ent[i] == 0) return;  // pass 1's record is complete
+  DecMsg m;
+  bool big = false;
+  m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
+                    cmd_cap, big);
+  m.ent0 = ent0[i];
   out[i] = m;
 }
 
@@ -443,7 +450,7 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
   }
   bool maxapp_valid = mi_nrep(cur.y) > 0;
   // remote planes: the first entry index of the plane's entry rows (set by
-  // the round's first Replicate placed here)
+  // the round's first Replicate with entries placed here; 0: none yet)
   uint64_t elo = maxapp_valid && rm ? v.elo_in[mmeta_ix(v, buf, from, to, g)]
                                     : 0;
   uint64_t acc = 0, drop = 0;
@@ -461,10 +468,47 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
     const bool rep = m.type == DRB_MSG_REPLICATE;
     const uint32_t kk =
         rep ? mi_nrep(cur.y) : rec_pos(false, mi_noth(cur.y), v.MB);
+    if (m.type == DRB_MSG_PROPOSE) {
+      // handleFollowerPropose's message from another NodeHost: its entries
+      // go to the sender's forward rows, one Propose per plane and round
+      // (a second one, or one the rows cannot hold, is dropped as by a full
+      // queue; so is any without forward rows, drb_config.forward_proposals)
+      bool fit = v.fwd_props && !rm && !(cur.y & MI_PROP) &&
+                 m.n_ent <= v.max_props;
+      for (uint32_t x = 0; fit && x < m.n_ent; ++x)
+        fit = ents[m.ent0 + x].cmd_len <= v.C16 * 16;
+      if (!fit) {
+        drop++;
+        continue;
+      }
+      const uint32_t fw = fwd_ps(v, buf, from);
+      for (uint32_t x = 0; x < m.n_ent; ++x) {
+        const drb_entry en = ents[m.ent0 + x];
+        const uint32_t b0 = en.cmd_len ? s[en.cmd_off] : 0u;
+        v.props[prop_ix(v, fw, x, 0, g)] = make_uint4(
+            (uint32_t)en.key, (uint32_t)(en.key >> 32), (uint32_t)en.client_id,
+            (uint32_t)(en.client_id >> 32));
+        v.props[prop_ix(v, fw, x, 1, g)] = make_uint4(
+            (uint32_t)en.series_id, (uint32_t)(en.series_id >> 32),
+            (uint32_t)en.responded_to, (uint32_t)(en.responded_to >> 32));
+        v.props[prop_ix(v, fw, x, 2, g)] = make_uint4(
+            en.type, en.cmd_len,
+            prop_fast(en.type, en.client_id, en.series_id, en.cmd_len, b0), 0);
+        for (uint32_t cc = 0; cc < v.C16; ++cc) {
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (uint32_t b = 0; b < 16 && cc * 16 + b < en.cmd_len; ++b)
+            w[b >> 2] |= (uint32_t)s[en.cmd_off + cc * 16 + b] << (8 * (b & 3));
+          v.props[prop_ix(v, fw, x, PROP_META + cc, g)] =
+              make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    }
     if (rep && rm) {
-      // entry rows [elo, elo + E): a Replicate outside them is dropped (the
-      // sender retries, as after any transport loss)
-      if (!maxapp_valid) elo = m.log_index + 1;
+      // entry rows [elo, elo + E), elo set by the round's first Replicate
+      // that carries entries (0: none yet; a commit-only Replicate needs no
+      // rows): a Replicate outside them is dropped (the sender retries, as
+      // after any transport loss)
+      if (m.n_ent && elo == 0) elo = m.log_index + 1;
       if (m.n_ent && (m.log_index + 1 < elo ||
                       m.log_index + m.n_ent - elo >= v.E)) {
         drop++;
@@ -538,8 +582,8 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
     }
     mbox[mbox_ix(v, buf, from, to, kk, 0, g)] = c0;
     mbox[mbox_ix(v, buf, from, to, kk, 1, g)] = c1;
-    const uint32_t inf =
-        msg_info(m.type, zero, m.reject != 0) | (other ? MI_TERM_OTHER : 0u);
+    const uint32_t inf = msg_info(m.type, zero, m.reject != 0, m.n_ent) |
+                         (other ? MI_TERM_OTHER : 0u);
     cur.y = (cur.y + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
     if (rep) {
       const uint64_t ma = m.log_index + m.n_ent;
@@ -804,6 +848,9 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (!e || (!stream && len)) return DRB_EINVAL;
   wirehost::crc_init();
   std::lock_guard<std::mutex> lock(e->ingest_mu);
+  // replicas spread over ranks: not between a round and its exchange
+  // (drb_exchange_mark, include/drb_engine.h)
+  if (e->v.remote_mask && e->exchanged_round != e->round) return DRB_EAGAIN;
   if (!e->ingest) e->ingest = new IngestState();
   IngestState &st = *e->ingest;
   const View &v = e->v;
@@ -1001,8 +1048,10 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                             d_scan, (int)nm, sm));
     k_ing_elems<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
         ds, d_scan, d_mbase, d_foff, d_mframe, d_moff, d_mlen, nm);
+    if (ing_grow(st.msgs, al256(nm * sizeof(DecMsg)))) return DRB_EDEVICE;
     k_ing_count<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-        ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad, nm, cmd_cap);
+        ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad,
+        (DecMsg *)st.msgs.p, nm, cmd_cap);
     HIPCHK(hipGetLastError());
   }
   std::vector<uint32_t> ccrc(nc), fbad(fr.size() + 1);
@@ -1081,12 +1130,11 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     const uint64_t tot = c0[5];
     if (any_deliver) {
       const size_t eb = al256((tot ? tot : 1) * sizeof(drb_entry));
-      if (ing_grow(st.ents, eb) || ing_grow(st.msgs, al256(nm * sizeof(DecMsg))))
-        return DRB_EDEVICE;
+      if (ing_grow(st.ents, eb)) return DRB_EDEVICE;
       DecMsg *dm = (DecMsg *)st.msgs.p;
       drb_entry *de = (drb_entry *)st.ents.p;
       k_ing_decode<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-          ds, d_moff, d_mlen, d_ent0, d_deliver, dm, de, nm, cmd_cap);
+          ds, d_moff, d_mlen, d_ent0, d_nent, d_deliver, dm, de, nm, cmd_cap);
       HIPCHK(hipGetLastError());
       tr.mark("decode");
       // 5. planes: keys, a stable radix sort, one lane per plane

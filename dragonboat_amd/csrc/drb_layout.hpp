@@ -334,8 +334,13 @@ struct View {
   // DRB_PHASE_PROF step builds: [2 roles][8] cycle sums per round phase
   // (drb_debug_phase; allocated when DRB_PHASE=1 at drb_engine_create)
   unsigned long long *phase;
-  uint4 *props;           // [P][max_props][PROP_META + C16][G]
+  uint4 *props;           // [P (+ 2R)][max_props][PROP_META + C16][G]
   uint32_t *prop_count;   // [P][G]
+  // drb_config.forward_proposals: a Propose's entries travel by value in
+  // proposal batch fwd_ps(buf, sender) = P + buf * R + sender, after the P
+  // staged ones
+  uint32_t fwd_props;
+  uint32_t P;
   uint4 *ri_in;           // [RS][G] {low, high}
   uint4 *rtr;             // [R][RTR_CAP][G] x 2 chunks {index, low},{high,0}
   uint32_t *rtr_count;    // [R][G]
@@ -542,6 +547,10 @@ __host__ __device__ inline uint64_t prop_ix(const View &v, uint32_t ps,
                                             uint64_t g) {
   return (((uint64_t)ps * v.max_props + j) * (PROP_META + v.C16) + chunk) *
              v.G + g;
+}
+__host__ __device__ inline uint32_t fwd_ps(const View &v, uint32_t buf,
+                                           uint32_t sender) {
+  return v.P + buf * v.R + sender;
 }
 __host__ __device__ inline uint64_t rres_ix(const View &v, uint32_t slot,
                                             uint32_t k, uint32_t j,

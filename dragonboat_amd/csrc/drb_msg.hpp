@@ -65,6 +65,15 @@ constexpr uint32_t MI_OFF_FOLLOWER = 1u << 22;  // the fast path for / a
 constexpr uint32_t MI_TERM = 1u << 23;        // a record carries the term
 constexpr uint32_t MI_TERM_OTHER = 1u << 24;  // a record's term != header's
 constexpr uint32_t MI_REJECT = 1u << 25;  // a rejecting ReplicateResp
+// a Propose record (drb_config.forward_proposals: at most one per plane and
+// round), and its entry count [27:31]: the entries travel by value in the
+// sender's forward batch (View.fwd_props, prop_ix)
+constexpr uint32_t MI_PROP = 1u << 26;
+constexpr int MI_NPROP = 27;
+__host__ __device__ inline uint32_t mi_nprop(uint32_t w) {
+  return (w >> MI_NPROP) & 0xfu;
+}
+constexpr uint32_t MAX_FWD_PROPS = 15;
 constexpr uint32_t MB_MAX = 24;  // records per (sender, receiver, round)
 __host__ __device__ inline uint32_t mi_nrep(uint32_t w) { return w & MI_NREP; }
 __host__ __device__ inline uint32_t mi_noth(uint32_t w) {
@@ -95,7 +104,8 @@ __host__ __device__ inline bool tag_is(uint32_t word, uint64_t round) {
 // the dense "heavy" part of its list (drb_engine.hip, k_active_scan)
 constexpr uint32_t TAG_HEAVY = 0x80u;
 __host__ __device__ inline uint8_t tag_byte(uint64_t round, uint32_t info) {
-  const bool heavy = mi_nrep(info) != 0 || ((info >> MI_NRR) & 0x1fu) != 0;
+  const bool heavy = mi_nrep(info) != 0 || ((info >> MI_NRR) & 0x1fu) != 0 ||
+                     (info & MI_PROP);
   return (uint8_t)((round & 0x7fu) | (heavy ? TAG_HEAVY : 0u));
 }
 __host__ __device__ inline bool tag_current(uint32_t byte, uint64_t round) {
@@ -143,18 +153,21 @@ __host__ __device__ inline bool is_ctx_type(uint32_t t) {
          t == DRB_MSG_READ_INDEX || t == DRB_MSG_READ_INDEX_RESP;
 }
 
-// header info contribution of one record
+// header info contribution of one record (n: a Propose's entries)
 __host__ __device__ inline uint32_t msg_info(uint32_t type, bool term_zero,
-                                             bool reject = false) {
+                                             bool reject = false,
+                                             uint32_t n = 0) {
   uint32_t i = type == DRB_MSG_REPLICATE ? 1u : 1u << MI_NOTH;  // counts
   if (reject && type == DRB_MSG_REPLICATE_RESP) i |= MI_REJECT;
+  if (type == DRB_MSG_PROPOSE)
+    i |= MI_PROP | ((n < MAX_FWD_PROPS ? n : MAX_FWD_PROPS) << MI_NPROP);
   if (type == DRB_MSG_READ_INDEX) i += 1u << MI_NRI;
   if (type == DRB_MSG_REPLICATE_RESP) i += 1u << MI_NRR;
   if (type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP)
     i |= MI_RESP;
   if (!(type == DRB_MSG_REPLICATE_RESP || type == DRB_MSG_HEARTBEAT_RESP ||
-        type == DRB_MSG_READ_INDEX))
-    i |= MI_OFF_LEADER;
+        type == DRB_MSG_READ_INDEX || type == DRB_MSG_PROPOSE))
+    i |= MI_OFF_LEADER;  // (a Propose without forward rows: the pre-pass)
   if (!(type == DRB_MSG_REPLICATE || type == DRB_MSG_HEARTBEAT ||
         type == DRB_MSG_READ_INDEX_RESP))
     i |= MI_OFF_FOLLOWER;
@@ -245,6 +258,12 @@ __host__ __device__ inline bool msg_encode(const Msg &m, uint32_t dest,
     case DRB_MSG_REQUEST_VOTE_RESP:
     case DRB_MSG_REQUEST_PREVOTE_RESP:
     case DRB_MSG_NOOP:
+      break;
+    case DRB_MSG_PROPOSE:  // {Type, From, Entries} (peer.go:118-124)
+      a = m.log_index;
+      b = m.hint;
+      c = m.hint_high;
+      has = (b | c) != 0;
       break;
     default:
       a = m.log_index;

@@ -77,8 +77,8 @@ namespace drb {
 #ifndef DRB_FPF
 #define DRB_FPF 8
 #endif
-// the leader's: the first DRB_LPF records of each of its first two senders
-// with records (LDS: 2 x DRB_LPF x 4 KB a workgroup; 0: off)
+// the leader's: the first DRB_LPF records of its first sender with records
+// (LDS: DRB_LPF x 4 KB a workgroup; 0: off, measured neutral, profiles/r03_lpf)
 #ifndef DRB_LPF
 #define DRB_LPF 0
 #endif
@@ -154,6 +154,7 @@ struct Rep {
   uint32_t c1mask;     // destinations that got a record with a c1 chunk
   uint32_t nrtr;
   uint32_t ndropped_ri;
+  uint32_t ndropped_props;  // reportDroppedProposal (entries)
   uint64_t guard_new;
   bool leader_update;
   bool oterm;  // raft launch: a record went out with a term not r.term
@@ -424,7 +425,7 @@ DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   if (mm.term != r.term && mm.term != 0) r.oterm = true;
   uint4 c0, c1;
   const bool has = msg_encode(mm, to_slot, &r.hc, c0, c1);
-  const uint32_t inf = msg_info(mm.type, mm.term == 0, m.reject != 0);
+  const uint32_t inf = msg_info(mm.type, mm.term == 0, m.reject != 0, m.n);
   w = (w + (inf & MI_CNTS)) | (inf & ~MI_CNTS);
   v.mbox[mbox_ix(v, L.wbuf, L.slot, to_slot, k, 0, L.g)] = c0;
   // the raft launch may change its term after this record: keep the
@@ -766,9 +767,12 @@ DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
 
 // ------------------------------------------------------------ handlers
 // handleLeaderReplicateResp (raft.go:1878-1908), via lw (2309-2323)
-template <int R>
+// BC = false: a commit advance is returned in *bc for the caller's
+// broadcast (the last thing the handler does), so one broadcast site
+// serves it and handleLeaderPropose (dispatch)
+template <int R, bool BC = true>
 DRB_DEV bool leader_replicate_resp(const Lane &L, Rep<R> &r, int s,
-                                   const Msg &m) {
+                                   const Msg &m, bool *bc = nullptr) {
   RemoteV x = rem_get<R>(L, s);
   x.a = 1;  // setActive
   bool upd = false;
@@ -781,10 +785,14 @@ DRB_DEV bool leader_replicate_resp(const Lane &L, Rep<R> &r, int s,
     }
     rem_put<R>(L, s, x);
     if (upd) {
-      if (try_commit(L, r))
-        broadcast_replicate(L, r);
-      else if (paused)
+      if (try_commit(L, r)) {
+        if (BC)
+          broadcast_replicate(L, r);
+        else
+          *bc = true;
+      } else if (paused) {
         send_replicate(L, r, s);
+      }
     }
   } else {
     // decreaseTo (remote.go:182-198)
@@ -842,6 +850,51 @@ DRB_DEV void leader_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
   } else {
     add_ready(L, r, r.committed, lo, hi);
   }
+}
+
+// handleLeaderPropose (raft.go:1794-1815) -> appendEntries (:944-955): the
+// n entries of proposal batch ps (staged, or a Propose's forward rows) at
+// last + 1.., Term = r.term; the caller then broadcastReplicateMessage
+template <int R>
+DRB_DEV void append_props(const Lane &L, Rep<R> &r, uint32_t ps, uint32_t n) {
+  const View &v = *L.v;
+  const uint32_t chunks = PROP_META + v.C16;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t idx = r.last + 1 + j;
+    const uint4 p0 = v.props[prop_ix(v, ps, j, 0, L.g)];
+    const uint4 p1 = v.props[prop_ix(v, ps, j, 1, L.g)];
+    const uint4 p2 = v.props[prop_ix(v, ps, j, 2, L.g)];
+    v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = mk4(r.term, lo64(p0));
+    v.ring[ring_ix(v, L.slot, idx, 1, L.g)] = mk4(hi64(p0), lo64(p1));
+    v.ring[ring_ix(v, L.slot, idx, 2, L.g)] = make_uint4(p1.z, p1.w, p2.x, p2.y);
+    for (uint32_t c = PROP_META; c < chunks; ++c)
+      v.ring[ring_ix(v, L.slot, idx, c, L.g)] = v.props[prop_ix(v, ps, j, c, L.g)];
+  }
+  r.last += n;
+  if (r.last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, r.last + 1 - v.W);
+  rem_try_update<R>(L, (int)L.slot, r.last);  // self remote
+  if (R == 1) try_commit(L, r);
+}
+
+// handleFollowerPropose (raft.go:2103-2116): the entry queue goes to the
+// leader as a Propose (From = self, Term 0: a request type) carrying the
+// entries by value in this replica's forward rows; dropped without a leader
+template <int R>
+DRB_DEV void forward_props(const Lane &L, Rep<R> &r, uint32_t ps, uint32_t n) {
+  const View &v = *L.v;
+  if (r.leader_id == 0 || r.leader_id > (uint64_t)R) {
+    r.ndropped_props += n;  // reportDroppedProposal
+    return;
+  }
+  const uint32_t chunks = PROP_META + v.C16;
+  const uint32_t fw = fwd_ps(v, L.wbuf, L.slot);
+  for (uint32_t j = 0; j < n; ++j)
+    for (uint32_t c = 0; c < chunks; ++c)
+      v.props[prop_ix(v, fw, j, c, L.g)] = v.props[prop_ix(v, ps, j, c, L.g)];
+  Msg m = {};
+  m.type = DRB_MSG_PROPOSE;
+  m.n = n;
+  emit(L, r, (uint32_t)(r.leader_id - 1), m);
 }
 
 // Where the entries of a Replicate from sender slot s are read: the
@@ -986,16 +1039,24 @@ DRB_DEV void follower_read_index_resp(const Lane &L, Rep<R> &r, int s,
   add_ready(L, r, m.log_index, m.hint, m.hint_high);
 }
 
-template <int R>
+// FWD: the instantiation carries forwarded proposals (EXT; an engine with
+// drb_config.forward_proposals runs it, drb_engine.hip launch_step)
+template <int R, bool FWD = true>
 DRB_DEV void dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
                       const EntSrc &src) {
   if (r.role == DRB_LEADER) {
-    if (m.type == DRB_MSG_REPLICATE_RESP)
-      leader_replicate_resp(L, r, s, m);
-    else if (m.type == DRB_MSG_HEARTBEAT_RESP)
+    bool bc = false;
+    if (m.type == DRB_MSG_REPLICATE_RESP) {
+      leader_replicate_resp<R, false>(L, r, s, m, &bc);
+    } else if (m.type == DRB_MSG_HEARTBEAT_RESP) {
       leader_heartbeat_resp(L, r, s, m);
-    else if (m.type == DRB_MSG_READ_INDEX)
+    } else if (m.type == DRB_MSG_READ_INDEX) {
       leader_read_index(L, r, m.hint, m.hint_high, (uint64_t)s + 1);
+    } else if (FWD && m.type == DRB_MSG_PROPOSE) {  // handleLeaderPropose
+      append_props(L, r, fwd_ps(*L.v, L.rbuf, (uint32_t)s), m.n);
+      bc = true;
+    }
+    if (bc) broadcast_replicate(L, r);
   } else {
     if (m.type == DRB_MSG_REPLICATE)
       follower_replicate(L, r, s, m, src);
@@ -1315,6 +1376,8 @@ DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
       el_request_vote(L, r, s, m);
     } else if (t == DRB_MSG_LEADER_TRANSFER) {
       el_leader_transfer(L, r, m.hint);
+    } else if (t == DRB_MSG_PROPOSE && (r.flags & F_XFER)) {
+      r.ndropped_props += m.n;  // leaderTransfering (raft.go:1796-1800)
     } else if (t == DRB_MSG_REPLICATE_RESP) {
       // the transfer target caught up: TimeoutNow (raft.go:1890-1895)
       if (leader_replicate_resp(L, r, s, m) &&
@@ -1348,6 +1411,8 @@ DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
       el_request_vote(L, r, s, m);
     } else if (t == DRB_MSG_READ_INDEX) {  // handleCandidateReadIndex
       r.ndropped_ri++;
+    } else if (t == DRB_MSG_PROPOSE) {  // handleCandidatePropose (2197)
+      r.ndropped_props += m.n;
     }
   }
 }
@@ -2094,6 +2159,7 @@ struct RoundParams {
   uint64_t tick_no;  // engine ticks so far, this round's included
   uint32_t ri_replica;  // staged ReadIndex at: 0 the leader, else ID
   uint32_t listed;      // 1: step the active list (k_active_*), see below
+  uint32_t prop_replica;  // staged proposals at: 0 the leader, else ID
 };
 
 // Whether this replica takes the lane's staged proposals / ReadIndex
@@ -2107,6 +2173,14 @@ DRB_DEV bool ri_here(const View &v, const RoundParams &p, uint32_t slot,
   if (p.ri_slot == DRB_NONE) return false;
   return p.ri_replica == 0 ? stage_here(v, slot, lead)
                            : slot + 1 == p.ri_replica;
+}
+// the staged proposals: the leader's, or replica prop_replica's (whose
+// NodeHost's entry queue they are; a follower forwards them)
+DRB_DEV bool prop_here(const View &v, const RoundParams &p, uint32_t slot,
+                       bool lead) {
+  if (p.prop_slot == DRB_NONE) return false;
+  return p.prop_replica == 0 ? stage_here(v, slot, lead)
+                             : slot + 1 == p.prop_replica;
 }
 
 // Idle rounds: a replica at rest -- its last round left
@@ -2132,7 +2206,7 @@ DRB_DEV bool idle_round(const View &v, const RoundParams &p, uint32_t slot,
     if ((uint32_t)s != slot &&
         tag_current((uint32_t)(tags >> (8 * s)) & 0xffu, p.round - 1))
       return false;
-  if (stage_here(v, slot, lead) && p.prop_slot != DRB_NONE &&
+  if (prop_here(v, p, slot, lead) &&
       v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
     return false;
   if (ri_here(v, p, slot, lead) &&
@@ -2253,7 +2327,9 @@ DRB_DEV void block_plane_summary(const View &v, BlockPos bp, uint32_t from,
 // SLOW: the raft launch of an elections engine (LEAD = EXT = true): it
 // steps the replicas on the slow list (F_SLOW) with the election state
 // machine (el_*, above) as well, whatever their role.
-template <int R, bool LEAD, bool EXT, bool SLOW = false>
+// FWD: forwarded proposals (drb_config.forward_proposals; an EXT
+// instantiation of its own, so C5's EXT kernels keep their registers)
+template <int R, bool LEAD, bool EXT, bool SLOW = false, bool FWD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_SLOW_WAVES : LEAD ? (EXT ? DRB_EXT_LEAD_WAVES : DRB_LEAD_WAVES) : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
@@ -2292,10 +2368,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[EXT ? 256 : 1];
   __shared__ uint64_t rq_lds[LEAD ? 2 * DRB_RI_DEPTH : 1][256];
-  // inbox prefetch (LDS-DMA): PFS senders x PFN records
+  // inbox prefetch (LDS-DMA): PFS senders x PFN records.  One sender row:
+  // the LDS destination of global_load_lds goes through M0 and must be
+  // wave-uniform, and the row a lane's first sender with records lands in
+  // is uniform only while there is one row (the first such sender differs
+  // between lanes)
   constexpr int PFN = SLOW ? 0 : LEAD ? DRB_LPF : DRB_FPF;
   constexpr bool FPF = PFN > 0;
-  constexpr int PFS = LEAD ? 2 : 1;
+  constexpr int PFS = 1;
   __shared__ uint4 pf_lds[FPF ? PFS : 1][FPF ? PFN : 1][FPF ? 256 : 1];
   constexpr int NPH = (DRB_PHASE_PROF && !SLOW) ? 8 : 1;
   __shared__ uint32_t ph_lds[NPH][NPH > 1 ? 256 : 1];
@@ -2387,6 +2467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     r.nmsgs = 0;
     r.nrtr = 0;
     r.ndropped_ri = 0;
+    r.ndropped_props = 0;
     r.guard_new = ~0ull;
     r.leader_update = false;
     r.oterm = false;
@@ -2430,6 +2511,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     uint32_t qz_from = 0;   // senders whose Quiesce message arrived
     uint64_t nri_packed = 0;  // 5-bit ReadIndex record count per sender
     uint64_t max_app = 0;
+    uint32_t prop_from = 0;     // senders with a Propose (MI_PROP)
+    uint64_t nprop_packed = 0;  // 4-bit forwarded entry count per sender
+    uint32_t n_fwd = 0;         // ... and their sum
     int pf_s[2] = {-1, -1};    // the senders whose records are in pf_lds
     uint32_t pf_nrp[2] = {0, 0};  // ... and their Replicate counts
 #pragma unroll
@@ -2460,7 +2544,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                 t == DRB_MSG_REQUEST_VOTE || t == DRB_MSG_REQUEST_VOTE_RESP ||
                 t == DRB_MSG_NOOP || t == DRB_MSG_LEADER_TRANSFER ||
                 t == DRB_MSG_TIMEOUT_NOW ||
-                (v.pre_vote && is_prevote_type(t));
+                (v.pre_vote && is_prevote_type(t)) ||
+                (v.fwd_props && t == DRB_MSG_PROPOSE);
             if (!ok && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
             n_lt += t == DRB_MSG_LEADER_TRANSFER;
           }
@@ -2506,6 +2591,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       nri_packed |= (uint64_t)((info >> MI_NRI) & 0x1fu) << (5 * s);
       n_rr += (info >> MI_NRR) & 0x1fu;
       if (info & MI_RESP) resp_from |= 1u << s;
+      if (info & MI_PROP) {
+        prop_from |= 1u << s;
+        if (FWD) {
+          nprop_packed |= (uint64_t)mi_nprop(info) << (4 * s);
+          n_fwd += mi_nprop(info);
+        }
+      }
       if (info & MI_REJECT) rej_from |= 1u << s;
       if (!is_leader && mi_nrep(info))
         max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
@@ -2532,7 +2624,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       }
       total_in += ns;
     }
-    uint32_t nprops = 0;
+    uint32_t nprops = 0;   // staged proposals this replica takes
+    uint32_t nappend = 0;  // leader: entries the round may append
     uint64_t in_lo = 0, in_hi = 0;
     // lowest index the round may still read: apply cursor, commit term,
     // applied-to term
@@ -2545,13 +2638,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       in_lo = lo64(c);
       in_hi = hi64(c);
     }
+    if ((FWD || is_leader) && prop_here(v, p, slot, is_leader))
+      nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
     if (is_leader) {
-      if (p.prop_slot != DRB_NONE && stage_here(v, slot, is_leader))
-        nprops = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
       // with elections a group can hold two leaders (a stale one and the
       // new one): its entry queue goes to the hosted leader in the highest
       // slot (the NodeHost the client reaches; tests/gpu_harness.py)
-      if (v.elections && nprops && v.place_world <= 1) {
+      if (v.elections && nprops && v.place_world <= 1 && !p.prop_replica) {
 #pragma unroll
         for (int s = 0; s < R; ++s)
           if ((uint32_t)s > slot &&
@@ -2570,6 +2663,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         if (!p2.z && fb == DRB_FB_NONE) fb = DRB_FB_ENTRY_TYPE;
         if (p2.y > v.C16 * 16 && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
       }
+      // the Proposes of the inbox (handleLeaderPropose): their entries in
+      // the senders' forward rows, checked as staged ones are
+      if (prop_from) {
+        if ((!FWD || !v.fwd_props) && fb == DRB_FB_NONE)
+          fb = DRB_FB_MESSAGE_TYPE;
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          const uint32_t ns = (uint32_t)(nprop_packed >> (4 * s)) & 0xfu;
+          for (uint32_t j = 0; FWD && v.fwd_props && j < ns; ++j) {
+            const uint4 p2 = v.props[prop_ix(v, fwd_ps(v, L.rbuf, (uint32_t)s),
+                                             j, 2, g)];
+            if (!p2.z && fb == DRB_FB_NONE) fb = DRB_FB_ENTRY_TYPE;
+            if (p2.y > v.C16 * 16 && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
+          }
+        }
+      }
+      nappend = nprops + n_fwd;
       // The window: the lowest index a Replicate of this round may read
       // for remote s is next - 1 (its LogTerm), or match - 1 after a
       // rejection lowers next (decreaseTo / enterRetryState, remote.go:
@@ -2608,7 +2718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         if ((ents_below || term_below) && fb == DRB_FB_NONE)
           fb = DRB_FB_CAPACITY;
       }
-      if (nprops && r.last + nprops >= keep + v.W && fb == DRB_FB_NONE)
+      if (nappend && r.last + nappend >= keep + v.W && fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
       // entry rows of a remote follower's plane: the round sends it
       // entries [floor, new last], floor = its next, or above its match
@@ -2627,7 +2737,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                 lowers ? resp_floor<R>(L, x, s,
                                        (uint32_t)((nin_packed >> (5 * s)) & 31u))
                        : x.n;
-            if (r.last + nprops + 1 > floor + v.E && fb == DRB_FB_NONE)
+            if (r.last + nappend + 1 > floor + v.E && fb == DRB_FB_NONE)
               fb = DRB_FB_CAPACITY;
           }
       }
@@ -2641,7 +2751,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         uint64_t adv = r.last > r.committed ? r.last - r.committed : 0;
         uint32_t nb = (uint32_t)umin64((uint64_t)n_rr, adv);
         uint32_t base = (in_lo != 0) + (p.tick ? 1 : 0) + (nprops ? 1 : 0) +
-                        n_ri_msgs * 2 + r.ri_count + nb + (SLOW ? 1 : 0);
+                        __builtin_popcount(prop_from) + n_ri_msgs * 2 +
+                        r.ri_count + nb + (SLOW ? 1 : 0);
 #pragma unroll
         for (int s = 0; s < R; ++s) {
           if ((uint32_t)s == slot) continue;
@@ -2680,18 +2791,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       // (handleFollowerPropose, raft.go:2103-2116): the CPU path's.  One
       // that steps down for a vote, a NoOP or CheckQuorum knows no leader
       // and drops them (below).
-      if (SLOW && nprops && higher_lead && fb == DRB_FB_NONE)
+      // (with forward rows it forwards them, as the reference does)
+      if (SLOW && nprops && higher_lead && !v.fwd_props && fb == DRB_FB_NONE)
         fb = DRB_FB_TERM_MISMATCH;
+      // a Propose the leader may not handle as leader (it steps down first)
+      if (SLOW && prop_from && higher_in && fb == DRB_FB_NONE)
+        fb = DRB_FB_MESSAGE_TYPE;
     } else {
       if (max_app && max_app >= keep_common + v.W &&
           fb == DRB_FB_NONE)
         fb = DRB_FB_CAPACITY;
+      // a Propose at a follower (or a candidate) is the CPU path's
+      // (handleFollowerPropose would forward it again)
+      if (prop_from && fb == DRB_FB_NONE) fb = DRB_FB_MESSAGE_TYPE;
+      // the entry queue this follower forwards: Cmds that fit the rows
+      for (uint32_t j = 0; j < nprops; ++j) {
+        const uint4 p2 = v.props[prop_ix(v, p.prop_slot, j, 2, g)];
+        if (p2.y > v.C16 * 16 && fb == DRB_FB_NONE) fb = DRB_FB_CAPACITY;
+      }
       // mailbox: one response per message of a sender, plus the
-      // forwarded ReadIndex (handleFollowerReadIndex)
+      // forwarded ReadIndex (handleFollowerReadIndex) and Propose
 #pragma unroll
       for (int s = 0; s < R; ++s)
         if ((uint32_t)s != slot &&
-            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) + (SLOW ? 1 : 0) +
+            ((nin_packed >> (5 * s)) & 31u) + (in_lo != 0) + (nprops != 0) +
+                    (SLOW ? 1 : 0) +
                     (SLOW ? n_lt + ((flags & F_XFER_REQ) ? 1u : 0u) : 0u) >
                 v.MB &&
             fb == DRB_FB_NONE)
@@ -2708,7 +2832,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     }
     if (p.encode_saves && fb == DRB_FB_NONE) {
       // EntriesToSave lie in [min(committed, saved_to) + 1, new last]
-      const uint64_t top = umax64(r.last + nprops, max_app);
+      const uint64_t top = umax64(r.last + nappend, max_app);
       const uint64_t base = umin64(r.committed, r.saved_to);
       uint64_t n_save = top > base ? top - base : 0;
       uint64_t slack = 0;
@@ -2826,7 +2950,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
             if (SLOW)
               el_dispatch(L, r, s, m, src);
             else
-              dispatch(L, r, s, m, src);
+              dispatch<R, FWD>(L, r, s, m, src);
           }
         }
       }
@@ -2866,46 +2990,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       // handleProposals (node.go:1275) -> handleLeaderPropose
       // (raft.go:1794-1815) -> appendEntries (raft.go:944-955); a leader
       // transferring its leadership drops them (raft.go:1796-1800)
-      if (SLOW && nprops && (r.flags & F_XFER)) {
-        c_dprop = nprops;
-      } else if (SLOW && nprops && r.role != DRB_LEADER) {
+      if (nprops && (SLOW ? r.role == DRB_LEADER : LEAD)) {
+        if (SLOW && (r.flags & F_XFER))
+          r.ndropped_props += nprops;  // leaderTransfering
+        else {
+          append_props(L, r, p.prop_slot, nprops);
+          broadcast_replicate(L, r);
+        }
+      } else if (FWD && nprops && r.role == DRB_FOLLOWER && v.fwd_props) {
+        forward_props(L, r, p.prop_slot, nprops);  // handleFollowerPropose
+      } else if (nprops) {
         // stepped down this round: handleCandidatePropose, or
         // handleFollowerPropose with no leader known (raft.go:2197-2201,
-        // 2103-2108) -- reportDroppedProposal
+        // 2103-2108) -- reportDroppedProposal; one that knows the new
+        // leader forwards (above), or without forward rows was routed to
+        // the CPU path by the pre-pass
         if (r.role == DRB_FOLLOWER && r.leader_id != 0)
-          set_error(r, DRB_FB_TERM_MISMATCH);  // excluded by the pre-pass
+          set_error(r, DRB_ERR_PROPOSE);
         else
-          c_dprop = nprops;
-      } else if (nprops) {
-        const uint32_t chunks = PROP_META + v.C16;
-        for (uint32_t j = 0; j < nprops; ++j) {
-          uint64_t idx = r.last + 1 + j;
-          uint4 p0 = v.props[prop_ix(v, p.prop_slot, j, 0, g)];
-          uint4 p1 = v.props[prop_ix(v, p.prop_slot, j, 1, g)];
-          uint4 p2 = v.props[prop_ix(v, p.prop_slot, j, 2, g)];
-          v.ring[ring_ix(v, slot, idx, 0, g)] = mk4(r.term, lo64(p0));
-          v.ring[ring_ix(v, slot, idx, 1, g)] = mk4(hi64(p0), lo64(p1));
-          v.ring[ring_ix(v, slot, idx, 2, g)] =
-              make_uint4(p1.z, p1.w, p2.x, p2.y);
-          for (uint32_t c = PROP_META; c < chunks; ++c)
-            v.ring[ring_ix(v, slot, idx, c, g)] =
-                v.props[prop_ix(v, p.prop_slot, j, c, g)];
-        }
-        r.last += nprops;
-        if (r.last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, r.last + 1 - v.W);
-        rem_try_update<R>(L, (int)slot, r.last);  // self remote
-        if (R == 1) try_commit(L, r);
-        broadcast_replicate(L, r);
+          r.ndropped_props += nprops;
       }
       // handleLeaderTransfer (node.go:1249-1257) -> Peer.RequestLeader-
       // Transfer (peer.go:106-113): a LeaderTransfer to itself, term 0
-#ifdef DRB_DBG_XFER
-      if (SLOW)
-        printf("xfer g %lu s %u flags %x role %u lid %lu tgt %u fb %u\n",
-               (unsigned long)g, slot, r.flags, r.role,
-               (unsigned long)r.leader_id, (unsigned)v.xfer_in[ix(v, slot, g)],
-               fb);
-#endif
       if (SLOW && (r.flags & F_XFER_REQ)) {
         r.flags &= ~F_XFER_REQ;
         const uint64_t target = v.xfer_in[ix(v, slot, g)];
@@ -2939,7 +3045,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       bool state_empty = r.term == 0 && vote == 0 && r.committed == 0;
       bool has_update = has_save || r.leader_update || r.nmsgs > 0 ||
                         has_apply || (!state_empty && state_changed) ||
-                        r.nrtr > 0 || r.ndropped_ri > 0 || c_dprop > 0;
+                        r.nrtr > 0 || r.ndropped_ri > 0 ||
+                        r.ndropped_props > 0;
       uint64_t apply_lo = 0, apply_hi = 0;
       if (has_update || confirmed_index != r.applied_index) {
         // validateUpdate / pushEntries (node.go:1100) / Peer.Commit
@@ -3091,6 +3198,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       c_msgs = r.nmsgs;
       c_rtr = r.nrtr;
       c_drop = r.ndropped_ri;
+      c_dprop = r.ndropped_props;
     }
     if (c_fb | c_err) flag_log(v, g, slot, r.fb, r.flags, p.round);
     // outbox headers for this round (tag = round), for the destinations

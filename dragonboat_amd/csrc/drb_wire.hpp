@@ -182,9 +182,35 @@ DRB_DEV EntryHdr wire_entry(const View &v, uint32_t slot, uint64_t idx,
 }
 
 // entries of a Replicate (raft.go:738-769): [LogIndex+1, LogIndex+n] of
-// the sender's log
+// the sender's log; of a forwarded Propose (raft.go:2103-2116): the sender's
+// forward rows, as proposed (no Term, no Index)
 DRB_DEV uint32_t wire_n_entries(const WireMsg &w) {
-  return w.m.type == DRB_MSG_REPLICATE ? w.m.n : 0;
+  return w.m.type == DRB_MSG_REPLICATE || w.m.type == DRB_MSG_PROPOSE ? w.m.n
+                                                                      : 0;
+}
+// entry q of message w and its Cmd's first chunk (the next ones G apart)
+DRB_DEV EntryHdr wire_msg_entry(const View &v, const WireArgs &a, uint64_t g,
+                                const WireMsg &w, uint32_t q,
+                                const uint4 **cmd0) {
+  if (w.m.type == DRB_MSG_PROPOSE) {
+    const uint32_t fw = fwd_ps(v, a.buf, a.from);
+    const uint4 p0 = v.props[prop_ix(v, fw, q, 0, g)];
+    const uint4 p1 = v.props[prop_ix(v, fw, q, 1, g)];
+    const uint4 p2 = v.props[prop_ix(v, fw, q, 2, g)];
+    EntryHdr e;
+    e.term = e.index = 0;
+    e.key = q_lo(p0);
+    e.client_id = q_hi(p0);
+    e.series_id = q_lo(p1);
+    e.responded_to = q_hi(p1);
+    e.type = p2.x;
+    e.cmd_len = p2.y;
+    *cmd0 = v.props + prop_ix(v, fw, q, PROP_META, g);
+    return e;
+  }
+  const uint64_t idx = w.m.log_index + 1 + q;
+  *cmd0 = v.ring + ring_ix(v, a.from, idx, ENT_META, g);
+  return wire_entry(v, a.from, idx, g);
 }
 
 // Message.Size (message.go:92-124) and Message.SizeUpperLimit
@@ -201,7 +227,8 @@ DRB_DEV void wire_sizes(const View &v, const WireArgs &a, uint64_t g,
   uint64_t up = 16 * 12 + 24;
   const uint32_t ne = wire_n_entries(w);
   for (uint32_t q = 0; q < ne; ++q) {
-    const EntryHdr e = wire_entry(v, a.from, m.log_index + 1 + q, g);
+    const uint4 *cmd0;
+    const EntryHdr e = wire_msg_entry(v, a, g, w, q, &cmd0);
     const uint32_t l = entry_size(e);
     n += 1 + l + sov64(l);
     up += 16 + 16 * 8 + e.cmd_len;  // EntryNonCmdFieldsSize (soft.go:20)
@@ -296,9 +323,10 @@ DRB_DEV void so_colfer_u64(StreamOut &o, uint32_t tag, uint64_t x) {
   }
 }
 
-// Entry.MarshalTo (raft_optimized.go:166-300), the Cmd from the window
-DRB_DEV void so_entry(StreamOut &o, const View &v, uint32_t slot,
-                      const EntryHdr &e, uint64_t g) {
+// Entry.MarshalTo (raft_optimized.go:166-300), the Cmd from the window (or
+// a Propose's forward rows): chunk c at cmd0[c * G]
+DRB_DEV void so_entry(StreamOut &o, const View &v, const EntryHdr &e,
+                      const uint4 *cmd0) {
   so_colfer_u64(o, 0, e.term);
   so_colfer_u64(o, 1, e.index);
   if (e.type != 0) {
@@ -313,7 +341,7 @@ DRB_DEV void so_entry(StreamOut &o, const View &v, uint32_t slot,
     so_byte(o, 7);
     so_varint(o, e.cmd_len);
     for (uint32_t c = 0; c * 16 < e.cmd_len; ++c) {
-      const uint4 q = v.ring[ring_ix(v, slot, e.index, ENT_META + c, g)];
+      const uint4 q = cmd0[(uint64_t)c * v.G];
       const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (uint32_t b = 0; b < 16; ++b)
@@ -352,10 +380,11 @@ DRB_DEV void so_message(StreamOut &o, const View &v, const WireArgs &a,
   so_varint(o, m.hint);
   const uint32_t ne = wire_n_entries(w);
   for (uint32_t q = 0; q < ne; ++q) {
-    const EntryHdr e = wire_entry(v, a.from, m.log_index + 1 + q, g);
+    const uint4 *cmd0;
+    const EntryHdr e = wire_msg_entry(v, a, g, w, q, &cmd0);
     so_byte(o, 0x5a);
     so_varint(o, entry_size(e));
-    so_entry(o, v, a.from, e, g);
+    so_entry(o, v, e, cmd0);
   }
   // Snapshot (field 12): the 24-byte empty pb.Snapshot
   so_byte(o, 0x62);

@@ -1,0 +1,346 @@
+// drb_worker.hpp -- a step worker's round outputs for the host
+// (drb_worker_export / drb_worker_wait, include/drb_engine.h), included at
+// the end of drb_engine.hip.
+//
+// engine.processSteps (engine.go:1304-1364) hands each node's Update to the
+// host every round: the ReadyToReads (node.processReadyToRead, node.go:1081),
+// the reads served behind them (pendingReadIndex.applied, request.go:
+// 930-953) and the applied entries (pendingProposals.applied, node.go:
+// 243-257).  Here one export covers every group of a replica slot:
+//   1. on the engine stream, behind the round: per lane the three record
+//      counts, one exclusive scan of {reads, values, applied} (hipCUB), and
+//      a compaction of the records into device staging[parity];
+//   2. on a copy stream of its own: a drain kernel moves staging[parity]
+//      into the caller's pinned host buffers (PCIe writes from the device,
+//      the counts to a mapped header), so the transfer overlaps the next
+//      rounds on the engine stream; staging[parity] is reused two exports
+//      later, behind that drain.
+// No host synchronisation until drb_worker_wait.
+#pragma once
+
+struct WorkerState {
+  hipStream_t sx = nullptr;
+  hipEvent_t ev_staged[2] = {nullptr, nullptr};
+  hipEvent_t ev_drained[2] = {nullptr, nullptr};
+  bool drained_valid[2] = {false, false};
+  drb_worker_read *rd[2] = {nullptr, nullptr};
+  uint64_t *val[2] = {nullptr, nullptr};
+  drb_worker_applied *ap[2] = {nullptr, nullptr};
+  uint64_t cap_rd = 0, cap_val = 0, cap_ap = 0;  // staging capacity
+  uint4 *cnt = nullptr, *off = nullptr;          // [G + 1]
+  void *tmp = nullptr;
+  size_t tmp_bytes = 0;
+  unsigned long long *tot = nullptr;  // device [2][4]
+  unsigned long long *hdr = nullptr;  // pinned, mapped [2][4]
+  unsigned long long *hdr_dev = nullptr;  // ... its device address
+  const drb_worker_bufs *owner[2] = {nullptr, nullptr};
+  uint64_t seq = 0;
+};
+
+namespace {
+
+struct U4Sum {
+  __host__ __device__ uint4 operator()(const uint4 &a, const uint4 &b) const {
+    return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+};
+
+// the applied range (applied_index, sm_index] of the round a replica last
+// ran, as drb_apply_results reads it (k_apply_results)
+__device__ inline void worker_apply_range(const View &v, uint32_t slot,
+                                          uint64_t g, uint64_t *lo,
+                                          uint64_t *hi) {
+  *lo = *hi = 0;
+  const uint32_t fl = v.u32[u32_ix(v, W_FLAGS, slot, g)];
+  const bool frozen =
+      (fl & (DRB_F_FALLBACK | DRB_F_ERROR)) && !(fl & DRB_F_APPLY_STOPPED);
+  if ((fl & DRB_F_HOSTED) && !frozen) {
+    *lo = pk_field(v, slot, g, PI_APPLIED_INDEX);
+    *hi = pk_field(v, slot, g, PI_SM_INDEX);
+  }
+}
+
+__global__ void k_worker_count(const View v, uint32_t slot, uint32_t n_reads,
+                               uint4 *cnt) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > v.G) return;
+  uint4 c = make_uint4(0, 0, 0, 0);
+  if (g < v.G) {
+    const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+    c.x = nr;
+    if (nr && n_reads) {
+      const uint32_t m = v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u);
+      c.y = (uint32_t)__popc(m) * n_reads;
+    }
+    uint64_t lo, hi;
+    worker_apply_range(v, slot, g, &lo, &hi);
+    c.z = hi > lo ? (uint32_t)(hi - lo) : 0u;
+  }
+  cnt[g] = c;  // cnt[G] = 0: the scan's last element is the total
+}
+
+__global__ void k_worker_compact(const View v, uint32_t slot,
+                                 uint32_t n_reads, const uint4 *off,
+                                 drb_worker_read *rd, uint64_t cap_rd,
+                                 uint64_t *val, uint64_t cap_val,
+                                 drb_worker_applied *ap, uint64_t cap_ap,
+                                 unsigned long long *tot) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == v.G) {  // the totals
+    tot[0] = off[g].x;
+    tot[1] = off[g].y;
+    tot[2] = off[g].z;
+  }
+  if (g >= v.G) return;
+  const uint4 o = off[g];
+  const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+  const uint32_t m =
+      nr && n_reads ? v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u) : 0u;
+  uint64_t vo = o.y;
+  for (uint32_t k = 0; k < nr; ++k) {
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    const uint4 c1 = v.rtr[rtr_ix(v, slot, k, 1, g)];
+    const bool served = (m >> k) & 1u;
+    if (o.x + k < cap_rd) {
+      drb_worker_read r;
+      r.group = g;
+      r.index = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+      r.ctx_low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
+      r.ctx_high = (uint64_t)c1.x | ((uint64_t)c1.y << 32);
+      r.n_values = served ? n_reads : 0u;
+      r.first = (uint32_t)vo;
+      rd[o.x + k] = r;
+    }
+    if (!served) continue;
+    for (uint32_t j = 0; j < n_reads; ++j, ++vo) {
+      if (vo >= cap_val) continue;
+      const uint2 w = v.read_res[rres_ix(v, slot, k, j, g)];
+      val[vo] = (uint64_t)w.x | ((uint64_t)w.y << 32);
+    }
+  }
+  uint64_t lo, hi;
+  worker_apply_range(v, slot, g, &lo, &hi);
+  for (uint64_t idx = lo + 1, a = o.z; idx <= hi && a < cap_ap; ++idx, ++a) {
+    const uint4 m0 = v.ring[ring_ix(v, slot, idx, 0, g)];
+    const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
+    const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
+    drb_worker_applied r;
+    r.group = g;
+    r.index = idx;
+    r.key = hi64(m0);
+    const uint64_t client = lo64(m1);
+    const uint32_t type = m2.z, clen = m2.w;
+    r.ignored = client == 0 ? 1u : 0u;
+    // KVTest.Update's Result.Value: the payload length (kvtest.go:161)
+    r.value = r.ignored ? 0
+                        : (type == DRB_ENTRY_ENCODED && clen ? clen - 1 : clen);
+    r.pad = 0;
+    ap[a] = r;
+  }
+}
+
+// bytes [0, n) of src into dst (16-byte aligned, n a multiple of 8), a
+// grid-stride walk of 16 B words
+__device__ inline void worker_drain_copy(uint8_t *dst, const uint8_t *src,
+                                         uint64_t n, uint64_t t,
+                                         uint64_t nt) {
+  const uint64_t n16 = n / 16;
+  for (uint64_t i = t; i < n16; i += nt)
+    ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+  if ((n & 15) && t == 0)
+    *(uint2 *)(dst + n16 * 16) = *(const uint2 *)(src + n16 * 16);
+}
+
+__global__ void k_worker_drain(const unsigned long long *tot,
+                               const drb_worker_read *rd, uint64_t cap_rd,
+                               drb_worker_read *hrd, const uint64_t *val,
+                               uint64_t cap_val, uint64_t *hval,
+                               const drb_worker_applied *ap, uint64_t cap_ap,
+                               drb_worker_applied *hap,
+                               unsigned long long *hdr) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t nrd = min((uint64_t)tot[0], cap_rd);
+  const uint64_t nval = min((uint64_t)tot[1], cap_val);
+  const uint64_t nap = min((uint64_t)tot[2], cap_ap);
+  if (hrd) worker_drain_copy((uint8_t *)hrd, (const uint8_t *)rd,
+                             nrd * sizeof(drb_worker_read), t, nt);
+  if (hval) worker_drain_copy((uint8_t *)hval, (const uint8_t *)val,
+                              nval * sizeof(uint64_t), t, nt);
+  if (hap) worker_drain_copy((uint8_t *)hap, (const uint8_t *)ap,
+                             nap * sizeof(drb_worker_applied), t, nt);
+  if (t == 0) {
+    hdr[0] = tot[0];
+    hdr[1] = tot[1];
+    hdr[2] = tot[2];
+  }
+}
+
+}  // namespace
+
+static void worker_free(drb_engine *e) {
+  WorkerState *w = e->worker;
+  if (!w) return;
+  if (w->sx) (void)hipStreamSynchronize(w->sx);
+  for (int k = 0; k < 2; ++k) {
+    if (w->ev_staged[k]) (void)hipEventDestroy(w->ev_staged[k]);
+    if (w->ev_drained[k]) (void)hipEventDestroy(w->ev_drained[k]);
+    if (w->rd[k]) (void)hipFree(w->rd[k]);
+    if (w->val[k]) (void)hipFree(w->val[k]);
+    if (w->ap[k]) (void)hipFree(w->ap[k]);
+  }
+  if (w->cnt) (void)hipFree(w->cnt);
+  if (w->off) (void)hipFree(w->off);
+  if (w->tmp) (void)hipFree(w->tmp);
+  if (w->tot) (void)hipFree(w->tot);
+  if (w->hdr) (void)hipHostFree(w->hdr);
+  if (w->sx) (void)hipStreamDestroy(w->sx);
+  delete w;
+  e->worker = nullptr;
+}
+
+// device staging of at least these capacities (grow-only; growing waits
+// for the exports in flight)
+static int worker_reserve(drb_engine *e, uint64_t crd, uint64_t cval,
+                          uint64_t cap) {
+  WorkerState &w = *e->worker;
+  if (crd <= w.cap_rd && cval <= w.cap_val && cap <= w.cap_ap) return DRB_OK;
+  HIPCHK(hipStreamSynchronize(w.sx));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  crd = std::max(crd, w.cap_rd);
+  cval = std::max(cval, w.cap_val);
+  cap = std::max(cap, w.cap_ap);
+  for (int k = 0; k < 2; ++k) {
+    if (w.rd[k]) HIPCHK(hipFree(w.rd[k]));
+    if (w.val[k]) HIPCHK(hipFree(w.val[k]));
+    if (w.ap[k]) HIPCHK(hipFree(w.ap[k]));
+    w.rd[k] = nullptr;
+    w.val[k] = nullptr;
+    w.ap[k] = nullptr;
+    HIPCHK(hipMalloc(&w.rd[k], std::max<uint64_t>(crd, 1) *
+                                   sizeof(drb_worker_read)));
+    HIPCHK(hipMalloc(&w.val[k], std::max<uint64_t>(cval, 1) * 8 + 16));
+    HIPCHK(hipMalloc(&w.ap[k], std::max<uint64_t>(cap, 1) *
+                                   sizeof(drb_worker_applied)));
+  }
+  w.cap_rd = crd;
+  w.cap_val = cval;
+  w.cap_ap = cap;
+  return DRB_OK;
+}
+
+static int worker_init(drb_engine *e) {
+  if (e->worker) return DRB_OK;
+  WorkerState *w = new WorkerState();
+  e->worker = w;
+  const uint64_t G = e->v.G;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(hipStreamCreateWithFlags(&w->sx, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k) {
+    HIPCHK(hipEventCreateWithFlags(&w->ev_staged[k], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&w->ev_drained[k], hipEventDisableTiming));
+  }
+  HIPCHK(hipMalloc(&w->cnt, (G + 1) * sizeof(uint4)));
+  HIPCHK(hipMalloc(&w->off, (G + 1) * sizeof(uint4)));
+  HIPCHK(hipcub::DeviceScan::ExclusiveScan(nullptr, w->tmp_bytes, w->cnt,
+                                           w->off, U4Sum(),
+                                           make_uint4(0, 0, 0, 0),
+                                           (int)(G + 1), e->stream));
+  HIPCHK(hipMalloc(&w->tmp, std::max<size_t>(w->tmp_bytes, 16)));
+  HIPCHK(hipMalloc(&w->tot, 8 * sizeof(unsigned long long)));
+  HIPCHK(hipHostMalloc((void **)&w->hdr, 8 * sizeof(unsigned long long),
+                       hipHostMallocMapped));
+  memset(w->hdr, 0, 8 * sizeof(unsigned long long));
+  HIPCHK(hipHostGetDevicePointer((void **)&w->hdr_dev, w->hdr, 0));
+  return DRB_OK;
+}
+
+extern "C" int drb_host_alloc(drb_engine *e, size_t bytes, void **p) {
+  if (!e || !p || !bytes) return DRB_EINVAL;
+  *p = nullptr;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(hipHostMalloc(p, bytes, hipHostMallocMapped));
+  return DRB_OK;
+}
+
+extern "C" int drb_host_free(drb_engine *e, void *p) {
+  if (!e) return DRB_EINVAL;
+  if (p) {
+    if (e->worker && e->worker->sx) HIPCHK(hipStreamSynchronize(e->worker->sx));
+    HIPCHK(hipHostFree(p));
+  }
+  return DRB_OK;
+}
+
+static int worker_dev_ptr(void *h, void **d) {
+  *d = nullptr;
+  if (!h) return DRB_OK;
+  HIPCHK(hipHostGetDevicePointer(d, h, 0));
+  return DRB_OK;
+}
+
+extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
+                                 const drb_worker_bufs *b) {
+  if (!e || !b || slot >= e->v.R) return DRB_EINVAL;
+  if ((b->reads_cap && !b->reads) || (b->values_cap && !b->values) ||
+      (b->applied_cap && !b->applied))
+    return DRB_EINVAL;
+  if (int rc = worker_init(e)) return rc;
+  WorkerState &w = *e->worker;
+  if (int rc = worker_reserve(e, b->reads_cap, b->values_cap, b->applied_cap))
+    return rc;
+  void *hrd, *hval, *hap;
+  if (worker_dev_ptr(b->reads, &hrd) || worker_dev_ptr(b->values, &hval) ||
+      worker_dev_ptr(b->applied, &hap))
+    return DRB_EINVAL;
+  const View &v = e->v;
+  // the reads of the last round, if it served them with results
+  const uint32_t n_reads =
+      v.read_res && e->reads_round == e->round ? e->reads_n : 0u;
+  const int k = (int)(w.seq & 1);
+  // staging[k] is free once the drain two exports back is done
+  if (w.drained_valid[k])
+    HIPCHK(hipStreamWaitEvent(e->stream, w.ev_drained[k], 0));
+  const unsigned blocks = (unsigned)((v.G + 1 + 255) / 256);
+  k_worker_count<<<blocks, 256, 0, e->stream>>>(v, slot, n_reads, w.cnt);
+  HIPCHK(hipGetLastError());
+  size_t tb = w.tmp_bytes;
+  HIPCHK(hipcub::DeviceScan::ExclusiveScan(w.tmp, tb, w.cnt, w.off, U4Sum(),
+                                           make_uint4(0, 0, 0, 0),
+                                           (int)(v.G + 1), e->stream));
+  k_worker_compact<<<blocks, 256, 0, e->stream>>>(
+      v, slot, n_reads, w.off, w.rd[k], b->reads_cap, w.val[k],
+      b->values_cap, w.ap[k], b->applied_cap, w.tot + 4 * k);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(w.ev_staged[k], e->stream));
+  // the transfer, on the copy stream: PCIe-bound, a few workgroups
+  HIPCHK(hipStreamWaitEvent(w.sx, w.ev_staged[k], 0));
+  k_worker_drain<<<256, 256, 0, w.sx>>>(
+      w.tot + 4 * k, w.rd[k], b->reads_cap, (drb_worker_read *)hrd, w.val[k],
+      b->values_cap, (uint64_t *)hval, w.ap[k], b->applied_cap,
+      (drb_worker_applied *)hap, w.hdr_dev + 4 * k);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(w.ev_drained[k], w.sx));
+  w.drained_valid[k] = true;
+  w.owner[k] = b;
+  w.seq++;
+  return DRB_OK;
+}
+
+extern "C" int drb_worker_wait(drb_engine *e, drb_worker_bufs *b) {
+  if (!e || !b || !e->worker) return DRB_EINVAL;
+  WorkerState &w = *e->worker;
+  int k = -1;
+  for (int q = 0; q < 2; ++q)
+    if (w.owner[q] == b && w.drained_valid[q]) k = q;
+  if (k < 0) return DRB_EINVAL;
+  HIPCHK(hipEventSynchronize(w.ev_drained[k]));
+  b->n_reads = w.hdr[4 * k];
+  b->n_values = w.hdr[4 * k + 1];
+  b->n_applied = w.hdr[4 * k + 2];
+  w.owner[k] = nullptr;
+  return b->n_reads > b->reads_cap || b->n_values > b->values_cap ||
+                 b->n_applied > b->applied_cap
+             ? DRB_ERANGE
+             : DRB_OK;
+}

@@ -107,6 +107,8 @@ SIGNATURES = {
     "drb_plane_regions": (C.c_int, [P, U32, U32, U32, C.c_int,
                                     C.POINTER(Region)]),
     "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
+    "drb_exchange_local_counted": (C.c_int, [C.POINTER(P), U32]),
+    "drb_exchange_mark": (C.c_int, [P]),
     "drb_encode_wire": (C.c_int, [P, U32, U32, C.POINTER(WireCfg),
                                   C.POINTER(WireOut)]),
     "drb_wire_buffer": (C.c_int, [P, C.POINTER(P), PU64]),
@@ -115,6 +117,10 @@ SIGNATURES = {
     "drb_ingest_buffer": (C.c_int, [P, SZ, C.POINTER(PU8)]),
     "drb_ingest_buffer_alloc": (C.c_int, [P, SZ, C.POINTER(PU8)]),
     "drb_ingest_buffer_free": (C.c_int, [P, PU8]),
+    "drb_worker_export": (C.c_int, [P, U32, C.POINTER(abi.WorkerBufs)]),
+    "drb_worker_wait": (C.c_int, [P, C.POINTER(abi.WorkerBufs)]),
+    "drb_host_alloc": (C.c_int, [P, SZ, C.POINTER(P)]),
+    "drb_host_free": (C.c_int, [P, P]),
 }
 
 
@@ -160,7 +166,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
                 tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0,
-                kv_overflow_buckets=0)
+                kv_overflow_buckets=0, forward_proposals=0)
 
 
 class Engine:
@@ -182,7 +188,8 @@ class Engine:
                    cfg["durable_log"], cfg["save_batched"],
                    cfg["save_tan"], cfg["elections"], cfg["tan_max_log"],
                    cfg["tan_multiplexed"], cfg["pre_vote"],
-                   cfg["max_reads_per_ctx"], cfg["kv_overflow_buckets"])
+                   cfg["max_reads_per_ctx"], cfg["kv_overflow_buckets"],
+                   cfg["forward_proposals"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -313,10 +320,10 @@ class Engine:
     # ---------------------------------------------------------- round
     def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE,
              reads_per_ctx=0, key_space=0, encode_saves=False, ri_replica=0,
-             listed=False):
+             listed=False, prop_replica=0):
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
                       key_space, int(bool(encode_saves)), ri_replica,
-                      int(bool(listed)))
+                      int(bool(listed)), prop_replica)
         out = RoundOut()
         _ck(lib().drb_step_round(self.h, C.byref(rin), C.byref(out)),
             "drb_step_round")
@@ -324,13 +331,14 @@ class Engine:
 
     def step_async(self, tick=False, prop_slot=abi.DRB_NONE,
                    ri_slot=abi.DRB_NONE, reads_per_ctx=0, key_space=0,
-                   encode_saves=False, ri_replica=0, listed=False):
+                   encode_saves=False, ri_replica=0, listed=False,
+                   prop_replica=0):
         """One round, stream-ordered; reads_per_ctx > 0 also serves the
         reads behind the round's ReadyToReads, encode_saves encodes the
         EntriesToSave (drb_round_in)."""
         rin = RoundIn(int(bool(tick)), prop_slot, ri_slot, reads_per_ctx,
                       key_space, int(bool(encode_saves)), ri_replica,
-                      int(bool(listed)))
+                      int(bool(listed)), prop_replica)
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
 
@@ -552,10 +560,19 @@ class Engine:
         return [(arr[i].ptr, arr[i].bytes) for i in range(n)]
 
     @staticmethod
-    def exchange_local(engines):
-        """One process holding every rank's engine: move the planes."""
+    def exchange_local(engines, counted=False):
+        """One process holding every rank's engine: move the planes
+        (full-capacity planes behind cross-stream events, or at the counted
+        sizes with host synchronisation)."""
         arr = (P * len(engines))(*[e.h for e in engines])
-        _ck(lib().drb_exchange_local(arr, len(engines)), "drb_exchange_local")
+        fn = lib().drb_exchange_local_counted if counted else \
+            lib().drb_exchange_local
+        _ck(fn(arr, len(engines)), "drb_exchange_local")
+
+    def exchange_mark(self):
+        """This rank's own exchange of the last round is enqueued (RCCL):
+        ingest may write the remote planes again (drb_exchange_mark)."""
+        _ck(lib().drb_exchange_mark(self.h), "drb_exchange_mark")
 
     def serve_reads(self, reads_per_ctx=9, key_space=256):
         _ck(lib().drb_serve_reads(self.h, reads_per_ctx, key_space),
@@ -630,6 +647,38 @@ class Engine:
         _ck(lib().drb_ingest_wire(self.h, ptr, n, deployment_id,
                                   C.byref(res)), "drb_ingest_wire")
         return {f: getattr(res, f) for f, _ in WireIn._fields_}
+
+    # ---------------------------------------------------------- step worker
+    def worker_bufs(self, reads_cap, values_cap, applied_cap):
+        """A drb_worker_bufs over fresh pinned host buffers (drb_host_alloc);
+        free them with free_worker_bufs."""
+        b = abi.WorkerBufs()
+        for name, typ, cap in (("reads", abi.WorkerRead, reads_cap),
+                               ("values", C.c_uint64, values_cap),
+                               ("applied", abi.WorkerApplied, applied_cap)):
+            p = P()
+            _ck(lib().drb_host_alloc(self.h, max(1, cap) * C.sizeof(typ),
+                                     C.byref(p)), "drb_host_alloc")
+            setattr(b, name, C.cast(p, C.POINTER(typ)))
+            setattr(b, name + "_cap", cap)
+        return b
+
+    def free_worker_bufs(self, b):
+        for name in ("reads", "values", "applied"):
+            _ck(lib().drb_host_free(self.h, C.cast(getattr(b, name), P)),
+                "drb_host_free")
+
+    def worker_export(self, slot, b):
+        """drb_worker_export: enqueue the last round's outputs of replica
+        slot `slot` into b (returns at once)."""
+        _ck(lib().drb_worker_export(self.h, slot, C.byref(b)),
+            "drb_worker_export")
+
+    def worker_wait(self, b):
+        """drb_worker_wait: (n_reads, n_values, n_applied); raises when a
+        count exceeded its buffer."""
+        _ck(lib().drb_worker_wait(self.h, C.byref(b)), "drb_worker_wait")
+        return b.n_reads, b.n_values, b.n_applied
 
     def crc32_batch(self, buffers):
         data = b"".join(buffers)

@@ -219,3 +219,6 @@ class PlaneExchange:
             run_ops(ops, lambda p, n: device_bytes(p, n, self.device),
                     self.group)
             torch.cuda.current_stream(self.device).synchronize()
+        # transports may ingest into the remote planes again (drb_ingest
+        # returns DRB_EAGAIN between a round and its exchange)
+        self.eng.exchange_mark()

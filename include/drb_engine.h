@@ -64,6 +64,8 @@ extern "C" {
 #define DRB_ENOMEM (-3)
 #define DRB_ENOSYS (-4)
 #define DRB_ERANGE (-5)
+#define DRB_EAGAIN (-6)  /* retry later: the call would race a step in
+                          * flight (drb_ingest before drb_exchange_*) */
 
 /* raftpb.MessageType (raftpb/types.go:8-37) */
 enum drb_message_type {
@@ -152,8 +154,12 @@ enum drb_fallback_reason {
                                  * changed */
   DRB_ERR_APPLY = 104,          /* statemachine.go:935-969 malformed entry */
   DRB_ERR_READINDEX = 105,      /* readindex.go:43-115 invariant */
-  DRB_ERR_TRANSFER = 106        /* raft.go:1929-1931 LeaderTransfer without
+  DRB_ERR_TRANSFER = 106,       /* raft.go:1929-1931 LeaderTransfer without
                                  * a target */
+  DRB_ERR_PROPOSE = 107         /* internal invariant: proposals at a replica
+                                 * that stepped down and knows a leader, with
+                                 * no forward rows (the pre-pass routes that
+                                 * round to the CPU path) */
 };
 
 /* remote (internal/raft/remote.go:72-80); remotes[] is indexed by slot. */
@@ -384,6 +390,17 @@ typedef struct drb_config {
    * is not reclaimed).  0: a full table stops the replica's apply
    * (DRB_F_APPLY_STOPPED). */
   uint64_t kv_overflow_buckets;
+  /* 1: proposals may be made at any replica (drb_round_in.prop_replica),
+   * as at any NodeHost: a follower forwards its entry queue to its leader
+   * as a Propose message, dropped when it knows no leader
+   * (handleFollowerPropose, raft.go:2103-2116), and the leader appends a
+   * received Propose's entries (handleLeaderPropose, raft.go:1794-1815).
+   * A Propose carries its entries by value in per-(round, sender) rows
+   * (max_props entries, at most 15); drb_ingest / drb_ingest_wire accept
+   * Propose messages from other NodeHosts into them (one per sender, round
+   * and group; a second is dropped as by a full MessageQueue).  Co-resident
+   * placement only. */
+  uint32_t forward_proposals;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -409,6 +426,11 @@ typedef struct drb_round_in {
    * into dense waves -- for rounds where most replicas are at rest (C5,
    * Quiesce); the result is the same.  Co-resident placement only. */
   uint32_t listed;
+  /* where the staged proposal batch lands (node.handleProposals,
+   * node.go:1275-1294): 0 the group's leader; k >= 1 replica ID k, whose
+   * NodeHost's entry queue it is -- a follower forwards it to its leader
+   * (needs drb_config.forward_proposals). */
+  uint32_t prop_replica;
 } drb_round_in;
 
 #define DRB_NONE 0xffffffffu
@@ -652,6 +674,59 @@ int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
                                     drb_ready_to_read *out, size_t cap,
                                     size_t *n_out);
 
+/*
+ * A step worker's round, handed to the host without a host synchronisation
+ * (engine.processSteps, engine.go:1304-1364: node.processReadyToRead,
+ * node.go:1081 -> pendingReadIndex.addReady, request.go:883; the reads
+ * served behind them, pendingReadIndex.applied, request.go:930-953 ->
+ * ReadLocalNode, nodehost.go:849; the applied entries,
+ * pendingProposals.applied, node.go:243-257).  drb_worker_export enqueues,
+ * behind the last round, a compaction of replica slot `slot`'s outputs
+ * into device staging (two buffers, by export parity) and, on a copy
+ * stream, their transfer into the caller's host buffers (drb_host_alloc):
+ * the transfer overlaps the next rounds.  drb_worker_wait blocks until
+ * that export's bytes are in its buffers and fills the counts.  Records in
+ * group order, each group's in release / index order.
+ */
+typedef struct drb_worker_read {  /* one ReadyToRead */
+  uint64_t group;      /* lane (ShardID = first_shard_id + group) */
+  uint64_t index;      /* its read index */
+  uint64_t ctx_low;
+  uint64_t ctx_high;
+  uint32_t n_values;   /* reads served behind it (0: deferred until the
+                        * index is applied, or no reads this round) */
+  uint32_t first;      /* their results: values[first, first + n_values) */
+} drb_worker_read;
+
+typedef struct drb_worker_applied {  /* one applied entry */
+  uint64_t group;
+  uint64_t index;
+  uint64_t key;        /* pb.Entry.Key: the proposal's RequestState */
+  uint64_t value;      /* sm.Result.Value (kvtest.go:161) */
+  uint32_t ignored;    /* 1: an empty no-op entry (statemachine.go:939) */
+  uint32_t pad;
+} drb_worker_applied;
+
+typedef struct drb_worker_bufs {
+  drb_worker_read *reads;      /* host buffers from drb_host_alloc */
+  uint64_t reads_cap;
+  /* per served read: LE32 value | (vlen | found << 31) << 32 (the value's
+   * first 4 bytes; all of it at C3's 4-byte values) */
+  uint64_t *values;
+  uint64_t values_cap;
+  drb_worker_applied *applied;
+  uint64_t applied_cap;
+  uint64_t n_reads, n_values, n_applied;  /* set by drb_worker_wait */
+} drb_worker_bufs;
+
+int drb_worker_export(drb_engine *e, uint32_t slot, const drb_worker_bufs *b);
+/* DRB_ERANGE when a count exceeded its cap (the counts are the full ones,
+ * the buffers hold the first cap records) */
+int drb_worker_wait(drb_engine *e, drb_worker_bufs *b);
+/* pinned host memory the engine's device can write (drb_worker_bufs) */
+int drb_host_alloc(drb_engine *e, size_t bytes, void **p);
+int drb_host_free(drb_engine *e, void *p);
+
 /* One ReadLocalNode result (nodehost.go:849 -> KVTest.Lookup,
  * kvtest.go:164-175) of the reads served behind a ReadyToRead: the read's
  * ctx and position, its key and what the lookup found.  value holds the
@@ -842,9 +917,30 @@ int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
  * Returns the region count (<= DRB_PLANE_REGIONS) or < 0. */
 int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
                       uint32_t word, int dir, drb_region *out);
-/* The whole exchange among engines[rank] of one process (peer copies on
- * the receivers' streams); every engine must have run the same round. */
+/* The whole exchange among engines[rank] of one process, every engine at
+ * the same round (NodeHost is one process per machine driving every GPU):
+ * every plane that can carry fast-path messages -- one with a leader slot
+ * at either end (drb_role_slots, OR over the engines), or every plane with
+ * drb_config.elections -- moves at its full capacity (all mailbox
+ * positions, both chunks, the header, the max-append word, the entry-row
+ * base and entry_mbox entry rows: what the pre-pass bounds), so no counts
+ * are read.  The peer copies are enqueued on the receivers' streams behind
+ * the senders' rounds (cross-stream events), and each sender's next round
+ * waits for the copies that read its outbox: no host synchronisation.
+ * The receivers read only what the plane headers count. */
 int drb_exchange_local(drb_engine *const *engines, uint32_t n);
+/* The same exchange at the planes' counted sizes (drb_plane_counts per
+ * engine, i.e. one stream synchronisation each, then the copies and a
+ * synchronisation of every stream): fewer bytes, host round trips. */
+int drb_exchange_local_counted(drb_engine *const *engines, uint32_t n);
+/* A process-per-GPU host (RCCL send/recv of drb_plane_regions on the
+ * engine stream) tells the engine its exchange of the last round is
+ * enqueued.  With replicas spread over ranks, drb_ingest / drb_ingest_wire
+ * return DRB_EAGAIN between a round's launch and its exchange: a message
+ * for a remote plane written then would be overwritten by the exchange's
+ * copy of that plane (the receiver's inbound header), so the transport
+ * retries after the exchange.  drb_exchange_local marks it itself. */
+int drb_exchange_mark(drb_engine *e);
 
 /*
  * The entries one replica slot applied in the last round, for

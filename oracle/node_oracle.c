@@ -921,14 +921,28 @@ int orc_cluster_setup_steady(orc_cluster *c, uint32_t leader_slot) {
 int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
                                 uint32_t max_per_group, const drb_entry *ents,
                                 const uint8_t *pool) {
+  return orc_cluster_stage_proposals_at(c, counts, max_per_group, ents, pool,
+                                        0);
+}
+
+/* NodeHost.Propose -> node.propose -> entryQueue.add (queue.go:60) at
+ * replica ID `replica` of every group (0: the group's leader replica, the
+ * NodeHost holding it); node.handleProposals hands the queue to
+ * Peer.ProposeEntries (node.go:1275-1294), and a follower forwards it to
+ * its leader (handleFollowerPropose, raft.go:2103-2116) */
+int orc_cluster_stage_proposals_at(orc_cluster *c, const uint32_t *counts,
+                                   uint32_t max_per_group,
+                                   const drb_entry *ents, const uint8_t *pool,
+                                   uint32_t replica) {
   uint32_t R = c->cfg.num_replicas;
   for (uint64_t g = 0; g < c->cfg.num_groups; g++) {
     if (!counts[g]) continue;
-    /* routed to the group's leader replica (the NodeHost holding it) */
     orc_node *ln = NULL;
     for (uint32_t s = 0; s < R; s++) {
       orc_node *n = node_at(c, g, s);
-      if (n->hosted && n->r->state == DRB_LEADER) ln = n;
+      const int here = replica ? s + 1 == replica
+                               : n->r->state == DRB_LEADER;
+      if (n->hosted && here) ln = n;
     }
     if (!ln) continue;
     for (uint32_t j = 0; j < counts[g]; j++) {

@@ -387,6 +387,11 @@ int orc_cluster_setup_steady(orc_cluster *c, uint32_t leader_slot);
 int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
                                 uint32_t max_per_group, const drb_entry *ents,
                                 const uint8_t *pool);
+/* the same at replica ID `replica` of every group (0: the leader) */
+int orc_cluster_stage_proposals_at(orc_cluster *c, const uint32_t *counts,
+                                   uint32_t max_per_group,
+                                   const drb_entry *ents, const uint8_t *pool,
+                                   uint32_t replica);
 /* stage one ReadIndex ctx per group (low==0: none) for next round */
 int orc_cluster_stage_read_index(orc_cluster *c, const uint64_t *low,
                                  const uint64_t *high);

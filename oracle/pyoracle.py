@@ -186,6 +186,8 @@ def _declare(L):
         "orc_cluster_free": (None, [P]),
         "orc_cluster_setup_steady": (C.c_int, [P, U32]),
         "orc_cluster_stage_proposals": (C.c_int, [P, PU32, U32, PE, PU8]),
+        "orc_cluster_stage_proposals_at": (C.c_int, [P, PU32, U32, PE, PU8,
+                                                     U32]),
         "orc_cluster_stage_read_index": (C.c_int, [P, PU64, PU64]),
         "orc_cluster_stage_read_index_at": (C.c_int, [P, PU64, PU64, U32]),
         "orc_cluster_request_leader_transfer": (C.c_int64, [P, U32, PU32]),
@@ -773,10 +775,13 @@ class Cluster:
     def setup_steady(self, leader_slot=0):
         _check(lib().orc_cluster_setup_steady(self.p, leader_slot))
 
-    def stage_proposals(self, counts, max_per_group, ents, pool):
-        """counts: uint32[G] array; ents: Entry[G*max] array; pool: uint8."""
-        _check(lib().orc_cluster_stage_proposals(self.p, counts,
-                                                 max_per_group, ents, pool))
+    def stage_proposals(self, counts, max_per_group, ents, pool, replica=0):
+        """counts: uint32[G] array; ents: Entry[G*max] array; pool: uint8.
+        At each group's leader, or at replica ID `replica` (a follower
+        forwards them to its leader, raft.go:2103-2116)."""
+        _check(lib().orc_cluster_stage_proposals_at(self.p, counts,
+                                                    max_per_group, ents, pool,
+                                                    replica))
 
     def stage_read_index(self, low, high, replica=0):
         """One ReadIndex ctx per group at its leader, or at replica ID

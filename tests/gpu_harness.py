@@ -79,7 +79,7 @@ class Pair:
 
     def stage(self, k=1, salt=None, read_index=False, groups=None,
               key_space=256, val_len=4, prop_slot=0, ri_slot=0,
-              ri_replica=0):
+              ri_replica=0, prop_replica=0):
         salt = self.rounds if salt is None else salt
         pin = ri_in = abi.DRB_NONE
         if self.cpu:  # no client input for groups on the CPU path
@@ -88,7 +88,7 @@ class Pair:
         if k:
             counts, ents, pool = workload.build_batch(
                 self.G, k, self.seed, salt, key_space, val_len, groups)
-            self.orc.stage_proposals(counts, k, ents, pool)
+            self.orc.stage_proposals(counts, k, ents, pool, prop_replica)
             # the engine's staging layout is [g][max_props]
             mp = self.eng.cfg["max_props"]
             eents = (abi.Entry * (self.G * mp))()
@@ -107,14 +107,15 @@ class Pair:
 
     def round(self, k=1, tick=False, read_index=False, groups=None,
               reads=0, read_key_space=256, encode_saves=False, ri_replica=0,
-              listed=False, **kw):
+              listed=False, prop_replica=0, **kw):
         pin, ri_in = self.stage(k, read_index=read_index, groups=groups,
-                                ri_replica=ri_replica, **kw)
+                                ri_replica=ri_replica,
+                                prop_replica=prop_replica, **kw)
         o = self.orc.round(tick=tick)
         e = self.eng.step(tick=tick, prop_slot=pin, ri_slot=ri_in,
                           reads_per_ctx=reads, key_space=read_key_space,
                           encode_saves=encode_saves, ri_replica=ri_replica,
-                          listed=listed)
+                          listed=listed, prop_replica=prop_replica)
         self.rounds += 1
         return o, e
 
@@ -274,8 +275,9 @@ class DistPair:
     Stepped in lock-step with one oracle cluster of all G groups."""
 
     def __init__(self, G, R=5, N=8, seed=0x5EEDD8B0, window=32, E=4,
-                 **engine_kw):
+                 counted=False, **engine_kw):
         self.G, self.R, self.N, self.seed = G, R, N, seed
+        self.counted = counted  # drb_exchange_local_counted
         self.lanes = (G + N - 1) // N
         self.engs = [Engine(num_groups=self.lanes, num_replicas=R,
                             window=window, total_groups=G, place_world=N,
@@ -322,7 +324,11 @@ class DistPair:
     def lane_group(self, r, s, j):
         return self.N * j + (r - s) % self.N
 
-    def round(self, k=1, tick=False, read_index=False, groups=None):
+    def exchange(self):
+        Engine.exchange_local(self.engs, counted=self.counted)
+
+    def round(self, k=1, tick=False, read_index=False, groups=None,
+              exchange=True):
         salt = self.rounds
         pin = ri_in = abi.DRB_NONE
         if k:
@@ -358,7 +364,8 @@ class DistPair:
         o = self.orc.round(tick=tick)
         outs = [e.step(tick=tick, prop_slot=pin, ri_slot=ri_in)
                 for e in self.engs]
-        Engine.exchange_local(self.engs)
+        if exchange:
+            self.exchange()
         self.rounds += 1
         tot = {}
         for f in ("committed_entries", "applied_entries", "messages",

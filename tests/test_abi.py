@@ -66,6 +66,9 @@ STRUCTS = {
     "drb_tan_record": abi.TanRecord,
     "drb_tan_state": abi.TanState,
     "drb_tan_log": abi.TanLog,
+    "drb_worker_read": abi.WorkerRead,
+    "drb_worker_applied": abi.WorkerApplied,
+    "drb_worker_bufs": abi.WorkerBufs,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}
@@ -138,6 +141,10 @@ def test_engine_without_gpu_fails_loudly():
     dict(num_groups=64, num_replicas=3, tan_multiplexed=1, save_cap=4096),
     dict(num_groups=64, num_replicas=3, save_tan=1, tan_multiplexed=1,
          save_cap=4096, place_world=2, place_rank=0, entry_mbox=64),
+    # forwarded proposals: 4-bit entry counts, co-resident planes
+    dict(num_groups=64, num_replicas=3, forward_proposals=1, max_props=16),
+    dict(num_groups=64, num_replicas=3, forward_proposals=1, place_world=2,
+         place_rank=0, entry_mbox=4),
 ])
 def test_create_rejects_invalid_config(kw):
     """drb_engine_create validates the configuration before it touches a

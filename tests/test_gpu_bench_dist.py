@@ -1,0 +1,58 @@
+"""bench.py --gpus N starts its own ranks (one process per GPU) when no
+launcher is around it, and reports the whole job: n_gpus = N and the
+committed entries of every rank summed (dragonboat shards groups
+over its step workers, internal/server/partition.go:38).  The pool's boxes
+have one GPU, so the two ranks share it over gloo here; on a node the same
+line runs one rank per GPU over RCCL.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G, K = 4096, 4
+
+
+def _bench(*extra, env=None):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(K),
+           "--warmup", "2", "--groups", str(G), "--kv-fill", "0",
+           "--no-wire", "--no-cpu-baseline", "--host-staged", "0",
+           "--tick-every", "1"] + list(extra)
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+              "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    p = subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True,
+                       timeout=300)
+    return p
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_launches_two_ranks():
+    p = _bench("--gpus", "2", "--dist-backend", "gloo")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2
+    assert res["steps"] == K
+    c = res["counters"]
+    # every rank commits one entry per group per round at the steady state:
+    # committed_per_round is the job's total / K / world
+    assert c["committed_per_round"] == G, c
+    total = c["committed_per_round"] * K * res["n_gpus"]
+    assert abs(res["value"] * res["ms_per_step"] * K / 1e3 - total) <= \
+        1e-6 * total + 1
+    assert c["fast_path_only"], c
+
+
+def test_bench_rejects_gpus_unlike_world_size():
+    # (no GPU needed: the check runs before anything touches one)
+    p = _bench("--gpus", "2", env={"WORLD_SIZE": "1", "RANK": "0",
+                                   "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE" in p.stderr

@@ -16,6 +16,7 @@ follower.  Every hosted replica is compared with the oracle every round.
 import pytest
 
 from dragonboat_amd import abi
+from dragonboat_amd.engine import DrbError
 from oracle import pyoracle as po
 from tests import wire_ref as wr
 from tests.gpu_harness import DistPair
@@ -91,3 +92,49 @@ def test_messages_for_other_ranks_are_dropped():
     # group g's replica 1 (slot 0) is on rank g % 2: half of them are here
     acc, drop = p.engs[0].ingest(*po.build_messages(msgs))
     assert (acc, drop) == (4, 4)
+
+
+@pytest.mark.parametrize("via", ["ingest", "wire"])
+def test_ingest_waits_for_the_exchange(via):
+    """Between a round's launch and its plane exchange the inbound planes
+    still belong to the exchange: a transport's ingest then is refused with
+    DRB_EAGAIN and places nothing (otherwise the exchange's copy of the
+    plane's header would overwrite what it wrote); the same messages after
+    the exchange land and are stepped bit-exact."""
+    G, N, R = 16, 2, 3
+    p = DistPair(G=G, R=R, N=N, E=8, max_props=2)
+    _host_elsewhere(p, 0)  # the CPU NodeHost holds the leaders
+    mine = [1, 2]
+    refused = 0
+    for r in range(8):
+        o, e = p.round(k=1, tick=(r % 2 == 0), exchange=False)
+        assert e["fallbacks"] == 0 and e["errors"] == 0, (r, e, p.why())
+        sends = _cpu_sends(p, 0)
+        for rank, msgs in sends.items():
+            if not msgs:
+                continue
+            eng = p.engs[rank]
+            with pytest.raises(DrbError, match="status -6"):
+                if via == "ingest":
+                    eng.ingest(*po.build_messages(msgs))
+                else:
+                    eng.ingest_wire(wr.expected_stream(msgs, DID, b"cpu:1"),
+                                    DID)
+            refused += 1
+        p.exchange()
+        for rank, msgs in sends.items():
+            if not msgs:
+                continue
+            eng = p.engs[rank]
+            if via == "ingest":
+                acc, drop = eng.ingest(*po.build_messages(msgs))
+            else:
+                got = eng.ingest_wire(wr.expected_stream(msgs, DID, b"cpu:1"),
+                                      DID)
+                acc, drop = got["accepted"], got["dropped"]
+            assert (acc, drop) == (len(msgs), 0), (r, rank, acc, drop)
+        errs = p.check(slots=mine)
+        assert not errs, (r, errs[:2])
+    assert refused > 0
+    assert all(p.replica(g, s).sm_index == p.orc.export(g, s).sm_index > 3
+               for g in range(G) for s in mine)

@@ -13,9 +13,11 @@ KV contents, the outbox, the served-read checksums and the EntriesToSave
 bytes + CRC.
 """
 import random
+import struct
 
 import pytest
 
+import bench
 from dragonboat_amd import workload
 from dragonboat_amd.engine import Engine
 from oracle import pyoracle as po
@@ -69,9 +71,11 @@ def test_fullsize_c3_sampled():
     generators, a LocalTick every round, 9 served reads per ctx, which now
     mostly find their key."""
     G, R, NP, FILL = 1 << 20, 3, 8, 400
+    # bench.py's C3 engine: the timed reads leave every client's result
     eng = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
                  max_props=1, prop_slots=NP, ri_slots=NP, mailbox=16,
-                 kv_slots=512, kv_val_cap=4)
+                 kv_slots=512, kv_val_cap=4,
+                 max_reads_per_ctx=bench.READS_PER_CTX)
     eng.init_steady(term=2, leader_slot=0, seed=SEED)
     gids = _sample(G)
     n = len(gids)
@@ -115,6 +119,8 @@ def test_fullsize_c3_sampled():
                 x = sums[i * R + s]
                 if x is not None:
                     assert esum[g * R + s] == x, (r, g, s)
+        if r % 4 == 3:  # the ReadLocalNode results of the sampled groups
+            _compare_read_results(eng, orc, gids, r)
         if r % 8 == 7:
             errs = _compare(eng, orc, gids, R)
             assert not errs, (r, errs[:3])
@@ -129,6 +135,30 @@ def test_fullsize_c3_sampled():
                 total += 1
                 found += key.to_bytes(8, "little") in kv
     assert found > 0.7 * total
+
+
+def _compare_read_results(eng, orc, gids, rnd, slot=0, reads=9, keys=256):
+    """drb_export_read_results of the sampled groups against the oracle:
+    per served read of every ReadyToRead whose index the replica applied,
+    the key, found, length and value (request.go:930-953 ->
+    nodehost.go:849 -> KVTest.Lookup, kvtest.go:164-175)."""
+    for i in range(0, len(gids), 7):
+        g = gids[i]
+        got = eng.export_read_results(slot, g, 1)
+        st = orc.export(i, slot)
+        kv = orc.export_kv(i, slot)
+        want = []
+        for (index, low, high) in orc.export_ready(i, slot):
+            if index > st.sm_index:
+                continue
+            for j in range(reads):
+                key = workload.mix64(low ^ (((j + 1) * workload.GOLDEN) &
+                                            workload.MASK)) % keys
+                v = kv.get(struct.pack("<Q", key))
+                want.append((g, index, low, j, key, int(v is not None),
+                             len(v) if v is not None else 0,
+                             int.from_bytes((v or b"")[:4], "little")))
+        assert got == want, (rnd, g, got[:2], want[:2])
 
 
 def test_fullsize_five_replicas_sampled():
@@ -155,43 +185,87 @@ def test_fullsize_five_replicas_sampled():
     assert not errs, errs[:3]
 
 
-@pytest.mark.parametrize("payload,rounds", [(128, 240), (1024, 40)])
-def test_fullsize_c5_sampled(payload, rounds):
-    """C5 as bench.py runs it: 4,194,304 groups, a fresh seeded 1 % of
-    them proposing each round (device generator, salt = round), values out
-    of line, EntriesToSave encoded, Quiesce on, listed rounds."""
-    G, R = 4 << 20, 3
-    vlen = {128: 116, 1024: 1011}[payload]
+def _c5_engine(G, R, payload, rounds, active_ppm, kv_slots=None,
+               ovf_buckets=None, save_extra=0, **kw):
+    """bench.py's C5 engine (bench.py main): kv_slots = C5_SLOTS, overflow
+    buckets G*R*C5_OVF_PER + 1024 from one engine-wide pool, the values in
+    one shared block pool sized by c5_pool_blocks for the rounds run."""
+    vlen = bench.C5_VAL[payload]
     cmd_cap = ((12 + (1 if vlen < 128 else 2) + vlen) + 15) // 16 * 16
     bound = 73 + cmd_cap
-    ks = 16 if payload == 128 else 8
     eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
                  max_props=1, prop_slots=2, ri_slots=1, mailbox=8,
-                 kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
-                 kv_pool_blocks=ks * G * R if payload == 128 else 4 * G * R,
-                 save_cap=(4 * bound + 15) // 16 * 16, quiesce=1)
-    eng.init_steady(term=2, leader_slot=0, seed=SEED)
-    gids = _sample(G, 1000)
+                 kv_slots=kv_slots or bench.C5_SLOTS,
+                 kv_val_cap=vlen + 13 & ~15,
+                 kv_pool_blocks=bench.c5_pool_blocks(G, R, rounds,
+                                                     active_ppm),
+                 kv_overflow_buckets=(ovf_buckets if ovf_buckets is not None
+                                      else int(G * R * bench.C5_OVF_PER) +
+                                      1024),
+                 save_cap=(4 * bound + 15) // 16 * 16 + save_extra, quiesce=1,
+                 **kw)
+    return eng, vlen
+
+
+def _c5_run(eng, orc, gids, R, vlen, rounds, active_ppm, check_every):
     n = len(gids)
-    orc = po.Cluster(n, R, seed=SEED, gids=gids, quiesce=True)
-    orc.setup_steady(0)
     for r in range(rounds):
-        act = workload.active_groups(n, SEED, r, 10000, gids=gids)
-        counts, ents, pool = workload.build_batch(n, 1, SEED, r, 256, vlen,
+        act = workload.active_groups(n, SEED, r, active_ppm, gids=gids)
+        counts, ents, pool = workload.build_batch(n, 1, SEED, r,
+                                                  bench.C5_KEYS, vlen,
                                                   groups=act, gids=gids)
         orc.stage_proposals(counts, 1, ents, pool)
-        eng.gen_kv_proposals(r % 2, 1, 256, vlen, SEED, r, active_ppm=10000)
+        eng.gen_kv_proposals(r % 2, 1, bench.C5_KEYS, vlen, SEED, r,
+                             active_ppm=active_ppm)
         o = orc.round(tick=True)
         e = eng.step(tick=True, prop_slot=r % 2, encode_saves=True,
                      listed=True)
         assert e.fallbacks == 0 and e.errors == 0, (r, e.to_dict())
-        if r % 60 == 59 or r == rounds - 1:
+        if r % check_every == check_every - 1 or r == rounds - 1:
             errs = _compare(eng, orc, gids, R, saves=True)
             assert not errs, (r, errs[:3])
+
+
+@pytest.mark.parametrize("payload,rounds", [(128, 240), (1024, 40)])
+def test_fullsize_c5_sampled(payload, rounds):
+    """C5 as bench.py runs it, with bench.py's own engine arguments:
+    4,194,304 groups, a fresh seeded 1 % of them proposing each round
+    (device generator, salt = round) over the 256-key space, values out of
+    line in the shared pool, KV overflow buckets, EntriesToSave encoded,
+    Quiesce on, listed rounds."""
+    G, R = 4 << 20, 3
+    eng, vlen = _c5_engine(G, R, payload, rounds, 10000)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    gids = _sample(G, 1000)
+    orc = po.Cluster(len(gids), R, seed=SEED, gids=gids, quiesce=True)
+    orc.setup_steady(0)
+    _c5_run(eng, orc, gids, R, vlen, rounds, 10000, 60)
+    n = len(gids)
     qs = sum(orc.export(i, s).qs_quiesced_since > 0
              for i in range(n) for s in range(R))
     if rounds > 220:
         assert qs > 0  # some sampled groups went quiet past the threshold
+
+
+def test_fullsize_c5_overflow_chains():
+    """The KV overflow chains at full size: 4-slot tables at 4,194,304
+    groups x 3 and a quarter of the groups proposing every round, so that
+    most replicas hold several times their table's keys -- chains of
+    buckets bump-allocated from the one engine-wide pool by 12.6 M
+    replicas at once (kvtest.go:145-162: KVTest's map grows).  Every
+    sampled replica's whole KV (table and chain) equals the oracle's."""
+    G, R, rounds, ppm = 4 << 20, 3, 40, 250000
+    eng, vlen = _c5_engine(G, R, 128, rounds, ppm, kv_slots=4,
+                           ovf_buckets=3 * G * R)
+    eng.init_steady(term=2, leader_slot=0, seed=SEED)
+    gids = _sample(G, 600)
+    orc = po.Cluster(len(gids), R, seed=SEED, gids=gids, quiesce=True)
+    orc.setup_steady(0)
+    _c5_run(eng, orc, gids, R, vlen, rounds, ppm, 20)
+    sizes = [len(eng.kv_export(g, s)) for g in gids for s in range(R)]
+    chained = sum(x > 4 for x in sizes)
+    assert chained > len(sizes) // 2, (chained, len(sizes))
+    assert max(sizes) >= 12, max(sizes)  # chains of two buckets and more
 
 
 def test_fullsize_failover_sampled():
@@ -257,15 +331,8 @@ def test_fullsize_c5_tan_sampled():
     check rounds the GPU's record of the round -- bytes, offset, sync, log
     -- and its writer position equal the oracle's."""
     G, R = 4 << 20, 3
-    vlen = 116
-    cmd_cap = ((12 + 1 + vlen) + 15) // 16 * 16
-    bound = 73 + cmd_cap
-    eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
-                 max_props=1, prop_slots=2, ri_slots=1, mailbox=8,
-                 kv_slots=16, kv_val_cap=vlen + 13 & ~15,
-                 kv_pool_blocks=16 * G * R,
-                 save_cap=(4 * bound + 15) // 16 * 16 + 128, save_tan=1,
-                 quiesce=1)
+    # bench.py's C5 engine with --save tan (its save_cap + 128)
+    eng, vlen = _c5_engine(G, R, 128, 48, 10000, save_extra=128, save_tan=1)
     eng.init_steady(term=2, leader_slot=0, seed=SEED)
     gids = _sample(G, 500)
     n = len(gids)
@@ -275,10 +342,12 @@ def test_fullsize_c5_tan_sampled():
     checked = 0
     for r in range(48):
         act = workload.active_groups(n, SEED, r, 10000, gids=gids)
-        counts, ents, pool = workload.build_batch(n, 1, SEED, r, 256, vlen,
+        counts, ents, pool = workload.build_batch(n, 1, SEED, r,
+                                                  bench.C5_KEYS, vlen,
                                                   groups=act, gids=gids)
         orc.stage_proposals(counts, 1, ents, pool)
-        eng.gen_kv_proposals(r % 2, 1, 256, vlen, SEED, r, active_ppm=10000)
+        eng.gen_kv_proposals(r % 2, 1, bench.C5_KEYS, vlen, SEED, r,
+                             active_ppm=10000)
         o = orc.round(tick=True)
         e = eng.step(tick=True, prop_slot=r % 2, encode_saves=True,
                      listed=True)

@@ -224,16 +224,19 @@ def test_entries_to_save_capacity_falls_back():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,R,G", [(8, 5, 44), (2, 3, 30), (3, 5, 31),
-                                   (4, 3, 20)])
-def test_replicas_spread_over_ranks_c4(N, R, G):
+@pytest.mark.parametrize("N,R,G,counted", [
+    (8, 5, 44, False), (2, 3, 30, False), (3, 5, 31, False),
+    (4, 3, 20, False), (8, 5, 44, True), (3, 5, 31, True)])
+def test_replicas_spread_over_ranks_c4(N, R, G, counted):
     """C4 placement: replica slot s of group g on rank
     (g + s) mod N; every cross-rank message and its entries travel in the
     mailbox planes moved between the ranks' engines (drb_plane_regions --
-    what RCCL moves between GPUs, here drb_exchange_local on one GPU).
-    Bit-exact against one oracle cluster of all G groups."""
+    what RCCL moves between GPUs, here drb_exchange_local on one GPU: the
+    full-capacity planes behind cross-stream events, or the counted sizes
+    with host synchronisation).  Bit-exact against one oracle cluster of
+    all G groups."""
     from tests.gpu_harness import DistPair
-    p = DistPair(G=G, R=R, N=N, max_props=4)
+    p = DistPair(G=G, R=R, N=N, max_props=4, counted=counted)
     assert not p.check(), "init"
     for r in range(12):
         k = 1 if r % 5 != 4 else (3 if r % 2 else 0)

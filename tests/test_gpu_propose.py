@@ -1,0 +1,188 @@
+"""GPU: proposals made at any replica (drb_round_in.prop_replica with
+drb_config.forward_proposals).
+
+A client may propose at any NodeHost.  The follower's node hands its entry
+queue to raft (node.handleProposals, node.go:1275-1294), which forwards it
+to the leader as a Propose message (handleFollowerPropose,
+raft.go:2103-2116; dropped while no leader is known), and the leader
+appends the received entries (handleLeaderPropose, raft.go:1794-1815) when
+it handles that message, in inbox order.  On the GPU the Propose travels as
+a mailbox record with its entries by value in the sender's forward rows;
+Proposes from another NodeHost arrive through drb_ingest and
+drb_ingest_wire.  Every round is compared with the oracle cluster (the
+reference step loop, pinned by TestProposal / TestProposalByProxy in
+tests/test_oracle_propose_kat.py): every replica field, the logs, the KV,
+the outboxes (the forwarded Propose with its entries included) and the
+ReadyToReads.  No replica leaves the GPU.
+"""
+import pytest
+
+from dragonboat_amd import abi, workload
+from oracle import pyoracle as po
+from tests import wire_ref as wr
+from tests.gpu_harness import Pair
+
+pytestmark = pytest.mark.gpu
+
+MSG = abi.MSG
+DID = 0xD1D
+
+
+def _round(p, stats=None, **kw):
+    o, e = p.round(**kw)
+    assert e.fallbacks == 0 and e.errors == 0, (p.rounds, e.to_dict(),
+                                                 p.why())
+    assert (e.committed_entries, e.messages, e.dropped_proposals) == \
+        (o.committed_entries, o.messages, o.dropped_proposals), \
+        (p.rounds, e.to_dict(), o.to_dict())
+    errs = p.check()
+    assert not errs, (p.rounds, errs[:2])
+    if stats is not None:
+        stats["committed"] += e.committed_entries
+        stats["dropped"] += e.dropped_proposals
+        stats["slow"] += e.elections_stepped
+    return e
+
+
+@pytest.mark.parametrize("R,k", [(3, 1), (3, 3), (5, 2)])
+def test_proposals_at_a_follower(R, k):
+    """Every group's entry queue is at replica 2 (a follower): each round's
+    proposals reach the leader a round later and commit like the leader's
+    own; ReadIndex at the leader and ticks every other round go on."""
+    G = 48
+    p = Pair(G=G, R=R, forward_proposals=1, max_props=k, mailbox=16)
+    st = {"committed": 0, "dropped": 0, "slow": 0}
+    for r in range(14):
+        _round(p, st, k=k, tick=(r % 2 == 0), read_index=(r % 3 == 0),
+               prop_replica=2)
+    assert st["committed"] >= G * k * 10 and st["dropped"] == 0, st
+
+
+def test_proposals_at_every_nodehost():
+    """The entry queue moves between NodeHosts round by round: the leader
+    (0 and its own ID), each follower, ragged groups."""
+    G, R = 40, 5
+    p = Pair(G=G, R=R, forward_proposals=1, max_props=2, mailbox=16)
+    st = {"committed": 0, "dropped": 0, "slow": 0}
+    for r in range(20):
+        groups = [g for g in range(G) if (g + r) % 4]
+        _round(p, st, k=1 + r % 2, tick=(r % 3 == 0), groups=groups,
+               read_index=(r % 2 == 1), prop_replica=[0, 1, 2, 3, 4, 5][r % 6])
+    assert st["committed"] > G * 8 and st["dropped"] == 0, st
+
+
+def test_proposals_at_followers_through_a_failover():
+    """Elections on the GPU: the leader stops while replica 2 keeps taking
+    proposals.  Followers forward to the stopped leader (lost with it), a
+    candidate drops them (handleCandidatePropose, raft.go:2197-2201), and
+    once a new leader is elected the followers forward to it -- or, where
+    replica 2 itself won, it appends them as the leader."""
+    G, R = 24, 3
+    p = Pair(G=G, R=R, elections=1, forward_proposals=1, max_props=1,
+             mailbox=16)
+    st = {"committed": 0, "dropped": 0, "slow": 0}
+    for r in range(3):
+        _round(p, st, k=1, tick=True, prop_replica=2)
+    for g in range(G):
+        p.orc.set_hosted(g, 0, False)
+    p.eng.host_slot(0, False)
+    elected = False
+    for r in range(60):
+        _round(p, st, k=1, tick=True, prop_replica=2 + (r % 2))
+        roles = [[x.role for x in p.eng.export_replicas(g, 1)] for g in
+                 range(G)]
+        if all(abi.LEADER in rs[1:] for rs in roles):
+            elected = True
+            break
+    assert elected and st["slow"] > 0 and st["dropped"] > 0, st
+    c0 = st["committed"]
+    for r in range(8):
+        _round(p, st, k=1, tick=(r % 2 == 0), prop_replica=2 + (r % 2))
+    assert st["committed"] - c0 >= G * 6, st
+
+
+def _unhost(p, groups, slot):
+    for g in groups:
+        p.orc.set_hosted(g, slot, False)
+        sts = p.eng.export_replicas(g, 1)
+        sts[slot].flags &= ~abi.F_HOSTED
+        p.eng.import_replicas(g, sts)
+
+
+@pytest.mark.parametrize("via", ["ingest", "wire"])
+def test_proposals_from_another_nodehost(via):
+    """Replica 3 lives on another NodeHost: its clients' proposals come in
+    as that node's Propose messages (with entries of 16 B, 60 B and
+    NoOP-session empty Cmds), through drb_ingest or as TCP bytes through
+    drb_ingest_wire, and the GPU leader appends them.  A second Propose of
+    the same sender in one round is dropped as by a full queue, on both
+    sides alike (the oracle receives only the first)."""
+    G, R = 30, 3
+    p = Pair(G=G, R=R, forward_proposals=1, max_props=3, mailbox=16,
+             kv_val_cap=64, cmd_cap=96)
+    st = {"committed": 0, "dropped": 0, "slow": 0}
+    for _ in range(2):
+        _round(p, st, k=1, tick=True)
+    _unhost(p, range(G), 2)
+    _round(p, st, k=1, tick=True)
+    for r in range(6):
+        msgs = []
+        for g in range(G):
+            n = 1 + (g + r) % 3
+            vl = [4, 60, 0][(g + r) % 3]
+            es = []
+            for j in range(n):
+                d = workload.proposal(p.seed, g, 1000 + r, j, 256,
+                                      vl if vl else 4)
+                if vl == 0:  # a NoOP-session empty proposal
+                    d = dict(d, client_id=0, cmd=b"", type=0)
+                es.append(po.ent(key=d["key"], client_id=d["client_id"],
+                                 type=d["type"], cmd=d["cmd"]))
+            msgs.append(po.msg(MSG["Propose"], from_=3, to=1, shard_id=g + 1,
+                               entries=es))
+        p.orc.ingest(msgs)
+        extra = [po.msg(MSG["Propose"], from_=3, to=1, shard_id=g + 1,
+                        entries=[po.ent(key=7)]) for g in range(0, G, 7)]
+        if via == "ingest":
+            marr, n, earr, pool = po.build_messages(msgs + extra)
+            acc, drop = p.eng.ingest(marr, n, earr, pool)
+        else:
+            data = wr.expected_stream(msgs + extra, DID, b"10.0.0.9:26001")
+            got = p.eng.ingest_wire(data, DID)
+            acc, drop = got["accepted"], got["dropped"]
+        assert (acc, drop) == (len(msgs), len(extra)), (acc, drop)
+        _round(p, st, k=1, tick=(r % 2 == 0))
+    _round(p, st, k=1, tick=True)
+    assert st["committed"] > G * 6, st
+
+
+def test_stepped_down_leader_forwards_its_queue():
+    """Elections: a leader whose inbox brings a higher-term leader's
+    message steps down before handleProposals, learns the new leader and
+    forwards its entry queue to it (handleFollowerPropose) instead of
+    leaving the round to the CPU path."""
+    G, R = 16, 3
+    p = Pair(G=G, R=R, elections=1, forward_proposals=1, max_props=1,
+             mailbox=16)
+    st = {"committed": 0, "dropped": 0, "slow": 0}
+    for r in range(3):
+        _round(p, st, k=1, tick=True)
+    E = list(range(0, G, 3))
+    _unhost(p, E, 0)
+    for r in range(60):
+        _round(p, st, k=1, tick=True, groups=[g for g in range(G)
+                                              if g not in E])
+        if all(abi.LEADER in [x.role for x in p.eng.export_replicas(g, 1)][1:]
+               for g in E):
+            break
+    # the old leaders return with proposals queued at them (replica 1)
+    for g in E:
+        p.orc.set_hosted(g, 0, True)
+        sts = p.eng.export_replicas(g, 1)
+        sts[0].flags |= abi.F_HOSTED
+        p.eng.import_replicas(g, sts)
+    for r in range(8):
+        _round(p, st, k=1, tick=True, prop_replica=1)
+    for g in E:
+        roles = [x.role for x in p.eng.export_replicas(g, 1)]
+        assert roles[0] == abi.FOLLOWER and roles.count(abi.LEADER) == 1
