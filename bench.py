@@ -147,6 +147,11 @@ def parse():
                          "behind the round (no host sync) or sized by an "
                          "all_gather of per-plane counts (dragonboat_amd/"
                          "exchange.py)")
+    ap.add_argument("--local-ranks", type=int, default=0,
+                    help="c4 in ONE process on one GPU: N engines (ranks of "
+                         "the placement) stepped together, their planes "
+                         "moved by drb_exchange_local (the device pull, no "
+                         "host synchronisation)")
     ap.add_argument("--host-staged", type=int, default=-1,
                     help="after the timed region, also time rounds whose "
                          "proposals come from host memory through "
@@ -246,6 +251,100 @@ def cpu_baseline(args, seconds):
                            else "writes only"))
 
 
+def run_c4_local(args):
+    """C4 placement with every rank's engine in this process on one GPU
+    (NodeHost is one process per machine): N engines hold replica slot s of
+    global group g at rank (g + s) mod N, lane g // N; every round each
+    engine's step is enqueued on its own stream, then drb_exchange_local
+    moves the planes (a pull kernel per receiver behind cross-stream
+    events).  The host never waits inside the timed loop."""
+    import torch
+    from dragonboat_amd import dist as ddist
+    from dragonboat_amd.engine import Engine
+    N, G, k = args.local_ranks, args.groups, args.k
+    R = args.replicas or 5
+    lanes = (G + N - 1) // N
+    NP = max(8, args.steps)
+    seed = ddist.BASE_SEED
+    torch.cuda.set_device(0)
+    engs = [Engine(num_groups=lanes, num_replicas=R, window=32, cmd_cap=32,
+                   max_props=max(1, k), prop_slots=NP, ri_slots=NP, mailbox=8,
+                   kv_slots=512, kv_val_cap=4, total_groups=G, place_world=N,
+                   place_rank=r, entry_mbox=k + 2, device=0)
+            for r in range(N)]
+    for e in engs:
+        e.init_steady(term=2, leader_slot=0, seed=seed)
+
+    def rnd(i, b, tick):
+        for e in engs:
+            e.step_async(tick=tick, prop_slot=b)
+        Engine.exchange_local(engs)
+
+    WARM, TIMED = 1 << 21, 1 << 22
+    for i in range(args.warmup):
+        for e in engs:
+            e.gen_kv_proposals(0, k, KEY_SPACE, 4, seed, WARM + i)
+        rnd(i, 0, True)
+    for b in range(args.steps):
+        for e in engs:
+            e.gen_kv_proposals(b, k, KEY_SPACE, 4, seed, TIMED + b)
+    for e in engs:
+        e.sync()
+        e.read_counters(reset=True)
+        e.exchange_bytes(reset=True)
+    torch.cuda.synchronize()
+    K = args.steps
+    te = max(1, args.tick_every or 1)
+    t0 = time.perf_counter()
+    for i in range(K):
+        rnd(i, i, i % te == 0)
+    for e in engs:
+        e.sync()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    outs = [e.read_counters(reset=True) for e in engs]
+    xb = [e.exchange_bytes(reset=True) for e in engs]
+    committed = sum(o.committed_entries for o in outs)
+    fb = sum(o.fallbacks + o.errors for o in outs)
+    alg = alg_bytes_per_group_round(R, k, 16, False, True) * G
+    res = {
+        "metric": "committed entries/sec (node) at %d 5-replica groups spread "
+                  "over %d in-process ranks on one GPU, 16B payload" % (G, N),
+        "value": committed / el, "unit": "committed entries/s",
+        "n_gpus": 1, "steps": K, "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / K, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (SURVEY 8d seeded PBKV writes)",
+        "config": {
+            "workload": "C4 placement in one process: %d groups x %d "
+                        "replicas, slot s of group g at local rank (g + s) "
+                        "mod %d, 16B PBKV writes k=%d/group/round, tick "
+                        "every %d round(s)" % (G, R, N, k, te),
+            "local_ranks": N, "groups_per_rank": lanes, "replicas": R,
+            "parallelism": "replicas spread over %d engines of one process "
+                           "on one GPU; drb_exchange_local (device pull)" % N},
+        "exchange": {
+            "bytes_per_round": sum(xb) / K,
+            "bytes_per_round_per_rank": sum(xb) / K / N,
+            "note": "inbound plane bytes the pull kernels moved (headers of "
+                    "the round, counted records, entry rows), "
+                    "drb_exchange_bytes"},
+        "roofline": {"bound": "hbm", "alg_bytes_per_round": alg,
+                     "achieved": alg / (el / K) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s",
+                     "frac": alg / (el / K) / 1e9 / HBM_PEAK_GBS,
+                     "note": "wall time per round of all N engines, "
+                             "exchange included"},
+        "counters": {"committed_per_round": committed / K,
+                     "fallbacks_and_errors": fb,
+                     "messages": sum(o.messages for o in outs)},
+    }
+    print(json.dumps(res))
+    for e in engs:
+        e.close()
+    return 0
+
+
 def self_launch(args):
     """bench.py --gpus N with no launcher around it: start N ranks, one
     process per GPU, as the driver's own torch.distributed.run line would,
@@ -273,6 +372,10 @@ def main():
                      % (args.gpus, os.environ["WORLD_SIZE"]))
     elif args.gpus is not None and args.gpus > 1:
         sys.exit(self_launch(args))
+    if args.local_ranks > 1:
+        if args.workload != "c4" or "WORLD_SIZE" in os.environ:
+            sys.exit("bench.py: --local-ranks is the one-process c4 run")
+        return run_c4_local(args)
     import torch
     import torch.distributed as dist
     from dragonboat_amd import dist as ddist

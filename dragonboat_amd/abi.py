@@ -137,7 +137,9 @@ class Config(C.Structure):
                 ("tan_multiplexed", C.c_uint32), ("pre_vote", C.c_uint32),
                 ("max_reads_per_ctx", C.c_uint32),
                 ("kv_overflow_buckets", C.c_uint64),
-                ("forward_proposals", C.c_uint32)]
+                ("forward_proposals", C.c_uint32),
+                ("nonvoting_slots", C.c_uint32),
+                ("witness_slots", C.c_uint32)]
 
 
 class ReadResult(C.Structure):

@@ -82,6 +82,8 @@ def _compile(args):
     t0 = time.time()
     subprocess.check_call(cmd)
     os.replace(tmp, obj)
+    # dated when the compile started: a source edited meanwhile is newer
+    os.utime(obj, (t0, t0))
     if verbose:
         print("%6.1f s  %s" % (time.time() - t0, os.path.basename(obj)),
               file=sys.stderr)
@@ -95,6 +97,7 @@ def build(force=False, verbose=False, out=None, defines=(), jobs=None,
     directory of their own, keyed by the defines), everything else from the
     in-tree build."""
     target = LIB if out is None else out
+    t_start = time.time()
     if out is None and not force and up_to_date():
         return LIB
     key = hashlib.sha1(" ".join(sorted(defines)).encode()).hexdigest()[:10]
@@ -126,6 +129,7 @@ def build(force=False, verbose=False, out=None, defines=(), jobs=None,
         print(" ".join(cmd[:6]) + " <%d objects>" % len(objs), file=sys.stderr)
     subprocess.check_call(cmd)
     os.replace(tmp, target)
+    os.utime(target, (t_start, t_start))  # (as the objects, _compile)
     return target
 
 

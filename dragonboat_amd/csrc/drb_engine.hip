@@ -87,6 +87,10 @@ struct drb_engine {
   uint32_t reads_n = 0, reads_ks = 0;
   void *xout = nullptr;  // batch exports' device output (grow-only)
   size_t xout_bytes = 0;
+  // drb_exchange_bytes: inbound plane bytes of the device pull (a device
+  // counter) and of region copies (host-side sum)
+  unsigned long long *xpull_bytes = nullptr;
+  uint64_t xcopy_bytes = 0;
 };
 
 static void wire_free(drb_engine *e);
@@ -239,6 +243,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
        cfg->entry_mbox > cfg->window || cfg->entry_mbox > 255))
     return DRB_EINVAL;
   if (cfg->election_rtt == 0 || cfg->heartbeat_rtt == 0) return DRB_EINVAL;
+  // member kinds: a slot is one kind; some voting member remains
+  if ((cfg->nonvoting_slots & cfg->witness_slots) ||
+      ((cfg->nonvoting_slots | cfg->witness_slots) >> cfg->num_replicas) ||
+      __builtin_popcount(cfg->nonvoting_slots | cfg->witness_slots) >=
+          (int)cfg->num_replicas)
+    return DRB_EINVAL;
   // forwarded proposals: a Propose's entry count travels in 4 header bits
   // (MI_NPROP); co-resident planes only
   if (cfg->forward_proposals &&
@@ -314,6 +324,9 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   v.heartbeat_rtt = cfg->heartbeat_rtt;
   v.check_quorum = cfg->check_quorum;
   v.quiesce = cfg->quiesce ? 1u : 0u;
+  v.nv_mask = cfg->nonvoting_slots;
+  v.wt_mask = cfg->witness_slots;
+  v.quorum = (uint32_t)(R - __builtin_popcount(v.nv_mask)) / 2 + 1;
   v.first_shard_id = cfg->first_shard_id;
   v.place_world = cfg->place_world > 1 ? cfg->place_world : 1;
   v.place_rank = v.place_world > 1 ? cfg->place_rank : 0;
@@ -942,7 +955,10 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
   // the same), one splitmix64 draw per randomized timeout afterwards
   v.u64[u64_ix(v, F_RNG, s, g)] =
       mix64(seed ^ (0xE2ull << 56) ^ (gid(v, s, g) * R + s));
-  v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader ? DRB_LEADER : DRB_FOLLOWER;
+  v.u32[u32_ix(v, W_ROLE, s, g)] = is_leader                  ? DRB_LEADER
+                                  : (v.nv_mask >> s) & 1u ? DRB_NONVOTING
+                                  : (v.wt_mask >> s) & 1u ? DRB_WITNESS
+                                                          : DRB_FOLLOWER;
   v.u32[u32_ix(v, W_FLAGS, s, g)] =
       gid(v, s, g) < v.total_groups ? DRB_F_HOSTED : 0u;
   v.u32[u32_ix(v, W_FB_REASON, s, g)] = 0;
@@ -993,6 +1009,8 @@ __global__ void k_init_steady(View v, uint64_t term, uint32_t leader,
 extern "C" int drb_init_steady(drb_engine *e, uint64_t term,
                                uint32_t leader_slot, uint64_t seed) {
   if (!e || leader_slot >= e->cfg.num_replicas || term < 2) return DRB_EINVAL;
+  if (((e->v.nv_mask | e->v.wt_mask) >> leader_slot) & 1u)
+    return DRB_EINVAL;  // the leader is a voting member
   if (e->cfg.cmd_cap < 32 || e->v.W < e->cfg.num_replicas + 2)
     return DRB_EINVAL;
   e->v.stage_slot = leader_slot;  // staged inputs go to the leaders
@@ -1914,10 +1932,11 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   pf.nrows = nf;
   // one-dimensional grids, rows interleaved per XCD (block_pos)
   const StepLaunchFn *launch = kStepLaunch[R - 1];
-  // forwarded proposals: the EXT kernels with the Propose paths
-  const int kl = e->v.fwd_props ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
-  const int kf = e->v.fwd_props ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT
-                                                     : SK_FOLLOW;
+  // forwarded proposals and member kinds: the EXT kernels with the Propose
+  // and nonVoting / witness paths
+  const bool fwd = e->v.fwd_props || e->v.nv_mask || e->v.wt_mask;
+  const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
+  const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
   if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
@@ -2046,10 +2065,15 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   p.prop_replica = in->prop_replica;
   if (p.prop_replica > e->v.R || (p.prop_replica && !e->v.fwd_props))
     return DRB_EINVAL;
-  if (e->v.elections)  // this round's slow list
-    HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
   if (p.ri_replica > e->v.R || (p.ri_replica && e->v.place_world > 1))
     return DRB_EINVAL;
+  // a witness neither proposes nor reads: ErrInvalidOperation (node.go:
+  // 425-429, nodehost.go:823, 909)
+  if ((p.prop_replica && ((e->v.wt_mask >> (p.prop_replica - 1)) & 1u)) ||
+      (p.ri_replica && ((e->v.wt_mask >> (p.ri_replica - 1)) & 1u)))
+    return DRB_EINVAL;
+  if (e->v.elections)  // this round's slow list
+    HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
   if (e->v.remote_mask)  // plane summaries of this round only
     HIPCHK(hipMemsetAsync(e->v.xrows, 0,
                           2ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
@@ -2400,9 +2424,20 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
       int rc = drb_export_log(e, g, from, m.log_index + 1, m.log_index + ne_,
                               ents + *ne, pool + *np, pcap - *np);
       if (rc) return rc;
+      const bool wt = (v.wt_mask >> to) & 1u;
       for (uint64_t q2 = 0; q2 < ne_; ++q2) {
-        ents[*ne + q2].cmd_off += *np;
-        used += ents[*ne + q2].cmd_len;
+        drb_entry &en = ents[*ne + q2];
+        used += en.cmd_len;  // the pool bytes drb_export_log wrote
+        if (wt && en.type != DRB_ENTRY_CONFIG_CHANGE) {
+          // a witness is sent metadata entries (makeMetadataEntries,
+          // raft.go:771-785)
+          const uint64_t t = en.term, x = en.index;
+          memset(&en, 0, sizeof(en));
+          en.type = DRB_ENTRY_METADATA;
+          en.term = t;
+          en.index = x;
+        }
+        en.cmd_off += *np;
       }
       *ne += ne_;
       *np += used;
@@ -2654,9 +2689,11 @@ static int exchange_copy(drb_engine *const *engines, uint32_t n,
         const int ns = drb_plane_regions(engines[r], a, b, w, 0, src);
         const int nd = drb_plane_regions(dst, a, b, w, 1, dreg);
         if (ns < 0 || ns != nd) return DRB_EINVAL;
-        for (int q = 0; q < ns; ++q)
+        for (int q = 0; q < ns; ++q) {
           HIPCHK(hipMemcpyAsync(dreg[q].ptr, src[q].ptr, src[q].bytes,
                                 hipMemcpyDefault, dst->stream));
+          dst->xcopy_bytes += src[q].bytes;
+        }
       }
   return DRB_OK;
 }
@@ -2673,11 +2710,142 @@ static uint32_t full_word(const View &v, bool leader_sender) {
   return ((v.MB & 0x1fu) << 5) | f;
 }
 
+// ---- the one-device pull: every engine of the process on one GPU
+// A receiver's kernel reads each sender's outbox plane header and copies,
+// lane by lane, what the header counts: the header, the Replicate records
+// [0, nrep) and the others [MB - noth, MB) (both chunks; with elections
+// their rterm rows), the max-append word, and the entry rows [elo, maxapp]
+// -- the bytes a counted exchange moves, with no host round trip.  A lane
+// whose sender header is not of this round keeps its inbound plane as it is
+// (its receiver reads only headers of the round, tag_is).
+constexpr uint32_t PULL_MAX = 16;
+struct PullSrc {
+  const uint4 *mbox, *meta, *embox;
+  const uint64_t *maxapp, *elo, *rterm;
+};
+struct PullArgs {
+  PullSrc src[PULL_MAX];
+  uint32_t N, d, buf;
+  uint32_t tag;
+};
+
+__global__ void __launch_bounds__(256)
+    k_plane_pull(View v, PullArgs a, unsigned long long *bytes) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t from = blockIdx.y / v.R, to = blockIdx.y % v.R;
+  uint64_t moved = 0;
+  if (g < v.G && from != to && pair_remote(v, from, to)) {
+    // the sender of plane (from, to) into rank d (drb_place_peer, dir 1)
+    const uint32_t N = a.N, dd = (to % N + N - from % N) % N;
+    const PullSrc &s = a.src[(a.d + N - dd) % N];
+    const uint64_t hi = mmeta_ix(v, a.buf, from, to, g);
+    const uint4 h = s.meta[hi];
+    if (tag_is(h.x, a.tag)) {
+      v.meta_in[hi] = h;
+      moved += 16;
+      const uint32_t nrep = mi_nrep(h.y), noth = mi_noth(h.y);
+      for (uint32_t j = 0; j < nrep + noth; ++j) {
+        const uint32_t k = rec_pos(j < nrep, j < nrep ? j : j - nrep, v.MB);
+        for (uint32_t c = 0; c < MSG_CHUNKS; ++c) {
+          const uint64_t ix = mbox_ix(v, a.buf, from, to, k, c, g);
+          v.mbox_in[ix] = s.mbox[ix];
+        }
+        if (v.rterm_in) {
+          const uint64_t ix = rterm_ix(v, a.buf, from, to, k, g);
+          v.rterm_in[ix] = s.rterm[ix];
+        }
+      }
+      moved += (uint64_t)(nrep + noth) *
+               (MSG_CHUNKS * 16 + (v.rterm_in ? 8 : 0));
+      if (nrep) {
+        const uint64_t mx = s.maxapp[hi], lo = s.elo[hi];
+        v.maxapp_in[hi] = mx;
+        v.elo_in[hi] = lo;
+        moved += 16;
+        if (v.E && lo != ~0ull && mx >= lo) {
+          const uint64_t rows = mx - lo + 1 < v.E ? mx - lo + 1 : v.E;
+          const uint32_t chunks = ENT_META + v.C16;
+          for (uint32_t e = 0; e < rows; ++e)
+            for (uint32_t c = 0; c < chunks; ++c) {
+              const uint64_t ix = embox_ix(v, a.buf, from, to, e, c, g);
+              v.embox_in[ix] = s.embox[ix];
+            }
+          moved += rows * chunks * 16;
+        }
+      }
+    }
+  }
+  // the bytes moved, a wave sum and one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) moved += __shfl_down(moved, o, 64);
+  if ((threadIdx.x & 63) == 0 && moved)
+    atomicAdd(bytes, (unsigned long long)moved);
+}
+
+static bool pull_ok(drb_engine *const *engines, uint32_t n) {
+  if (n > PULL_MAX) return false;
+  for (uint32_t r = 1; r < n; ++r)
+    if (engines[r]->cfg.device != engines[0]->cfg.device) return false;
+  return true;
+}
+
+static int exchange_pull(drb_engine *const *engines, uint32_t n) {
+  const View &v0 = engines[0]->v;
+  PullArgs a;
+  memset(&a, 0, sizeof(a));
+  a.N = n;
+  a.buf = (uint32_t)(engines[0]->round & 1);  // the last round's outbox
+  a.tag = (uint32_t)engines[0]->round;
+  for (uint32_t r = 0; r < n; ++r) {
+    const View &v = engines[r]->v;
+    a.src[r] = {v.mbox, v.mbox_meta, v.embox, v.mbox_maxapp, v.elo, v.rterm};
+    HIPCHK(hipEventRecord(engines[r]->ev_xsend, engines[r]->stream));
+  }
+  const dim3 grid((unsigned)((v0.G + 255) / 256), v0.R * v0.R);
+  for (uint32_t d = 0; d < n; ++d) {
+    drb_engine *e = engines[d];
+    if (!e->xpull_bytes && dalloc(e, &e->xpull_bytes, 1)) return DRB_ENOMEM;
+    for (uint32_t r = 0; r < n; ++r)
+      if (r != d) HIPCHK(hipStreamWaitEvent(e->stream, engines[r]->ev_xsend, 0));
+    a.d = d;
+    k_plane_pull<<<grid, 256, 0, e->stream>>>(e->v, a, e->xpull_bytes);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev_xrecv, e->stream));
+  }
+  // a sender's next round overwrites the other outbox buffer, the one after
+  // it this one: its stream waits for the pulls that read it
+  for (uint32_t r = 0; r < n; ++r)
+    for (uint32_t d = 0; d < n; ++d)
+      if (r != d)
+        HIPCHK(hipStreamWaitEvent(engines[r]->stream, engines[d]->ev_xrecv, 0));
+  return DRB_OK;
+}
+
+extern "C" int drb_exchange_bytes(drb_engine *e, uint64_t *bytes, int reset) {
+  if (!e || !bytes) return DRB_EINVAL;
+  unsigned long long b = 0;
+  if (e->xpull_bytes) {
+    HIPCHK(hipMemcpyAsync(&b, e->xpull_bytes, 8, hipMemcpyDeviceToHost,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (reset) HIPCHK(hipMemsetAsync(e->xpull_bytes, 0, 8, e->stream));
+  }
+  *bytes = e->xcopy_bytes + b;
+  if (reset) e->xcopy_bytes = 0;
+  return DRB_OK;
+}
+
 extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
   if (int rc = exchange_check(engines, n)) return rc;
   const View &v = engines[0]->v;
   const uint32_t R = v.R;
   ExchangeLocks locks(engines, n);
+  if (pull_ok(engines, n)) {  // one GPU: counted, on the device
+    if (engines[0]->round == 0) return DRB_OK;
+    if (int rc = exchange_pull(engines, n)) return rc;
+    for (uint32_t r = 0; r < n; ++r)
+      engines[r]->exchanged_round = engines[r]->round;
+    return DRB_OK;
+  }
   // plane (a, b) can carry fast-path messages when a or b holds a leader on
   // some engine (followers send only to leaders); every plane when roles
   // change on the device
@@ -3444,6 +3612,95 @@ __global__ void k_batch_reads(const View v, uint32_t slot, uint64_t g0,
   }
 }
 
+// ---- full ReadLocalNode values (drb_export_read_values)
+// the slot of key8 in replica slot `slot`'s KV at lane g (table probes, then
+// the overflow chain), or null
+__device__ const uint4 *kv_find(const View &v, uint32_t slot, uint64_t g,
+                                uint64_t key8) {
+  const uint4 *tbl = v.kv + kv_ix(v, slot, g, 0);
+  const uint32_t home = (uint32_t)kv_hash(key8, 8) & (v.KS - 1);
+  for (uint32_t t = 0; t < v.KS; ++t) {
+    const uint4 *sl = tbl + (uint64_t)kv_probe(v, home, t) * v.KVW;
+    if (!kv_used(sl[0])) return nullptr;
+    if (kv_match(sl[0], key8, 8)) return sl;
+  }
+  if (v.kv_ovf_head) {
+    bool hit = false;
+    const uint4 *sl = kv_ovf_walk(v, slot, g, key8, 8, false, hit);
+    if (hit) return sl;
+  }
+  return nullptr;
+}
+
+// value bytes of the served reads of lane g, each padded to 16 B
+__global__ void k_value_count(const View v, uint32_t slot, uint64_t g0,
+                              uint64_t n, uint32_t n_reads, uint64_t *cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  uint64_t c = 0;
+  if (i < n) {
+    const uint64_t g = g0 + i;
+    const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+    const uint32_t m = nr ? v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u)
+                          : 0u;
+    for (uint32_t k = 0; k < nr; ++k)
+      if ((m >> k) & 1u)
+        for (uint32_t j = 0; j < n_reads; ++j) {
+          const uint2 w = v.read_res[rres_ix(v, slot, k, j, g)];
+          if (w.y >> 31) c += ((w.y & 0x7fffffffu) + 15) & ~15u;
+        }
+  }
+  cnt[i] = c;
+}
+
+// the values themselves: lookup again (the KV is as the round served it)
+// and copy 16 B at a time into the pool at the read's offset
+__global__ void k_batch_values(const View v, uint32_t slot, uint64_t g0,
+                               uint64_t n, uint32_t n_reads,
+                               uint32_t key_space, const uint32_t *off,
+                               const uint64_t *voff, uint64_t *value_off,
+                               uint4 *pool, unsigned long long *bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t g = g0 + i;
+  const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+  if (!nr) return;
+  const uint32_t m = v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u);
+  uint64_t o = off[i], vo = voff[i];
+  for (uint32_t k = 0; k < nr; ++k) {
+    if (!((m >> k) & 1u)) continue;
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    const uint64_t low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
+    for (uint32_t j = 0; j < n_reads; ++j, ++o) {
+      const uint2 w = v.read_res[rres_ix(v, slot, k, j, g)];
+      value_off[o] = vo;
+      if (!(w.y >> 31)) continue;
+      const uint32_t vlen = w.y & 0x7fffffffu;
+      const uint64_t x =
+          mix64(low ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
+      const uint4 *sl = kv_find(v, slot, g, x % key_space);
+      uint4 *dst = pool + vo / 16;
+      vo += (vlen + 15) & ~15u;
+      if (!sl || ((sl[0].z >> 8) & 0xfffu) != vlen) {
+        atomicAdd(bad, 1ull);  // the KV changed since the round served it
+        continue;
+      }
+      if (v.kv_ool) {  // the key's value block
+        const uint4 *src = v.kv_pool + (uint64_t)sl[1].x * v.VB;
+        for (uint32_t c = 0; c * 16 < vlen; ++c) dst[c] = src[c];
+      } else {  // inline: 4 bytes in the header word, then the slot chunks
+        uint4 prev = make_uint4(sl[0].w, 0, 0, 0);
+        for (uint32_t c = 0; c * 16 < vlen; ++c) {
+          const uint4 nx = c + 1 < v.KVW ? sl[c + 1] : make_uint4(0, 0, 0, 0);
+          // bytes [16 c, 16 c + 16) of (w, sl[1], sl[2], ...)
+          dst[c] = make_uint4(prev.x, nx.x, nx.y, nx.z);
+          prev = make_uint4(nx.w, 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
 static int xout(drb_engine *e, size_t bytes, void **p) {
   if (bytes > e->xout_bytes) {
     if (e->xout) HIPCHK(hipFree(e->xout));
@@ -3522,6 +3779,79 @@ extern "C" int drb_export_read_results(drb_engine *e, uint32_t slot,
                                        size_t *n_out) {
   return batch_export(e, slot, first_group, n_groups, BK_READS, out,
                       sizeof(drb_read_result), cap, n_out);
+}
+
+extern "C" int drb_export_read_values(drb_engine *e, uint32_t slot,
+                                      uint64_t first_group, uint64_t n_groups,
+                                      drb_read_result *out,
+                                      uint64_t *value_off, size_t cap,
+                                      uint8_t *pool, size_t pool_cap,
+                                      size_t *n_out, size_t *pool_bytes) {
+  if (!e || !n_out || !pool_bytes || (cap && (!out || !value_off)))
+    return DRB_EINVAL;
+  *pool_bytes = 0;
+  int rc = batch_export(e, slot, first_group, n_groups, BK_READS, out,
+                        sizeof(drb_read_result), cap, n_out);
+  if (rc || !*n_out) return rc;
+  // the record offsets again (batch_export's scratch), and the value ones
+  const View &v = e->v;
+  const uint64_t n = n_groups;
+  const uint32_t n_reads = e->reads_n;
+  size_t tb = 0, tb2 = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint32_t *)nullptr,
+                                          (uint32_t *)nullptr, (int)(n + 1),
+                                          e->stream));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (uint64_t *)nullptr,
+                                          (uint64_t *)nullptr, (int)(n + 1),
+                                          e->stream));
+  const size_t a = ((n + 1) * 4 + 255) & ~(size_t)255;
+  const size_t a8 = ((n + 1) * 8 + 255) & ~(size_t)255;
+  const size_t tmax = tb > tb2 ? tb : tb2;
+  void *s;
+  if (scratch(e, 2 * a + 2 * a8 + tmax + 256, &s)) return DRB_EDEVICE;
+  uint32_t *cnt = (uint32_t *)s;
+  uint32_t *off = (uint32_t *)((char *)s + a);
+  uint64_t *vcnt = (uint64_t *)((char *)s + 2 * a);
+  uint64_t *voff = (uint64_t *)((char *)s + 2 * a + a8);
+  unsigned long long *bad = (unsigned long long *)((char *)s + 2 * a + 2 * a8);
+  void *tmp = (char *)s + 2 * a + 2 * a8 + 256;
+  const unsigned blocks = (unsigned)((n + 1 + 255) / 256);
+  k_batch_count<<<blocks, 256, 0, e->stream>>>(v, slot, first_group, n,
+                                               BK_READS, n_reads, cnt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)(n + 1),
+                                          e->stream));
+  k_value_count<<<blocks, 256, 0, e->stream>>>(v, slot, first_group, n,
+                                               n_reads, vcnt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, vcnt, voff, (int)(n + 1),
+                                          e->stream));
+  uint64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, voff + n, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemsetAsync(bad, 0, 8, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *pool_bytes = (size_t)total;
+  if (total > pool_cap || (total && !pool)) return DRB_ERANGE;
+  // device staging: the offsets, then the pool
+  const size_t ob = ((size_t)*n_out * 8 + 255) & ~(size_t)255;
+  void *d;
+  if (xout(e, ob + (size_t)total + 16, &d)) return DRB_EDEVICE;
+  uint64_t *doff = (uint64_t *)d;
+  uint4 *dpool = (uint4 *)((char *)d + ob);
+  const unsigned wb = (unsigned)((n + 255) / 256);
+  k_batch_values<<<wb, 256, 0, e->stream>>>(v, slot, first_group, n, n_reads,
+                                            e->reads_ks, off, voff, doff,
+                                            dpool, bad);
+  HIPCHK(hipGetLastError());
+  unsigned long long nbad = 0;
+  HIPCHK(hipMemcpyAsync(value_off, doff, (size_t)*n_out * 8,
+                        hipMemcpyDeviceToHost, e->stream));
+  if (total)
+    HIPCHK(hipMemcpyAsync(pool, dpool, (size_t)total, hipMemcpyDeviceToHost,
+                          e->stream));
+  HIPCHK(hipMemcpyAsync(&nbad, bad, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return nbad ? DRB_EDEVICE : DRB_OK;
 }
 
 // ---------------------------------------------------------------- worker

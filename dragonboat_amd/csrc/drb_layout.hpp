@@ -298,6 +298,10 @@ struct View {
   uint32_t max_props;
   uint32_t election_rtt, heartbeat_rtt, check_quorum;
   uint32_t quiesce;  // Config.Quiesce; qs.electionTick = 2 x election_rtt
+  // member kinds per replica slot (drb_config.nonvoting_slots /
+  // witness_slots) and the quorum of the voting members (remotes +
+  // witnesses, raft.go:383-389)
+  uint32_t nv_mask, wt_mask, quorum;
   uint64_t first_shard_id;
 
   uint64_t *u64;          // [NUM_U64][R][G] (overflow, tick/kv counts)

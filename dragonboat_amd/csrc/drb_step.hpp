@@ -198,6 +198,10 @@ struct Lane {
   // instantiation: C5's heartbeat rounds change none; the C3 path keeps
   // its registers for the unconditional stores)
   bool dirty;
+  // member kinds (drb_config.nonvoting_slots / witness_slots) are stepped
+  // by the FWD instantiations (and the raft launch) only; the C3 and C5
+  // kernels compile them out
+  bool members = false;
 };
 
 // ------------------------------------------------------------ helpers
@@ -448,6 +452,44 @@ DRB_DEV void emit(const Lane &L, Rep<R> &r, uint32_t to_slot, const Msg &m) {
   }
 }
 
+// ------------------------------------------------------------ members
+// member kinds of the replica slots (drb_config.nonvoting_slots /
+// witness_slots): slot s of every group
+DRB_DEV uint32_t nv_mask_of(const Lane &L) {
+  return L.members ? L.v->nv_mask : 0u;
+}
+DRB_DEV uint32_t wt_mask_of(const Lane &L) {
+  return L.members ? L.v->wt_mask : 0u;
+}
+DRB_DEV bool is_nonvoting(const Lane &L, uint32_t s) {
+  return (nv_mask_of(L) >> s) & 1u;
+}
+DRB_DEV bool is_witness(const Lane &L, uint32_t s) {
+  return (wt_mask_of(L) >> s) & 1u;
+}
+// quorum (raft.go:385-389): voting members (remotes + witnesses) / 2 + 1
+template <int R>
+DRB_DEV uint32_t quorum_of(const Lane &L) {
+  return L.members ? L.v->quorum : (uint32_t)(R / 2 + 1);
+}
+// a nonVoting or witness replica's state (raft.go:973-999)
+DRB_DEV bool passive_role(uint32_t role) {
+  return role == DRB_NONVOTING || role == DRB_WITNESS;
+}
+// the remote-dirty bit 3 of every nonVoting slot (RemLds.dirty nibbles)
+DRB_DEV uint32_t nv_bits8(uint32_t nv_mask) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if ((nv_mask >> s) & 1u) b |= 8u << (4 * s);
+  return b;
+}
+// isSingleNodeQuorum (raft.go:391-393): quorum over the voting members
+template <int R>
+DRB_DEV bool single_quorum(const Lane &L) {
+  return R == 1 || (nv_mask_of(L) && quorum_of<R>(L) == 1);
+}
+
 // ------------------------------------------------------------ remote FSM
 // The remotes live in registers; a runtime slot index selects through a
 // short chain of v_cndmask instead of indexing an array (which would put
@@ -602,6 +644,9 @@ DRB_DEV void broadcast_heartbeat_hint(const Lane &L, Rep<R> &r, uint64_t lo,
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     if ((uint32_t)s == L.slot) continue;
+    // the voting members (remotes, witnesses) with the ctx, the nonVotings
+    // only without one (raft.go:859-871)
+    if (is_nonvoting(L, (uint32_t)s) && (lo | hi) != 0) continue;
     Msg m = {};
     m.type = DRB_MSG_HEARTBEAT;
     m.commit = umin64(rem_get<R>(L, s).m, r.committed);
@@ -627,9 +672,13 @@ DRB_DEV void broadcast_heartbeat(const Lane &L, Rep<R> &r) {
 // sortMatchValues + tryCommit (raft.go:884-942): quorum-th largest match
 template <int R>
 DRB_DEV bool try_commit(const Lane &L, Rep<R> &r) {
+  // the remotes' and witnesses' matches (raft.go:917-924); a nonVoting's
+  // counts as 0, which sorts below them and leaves the quorum-th largest
+  // voting match at m[R - quorum]
   uint64_t m[R];
 #pragma unroll
-  for (int s = 0; s < R; ++s) m[s] = rl_of<R>(L).m[s][L.tid];
+  for (int s = 0; s < R; ++s)
+    m[s] = is_nonvoting(L, (uint32_t)s) ? 0 : rl_of<R>(L).m[s][L.tid];
   // sorting network (odd-even transposition), ascending
 #pragma unroll
   for (int p = 0; p < R; ++p)
@@ -639,8 +688,12 @@ DRB_DEV bool try_commit(const Lane &L, Rep<R> &r) {
       m[i] = umin64(a, b);
       m[i + 1] = umax64(a, b);
     }
-  constexpr int quorum = R / 2 + 1;
-  uint64_t q = m[R - quorum];
+  uint64_t q = m[R - (R / 2 + 1)];  // the quorum without nonVotings
+  if (nv_mask_of(L)) {
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+      if ((uint32_t)s == R - quorum_of<R>(L)) q = m[s];
+  }
   // entryLog.tryCommit (logentry.go:395-410)
   if (q <= r.committed) return false;
   uint64_t lterm = log_term(L, r, q);
@@ -718,8 +771,8 @@ DRB_DEV void ri_confirm(const Lane &L, Rep<R> &r, uint64_t lo, uint64_t hi,
       r.ri_cf[d] |= 1u << from_slot;
       cf = r.ri_cf[d];
     }
-  constexpr int quorum = R / 2 + 1;
-  if ((int)__builtin_popcount(cf) + 1 < quorum) return;
+  // the voting members' quorum (a nonVoting is sent no ctx to confirm)
+  if ((int)__builtin_popcount(cf) + 1 < (int)quorum_of<R>(L)) return;
   uint64_t sidx = 0;
 #pragma unroll
   for (int d = 0; d < DRB_RI_DEPTH; ++d)
@@ -840,7 +893,9 @@ DRB_DEV bool committed_at_term(const Lane &L, Rep<R> &r) {
 template <int R>
 DRB_DEV void leader_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
                                uint64_t hi, uint64_t from) {
-  if (R > 1) {
+  if (from && is_witness(L, (uint32_t)(from - 1))) {
+    return;  // dropped: a witness node (raft.go:1848-1849)
+  } else if (!single_quorum<R>(L)) {
     if (!committed_at_term(L, r)) {
       r.ndropped_ri++;  // reportDroppedReadIndex
       return;
@@ -849,6 +904,16 @@ DRB_DEV void leader_read_index(const Lane &L, Rep<R> &r, uint64_t lo,
     broadcast_heartbeat_hint(L, r, lo, hi);
   } else {
     add_ready(L, r, r.committed, lo, hi);
+    // a nonVoting requester is answered (raft.go:1863-1873)
+    if (R > 1 && from && from != (uint64_t)L.slot + 1 &&
+        is_nonvoting(L, (uint32_t)(from - 1))) {
+      Msg m = {};
+      m.type = DRB_MSG_READ_INDEX_RESP;
+      m.log_index = r.committed;
+      m.hint = lo;
+      m.hint_high = hi;
+      emit(L, r, (uint32_t)(from - 1), m);
+    }
   }
 }
 
@@ -873,7 +938,7 @@ DRB_DEV void append_props(const Lane &L, Rep<R> &r, uint32_t ps, uint32_t n) {
   r.last += n;
   if (r.last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, r.last + 1 - v.W);
   rem_try_update<R>(L, (int)L.slot, r.last);  // self remote
-  if (R == 1) try_commit(L, r);
+  if (single_quorum<R>(L)) try_commit(L, r);
 }
 
 // handleFollowerPropose (raft.go:2103-2116): the entry queue goes to the
@@ -974,11 +1039,25 @@ DRB_DEV void follower_replicate(const Lane &L, Rep<R> &r, int s,
       // [term_start, last] == r.term invariant (terms never decrease
       // along a log and never exceed the leader's term)
       const uint32_t chunks = ENT_META + v.C16;
+      // a witness keeps metadata entries: Index and Term, config changes as
+      // they are (makeMetadataEntries, raft.go:771-785; the leader's send)
+      const bool wt = is_witness(L, L.slot);
       uint64_t ts = new_last + 1;
       for (uint64_t idx = ci; idx <= new_last; ++idx) {
         uint4 m0 = ent_chunk(L, src, (uint32_t)s, idx, 0);
-        v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = m0;
         if (ts > new_last && lo64(m0) == r.term) ts = idx;
+        if (wt) {
+          const uint4 m2 = ent_chunk(L, src, (uint32_t)s, idx, 2);
+          if (m2.z != DRB_ENTRY_CONFIG_CHANGE) {
+            m0.z = m0.w = 0;  // key
+            v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = m0;
+            v.ring[ring_ix(v, L.slot, idx, 1, L.g)] = make_uint4(0, 0, 0, 0);
+            v.ring[ring_ix(v, L.slot, idx, 2, L.g)] =
+                make_uint4(0, 0, DRB_ENTRY_METADATA, 0);
+            continue;
+          }
+        }
+        v.ring[ring_ix(v, L.slot, idx, 0, L.g)] = m0;
         for (uint32_t c = 1; c < chunks; ++c)
           v.ring[ring_ix(v, L.slot, idx, c, L.g)] =
               ent_chunk(L, src, (uint32_t)s, idx, c);
@@ -1154,7 +1233,7 @@ DRB_DEV void el_become_leader(const Lane &L, Rep<R> &r) {
   if (r.last + 1 > v.W) r.ring_lo = umax64(r.ring_lo, r.last + 1 - v.W);
   if (r.term_start > idx) r.term_start = idx;
   rem_try_update<R>(L, (int)L.slot, r.last);  // self remote
-  if (R == 1) try_commit(L, r);
+  if (single_quorum<R>(L)) try_commit(L, r);
 }
 
 // handleVoteResp (raft.go:1125-1147): granted votes so far
@@ -1178,7 +1257,7 @@ DRB_DEV void el_campaign(const Lane &L, Rep<R> &r, bool xfer = false) {
   r.leader_update = true;
   st_f(L, r, F_VOTE, (uint64_t)L.slot + 1);
   el_vote_resp(r, L.slot, false);
-  if (R == 1) {  // a single-node quorum
+  if (single_quorum<R>(L)) {  // a single-node quorum
     el_become_leader(L, r);
     return;
   }
@@ -1188,8 +1267,9 @@ DRB_DEV void el_campaign(const Lane &L, Rep<R> &r, bool xfer = false) {
   m.log_term = log_term(L, r, r.last);
   m.hint = xfer ? (uint64_t)L.slot + 1 : 0;
 #pragma unroll
-  for (int s = 0; s < R; ++s)
-    if ((uint32_t)s != L.slot) emit(L, r, (uint32_t)s, m);
+  for (int s = 0; s < R; ++s)  // votingMembers (raft.go:1202)
+    if ((uint32_t)s != L.slot && !is_nonvoting(L, (uint32_t)s))
+      emit(L, r, (uint32_t)s, m);
 }
 
 // preVoteCampaign (raft.go:1149-1174) after becomePreVoteCandidate
@@ -1201,7 +1281,7 @@ DRB_DEV void el_pre_vote_campaign(const Lane &L, Rep<R> &r) {
   set_leader(r, 0);
   r.leader_update = true;
   el_vote_resp(r, L.slot, false);
-  if (R == 1) {  // a single-node quorum
+  if (single_quorum<R>(L)) {  // a single-node quorum
     el_campaign(L, r);
     return;
   }
@@ -1211,8 +1291,9 @@ DRB_DEV void el_pre_vote_campaign(const Lane &L, Rep<R> &r) {
   m.log_index = r.last;
   m.log_term = log_term(L, r, r.last);
 #pragma unroll
-  for (int s = 0; s < R; ++s)
-    if ((uint32_t)s != L.slot) emit(L, r, (uint32_t)s, m);
+  for (int s = 0; s < R; ++s)  // votingMembers (raft.go:1160)
+    if ((uint32_t)s != L.slot && !is_nonvoting(L, (uint32_t)s))
+      emit(L, r, (uint32_t)s, m);
 }
 
 // handleNodeElection (raft.go:1632-1668): not while a config change may be
@@ -1252,6 +1333,10 @@ DRB_DEV void el_leader_transfer(const Lane &L, Rep<R> &r, uint64_t target) {
   if (r.flags & F_XFER) return;                // a transfer is ongoing
   if (target == (uint64_t)L.slot + 1) return;  // pointing to itself
   if (target > (uint64_t)R) return;            // unknown target
+  // r.remotes only: a nonVoting or witness is no target (raft.go:1942-1946)
+  if (is_nonvoting(L, (uint32_t)target - 1) ||
+      is_witness(L, (uint32_t)target - 1))
+    return;
   r.flags = (r.flags & ~F_XFER) | ((uint32_t)target << F_XFER_SHIFT);
   r.election_tick = 0;
   if (rem_get<R>(L, (int)target - 1).m == r.last)
@@ -1301,7 +1386,7 @@ DRB_DEV void el_request_pre_vote(const Lane &L, Rep<R> &r, int s,
 // handlePreVoteCandidateRequestPreVoteResp (raft.go:2259-2276)
 template <int R>
 DRB_DEV void el_pre_vote_resp(const Lane &L, Rep<R> &r, int s, const Msg &m) {
-  constexpr uint32_t quorum = R / 2 + 1;
+  const uint32_t quorum = quorum_of<R>(L);
   const uint32_t granted = el_vote_resp(r, (uint32_t)s, m.reject != 0);
   const uint32_t answered = __builtin_popcount(r.votes & 0xffu);
   if (granted == quorum)
@@ -1314,7 +1399,7 @@ DRB_DEV void el_pre_vote_resp(const Lane &L, Rep<R> &r, int s, const Msg &m) {
 template <int R>
 DRB_DEV void el_candidate_vote_resp(const Lane &L, Rep<R> &r, int s,
                                     const Msg &m) {
-  constexpr uint32_t quorum = R / 2 + 1;
+  const uint32_t quorum = quorum_of<R>(L);
   const uint32_t granted = el_vote_resp(r, (uint32_t)s, m.reject != 0);
   const uint32_t answered = __builtin_popcount(r.votes & 0xffu);
   if (granted == quorum) {
@@ -1348,6 +1433,13 @@ DRB_DEV bool el_term_gate(const Lane &L, Rep<R> &r, int s, const Msg &m) {
         (m.type == DRB_MSG_REQUEST_PREVOTE_RESP && !m.reject))
       return false;
     const uint64_t leader = el_leader_message(m.type) ? (uint64_t)s + 1 : 0;
+    if (r.role == DRB_NONVOTING || r.role == DRB_WITNESS) {
+      // becomeNonVoting / becomeWitness (raft.go:973-999)
+      el_reset(L, r, m.term, true);
+      set_leader(r, leader);
+      r.leader_update = true;
+      return false;
+    }
     el_become_follower(L, r, m.term, leader,
                        m.type != DRB_MSG_REQUEST_VOTE);  // ...KE keeps ticks
     return false;
@@ -1387,6 +1479,16 @@ DRB_DEV void el_dispatch(const Lane &L, Rep<R> &r, int s, const Msg &m,
     } else if (t != DRB_MSG_REQUEST_PREVOTE_RESP) {
       dispatch(L, r, s, m, src);
     }
+  } else if (r.role == DRB_NONVOTING || r.role == DRB_WITNESS) {
+    // raft.go:2396-2416, re-routed to the follower's handlers
+    if (t == DRB_MSG_REQUEST_VOTE)
+      el_request_vote(L, r, s, m);
+    else if (t == DRB_MSG_REPLICATE || t == DRB_MSG_HEARTBEAT)
+      dispatch(L, r, s, m, src);
+    else if (r.role == DRB_NONVOTING && t == DRB_MSG_READ_INDEX)
+      follower_read_index(L, r, m.hint, m.hint_high);
+    else if (r.role == DRB_NONVOTING && t == DRB_MSG_READ_INDEX_RESP)
+      dispatch(L, r, s, m, src);
   } else if (r.role == DRB_FOLLOWER) {
     if (t == DRB_MSG_REQUEST_VOTE)
       el_request_vote(L, r, s, m);
@@ -1431,15 +1533,16 @@ DRB_DEV void el_tick(const Lane &L, Rep<R> &r, bool xfer = false) {
     if (r.election_tick >= v.election_rtt) {
       r.election_tick = 0;
       if (v.check_quorum) {  // leaderHasQuorum (raft.go:395-405)
-        int c = 0;
+        uint32_t c = 0;
 #pragma unroll
-        for (int s = 0; s < R; ++s) {
+        for (int s = 0; s < R; ++s) {  // over the voting members
+          if (is_nonvoting(L, (uint32_t)s)) continue;
           RemoteV x = rem_get<R>(L, s);
           if ((uint32_t)s == L.slot || x.a) c++;
           x.a = 0;
           rem_put<R>(L, s, x);
         }
-        if (c < R / 2 + 1) el_become_follower(L, r, r.term, 0, true);
+        if (c < quorum_of<R>(L)) el_become_follower(L, r, r.term, 0, true);
       }
     }
     if (abort_xfer) r.flags &= ~F_XFER;
@@ -1451,6 +1554,8 @@ DRB_DEV void el_tick(const Lane &L, Rep<R> &r, bool xfer = false) {
     return;
   }
   r.election_tick++;
+  // a nonVoting or witness takes no part in elections (raft.go:596-600)
+  if (r.role == DRB_NONVOTING || r.role == DRB_WITNESS) return;
   if (r.election_tick >= ld_f(L, r, F_RAND_TIMEOUT)) {
     r.election_tick = 0;
     el_election(L, r, xfer);
@@ -2412,6 +2517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   L.wbuf = (uint32_t)(p.round & 1);
   L.slow = SLOW;
   L.dirty = EXT && DRB_REM_DIRTY;
+  L.members = FWD;
   uint32_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint32_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
@@ -2494,9 +2600,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     const bool is_leader = SLOW ? r.role == DRB_LEADER : LEAD;
     if (SLOW) {
       if (role != DRB_LEADER && role != DRB_FOLLOWER && role != DRB_CANDIDATE &&
-          role != DRB_PREVOTE_CANDIDATE)
+          role != DRB_PREVOTE_CANDIDATE && !passive_role(role))
         fb = DRB_FB_ROLE;
-    } else if (!LEAD && (role != DRB_FOLLOWER || r.ri_count != 0)) {
+    } else if (!LEAD && ((role != DRB_FOLLOWER && !passive_role(role)) ||
+                         r.ri_count != 0)) {
       fb = DRB_FB_ROLE;
     } else if (flags & (F_XFER | F_XFER_REQ)) {
       fb = DRB_FB_ROLE;  // a leader transfer: the raft launch's
@@ -2776,14 +2883,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                          qs_quiet_tick(v, r, qz_from);
       if (p.tick && !qtick && v.check_quorum &&
           r.election_tick + 1 >= v.election_rtt) {
-        int c = 1;
+        uint32_t c = 1;
 #pragma unroll
-        for (int s = 0; s < R; ++s)
-          if ((uint32_t)s != slot &&
+        for (int s = 0; s < R; ++s)  // the voting members (raft.go:395-405)
+          if ((uint32_t)s != slot && !is_nonvoting(L, (uint32_t)s) &&
               (rem_get<R>(L, s).a || ((resp_from >> s) & 1)))
             c++;
         // (the raft launch steps the leader down at the tick, el_tick)
-        if (c < R / 2 + 1 && !SLOW && fb == DRB_FB_NONE)
+        if (c < quorum_of<R>(L) && !SLOW && fb == DRB_FB_NONE)
           fb = DRB_FB_CHECK_QUORUM;
       }
       // a leader that may step down before handleProposals and learn the
@@ -2826,7 +2933,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                          qs_quiet_tick(v, r, qz_from);
       if (!SLOW && p.tick && !qtick) {
         uint64_t et = (total_in ? 0 : r.election_tick) + 1;
-        if (et >= ld_f(L, r, F_RAND_TIMEOUT) && fb == DRB_FB_NONE)
+        // (a nonVoting or witness member never campaigns, nonLeaderTick)
+        if (et >= ld_f(L, r, F_RAND_TIMEOUT) && fb == DRB_FB_NONE &&
+            !passive_role(role))
           fb = DRB_FB_ELECTION;
       }
     }
@@ -2972,10 +3081,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           if (r.election_tick >= v.election_rtt) {
             r.election_tick = 0;
             if (v.check_quorum) {
-              // leaderHasQuorum (raft.go:395-405): quorum held (pre-pass)
+              // leaderHasQuorum (raft.go:395-405): quorum held (pre-pass);
+              // the voting members' active flags are cleared
 #pragma unroll
-              for (int s = 0; s < R; ++s) rl_of<R>(L).a[s][L.tid] = 0;
-              if (L.dirty) rl_of<R>(L).dirty[L.tid] |= 0x88888888u;
+              for (int s = 0; s < R; ++s)
+                if (!is_nonvoting(L, (uint32_t)s)) rl_of<R>(L).a[s][L.tid] = 0;
+              if (L.dirty)
+                rl_of<R>(L).dirty[L.tid] |=
+                    0x88888888u & ~nv_bits8(nv_mask_of(L));
             }
           }
           r.heartbeat_tick++;
@@ -2997,15 +3110,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           append_props(L, r, p.prop_slot, nprops);
           broadcast_replicate(L, r);
         }
-      } else if (FWD && nprops && r.role == DRB_FOLLOWER && v.fwd_props) {
-        forward_props(L, r, p.prop_slot, nprops);  // handleFollowerPropose
+      } else if (FWD && nprops &&
+                 (r.role == DRB_FOLLOWER || r.role == DRB_NONVOTING) &&
+                 v.fwd_props) {
+        // handleFollowerPropose, handleNonVotingPropose (raft.go:2103-2116,
+        // 2071-2073)
+        forward_props(L, r, p.prop_slot, nprops);
       } else if (nprops) {
         // stepped down this round: handleCandidatePropose, or
         // handleFollowerPropose with no leader known (raft.go:2197-2201,
         // 2103-2108) -- reportDroppedProposal; one that knows the new
         // leader forwards (above), or without forward rows was routed to
         // the CPU path by the pre-pass
-        if (r.role == DRB_FOLLOWER && r.leader_id != 0)
+        if ((r.role == DRB_FOLLOWER || r.role == DRB_NONVOTING) &&
+            r.leader_id != 0)
           set_error(r, DRB_ERR_PROPOSE);
         else
           r.ndropped_props += nprops;

@@ -210,7 +210,15 @@ DRB_DEV EntryHdr wire_msg_entry(const View &v, const WireArgs &a, uint64_t g,
   }
   const uint64_t idx = w.m.log_index + 1 + q;
   *cmd0 = v.ring + ring_ix(v, a.from, idx, ENT_META, g);
-  return wire_entry(v, a.from, idx, g);
+  EntryHdr e = wire_entry(v, a.from, idx, g);
+  // a witness is sent metadata entries: Index and Term, config changes as
+  // they are (makeMetadataEntries, raft.go:771-785)
+  if (((v.wt_mask >> a.to) & 1u) && e.type != DRB_ENTRY_CONFIG_CHANGE) {
+    e.key = e.client_id = e.series_id = e.responded_to = 0;
+    e.type = DRB_ENTRY_METADATA;
+    e.cmd_len = 0;
+  }
+  return e;
 }
 
 // Message.Size (message.go:92-124) and Message.SizeUpperLimit

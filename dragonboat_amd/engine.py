@@ -84,6 +84,10 @@ SIGNATURES = {
     "drb_export_read_results": (C.c_int, [P, U32, U64, U64,
                                           C.POINTER(abi.ReadResult), SZ,
                                           C.POINTER(SZ)]),
+    "drb_export_read_values": (C.c_int, [P, U32, U64, U64,
+                                         C.POINTER(abi.ReadResult), PU64, SZ,
+                                         PU8, SZ, C.POINTER(SZ),
+                                         C.POINTER(SZ)]),
     "drb_serve_reads": (C.c_int, [P, U32, U32]),
     "drb_export_read_sums": (C.c_int, [P, U64, U64, PU64]),
     "drb_kv_lookup": (C.c_int, [P, U64, U32, PU8, U32, PU8, U32, PU32]),
@@ -109,6 +113,7 @@ SIGNATURES = {
     "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
     "drb_exchange_local_counted": (C.c_int, [C.POINTER(P), U32]),
     "drb_exchange_mark": (C.c_int, [P]),
+    "drb_exchange_bytes": (C.c_int, [P, C.POINTER(U64), C.c_int]),
     "drb_encode_wire": (C.c_int, [P, U32, U32, C.POINTER(WireCfg),
                                   C.POINTER(WireOut)]),
     "drb_wire_buffer": (C.c_int, [P, C.POINTER(P), PU64]),
@@ -166,7 +171,8 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 kv_pool_blocks=0, flagged_cap=0, quiesce=0, durable_log=0,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
                 tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0,
-                kv_overflow_buckets=0, forward_proposals=0)
+                kv_overflow_buckets=0, forward_proposals=0,
+                nonvoting_slots=0, witness_slots=0)
 
 
 class Engine:
@@ -189,7 +195,8 @@ class Engine:
                    cfg["save_tan"], cfg["elections"], cfg["tan_max_log"],
                    cfg["tan_multiplexed"], cfg["pre_vote"],
                    cfg["max_reads_per_ctx"], cfg["kv_overflow_buckets"],
-                   cfg["forward_proposals"])
+                   cfg["forward_proposals"], cfg["nonvoting_slots"],
+                   cfg["witness_slots"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -446,6 +453,34 @@ class Engine:
         return [(r.shard_id - base, r.index, r.ctx_low, r.read, r.key,
                  r.found, r.vlen, r.value) for r in arr[:n]]
 
+    def export_read_values(self, slot, first_group=0, n_groups=None,
+                           cap=1 << 16, pool_cap=1 << 20):
+        """[(group, index, ctx_low, read j, key, found, value bytes or None)]
+        of the reads replica slot served in the last round, values whole
+        (drb_export_read_values)."""
+        n_groups = self.G - first_group if n_groups is None else n_groups
+        while True:
+            arr = (abi.ReadResult * max(1, cap))()
+            off = (U64 * max(1, cap))()
+            pool = (C.c_uint8 * max(16, pool_cap))()
+            n, pb = SZ(), SZ()
+            rc = lib().drb_export_read_values(
+                self.h, slot, first_group, n_groups, arr, off, cap, pool,
+                pool_cap, C.byref(n), C.byref(pb))
+            if rc == abi.DRB_ERANGE and (n.value > cap or pb.value > pool_cap):
+                cap, pool_cap = max(cap, n.value), max(pool_cap, pb.value)
+                continue
+            _ck(rc, "drb_export_read_values")
+            break
+        base = self.cfg["first_shard_id"]
+        out = []
+        for i in range(n.value):
+            r = arr[i]
+            val = bytes(pool[off[i]:off[i] + r.vlen]) if r.found else None
+            out.append((r.shard_id - base, r.index, r.ctx_low, r.read, r.key,
+                        r.found, val))
+        return out
+
     def kv_export(self, g, slot):
         cap = self.cfg["kv_slots"]
         vcap = self.cfg["kv_val_cap"]
@@ -568,6 +603,14 @@ class Engine:
         fn = lib().drb_exchange_local_counted if counted else \
             lib().drb_exchange_local
         _ck(fn(arr, len(engines)), "drb_exchange_local")
+
+    def exchange_bytes(self, reset=False):
+        """Inbound plane bytes moved into this engine by the exchanges
+        (drb_exchange_bytes)."""
+        b = U64()
+        _ck(lib().drb_exchange_bytes(self.h, C.byref(b), int(bool(reset))),
+            "drb_exchange_bytes")
+        return b.value
 
     def exchange_mark(self):
         """This rank's own exchange of the last round is enqueued (RCCL):

@@ -401,6 +401,19 @@ typedef struct drb_config {
    * and group; a second is dropped as by a full MessageQueue).  Co-resident
    * placement only. */
   uint32_t forward_proposals;
+  /* Member kinds of the replica slots (the shards' pb.Membership, the same
+   * for every group): bit s of nonvoting_slots makes replica slot s a
+   * nonVoting -- replicated, sent heartbeats without a ReadIndex ctx, not
+   * counted in commit, CheckQuorum or ReadIndex quorums, never campaigning
+   * (raft.go:787-871, 917-924, 395-405, 596-600) -- and bit s of
+   * witness_slots a witness -- counted in the quorums, sent metadata-only
+   * entries (makeMetadataEntries, raft.go:756-785), applying them as
+   * no-ops, never campaigning, ReadIndex from it dropped
+   * (raft.go:1848-1849).  The quorum is over the voting members (remotes
+   * and witnesses, raft.go:383-389).  drb_init_steady gives those slots
+   * their roles; the leader slot must be a voting member. */
+  uint32_t nonvoting_slots;
+  uint32_t witness_slots;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -754,6 +767,18 @@ typedef struct drb_read_result {
 int drb_export_read_results(drb_engine *e, uint32_t slot, uint64_t first_group,
                             uint64_t n_groups, drb_read_result *out,
                             size_t cap, size_t *n_out);
+/* The same results with every found value whole (ReadLocalNode returns the
+ * value, nodehost.go:849 -> KVTest.Lookup kvtest.go:164-175; C5's 116 B /
+ * 1011 B values included): value_off[i] is the byte offset in pool of
+ * result i's value (vlen bytes, offsets 16-aligned), gathered on the device
+ * from the KV as the round served it and copied in one transfer.
+ * *pool_bytes is the pool size the values need; pool_cap below it is
+ * DRB_ERANGE (the records are then out already).  Call before the next
+ * round. */
+int drb_export_read_values(drb_engine *e, uint32_t slot, uint64_t first_group,
+                           uint64_t n_groups, drb_read_result *out,
+                           uint64_t *value_off, size_t cap, uint8_t *pool,
+                           size_t pool_cap, size_t *n_out, size_t *pool_bytes);
 
 /*
  * Serves the linearizable reads behind the ReadyToReads of the last round:
@@ -918,17 +943,27 @@ int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
 int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
                       uint32_t word, int dir, drb_region *out);
 /* The whole exchange among engines[rank] of one process, every engine at
- * the same round (NodeHost is one process per machine driving every GPU):
- * every plane that can carry fast-path messages -- one with a leader slot
- * at either end (drb_role_slots, OR over the engines), or every plane with
- * drb_config.elections -- moves at its full capacity (all mailbox
- * positions, both chunks, the header, the max-append word, the entry-row
- * base and entry_mbox entry rows: what the pre-pass bounds), so no counts
- * are read.  The peer copies are enqueued on the receivers' streams behind
- * the senders' rounds (cross-stream events), and each sender's next round
- * waits for the copies that read its outbox: no host synchronisation.
+ * the same round (NodeHost is one process per machine driving every GPU;
+ * Transport.Send -> handleRequest, transport.go:346, :305).  No host
+ * synchronisation either way: the work is enqueued on the receivers'
+ * streams behind the senders' rounds (cross-stream events), and each
+ * sender's next round waits for the work that read its outbox.
+ *  - Every engine on one device (n <= 16): a pull kernel per receiver reads
+ *    each sender plane's header on the device and copies, lane by lane,
+ *    only what it counts (records, rterm rows, max-append word, entry rows
+ *    up to the last entry sent) -- a counted exchange without host reads.
+ *  - Otherwise: every plane that can carry fast-path messages -- one with a
+ *    leader slot at either end (drb_role_slots, OR over the engines), or
+ *    every plane with drb_config.elections -- moves at its full capacity
+ *    (all mailbox positions, both chunks, the header, the max-append word,
+ *    the entry-row base and entry_mbox entry rows: what the pre-pass
+ *    bounds) by peer copies, so no counts are read.
  * The receivers read only what the plane headers count. */
 int drb_exchange_local(drb_engine *const *engines, uint32_t n);
+/* Inbound plane bytes the exchanges moved into this engine since the last
+ * reset (the device pull's own count plus region copies); synchronises the
+ * engine stream. */
+int drb_exchange_bytes(drb_engine *e, uint64_t *bytes, int reset);
 /* The same exchange at the planes' counted sizes (drb_plane_counts per
  * engine, i.e. one stream synchronisation each, then the copies and a
  * synchronisation of every stream): fewer bytes, host round trips. */

@@ -918,6 +918,36 @@ int orc_cluster_setup_steady(orc_cluster *c, uint32_t leader_slot) {
   return 0;
 }
 
+/* Member kinds (the shard's membership, pb.Membership's NonVotings and
+ * Witnesses): replica slot s is a nonVoting when bit s of nonvoting_mask is
+ * set, a witness when bit s of witness_mask is; every replica's raft gets
+ * them in its remotes' kinds (r.nonVotings / r.witnesses, raft.go:199-239)
+ * and those replicas their states.  The harness sets the membership after
+ * setup_steady, as a membership restored from a snapshot would be; the
+ * leader must be a voting member. */
+int orc_cluster_set_member_kinds(orc_cluster *c, uint32_t nonvoting_mask,
+                                 uint32_t witness_mask) {
+  const uint32_t R = c->cfg.num_replicas;
+  if (nonvoting_mask & witness_mask) return -1;
+  for (uint64_t g = 0; g < c->cfg.num_groups; g++)
+    for (uint32_t s = 0; s < R; s++) {
+      orc_raft *r = node_at(c, g, s)->r;
+      for (uint32_t t = 0; t < R; t++) {
+        const int kind = (nonvoting_mask >> t) & 1u   ? ORC_NONVOTING
+                         : (witness_mask >> t) & 1u ? ORC_WITNESS
+                                                     : ORC_VOTING;
+        const int i = raft_rem_idx(r, t + 1);
+        if (i < 0) return -1;
+        r->rem_kind[i] = (uint8_t)kind;
+        if (t == s && kind != ORC_VOTING) {
+          if (r->state == DRB_LEADER) return -1;
+          r->state = kind == ORC_NONVOTING ? DRB_NONVOTING : DRB_WITNESS;
+        }
+      }
+    }
+  return 0;
+}
+
 int orc_cluster_stage_proposals(orc_cluster *c, const uint32_t *counts,
                                 uint32_t max_per_group, const drb_entry *ents,
                                 const uint8_t *pool) {

@@ -36,6 +36,10 @@ extern "C" {
 #endif
 
 #define ORC_MAX_PEERS 16
+/* orc_raft.rem_kind: r.remotes, r.nonVotings, r.witnesses */
+#define ORC_VOTING 0
+#define ORC_NONVOTING 1
+#define ORC_WITNESS 2
 
 typedef struct orc_blob {
   uint32_t refs;
@@ -133,6 +137,10 @@ typedef struct orc_raft {
   int nrem;
   uint64_t rem_id[ORC_MAX_PEERS]; /* sorted ascending */
   orc_remote rem[ORC_MAX_PEERS];
+  /* the member kind of each: r.remotes (0), r.nonVotings (1), r.witnesses
+   * (2) (raft.go:199-239); the raft's own is its state (nonVoting / witness
+   * replicas are in those states for good) */
+  uint8_t rem_kind[ORC_MAX_PEERS];
   int nvotes;
   uint64_t vote_id[ORC_MAX_PEERS];
   int vote_ok[ORC_MAX_PEERS];
@@ -201,6 +209,15 @@ orc_raft *orc_raft_new_test(uint64_t id, const uint64_t *peers, int npeers,
                             uint64_t election, uint64_t heartbeat,
                             orc_logdb *db);
 void orc_raft_free(orc_raft *r);
+/* newTestNonVoting / newTestWitness: kind ORC_NONVOTING / ORC_WITNESS */
+orc_raft *orc_raft_new_test_kind(uint64_t id, const uint64_t *peers,
+                                 int npeers, const uint64_t *others,
+                                 int nothers, int kind, uint64_t election,
+                                 uint64_t heartbeat, orc_logdb *db);
+/* addNode (kind ORC_VOTING) / addNonVoting / addWitness */
+int orc_raft_add_member(orc_raft *r, uint64_t id, int kind);
+/* the member kind of replica id (-1: unknown) */
+int orc_raft_remote_kind(orc_raft *r, uint64_t id);
 int orc_raft_handle(orc_raft *r, const drb_message *m, const drb_entry *ents,
                     const uint8_t *pool);
 int orc_raft_peer_handle(orc_raft *r, const drb_message *m,
@@ -392,6 +409,10 @@ int orc_cluster_stage_proposals_at(orc_cluster *c, const uint32_t *counts,
                                    uint32_t max_per_group,
                                    const drb_entry *ents, const uint8_t *pool,
                                    uint32_t replica);
+/* replica slots that are nonVotings / witnesses in every group (after
+ * setup_steady; the leader slot must be a voting member) */
+int orc_cluster_set_member_kinds(orc_cluster *c, uint32_t nonvoting_mask,
+                                 uint32_t witness_mask);
 /* stage one ReadIndex ctx per group (low==0: none) for next round */
 int orc_cluster_stage_read_index(orc_cluster *c, const uint64_t *low,
                                  const uint64_t *high);

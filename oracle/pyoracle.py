@@ -86,6 +86,10 @@ def _declare(L):
         "orc_logdb_compact": (C.c_int, [P, U64]),
         "orc_logdb_set_state": (None, [P, U64, U64, U64]),
         "orc_raft_new_test": (P, [U64, PU64, C.c_int, U64, U64, P]),
+        "orc_raft_new_test_kind": (P, [U64, PU64, C.c_int, PU64, C.c_int,
+                                       C.c_int, U64, U64, P]),
+        "orc_raft_add_member": (C.c_int, [P, U64, C.c_int]),
+        "orc_raft_remote_kind": (C.c_int, [P, U64]),
         "orc_raft_free": (None, [P]),
         "orc_raft_handle": (C.c_int, [P, PM, PE, PU8]),
         "orc_raft_peer_handle": (C.c_int, [P, PM, PE, PU8]),
@@ -186,6 +190,7 @@ def _declare(L):
         "orc_cluster_free": (None, [P]),
         "orc_cluster_setup_steady": (C.c_int, [P, U32]),
         "orc_cluster_stage_proposals": (C.c_int, [P, PU32, U32, PE, PU8]),
+        "orc_cluster_set_member_kinds": (C.c_int, [P, U32, U32]),
         "orc_cluster_stage_proposals_at": (C.c_int, [P, PU32, U32, PE, PU8,
                                                      U32]),
         "orc_cluster_stage_read_index": (C.c_int, [P, PU64, PU64]),
@@ -510,6 +515,39 @@ class TestRaft:
         return bool(_check(lib().orc_raft_term_not_matched(self.p, marr, earr,
                                                            pool)))
 
+    # member kinds (oracle.h ORC_VOTING / ORC_NONVOTING / ORC_WITNESS)
+    VOTING, NONVOTING, WITNESS = 0, 1, 2
+
+    @classmethod
+    def with_kind(cls, id, peers, others, kind, election, heartbeat,
+                  logdb=None):
+        """newTestNonVoting / newTestWitness (raft_etcd_test.go:3099-3140):
+        others are the nonVotings (kind NONVOTING) or witnesses (WITNESS),
+        this replica among them."""
+        self = cls.__new__(cls)
+        self.logdb = logdb or LogDB()
+        ps = (U64 * max(1, len(peers)))(*peers)
+        os_ = (U64 * max(1, len(others)))(*others)
+        self.p = lib().orc_raft_new_test_kind(id, ps, len(peers), os_,
+                                              len(others), kind, election,
+                                              heartbeat, self.logdb.p)
+        if not self.p:
+            raise OracleError(lib().orc_last_error().decode())
+        self.id = id
+        return self
+
+    def add_node(self, id):
+        _check(lib().orc_raft_add_member(self.p, id, self.VOTING))
+
+    def add_nonvoting(self, id):
+        _check(lib().orc_raft_add_member(self.p, id, self.NONVOTING))
+
+    def add_witness(self, id):
+        _check(lib().orc_raft_add_member(self.p, id, self.WITNESS))
+
+    def remote_kind(self, id):
+        return lib().orc_raft_remote_kind(self.p, id)
+
     def network_reset(self, id, ids):
         arr = (U64 * len(ids))(*ids)
         _check(lib().orc_raft_network_reset(self.p, id, arr, len(ids)))
@@ -774,6 +812,11 @@ class Cluster:
 
     def setup_steady(self, leader_slot=0):
         _check(lib().orc_cluster_setup_steady(self.p, leader_slot))
+
+    def set_member_kinds(self, nonvoting_mask=0, witness_mask=0):
+        """Replica slots that are nonVotings / witnesses in every group."""
+        _check(lib().orc_cluster_set_member_kinds(self.p, nonvoting_mask,
+                                                  witness_mask))
 
     def stage_proposals(self, counts, max_per_group, ents, pool, replica=0):
         """counts: uint32[G] array; ents: Entry[G*max] array; pool: uint8.

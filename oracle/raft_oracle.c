@@ -937,18 +937,30 @@ static void raft_set_remote(orc_raft *r, uint64_t id, uint64_t match,
     while (i > 0 && r->rem_id[i - 1] > id) {
       r->rem_id[i] = r->rem_id[i - 1];
       r->rem[i] = r->rem[i - 1];
+      r->rem_kind[i] = r->rem_kind[i - 1];
       i--;
     }
     r->nrem++;
     r->rem_id[i] = id;
+    r->rem_kind[i] = ORC_VOTING;
   }
   memset(&r->rem[i], 0, sizeof(orc_remote));
   r->rem[i].match = match;
   r->rem[i].next = next;
 }
 
-/* numVotingMembers / quorum (raft.go:383-389) */
-static int raft_num_voting(const orc_raft *r) { return r->nrem; }
+/* the member kind of replica id (0: none of them) */
+static int raft_is_kind(const orc_raft *r, uint64_t id, int kind) {
+  const int i = raft_rem_idx(r, id);
+  return i >= 0 && r->rem_kind[i] == kind;
+}
+
+/* numVotingMembers / quorum (raft.go:383-389): remotes and witnesses */
+static int raft_num_voting(const orc_raft *r) {
+  int n = 0;
+  for (int i = 0; i < r->nrem; i++) n += r->rem_kind[i] != ORC_NONVOTING;
+  return n;
+}
 static int raft_quorum(const orc_raft *r) { return raft_num_voting(r) / 2 + 1; }
 static int raft_single_node_quorum(const orc_raft *r) {
   return raft_quorum(r) == 1;
@@ -1054,6 +1066,19 @@ static int raft_make_replicate(orc_raft *r, uint64_t to, uint64_t next,
       orc_panic("expected last index in Replicate %llu, got %llu",
                 (unsigned long long)exp, (unsigned long long)li);
   }
+  /* a witness is sent metadata entries (makeMetadataEntries, raft.go:
+   * 756-785): Index and Term of each, config changes as they are */
+  if (raft_is_kind(r, to, ORC_WITNESS))
+    for (size_t i = 0; i < ents.n; i++) {
+      orc_entry *e = &ents.v[i];
+      if (e->type == DRB_ENTRY_CONFIG_CHANGE) continue;
+      const uint64_t t = e->term, x = e->index;
+      blob_unref(e->cmd);
+      memset(e, 0, sizeof(*e));
+      e->type = DRB_ENTRY_METADATA;
+      e->term = t;
+      e->index = x;
+    }
   *m = new_msg(DRB_MSG_REPLICATE, to);
   m->log_index = next - 1;
   m->log_term = term;
@@ -1098,11 +1123,18 @@ static void raft_send_heartbeat(orc_raft *r, uint64_t to, orc_ctx hint,
   raft_send(r, &m);
 }
 
-/* broadcastHeartbeatMessageWithHint (raft.go:859-871) */
+/* broadcastHeartbeatMessageWithHint (raft.go:859-871): the voting members
+ * (remotes and witnesses) with the ctx, the nonVotings only without one */
 static void raft_broadcast_heartbeat_hint(orc_raft *r, orc_ctx ctx) {
   for (int i = 0; i < r->nrem; i++)
-    if (r->rem_id[i] != r->replica_id)
+    if (r->rem_id[i] != r->replica_id && r->rem_kind[i] != ORC_NONVOTING)
       raft_send_heartbeat(r, r->rem_id[i], ctx, r->rem[i].match);
+  if (ctx.low == 0 && ctx.high == 0) {
+    orc_ctx zero = {0, 0};
+    for (int i = 0; i < r->nrem; i++)
+      if (r->rem_kind[i] == ORC_NONVOTING)
+        raft_send_heartbeat(r, r->rem_id[i], zero, r->rem[i].match);
+  }
 }
 
 /* broadcastHeartbeatMessage (raft.go:849-857) */
@@ -1141,7 +1173,9 @@ void orc_sort_match_values(uint64_t *v, int n) {
 static int raft_try_commit(orc_raft *r) {
   if (r->state != DRB_LEADER) orc_panic("is not leader");
   if (raft_num_voting(r) != r->nmatched) raft_reset_matched(r);
-  for (int i = 0; i < r->nrem; i++) r->matched[i] = r->rem[i].match;
+  /* the remotes' and the witnesses' matches */
+  for (int i = 0, k = 0; i < r->nrem; i++)
+    if (r->rem_kind[i] != ORC_NONVOTING) r->matched[k++] = r->rem[i].match;
   orc_sort_match_values(r->matched, r->nmatched);
   uint64_t q = r->matched[raft_num_voting(r) - raft_quorum(r)];
   int ok;
@@ -1176,6 +1210,8 @@ static void raft_to_follower(orc_raft *r, uint64_t term, uint64_t leader,
 static void raft_become_candidate(orc_raft *r) {
   if (r->state == DRB_LEADER)
     orc_panic("transitioning to candidate state from leader");
+  if (r->state == DRB_NONVOTING) orc_panic("nonVoting is becoming candidate");
+  if (r->state == DRB_WITNESS) orc_panic("witness is becoming candidate");
   r->state = DRB_CANDIDATE;
   raft_reset(r, r->term + 1, 1);
   raft_set_leader_id(r, 0);
@@ -1246,8 +1282,9 @@ static void raft_campaign(orc_raft *r) {
   uint64_t index = log_last(&r->log);
   uint64_t last_term;
   if (log_term(&r->log, index, &last_term)) orc_panic("campaign: log error");
-  for (int i = 0; i < r->nrem; i++) {
-    if (r->rem_id[i] == r->replica_id) continue;
+  for (int i = 0; i < r->nrem; i++) {  /* votingMembers (raft.go:1202) */
+    if (r->rem_id[i] == r->replica_id || r->rem_kind[i] == ORC_NONVOTING)
+      continue;
     orc_msg m = new_msg(DRB_MSG_REQUEST_VOTE, r->rem_id[i]);
     m.term = term;
     m.log_index = index;
@@ -1262,6 +1299,8 @@ static void raft_become_pre_vote_candidate(orc_raft *r) {
   if (!r->pre_vote) orc_panic("becomePreVoteCandidate: preVote not enabled");
   if (r->state == DRB_LEADER)
     orc_panic("transitioning to candidate state from leader");
+  if (r->state == DRB_NONVOTING) orc_panic("nonVoting is becoming candidate");
+  if (r->state == DRB_WITNESS) orc_panic("witness is becoming candidate");
   r->state = DRB_PREVOTE_CANDIDATE;
   raft_reset(r, r->term, 1);
   raft_set_leader_id(r, 0);
@@ -1280,8 +1319,9 @@ static void raft_pre_vote_campaign(orc_raft *r) {
   uint64_t last_term;
   if (log_term(&r->log, index, &last_term))
     orc_panic("preVoteCampaign: log error");
-  for (int i = 0; i < r->nrem; i++) {
-    if (r->rem_id[i] == r->replica_id) continue;
+  for (int i = 0; i < r->nrem; i++) {  /* votingMembers (raft.go:1160) */
+    if (r->rem_id[i] == r->replica_id || r->rem_kind[i] == ORC_NONVOTING)
+      continue;
     orc_msg m = new_msg(DRB_MSG_REQUEST_PREVOTE, r->rem_id[i]);
     m.term = r->term + 1;
     m.log_index = index;
@@ -1348,10 +1388,15 @@ static int raft_term_not_matched(orc_raft *r, const orc_msg *m) {
                          (m->type == DRB_MSG_REQUEST_PREVOTE_RESP && !m->reject);
     if (!prevote_higher) {
       uint64_t leader = is_leader_message(m->type) ? m->from : 0;
-      if (m->type == DRB_MSG_REQUEST_VOTE)
+      if (r->state == DRB_NONVOTING || r->state == DRB_WITNESS) {
+        /* becomeNonVoting / becomeWitness (raft.go:973-999) */
+        raft_reset(r, m->term, 1);
+        raft_set_leader_id(r, leader);
+      } else if (m->type == DRB_MSG_REQUEST_VOTE) {
         raft_to_follower(r, m->term, leader, 0); /* becomeFollowerKE */
-      else
+      } else {
         raft_to_follower(r, m->term, leader, 1);
+      }
     }
   } else if (m->term < r->term) {
     if (m->type == DRB_MSG_REQUEST_PREVOTE ||
@@ -1397,10 +1442,11 @@ static void raft_report_dropped_ri(orc_raft *r, const orc_msg *m) {
   r->ndropped_ri++;
 }
 
-/* leaderHasQuorum (raft.go:395-405) */
+/* leaderHasQuorum (raft.go:395-405): over the voting members */
 static int raft_leader_has_quorum(orc_raft *r) {
   int c = 0;
   for (int i = 0; i < r->nrem; i++) {
+    if (r->rem_kind[i] == ORC_NONVOTING) continue;
     if (r->rem_id[i] == r->replica_id || r->rem[i].active) {
       c++;
       r->rem[i].active = 0;
@@ -1440,6 +1486,9 @@ static void raft_tick(orc_raft *r) {
     return;
   }
   r->election_tick++;
+  /* a nonVoting or witness replica takes no part in elections (raft.go:
+   * 596-600) */
+  if (r->state == DRB_NONVOTING || r->state == DRB_WITNESS) return;
   if (r->election_tick >= r->randomized_election_timeout) {
     r->election_tick = 0;
     orc_msg el = new_msg(DRB_MSG_ELECTION, 0);
@@ -1521,7 +1570,9 @@ static void handle_leader_heartbeat_resp(orc_raft *r, const orc_msg *m,
 /* handleLeaderReadIndex (raft.go:1842-1876) */
 static void handle_leader_read_index(orc_raft *r, const orc_msg *m) {
   orc_ctx ctx = {m->hint, m->hint_high};
-  if (!raft_single_node_quorum(r)) {
+  if (raft_is_kind(r, m->from, ORC_WITNESS)) {
+    return; /* dropped: a witness node (raft.go:1848-1849) */
+  } else if (!raft_single_node_quorum(r)) {
     if (!raft_has_committed_at_term(r)) {
       raft_report_dropped_ri(r, m);
       return;
@@ -1530,7 +1581,15 @@ static void handle_leader_read_index(orc_raft *r, const orc_msg *m) {
     raft_broadcast_heartbeat_hint(r, ctx);
   } else {
     raft_add_ready(r, r->log.committed, ctx);
-    /* ReadIndexResp to a non-voting requester: none on this path */
+    if (m->from != r->replica_id &&
+        raft_is_kind(r, m->from, ORC_NONVOTING)) {  /* raft.go:1863-1872 */
+      orc_msg resp = new_msg(DRB_MSG_READ_INDEX_RESP, m->from);
+      resp.log_index = r->log.committed;
+      resp.hint = m->hint;
+      resp.hint_high = m->hint_high;
+      resp.commit = m->commit;
+      raft_send(r, &resp);
+    }
   }
 }
 
@@ -1562,7 +1621,7 @@ static void handle_leader_transfer(orc_raft *r, const orc_msg *m) {
   if (raft_leader_transfering(r)) return; /* a transfer is ongoing */
   if (r->replica_id == target) return;    /* pointing to itself */
   int i = raft_rem_idx(r, target);
-  if (i < 0) return; /* unknown target */
+  if (i < 0 || r->rem_kind[i] != ORC_VOTING) return; /* unknown target */
   r->leader_transfer_target = target;
   r->election_tick = 0;
   /* fast path, or wait for the target to catch up (p29, raft thesis) */
@@ -1846,6 +1905,72 @@ static void raft_dispatch(orc_raft *r, orc_msg *m) {
           else
             raft_tick(r);
           return;
+        default:
+          return;
+      }
+    case DRB_NONVOTING: /* raft.go:2396-2407, re-routed to the follower's */
+    case DRB_WITNESS:   /* raft.go:2409-2416 */
+      switch (t) {
+        case DRB_MSG_REPLICATE: /* handleNonVoting/WitnessReplicate */
+          r->election_tick = 0;
+          raft_set_leader_id(r, m->from);
+          raft_handle_replicate_message(r, m);
+          return;
+        case DRB_MSG_HEARTBEAT:
+          r->election_tick = 0;
+          raft_set_leader_id(r, m->from);
+          raft_handle_heartbeat_message(r, m);
+          return;
+        case DRB_MSG_REQUEST_VOTE:
+          handle_node_request_vote(r, m);
+          return;
+        case DRB_MSG_REQUEST_PREVOTE:
+          handle_node_request_pre_vote(r, m);
+          return;
+        case DRB_MSG_LOCAL_TICK:
+          if (m->reject)
+            raft_quiesced_tick(r);
+          else
+            raft_tick(r);
+          return;
+        default:
+          break;
+      }
+      if (r->state == DRB_WITNESS) return; /* no other handlers */
+      switch (t) {
+        case DRB_MSG_PROPOSE: /* handleNonVotingPropose (raft.go:2071) */
+          if (r->leader_id == 0) {
+            r->ndropped_entries += m->ents.n;
+            return;
+          }
+          {
+            orc_msg fwd = *m;
+            memset(&fwd.ents, 0, sizeof(fwd.ents));
+            ev_copy_range(&fwd.ents, m->ents.v, m->ents.n);
+            fwd.to = r->leader_id;
+            raft_send(r, &fwd);
+          }
+          return;
+        case DRB_MSG_READ_INDEX: /* handleNonVotingReadIndex (raft.go:2075) */
+          if (r->leader_id == 0) {
+            raft_report_dropped_ri(r, m);
+            return;
+          }
+          {
+            orc_msg fwd = new_msg(DRB_MSG_READ_INDEX, r->leader_id);
+            fwd.hint = m->hint;
+            fwd.hint_high = m->hint_high;
+            fwd.commit = m->commit;
+            raft_send(r, &fwd);
+          }
+          return;
+        case DRB_MSG_READ_INDEX_RESP: { /* raft.go:2079-2085 */
+          orc_ctx ctx = {m->hint, m->hint_high};
+          r->election_tick = 0;
+          raft_set_leader_id(r, m->from);
+          raft_add_ready(r, m->log_index, ctx);
+          return;
+        }
         default:
           return;
       }
@@ -2546,15 +2671,84 @@ void raft_become_follower(orc_raft *r, uint64_t term, uint64_t leader) {
 
 /* newNetworkWithConfig for a *raft peer (raft_etcd_test.go:2931-2954):
  * replicaID = id, every address a fresh remote, then reset(term, true). */
+/* newNetworkWithConfig for a *raft (raft_etcd_test.go:2932-2957): the
+ * remotes become ids 1..n, each keeping the kind it had (nonVoting,
+ * witness, else voting) */
 int orc_raft_network_reset(orc_raft *r, uint64_t id, const uint64_t *ids,
                            int n) {
   ORC_TRY(-1);
+  uint8_t kind[ORC_MAX_PEERS];
+  for (int i = 0; i < n; i++) {
+    const int k = raft_rem_idx(r, ids[i]);
+    kind[i] = k >= 0 ? r->rem_kind[k] : ORC_VOTING;
+  }
   r->replica_id = id;
   r->nrem = 0;
-  for (int i = 0; i < n; i++) raft_set_remote(r, ids[i], 0, 0);
+  for (int i = 0; i < n; i++) {
+    raft_set_remote(r, ids[i], 0, 0);
+    r->rem_kind[raft_rem_idx(r, ids[i])] = kind[i];
+  }
   raft_reset(r, r->term, 1);
   ORC_END;
   return 0;
+}
+
+/* newTestNonVoting / newTestWitness (raft_etcd_test.go:3099-3140): the
+ * raft starts as a nonVoting (witness) with the given remotes and
+ * nonVotings (witnesses) */
+orc_raft *orc_raft_new_test_kind(uint64_t id, const uint64_t *peers,
+                                 int npeers, const uint64_t *others,
+                                 int nothers, int kind, uint64_t election,
+                                 uint64_t heartbeat, orc_logdb *db) {
+  orc_raft *r = orc_raft_new_test(id, peers, npeers, election, heartbeat, db);
+  if (!r) return NULL;
+  r->state = kind == ORC_NONVOTING ? DRB_NONVOTING : DRB_WITNESS;
+  for (int i = 0; i < nothers; i++) {
+    raft_set_remote(r, others[i], 0, 1);
+    r->rem_kind[raft_rem_idx(r, others[i])] = (uint8_t)kind;
+  }
+  return r;
+}
+
+/* addNode / addNonVoting / addWitness (raft.go:1236-1282) */
+int orc_raft_add_member(orc_raft *r, uint64_t id, int kind) {
+  ORC_TRY(-1);
+  r->pending_config_change = 0;  /* clearPendingConfigChange */
+  const int i = raft_rem_idx(r, id);
+  if (kind == ORC_VOTING) {
+    if (id == r->replica_id && r->state == DRB_WITNESS)
+      orc_panic("is witness");
+    if (i >= 0 && r->rem_kind[i] == ORC_VOTING) {
+      /* already a voting member */
+    } else if (i >= 0 && r->rem_kind[i] == ORC_NONVOTING) {
+      /* promoting to full member with inherited progress info */
+      r->rem_kind[i] = ORC_VOTING;
+      if (id == r->replica_id) {  /* local peer promoted: becomeFollower */
+        r->state = DRB_FOLLOWER;
+        raft_reset(r, r->term, 1);
+        raft_set_leader_id(r, r->leader_id);
+      }
+    } else if (i >= 0) {
+      orc_panic("could not promote witness to full member");
+    } else {
+      raft_set_remote(r, id, 0, log_last(&r->log) + 1);
+    }
+  } else {
+    if (id == r->replica_id &&
+        r->state != (kind == ORC_NONVOTING ? DRB_NONVOTING : DRB_WITNESS))
+      orc_panic("is not a %s", kind == ORC_NONVOTING ? "nonVoting" : "witness");
+    if (i < 0 || r->rem_kind[i] != kind) {
+      raft_set_remote(r, id, 0, log_last(&r->log) + 1);
+      r->rem_kind[raft_rem_idx(r, id)] = (uint8_t)kind;
+    }
+  }
+  ORC_END;
+  return 0;
+}
+
+int orc_raft_remote_kind(orc_raft *r, uint64_t id) {
+  const int i = raft_rem_idx(r, id);
+  return i < 0 ? -1 : r->rem_kind[i];
 }
 
 /* ---- election KAT hooks (raft_etcd_test.go, raft_test.go) ------------- */

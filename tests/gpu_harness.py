@@ -71,6 +71,10 @@ class Pair:
         self.orc = po.Cluster(G, R, seed=seed, election_rtt=election_rtt,
                               quiesce=quiesce)
         self.orc.setup_steady(leader_slot)
+        nv, wt = (engine_kw.get("nonvoting_slots", 0),
+                  engine_kw.get("witness_slots", 0))
+        if nv or wt:  # member kinds (drb_config.nonvoting_slots, ...)
+            self.orc.set_member_kinds(nv, wt)
         if engine_kw.get("pre_vote"):
             self.orc.set_pre_vote(True)
         self.eng.init_steady(term=2, leader_slot=leader_slot, seed=seed)

@@ -102,3 +102,38 @@ def test_kv_overflow_pool_exhausted_stops_apply():
             return
         assert not p.check(), r
     raise AssertionError("the overflow pool never ran out")
+
+
+@pytest.mark.parametrize("val_len,cmd_cap,val_cap,kv_slots", [
+    (4, 32, 4, 64),
+    (60, 80, 64, 4),       # inline values, through the chain
+    (116, 144, 128, 64),   # C5 128 B: values out of line
+    (116, 144, 128, 4)])
+def test_read_values_whole(val_len, cmd_cap, val_cap, kv_slots):
+    """drb_export_read_values: every served read's ReadLocalNode value
+    whole (nodehost.go:849 -> KVTest.Lookup, kvtest.go:164-175), compared
+    with the oracle's KV -- inline and out-of-line values, table and
+    overflow chain."""
+    import struct
+    from dragonboat_amd import workload
+    G, KS = 16, 64
+    p = Pair(G=G, R=3, cmd_cap=cmd_cap, kv_val_cap=val_cap, kv_slots=kv_slots,
+             kv_overflow_buckets=G * 3 * 16, max_props=4,
+             max_reads_per_ctx=9)
+    n = 0
+    for r in range(12):
+        o, e = p.round(k=2, tick=(r % 3 == 0), read_index=True, reads=9,
+                       read_key_space=KS, key_space=KS, val_len=val_len)
+        assert e.fallbacks == 0 and e.errors == 0, (r, p.why())
+        got = p.eng.export_read_values(0, pool_cap=64)  # grows on ERANGE
+        short = p.eng.export_read_results(0)
+        assert [x[:6] for x in got] == [x[:6] for x in short], r
+        for (g, index, low, j, key, found, val) in got:
+            kv = p.orc.export_kv(g, 0)
+            want = kv.get(struct.pack("<Q", key))
+            assert val == want, (r, g, j)
+            x = workload.mix64(low ^ (((j + 1) * workload.GOLDEN) &
+                                      workload.MASK)) % KS
+            assert key == x
+        n += sum(1 for x in got if x[5])
+    assert n > 100
