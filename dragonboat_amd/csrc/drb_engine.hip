@@ -91,6 +91,9 @@ struct drb_engine {
   // counter) and of region copies (host-side sum)
   unsigned long long *xpull_bytes = nullptr;
   uint64_t xcopy_bytes = 0;
+  // the leaders' served reads one thread per read (k_read_lanes) instead of
+  // inside the leader kernel; DRB_READ_LANES=0/1 in the environment
+  bool read_lanes = false;
 };
 
 static void wire_free(drb_engine *e);
@@ -264,6 +267,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->bytes = 0;
   e->scratch = nullptr;
   e->scratch_bytes = 0;
+  if (const char *rl = getenv("DRB_READ_LANES")) e->read_lanes = rl[0] == '1';
   if (hipSetDevice(cfg->device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
           hipSuccess ||
@@ -1775,6 +1779,104 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
                                                      uint32_t n_reads,
                                                      uint32_t key_space,
                                                      uint32_t slots);
+// The leaders' served reads, one thread per read (drb_engine.read_lanes):
+// a workgroup takes the same 256 lanes as a step-kernel block, 64 of them
+// at a time with n_reads threads each, so every lookup of a round is an
+// independent thread instead of one of a lane's dependent batches.  Same
+// results, checksums, served masks and counters as serve_reads_lane.
+constexpr uint32_t READ_LANES_MAX = 16;  // n_reads per thread group
+__global__ __launch_bounds__(1024) void k_read_lanes(const View v,
+                                                     uint32_t n_reads,
+                                                     uint32_t key_space,
+                                                     uint32_t slots) {
+  __shared__ uint64_t term[64 * READ_LANES_MAX];
+  __shared__ uint32_t cnt[2];
+  const uint32_t slot = (slots >> (4 * blockIdx.y)) & 0xfu;
+  const uint32_t T = n_reads, gi = threadIdx.x / T, j = threadIdx.x % T;
+  const uint32_t mask = v.KS - 1;
+  const bool ks_pow2 = (key_space & (key_space - 1)) == 0;
+  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+  uint32_t served = 0, deferred = 0;
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + q * 64 + gi;
+    uint32_t nr = 0;
+    uint64_t sm = 0;
+    if (g < v.G) {
+      nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+      if (nr) {  // the applied index (k_serve_reads)
+        const uint4 c0 = v.pk[pk_ix(v, 0, slot, g)];
+        const uint4 c1 = v.pk[pk_ix(v, 1, slot, g)];
+        const uint64_t last = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+        const uint32_t code = c1.z & 0xffffu;
+        sm = code == PK_ESC16 ? v.u64[u64_ix(v, F_SM_INDEX, slot, g)]
+                              : pk_idx_value(code, last, false);
+      }
+    }
+    uint64_t sum = 0;
+    uint32_t smask = 0;
+    const uint4 *tbl = v.kv + kv_ix(v, slot, g < v.G ? g : 0, 0);
+    for (uint32_t k = 0; k < nr; ++k) {
+      const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+      if (lo64(c0) > sm) {  // pendingReadIndex: not applied yet
+        deferred++;
+        continue;
+      }
+      smask |= 1u << k;
+      const uint64_t x =
+          mix64(hi64(c0) ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
+      const uint64_t key = ks_pow2 ? (x & (key_space - 1)) : x % key_space;
+      const uint32_t home = (uint32_t)kv_hash(key, 8) & mask;
+      uint4 h[DRB_READ_W];
+#pragma unroll
+      for (uint32_t t = 0; t < DRB_READ_W; ++t)
+        h[t] = t < v.KS ? tbl[(uint64_t)kv_probe(v, home, t) * v.KVW]
+                        : make_uint4(0, 0, 0, 0);
+      uint64_t w = ~0ull;
+      bool done = false;
+#pragma unroll
+      for (uint32_t t = 0; t < DRB_READ_W; ++t) {
+        if (done) continue;
+        if (!kv_used(h[t])) {
+          done = true;
+        } else if (kv_match(h[t], key, 8)) {
+          w = kv_word(h[t]);
+          done = true;
+        }
+      }
+      if (!done && (v.KS > DRB_READ_W || v.kv_ovf_head))
+        w = kv_probe_word<true>(v, tbl, home, DRB_READ_W, key, 8, slot, g);
+      sum += mix64(w ^ key ^ ((uint64_t)j << 56));
+      served++;
+      if (v.read_res)
+        v.read_res[rres_ix(v, slot, k, j, g)] =
+            w == ~0ull ? make_uint2(0, 0)
+                       : make_uint2((uint32_t)w,
+                                    (uint32_t)(w >> 32) | 0x80000000u);
+    }
+    term[threadIdx.x] = sum;
+    __syncthreads();
+    if (j == 0 && nr) {  // the lane's checksum and served mask
+      uint64_t t = 0;
+      for (uint32_t i = 0; i < T; ++i) t += term[gi * T + i];
+      v.read_sum[ix(v, slot, g)] = t;
+      if (v.read_res) v.read_served[ix(v, slot, g)] = smask;
+    }
+    __syncthreads();
+  }
+  // the counters of the leader kernel's row for these 256 lanes
+  served = wave_sum(served);
+  deferred = wave_sum(deferred);
+  if ((threadIdx.x & 63) == 0 && (served | deferred)) {
+    atomicAdd(&cnt[0], served);
+    atomicAdd(&cnt[1], deferred);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && cnt[threadIdx.x]) {
+    const uint64_t row = (uint64_t)slot * gridDim.x + blockIdx.x;  // role 0
+    v.counters[row * NUM_COUNTERS + C_READS + threadIdx.x] += cnt[threadIdx.x];
+  }
+}
+
 // Each role's launch covers only the slots where that role occurs (the
 // role map, refreshed after every host-side state change): in the steady
 // state the leader kernel's grid is one slot high, not R.
@@ -1924,6 +2026,10 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   }
   const bool split = DRB_SERVE_SPLIT && !DRB_ROLE_STREAMS && nl && p0.n_reads;
   if (split) pl.n_reads = 0;
+  // the leaders' reads as one thread per read, behind the leader kernel
+  const bool rlanes = !split && e->read_lanes && nl && p0.n_reads &&
+                      p0.n_reads <= READ_LANES_MAX;
+  if (rlanes) pl.n_reads = 0;
   // the EXT instantiation only where its paths can run (drb_step.hpp)
   const bool ext =
       e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves || e->v.quiesce ||
@@ -1938,6 +2044,9 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
   const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
   if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
+  if (rlanes)
+    k_read_lanes<<<dim3(gx, nl), 64 * p0.n_reads, 0, e->stream>>>(
+        e->v, p0.n_reads, p0.key_space, pl.slots);
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);

@@ -29,9 +29,14 @@ def _read_key(low, j, key_space):
     return x % key_space
 
 
-@pytest.mark.parametrize("ri_replica", [0, 2])
-def test_batched_ready_to_reads_and_read_results(ri_replica):
+@pytest.mark.parametrize("ri_replica,read_lanes", [(0, "0"), (2, "0"),
+                                                   (0, "1"), (2, "1")])
+def test_batched_ready_to_reads_and_read_results(ri_replica, read_lanes,
+                                                 monkeypatch):
+    """read_lanes "1": the leaders' reads served one thread per read
+    (k_read_lanes, DRB_READ_LANES) instead of inside the leader kernel."""
     G, R = 300, 3
+    monkeypatch.setenv("DRB_READ_LANES", read_lanes)
     p = Pair(G=G, R=R, max_reads_per_ctx=READS)
     slot = 0 if ri_replica == 0 else ri_replica - 1
     n_rtr = n_res = found = 0
@@ -54,6 +59,11 @@ def test_batched_ready_to_reads_and_read_results(ri_replica):
         res = p.eng.export_read_results(slot)
         sums, served, deferred = p.orc.serve_reads(READS, KEYS)
         assert len(res) == served == e.reads_served, rnd
+        assert e.reads_deferred == deferred, rnd
+        esums = p.eng.export_read_sums(0, G)
+        for i, x in enumerate(sums):
+            if x is not None:
+                assert esums[i] == x, (rnd, i)
         exp = []
         for g in range(G):
             st = p.orc.export(g, slot)
