@@ -147,6 +147,10 @@ def parse():
                          "behind the round (no host sync) or sized by an "
                          "all_gather of per-plane counts (dragonboat_amd/"
                          "exchange.py)")
+    ap.add_argument("--read-results", type=int, default=1,
+                    help="c3: the timed reads write each client's "
+                         "ReadLocalNode result (drb_config.max_reads_per_"
+                         "ctx); 0 keeps only the per-replica checksum")
     ap.add_argument("--local-ranks", type=int, default=0,
                     help="c4 in ONE process on one GPU: N engines (ranks of "
                          "the placement) stepped together, their planes "
@@ -471,7 +475,8 @@ def main():
                      elections=args.elections,
                      # the timed reads leave each client's ReadLocalNode
                      # result (drb_export_read_results / the step worker)
-                     max_reads_per_ctx=READS_PER_CTX if reads else 0,
+                     max_reads_per_ctx=(READS_PER_CTX if reads and
+                                        args.read_results else 0),
                      first_shard_id=first_shard, device=local)
     eng.init_steady(term=2, leader_slot=0, seed=seed)
     stream = torch.cuda.ExternalStream(eng.stream)
@@ -768,7 +773,7 @@ def main():
                     "+ scans and a layout kernel), timed around the whole "
                     "loop; not `value`"}
         if args.step_worker < 0:
-            args.step_worker = int(reads and not c2)
+            args.step_worker = int(reads and not c2 and args.read_results)
         if args.step_worker:
             # engine.processSteps as a whole (engine.go:1304-1364): the
             # entry queue up, the round, and every output a step worker

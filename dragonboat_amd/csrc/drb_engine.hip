@@ -1779,72 +1779,82 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
                                                      uint32_t n_reads,
                                                      uint32_t key_space,
                                                      uint32_t slots);
-// The leaders' served reads, one thread per read (drb_engine.read_lanes):
-// a workgroup takes the same 256 lanes as a step-kernel block, 64 of them
-// at a time with n_reads threads each, so every lookup of a round is an
-// independent thread instead of one of a lane's dependent batches.  Same
-// results, checksums, served masks and counters as serve_reads_lane.
-constexpr uint32_t READ_LANES_MAX = 16;  // n_reads per thread group
-__global__ __launch_bounds__(1024) void k_read_lanes(const View v,
+// The leaders' served reads as their own launch (drb_engine.read_lanes):
+// one quad of lanes per read.  The 4 lanes of a quad load the 4 slots of
+// the read's home probe group -- one 64 B line, one memory request for the
+// quad instead of four per lane -- and resolve the probe order by ballot
+// (the first empty slot or match; a full group with no match continues
+// serially in the quad's first lane).  A workgroup takes 256 / (4 n_reads)
+// groups of n_reads quads.  Same results, checksums, served masks and counters as
+// serve_reads_lane.
+constexpr uint32_t READ_LANES_MAX = 16;  // n_reads
+__global__ __launch_bounds__(256) void k_read_lanes(const View v,
                                                      uint32_t n_reads,
                                                      uint32_t key_space,
-                                                     uint32_t slots) {
-  __shared__ uint64_t term[64 * READ_LANES_MAX];
+                                                     uint32_t slots,
+                                                     uint32_t role) {
+  __shared__ unsigned long long gsum[64];
   __shared__ uint32_t cnt[2];
   const uint32_t slot = (slots >> (4 * blockIdx.y)) & 0xfu;
-  const uint32_t T = n_reads, gi = threadIdx.x / T, j = threadIdx.x % T;
+  const uint32_t T = 4 * n_reads, GB = 256 / T;
+  const uint32_t gl = threadIdx.x / T, j = (threadIdx.x % T) >> 2,
+                 q = threadIdx.x & 3u;
+  if (threadIdx.x < GB) gsum[threadIdx.x] = 0;
+  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t g = (uint64_t)blockIdx.x * GB + gl;
+  const bool ok = gl < GB && g < v.G;
   const uint32_t mask = v.KS - 1;
   const bool ks_pow2 = (key_space & (key_space - 1)) == 0;
-  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
-  uint32_t served = 0, deferred = 0;
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint64_t g = (uint64_t)blockIdx.x * 256 + q * 64 + gi;
-    uint32_t nr = 0;
-    uint64_t sm = 0;
-    if (g < v.G) {
-      nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
-      if (nr) {  // the applied index (k_serve_reads)
-        const uint4 c0 = v.pk[pk_ix(v, 0, slot, g)];
-        const uint4 c1 = v.pk[pk_ix(v, 1, slot, g)];
-        const uint64_t last = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
-        const uint32_t code = c1.z & 0xffffu;
-        sm = code == PK_ESC16 ? v.u64[u64_ix(v, F_SM_INDEX, slot, g)]
-                              : pk_idx_value(code, last, false);
+  const bool quad = kv_spl(v) == 4 && v.KS >= 4;  // 16 B slots: a 64 B group
+  uint32_t nr = 0, smask = 0, served = 0, deferred = 0;
+  uint64_t sm = 0;
+  if (ok) {
+    nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+    if (nr) {  // the applied index (k_serve_reads)
+      const uint4 c0 = v.pk[pk_ix(v, 0, slot, g)];
+      const uint4 c1 = v.pk[pk_ix(v, 1, slot, g)];
+      const uint64_t last = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+      const uint32_t code = c1.z & 0xffffu;
+      sm = code == PK_ESC16 ? v.u64[u64_ix(v, F_SM_INDEX, slot, g)]
+                            : pk_idx_value(code, last, false);
+    }
+  }
+  const uint4 *tbl = v.kv + kv_ix(v, slot, ok ? g : 0, 0);
+  const uint32_t base = threadIdx.x & 63u & ~3u;  // the quad in its wave
+  uint64_t sum = 0;
+  for (uint32_t k = 0; k < nr; ++k) {  // (uniform within a quad)
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    if (lo64(c0) > sm) {  // pendingReadIndex: not applied yet
+      deferred += q == 0;
+      continue;
+    }
+    smask |= 1u << k;
+    const uint64_t x =
+        mix64(hi64(c0) ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
+    const uint64_t key = ks_pow2 ? (x & (key_space - 1)) : x % key_space;
+    const uint32_t home = (uint32_t)kv_hash(key, 8) & mask;
+    uint64_t w = ~0ull;
+    bool more = true;
+    if (quad) {
+      const uint4 h = tbl[(uint64_t)kv_probe(v, home, q) * v.KVW];
+      const bool empty = !kv_used(h), hit = kv_match(h, key, 8);
+      const uint64_t be = __ballot(empty), bh = __ballot(hit);
+      const uint32_t e4 = (uint32_t)(be >> base) & 15u,
+                     h4 = (uint32_t)(bh >> base) & 15u;
+      const uint32_t stop = e4 | h4;
+      const uint64_t hw = kv_word(h);
+      const uint32_t first = stop ? (uint32_t)__builtin_ctz(stop) : 0u;
+      const uint64_t wf = __shfl(hw, (int)((threadIdx.x & ~3u) + first), 64);
+      if (stop) {
+        more = false;
+        if ((h4 >> first) & 1u) w = wf;
       }
     }
-    uint64_t sum = 0;
-    uint32_t smask = 0;
-    const uint4 *tbl = v.kv + kv_ix(v, slot, g < v.G ? g : 0, 0);
-    for (uint32_t k = 0; k < nr; ++k) {
-      const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
-      if (lo64(c0) > sm) {  // pendingReadIndex: not applied yet
-        deferred++;
-        continue;
-      }
-      smask |= 1u << k;
-      const uint64_t x =
-          mix64(hi64(c0) ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
-      const uint64_t key = ks_pow2 ? (x & (key_space - 1)) : x % key_space;
-      const uint32_t home = (uint32_t)kv_hash(key, 8) & mask;
-      uint4 h[DRB_READ_W];
-#pragma unroll
-      for (uint32_t t = 0; t < DRB_READ_W; ++t)
-        h[t] = t < v.KS ? tbl[(uint64_t)kv_probe(v, home, t) * v.KVW]
-                        : make_uint4(0, 0, 0, 0);
-      uint64_t w = ~0ull;
-      bool done = false;
-#pragma unroll
-      for (uint32_t t = 0; t < DRB_READ_W; ++t) {
-        if (done) continue;
-        if (!kv_used(h[t])) {
-          done = true;
-        } else if (kv_match(h[t], key, 8)) {
-          w = kv_word(h[t]);
-          done = true;
-        }
-      }
-      if (!done && (v.KS > DRB_READ_W || v.kv_ovf_head))
-        w = kv_probe_word<true>(v, tbl, home, DRB_READ_W, key, 8, slot, g);
+    if (q == 0) {
+      if (more)  // a full first group (or another slot geometry)
+        w = kv_probe_word<true>(v, tbl, home, quad ? 4u : 0u, key, 8, slot,
+                                g);
       sum += mix64(w ^ key ^ ((uint64_t)j << 56));
       served++;
       if (v.read_res)
@@ -1853,17 +1863,8 @@ __global__ __launch_bounds__(1024) void k_read_lanes(const View v,
                        : make_uint2((uint32_t)w,
                                     (uint32_t)(w >> 32) | 0x80000000u);
     }
-    term[threadIdx.x] = sum;
-    __syncthreads();
-    if (j == 0 && nr) {  // the lane's checksum and served mask
-      uint64_t t = 0;
-      for (uint32_t i = 0; i < T; ++i) t += term[gi * T + i];
-      v.read_sum[ix(v, slot, g)] = t;
-      if (v.read_res) v.read_served[ix(v, slot, g)] = smask;
-    }
-    __syncthreads();
   }
-  // the counters of the leader kernel's row for these 256 lanes
+  if (q == 0 && nr) atomicAdd(&gsum[gl], (unsigned long long)sum);
   served = wave_sum(served);
   deferred = wave_sum(deferred);
   if ((threadIdx.x & 63) == 0 && (served | deferred)) {
@@ -1871,9 +1872,18 @@ __global__ __launch_bounds__(1024) void k_read_lanes(const View v,
     atomicAdd(&cnt[1], deferred);
   }
   __syncthreads();
+  if (ok && nr && j == 0 && q == 0) {  // the lane's checksum and mask
+    v.read_sum[ix(v, slot, g)] = gsum[gl];
+    if (v.read_res) v.read_served[ix(v, slot, g)] = smask;
+  }
+  // the counters: any row of the role and slot (k_sum_counters adds them)
   if (threadIdx.x < 2 && cnt[threadIdx.x]) {
-    const uint64_t row = (uint64_t)slot * gridDim.x + blockIdx.x;  // role 0
-    v.counters[row * NUM_COUNTERS + C_READS + threadIdx.x] += cnt[threadIdx.x];
+    const uint64_t gx = (v.G + 255) / 256;
+    const uint64_t row = ((uint64_t)role * v.R + slot) * gx +
+                         ((uint64_t)blockIdx.x * GB / 256) % gx;
+    atomicAdd((unsigned long long *)&v.counters[row * NUM_COUNTERS + C_READS +
+                                                threadIdx.x],
+              (unsigned long long)cnt[threadIdx.x]);
   }
 }
 
@@ -2027,6 +2037,8 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const bool split = DRB_SERVE_SPLIT && !DRB_ROLE_STREAMS && nl && p0.n_reads;
   if (split) pl.n_reads = 0;
   // the leaders' reads as one thread per read, behind the leader kernel
+  // (a follower's ReadyToReads come from its own forwarded ReadIndex, a
+  // round later and rarely: the follower kernel keeps serving them)
   const bool rlanes = !split && e->read_lanes && nl && p0.n_reads &&
                       p0.n_reads <= READ_LANES_MAX;
   if (rlanes) pl.n_reads = 0;
@@ -2044,9 +2056,11 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
   const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
   if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
-  if (rlanes)
-    k_read_lanes<<<dim3(gx, nl), 64 * p0.n_reads, 0, e->stream>>>(
-        e->v, p0.n_reads, p0.key_space, pl.slots);
+  if (rlanes) {
+    const uint32_t T = 4 * p0.n_reads, GB = 256 / T;
+    k_read_lanes<<<dim3((unsigned)((e->v.G + GB - 1) / GB), nl), GB * T, 0,
+                   e->stream>>>(e->v, p0.n_reads, p0.key_space, pl.slots, 0);
+  }
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
@@ -2840,8 +2854,12 @@ struct PullArgs {
 
 __global__ void __launch_bounds__(256)
     k_plane_pull(View v, PullArgs a, unsigned long long *bytes) {
+  // thread (lane g, plane, position k): the plane's record at mailbox
+  // position k and its entry row k -- a header read (shared by the plane's
+  // threads through the caches) and then independent copies
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t from = blockIdx.y / v.R, to = blockIdx.y % v.R;
+  const uint32_t k = blockIdx.z;
   uint64_t moved = 0;
   if (g < v.G && from != to && pair_remote(v, from, to)) {
     // the sender of plane (from, to) into rank d (drb_place_peer, dir 1)
@@ -2850,36 +2868,37 @@ __global__ void __launch_bounds__(256)
     const uint64_t hi = mmeta_ix(v, a.buf, from, to, g);
     const uint4 h = s.meta[hi];
     if (tag_is(h.x, a.tag)) {
-      v.meta_in[hi] = h;
-      moved += 16;
       const uint32_t nrep = mi_nrep(h.y), noth = mi_noth(h.y);
-      for (uint32_t j = 0; j < nrep + noth; ++j) {
-        const uint32_t k = rec_pos(j < nrep, j < nrep ? j : j - nrep, v.MB);
+      if (k == 0) {
+        v.meta_in[hi] = h;
+        moved += 16;
+      }
+      if (k < v.MB && (k < nrep || k >= v.MB - noth)) {
         for (uint32_t c = 0; c < MSG_CHUNKS; ++c) {
           const uint64_t ix = mbox_ix(v, a.buf, from, to, k, c, g);
           v.mbox_in[ix] = s.mbox[ix];
         }
+        moved += MSG_CHUNKS * 16;
         if (v.rterm_in) {
           const uint64_t ix = rterm_ix(v, a.buf, from, to, k, g);
           v.rterm_in[ix] = s.rterm[ix];
+          moved += 8;
         }
       }
-      moved += (uint64_t)(nrep + noth) *
-               (MSG_CHUNKS * 16 + (v.rterm_in ? 8 : 0));
-      if (nrep) {
+      if (nrep && (k == 0 || k < v.E)) {
         const uint64_t mx = s.maxapp[hi], lo = s.elo[hi];
-        v.maxapp_in[hi] = mx;
-        v.elo_in[hi] = lo;
-        moved += 16;
-        if (v.E && lo != ~0ull && mx >= lo) {
-          const uint64_t rows = mx - lo + 1 < v.E ? mx - lo + 1 : v.E;
+        if (k == 0) {
+          v.maxapp_in[hi] = mx;
+          v.elo_in[hi] = lo;
+          moved += 16;
+        }
+        if (k < v.E && lo != ~0ull && mx >= lo && k <= mx - lo) {
           const uint32_t chunks = ENT_META + v.C16;
-          for (uint32_t e = 0; e < rows; ++e)
-            for (uint32_t c = 0; c < chunks; ++c) {
-              const uint64_t ix = embox_ix(v, a.buf, from, to, e, c, g);
-              v.embox_in[ix] = s.embox[ix];
-            }
-          moved += rows * chunks * 16;
+          for (uint32_t c = 0; c < chunks; ++c) {
+            const uint64_t ix = embox_ix(v, a.buf, from, to, k, c, g);
+            v.embox_in[ix] = s.embox[ix];
+          }
+          moved += chunks * 16;
         }
       }
     }
@@ -2909,7 +2928,8 @@ static int exchange_pull(drb_engine *const *engines, uint32_t n) {
     a.src[r] = {v.mbox, v.mbox_meta, v.embox, v.mbox_maxapp, v.elo, v.rterm};
     HIPCHK(hipEventRecord(engines[r]->ev_xsend, engines[r]->stream));
   }
-  const dim3 grid((unsigned)((v0.G + 255) / 256), v0.R * v0.R);
+  const dim3 grid((unsigned)((v0.G + 255) / 256), v0.R * v0.R,
+                  v0.MB > v0.E ? v0.MB : (v0.E ? v0.E : 1u));
   for (uint32_t d = 0; d < n; ++d) {
     drb_engine *e = engines[d];
     if (!e->xpull_bytes && dalloc(e, &e->xpull_bytes, 1)) return DRB_ENOMEM;

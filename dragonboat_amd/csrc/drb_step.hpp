@@ -2481,6 +2481,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   constexpr int PFN = SLOW ? 0 : LEAD ? DRB_LPF : DRB_FPF;
   constexpr bool FPF = PFN > 0;
   constexpr int PFS = 1;
+  // the LDS row of a prefetch goes through M0 (wave-uniform): one sender
+  // row only, whose index does not depend on the lane
+  static_assert(PFS == 1 || !FPF, "per-lane prefetch rows need PFS == 1");
   __shared__ uint4 pf_lds[FPF ? PFS : 1][FPF ? PFN : 1][FPF ? 256 : 1];
   constexpr int NPH = (DRB_PHASE_PROF && !SLOW) ? 8 : 1;
   __shared__ uint32_t ph_lds[NPH][NPH > 1 ? 256 : 1];
