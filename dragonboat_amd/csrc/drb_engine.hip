@@ -94,6 +94,9 @@ struct drb_engine {
   // the leaders' served reads one thread per read (k_read_lanes) instead of
   // inside the leader kernel; DRB_READ_LANES=0/1 in the environment
   bool read_lanes = false;
+  // drb_plane_counts has read the plane summaries (xrows): the rounds clear
+  // them from then on
+  bool xrows_used = false;
 };
 
 static void wire_free(drb_engine *e);
@@ -1780,30 +1783,28 @@ __global__ __launch_bounds__(256) void k_serve_reads(const View v,
                                                      uint32_t key_space,
                                                      uint32_t slots);
 // The leaders' served reads as their own launch (drb_engine.read_lanes):
-// one quad of lanes per read.  The 4 lanes of a quad load the 4 slots of
-// the read's home probe group -- one 64 B line, one memory request for the
-// quad instead of four per lane -- and resolve the probe order by ballot
-// (the first empty slot or match; a full group with no match continues
-// serially in the quad's first lane).  A workgroup takes 256 / (4 n_reads)
-// groups of n_reads quads.  Same results, checksums, served masks and counters as
-// serve_reads_lane.
+// a workgroup takes 64 groups, one quad of lanes per group.  For each read
+// the quad's 4 lanes load the 4 slots of its home probe group -- one 64 B
+// line, one memory request per quad -- and resolve the probe order by
+// ballot (the first empty slot or match; a full group with no match
+// continues serially in the quad's first lane).  The n_reads lookups of a
+// ctx are all issued before any is resolved, and the results go out as
+// rows of consecutive groups.  Same results, checksums, served masks and
+// counters as serve_reads_lane.
 constexpr uint32_t READ_LANES_MAX = 16;  // n_reads
+constexpr uint32_t READ_QBATCH = 9;      // lookups in flight per lane
 __global__ __launch_bounds__(256) void k_read_lanes(const View v,
                                                      uint32_t n_reads,
                                                      uint32_t key_space,
                                                      uint32_t slots,
                                                      uint32_t role) {
-  __shared__ unsigned long long gsum[64];
   __shared__ uint32_t cnt[2];
   const uint32_t slot = (slots >> (4 * blockIdx.y)) & 0xfu;
-  const uint32_t T = 4 * n_reads, GB = 256 / T;
-  const uint32_t gl = threadIdx.x / T, j = (threadIdx.x % T) >> 2,
-                 q = threadIdx.x & 3u;
-  if (threadIdx.x < GB) gsum[threadIdx.x] = 0;
+  const uint32_t q = threadIdx.x & 3u;
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t g = (uint64_t)blockIdx.x * GB + gl;
-  const bool ok = gl < GB && g < v.G;
+  const bool ok = g < v.G;
   const uint32_t mask = v.KS - 1;
   const bool ks_pow2 = (key_space & (key_space - 1)) == 0;
   const bool quad = kv_spl(v) == 4 && v.KS >= 4;  // 16 B slots: a 64 B group
@@ -1826,45 +1827,65 @@ __global__ __launch_bounds__(256) void k_read_lanes(const View v,
   for (uint32_t k = 0; k < nr; ++k) {  // (uniform within a quad)
     const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
     if (lo64(c0) > sm) {  // pendingReadIndex: not applied yet
-      deferred += q == 0;
+      if (q == 0) deferred += n_reads;
       continue;
     }
     smask |= 1u << k;
-    const uint64_t x =
-        mix64(hi64(c0) ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
-    const uint64_t key = ks_pow2 ? (x & (key_space - 1)) : x % key_space;
-    const uint32_t home = (uint32_t)kv_hash(key, 8) & mask;
-    uint64_t w = ~0ull;
-    bool more = true;
-    if (quad) {
-      const uint4 h = tbl[(uint64_t)kv_probe(v, home, q) * v.KVW];
-      const bool empty = !kv_used(h), hit = kv_match(h, key, 8);
-      const uint64_t be = __ballot(empty), bh = __ballot(hit);
-      const uint32_t e4 = (uint32_t)(be >> base) & 15u,
-                     h4 = (uint32_t)(bh >> base) & 15u;
-      const uint32_t stop = e4 | h4;
-      const uint64_t hw = kv_word(h);
-      const uint32_t first = stop ? (uint32_t)__builtin_ctz(stop) : 0u;
-      const uint64_t wf = __shfl(hw, (int)((threadIdx.x & ~3u) + first), 64);
-      if (stop) {
-        more = false;
-        if ((h4 >> first) & 1u) w = wf;
+    for (uint32_t j0 = 0; j0 < n_reads; j0 += READ_QBATCH) {
+    // (the keys are recomputed at resolution: registers for the loads)
+    auto key_of = [&](uint32_t j) {
+      const uint64_t x =
+          mix64(hi64(c0) ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
+      return ks_pow2 ? (x & (key_space - 1)) : x % key_space;
+    };
+    uint4 h[READ_QBATCH];
+#pragma unroll
+    for (uint32_t t = 0; t < READ_QBATCH; ++t) {
+      const uint32_t j = j0 + t;
+      if (j >= n_reads) continue;
+      const uint32_t hm = (uint32_t)kv_hash(key_of(j), 8) & mask;
+      h[t] = quad ? tbl[(uint64_t)kv_probe(v, hm, q) * v.KVW]
+                  : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < READ_QBATCH; ++t) {
+      const uint32_t j = j0 + t;
+      if (j >= n_reads) continue;
+      const uint64_t key = key_of(j);
+      uint64_t w = ~0ull;
+      bool more = true;
+      if (quad) {
+        const bool empty = !kv_used(h[t]), hit = kv_match(h[t], key, 8);
+        const uint32_t e4 = (uint32_t)(__ballot(empty) >> base) & 15u,
+                       h4 = (uint32_t)(__ballot(hit) >> base) & 15u;
+        const uint32_t stop = e4 | h4;
+        const uint32_t first = stop ? (uint32_t)__builtin_ctz(stop) : 0u;
+        const uint64_t wf =
+            __shfl(kv_word(h[t]), (int)((threadIdx.x & ~3u) + first), 64);
+        if (stop) {
+          more = false;
+          if ((h4 >> first) & 1u) w = wf;
+        }
+      }
+      if (q == 0) {
+        if (more)  // a full first group (or another slot geometry)
+          w = kv_probe_word<true>(v, tbl, (uint32_t)kv_hash(key, 8) & mask,
+                                  quad ? 4u : 0u, key, 8, slot, g);
+        sum += mix64(w ^ key ^ ((uint64_t)j << 56));
+        served++;
+        if (v.read_res)
+          v.read_res[rres_ix(v, slot, k, j, g)] =
+              w == ~0ull ? make_uint2(0, 0)
+                         : make_uint2((uint32_t)w,
+                                      (uint32_t)(w >> 32) | 0x80000000u);
       }
     }
-    if (q == 0) {
-      if (more)  // a full first group (or another slot geometry)
-        w = kv_probe_word<true>(v, tbl, home, quad ? 4u : 0u, key, 8, slot,
-                                g);
-      sum += mix64(w ^ key ^ ((uint64_t)j << 56));
-      served++;
-      if (v.read_res)
-        v.read_res[rres_ix(v, slot, k, j, g)] =
-            w == ~0ull ? make_uint2(0, 0)
-                       : make_uint2((uint32_t)w,
-                                    (uint32_t)(w >> 32) | 0x80000000u);
     }
   }
-  if (q == 0 && nr) atomicAdd(&gsum[gl], (unsigned long long)sum);
+  if (ok && nr && q == 0) {  // the lane's checksum and served mask
+    v.read_sum[ix(v, slot, g)] = sum;
+    if (v.read_res) v.read_served[ix(v, slot, g)] = smask;
+  }
   served = wave_sum(served);
   deferred = wave_sum(deferred);
   if ((threadIdx.x & 63) == 0 && (served | deferred)) {
@@ -1872,17 +1893,12 @@ __global__ __launch_bounds__(256) void k_read_lanes(const View v,
     atomicAdd(&cnt[1], deferred);
   }
   __syncthreads();
-  if (ok && nr && j == 0 && q == 0) {  // the lane's checksum and mask
-    v.read_sum[ix(v, slot, g)] = gsum[gl];
-    if (v.read_res) v.read_served[ix(v, slot, g)] = smask;
-  }
   // the counters: any row of the role and slot (k_sum_counters adds them)
   if (threadIdx.x < 2 && cnt[threadIdx.x]) {
     const uint64_t gx = (v.G + 255) / 256;
-    const uint64_t row = ((uint64_t)role * v.R + slot) * gx +
-                         ((uint64_t)blockIdx.x * GB / 256) % gx;
-    atomicAdd((unsigned long long *)&v.counters[row * NUM_COUNTERS + C_READS +
-                                                threadIdx.x],
+    const uint64_t row =
+        ((uint64_t)role * v.R + slot) * gx + (blockIdx.x / 4) % gx;
+    atomicAdd(&v.counters[row * NUM_COUNTERS + C_READS + threadIdx.x],
               (unsigned long long)cnt[threadIdx.x]);
   }
 }
@@ -2056,11 +2072,9 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
   const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
   if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
-  if (rlanes) {
-    const uint32_t T = 4 * p0.n_reads, GB = 256 / T;
-    k_read_lanes<<<dim3((unsigned)((e->v.G + GB - 1) / GB), nl), GB * T, 0,
+  if (rlanes)
+    k_read_lanes<<<dim3((unsigned)((e->v.G + 63) / 64), nl), 256, 0,
                    e->stream>>>(e->v, p0.n_reads, p0.key_space, pl.slots, 0);
-  }
   if (split) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
@@ -2197,11 +2211,14 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
     return DRB_EINVAL;
   if (e->v.elections)  // this round's slow list
     HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
-  if (e->v.remote_mask)  // plane summaries of this round only
+  // plane summaries of this round only -- once a host reads them
+  // (drb_plane_counts: the counted exchange); until then they only grow (a
+  // max / or over rounds, an over-estimate a first counted read can take)
+  if (e->v.remote_mask && e->xrows_used)
     HIPCHK(hipMemsetAsync(e->v.xrows, 0,
                           2ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
                           e->stream));
-  if (e->v.xslow)
+  if (e->v.xslow && e->xrows_used)
     HIPCHK(hipMemsetAsync(e->v.xslow, 0,
                           4ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
                           e->stream));
@@ -2702,6 +2719,7 @@ extern "C" int drb_plane_counts(drb_engine *e, uint32_t *words) {
     memset(words, 0, RR * sizeof(uint32_t));
     return DRB_OK;
   }
+  e->xrows_used = true;  // the rounds clear the summaries from now on
   const uint32_t blocks = (uint32_t)((v.G + 255) / 256);
   k_plane_sum<<<RR, 256, 0, e->stream>>>(v.xrows, v.xslow, RR, blocks,
                                          e->xcount);
@@ -2842,6 +2860,7 @@ static uint32_t full_word(const View &v, bool leader_sender) {
 // whose sender header is not of this round keeps its inbound plane as it is
 // (its receiver reads only headers of the round, tag_is).
 constexpr uint32_t PULL_MAX = 16;
+constexpr uint32_t PULL_BATCH = 8;  // record / row chunks in flight per lane
 struct PullSrc {
   const uint4 *mbox, *meta, *embox;
   const uint64_t *maxapp, *elo, *rterm;
@@ -2854,12 +2873,8 @@ struct PullArgs {
 
 __global__ void __launch_bounds__(256)
     k_plane_pull(View v, PullArgs a, unsigned long long *bytes) {
-  // thread (lane g, plane, position k): the plane's record at mailbox
-  // position k and its entry row k -- a header read (shared by the plane's
-  // threads through the caches) and then independent copies
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t from = blockIdx.y / v.R, to = blockIdx.y % v.R;
-  const uint32_t k = blockIdx.z;
   uint64_t moved = 0;
   if (g < v.G && from != to && pair_remote(v, from, to)) {
     // the sender of plane (from, to) into rank d (drb_place_peer, dir 1)
@@ -2868,37 +2883,65 @@ __global__ void __launch_bounds__(256)
     const uint64_t hi = mmeta_ix(v, a.buf, from, to, g);
     const uint4 h = s.meta[hi];
     if (tag_is(h.x, a.tag)) {
+      v.meta_in[hi] = h;
+      moved += 16;
       const uint32_t nrep = mi_nrep(h.y), noth = mi_noth(h.y);
-      if (k == 0) {
-        v.meta_in[hi] = h;
-        moved += 16;
+      const uint32_t n = nrep + noth;
+      uint64_t mx = 0, lo = ~0ull;
+      if (nrep) {
+        mx = s.maxapp[hi];
+        lo = s.elo[hi];
       }
-      if (k < v.MB && (k < nrep || k >= v.MB - noth)) {
-        for (uint32_t c = 0; c < MSG_CHUNKS; ++c) {
-          const uint64_t ix = mbox_ix(v, a.buf, from, to, k, c, g);
-          v.mbox_in[ix] = s.mbox[ix];
-        }
-        moved += MSG_CHUNKS * 16;
-        if (v.rterm_in) {
-          const uint64_t ix = rterm_ix(v, a.buf, from, to, k, g);
-          v.rterm_in[ix] = s.rterm[ix];
-          moved += 8;
-        }
-      }
-      if (nrep && (k == 0 || k < v.E)) {
-        const uint64_t mx = s.maxapp[hi], lo = s.elo[hi];
-        if (k == 0) {
-          v.maxapp_in[hi] = mx;
-          v.elo_in[hi] = lo;
-          moved += 16;
-        }
-        if (k < v.E && lo != ~0ull && mx >= lo && k <= mx - lo) {
-          const uint32_t chunks = ENT_META + v.C16;
-          for (uint32_t c = 0; c < chunks; ++c) {
-            const uint64_t ix = embox_ix(v, a.buf, from, to, k, c, g);
-            v.embox_in[ix] = s.embox[ix];
+      // the records, PULL_BATCH at a time: every load of a batch issued
+      // before its stores (one memory round trip per batch)
+      for (uint32_t j0 = 0; j0 < n; j0 += PULL_BATCH) {
+        uint4 r0[PULL_BATCH], r1[PULL_BATCH];
+#pragma unroll
+        for (uint32_t t = 0; t < PULL_BATCH; ++t) {
+          const uint32_t jj = j0 + t;
+          const uint32_t k = rec_pos(jj < nrep, jj < nrep ? jj : jj - nrep, v.MB);
+          if (jj < n) {
+            r0[t] = s.mbox[mbox_ix(v, a.buf, from, to, k, 0, g)];
+            r1[t] = s.mbox[mbox_ix(v, a.buf, from, to, k, 1, g)];
           }
-          moved += chunks * 16;
+        }
+#pragma unroll
+        for (uint32_t t = 0; t < PULL_BATCH; ++t) {
+          const uint32_t jj = j0 + t;
+          const uint32_t k = rec_pos(jj < nrep, jj < nrep ? jj : jj - nrep, v.MB);
+          if (jj < n) {
+            v.mbox_in[mbox_ix(v, a.buf, from, to, k, 0, g)] = r0[t];
+            v.mbox_in[mbox_ix(v, a.buf, from, to, k, 1, g)] = r1[t];
+            if (v.rterm_in) {
+              const uint64_t ix = rterm_ix(v, a.buf, from, to, k, g);
+              v.rterm_in[ix] = s.rterm[ix];
+            }
+          }
+        }
+      }
+      moved += (uint64_t)n * (MSG_CHUNKS * 16 + (v.rterm_in ? 8 : 0));
+      if (nrep) {
+        v.maxapp_in[hi] = mx;
+        v.elo_in[hi] = lo;
+        moved += 16;
+        if (v.E && lo != ~0ull && mx >= lo) {
+          const uint64_t rows = mx - lo + 1 < v.E ? mx - lo + 1 : v.E;
+          const uint32_t chunks = ENT_META + v.C16;
+          const uint32_t total = (uint32_t)rows * chunks;
+          for (uint32_t c0 = 0; c0 < total; c0 += PULL_BATCH) {
+            uint4 q[PULL_BATCH];
+#pragma unroll
+            for (uint32_t t = 0; t < PULL_BATCH; ++t)
+              if (c0 + t < total)
+                q[t] = s.embox[embox_ix(v, a.buf, from, to, (c0 + t) / chunks,
+                                        (c0 + t) % chunks, g)];
+#pragma unroll
+            for (uint32_t t = 0; t < PULL_BATCH; ++t)
+              if (c0 + t < total)
+                v.embox_in[embox_ix(v, a.buf, from, to, (c0 + t) / chunks,
+                                    (c0 + t) % chunks, g)] = q[t];
+          }
+          moved += (uint64_t)total * 16;
         }
       }
     }
@@ -2928,8 +2971,7 @@ static int exchange_pull(drb_engine *const *engines, uint32_t n) {
     a.src[r] = {v.mbox, v.mbox_meta, v.embox, v.mbox_maxapp, v.elo, v.rterm};
     HIPCHK(hipEventRecord(engines[r]->ev_xsend, engines[r]->stream));
   }
-  const dim3 grid((unsigned)((v0.G + 255) / 256), v0.R * v0.R,
-                  v0.MB > v0.E ? v0.MB : (v0.E ? v0.E : 1u));
+  const dim3 grid((unsigned)((v0.G + 255) / 256), v0.R * v0.R);
   for (uint32_t d = 0; d < n; ++d) {
     drb_engine *e = engines[d];
     if (!e->xpull_bytes && dalloc(e, &e->xpull_bytes, 1)) return DRB_ENOMEM;

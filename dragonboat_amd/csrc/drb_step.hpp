@@ -91,6 +91,10 @@ namespace drb {
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
+// the served reads before the state store (1) or after the outbox headers
+#ifndef DRB_READS_EARLY
+#define DRB_READS_EARLY 0
+#endif
 // timing only: per-phase cycle sums of the leader / follower lanes
 // (View.phase, drb_debug_phase); 0 in shipped builds
 #ifndef DRB_PHASE_PROF
@@ -3282,6 +3286,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         }
         last_final = r.last;
       }
+      // DRB_READS_EARLY: the served reads issued before the state store and
+      // the outbox headers (their loads then overlap those stores)
+      if (DRB_READS_EARLY && LEAD && p.n_reads && !(DRB_ABLATE & 2))
+        serve_reads_lane<EXT>(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
+                              p.key_space, c_served, c_deferred);
       sent_c1 = r.c1mask;
       // ring guard for the next round's appends
       r.ring_guard = r.guard_new;
@@ -3360,7 +3369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     if (p.encode_saves && c_saved == 0) v.save_len[ix(v, slot, g)] = 0;
     DRB_PH(6);  // state store + outbox headers
     // ReadLocalNode of the released reads, against the state just applied
-    if (p.n_reads && !(DRB_ABLATE & 2))
+    if ((!DRB_READS_EARLY || !LEAD) && p.n_reads && !(DRB_ABLATE & 2))
       serve_reads_lane<EXT>(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
                        p.key_space, c_served, c_deferred);
     DRB_PH(7);  // served reads
