@@ -266,8 +266,8 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
                             const uint32_t *mlen, const uint32_t *mframe,
                             uint32_t *n_ent, uint32_t *err,
                             uint32_t *frame_bad, DecMsg *out, uint64_t n,
-                            uint32_t cmd_cap) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                            uint32_t cmd_cap, uint64_t i0 = 0) {
+  const uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   DecMsg m;
   bool big = false;
@@ -293,8 +293,8 @@ __global__ void k_widen_step(const uint32_t *in, uint64_t *out, uint64_t n) {
 __global__ void k_ing_elems(const uint8_t *s, const uint64_t *scan,
                             const uint64_t *mbase, const uint64_t *foff,
                             const uint32_t *mframe, uint64_t *moff,
-                            uint32_t *mlen, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                            uint32_t *mlen, uint64_t n, uint64_t i0 = 0) {
+  const uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t f = mframe[i];
   const uint64_t first = mbase[f];
@@ -330,6 +330,9 @@ __global__ void k_ing_frames(const uint64_t *mbase, uint32_t nf,
 // drb_wire_in tallies (ctr[2] snapshots, [3] messages, [4] filtered,
 // [5] entries), one atomic per wave and counter
 constexpr uint32_t ING_TALLY_ROWS = 64;
+// drb_ingest_wire uploads the stream in pieces of whole frames of at least
+// this many bytes; each piece's CRC and count kernels start when it lands
+constexpr size_t ING_PIECE = 32u << 20;
 __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
                             const uint32_t *err, const uint32_t *n_ent,
                             uint32_t *nsc, uint8_t *deliver, uint64_t n,
@@ -768,9 +771,15 @@ struct IngestState {
   // the frames of the last call; their Requests vectors keep their
   // capacity, so a warm call neither faults nor unmaps ~12 B per message
   std::vector<wirehost::Frame> frames;
+  // the stream goes up in pieces on its own stream, one event each, so the
+  // CRC and count kernels of a piece run while the later pieces upload
+  hipStream_t up = nullptr;
+  std::vector<hipEvent_t> ev;
 };
 static void ingest_free(IngestState *st) {
   if (!st) return;
+  for (hipEvent_t x : st->ev) (void)hipEventDestroy(x);
+  if (st->up) (void)hipStreamDestroy(st->up);
   if (st->pinned) (void)hipHostFree(st->pinned);
   if (st->steps) (void)hipHostFree(st->steps);
   for (IngestBuf *b : {&st->stream, &st->msgs, &st->ents, &st->sort,
@@ -902,16 +911,51 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // read by the DMA engine asynchronously) as soon as this call returns
   struct SyncOnReturn {
     hipStream_t s;
-    ~SyncOnReturn() { (void)hipStreamSynchronize(s); }
-  } sync_on_return{e->stream};
+    IngestState *st;
+    ~SyncOnReturn() {
+      if (st->up) (void)hipStreamSynchronize(st->up);
+      (void)hipStreamSynchronize(s);
+    }
+  } sync_on_return{e->stream, &st};
   // 2. the stream goes up (its own host thread: a pageable source makes
   // the copy synchronous) while Requests boundaries are found, one host
   // thread per frame (a frame holds up to 64 MiB of messages), at most 16
+  // pieces: runs of whole frames of at least ING_PIECE bytes
+  std::vector<size_t> pf;  // first frame of each piece, then nf
+  for (size_t f = 0, acc = 0; f < fr.size(); ++f) {
+    if (pf.empty() || acc >= ING_PIECE) {
+      pf.push_back(f);
+      acc = 0;
+    }
+    acc += 20 + (size_t)fr[f].size;
+  }
+  pf.push_back(fr.size());
+  const size_t np = pf.size() - 1;
+  if (!st.up &&
+      hipStreamCreateWithFlags(&st.up, hipStreamNonBlocking) != hipSuccess)
+    return DRB_EDEVICE;
+  while (st.ev.size() < np) {
+    hipEvent_t x;
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+      return DRB_EDEVICE;
+    st.ev.push_back(x);
+  }
+  // the upload stream starts behind what the engine stream has enqueued
+  // (the device buffer may still be read by an earlier call's kernels)
+  HIPCHK(hipEventRecord(st.ev[0], sm));
+  HIPCHK(hipStreamWaitEvent(st.up, st.ev[0], 0));
   {
     hipError_t up_err = hipSuccess;
     std::thread up([&]() {
-      if (walked)
-        up_err = hipMemcpyAsync(ds, stream, walked, hipMemcpyHostToDevice, sm);
+      for (size_t q = 0; q < np && up_err == hipSuccess; ++q) {
+        const size_t a = q ? fr[pf[q]].off - 20 : 0;
+        const size_t b = pf[q + 1] < fr.size() ? fr[pf[q + 1]].off - 20
+                                                : walked;
+        if (b > a)
+          up_err = hipMemcpyAsync(ds + a, stream + a, b - a,
+                                  hipMemcpyHostToDevice, st.up);
+        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.up);
+      }
     });
     const size_t nt = std::min<size_t>(16, fr.size());
     std::vector<std::thread> th;
@@ -1002,8 +1046,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (nc) {
     HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice, sm));
-    k_crc_chunks<<<(unsigned)nc, 256, 0, sm>>>(ds, d_coff, d_clen, d_ccrc);
-    HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemsetAsync(d_fbad, 0, (fr.size() + 1) * 4, sm));
   HIPCHK(hipMemsetAsync(d_ctr, 0, ING_TALLY_ROWS * 8 * 8, sm));
@@ -1046,12 +1088,25 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                                                 d_step64, nm);
     HIPCHK(hipcub::DeviceScan::InclusiveSum(d_scan_tmp, scan_tb, d_step64,
                                             d_scan, (int)nm, sm));
-    k_ing_elems<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-        ds, d_scan, d_mbase, d_foff, d_mframe, d_moff, d_mlen, nm);
     if (ing_grow(st.msgs, al256(nm * sizeof(DecMsg)))) return DRB_EDEVICE;
-    k_ing_count<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-        ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad,
-        (DecMsg *)st.msgs.p, nm, cmd_cap);
+  }
+  // per piece, once its bytes are up: the payload CRCs of its chunks and
+  // its messages' element boundaries and counts
+  for (size_t q = 0; q < np; ++q) {
+    HIPCHK(hipStreamWaitEvent(sm, st.ev[q], 0));
+    const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
+    if (c1 > c0)
+      k_crc_chunks<<<c1 - c0, 256, 0, sm>>>(ds, d_coff + c0, d_clen + c0,
+                                            d_ccrc + c0);
+    const uint64_t m0 = mbase[pf[q]], m1 = mbase[pf[q + 1]];
+    if (m1 > m0) {
+      const unsigned gb = (unsigned)((m1 - m0 + 255) / 256);
+      k_ing_elems<<<gb, 256, 0, sm>>>(ds, d_scan, d_mbase, d_foff, d_mframe,
+                                      d_moff, d_mlen, m1, m0);
+      k_ing_count<<<gb, 256, 0, sm>>>(ds, d_moff, d_mlen, d_mframe, d_nent,
+                                      d_err, d_fbad, (DecMsg *)st.msgs.p, m1,
+                                      cmd_cap, m0);
+    }
     HIPCHK(hipGetLastError());
   }
   std::vector<uint32_t> ccrc(nc), fbad(fr.size() + 1);
