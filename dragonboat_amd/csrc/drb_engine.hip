@@ -94,6 +94,9 @@ struct drb_engine {
   // the leaders' served reads one thread per read (k_read_lanes) instead of
   // inside the leader kernel; DRB_READ_LANES=0/1 in the environment
   bool read_lanes = false;
+  // the follower kernel on stream2, concurrent with the leader kernel
+  // (DRB_ROLE_STREAMS=0/1 in the environment; measured 3 % slower at C3)
+  bool role_streams = false;
   // drb_plane_counts has read the plane summaries (xrows): the rounds clear
   // them from then on
   bool xrows_used = false;
@@ -271,6 +274,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->scratch = nullptr;
   e->scratch_bytes = 0;
   if (const char *rl = getenv("DRB_READ_LANES")) e->read_lanes = rl[0] == '1';
+  if (const char *rs = getenv("DRB_ROLE_STREAMS")) e->role_streams = rs[0] == '1';
   if (hipSetDevice(cfg->device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
           hipSuccess ||
@@ -2045,12 +2049,15 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   uint32_t nl = 0, nf = 0;
   pl.slots = slot_list(e->role_slots[0], &nl);
   pf.slots = slot_list(e->role_slots[1], &nf);
-  hipStream_t sf = DRB_ROLE_STREAMS ? e->stream2 : e->stream;
-  if (DRB_ROLE_STREAMS) {
+  // the two roles concurrently where their launches alone cannot fill the
+  // device (DRB_ROLE_STREAMS, or e->role_streams: small engines)
+  const bool rs = DRB_ROLE_STREAMS || e->role_streams;
+  hipStream_t sf = rs ? e->stream2 : e->stream;
+  if (rs) {
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
   }
-  const bool split = DRB_SERVE_SPLIT && !DRB_ROLE_STREAMS && nl && p0.n_reads;
+  const bool split = DRB_SERVE_SPLIT && !rs && nl && p0.n_reads;
   if (split) pl.n_reads = 0;
   // the leaders' reads as one thread per read, behind the leader kernel
   // (a follower's ReadyToReads come from its own forwarded ReadIndex, a
@@ -2086,7 +2093,7 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
   }
-  if (DRB_ROLE_STREAMS) {
+  if (rs) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
   }

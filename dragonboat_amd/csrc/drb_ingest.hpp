@@ -761,7 +761,7 @@ static int ing_grow(IngestBuf &b, size_t need) {
   return DRB_OK;
 }
 struct IngestState {
-  IngestBuf stream, msgs, ents, sort, misc;
+  IngestBuf stream, msgs, ents, sort, misc, chunks;
   bool k64_ready = false;     // c_crc_k64 uploaded
   uint8_t *pinned = nullptr;  // drb_ingest_buffer (hipHostMalloc)
   size_t pinned_cap = 0;
@@ -773,17 +773,19 @@ struct IngestState {
   std::vector<wirehost::Frame> frames;
   // the stream goes up in pieces on its own stream, one event each, so the
   // CRC and count kernels of a piece run while the later pieces upload
-  hipStream_t up = nullptr;
-  std::vector<hipEvent_t> ev;
+  hipStream_t up = nullptr, crc = nullptr;
+  std::vector<hipEvent_t> ev, evc;  // per piece: CRC'd, uploaded
 };
 static void ingest_free(IngestState *st) {
   if (!st) return;
   for (hipEvent_t x : st->ev) (void)hipEventDestroy(x);
+  for (hipEvent_t x : st->evc) (void)hipEventDestroy(x);
   if (st->up) (void)hipStreamDestroy(st->up);
+  if (st->crc) (void)hipStreamDestroy(st->crc);
   if (st->pinned) (void)hipHostFree(st->pinned);
   if (st->steps) (void)hipHostFree(st->steps);
   for (IngestBuf *b : {&st->stream, &st->msgs, &st->ents, &st->sort,
-                       &st->misc})
+                       &st->misc, &st->chunks})
     if (b->p) (void)hipFree(b->p);
   delete st;
 }
@@ -914,12 +916,32 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     IngestState *st;
     ~SyncOnReturn() {
       if (st->up) (void)hipStreamSynchronize(st->up);
+      if (st->crc) (void)hipStreamSynchronize(st->crc);
       (void)hipStreamSynchronize(s);
     }
   } sync_on_return{e->stream, &st};
   // 2. the stream goes up (its own host thread: a pageable source makes
   // the copy synchronous) while Requests boundaries are found, one host
   // thread per frame (a frame holds up to 64 MiB of messages), at most 16
+  // the payload CRCs in 16 KB chunks (the chunk lists go up first)
+  constexpr uint64_t CH = 16384;
+  std::vector<uint64_t> coff;
+  std::vector<uint32_t> clen;
+  std::vector<uint32_t> cfirst(fr.size() + 1, 0);
+  for (size_t f = 0; f < fr.size(); ++f) {
+    cfirst[f] = (uint32_t)coff.size();
+    for (uint64_t o = 0; o < fr[f].size; o += CH) {
+      coff.push_back(fr[f].off + o);
+      clen.push_back((uint32_t)std::min<uint64_t>(CH, fr[f].size - o));
+    }
+  }
+  cfirst[fr.size()] = (uint32_t)coff.size();
+  const size_t nc = coff.size();
+  if (ing_grow(st.chunks, al256(nc * 8 + 8) + 2 * al256(nc * 4 + 4)))
+    return DRB_EDEVICE;
+  uint64_t *d_coff = (uint64_t *)st.chunks.p;
+  uint32_t *d_clen = (uint32_t *)((uint8_t *)st.chunks.p + al256(nc * 8 + 8));
+  uint32_t *d_ccrc = (uint32_t *)((uint8_t *)d_clen + al256(nc * 4 + 4));
   // pieces: runs of whole frames of at least ING_PIECE bytes
   std::vector<size_t> pf;  // first frame of each piece, then nf
   for (size_t f = 0, acc = 0; f < fr.size(); ++f) {
@@ -934,19 +956,32 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (!st.up &&
       hipStreamCreateWithFlags(&st.up, hipStreamNonBlocking) != hipSuccess)
     return DRB_EDEVICE;
-  while (st.ev.size() < np) {
-    hipEvent_t x;
-    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+  if (!st.crc &&
+      hipStreamCreateWithFlags(&st.crc, hipStreamNonBlocking) != hipSuccess)
+    return DRB_EDEVICE;
+  while (st.ev.size() < (np ? np : 1)) {  // (ev[0] also for the start)
+    hipEvent_t x, y;
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&y, hipEventDisableTiming) != hipSuccess)
       return DRB_EDEVICE;
     st.ev.push_back(x);
+    st.evc.push_back(y);
   }
-  // the upload stream starts behind what the engine stream has enqueued
-  // (the device buffer may still be read by an earlier call's kernels)
+  // the upload and CRC streams start behind what the engine stream has
+  // enqueued (the device buffers may still be read by an earlier call)
   HIPCHK(hipEventRecord(st.ev[0], sm));
   HIPCHK(hipStreamWaitEvent(st.up, st.ev[0], 0));
+  HIPCHK(hipStreamWaitEvent(st.crc, st.ev[0], 0));
+  if (nc) {
+    HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice,
+                          st.crc));
+    HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice,
+                          st.crc));
+  }
   {
     hipError_t up_err = hipSuccess;
     std::thread up([&]() {
+      up_err = hipSetDevice(e->cfg.device);  // (the current device is per thread)
       for (size_t q = 0; q < np && up_err == hipSuccess; ++q) {
         const size_t a = q ? fr[pf[q]].off - 20 : 0;
         const size_t b = pf[q + 1] < fr.size() ? fr[pf[q + 1]].off - 20
@@ -954,7 +989,17 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         if (b > a)
           up_err = hipMemcpyAsync(ds + a, stream + a, b - a,
                                   hipMemcpyHostToDevice, st.up);
-        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.up);
+        // the piece's payload CRCs on their own stream as it lands
+        if (up_err == hipSuccess) up_err = hipEventRecord(st.evc[q], st.up);
+        if (up_err == hipSuccess)
+          up_err = hipStreamWaitEvent(st.crc, st.evc[q], 0);
+        const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
+        if (up_err == hipSuccess && c1 > c0) {
+          k_crc_chunks<<<c1 - c0, 256, 0, st.crc>>>(ds, d_coff + c0,
+                                                   d_clen + c0, d_ccrc + c0);
+          up_err = hipGetLastError();
+        }
+        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.crc);
       }
     });
     const size_t nt = std::min<size_t>(16, fr.size());
@@ -971,20 +1016,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint64_t nm = 0;
   for (const auto &f : fr) nm += f.step.size();
   tr.mark("up+scan");
-  // 3. the stream up, the payload CRCs in 16 KB chunks
-  constexpr uint64_t CH = 16384;
-  std::vector<uint64_t> coff;
-  std::vector<uint32_t> clen;
-  std::vector<uint32_t> cfirst(fr.size() + 1, 0);
-  for (size_t f = 0; f < fr.size(); ++f) {
-    cfirst[f] = (uint32_t)coff.size();
-    for (uint64_t o = 0; o < fr[f].size; o += CH) {
-      coff.push_back(fr[f].off + o);
-      clen.push_back((uint32_t)std::min<uint64_t>(CH, fr[f].size - o));
-    }
-  }
-  cfirst[fr.size()] = (uint32_t)coff.size();
-  const size_t nc = coff.size();
+  // 3. the stream up (its payload CRCs ran per piece)
   // misc: chunk offsets/lens/crcs, message offsets/lens/frames, counts,
   // errors, entry bases, deliver flags, per-frame error, 2 counters
   const size_t m1 = nm ? nm : 1;
@@ -992,7 +1024,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   size_t scan_tb = 0;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, scan_tb, (uint64_t *)nullptr,
                                           (uint64_t *)nullptr, (int)m1, sm));
-  const size_t mb = al256(nc * 8) + al256(nc * 4) * 2 + al256(m1 * 8) * 3 +
+  const size_t mb = al256(m1 * 8) * 3 +
                     al256(m1 * 4) * 7 + al256(m1) +
                     al256((nf + 1) * 4) + al256((nf + 1) * 8) * 2 +
                     al256(nf + 1) + ING_TALLY_ROWS * 64 + al256(scan_tb);
@@ -1003,9 +1035,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     q += al256(b);
     return r;
   };
-  uint64_t *d_coff = (uint64_t *)take(nc * 8);
-  uint32_t *d_clen = (uint32_t *)take(nc * 4);
-  uint32_t *d_ccrc = (uint32_t *)take(nc * 4);
   uint64_t *d_moff = (uint64_t *)take(m1 * 8);
   uint32_t *d_mlen = (uint32_t *)take(m1 * 4);
   uint32_t *d_mframe = (uint32_t *)take(m1 * 4);
@@ -1043,10 +1072,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // each frame's Requests go up straight from its scan vectors
   std::vector<uint64_t> mbase(nf + 1, 0);
   for (size_t f = 0; f < nf; ++f) mbase[f + 1] = mbase[f] + fr[f].step.size();
-  if (nc) {
-    HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice, sm));
-    HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice, sm));
-  }
   HIPCHK(hipMemsetAsync(d_fbad, 0, (fr.size() + 1) * 4, sm));
   HIPCHK(hipMemsetAsync(d_ctr, 0, ING_TALLY_ROWS * 8 * 8, sm));
   const uint32_t cmd_cap = v.C16 * 16;
@@ -1090,14 +1115,10 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                             d_scan, (int)nm, sm));
     if (ing_grow(st.msgs, al256(nm * sizeof(DecMsg)))) return DRB_EDEVICE;
   }
-  // per piece, once its bytes are up: the payload CRCs of its chunks and
-  // its messages' element boundaries and counts
+  // per piece, once its bytes are up (and CRC'd): its messages' element
+  // boundaries and counts
   for (size_t q = 0; q < np; ++q) {
     HIPCHK(hipStreamWaitEvent(sm, st.ev[q], 0));
-    const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
-    if (c1 > c0)
-      k_crc_chunks<<<c1 - c0, 256, 0, sm>>>(ds, d_coff + c0, d_clen + c0,
-                                            d_ccrc + c0);
     const uint64_t m0 = mbase[pf[q]], m1 = mbase[pf[q + 1]];
     if (m1 > m0) {
       const unsigned gb = (unsigned)((m1 - m0 + 255) / 256);

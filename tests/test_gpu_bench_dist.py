@@ -56,3 +56,25 @@ def test_bench_rejects_gpus_unlike_world_size():
                                    "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE" in p.stderr
+
+
+def test_bench_local_ranks_is_the_c4_run():
+    # (no GPU needed: rejected before anything touches one)
+    p = _bench("--local-ranks", "2")
+    assert p.returncode != 0
+    assert "local-ranks" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_c4_local_ranks():
+    """bench.py --workload c4 --local-ranks 4: four engines of one process
+    on the one GPU, their planes moved by drb_exchange_local's device pull;
+    every group commits one entry a round and the pull reports its bytes."""
+    p = _bench("--workload", "c4", "--local-ranks", "4")
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([x for x in p.stdout.splitlines()
+                      if x.startswith("{")][-1])
+    assert res["config"]["local_ranks"] == 4
+    assert res["counters"]["committed_per_round"] == G
+    assert res["counters"]["fallbacks_and_errors"] == 0
+    assert res["exchange"]["bytes_per_round"] > 0
