@@ -923,6 +923,23 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // 2. the stream goes up (its own host thread: a pageable source makes
   // the copy synchronous) while Requests boundaries are found, one host
   // thread per frame (a frame holds up to 64 MiB of messages), at most 16
+  // the CRC tables, before the first CRC kernel (the upload thread's)
+  if (!e->crc_tab_ready) {
+    uint32_t tab[8][256];
+    for (uint32_t a = 0; a < 256; ++a) tab[0][a] = wirehost::crc_tab[a];
+    for (uint32_t a = 0; a < 256; ++a)
+      for (int s = 1; s < 8; ++s)
+        tab[s][a] = tab[0][tab[s - 1][a] & 0xff] ^ (tab[s - 1][a] >> 8);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
+    e->crc_tab_ready = true;
+  }
+  if (!st.k64_ready) {  // x^(8 * 64 * (255 - t)) mod P
+    uint32_t k64[256];
+    for (int t = 0; t < 256; ++t)
+      k64[t] = wirehost::crc32_combine(1u << 31, 0, 64ull * (255 - t));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_k64), k64, sizeof(k64)));
+    st.k64_ready = true;
+  }
   // the payload CRCs in 16 KB chunks (the chunk lists go up first)
   constexpr uint64_t CH = 16384;
   std::vector<uint64_t> coff;
@@ -1053,22 +1070,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint8_t *d_fstate = take(nf + 1);
   unsigned long long *d_ctr =
       (unsigned long long *)take(ING_TALLY_ROWS * 8 * 8);
-  if (!e->crc_tab_ready) {
-    uint32_t tab[8][256];
-    for (uint32_t a = 0; a < 256; ++a) tab[0][a] = wirehost::crc_tab[a];
-    for (uint32_t a = 0; a < 256; ++a)
-      for (int s = 1; s < 8; ++s)
-        tab[s][a] = tab[0][tab[s - 1][a] & 0xff] ^ (tab[s - 1][a] >> 8);
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab)));
-    e->crc_tab_ready = true;
-  }
-  if (!st.k64_ready) {  // x^(8 * 64 * (255 - t)) mod P
-    uint32_t k64[256];
-    for (int t = 0; t < 256; ++t)
-      k64[t] = wirehost::crc32_combine(1u << 31, 0, 64ull * (255 - t));
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_k64), k64, sizeof(k64)));
-    st.k64_ready = true;
-  }
   // each frame's Requests go up straight from its scan vectors
   std::vector<uint64_t> mbase(nf + 1, 0);
   for (size_t f = 0; f < nf; ++f) mbase[f + 1] = mbase[f] + fr[f].step.size();

@@ -255,3 +255,16 @@ def test_ingest_wire_filters_and_bad_frames():
         b"abc")) + b"abc"
     got = t.foll.ingest_wire(chunk + data[:first], t.did)
     assert got["bad"] == 0 and got["snapshots"] == 1 and got["frames"] == 2
+
+
+@pytest.mark.parametrize("kind", ["witness", "nonvoting"])
+def test_wire_planes_with_member_kinds(kind):
+    """A 3 + 1 group: the leader's plane to a witness carries metadata
+    entries (makeMetadataEntries, raft.go:771-785), the one to a nonVoting
+    the entries whole; both byte for byte against the oracle's outbox."""
+    p = Pair(G=32, R=4, **{kind + "_slots": 1 << 3})
+    for r in range(4):
+        o, e = p.round(k=1 + r % 2, tick=(r % 2 == 0), read_index=(r == 2))
+        assert e.fallbacks == 0 and e.errors == 0
+        _check_planes(p, did=77, limits=[0, 2000],
+                      planes=[(0, 3), (3, 0), (0, 1)])
