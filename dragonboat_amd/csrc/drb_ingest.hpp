@@ -989,11 +989,20 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   HIPCHK(hipEventRecord(st.ev[0], sm));
   HIPCHK(hipStreamWaitEvent(st.up, st.ev[0], 0));
   HIPCHK(hipStreamWaitEvent(st.crc, st.ev[0], 0));
+  // where the payload CRCs run (DRB_INGEST_MODE, measured in DESIGN §10):
+  // 0 on the engine stream per piece after the Requests scans, 1 on a
+  // stream of their own as each piece lands, 2 on the engine stream as each
+  // piece lands
+  static const int mode = [] {
+    const char *m = getenv("DRB_INGEST_MODE");
+    return m ? atoi(m) : 0;
+  }();
+  hipStream_t cs = mode == 1 ? st.crc : sm;
   if (nc) {
     HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice,
-                          st.crc));
+                          cs));
     HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice,
-                          st.crc));
+                          cs));
   }
   {
     hipError_t up_err = hipSuccess;
@@ -1006,17 +1015,20 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         if (b > a)
           up_err = hipMemcpyAsync(ds + a, stream + a, b - a,
                                   hipMemcpyHostToDevice, st.up);
-        // the piece's payload CRCs on their own stream as it lands
+        if (mode == 0) {  // the piece is up
+          if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.up);
+          continue;
+        }
+        // the piece's payload CRCs as it lands
         if (up_err == hipSuccess) up_err = hipEventRecord(st.evc[q], st.up);
-        if (up_err == hipSuccess)
-          up_err = hipStreamWaitEvent(st.crc, st.evc[q], 0);
+        if (up_err == hipSuccess) up_err = hipStreamWaitEvent(cs, st.evc[q], 0);
         const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
         if (up_err == hipSuccess && c1 > c0) {
-          k_crc_chunks<<<c1 - c0, 256, 0, st.crc>>>(ds, d_coff + c0,
-                                                   d_clen + c0, d_ccrc + c0);
+          k_crc_chunks<<<c1 - c0, 256, 0, cs>>>(ds, d_coff + c0, d_clen + c0,
+                                               d_ccrc + c0);
           up_err = hipGetLastError();
         }
-        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.crc);
+        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], cs);
       }
     });
     const size_t nt = std::min<size_t>(16, fr.size());
@@ -1119,7 +1131,11 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // per piece, once its bytes are up (and CRC'd): its messages' element
   // boundaries and counts
   for (size_t q = 0; q < np; ++q) {
-    HIPCHK(hipStreamWaitEvent(sm, st.ev[q], 0));
+    if (mode != 2) HIPCHK(hipStreamWaitEvent(sm, st.ev[q], 0));
+    const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
+    if (mode == 0 && c1 > c0)
+      k_crc_chunks<<<c1 - c0, 256, 0, sm>>>(ds, d_coff + c0, d_clen + c0,
+                                            d_ccrc + c0);
     const uint64_t m0 = mbase[pf[q]], m1 = mbase[pf[q + 1]];
     if (m1 > m0) {
       const unsigned gb = (unsigned)((m1 - m0 + 255) / 256);
