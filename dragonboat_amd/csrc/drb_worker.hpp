@@ -35,10 +35,6 @@ struct WorkerState {
   unsigned long long *hdr_dev = nullptr;  // ... its device address
   const drb_worker_bufs *owner[2] = {nullptr, nullptr};
   uint64_t seq = 0;
-  // the counts the last drb_worker_wait saw: the next export's DMA size
-  // (rounds of a steady workload repeat them); the drain kernel writes
-  // only what a round has beyond it
-  uint64_t last[3] = {0, 0, 0};
 };
 
 namespace {
@@ -143,15 +139,15 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
   }
 }
 
-// bytes [b, n) of src into dst (b a multiple of 16, n of 8; 16-byte
-// aligned buffers), a grid-stride walk of 16 B words
+// bytes [0, n) of src into dst (16-byte aligned, n a multiple of 8), a
+// grid-stride walk of 16 B words
 __device__ inline void worker_drain_copy(uint8_t *dst, const uint8_t *src,
-                                         uint64_t b, uint64_t n, uint64_t t,
+                                         uint64_t n, uint64_t t,
                                          uint64_t nt) {
   const uint64_t n16 = n / 16;
-  for (uint64_t i = b / 16 + t; i < n16; i += nt)
+  for (uint64_t i = t; i < n16; i += nt)
     ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
-  if ((n & 15) && t == 0 && n16 * 16 >= b)
+  if ((n & 15) && t == 0)
     *(uint2 *)(dst + n16 * 16) = *(const uint2 *)(src + n16 * 16);
 }
 
@@ -161,22 +157,17 @@ __global__ void k_worker_drain(const unsigned long long *tot,
                                uint64_t cap_val, uint64_t *hval,
                                const drb_worker_applied *ap, uint64_t cap_ap,
                                drb_worker_applied *hap,
-                               unsigned long long *hdr, uint64_t d_rd,
-                               uint64_t d_val, uint64_t d_ap) {
+                               unsigned long long *hdr) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t nrd = min((uint64_t)tot[0], cap_rd);
   const uint64_t nval = min((uint64_t)tot[1], cap_val);
   const uint64_t nap = min((uint64_t)tot[2], cap_ap);
-  // (records [0, d_*) went by DMA)
   if (hrd) worker_drain_copy((uint8_t *)hrd, (const uint8_t *)rd,
-                             d_rd * sizeof(drb_worker_read),
                              nrd * sizeof(drb_worker_read), t, nt);
   if (hval) worker_drain_copy((uint8_t *)hval, (const uint8_t *)val,
-                              d_val * sizeof(uint64_t),
                               nval * sizeof(uint64_t), t, nt);
   if (hap) worker_drain_copy((uint8_t *)hap, (const uint8_t *)ap,
-                             d_ap * sizeof(drb_worker_applied),
                              nap * sizeof(drb_worker_applied), t, nt);
   if (t == 0) {
     hdr[0] = tot[0];
@@ -322,30 +313,12 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
       b->values_cap, w.ap[k], b->applied_cap, w.tot + 4 * k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(w.ev_staged[k], e->stream));
-  // the transfer, on the copy stream: PCIe-bound.  The record counts the
-  // last wait saw go by DMA (the copy engines), rounded down to an even
-  // count (16 B multiples); a drain kernel writes what the round has
-  // beyond them, and the counts
+  // the transfer, on the copy stream: PCIe-bound, a few workgroups
   HIPCHK(hipStreamWaitEvent(w.sx, w.ev_staged[k], 0));
-  const uint64_t d_rd = b->reads ? std::min(w.last[0], b->reads_cap) & ~1ull : 0;
-  const uint64_t d_val =
-      b->values ? std::min(w.last[1], b->values_cap) & ~1ull : 0;
-  const uint64_t d_ap =
-      b->applied ? std::min(w.last[2], b->applied_cap) & ~1ull : 0;
-  if (d_rd)
-    HIPCHK(hipMemcpyAsync(b->reads, w.rd[k], d_rd * sizeof(drb_worker_read),
-                          hipMemcpyDeviceToHost, w.sx));
-  if (d_val)
-    HIPCHK(hipMemcpyAsync(b->values, w.val[k], d_val * 8,
-                          hipMemcpyDeviceToHost, w.sx));
-  if (d_ap)
-    HIPCHK(hipMemcpyAsync(b->applied, w.ap[k],
-                          d_ap * sizeof(drb_worker_applied),
-                          hipMemcpyDeviceToHost, w.sx));
   k_worker_drain<<<256, 256, 0, w.sx>>>(
       w.tot + 4 * k, w.rd[k], b->reads_cap, (drb_worker_read *)hrd, w.val[k],
       b->values_cap, (uint64_t *)hval, w.ap[k], b->applied_cap,
-      (drb_worker_applied *)hap, w.hdr_dev + 4 * k, d_rd, d_val, d_ap);
+      (drb_worker_applied *)hap, w.hdr_dev + 4 * k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(w.ev_drained[k], w.sx));
   w.drained_valid[k] = true;
@@ -365,9 +338,6 @@ extern "C" int drb_worker_wait(drb_engine *e, drb_worker_bufs *b) {
   b->n_reads = w.hdr[4 * k];
   b->n_values = w.hdr[4 * k + 1];
   b->n_applied = w.hdr[4 * k + 2];
-  w.last[0] = b->n_reads;
-  w.last[1] = b->n_values;
-  w.last[2] = b->n_applied;
   w.owner[k] = nullptr;
   return b->n_reads > b->reads_cap || b->n_values > b->values_cap ||
                  b->n_applied > b->applied_cap
