@@ -289,6 +289,10 @@ class DistPair:
                      for r in range(N)]
         self.orc = po.Cluster(G, R, seed=seed)
         self.orc.setup_steady(0)
+        nv, wt = (engine_kw.get("nonvoting_slots", 0),
+                  engine_kw.get("witness_slots", 0))
+        if nv or wt:  # member kinds (drb_config.nonvoting_slots, ...)
+            self.orc.set_member_kinds(nv, wt)
         if engine_kw.get("pre_vote"):
             self.orc.set_pre_vote(True)
         for e in self.engs:

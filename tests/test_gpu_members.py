@@ -156,3 +156,23 @@ def test_member_never_campaigns(kind):
     for r in range(6):
         _round(p, st, k=1, tick=(r % 2 == 0), read_index=True,
                ri_replica=0)
+
+
+@pytest.mark.parametrize("kind,N", [("witness", 2), ("nonvoting", 3)])
+def test_members_under_c4_placement(kind, N):
+    """Replicas spread over ranks (C4 placement, drb_exchange_local's pull):
+    a 4 + 1 group whose slot 4 is a witness / nonVoting; the metadata
+    entries travel in the entry rows of the planes, the quorum is the
+    voters'."""
+    from tests.gpu_harness import DistPair
+    G, R = 40, 5
+    p = DistPair(G=G, R=R, N=N, max_props=2, **{kind + "_slots": 1 << 4})
+    assert not p.check(), "init"
+    for r in range(10):
+        o, e = p.round(k=1 + r % 2, tick=(r % 2 == 0),
+                       read_index=(r % 3 == 0))
+        assert e["fallbacks"] == 0 and e["errors"] == 0, (r, e)
+        assert (e["committed_entries"], e["messages"]) == \
+            (o.committed_entries, o.messages), (r, e, o.to_dict())
+        errs = p.check()
+        assert not errs, (r, errs[:3])
