@@ -91,6 +91,10 @@ namespace drb {
 #ifndef DRB_ABLATE
 #define DRB_ABLATE 0
 #endif
+// served-read results stored nontemporally (1) or plainly (0)
+#ifndef DRB_NT_RESULTS
+#define DRB_NT_RESULTS 0
+#endif
 // the leader's served reads before its state store (1) or after the outbox
 // headers (0): measured 0.3-0.8 % faster at C3 (profiles/r04_reads)
 #ifndef DRB_READS_EARLY
@@ -2105,10 +2109,20 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
         sum += mix64(w ^ key[t] ^ ((uint64_t)j << 56));
         served++;
         if (v.read_res)  // ReadLocalNode's result for the client
-          v.read_res[rres_ix(v, slot, k, j, g)] =
-              w == ~0ull ? make_uint2(0, 0)
-                         : make_uint2((uint32_t)w,
-                                      (uint32_t)(w >> 32) | 0x80000000u);
+        {
+          const uint64_t rv =
+              w == ~0ull ? 0ull
+                         : (w & 0xffffffffull) |
+                               ((uint64_t)((uint32_t)(w >> 32) | 0x80000000u)
+                                << 32);
+          uint64_t *dst = (uint64_t *)&v.read_res[rres_ix(v, slot, k, j, g)];
+          // the client results are read by the host, not by a later round:
+          // DRB_NT_RESULTS stores them past the caches
+          if (DRB_NT_RESULTS)
+            __builtin_nontemporal_store(rv, dst);
+          else
+            *dst = rv;
+        }
       }
     }
   }
