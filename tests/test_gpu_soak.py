@@ -1,0 +1,77 @@
+"""GPU: randomized rounds over the features together, bit-exact every round.
+
+Each round draws, from a seeded generator: how many proposals a group
+queues (0-2) and at which replica (the leader, a follower, a nonVoting --
+drb_round_in.prop_replica with forward_proposals), whether a LocalTick
+fires, whether a ReadIndex batch is staged and at which replica, and now
+and then a replica slot of some groups stops or comes back (elections on
+the GPU re-elect where a leader stopped).  Member kinds vary by case (all
+voters; a witness; a nonVoting).  After every round the engine is compared
+with the oracle cluster (the reference step loop: tests/gpu_harness.py):
+every replica field, the logs, the KV, the outboxes and the ReadyToReads,
+and the round counters.  No replica may leave the GPU.
+"""
+import random
+
+import pytest
+
+from dragonboat_amd import abi
+from tests.gpu_harness import Pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _set_hosted(p, groups, slot, hosted):
+    for g in groups:
+        p.orc.set_hosted(g, slot, hosted)
+        sts = p.eng.export_replicas(g, 1)
+        if hosted:
+            sts[slot].flags |= abi.F_HOSTED
+        else:
+            sts[slot].flags &= ~abi.F_HOSTED
+        p.eng.import_replicas(g, sts)
+
+
+@pytest.mark.parametrize("case", ["voters", "witness", "nonvoting"])
+@pytest.mark.parametrize("seed", [11, 12])
+def test_random_rounds(case, seed):
+    rng = random.Random(seed * 1000 + len(case))
+    G, R = 48, 4
+    kw = {}
+    if case != "voters":
+        kw[case + "_slots"] = 1 << 3
+    p = Pair(G=G, R=R, elections=1, forward_proposals=1, max_props=2,
+             mailbox=16, **kw)
+    # replica IDs (0: the leader); a witness neither proposes nor reads
+    ids = [0, 1, 2, 3] + ([4] if case != "witness" else [])
+    stopped = {}  # slot -> groups
+    committed = 0
+    for rnd in range(40):
+        # now and then a replica slot of a third of the groups stops, or
+        # the stopped ones come back
+        if rnd % 8 == 3 and not stopped:
+            s = rng.choice([0, 1, 2])
+            gs = [g for g in range(G) if rng.random() < 0.33]
+            _set_hosted(p, gs, s, False)
+            stopped[s] = gs
+        elif rnd % 8 == 7 and stopped:
+            for s, gs in stopped.items():
+                _set_hosted(p, gs, s, True)
+            stopped = {}
+        # (clients reach running NodeHosts only)
+        up = [i for i in ids if i == 0 or (i - 1) not in stopped]
+        k = rng.choice([0, 1, 1, 2])
+        o, e = p.round(k=k, tick=rng.random() < 0.7,
+                       read_index=rng.random() < 0.5,
+                       ri_replica=rng.choice(up),
+                       prop_replica=rng.choice(up) if k else 0)
+        assert e.fallbacks == 0 and e.errors == 0, (rnd, e.to_dict(),
+                                                     p.why())
+        assert (e.committed_entries, e.messages, e.ready_to_reads,
+                e.dropped_proposals) == \
+            (o.committed_entries, o.messages, o.ready_to_reads,
+             o.dropped_proposals), (rnd, e.to_dict(), o.to_dict())
+        errs = p.check()
+        assert not errs, (rnd, errs[:2])
+        committed += e.committed_entries
+    assert committed > G * 10
