@@ -773,7 +773,7 @@ struct IngestState {
   std::vector<wirehost::Frame> frames;
   // the stream goes up in pieces on its own stream, one event each, so the
   // CRC and count kernels of a piece run while the later pieces upload
-  hipStream_t up = nullptr, crc = nullptr;
+  hipStream_t up = nullptr, crc = nullptr, up2 = nullptr;
   std::vector<hipEvent_t> ev, evc;  // per piece: CRC'd, uploaded
 };
 static void ingest_free(IngestState *st) {
@@ -781,6 +781,7 @@ static void ingest_free(IngestState *st) {
   for (hipEvent_t x : st->ev) (void)hipEventDestroy(x);
   for (hipEvent_t x : st->evc) (void)hipEventDestroy(x);
   if (st->up) (void)hipStreamDestroy(st->up);
+  if (st->up2) (void)hipStreamDestroy(st->up2);
   if (st->crc) (void)hipStreamDestroy(st->crc);
   if (st->pinned) (void)hipHostFree(st->pinned);
   if (st->steps) (void)hipHostFree(st->steps);
@@ -916,6 +917,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     IngestState *st;
     ~SyncOnReturn() {
       if (st->up) (void)hipStreamSynchronize(st->up);
+      if (st->up2) (void)hipStreamSynchronize(st->up2);
       if (st->crc) (void)hipStreamSynchronize(st->crc);
       (void)hipStreamSynchronize(s);
     }
@@ -960,9 +962,14 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint32_t *d_clen = (uint32_t *)((uint8_t *)st.chunks.p + al256(nc * 8 + 8));
   uint32_t *d_ccrc = (uint32_t *)((uint8_t *)d_clen + al256(nc * 4 + 4));
   // pieces: runs of whole frames of at least ING_PIECE bytes
+  // (DRB_INGEST_PIECE_MB overrides it for the A/B)
+  static const size_t piece = [] {
+    const char *m = getenv("DRB_INGEST_PIECE_MB");
+    return m && atoi(m) > 0 ? (size_t)atoi(m) << 20 : ING_PIECE;
+  }();
   std::vector<size_t> pf;  // first frame of each piece, then nf
   for (size_t f = 0, acc = 0; f < fr.size(); ++f) {
-    if (pf.empty() || acc >= ING_PIECE) {
+    if (pf.empty() || acc >= piece) {
       pf.push_back(f);
       acc = 0;
     }
@@ -973,6 +980,15 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (!st.up &&
       hipStreamCreateWithFlags(&st.up, hipStreamNonBlocking) != hipSuccess)
     return DRB_EDEVICE;
+  if (!st.up2 &&
+      hipStreamCreateWithFlags(&st.up2, hipStreamNonBlocking) != hipSuccess)
+    return DRB_EDEVICE;
+  // the pieces alternate between two upload streams (DRB_INGEST_STREAMS=2:
+  // two copy engines at once) or go through one
+  static const int nup = [] {
+    const char *m = getenv("DRB_INGEST_STREAMS");
+    return m && atoi(m) == 2 ? 2 : 1;
+  }();
   if (!st.crc &&
       hipStreamCreateWithFlags(&st.crc, hipStreamNonBlocking) != hipSuccess)
     return DRB_EDEVICE;
@@ -988,6 +1004,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // enqueued (the device buffers may still be read by an earlier call)
   HIPCHK(hipEventRecord(st.ev[0], sm));
   HIPCHK(hipStreamWaitEvent(st.up, st.ev[0], 0));
+  HIPCHK(hipStreamWaitEvent(st.up2, st.ev[0], 0));
   HIPCHK(hipStreamWaitEvent(st.crc, st.ev[0], 0));
   // where the payload CRCs run (DRB_INGEST_MODE, measured in DESIGN §10):
   // 0 on the engine stream per piece after the Requests scans, 1 on a
@@ -1012,15 +1029,16 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         const size_t a = q ? fr[pf[q]].off - 20 : 0;
         const size_t b = pf[q + 1] < fr.size() ? fr[pf[q + 1]].off - 20
                                                 : walked;
+        hipStream_t us = nup == 2 && (q & 1) ? st.up2 : st.up;
         if (b > a)
           up_err = hipMemcpyAsync(ds + a, stream + a, b - a,
-                                  hipMemcpyHostToDevice, st.up);
+                                  hipMemcpyHostToDevice, us);
         if (mode == 0) {  // the piece is up
-          if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.up);
+          if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], us);
           continue;
         }
         // the piece's payload CRCs as it lands
-        if (up_err == hipSuccess) up_err = hipEventRecord(st.evc[q], st.up);
+        if (up_err == hipSuccess) up_err = hipEventRecord(st.evc[q], us);
         if (up_err == hipSuccess) up_err = hipStreamWaitEvent(cs, st.evc[q], 0);
         const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
         if (up_err == hipSuccess && c1 > c0) {
