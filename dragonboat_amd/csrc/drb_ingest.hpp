@@ -614,6 +614,10 @@ namespace wirehost {
 
 static uint32_t crc_tab[256];
 static uint32_t x2n[32];  // x^(2^k) mod P (zlib x2n_table)
+// the shift over one 16 KB payload chunk, multmodp(x^(8 * 16384), a), as
+// four byte tables (the operator is linear in a): a chunk's CRC folds into
+// its frame's in four lookups instead of two multmodp loops
+static uint32_t sh16k[4][256];
 static std::once_flag crc_once;
 
 static void crc_build() {
@@ -626,6 +630,13 @@ static void crc_build() {
   uint32_t p = 1u << 30;  // x^1
   x2n[0] = p;
   for (int n = 1; n < 32; ++n) x2n[n] = p = drb::gf2_multmodp(p, p);
+  uint32_t op = 1u << 31;  // x^0, then x^(8 * 16384)
+  uint32_t k = 3;
+  for (uint64_t n = 16384; n; n >>= 1, ++k)
+    if (n & 1) op = drb::gf2_multmodp(x2n[k & 31], op);
+  for (int b = 0; b < 4; ++b)
+    for (uint32_t v = 0; v < 256; ++v)
+      sh16k[b][v] = drb::gf2_multmodp(op, v << (8 * b));
 }
 // thread-safe: transport threads may call drb_ingest_wire concurrently
 static void crc_init() { std::call_once(crc_once, crc_build); }
@@ -643,6 +654,12 @@ static uint32_t crc32_combine(uint32_t a, uint32_t b, uint64_t len_b) {
   for (uint64_t n = len_b; n; n >>= 1, ++k)
     if (n & 1) p = drb::gf2_multmodp(x2n[k & 31], p);
   return drb::gf2_multmodp(p, a) ^ b;
+}
+
+// crc32_combine(a, b, 16384)
+static inline uint32_t crc32_combine16k(uint32_t a, uint32_t b) {
+  return sh16k[0][a & 0xff] ^ sh16k[1][(a >> 8) & 0xff] ^
+         sh16k[2][(a >> 16) & 0xff] ^ sh16k[3][a >> 24] ^ b;
 }
 
 static uint64_t be(const uint8_t *p, int n) {
@@ -1185,7 +1202,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       // CRC(M) = f(M) ^ (~0 * x^(8|M|) mod P) ^ ~0
       uint32_t c = 0;
       for (uint32_t k = cfirst[f]; k < cfirst[f + 1]; ++k)
-        c = wirehost::crc32_combine(c, ccrc[k], clen[k]);
+        c = clen[k] == CH ? wirehost::crc32_combine16k(c, ccrc[k])
+                          : wirehost::crc32_combine(c, ccrc[k], clen[k]);
       c ^= wirehost::crc32_combine(0xffffffffu, 0, fr[f].size) ^ 0xffffffffu;
       const size_t nmf = fr[f].step.size();
       if (c != fr[f].pcrc || !fr[f].scan_ok || (fbad[f] & 1u)) {
@@ -1256,8 +1274,14 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       k_ing_keys<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
           v, dm, kin, vin, nm, d_ctr);
       HIPCHK(hipGetLastError());
+      // the key bits that can differ: plane keys < G·R·R, and the ~0 of a
+      // refused message keeps all ones in those bits, so it still sorts last
+      int kbits = 1;
+      while (kbits < 32 &&
+             ((uint64_t)1 << kbits) <= (uint64_t)v.G * v.R * v.R)
+        ++kbits;
       HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout,
-                                                (int)nm, 0, 32, sm));
+                                                (int)nm, 0, kbits, sm));
       k_ing_place<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
           v, ds, dm, de, kout, vout, nm, (uint32_t)(e->round & 1),
           (uint32_t)e->round, d_ctr);
