@@ -161,17 +161,17 @@ class ApplyResult(C.Structure):
 
 
 class WorkerRead(C.Structure):
-    """drb_worker_read: a ReadyToRead and where its served reads are."""
-    _fields_ = [("group", C.c_uint64), ("index", C.c_uint64),
-                ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64),
-                ("n_values", C.c_uint32), ("first", C.c_uint32)]
+    """drb_worker_read: a ReadyToRead and where its served reads start
+    (values[first, next record's first))."""
+    _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64),
+                ("ctx_high", C.c_uint64), ("group", C.c_uint32),
+                ("first", C.c_uint32)]
 
 
 class WorkerApplied(C.Structure):
     """drb_worker_applied: one applied entry (pendingProposals.applied)."""
-    _fields_ = [("group", C.c_uint64), ("index", C.c_uint64),
-                ("key", C.c_uint64), ("value", C.c_uint64),
-                ("ignored", C.c_uint32), ("pad", C.c_uint32)]
+    _fields_ = [("key", C.c_uint64), ("value", C.c_uint64),
+                ("group", C.c_uint32), ("ignored", C.c_uint32)]
 
 
 class WorkerBufs(C.Structure):

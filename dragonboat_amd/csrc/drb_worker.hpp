@@ -103,12 +103,11 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
     const bool served = (m >> k) & 1u;
     if (o.x + k < cap_rd) {
       drb_worker_read r;
-      r.group = g;
       r.index = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
       r.ctx_low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
       r.ctx_high = (uint64_t)c1.x | ((uint64_t)c1.y << 32);
-      r.n_values = served ? n_reads : 0u;
-      r.first = (uint32_t)vo;
+      r.group = (uint32_t)g;
+      r.first = (uint32_t)vo;  // (its n_reads results follow when served)
       rd[o.x + k] = r;
     }
     if (!served) continue;
@@ -125,8 +124,6 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
     const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
     const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
     drb_worker_applied r;
-    r.group = g;
-    r.index = idx;
     r.key = hi64(m0);
     const uint64_t client = lo64(m1);
     const uint32_t type = m2.z, clen = m2.w;
@@ -134,7 +131,7 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
     // KVTest.Update's Result.Value: the payload length (kvtest.go:161)
     r.value = r.ignored ? 0
                         : (type == DRB_ENTRY_ENCODED && clen ? clen - 1 : clen);
-    r.pad = 0;
+    r.group = (uint32_t)g;
     ap[a] = r;
   }
 }
@@ -285,6 +282,9 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
   if ((b->reads_cap && !b->reads) || (b->values_cap && !b->values) ||
       (b->applied_cap && !b->applied))
     return DRB_EINVAL;
+  // (the records hold the lane and the value offset in 32 bits)
+  if (e->v.G > 0xffffffffull || b->values_cap > 0xffffffffull)
+    return DRB_ERANGE;
   if (int rc = worker_init(e)) return rc;
   WorkerState &w = *e->worker;
   if (int rc = worker_reserve(e, b->reads_cap, b->values_cap, b->applied_cap))

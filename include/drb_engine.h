@@ -701,23 +701,22 @@ int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
  * that export's bytes are in its buffers and fills the counts.  Records in
  * group order, each group's in release / index order.
  */
-typedef struct drb_worker_read {  /* one ReadyToRead */
-  uint64_t group;      /* lane (ShardID = first_shard_id + group) */
+typedef struct drb_worker_read {  /* one ReadyToRead, 32 B */
   uint64_t index;      /* its read index */
   uint64_t ctx_low;
   uint64_t ctx_high;
-  uint32_t n_values;   /* reads served behind it (0: deferred until the
-                        * index is applied, or no reads this round) */
-  uint32_t first;      /* their results: values[first, first + n_values) */
+  uint32_t group;      /* lane (ShardID = first_shard_id + group) */
+  uint32_t first;      /* its served reads' results: values[first, end),
+                        * end = the next record's first (n_values after
+                        * the last); empty when the ctx was deferred until
+                        * its index is applied, or no reads ran */
 } drb_worker_read;
 
-typedef struct drb_worker_applied {  /* one applied entry */
-  uint64_t group;
-  uint64_t index;
+typedef struct drb_worker_applied {  /* one applied entry, 24 B */
   uint64_t key;        /* pb.Entry.Key: the proposal's RequestState */
   uint64_t value;      /* sm.Result.Value (kvtest.go:161) */
+  uint32_t group;
   uint32_t ignored;    /* 1: an empty no-op entry (statemachine.go:939) */
-  uint32_t pad;
 } drb_worker_applied;
 
 typedef struct drb_worker_bufs {
