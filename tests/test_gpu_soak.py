@@ -11,6 +11,7 @@ with the oracle cluster (the reference step loop: tests/gpu_harness.py):
 every replica field, the logs, the KV, the outboxes and the ReadyToReads,
 and the round counters.  No replica may leave the GPU.
 """
+import os
 import random
 
 import pytest
@@ -32,8 +33,17 @@ def _set_hosted(p, groups, slot, hosted):
         p.eng.import_replicas(g, sts)
 
 
+def _seeds():
+    # DRB_SOAK_SEEDS="a-b" widens the run (tools, not the default suite)
+    r = os.environ.get("DRB_SOAK_SEEDS")
+    if r:
+        a, b = (int(x) for x in r.split("-"))
+        return list(range(a, b + 1))
+    return [11, 12]
+
+
 @pytest.mark.parametrize("case", ["voters", "witness", "nonvoting"])
-@pytest.mark.parametrize("seed", [11, 12])
+@pytest.mark.parametrize("seed", _seeds())
 def test_random_rounds(case, seed):
     rng = random.Random(seed * 1000 + len(case))
     G, R = 48, 4
