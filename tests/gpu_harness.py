@@ -174,7 +174,7 @@ class Pair:
                 continue
             if st.role == abi.LEADER:
                 lead += 1
-            elif st.role != abi.FOLLOWER:
+            elif st.role not in (abi.FOLLOWER, abi.NONVOTING, abi.WITNESS):
                 return False
             if self.orc.export_outbox(g, s) or st.ri_count:
                 return False
