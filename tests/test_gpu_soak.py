@@ -53,8 +53,12 @@ def test_random_rounds(case, seed):
     kw = {}
     if case != "voters":
         kw[case + "_slots"] = 1 << 3
+    # (the mailbox bound the pre-pass checks is an upper bound of a
+    # round's sends per follower -- tick, proposals, ReadIndex broadcasts,
+    # commit notifications, one answer per message in -- which this mix
+    # drives past 16 at R = 4 now and then; 24 is the mailbox's maximum)
     p = Pair(G=G, R=R, elections=1, forward_proposals=1, max_props=2,
-             mailbox=16, **kw)
+             mailbox=24, **kw)
     # replica IDs (0: the leader); a witness neither proposes nor reads
     ids = [0, 1, 2, 3] + ([4] if case != "witness" else [])
     stopped = {}  # slot -> groups
@@ -89,8 +93,13 @@ def test_random_rounds(case, seed):
             assert reason == abi.FB["CAPACITY"] and \
                 not flags & abi.F_ERROR, (rnd, g, s, reason, flags)
             if g not in p.cpu:
-                ri_full += p.eng.export_replicas(g, 1)[s].ri_count == \
-                    abi.DRB_RI_DEPTH
+                st = p.eng.export_replicas(g, 1)[s]
+                ri_full += st.ri_count == abi.DRB_RI_DEPTH
+                if os.environ.get("DRB_SOAK_VERBOSE") and fallbacks < 2:
+                    d = st.to_dict(p.R)
+                    print("fallback", rnd, g, s, {k: d[k] for k in (
+                        "last_index", "committed", "ri_count", "remotes",
+                        "ring_lo", "term_start") if k in d}, d["ri"])
                 p.to_cpu(g)
                 fallbacks += 1
         if not recs and not p.cpu:
