@@ -2801,8 +2801,13 @@ static int exchange_check(drb_engine *const *engines, uint32_t n) {
   const uint32_t R = engines[0]->v.R;
   for (uint32_t r = 0; r < n; ++r) {
     const drb_engine *e = engines[r];
+    // (the planes' shapes must match: the pull indexes a sender's planes
+    // with the receiver's layout)
+    const View &v0 = engines[0]->v;
     if (!e || e->v.R != R || e->v.place_world != n || e->v.place_rank != r ||
-        e->round != engines[0]->round || e->v.G != engines[0]->v.G)
+        e->round != engines[0]->round || e->v.G != v0.G ||
+        e->v.MB != v0.MB || e->v.E != v0.E || e->v.C16 != v0.C16 ||
+        (e->v.rterm_in == nullptr) != (v0.rterm_in == nullptr))
       return DRB_EINVAL;
   }
   return DRB_OK;
