@@ -259,6 +259,36 @@ __global__ __launch_bounds__(256) void k_crc_chunks(const uint8_t *data,
   if (threadIdx.x == 0) fraw[b] = red[0] ^ red[1] ^ red[2] ^ red[3];
 }
 
+// The upload as a pull (DRB_INGEST_ZC=1, a pinned source only): the device
+// reads the mapped host stream over PCIe with 16 B loads, four in flight a
+// lane, instead of a copy-engine DMA.  dst and src share their alignment
+// mod 16 (the caller checks), n bytes.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_zc_pull(uint8_t *dst,
+                                                 const uint8_t *src,
+                                                 uint64_t n) {
+  const uint64_t gt = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+  const uint64_t h = head < n ? head : n;
+  if (gt < h) dst[gt] = src[gt];
+  const uint64_t nv = (n - h) >> 4;
+  u32x4 *d = (u32x4 *)(dst + h);
+  const u32x4 *s = (const u32x4 *)(src + h);
+  const uint64_t stride = gridDim.x * 256ull;
+  constexpr int U = 4;
+  for (uint64_t i = gt; i < nv; i += stride * U) {
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u * stride < nv) x[u] = __builtin_nontemporal_load(s + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u * stride < nv) d[i + u * stride] = x[u];
+  }
+  const uint64_t t0 = h + (nv << 4);
+  if (gt < n - t0) dst[t0 + gt] = src[t0 + gt];
+}
+
 // pass 1: entry counts and errors, and the record of every message (the
 // decode pass parses again only the messages with entries); the frame of a
 // malformed message is marked (the host stops the stream there)
@@ -336,7 +366,8 @@ constexpr size_t ING_PIECE = 32u << 20;
 __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
                             const uint32_t *err, const uint32_t *n_ent,
                             uint32_t *nsc, uint8_t *deliver, uint64_t n,
-                            unsigned long long *ctr) {
+                            unsigned long long *ctr, DecMsg *dm,
+                            uint32_t *dlist) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t st = 0, r = ING_BAD, ne = 0;
   if (i < n) {
@@ -348,6 +379,25 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
   if (i < n) {
     nsc[i] = dl ? ne : 0u;
     deliver[i] = dl ? 1 : 0;
+    if (!dl) dm[i].err = ING_BAD;  // not delivered: sorts last
+  }
+  // the delivered messages with entries, for the decode: one slot range per
+  // workgroup (their order does not matter, each decodes into its own
+  // records)
+  const uint64_t bd = __ballot(dl && ne);
+  __shared__ uint32_t wn[4], wbase;
+  if ((threadIdx.x & 63) == 0) wn[threadIdx.x >> 6] = (uint32_t)__popcll(bd);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wn[0] + wn[1] + wn[2] + wn[3];
+    wbase = t ? (uint32_t)atomicAdd(&ctr[6], (unsigned long long)t) : 0u;
+  }
+  __syncthreads();
+  if (dl && ne) {
+    uint32_t at = wbase;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) at += wn[w];
+    dlist[at + __popcll(bd & ((1ull << (threadIdx.x & 63)) - 1))] =
+        (uint32_t)i;
   }
   const bool snap = st != 0 && r == ING_SNAPSHOT;
   const bool msg = st == 1 && r != ING_SNAPSHOT;
@@ -376,16 +426,13 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
 // 1's); a message not delivered is marked so that it sorts last
 __global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
                              const uint32_t *mlen, const uint32_t *ent0,
-                             const uint32_t *n_ent, const uint8_t *deliver,
-                             DecMsg *out, drb_entry *ents, uint64_t n,
-                             uint32_t cmd_cap) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (!deliver[i]) {
-    out[i].err = ING_BAD;
-    return;
-  }
-  if (n_ent[i] == 0) return;  // pass 1's record is complete
+                             const uint32_t *dlist, DecMsg *out,
+                             drb_entry *ents, uint64_t n, uint32_t cmd_cap) {
+  // only the delivered messages with entries (k_ing_tally's list): the
+  // others' pass-1 records are complete, or marked not delivered
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = dlist[j];
   DecMsg m;
   bool big = false;
   m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
@@ -1032,6 +1079,19 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     return m ? atoi(m) : 0;
   }();
   hipStream_t cs = mode == 1 ? st.crc : sm;
+  // the pull upload (k_zc_pull) when asked for and the stream is pinned,
+  // mapped host memory aligned as the device buffer is
+  const uint8_t *hsrc = nullptr;
+  if (const char *z = getenv("DRB_INGEST_ZC"); z && z[0] == '1' && len) {
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, stream) == hipSuccess &&
+        pa.type == hipMemoryTypeHost && pa.devicePointer && pa.hostPointer &&
+        ((uintptr_t)stream & 15) == 0)
+      hsrc = (const uint8_t *)pa.devicePointer +
+             (stream - (const uint8_t *)pa.hostPointer);
+    if ((uintptr_t)hsrc & 15) hsrc = nullptr;
+    (void)hipGetLastError();  // (a pageable stream: not an error here)
+  }
   if (nc) {
     HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice,
                           cs));
@@ -1047,9 +1107,16 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         const size_t b = pf[q + 1] < fr.size() ? fr[pf[q + 1]].off - 20
                                                 : walked;
         hipStream_t us = nup == 2 && (q & 1) ? st.up2 : st.up;
-        if (b > a)
+        if (b > a && hsrc) {
+          const uint64_t nv = (b - a) / 16 + 1;
+          const unsigned nb = (unsigned)std::min<uint64_t>(
+              4096, (nv + 1023) / 1024);
+          k_zc_pull<<<nb, 256, 0, us>>>(ds + a, hsrc + a, b - a);
+          up_err = hipGetLastError();
+        } else if (b > a) {
           up_err = hipMemcpyAsync(ds + a, stream + a, b - a,
                                   hipMemcpyHostToDevice, us);
+        }
         if (mode == 0) {  // the piece is up
           if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], us);
           continue;
@@ -1089,7 +1156,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, scan_tb, (uint64_t *)nullptr,
                                           (uint64_t *)nullptr, (int)m1, sm));
   const size_t mb = al256(m1 * 8) * 3 +
-                    al256(m1 * 4) * 7 + al256(m1) +
+                    al256(m1 * 4) * 8 + al256(m1) +
                     al256((nf + 1) * 4) + al256((nf + 1) * 8) * 2 +
                     al256(nf + 1) + ING_TALLY_ROWS * 64 + al256(scan_tb);
   if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
@@ -1107,6 +1174,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint32_t *d_nsc = (uint32_t *)take(m1 * 4);
   uint32_t *d_ent0 = (uint32_t *)take(m1 * 4);
   uint8_t *d_deliver = take(m1);
+  uint32_t *d_dlist = (uint32_t *)take(m1 * 4);
   uint32_t *d_fbad = (uint32_t *)take((nf + 1) * 4);
   uint64_t *d_mbase = (uint64_t *)take((nf + 1) * 8);
   uint64_t *d_foff = (uint64_t *)take((nf + 1) * 8);
@@ -1147,8 +1215,24 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         });
       for (auto &x : th) x.join();
     }
-    HIPCHK(hipMemcpyAsync(d_step, st.steps, nm * 4, hipMemcpyHostToDevice,
-                          sm));
+    // pulled by a kernel from the mapped pinned buffer, not DMA'd: a copy
+    // queued here waits on the copy engine behind the stream's remaining
+    // pieces, and the per-piece counts below need it (profiles/r04_ingest)
+    // (DRB_INGEST_STEPS_DMA=1: the DMA, for the A/B)
+    void *hsteps = nullptr;
+    const char *sd = getenv("DRB_INGEST_STEPS_DMA");
+    if (!(sd && sd[0] == '1') &&
+        hipHostGetDevicePointer(&hsteps, st.steps, 0) == hipSuccess &&
+        hsteps && ((uintptr_t)hsteps & 15) == 0) {
+      const uint64_t nv = nm * 4 / 16 + 1;
+      k_zc_pull<<<(unsigned)std::min<uint64_t>(1024, (nv + 1023) / 1024), 256,
+                  0, sm>>>((uint8_t *)d_step, (const uint8_t *)hsteps, nm * 4);
+      HIPCHK(hipGetLastError());
+    } else {
+      (void)hipGetLastError();
+      HIPCHK(hipMemcpyAsync(d_step, st.steps, nm * 4, hipMemcpyHostToDevice,
+                            sm));
+    }
     HIPCHK(hipMemcpyAsync(d_mbase, mbase.data(), (nf + 1) * 8,
                           hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(d_foff, foff.data(), (nf + 1) * 8,
@@ -1232,7 +1316,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(hipMemcpyAsync(d_fstate, fstate.data(), nf + 1,
                           hipMemcpyHostToDevice, sm));
     k_ing_tally<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-        d_mframe, d_fstate, d_err, d_nent, d_nsc, d_deliver, nm, d_ctr);
+        d_mframe, d_fstate, d_err, d_nent, d_nsc, d_deliver, nm, d_ctr,
+        (DecMsg *)st.msgs.p, d_dlist);
     HIPCHK(hipGetLastError());
     size_t tb = 0, tb2 = 0;
     uint32_t *kin = nullptr, *kout = nullptr, *vin = nullptr, *vout = nullptr;
@@ -1247,12 +1332,12 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     void *tmp = sp + 4 * al256(nm * 4);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_nsc, d_ent0, (int)nm,
                                             sm));
-    unsigned long long rows[ING_TALLY_ROWS * 8], c0[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long rows[ING_TALLY_ROWS * 8], c0[7] = {0, 0, 0, 0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(rows, d_ctr, sizeof(rows), hipMemcpyDeviceToHost,
                           sm));
     HIPCHK(hipStreamSynchronize(sm));
     for (uint32_t q = 0; q < ING_TALLY_ROWS; ++q)
-      for (int k = 2; k < 6; ++k) c0[k] += rows[q * 8 + k];
+      for (int k = 2; k < 7; ++k) c0[k] += rows[q * 8 + k];
     res.snapshots += c0[2];
     res.messages = c0[3];
     res.dropped += c0[4];
@@ -1262,9 +1347,12 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       if (ing_grow(st.ents, eb)) return DRB_EDEVICE;
       DecMsg *dm = (DecMsg *)st.msgs.p;
       drb_entry *de = (drb_entry *)st.ents.p;
-      k_ing_decode<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
-          ds, d_moff, d_mlen, d_ent0, d_nent, d_deliver, dm, de, nm, cmd_cap);
-      HIPCHK(hipGetLastError());
+      const uint64_t nd = c0[6];  // delivered messages with entries
+      if (nd) {
+        k_ing_decode<<<(unsigned)((nd + 255) / 256), 256, 0, sm>>>(
+            ds, d_moff, d_mlen, d_ent0, d_dlist, dm, de, nd, cmd_cap);
+        HIPCHK(hipGetLastError());
+      }
       tr.mark("decode");
       // 5. planes: keys, a stable radix sort, one lane per plane
       kin = (uint32_t *)sp;
