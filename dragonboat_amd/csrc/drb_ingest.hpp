@@ -43,7 +43,40 @@ struct DecMsg {
 };
 constexpr uint32_t ING_OK = 0, ING_BAD = 1, ING_SNAPSHOT = 2, ING_BIG = 3;
 
-__device__ inline bool d_varint(const uint8_t *d, uint32_t n, uint32_t &i,
+// A lane's byte cursor over the uploaded stream.  WIN: the aligned 16 B
+// block holding the last byte read stays in registers, one load per 16
+// bytes instead of a dependent load per byte (the stream's device buffer is
+// padded past its last frame, al256(walked + 16), so a block that holds a
+// message's last byte is inside it) -- measured 2-4 % slower than the plain
+// per-byte loads, which hit the L1; DRB_INGEST_WINDOW=1 selects it.
+template <bool WIN = true>
+struct Bytes {
+  const uint8_t *p;
+  uintptr_t wa = ~(uintptr_t)0;
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  __device__ explicit Bytes(const uint8_t *d) : p(d) {}
+  __device__ inline uint32_t operator[](uint64_t i) {
+    if (!WIN) return p[i];  // a load per byte (the default)
+    const uintptr_t a = (uintptr_t)(p + i);
+    const uintptr_t b = a & ~(uintptr_t)15;
+    if (b != wa) {
+      const uint4 x = *(const uint4 *)b;
+      w0 = x.x;
+      w1 = x.y;
+      w2 = x.z;
+      w3 = x.w;
+      wa = b;
+    }
+    const uint32_t o = (uint32_t)(a & 15);
+    const uint32_t dw = o < 8 ? (o < 4 ? w0 : w1) : (o < 12 ? w2 : w3);
+    return (dw >> ((o & 3) * 8)) & 0xffu;
+  }
+};
+
+// (every index below is from the message's first byte; d_entry's from the
+// entry's, at offset e0)
+template <class B>
+__device__ inline bool d_varint(B &d, uint32_t n, uint32_t &i,
                                 uint64_t &v) {
   v = 0;
   for (uint32_t s = 0; s < 70; s += 7) {
@@ -56,7 +89,8 @@ __device__ inline bool d_varint(const uint8_t *d, uint32_t n, uint32_t &i,
 }
 
 // skipRaft (raft.pb.go): an unknown field
-__device__ inline bool d_skip(const uint8_t *d, uint32_t n, uint32_t &i,
+template <class B>
+__device__ inline bool d_skip(B &d, uint32_t n, uint32_t &i,
                               uint64_t wire) {
   uint64_t x;
   switch (wire & 7) {
@@ -73,19 +107,20 @@ __device__ inline bool d_skip(const uint8_t *d, uint32_t n, uint32_t &i,
 
 // colfer u64 field body (raft_optimized.go:316-350): varint whose 9th
 // byte is taken whole, or 8 bytes big endian after a 0x80-flagged tag
-__device__ inline bool d_colfer_u64(const uint8_t *d, uint32_t n, uint32_t &i,
-                                    bool flag, uint64_t &v) {
+template <class B>
+__device__ inline bool d_colfer_u64(B &d, uint32_t e0, uint32_t n,
+                                    uint32_t &i, bool flag, uint64_t &v) {
   if (flag) {
     if (i + 8 >= n) return false;
     v = 0;
-    for (int k = 0; k < 8; ++k) v = (v << 8) | d[i + k];
+    for (int k = 0; k < 8; ++k) v = (v << 8) | d[e0 + i + k];
     i += 8;
     return true;
   }
   v = 0;
   for (uint32_t s = 0;; s += 7) {
     if (i + 1 >= n) return false;
-    const uint64_t b = d[i++];
+    const uint64_t b = d[e0 + i++];
     if (s == 56 || b < 0x80) {
       v |= b << s;
       return true;
@@ -94,22 +129,24 @@ __device__ inline bool d_colfer_u64(const uint8_t *d, uint32_t n, uint32_t &i,
   }
 }
 
-// colfer Entry.Unmarshal (raft_optimized.go:308-656); cmd_off is the Cmd's
-// offset from d
-__device__ inline bool d_entry(const uint8_t *d, uint32_t n, drb_entry &e) {
+// colfer Entry.Unmarshal (raft_optimized.go:308-656) of the n bytes at e0;
+// cmd_off is the Cmd's offset from e0
+template <class B>
+__device__ inline bool d_entry(B &d, uint32_t e0, uint32_t n,
+                               drb_entry &e) {
   e.term = e.index = e.key = e.client_id = e.series_id = e.responded_to = 0;
   e.type = e.cmd_len = 0;
   e.cmd_off = 0;
   if (n == 0) return false;
   uint32_t i = 1;
-  uint32_t h = d[0];
+  uint32_t h = d[e0];
   for (uint32_t tag = 0; tag < 7; ++tag) {
     if ((h & 0x7fu) != tag || h == 0x7fu) continue;
     if (tag == 2) {  // Type: uint32 varint, 0x80 flag = negated
       uint64_t x = 0;
       for (uint32_t s = 0;; s += 7) {
         if (i + 1 >= n) return false;
-        const uint64_t b = d[i++];
+        const uint64_t b = d[e0 + i++];
         x |= (b & 0x7f) << s;
         if (b < 0x80) break;
         if (s > 28) return false;
@@ -117,7 +154,7 @@ __device__ inline bool d_entry(const uint8_t *d, uint32_t n, drb_entry &e) {
       e.type = (h & 0x80u) ? (uint32_t)(~(uint32_t)x + 1) : (uint32_t)x;
     } else {
       uint64_t x;
-      if (!d_colfer_u64(d, n, i, (h & 0x80u) != 0, x)) return false;
+      if (!d_colfer_u64(d, e0, n, i, (h & 0x80u) != 0, x)) return false;
       switch (tag) {
         case 0: e.term = x; break;
         case 1: e.index = x; break;
@@ -127,13 +164,13 @@ __device__ inline bool d_entry(const uint8_t *d, uint32_t n, drb_entry &e) {
         default: e.responded_to = x; break;
       }
     }
-    h = d[i++];
+    h = d[e0 + i++];
   }
   if (h == 7) {  // Cmd (raft_optimized.go:603-641)
     uint64_t x = 0;
     for (uint32_t s = 0;; s += 7) {
       if (i >= n) return false;
-      const uint64_t b = d[i++];
+      const uint64_t b = d[e0 + i++];
       x |= (b & 0x7f) << s;
       if (b < 0x80) break;
       if (s > 56) return false;
@@ -142,7 +179,7 @@ __device__ inline bool d_entry(const uint8_t *d, uint32_t n, drb_entry &e) {
     e.cmd_off = i;
     e.cmd_len = (uint32_t)x;
     i += (uint32_t)x;
-    h = d[i++];
+    h = d[e0 + i++];
   }
   return h == 0x7fu && i == n;
 }
@@ -153,9 +190,12 @@ __constant__ uint8_t c_empty_snapshot[24] = {
 
 // Message.Unmarshal (raft_optimized.go:659-983).  ents == nullptr: count
 // the entries only.  Returns ING_*; *big when a Cmd exceeds cmd_cap.
-__device__ inline uint32_t d_message(const uint8_t *d, uint32_t n, DecMsg &m,
-                                     drb_entry *ents, uint64_t base,
-                                     uint32_t cmd_cap, bool &big) {
+template <bool WIN>
+__device__ inline uint32_t d_message(const uint8_t *msg, uint32_t n,
+                                     DecMsg &m, drb_entry *ents,
+                                     uint64_t base, uint32_t cmd_cap,
+                                     bool &big) {
+  Bytes<WIN> d(msg);
   m.shard = m.from = m.to = m.term = m.log_term = m.log_index = m.commit = 0;
   m.hint = m.hint_high = 0;
   m.type = m.reject = m.n_ent = 0;
@@ -186,7 +226,7 @@ __device__ inline uint32_t d_message(const uint8_t *d, uint32_t n, DecMsg &m,
       if (wt != 2 || !d_varint(d, n, i, l) || l > n - i) return ING_BAD;
       if (field == 11) {
         drb_entry e;
-        if (!d_entry(d + i, (uint32_t)l, e)) return ING_BAD;
+        if (!d_entry(d, i, (uint32_t)l, e)) return ING_BAD;
         if (e.cmd_len > cmd_cap) big = true;
         if (ents) {
           e.cmd_off += base + i;  // the Cmd's offset in the stream
@@ -292,6 +332,7 @@ __global__ __launch_bounds__(256) void k_zc_pull(uint8_t *dst,
 // pass 1: entry counts and errors, and the record of every message (the
 // decode pass parses again only the messages with entries); the frame of a
 // malformed message is marked (the host stops the stream there)
+template <bool WIN>
 __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
                             const uint32_t *mlen, const uint32_t *mframe,
                             uint32_t *n_ent, uint32_t *err,
@@ -301,7 +342,7 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   if (i >= n) return;
   DecMsg m;
   bool big = false;
-  uint32_t r = d_message(s + moff[i], mlen[i], m, nullptr, 0, cmd_cap, big);
+  uint32_t r = d_message<WIN>(s + moff[i], mlen[i], m, nullptr, 0, cmd_cap, big);
   if (r == ING_OK && big) r = ING_BIG;
   n_ent[i] = r == ING_OK ? m.n_ent : 0;
   err[i] = r;
@@ -366,8 +407,7 @@ constexpr size_t ING_PIECE = 32u << 20;
 __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
                             const uint32_t *err, const uint32_t *n_ent,
                             uint32_t *nsc, uint8_t *deliver, uint64_t n,
-                            unsigned long long *ctr, DecMsg *dm,
-                            uint32_t *dlist) {
+                            unsigned long long *ctr, DecMsg *dm) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t st = 0, r = ING_BAD, ne = 0;
   if (i < n) {
@@ -380,24 +420,6 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
     nsc[i] = dl ? ne : 0u;
     deliver[i] = dl ? 1 : 0;
     if (!dl) dm[i].err = ING_BAD;  // not delivered: sorts last
-  }
-  // the delivered messages with entries, for the decode: one slot range per
-  // workgroup (their order does not matter, each decodes into its own
-  // records)
-  const uint64_t bd = __ballot(dl && ne);
-  __shared__ uint32_t wn[4], wbase;
-  if ((threadIdx.x & 63) == 0) wn[threadIdx.x >> 6] = (uint32_t)__popcll(bd);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = wn[0] + wn[1] + wn[2] + wn[3];
-    wbase = t ? (uint32_t)atomicAdd(&ctr[6], (unsigned long long)t) : 0u;
-  }
-  __syncthreads();
-  if (dl && ne) {
-    uint32_t at = wbase;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) at += wn[w];
-    dlist[at + __popcll(bd & ((1ull << (threadIdx.x & 63)) - 1))] =
-        (uint32_t)i;
   }
   const bool snap = st != 0 && r == ING_SNAPSHOT;
   const bool msg = st == 1 && r != ING_SNAPSHOT;
@@ -424,18 +446,19 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
 
 // pass 2: the entries of the messages to deliver (their records are pass
 // 1's); a message not delivered is marked so that it sorts last
+template <bool WIN>
 __global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
                              const uint32_t *mlen, const uint32_t *ent0,
-                             const uint32_t *dlist, DecMsg *out,
+                             const uint32_t *n_ent, DecMsg *out,
                              drb_entry *ents, uint64_t n, uint32_t cmd_cap) {
-  // only the delivered messages with entries (k_ing_tally's list): the
-  // others' pass-1 records are complete, or marked not delivered
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t i = dlist[j];
+  // (a compacted list of these messages, one lane each, measured slower:
+  // 0.80 ms against 0.62, profiles/r04_ingest)
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || n_ent[i] == 0) return;  // pass 1's record is complete
+  // (k_ing_tally marked the messages not delivered)
   DecMsg m;
   bool big = false;
-  m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
+  m.err = d_message<WIN>(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
                     cmd_cap, big);
   m.ent0 = ent0[i];
   out[i] = m;
@@ -1079,6 +1102,11 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     return m ? atoi(m) : 0;
   }();
   hipStream_t cs = mode == 1 ? st.crc : sm;
+  // the parse passes' byte reads: one load a byte (default), or through a
+  // lane's 16 B window (DRB_INGEST_WINDOW=1; measured 2-4 % slower on the
+  // C3 plane, profiles/r04_ingest: the per-byte loads hit the L1)
+  const char *bw = getenv("DRB_INGEST_WINDOW");
+  const bool bytewise = !(bw && bw[0] == '1');
   // the pull upload (k_zc_pull) when asked for and the stream is pinned,
   // mapped host memory aligned as the device buffer is
   const uint8_t *hsrc = nullptr;
@@ -1156,7 +1184,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, scan_tb, (uint64_t *)nullptr,
                                           (uint64_t *)nullptr, (int)m1, sm));
   const size_t mb = al256(m1 * 8) * 3 +
-                    al256(m1 * 4) * 8 + al256(m1) +
+                    al256(m1 * 4) * 7 + al256(m1) +
                     al256((nf + 1) * 4) + al256((nf + 1) * 8) * 2 +
                     al256(nf + 1) + ING_TALLY_ROWS * 64 + al256(scan_tb);
   if (ing_grow(st.misc, mb)) return DRB_EDEVICE;
@@ -1174,7 +1202,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint32_t *d_nsc = (uint32_t *)take(m1 * 4);
   uint32_t *d_ent0 = (uint32_t *)take(m1 * 4);
   uint8_t *d_deliver = take(m1);
-  uint32_t *d_dlist = (uint32_t *)take(m1 * 4);
   uint32_t *d_fbad = (uint32_t *)take((nf + 1) * 4);
   uint64_t *d_mbase = (uint64_t *)take((nf + 1) * 8);
   uint64_t *d_foff = (uint64_t *)take((nf + 1) * 8);
@@ -1260,7 +1287,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       const unsigned gb = (unsigned)((m1 - m0 + 255) / 256);
       k_ing_elems<<<gb, 256, 0, sm>>>(ds, d_scan, d_mbase, d_foff, d_mframe,
                                       d_moff, d_mlen, m1, m0);
-      k_ing_count<<<gb, 256, 0, sm>>>(ds, d_moff, d_mlen, d_mframe, d_nent,
+      (bytewise ? k_ing_count<false> : k_ing_count<true>)<<<gb, 256, 0, sm>>>(ds, d_moff, d_mlen, d_mframe, d_nent,
                                       d_err, d_fbad, (DecMsg *)st.msgs.p, m1,
                                       cmd_cap, m0);
     }
@@ -1317,7 +1344,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                           hipMemcpyHostToDevice, sm));
     k_ing_tally<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
         d_mframe, d_fstate, d_err, d_nent, d_nsc, d_deliver, nm, d_ctr,
-        (DecMsg *)st.msgs.p, d_dlist);
+        (DecMsg *)st.msgs.p);
     HIPCHK(hipGetLastError());
     size_t tb = 0, tb2 = 0;
     uint32_t *kin = nullptr, *kout = nullptr, *vin = nullptr, *vout = nullptr;
@@ -1332,12 +1359,12 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     void *tmp = sp + 4 * al256(nm * 4);
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, d_nsc, d_ent0, (int)nm,
                                             sm));
-    unsigned long long rows[ING_TALLY_ROWS * 8], c0[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long rows[ING_TALLY_ROWS * 8], c0[6] = {0, 0, 0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(rows, d_ctr, sizeof(rows), hipMemcpyDeviceToHost,
                           sm));
     HIPCHK(hipStreamSynchronize(sm));
     for (uint32_t q = 0; q < ING_TALLY_ROWS; ++q)
-      for (int k = 2; k < 7; ++k) c0[k] += rows[q * 8 + k];
+      for (int k = 2; k < 6; ++k) c0[k] += rows[q * 8 + k];
     res.snapshots += c0[2];
     res.messages = c0[3];
     res.dropped += c0[4];
@@ -1347,12 +1374,10 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       if (ing_grow(st.ents, eb)) return DRB_EDEVICE;
       DecMsg *dm = (DecMsg *)st.msgs.p;
       drb_entry *de = (drb_entry *)st.ents.p;
-      const uint64_t nd = c0[6];  // delivered messages with entries
-      if (nd) {
-        k_ing_decode<<<(unsigned)((nd + 255) / 256), 256, 0, sm>>>(
-            ds, d_moff, d_mlen, d_ent0, d_dlist, dm, de, nd, cmd_cap);
-        HIPCHK(hipGetLastError());
-      }
+      (bytewise ? k_ing_decode<false> : k_ing_decode<true>)<<<
+          (unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+          ds, d_moff, d_mlen, d_ent0, d_nsc, dm, de, nm, cmd_cap);
+      HIPCHK(hipGetLastError());
       tr.mark("decode");
       // 5. planes: keys, a stable radix sort, one lane per plane
       kin = (uint32_t *)sp;
