@@ -30,6 +30,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <thread>
 
 namespace drb {
@@ -353,9 +354,13 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   if (r == ING_BIG) atomicOr(&frame_bad[mframe[i]], 2u);
 }
 
-__global__ void k_widen_step(const uint32_t *in, uint64_t *out, uint64_t n) {
+// the steps as they went up: 2 B each when every step fits (the common
+// case: half the PCIe bytes), else 4 B
+__global__ void k_widen_step(const void *in, uint64_t *out, uint64_t n,
+                             bool narrow) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = in[i];
+  if (i < n)
+    out[i] = narrow ? ((const uint16_t *)in)[i] : ((const uint32_t *)in)[i];
 }
 
 // Requests element i: its tag at the frame's payload offset plus the
@@ -1249,7 +1254,29 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       HIPCHK(hipHostMalloc((void **)&st.steps, nm * 4, hipHostMallocDefault));
       st.steps_cap = nm;
     }
+    // 2 B steps when every one fits (a message under 64 KB), else 4 B
+    std::atomic<bool> wide{false};
     {
+      const size_t nt = std::min<size_t>(16, nf);
+      std::vector<std::thread> th;
+      uint16_t *s16 = (uint16_t *)st.steps;
+      for (size_t t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+          for (size_t f = t; f < nf && !wide.load(std::memory_order_relaxed);
+               f += nt) {
+            const uint32_t *a = fr[f].step.data();
+            uint16_t *o = s16 + mbase[f];
+            uint32_t any = 0;
+            for (size_t k = 0, n = fr[f].step.size(); k < n; ++k) {
+              any |= a[k];
+              o[k] = (uint16_t)a[k];
+            }
+            if (any >> 16) wide.store(true);
+          }
+        });
+      for (auto &x : th) x.join();
+    }
+    if (wide) {
       const size_t nt = std::min<size_t>(16, nf);
       std::vector<std::thread> th;
       for (size_t t = 0; t < nt; ++t)
@@ -1261,6 +1288,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         });
       for (auto &x : th) x.join();
     }
+    const uint64_t step_bytes = nm * (wide ? 4 : 2);
     // pulled by a kernel from the mapped pinned buffer, not DMA'd: a copy
     // queued here waits on the copy engine behind the stream's remaining
     // pieces, and the per-piece counts below need it (profiles/r04_ingest)
@@ -1270,14 +1298,15 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     if (!(sd && sd[0] == '1') &&
         hipHostGetDevicePointer(&hsteps, st.steps, 0) == hipSuccess &&
         hsteps && ((uintptr_t)hsteps & 15) == 0) {
-      const uint64_t nv = nm * 4 / 16 + 1;
+      const uint64_t nv = step_bytes / 16 + 1;
       k_zc_pull<<<(unsigned)std::min<uint64_t>(1024, (nv + 1023) / 1024), 256,
-                  0, sm>>>((uint8_t *)d_step, (const uint8_t *)hsteps, nm * 4);
+                  0, sm>>>((uint8_t *)d_step, (const uint8_t *)hsteps,
+                           step_bytes);
       HIPCHK(hipGetLastError());
     } else {
       (void)hipGetLastError();
-      HIPCHK(hipMemcpyAsync(d_step, st.steps, nm * 4, hipMemcpyHostToDevice,
-                            sm));
+      HIPCHK(hipMemcpyAsync(d_step, st.steps, step_bytes,
+                            hipMemcpyHostToDevice, sm));
     }
     HIPCHK(hipMemcpyAsync(d_mbase, mbase.data(), (nf + 1) * 8,
                           hipMemcpyHostToDevice, sm));
@@ -1287,8 +1316,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         d_mbase, (uint32_t)nf, d_mframe, nm);
     // offsets and lengths from the elements' steps: a scan, then each
     // element's tag and length varints read from the uploaded stream
-    k_widen_step<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(d_step,
-                                                                d_step64, nm);
+    k_widen_step<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+        d_step, d_step64, nm, !wide);
     HIPCHK(hipcub::DeviceScan::InclusiveSum(d_scan_tmp, scan_tb, d_step64,
                                             d_scan, (int)nm, sm));
     if (ing_grow(st.msgs, al256(nm * sizeof(DecMsg)))) return DRB_EDEVICE;
