@@ -886,11 +886,13 @@ struct IngestState {
   // CRC and count kernels of a piece run while the later pieces upload
   hipStream_t up = nullptr, crc = nullptr, up2 = nullptr;
   std::vector<hipEvent_t> ev, evc;  // per piece: CRC'd, uploaded
+  hipEvent_t evv = nullptr;  // the verdicts' inputs are down (speculation)
 };
 static void ingest_free(IngestState *st) {
   if (!st) return;
   for (hipEvent_t x : st->ev) (void)hipEventDestroy(x);
   for (hipEvent_t x : st->evc) (void)hipEventDestroy(x);
+  if (st->evv) (void)hipEventDestroy(st->evv);
   if (st->up) (void)hipStreamDestroy(st->up);
   if (st->up2) (void)hipStreamDestroy(st->up2);
   if (st->crc) (void)hipStreamDestroy(st->crc);
@@ -1401,10 +1403,26 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     HIPCHK(hipMemcpyAsync(ccrc.data(), d_ccrc, nc * 4, hipMemcpyDeviceToHost, sm));
   HIPCHK(hipMemcpyAsync(fbad.data(), d_fbad, (fr.size() + 1) * 4,
                         hipMemcpyDeviceToHost, sm));
-  if (spec)
+  // the key bits that can differ: plane keys < G·R·R, and the ~0 of a
+  // refused message keeps all ones in those bits, so it still sorts last
+  int kbits = 1;
+  while (kbits < 32 && ((uint64_t)1 << kbits) <= (uint64_t)v.G * v.R * v.R)
+    ++kbits;
+  if (spec) {
+    // the plane sort of the speculative keys runs while the host checks
+    // the verdicts
     HIPCHK(hipMemcpyAsync(rows, d_ctr, sizeof(rows), hipMemcpyDeviceToHost,
                           sm));
-  HIPCHK(hipStreamSynchronize(sm));
+    if (!st.evv &&
+        hipEventCreateWithFlags(&st.evv, hipEventDisableTiming) != hipSuccess)
+      return DRB_EDEVICE;
+    HIPCHK(hipEventRecord(st.evv, sm));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout,
+                                              (int)nm, 0, kbits, sm));
+    HIPCHK(hipEventSynchronize(st.evv));
+  } else {
+    HIPCHK(hipStreamSynchronize(sm));
+  }
   tr.mark("crc+cnt");
   // 4. the frames delivered: up to the first with a bad CRC or a batch that
   // does not decode (ErrBadMessage closes the connection, tcp.go:528-530)
@@ -1489,14 +1507,9 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
             v, dm, kin, vin, nm, d_ctr);
         HIPCHK(hipGetLastError());
       }
-      // the key bits that can differ: plane keys < G·R·R, and the ~0 of a
-      // refused message keeps all ones in those bits, so it still sorts last
-      int kbits = 1;
-      while (kbits < 32 &&
-             ((uint64_t)1 << kbits) <= (uint64_t)v.G * v.R * v.R)
-        ++kbits;
-      HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout,
-                                                (int)nm, 0, kbits, sm));
+      if (!spec_ok)
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin,
+                                                  vout, (int)nm, 0, kbits, sm));
       k_ing_place<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
           v, ds, dm, (const drb_entry *)st.ents.p, kout, vout, nm,
           (uint32_t)(e->round & 1), (uint32_t)e->round, d_ctr);
