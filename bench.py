@@ -26,6 +26,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 READS_PER_CTX = 9      # C3: 9 ReadIndex reads per write, one ctx per round
+# C2/C3: fresh-key write rounds before timing, so that every replica's
+# table holds (nearly) all of its group's KEY_SPACE keys -- load ~0.50 of
+# 512 slots (tests/test_gpu_fullsize.py pins the timed rounds at this fill)
+C3_KV_FILL = 1536
 KEY_SPACE = 256        # K = 256 keys per group
 
 
@@ -422,7 +426,7 @@ def main():
     # all resident in HBM before the timed region
     NP = max(8, args.steps)
     if args.kv_fill < 0:
-        args.kv_fill = 0 if (c4 or c5) else 1536
+        args.kv_fill = 0 if (c4 or c5) else C3_KV_FILL
     xch = None
     if c4:  # one global set of G groups spread over the world
         lanes = (G + world - 1) // world

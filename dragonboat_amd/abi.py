@@ -260,7 +260,16 @@ class WireIn(C.Structure):
     _fields_ = [("frames", C.c_uint64), ("messages", C.c_uint64),
                 ("accepted", C.c_uint64), ("dropped", C.c_uint64),
                 ("snapshots", C.c_uint64), ("consumed", C.c_uint64),
-                ("bad", C.c_uint64)]
+                ("bad", C.c_uint64), ("diverted", C.c_uint64)]
+
+
+class WireCpu(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("length", C.c_uint32),
+                ("fate", C.c_uint32)]
+
+
+# drb_ingest_fate
+ING_PLACED, ING_DROPPED, ING_DIVERTED, ING_SNAPSHOT = range(4)
 
 
 class RoundIn(C.Structure):

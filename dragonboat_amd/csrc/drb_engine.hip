@@ -91,12 +91,6 @@ struct drb_engine {
   // counter) and of region copies (host-side sum)
   unsigned long long *xpull_bytes = nullptr;
   uint64_t xcopy_bytes = 0;
-  // the leaders' served reads one thread per read (k_read_lanes) instead of
-  // inside the leader kernel; DRB_READ_LANES=0/1 in the environment
-  bool read_lanes = false;
-  // the follower kernel on stream2, concurrent with the leader kernel
-  // (DRB_ROLE_STREAMS=0/1 in the environment; measured 3 % slower at C3)
-  bool role_streams = false;
   // drb_plane_counts has read the plane summaries (xrows): the rounds clear
   // them from then on
   bool xrows_used = false;
@@ -273,8 +267,6 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->bytes = 0;
   e->scratch = nullptr;
   e->scratch_bytes = 0;
-  if (const char *rl = getenv("DRB_READ_LANES")) e->read_lanes = rl[0] == '1';
-  if (const char *rs = getenv("DRB_ROLE_STREAMS")) e->role_streams = rs[0] == '1';
   if (hipSetDevice(cfg->device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
           hipSuccess ||
@@ -1455,6 +1447,28 @@ extern "C" int drb_request_leader_transfer(drb_engine *e, uint32_t slot,
 }
 
 // ---------------------------------------------------------------- ingest
+// A receiver whose inbox cannot hold a message leaves the fast path before
+// its next round: DRB_F_FALLBACK with DRB_FB_CAPACITY, one flagged record
+// (the first marker only; several planes of one receiver may race here).
+// The message and the receiver's later ones go to the CPU path
+// (include/drb_engine.h, drb_ingest_ex).
+DRB_DEV void ing_flag_capacity(const View &v, uint64_t g, uint32_t slot,
+                               uint64_t round) {
+  const uint32_t old =
+      atomicOr(&v.u32[u32_ix(v, W_FLAGS, slot, g)], DRB_F_FALLBACK);
+  if (!(old & (DRB_F_FALLBACK | DRB_F_ERROR))) {
+    v.u32[u32_ix(v, W_FB_REASON, slot, g)] = DRB_FB_CAPACITY;
+    flag_log(v, g, slot, DRB_FB_CAPACITY, old | DRB_F_FALLBACK, round);
+  }
+}
+// recv[i] = group << 8 | slot
+__global__ void k_ing_flag(View v, const uint64_t *recv, uint64_t n,
+                           uint64_t round) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ing_flag_capacity(v, recv[i] >> 8, (uint32_t)(recv[i] & 0xffu),
+                               round);
+}
+
 // drb_ingest: the whole batch in a fixed number of device transfers.  The
 // host decides every message's fate from one gather of the replicas'
 // flags and one of the current (sender, receiver) headers; then the
@@ -1474,9 +1488,10 @@ struct InPlane {  // one (group, from, to) plane of this call
 };
 }  // namespace
 
-extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
-                          const drb_entry *ents, const uint8_t *pool,
-                          uint64_t *accepted, uint64_t *dropped) {
+extern "C" int drb_ingest_ex(drb_engine *e, const drb_message *msgs, size_t n,
+                             const drb_entry *ents, const uint8_t *pool,
+                             uint8_t *status, uint64_t *accepted,
+                             uint64_t *dropped, uint64_t *diverted) {
   if (!e || (n && !msgs)) return DRB_EINVAL;
   const View &v = e->v;
   std::lock_guard<std::mutex> lock(e->ingest_mu);
@@ -1484,24 +1499,29 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   if (v.remote_mask && e->exchanged_round != e->round) return DRB_EAGAIN;
   const uint32_t buf = (uint32_t)(e->round & 1);  // read by round+1
   const uint32_t tag = (uint32_t)e->round;
-  uint64_t acc = 0, drop = 0;
+  uint64_t acc = 0, drop = 0, div = 0;
+  // each message's fate (drb_ingest_fate); PLACED until decided otherwise
+  std::vector<uint8_t> fate(n, DRB_ING_PLACED);
   // 1. shape checks, then the hosted flags of every target and sender
-  std::vector<uint8_t> ok(n, 0);
   std::vector<uint64_t> fidx;
   fidx.reserve(2 * n);
   std::vector<uint64_t> lane(n, 0);  // the receiver's lane (ing_target)
   for (size_t i = 0; i < n; ++i) {
     const drb_message &m = msgs[i];
     uint64_t g = 0;
-    ok[i] = ing_target(v, m.shard_id, m.from, m.to, &g) &&
-            m.n_entries <= v.W;
-    if (!ok[i]) continue;
+    // (an unknown shard, a receiver of another rank: nodehost.go:2089-2098)
+    if (!ing_target(v, m.shard_id, m.from, m.to, &g)) {
+      fate[i] = DRB_ING_DROPPED;
+      continue;
+    }
     lane[i] = g;
     fidx.push_back(u32_ix(v, W_FLAGS, (uint32_t)(m.to - 1), g));
     fidx.push_back(u32_ix(v, W_FLAGS, (uint32_t)(m.from - 1), g));
   }
   std::vector<uint32_t> fl;
   if (gather(e, v.u32, fidx, fl)) return DRB_EDEVICE;
+  // receivers flagged in this call (group * R + slot)
+  std::unordered_map<uint64_t, uint8_t> flagged;
   // 2. the planes touched and their current headers
   std::unordered_map<uint64_t, uint32_t> pid;  // (g, from, to) -> plane
   std::vector<InPlane> planes;
@@ -1510,25 +1530,24 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   uint32_t last_plane = 0;
   size_t q = 0;
   for (size_t i = 0; i < n; ++i) {
-    if (!ok[i]) {
-      drop++;
-      continue;
-    }
+    if (fate[i] != DRB_ING_PLACED) continue;
     const drb_message &m = msgs[i];
     const uint32_t ft = fl[q++], ff = fl[q++];
-    const bool live = (ft & DRB_F_HOSTED) &&
-                      !(ft & (DRB_F_FALLBACK | DRB_F_ERROR));
     const uint32_t from = (uint32_t)(m.from - 1), to = (uint32_t)(m.to - 1);
+    const uint64_t g = lane[i];
     // (a sender slot on another rank: this lane's is another group)
     const bool from_hosted = !pair_remote(v, from, to) &&
                              (ff & DRB_F_HOSTED) &&
                              !(ff & (DRB_F_FALLBACK | DRB_F_ERROR));
-    if (!live || from_hosted) {  // the transport delivers remote senders only
-      drop++;
-      ok[i] = 0;
+    if (!(ft & DRB_F_HOSTED) || from_hosted) {
+      // the transport delivers remote senders to hosted replicas only
+      fate[i] = DRB_ING_DROPPED;
       continue;
     }
-    const uint64_t g = lane[i];
+    if (ft & (DRB_F_FALLBACK | DRB_F_ERROR)) {  // the CPU raft.Peer's
+      fate[i] = DRB_ING_DIVERTED;
+      continue;
+    }
     const uint64_t key = (g * v.R + from) * v.R + to;
     if (key == last_key) {  // a transport batch keeps a group's messages
       mplane[i] = last_plane;  // together
@@ -1586,36 +1605,57 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   std::vector<uint4> rval[2], eval[2], fwval;
   std::vector<uint4> ch(ENT_META + v.C16);
   for (size_t i = 0; i < n; ++i) {
-    if (!ok[i]) continue;
+    if (fate[i] != DRB_ING_PLACED) continue;
     const drb_message &m = msgs[i];
     InPlane &pl = planes[mplane[i]];
     uint4 &cur = pl.cur;
-    if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
-      cur.x |= MQ_QUIESCE;
-      acc++;
+    const uint64_t rk = pl.g * v.R + pl.to;
+    if (flagged.count(rk)) {  // the receiver left the fast path in this call
+      fate[i] = DRB_ING_DIVERTED;
       continue;
     }
-    if (mi_count(cur.y) >= v.MB) {  // MessageQueue full (message.go:105-123)
-      drop++;
+    // a GPU capacity: the receiver goes to the CPU path with this message
+    auto capacity = [&]() {
+      flagged.emplace(rk, 1);
+      fate[i] = DRB_ING_DIVERTED;
+    };
+    if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
+      cur.x |= MQ_QUIESCE;
+      continue;
+    }
+    if (mi_count(cur.y) >= v.MB) {  // the plane's records
+      capacity();
       continue;
     }
     const bool rep = m.type == DRB_MSG_REPLICATE;
     const int r = pl.remote ? 1 : 0;
     const uint32_t k = rep ? mi_nrep(cur.y)
                            : rec_pos(false, mi_noth(cur.y), v.MB);
+    bool fit = true;
+    for (uint64_t x = 0; fit && x < m.n_entries; ++x)
+      fit = ents[m.entries_off + x].cmd_len <= v.C16 * 16;
     if (m.type == DRB_MSG_PROPOSE) {
       // handleFollowerPropose's message from another NodeHost: its entries
       // go to the sender's forward rows, one Propose per plane and round
-      // (a second one, or one the rows cannot hold, is dropped as by a full
-      // queue; so is any without forward rows, drb_config.forward_proposals)
-      bool fit = v.fwd_props && !pl.remote && !(cur.y & MI_PROP) &&
-                 m.n_entries <= v.max_props;
-      for (uint64_t x = 0; fit && x < m.n_entries; ++x)
-        fit = ents[m.entries_off + x].cmd_len <= v.C16 * 16;
-      if (!fit) {
-        drop++;
-        continue;
-      }
+      // (drb_config.forward_proposals)
+      fit = fit && v.fwd_props && !pl.remote && !(cur.y & MI_PROP) &&
+            m.n_entries <= v.max_props;
+    }
+    if (rep && pl.remote && m.n_entries) {
+      // entry rows [elo, elo + E), elo set by the round's first Replicate
+      // that carries entries (0: none yet; a commit-only Replicate needs no
+      // rows)
+      const uint64_t elo = pl.elo ? pl.elo : m.log_index + 1;
+      fit = fit && m.log_index + 1 >= elo &&
+            m.log_index + m.n_entries - elo < v.E;
+      if (fit) pl.elo = elo;
+    }
+    if (rep && m.n_entries > v.W) fit = false;  // (the window rows)
+    if (!fit) {
+      capacity();
+      continue;
+    }
+    if (m.type == DRB_MSG_PROPOSE) {
       const uint32_t fw = fwd_ps(v, buf, pl.from);
       for (uint64_t x = 0; x < m.n_entries; ++x) {
         const drb_entry &en = ents[m.entries_off + x];
@@ -1634,24 +1674,11 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
         }
       }
     }
-    if (rep && pl.remote) {
-      // entry rows [elo, elo + E), elo set by the round's first Replicate
-      // that carries entries (0: none yet; a commit-only Replicate needs no
-      // rows): a Replicate outside them is dropped (the sender retries, as
-      // after any transport loss)
-      if (m.n_entries && pl.elo == 0) pl.elo = m.log_index + 1;
-      if (m.n_entries && (m.log_index + 1 < pl.elo ||
-                          m.log_index + m.n_entries - pl.elo >= v.E)) {
-        drop++;
-        continue;
-      }
-    }
     if (rep && m.n_entries) {
       // the entries travel in the sender's (unhosted) window slot, or in the
       // plane's entry rows when the plane is remote
       for (uint64_t x = 0; x < m.n_entries; ++x) {
         drb_entry en = ents[m.entries_off + x];
-        if (en.cmd_len > v.C16 * 16) return DRB_ERANGE;
         en.index = m.log_index + 1 + x;
         entry_to_chunks(v, en, pool, ch.data());
         for (uint32_t c = 0; c < ENT_META + v.C16; ++c) {
@@ -1710,7 +1737,11 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
       pl.maxapp = pl.maxapp_valid ? std::max(pl.maxapp, ma) : ma;
       pl.maxapp_valid = true;
     }
-    acc++;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    acc += fate[i] == DRB_ING_PLACED;
+    drop += fate[i] == DRB_ING_DROPPED;
+    div += fate[i] == DRB_ING_DIVERTED;
   }
   // 4. down: entries, records, headers, max-append, the round tag bytes
   std::vector<uint4> hval[2];
@@ -1759,154 +1790,37 @@ extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
   for (size_t w = 0; w < tidx.size(); ++w)
     tv[w] = (tv[w] & ~tmask[w]) | (tmask[w] & tbyte[w]);
   if (scatter(e, v.inbox_tag, tidx, tv)) return DRB_EDEVICE;
+  // 5. the receivers that left the fast path in this call
+  if (!flagged.empty()) {
+    std::vector<uint64_t> rv;
+    for (const auto &kv : flagged)
+      rv.push_back(((kv.first / v.R) << 8) | (kv.first % v.R));
+    uint64_t *d = nullptr;
+    void *sc = nullptr;
+    if (scratch(e, rv.size() * 8, &sc)) return DRB_EDEVICE;
+    d = (uint64_t *)sc;
+    HIPCHK(hipMemcpyAsync(d, rv.data(), rv.size() * 8, hipMemcpyHostToDevice,
+                          e->stream));
+    k_ing_flag<<<(unsigned)((rv.size() + 255) / 256), 256, 0, e->stream>>>(
+        e->v, d, rv.size(), e->round);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));  // (rv and the scratch)
+  }
+  if (status && n) memcpy(status, fate.data(), n);
   if (accepted) *accepted = acc;
   if (dropped) *dropped = drop;
+  if (diverted) *diverted = div;
   return DRB_OK;
 }
 
-// ---------------------------------------------------------------- step
-// The leader and follower kernels of a round touch disjoint state (each
-// reads round t-1's mailbox and writes round t's), so they may run
-// concurrently (DRB_ROLE_STREAMS=1: the follower kernel on a second
-// stream, forked from and joined back into the engine stream).  Measured
-// on MI355X at C3 that was 3 % slower than back-to-back launches, so the
-// default is one stream.
-#ifndef DRB_ROLE_STREAMS
-#define DRB_ROLE_STREAMS 0
-#endif
-// The leaders' served reads as their own launch on the second stream,
-// concurrent with the follower kernel (which serves its own replicas'
-// reads in-round); DRB_SERVE_SPLIT=0 (default) serves them inside the
-// leader kernel.  Measured at C3: the split ran 4.5 % slower -- the two
-// kernels compete for the same saturated memory system.
-#ifndef DRB_SERVE_SPLIT
-#define DRB_SERVE_SPLIT 0
-#endif
-__global__ __launch_bounds__(256) void k_serve_reads(const View v,
-                                                     uint32_t n_reads,
-                                                     uint32_t key_space,
-                                                     uint32_t slots);
-// The leaders' served reads as their own launch (drb_engine.read_lanes):
-// a workgroup takes 64 groups, one quad of lanes per group.  For each read
-// the quad's 4 lanes load the 4 slots of its home probe group -- one 64 B
-// line, one memory request per quad -- and resolve the probe order by
-// ballot (the first empty slot or match; a full group with no match
-// continues serially in the quad's first lane).  The n_reads lookups of a
-// ctx are all issued before any is resolved, and the results go out as
-// rows of consecutive groups.  Same results, checksums, served masks and
-// counters as serve_reads_lane.
-constexpr uint32_t READ_LANES_MAX = 16;  // n_reads
-constexpr uint32_t READ_QBATCH = 9;      // lookups in flight per lane
-__global__ __launch_bounds__(256) void k_read_lanes(const View v,
-                                                     uint32_t n_reads,
-                                                     uint32_t key_space,
-                                                     uint32_t slots,
-                                                     uint32_t role) {
-  __shared__ uint32_t cnt[2];
-  const uint32_t slot = (slots >> (4 * blockIdx.y)) & 0xfu;
-  const uint32_t q = threadIdx.x & 3u;
-  const uint64_t g = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
-  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const bool ok = g < v.G;
-  const uint32_t mask = v.KS - 1;
-  const bool ks_pow2 = (key_space & (key_space - 1)) == 0;
-  const bool quad = kv_spl(v) == 4 && v.KS >= 4;  // 16 B slots: a 64 B group
-  uint32_t nr = 0, smask = 0, served = 0, deferred = 0;
-  uint64_t sm = 0;
-  if (ok) {
-    nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
-    if (nr) {  // the applied index (k_serve_reads)
-      const uint4 c0 = v.pk[pk_ix(v, 0, slot, g)];
-      const uint4 c1 = v.pk[pk_ix(v, 1, slot, g)];
-      const uint64_t last = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
-      const uint32_t code = c1.z & 0xffffu;
-      sm = code == PK_ESC16 ? v.u64[u64_ix(v, F_SM_INDEX, slot, g)]
-                            : pk_idx_value(code, last, false);
-    }
-  }
-  const uint4 *tbl = v.kv + kv_ix(v, slot, ok ? g : 0, 0);
-  const uint32_t base = threadIdx.x & 63u & ~3u;  // the quad in its wave
-  uint64_t sum = 0;
-  for (uint32_t k = 0; k < nr; ++k) {  // (uniform within a quad)
-    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
-    if (lo64(c0) > sm) {  // pendingReadIndex: not applied yet
-      if (q == 0) deferred += n_reads;
-      continue;
-    }
-    smask |= 1u << k;
-    for (uint32_t j0 = 0; j0 < n_reads; j0 += READ_QBATCH) {
-    // (the keys are recomputed at resolution: registers for the loads)
-    auto key_of = [&](uint32_t j) {
-      const uint64_t x =
-          mix64(hi64(c0) ^ ((uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull));
-      return ks_pow2 ? (x & (key_space - 1)) : x % key_space;
-    };
-    uint4 h[READ_QBATCH];
-#pragma unroll
-    for (uint32_t t = 0; t < READ_QBATCH; ++t) {
-      const uint32_t j = j0 + t;
-      if (j >= n_reads) continue;
-      const uint32_t hm = (uint32_t)kv_hash(key_of(j), 8) & mask;
-      h[t] = quad ? tbl[(uint64_t)kv_probe(v, hm, q) * v.KVW]
-                  : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (uint32_t t = 0; t < READ_QBATCH; ++t) {
-      const uint32_t j = j0 + t;
-      if (j >= n_reads) continue;
-      const uint64_t key = key_of(j);
-      uint64_t w = ~0ull;
-      bool more = true;
-      if (quad) {
-        const bool empty = !kv_used(h[t]), hit = kv_match(h[t], key, 8);
-        const uint32_t e4 = (uint32_t)(__ballot(empty) >> base) & 15u,
-                       h4 = (uint32_t)(__ballot(hit) >> base) & 15u;
-        const uint32_t stop = e4 | h4;
-        const uint32_t first = stop ? (uint32_t)__builtin_ctz(stop) : 0u;
-        const uint64_t wf =
-            __shfl(kv_word(h[t]), (int)((threadIdx.x & ~3u) + first), 64);
-        if (stop) {
-          more = false;
-          if ((h4 >> first) & 1u) w = wf;
-        }
-      }
-      if (q == 0) {
-        if (more)  // a full first group (or another slot geometry)
-          w = kv_probe_word<true>(v, tbl, (uint32_t)kv_hash(key, 8) & mask,
-                                  quad ? 4u : 0u, key, 8, slot, g);
-        sum += mix64(w ^ key ^ ((uint64_t)j << 56));
-        served++;
-        if (v.read_res)
-          v.read_res[rres_ix(v, slot, k, j, g)] =
-              w == ~0ull ? make_uint2(0, 0)
-                         : make_uint2((uint32_t)w,
-                                      (uint32_t)(w >> 32) | 0x80000000u);
-      }
-    }
-    }
-  }
-  if (ok && nr && q == 0) {  // the lane's checksum and served mask
-    v.read_sum[ix(v, slot, g)] = sum;
-    if (v.read_res) v.read_served[ix(v, slot, g)] = smask;
-  }
-  served = wave_sum(served);
-  deferred = wave_sum(deferred);
-  if ((threadIdx.x & 63) == 0 && (served | deferred)) {
-    atomicAdd(&cnt[0], served);
-    atomicAdd(&cnt[1], deferred);
-  }
-  __syncthreads();
-  // the counters: any row of the role and slot (k_sum_counters adds them)
-  if (threadIdx.x < 2 && cnt[threadIdx.x]) {
-    const uint64_t gx = (v.G + 255) / 256;
-    const uint64_t row =
-        ((uint64_t)role * v.R + slot) * gx + (blockIdx.x / 4) % gx;
-    atomicAdd(&v.counters[row * NUM_COUNTERS + C_READS + threadIdx.x],
-              (unsigned long long)cnt[threadIdx.x]);
-  }
+extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
+                          const drb_entry *ents, const uint8_t *pool,
+                          uint64_t *accepted, uint64_t *dropped) {
+  return drb_ingest_ex(e, msgs, n, ents, pool, nullptr, accepted, dropped,
+                       nullptr);
 }
 
+// ---------------------------------------------------------------- step
 // Each role's launch covers only the slots where that role occurs (the
 // role map, refreshed after every host-side state change): in the steady
 // state the leader kernel's grid is one slot high, not R.
@@ -2049,29 +1963,15 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   uint32_t nl = 0, nf = 0;
   pl.slots = slot_list(e->role_slots[0], &nl);
   pf.slots = slot_list(e->role_slots[1], &nf);
-  // the two roles concurrently where their launches alone cannot fill the
-  // device (DRB_ROLE_STREAMS, or e->role_streams: small engines)
-  const bool rs = DRB_ROLE_STREAMS || e->role_streams;
-  hipStream_t sf = rs ? e->stream2 : e->stream;
-  if (rs) {
-    (void)hipEventRecord(e->ev_fork, e->stream);
-    (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
-  }
-  const bool split = DRB_SERVE_SPLIT && !rs && nl && p0.n_reads;
-  if (split) pl.n_reads = 0;
-  // the leaders' reads as one thread per read, behind the leader kernel
-  // (a follower's ReadyToReads come from its own forwarded ReadIndex, a
-  // round later and rarely: the follower kernel keeps serving them)
-  const bool rlanes = !split && e->read_lanes && nl && p0.n_reads &&
-                      p0.n_reads <= READ_LANES_MAX;
-  if (rlanes) pl.n_reads = 0;
   // the EXT instantiation only where its paths can run (drb_step.hpp)
   const bool ext =
       e->v.C16 > 4 || e->v.kv_ool || p0.encode_saves || e->v.quiesce ||
       e->v.kv_ovf_cap;
   pl.nrows = nl;
   pf.nrows = nf;
-  // one-dimensional grids, rows interleaved per XCD (block_pos)
+  // one-dimensional grids of the role's slot rows, row-major (block_pos);
+  // both launches back to back on the engine stream (they touch disjoint
+  // state; on two streams they measured 3 % slower at C3)
   const StepLaunchFn *launch = kStepLaunch[R - 1];
   // forwarded proposals and member kinds: the EXT kernels with the Propose
   // and nonVoting / witness paths
@@ -2079,24 +1979,7 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
   const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
   if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
-  if (rlanes)
-    k_read_lanes<<<dim3((unsigned)((e->v.G + 63) / 64), nl), 256, 0,
-                   e->stream>>>(e->v, p0.n_reads, p0.key_space, pl.slots, 0);
-  if (split) {
-    (void)hipEventRecord(e->ev_fork, e->stream);
-    (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
-    k_serve_reads<<<dim3(gx, nl), 256, 0, e->stream2>>>(
-        e->v, p0.n_reads, p0.key_space, pl.slots);
-  }
-  if (nf) launch[kf](e->v, pf, gx * nf, sf);
-  if (split) {
-    (void)hipEventRecord(e->ev_join, e->stream2);
-    (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
-  }
-  if (rs) {
-    (void)hipEventRecord(e->ev_join, e->stream2);
-    (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
-  }
+  if (nf) launch[kf](e->v, pf, gx * nf, e->stream);
   if (e->v.elections) {  // the replicas the two launches routed (F_SLOW)
     RoundParams ps = p0;
     ps.slots = 0;
@@ -2508,19 +2391,61 @@ extern "C" int drb_step_round(drb_engine *e, const drb_round_in *in,
 }
 
 // ---------------------------------------------------------------- outputs
+// entries [lo, hi] of a remote plane's entry rows (their first index elo),
+// as drb_export_log writes them
+static int export_entry_rows(drb_engine *e, uint32_t buf, uint64_t g,
+                             uint32_t from, uint32_t to, uint64_t elo,
+                             uint64_t lo, uint64_t hi, drb_entry *out,
+                             uint8_t *pool, size_t pool_cap) {
+  const View &v = e->v;
+  if (hi < lo) return DRB_OK;
+  if (lo < elo || hi - elo >= v.E) return DRB_ERANGE;
+  std::vector<uint64_t> idx;
+  for (uint64_t i = lo; i <= hi; ++i)
+    for (uint32_t c = 0; c < ENT_META + v.C16; ++c)
+      idx.push_back(embox_ix(v, buf, from, to, (uint32_t)(i - elo), c, g));
+  std::vector<uint4> val;
+  if (gather(e, v.embox_in, idx, val)) return DRB_EDEVICE;
+  size_t used = 0, k = 0;
+  for (uint64_t i = lo; i <= hi; ++i, ++k) {
+    const uint4 *c = &val[k * (ENT_META + v.C16)];
+    drb_entry &o = out[k];
+    o.term = lo64h(c[0]);
+    o.key = hi64h(c[0]);
+    o.client_id = lo64h(c[1]);
+    o.series_id = hi64h(c[1]);
+    o.responded_to = lo64h(c[2]);
+    o.type = c[2].z;
+    o.cmd_len = c[2].w;
+    o.index = i;
+    o.cmd_off = used;
+    if (o.cmd_len > v.C16 * 16 || used + o.cmd_len > pool_cap)
+      return DRB_ERANGE;
+    memcpy(pool + used, &c[ENT_META], o.cmd_len);
+    used += o.cmd_len;
+  }
+  return DRB_OK;
+}
+
+// the messages of one (sender, receiver) plane of mailbox buffer `buf`
+// whose header carries round tag `tag`; remote: the inbound copies of a
+// plane whose sender slot lives on another rank (C4 placement), entries in
+// the plane's entry rows
 static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
                        uint32_t from, uint32_t to, drb_message *out,
                        size_t cap, size_t *nm, drb_entry *ents, size_t ecap,
                        size_t *ne, uint8_t *pool, size_t pcap, size_t *np,
-                       uint4 meta) {
+                       uint4 meta, uint64_t tag, bool remote = false) {
   const View &v = e->v;
-  const bool cur = tag_is(meta.x, e->round);
+  const bool cur = tag_is(meta.x, tag);
+  uint4 *const mbox = remote ? v.mbox_in : v.mbox;
+  uint64_t *const rterm = remote ? v.rterm_in : v.rterm;
   const uint32_t k = cur ? mi_count(meta.y) : 0;
   if (cur && (meta.x & MQ_QUIESCE)) {  // sendEnterQuiesceMessages
     if (*nm >= cap) return DRB_ERANGE;
     drb_message &m = out[(*nm)++];
     memset(&m, 0, sizeof(m));
-    m.shard_id = v.first_shard_id + gid(v, from, g);
+    m.shard_id = v.first_shard_id + gid(v, remote ? to : from, g);
     m.from = from + 1;
     m.to = to + 1;
     m.type = DRB_MSG_QUIESCE;
@@ -2537,21 +2462,27 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
     for (uint32_t c = 0; c < MSG_CHUNKS; ++c)
       idx.push_back(mbox_ix(v, buf, from, to, pos[q], c, g));
   std::vector<uint4> val;
-  if (gather(e, v.mbox, idx, val)) return DRB_EDEVICE;
+  if (gather(e, mbox, idx, val)) return DRB_EDEVICE;
+  uint64_t elo = 0;  // remote: the entry rows' first index
+  if (remote && mi_nrep(meta.y)) {
+    std::vector<uint64_t> li{mmeta_ix(v, buf, from, to, g)}, lv;
+    if (gather(e, v.elo_in, li, lv)) return DRB_EDEVICE;
+    elo = lv[0];
+  }
   uint64_t prev_lo = 0, prev_hi = 0;
   for (uint32_t q = 0; q < k; ++q) {
     if (*nm >= cap) return DRB_ERANGE;
     const uint4 *c = &val[q * MSG_CHUNKS];
     uint64_t rt = q_hi(meta);
-    if ((c[0].x & MF_TERM_OTHER) && v.rterm) {  // elections: its own term
+    if ((c[0].x & MF_TERM_OTHER) && rterm) {  // its own term
       std::vector<uint64_t> ti{rterm_ix(v, buf, from, to, pos[q], g)}, tv;
-      if (gather(e, v.rterm, ti, tv)) return DRB_EDEVICE;
+      if (gather(e, rterm, ti, tv)) return DRB_EDEVICE;
       rt = tv[0];
     }
     Msg mm = msg_decode(c[0], c[1], rt, prev_lo, prev_hi);
     drb_message &m = out[(*nm)++];
     memset(&m, 0, sizeof(m));
-    m.shard_id = v.first_shard_id + gid(v, from, g);
+    m.shard_id = v.first_shard_id + gid(v, remote ? to : from, g);
     m.from = from + 1;
     m.to = to + 1;
     m.type = mm.type;
@@ -2568,8 +2499,12 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
     if (m.type == DRB_MSG_REPLICATE && ne_) {
       if (*ne + ne_ > ecap) return DRB_ERANGE;
       size_t used = 0;
-      int rc = drb_export_log(e, g, from, m.log_index + 1, m.log_index + ne_,
-                              ents + *ne, pool + *np, pcap - *np);
+      int rc = remote ? export_entry_rows(e, buf, g, from, to, elo,
+                                          m.log_index + 1, m.log_index + ne_,
+                                          ents + *ne, pool + *np, pcap - *np)
+                      : drb_export_log(e, g, from, m.log_index + 1,
+                                       m.log_index + ne_, ents + *ne,
+                                       pool + *np, pcap - *np);
       if (rc) return rc;
       const bool wt = (v.wt_mask >> to) & 1u;
       for (uint64_t q2 = 0; q2 < ne_; ++q2) {
@@ -2643,7 +2578,37 @@ extern "C" int drb_export_outbox(drb_engine *e, uint64_t group,
     for (uint32_t to = 0; to < v.R; ++to) {
       if (to == from_slot) continue;
       int rc = export_pair(e, buf, group, from_slot, to, out, cap, &nm, ents,
-                           ent_cap, &ne, pool, pool_cap, &np, meta[to]);
+                           ent_cap, &ne, pool, pool_cap, &np, meta[to],
+                           e->round);
+      if (rc) return rc;
+    }
+  }
+  if (n_msgs) *n_msgs = nm;
+  return DRB_OK;
+}
+
+extern "C" int drb_export_inbox(drb_engine *e, uint64_t group, uint32_t slot,
+                                int last_round, drb_message *out, size_t cap,
+                                drb_entry *ents, size_t ent_cap, uint8_t *pool,
+                                size_t pool_cap, size_t *n_msgs) {
+  if (!e || group >= e->cfg.num_groups || slot >= e->cfg.num_replicas)
+    return DRB_ERANGE;
+  const View &v = e->v;
+  size_t nm = 0, ne = 0, np = 0;
+  // the inbox round t + 1 takes is buffer t & 1 with tag t (what round t
+  // sent and what was ingested since); the one round t took, t - 1
+  const uint64_t tag = last_round ? e->round - 1 : e->round;
+  if (!(last_round && e->round == 0)) {
+    const uint32_t buf = (uint32_t)(tag & 1);
+    for (uint32_t from = 0; from < v.R; ++from) {
+      if (from == slot) continue;
+      const bool rm = pair_remote(v, from, slot);
+      std::vector<uint64_t> mi{mmeta_ix(v, buf, from, slot, group)};
+      std::vector<uint4> meta;
+      if (gather(e, rm ? v.meta_in : v.mbox_meta, mi, meta))
+        return DRB_EDEVICE;
+      int rc = export_pair(e, buf, group, from, slot, out, cap, &nm, ents,
+                           ent_cap, &ne, pool, pool_cap, &np, meta[0], tag, rm);
       if (rc) return rc;
     }
   }

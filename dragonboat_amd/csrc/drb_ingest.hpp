@@ -44,34 +44,13 @@ struct DecMsg {
 };
 constexpr uint32_t ING_OK = 0, ING_BAD = 1, ING_SNAPSHOT = 2, ING_BIG = 3;
 
-// A lane's byte cursor over the uploaded stream.  WIN: the aligned 16 B
-// block holding the last byte read stays in registers, one load per 16
-// bytes instead of a dependent load per byte (the stream's device buffer is
-// padded past its last frame, al256(walked + 16), so a block that holds a
-// message's last byte is inside it) -- measured 2-4 % slower than the plain
-// per-byte loads, which hit the L1; DRB_INGEST_WINDOW=1 selects it.
-template <bool WIN = true>
+// A lane's byte cursor over the uploaded stream: one load per byte, which
+// hit the L1 (a 16 B register window measured 2-4 % slower on the C3
+// plane, profiles/r04_ingest)
 struct Bytes {
   const uint8_t *p;
-  uintptr_t wa = ~(uintptr_t)0;
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   __device__ explicit Bytes(const uint8_t *d) : p(d) {}
-  __device__ inline uint32_t operator[](uint64_t i) {
-    if (!WIN) return p[i];  // a load per byte (the default)
-    const uintptr_t a = (uintptr_t)(p + i);
-    const uintptr_t b = a & ~(uintptr_t)15;
-    if (b != wa) {
-      const uint4 x = *(const uint4 *)b;
-      w0 = x.x;
-      w1 = x.y;
-      w2 = x.z;
-      w3 = x.w;
-      wa = b;
-    }
-    const uint32_t o = (uint32_t)(a & 15);
-    const uint32_t dw = o < 8 ? (o < 4 ? w0 : w1) : (o < 12 ? w2 : w3);
-    return (dw >> ((o & 3) * 8)) & 0xffu;
-  }
+  __device__ inline uint32_t operator[](uint64_t i) const { return p[i]; }
 };
 
 // (every index below is from the message's first byte; d_entry's from the
@@ -191,12 +170,11 @@ __constant__ uint8_t c_empty_snapshot[24] = {
 
 // Message.Unmarshal (raft_optimized.go:659-983).  ents == nullptr: count
 // the entries only.  Returns ING_*; *big when a Cmd exceeds cmd_cap.
-template <bool WIN>
 __device__ inline uint32_t d_message(const uint8_t *msg, uint32_t n,
                                      DecMsg &m, drb_entry *ents,
                                      uint64_t base, uint32_t cmd_cap,
                                      bool &big) {
-  Bytes<WIN> d(msg);
+  Bytes d(msg);
   m.shard = m.from = m.to = m.term = m.log_term = m.log_index = m.commit = 0;
   m.hint = m.hint_high = 0;
   m.type = m.reject = m.n_ent = 0;
@@ -300,10 +278,11 @@ __global__ __launch_bounds__(256) void k_crc_chunks(const uint8_t *data,
   if (threadIdx.x == 0) fraw[b] = red[0] ^ red[1] ^ red[2] ^ red[3];
 }
 
-// The upload as a pull (DRB_INGEST_ZC=1, a pinned source only): the device
-// reads the mapped host stream over PCIe with 16 B loads, four in flight a
-// lane, instead of a copy-engine DMA.  dst and src share their alignment
-// mod 16 (the caller checks), n bytes.
+// A pull over PCIe from mapped pinned host memory: 16 B loads, four in
+// flight a lane.  dst and src share their alignment mod 16 (the caller
+// checks), n bytes.  (drb_ingest_wire pulls the frames' element steps this
+// way; the stream itself goes up by DMA, which measured ~56 GB/s against
+// the pull's ~45 and leaves the CUs free)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_zc_pull(uint8_t *dst,
                                                  const uint8_t *src,
@@ -333,7 +312,6 @@ __global__ __launch_bounds__(256) void k_zc_pull(uint8_t *dst,
 // pass 1: entry counts and errors, and the record of every message (the
 // decode pass parses again only the messages with entries); the frame of a
 // malformed message is marked (the host stops the stream there)
-template <bool WIN>
 __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
                             const uint32_t *mlen, const uint32_t *mframe,
                             uint32_t *n_ent, uint32_t *err,
@@ -343,7 +321,7 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   if (i >= n) return;
   DecMsg m;
   bool big = false;
-  uint32_t r = d_message<WIN>(s + moff[i], mlen[i], m, nullptr, 0, cmd_cap, big);
+  uint32_t r = d_message(s + moff[i], mlen[i], m, nullptr, 0, cmd_cap, big);
   if (r == ING_OK && big) r = ING_BIG;
   n_ent[i] = r == ING_OK ? m.n_ent : 0;
   err[i] = r;
@@ -351,7 +329,6 @@ __global__ void k_ing_count(const uint8_t *s, const uint64_t *moff,
   m.ent0 = 0;
   out[i] = m;
   if (r == ING_BAD) atomicOr(&frame_bad[mframe[i]], 1u);
-  if (r == ING_BIG) atomicOr(&frame_bad[mframe[i]], 2u);
 }
 
 // the steps as they went up: 2 B each when every step fits (the common
@@ -421,20 +398,22 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
     r = err[i];
     ne = n_ent[i];
   }
-  const bool dl = st == 1 && r == ING_OK;
+  // (a message with a Cmd over cmd_cap is delivered undecoded: its
+  // placement diverts it to the CPU path, ING_BIG)
+  const bool dl = st == 1 && (r == ING_OK || r == ING_BIG);
   if (i < n) {
-    nsc[i] = dl ? ne : 0u;
+    nsc[i] = dl && r == ING_OK ? ne : 0u;
     deliver[i] = dl ? 1 : 0;
     if (!dl)
       dm[i].err = ING_BAD;  // not delivered: sorts last
     else if (restore)       // after a speculation that did not hold
-      dm[i].err = ING_OK;
+      dm[i].err = r;
   }
   const bool snap = st != 0 && r == ING_SNAPSHOT;
   const bool msg = st == 1 && r != ING_SNAPSHOT;
   const bool filt = st == 2 && r != ING_SNAPSHOT;
   const uint64_t b0 = __ballot(snap), b1 = __ballot(msg), b2 = __ballot(filt);
-  uint32_t e = dl ? ne : 0u;
+  uint32_t e = dl && r == ING_OK ? ne : 0u;
   for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o);
   // per workgroup, then one of ING_TALLY_ROWS counter rows (64 B apart):
   // ~25k workgroups adding to one line serialised at its L2 channel
@@ -455,7 +434,6 @@ __global__ void k_ing_tally(const uint32_t *mframe, const uint8_t *fstate,
 
 // pass 2: the entries of the messages to deliver (their records are pass
 // 1's); a message not delivered is marked so that it sorts last
-template <bool WIN>
 __global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
                              const uint32_t *mlen, const uint32_t *ent0,
                              const uint32_t *n_ent, DecMsg *out,
@@ -473,7 +451,7 @@ __global__ void k_ing_decode(const uint8_t *s, const uint64_t *moff,
   }
   DecMsg m;
   bool big = false;
-  m.err = d_message<WIN>(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
+  m.err = d_message(s + moff[i], mlen[i], m, ents + ent0[i], moff[i],
                     cmd_cap, big);
   m.ent0 = ent0[i];
   out[i] = m;
@@ -488,8 +466,9 @@ __global__ void k_ing_carry(uint32_t *ent0, const uint32_t *nsc, uint64_t m0,
   ent0[i] += ent0[m0 - 1] + nsc[m0 - 1];
 }
 
-// plane keys (group, sender slot, receiver slot); messages drb_ingest would
-// refuse on their shape, or not delivered, sort last (~0)
+// plane keys (group, sender slot, receiver slot); messages for a shard or
+// replica this engine does not host (dropped, nodehost.go:2089-2098), or not
+// delivered, sort last (~0)
 __global__ void k_ing_keys(const View v, const DecMsg *dm, uint32_t *key,
                            uint32_t *val, uint64_t n,
                            unsigned long long *ctr, uint64_t i0 = 0) {
@@ -497,10 +476,9 @@ __global__ void k_ing_keys(const View v, const DecMsg *dm, uint32_t *key,
   if (i >= n) return;
   const DecMsg m = dm[i];
   uint32_t k = ~0u;
-  if (m.err == ING_OK) {
+  if (m.err == ING_OK || m.err == ING_BIG) {
     uint64_t g;
-    bool ok = ing_target(v, m.shard, m.from, m.to, &g) && m.n_ent <= v.W;
-    if (ok)
+    if (ing_target(v, m.shard, m.from, m.to, &g))
       k = (uint32_t)((g * v.R + (m.from - 1)) * v.R + (m.to - 1));
     else
       atomicAdd(&ctr[1], 1ull);  // dropped
@@ -509,12 +487,44 @@ __global__ void k_ing_keys(const View v, const DecMsg *dm, uint32_t *key,
   val[i] = (uint32_t)i;
 }
 
+// the CPU path's messages of a drb_ingest_wire call (drb_wire_cpu), in no
+// particular order (the host sorts them by offset)
+DRB_DEV void ing_cpu_push(drb_wire_cpu *cpu, unsigned long long *cpu_n,
+                          uint64_t cap, uint64_t off, uint32_t len,
+                          uint32_t fate) {
+  const unsigned long long q = atomicAdd(cpu_n, 1ull);
+  if (q < cap) {
+    cpu[q].offset = off;
+    cpu[q].length = len;
+    cpu[q].fate = fate;
+  }
+}
+
+// the InstallSnapshot messages of the delivered frames (the CPU path's)
+__global__ void k_ing_snaps(const uint32_t *mframe, const uint8_t *fstate,
+                            const uint32_t *err, const uint64_t *moff,
+                            const uint32_t *mlen, uint64_t n,
+                            drb_wire_cpu *cpu, unsigned long long *cpu_n,
+                            uint64_t cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && err[i] == ING_SNAPSHOT && fstate[mframe[i]] == 1)
+    ing_cpu_push(cpu, cpu_n, cap, moff[i], mlen[i], DRB_ING_SNAPSHOT);
+}
+
 // one lane per plane (the head of a run of equal keys): MessageQueue.Add of
-// its messages in stream order (drb_engine.hip drb_ingest, restated)
+// its messages in stream order (drb_engine.hip drb_ingest_ex, restated): a
+// message the plane cannot hold -- its records, a second Propose or one the
+// forward rows cannot take, a Replicate beyond a remote plane's entry rows
+// or the window, a Cmd over cmd_cap -- sends the receiver to the CPU path
+// (ing_flag_capacity) with it and the plane's later messages; a receiver
+// already off the fast path takes none (the CPU raft.Peer's)
 __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
                             const drb_entry *ents, const uint32_t *key,
                             const uint32_t *idx, uint64_t n, uint32_t buf,
-                            uint32_t tag, unsigned long long *ctr) {
+                            uint32_t tag, unsigned long long *ctr,
+                            const uint64_t *moff, const uint32_t *mlen,
+                            drb_wire_cpu *cpu, unsigned long long *cpu_n,
+                            uint64_t cpu_cap, uint64_t round) {
   const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i0 >= n) return;
   const uint32_t k = key[i0];
@@ -530,16 +540,20 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
   uint4 *const mmeta = rm ? v.meta_in : v.mbox_meta;
   uint64_t *const mmax = rm ? v.maxapp_in : v.mbox_maxapp;
   uint64_t *const rterm = rm ? v.rterm_in : v.rterm;
+  unsigned long long *row = ctr + (blockIdx.x % ING_TALLY_ROWS) * 8;
   const uint32_t ft = v.u32[u32_ix(v, W_FLAGS, to, g)];
-  const bool live = (ft & DRB_F_HOSTED) && !(ft & (DRB_F_FALLBACK | DRB_F_ERROR));
   // (co-resident senders step here; another rank's lane holds another group)
   const uint32_t ff = rm ? 0u : v.u32[u32_ix(v, W_FLAGS, from, g)];
   const bool from_hosted =
       (ff & DRB_F_HOSTED) && !(ff & (DRB_F_FALLBACK | DRB_F_ERROR));
-  if (!live || from_hosted) {  // the transport delivers remote senders only
-    atomicAdd(&ctr[1], (unsigned long long)(i1 - i0));
+  if (!(ft & DRB_F_HOSTED) || from_hosted) {
+    // the transport delivers remote senders to hosted replicas only
+    atomicAdd(&row[1], (unsigned long long)(i1 - i0));
     return;
   }
+  // a receiver off the fast path: every message is the CPU path's
+  bool div = (ft & (DRB_F_FALLBACK | DRB_F_ERROR)) != 0;
+  const bool was_off = div;
   uint4 cur = mmeta[mmeta_ix(v, buf, from, to, g)];
   uint64_t maxapp = mmax[mmeta_ix(v, buf, from, to, g)];
   if (!tag_is(cur.x, tag)) {  // nothing there yet this round
@@ -550,34 +564,45 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
   // the round's first Replicate with entries placed here; 0: none yet)
   uint64_t elo = maxapp_valid && rm ? v.elo_in[mmeta_ix(v, buf, from, to, g)]
                                     : 0;
-  uint64_t acc = 0, drop = 0;
+  uint64_t acc = 0, ndiv = 0;
   for (uint64_t j = i0; j < i1; ++j) {
-    const DecMsg m = dm[idx[j]];
-    if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
-      cur.x |= MQ_QUIESCE;
-      acc++;
-      continue;
-    }
-    if (mi_count(cur.y) >= v.MB) {  // MessageQueue full (message.go:105-123)
-      drop++;
-      continue;
-    }
+    const uint32_t mi = idx[j];
+    const DecMsg m = dm[mi];
     const bool rep = m.type == DRB_MSG_REPLICATE;
+    if (!div) {
+      if (m.type == DRB_MSG_QUIESCE) {  // node-level: a header bit
+        cur.x |= MQ_QUIESCE;
+        acc++;
+        continue;
+      }
+      bool fit = m.err == ING_OK && mi_count(cur.y) < v.MB;
+      if (fit && m.type == DRB_MSG_PROPOSE) {
+        // handleFollowerPropose's message from another NodeHost: its
+        // entries go to the sender's forward rows, one Propose per plane and
+        // round (drb_config.forward_proposals)
+        fit = v.fwd_props && !rm && !(cur.y & MI_PROP) &&
+              m.n_ent <= v.max_props;
+        for (uint32_t x = 0; fit && x < m.n_ent; ++x)
+          fit = ents[m.ent0 + x].cmd_len <= v.C16 * 16;
+      }
+      if (fit && rep && m.n_ent > v.W) fit = false;  // (the window rows)
+      if (fit && rep && rm && m.n_ent) {
+        // entry rows [elo, elo + E), elo set by the round's first
+        // Replicate that carries entries (a commit-only one needs none)
+        const uint64_t e0 = elo ? elo : m.log_index + 1;
+        fit = m.log_index + 1 >= e0 && m.log_index + m.n_ent - e0 < v.E;
+        if (fit) elo = e0;
+      }
+      div = !fit;
+    }
+    if (div) {  // the CPU path's, in stream order after what was placed
+      ing_cpu_push(cpu, cpu_n, cpu_cap, moff[mi], mlen[mi], DRB_ING_DIVERTED);
+      ndiv++;
+      continue;
+    }
     const uint32_t kk =
         rep ? mi_nrep(cur.y) : rec_pos(false, mi_noth(cur.y), v.MB);
     if (m.type == DRB_MSG_PROPOSE) {
-      // handleFollowerPropose's message from another NodeHost: its entries
-      // go to the sender's forward rows, one Propose per plane and round
-      // (a second one, or one the rows cannot hold, is dropped as by a full
-      // queue; so is any without forward rows, drb_config.forward_proposals)
-      bool fit = v.fwd_props && !rm && !(cur.y & MI_PROP) &&
-                 m.n_ent <= v.max_props;
-      for (uint32_t x = 0; fit && x < m.n_ent; ++x)
-        fit = ents[m.ent0 + x].cmd_len <= v.C16 * 16;
-      if (!fit) {
-        drop++;
-        continue;
-      }
       const uint32_t fw = fwd_ps(v, buf, from);
       for (uint32_t x = 0; x < m.n_ent; ++x) {
         const drb_entry en = ents[m.ent0 + x];
@@ -598,18 +623,6 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
           v.props[prop_ix(v, fw, x, PROP_META + cc, g)] =
               make_uint4(w[0], w[1], w[2], w[3]);
         }
-      }
-    }
-    if (rep && rm) {
-      // entry rows [elo, elo + E), elo set by the round's first Replicate
-      // that carries entries (0: none yet; a commit-only Replicate needs no
-      // rows): a Replicate outside them is dropped (the sender retries, as
-      // after any transport loss)
-      if (m.n_ent && elo == 0) elo = m.log_index + 1;
-      if (m.n_ent && (m.log_index + 1 < elo ||
-                      m.log_index + m.n_ent - elo >= v.E)) {
-        drop++;
-        continue;
       }
     }
     if (rep && m.n_ent) {
@@ -689,16 +702,18 @@ __global__ void k_ing_place(const View v, const uint8_t *s, const DecMsg *dm,
     }
     acc++;
   }
-  mmeta[mmeta_ix(v, buf, from, to, g)] = cur;
-  mmax[mmeta_ix(v, buf, from, to, g)] = maxapp;
-  if (rm && maxapp_valid) v.elo_in[mmeta_ix(v, buf, from, to, g)] = elo;
-  if (!rm && (mi_count(cur.y) || (cur.x & MQ_QUIESCE)))  // its tag byte
-    ((uint8_t *)&v.inbox_tag[((uint64_t)buf * v.R + to) * v.G + g])[from] =
-        tag_byte(tag, cur.y);
+  if (acc) {
+    mmeta[mmeta_ix(v, buf, from, to, g)] = cur;
+    mmax[mmeta_ix(v, buf, from, to, g)] = maxapp;
+    if (rm && maxapp_valid) v.elo_in[mmeta_ix(v, buf, from, to, g)] = elo;
+    if (!rm && (mi_count(cur.y) || (cur.x & MQ_QUIESCE)))  // its tag byte
+      ((uint8_t *)&v.inbox_tag[((uint64_t)buf * v.R + to) * v.G + g])[from] =
+          tag_byte(tag, cur.y);
+  }
+  if (ndiv && !was_off) ing_flag_capacity(v, g, to, round);
   // (a lane per plane: the adds spread over the counter rows)
-  unsigned long long *row = ctr + (blockIdx.x % ING_TALLY_ROWS) * 8;
   if (acc) atomicAdd(&row[0], (unsigned long long)acc);
-  if (drop) atomicAdd(&row[1], (unsigned long long)drop);
+  if (ndiv) atomicAdd(&row[6], (unsigned long long)ndiv);
 }
 
 }  // namespace drb
@@ -872,7 +887,9 @@ static int ing_grow(IngestBuf &b, size_t need) {
   return DRB_OK;
 }
 struct IngestState {
-  IngestBuf stream, msgs, ents, sort, misc, chunks;
+  IngestBuf stream, msgs, ents, sort, misc, chunks, cpu;
+  // the CPU path's messages of the last call, in stream order
+  std::vector<drb_wire_cpu> cpu_msgs;
   bool k64_ready = false;     // c_crc_k64 uploaded
   uint8_t *pinned = nullptr;  // drb_ingest_buffer (hipHostMalloc)
   size_t pinned_cap = 0;
@@ -884,22 +901,19 @@ struct IngestState {
   std::vector<wirehost::Frame> frames;
   // the stream goes up in pieces on its own stream, one event each, so the
   // CRC and count kernels of a piece run while the later pieces upload
-  hipStream_t up = nullptr, crc = nullptr, up2 = nullptr;
-  std::vector<hipEvent_t> ev, evc;  // per piece: CRC'd, uploaded
+  hipStream_t up = nullptr;
+  std::vector<hipEvent_t> ev;  // per piece: uploaded
   hipEvent_t evv = nullptr;  // the verdicts' inputs are down (speculation)
 };
 static void ingest_free(IngestState *st) {
   if (!st) return;
   for (hipEvent_t x : st->ev) (void)hipEventDestroy(x);
-  for (hipEvent_t x : st->evc) (void)hipEventDestroy(x);
   if (st->evv) (void)hipEventDestroy(st->evv);
   if (st->up) (void)hipStreamDestroy(st->up);
-  if (st->up2) (void)hipStreamDestroy(st->up2);
-  if (st->crc) (void)hipStreamDestroy(st->crc);
   if (st->pinned) (void)hipHostFree(st->pinned);
   if (st->steps) (void)hipHostFree(st->steps);
   for (IngestBuf *b : {&st->stream, &st->msgs, &st->ents, &st->sort,
-                       &st->misc, &st->chunks})
+                       &st->misc, &st->chunks, &st->cpu})
     if (b->p) (void)hipFree(b->p);
   delete st;
 }
@@ -981,6 +995,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   const View &v = e->v;
   drb_wire_in res;
   memset(&res, 0, sizeof(res));
+  st.cpu_msgs.clear();
   IngestTrace tr(e->stream);
   // 1. frames: magic + requestHeader + its CRC (tcp.go:64-112, 180-237)
   std::vector<wirehost::Frame> &fr = st.frames;
@@ -1030,8 +1045,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     IngestState *st;
     ~SyncOnReturn() {
       if (st->up) (void)hipStreamSynchronize(st->up);
-      if (st->up2) (void)hipStreamSynchronize(st->up2);
-      if (st->crc) (void)hipStreamSynchronize(st->crc);
       (void)hipStreamSynchronize(s);
     }
   } sync_on_return{e->stream, &st};
@@ -1075,14 +1088,9 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   uint32_t *d_clen = (uint32_t *)((uint8_t *)st.chunks.p + al256(nc * 8 + 8));
   uint32_t *d_ccrc = (uint32_t *)((uint8_t *)d_clen + al256(nc * 4 + 4));
   // pieces: runs of whole frames of at least ING_PIECE bytes
-  // (DRB_INGEST_PIECE_MB overrides it for the A/B)
-  static const size_t piece = [] {
-    const char *m = getenv("DRB_INGEST_PIECE_MB");
-    return m && atoi(m) > 0 ? (size_t)atoi(m) << 20 : ING_PIECE;
-  }();
   std::vector<size_t> pf;  // first frame of each piece, then nf
   for (size_t f = 0, acc = 0; f < fr.size(); ++f) {
-    if (pf.empty() || acc >= piece) {
+    if (pf.empty() || acc >= ING_PIECE) {
       pf.push_back(f);
       acc = 0;
     }
@@ -1093,64 +1101,24 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   if (!st.up &&
       hipStreamCreateWithFlags(&st.up, hipStreamNonBlocking) != hipSuccess)
     return DRB_EDEVICE;
-  if (!st.up2 &&
-      hipStreamCreateWithFlags(&st.up2, hipStreamNonBlocking) != hipSuccess)
-    return DRB_EDEVICE;
-  // the pieces alternate between two upload streams (DRB_INGEST_STREAMS=2:
-  // two copy engines at once) or go through one
-  static const int nup = [] {
-    const char *m = getenv("DRB_INGEST_STREAMS");
-    return m && atoi(m) == 2 ? 2 : 1;
-  }();
-  if (!st.crc &&
-      hipStreamCreateWithFlags(&st.crc, hipStreamNonBlocking) != hipSuccess)
-    return DRB_EDEVICE;
   while (st.ev.size() < (np ? np : 1)) {  // (ev[0] also for the start)
-    hipEvent_t x, y;
-    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&y, hipEventDisableTiming) != hipSuccess)
+    hipEvent_t x;
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
       return DRB_EDEVICE;
     st.ev.push_back(x);
-    st.evc.push_back(y);
   }
-  // the upload and CRC streams start behind what the engine stream has
-  // enqueued (the device buffers may still be read by an earlier call)
+  // the upload starts behind what the engine stream has enqueued (the
+  // device buffers may still be read by an earlier call)
   HIPCHK(hipEventRecord(st.ev[0], sm));
   HIPCHK(hipStreamWaitEvent(st.up, st.ev[0], 0));
-  HIPCHK(hipStreamWaitEvent(st.up2, st.ev[0], 0));
-  HIPCHK(hipStreamWaitEvent(st.crc, st.ev[0], 0));
-  // where the payload CRCs run (DRB_INGEST_MODE, measured in DESIGN §10):
-  // 0 on the engine stream per piece after the Requests scans, 1 on a
-  // stream of their own as each piece lands, 2 on the engine stream as each
-  // piece lands
-  static const int mode = [] {
-    const char *m = getenv("DRB_INGEST_MODE");
-    return m ? atoi(m) : 0;
-  }();
-  hipStream_t cs = mode == 1 ? st.crc : sm;
-  // the parse passes' byte reads: one load a byte (default), or through a
-  // lane's 16 B window (DRB_INGEST_WINDOW=1; measured 2-4 % slower on the
-  // C3 plane, profiles/r04_ingest: the per-byte loads hit the L1)
-  const char *bw = getenv("DRB_INGEST_WINDOW");
-  const bool bytewise = !(bw && bw[0] == '1');
-  // the pull upload (k_zc_pull) when asked for and the stream is pinned,
-  // mapped host memory aligned as the device buffer is
-  const uint8_t *hsrc = nullptr;
-  if (const char *z = getenv("DRB_INGEST_ZC"); z && z[0] == '1' && len) {
-    hipPointerAttribute_t pa;
-    if (hipPointerGetAttributes(&pa, stream) == hipSuccess &&
-        pa.type == hipMemoryTypeHost && pa.devicePointer && pa.hostPointer &&
-        ((uintptr_t)stream & 15) == 0)
-      hsrc = (const uint8_t *)pa.devicePointer +
-             (stream - (const uint8_t *)pa.hostPointer);
-    if ((uintptr_t)hsrc & 15) hsrc = nullptr;
-    (void)hipGetLastError();  // (a pageable stream: not an error here)
-  }
+  // (the payload CRCs run on the engine stream per piece, after its bytes
+  // landed; on a stream of their own as each piece lands they measured no
+  // faster)
   if (nc) {
     HIPCHK(hipMemcpyAsync(d_coff, coff.data(), nc * 8, hipMemcpyHostToDevice,
-                          cs));
+                          sm));
     HIPCHK(hipMemcpyAsync(d_clen, clen.data(), nc * 4, hipMemcpyHostToDevice,
-                          cs));
+                          sm));
   }
   {
     hipError_t up_err = hipSuccess;
@@ -1160,31 +1128,10 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         const size_t a = q ? fr[pf[q]].off - 20 : 0;
         const size_t b = pf[q + 1] < fr.size() ? fr[pf[q + 1]].off - 20
                                                 : walked;
-        hipStream_t us = nup == 2 && (q & 1) ? st.up2 : st.up;
-        if (b > a && hsrc) {
-          const uint64_t nv = (b - a) / 16 + 1;
-          const unsigned nb = (unsigned)std::min<uint64_t>(
-              4096, (nv + 1023) / 1024);
-          k_zc_pull<<<nb, 256, 0, us>>>(ds + a, hsrc + a, b - a);
-          up_err = hipGetLastError();
-        } else if (b > a) {
+        if (b > a)
           up_err = hipMemcpyAsync(ds + a, stream + a, b - a,
-                                  hipMemcpyHostToDevice, us);
-        }
-        if (mode == 0) {  // the piece is up
-          if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], us);
-          continue;
-        }
-        // the piece's payload CRCs as it lands
-        if (up_err == hipSuccess) up_err = hipEventRecord(st.evc[q], us);
-        if (up_err == hipSuccess) up_err = hipStreamWaitEvent(cs, st.evc[q], 0);
-        const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
-        if (up_err == hipSuccess && c1 > c0) {
-          k_crc_chunks<<<c1 - c0, 256, 0, cs>>>(ds, d_coff + c0, d_clen + c0,
-                                               d_ccrc + c0);
-          up_err = hipGetLastError();
-        }
-        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], cs);
+                                  hipMemcpyHostToDevice, st.up);
+        if (up_err == hipSuccess) up_err = hipEventRecord(st.ev[q], st.up);
       }
     });
     const size_t nt = std::min<size_t>(16, fr.size());
@@ -1294,11 +1241,8 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     // pulled by a kernel from the mapped pinned buffer, not DMA'd: a copy
     // queued here waits on the copy engine behind the stream's remaining
     // pieces, and the per-piece counts below need it (profiles/r04_ingest)
-    // (DRB_INGEST_STEPS_DMA=1: the DMA, for the A/B)
     void *hsteps = nullptr;
-    const char *sd = getenv("DRB_INGEST_STEPS_DMA");
-    if (!(sd && sd[0] == '1') &&
-        hipHostGetDevicePointer(&hsteps, st.steps, 0) == hipSuccess &&
+    if (hipHostGetDevicePointer(&hsteps, st.steps, 0) == hipSuccess &&
         hsteps && ((uintptr_t)hsteps & 15) == 0) {
       const uint64_t nv = step_bytes / 16 + 1;
       k_zc_pull<<<(unsigned)std::min<uint64_t>(1024, (nv + 1023) / 1024), 256,
@@ -1352,9 +1296,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // beside the upload of the rest, into the entry buffer as the last call
   // left it; a speculation that does not hold (or an entry buffer too
   // small) is redone after the verdicts, as without it.
-  // (DRB_INGEST_SPEC=0: off, for the A/B)
-  const char *spe = getenv("DRB_INGEST_SPEC");
-  const bool spec = nm && !(spe && spe[0] == '0');
+  const bool spec = nm != 0;
   std::vector<uint8_t> fspec(nf + 1, 0);
   const uint64_t ecap = st.ents.cap / sizeof(drb_entry);
   if (spec) {
@@ -1367,9 +1309,9 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // per piece, once its bytes are up (and CRC'd): its messages' element
   // boundaries and counts
   for (size_t q = 0; q < np; ++q) {
-    if (mode != 2) HIPCHK(hipStreamWaitEvent(sm, st.ev[q], 0));
+    HIPCHK(hipStreamWaitEvent(sm, st.ev[q], 0));
     const uint32_t c0 = cfirst[pf[q]], c1 = cfirst[pf[q + 1]];
-    if (mode == 0 && c1 > c0)
+    if (c1 > c0)
       k_crc_chunks<<<c1 - c0, 256, 0, sm>>>(ds, d_coff + c0, d_clen + c0,
                                             d_ccrc + c0);
     const uint64_t m0 = mbase[pf[q]], m1 = mbase[pf[q + 1]];
@@ -1377,7 +1319,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
       const unsigned gb = (unsigned)((m1 - m0 + 255) / 256);
       k_ing_elems<<<gb, 256, 0, sm>>>(ds, d_scan, d_mbase, d_foff, d_mframe,
                                       d_moff, d_mlen, m1, m0);
-      (bytewise ? k_ing_count<false> : k_ing_count<true>)<<<gb, 256, 0, sm>>>(
+      k_ing_count<<<gb, 256, 0, sm>>>(
           ds, d_moff, d_mlen, d_mframe, d_nent, d_err, d_fbad, dm, m1,
           cmd_cap, m0);
       if (spec) {
@@ -1388,8 +1330,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                                 d_ent0 + m0, (int)(m1 - m0),
                                                 sm));
         k_ing_carry<<<gb, 256, 0, sm>>>(d_ent0, d_nsc, m0, m1);
-        (bytewise ? k_ing_decode<false> : k_ing_decode<true>)<<<gb, 256, 0,
-                                                                sm>>>(
+        k_ing_decode<<<gb, 256, 0, sm>>>(
             ds, d_moff, d_mlen, d_ent0, d_nsc, dm, (drb_entry *)st.ents.p, m1,
             cmd_cap, ecap, d_ctr, m0);
         k_ing_keys<<<gb, 256, 0, sm>>>(v, dm, kin, vin, m1, d_ctr, m0);
@@ -1428,7 +1369,6 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
   // does not decode (ErrBadMessage closes the connection, tcp.go:528-530)
   std::vector<uint8_t> fstate(nf + 1, 0);
   size_t consumed = 0;
-  bool big = false;
   bool any_deliver = false;
   {
     size_t mi = 0;
@@ -1453,14 +1393,12 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
         continue;
       }
       const bool keep = fr[f].did == deployment_id && fr[f].bv == 210;
-      if (keep && (fbad[f] & 2u)) big = true;
       fstate[f] = keep ? 1 : 2;
       any_deliver |= keep && nmf;
       mi += nmf;
     }
   }
   if (bad_header && !res.bad) res.bad = 1;
-  if (big) return DRB_ERANGE;  // a Cmd the window rows cannot hold
   res.consumed = consumed;
   bool spec_ok = spec && fstate == fspec;
   if (spec_ok) {
@@ -1492,12 +1430,20 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
     res.messages = c0[3];
     res.dropped += c0[4];
     const uint64_t tot = c0[5];
+    // the CPU path's messages: InstallSnapshots, and what placement diverts
+    if (ing_grow(st.cpu, al256(8) + nm * sizeof(drb_wire_cpu)))
+      return DRB_EDEVICE;
+    unsigned long long *d_cpu_n = (unsigned long long *)st.cpu.p;
+    drb_wire_cpu *d_cpu = (drb_wire_cpu *)((uint8_t *)st.cpu.p + al256(8));
+    HIPCHK(hipMemsetAsync(d_cpu_n, 0, 8, sm));
+    if (c0[2])
+      k_ing_snaps<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+          d_mframe, d_fstate, d_err, d_moff, d_mlen, nm, d_cpu, d_cpu_n, nm);
     if (any_deliver) {
       if (!spec_ok) {
         const size_t eb = al256((tot ? tot : 1) * sizeof(drb_entry));
         if (ing_grow(st.ents, eb)) return DRB_EDEVICE;
-        (bytewise ? k_ing_decode<false> : k_ing_decode<true>)<<<
-            (unsigned)((nm + 255) / 256), 256, 0, sm>>>(
+        k_ing_decode<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
             ds, d_moff, d_mlen, d_ent0, d_nsc, dm, (drb_entry *)st.ents.p, nm,
             cmd_cap, st.ents.cap / sizeof(drb_entry), d_ctr, 0);
         HIPCHK(hipGetLastError());
@@ -1512,18 +1458,45 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                                   vout, (int)nm, 0, kbits, sm));
       k_ing_place<<<(unsigned)((nm + 255) / 256), 256, 0, sm>>>(
           v, ds, dm, (const drb_entry *)st.ents.p, kout, vout, nm,
-          (uint32_t)(e->round & 1), (uint32_t)e->round, d_ctr);
+          (uint32_t)(e->round & 1), (uint32_t)e->round, d_ctr, d_moff,
+          d_mlen, d_cpu, d_cpu_n, nm, e->round);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(rows, d_ctr, sizeof(rows), hipMemcpyDeviceToHost,
                             sm));
-      HIPCHK(hipStreamSynchronize(sm));
+    }
+    unsigned long long ncpu = 0;
+    HIPCHK(hipMemcpyAsync(&ncpu, d_cpu_n, 8, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipStreamSynchronize(sm));
+    if (any_deliver)
       for (uint32_t q = 0; q < ING_TALLY_ROWS; ++q) {
         res.accepted += rows[q * 8];
         res.dropped += rows[q * 8 + 1];
+        res.diverted += rows[q * 8 + 6];
       }
+    if (ncpu) {
+      st.cpu_msgs.resize(std::min<uint64_t>(ncpu, nm));
+      HIPCHK(hipMemcpyAsync(st.cpu_msgs.data(), d_cpu,
+                            st.cpu_msgs.size() * sizeof(drb_wire_cpu),
+                            hipMemcpyDeviceToHost, sm));
+      HIPCHK(hipStreamSynchronize(sm));
+      std::sort(st.cpu_msgs.begin(), st.cpu_msgs.end(),
+                [](const drb_wire_cpu &a, const drb_wire_cpu &b) {
+                  return a.offset < b.offset;
+                });
     }
   }
   tr.mark("place");
   if (out) *out = res;
+  return DRB_OK;
+}
+
+extern "C" int drb_ingest_wire_cpu(drb_engine *e, drb_wire_cpu *out,
+                                   size_t cap, size_t *n_out) {
+  if (!e || (cap && !out)) return DRB_EINVAL;
+  std::lock_guard<std::mutex> lock(e->ingest_mu);
+  const size_t n = e->ingest ? e->ingest->cpu_msgs.size() : 0;
+  if (n_out) *n_out = n;
+  if (n > cap) return DRB_ERANGE;
+  if (n) memcpy(out, e->ingest->cpu_msgs.data(), n * sizeof(drb_wire_cpu));
   return DRB_OK;
 }

@@ -51,8 +51,6 @@ namespace drb {
 #ifndef DRB_FOLLOW_WAVES
 #define DRB_FOLLOW_WAVES 4
 #endif
-// timing experiments only (tools/variants.sh), never in a shipped build:
-// bit 0 skips the KV apply, bit 1 the in-round served reads
 // KV slots loaded per probe step (apply upserts, lookups past the first two).
 // Measured at C3 (same box): W=1 1.016, 2 1.033, 4 1.063, 8 1.240 ms/round,
 // and kv_slots 1024 no faster than 512: the probe chains are not what the
@@ -77,39 +75,18 @@ namespace drb {
 #ifndef DRB_FPF
 #define DRB_FPF 8
 #endif
-// the leader's: the first DRB_LPF records of its first sender with records
-// (LDS: DRB_LPF x 4 KB a workgroup; 0: off, measured neutral, profiles/r03_lpf)
-#ifndef DRB_LPF
-#define DRB_LPF 0
-#endif
+// (the leader's first records the same way measured neutral or slower,
+// profiles/r03_lpf: the leader prefetches nothing)
 #ifndef DRB_QS_DIRTY
 #define DRB_QS_DIRTY 1
 #endif
 #ifndef DRB_REM_DIRTY
 #define DRB_REM_DIRTY 1
 #endif
-#ifndef DRB_ABLATE
-#define DRB_ABLATE 0
-#endif
-// served-read results stored nontemporally (1) or plainly (0)
-#ifndef DRB_NT_RESULTS
-#define DRB_NT_RESULTS 0
-#endif
-// the leader's served reads before its state store (1) or after the outbox
-// headers (0): measured 0.3-0.8 % faster at C3 (profiles/r04_reads)
-#ifndef DRB_READS_EARLY
-#define DRB_READS_EARLY 1
-#endif
 // timing only: per-phase cycle sums of the leader / follower lanes
 // (View.phase, drb_debug_phase); 0 in shipped builds
 #ifndef DRB_PHASE_PROF
 #define DRB_PHASE_PROF 0
-#endif
-// interleave a launch's slot rows per XCD (block_pos); 0: row-major.
-// Measured (profiles/r01_pair_xcd, r01_c4_pair): neutral at C3, 7 % slower
-// at C4 N=1 (four follower rows), so off by default
-#ifndef DRB_PAIR_XCD
-#define DRB_PAIR_XCD 0
 #endif
 
 constexpr uint64_t MAX_ENTRY_SIZE = 64ull * 1024 * 1024;  // soft.go:186
@@ -223,6 +200,7 @@ DRB_DEV uint64_t &rq_hi(const Lane &L, int d) {
 }
 DRB_DEV uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 DRB_DEV uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+DRB_DEV uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 
 template <int R>
@@ -1817,12 +1795,6 @@ DRB_DEV int apply_entry(const Lane &L, Rep<R> &r, uint64_t index) {
       (!EXT || voff + 4 <= 64 ? cmd_u32_at(cmd, voff)
                               : value_chunk(L, index, voff, vlen, 0, 0).x) &
       byte_mask(vlen);
-  if (DRB_ABLATE & 4) {  // timing only: parse, no table access
-    r.sm_index = index;
-    r.sm_term = term;
-    r.applied_any = true;
-    return (int)(w0 & 1) | 1;
-  }
   // open-addressing upsert into this replica's table: DRB_PROBE_W slots
   // are loaded per step (one memory round trip), then resolved in order
   const uint32_t home = (uint32_t)kv_hash(key8, klen) & (v.KS - 1);
@@ -2116,12 +2088,8 @@ DRB_DEV void serve_reads_lane(const View &v, uint32_t slot, uint64_t g,
                                ((uint64_t)((uint32_t)(w >> 32) | 0x80000000u)
                                 << 32);
           uint64_t *dst = (uint64_t *)&v.read_res[rres_ix(v, slot, k, j, g)];
-          // the client results are read by the host, not by a later round:
-          // DRB_NT_RESULTS stores them past the caches
-          if (DRB_NT_RESULTS)
-            __builtin_nontemporal_store(rv, dst);
-          else
-            *dst = rv;
+          // (stored nontemporally they measured the same, profiles/r04_reads)
+          *dst = rv;
         }
       }
     }
@@ -2340,14 +2308,11 @@ DRB_DEV bool idle_round(const View &v, const RoundParams &p, uint32_t slot,
   return true;
 }
 
-// The logical (x = group block, y = slot row) of this workgroup.  The
-// launch is one-dimensional, gx * nrows workgroups, and the dispatcher
-// deals consecutive workgroups round-robin over the 8 XCDs.  With gx a
-// multiple of 8 the rows are interleaved in runs of 8: workgroups 8k..8k+7
-// of a run of 8 * nrows are group blocks 8c..8c+7 of row k, so the R - 1
-// follower replicas of one group block land on the same XCD (same L2)
-// back to back and share the leader's window rows and mailbox lines there
-// (MI355X_MICROARCH.md: one L2 per XCD).  Otherwise rows are row-major.
+// The logical (x = group block, y = slot row) of this workgroup: the launch
+// is one-dimensional, gx * nrows workgroups, row-major.  (Rows interleaved
+// in runs of 8, so that a group block's follower replicas share an XCD's
+// L2, measured neutral at C3 and 7 % slower at C4 N = 1:
+// profiles/r01_pair_xcd, r01_c4_pair.)
 struct BlockPos {
   uint32_t x, y, gx;
 };
@@ -2356,14 +2321,8 @@ DRB_DEV BlockPos block_pos(const RoundParams &p) {
   const uint32_t b = blockIdx.x, gx = gridDim.x / n;
   BlockPos bp;
   bp.gx = gx;
-  if (DRB_PAIR_XCD && n > 1 && (gx & 7u) == 0) {
-    const uint32_t run = b / (8u * n), w = b % (8u * n);
-    bp.y = w >> 3;
-    bp.x = run * 8u + (w & 7u);
-  } else {
-    bp.y = b / gx;
-    bp.x = b % gx;
-  }
+  bp.y = b / gx;
+  bp.x = b % gx;
   return bp;
 }
 
@@ -2497,7 +2456,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   // wave-uniform, and the row a lane's first sender with records lands in
   // is uniform only while there is one row (the first such sender differs
   // between lanes)
-  constexpr int PFN = SLOW ? 0 : LEAD ? DRB_LPF : DRB_FPF;
+  constexpr int PFN = SLOW || LEAD ? 0 : DRB_FPF;
   constexpr bool FPF = PFN > 0;
   constexpr int PFS = 1;
   // the LDS row of a prefetch goes through M0 (wave-uniform): one sender
@@ -2638,7 +2597,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     uint32_t total_in = 0, n_ri_msgs = 0, n_rr = 0, resp_from = 0;
     uint32_t rej_from = 0;  // senders with a rejecting ReplicateResp
     uint32_t qz_from = 0;   // senders whose Quiesce message arrived
-    uint64_t nri_packed = 0;  // 5-bit ReadIndex record count per sender
+    // leader: 5-bit count per sender s of the sends back to s that its own
+    // records and queued requests can cause (the mailbox bound below)
+    uint64_t own_packed = 0;
     uint64_t max_app = 0;
     uint32_t prop_from = 0;     // senders with a Propose (MI_PROP)
     uint64_t nprop_packed = 0;  // 4-bit forwarded entry count per sender
@@ -2716,9 +2677,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
             fb == DRB_FB_NONE)
           fb = DRB_FB_TERM_MISMATCH;
       }
-      n_ri_msgs += (info >> MI_NRI) & 0x1fu;
-      nri_packed |= (uint64_t)((info >> MI_NRI) & 0x1fu) << (5 * s);
-      n_rr += (info >> MI_NRR) & 0x1fu;
+      const uint32_t nri_s = (info >> MI_NRI) & 0x1fu;
+      const uint32_t nrr_s = (info >> MI_NRR) & 0x1fu;
+      n_ri_msgs += nri_s;
+      n_rr += nrr_s;
+      if (LEAD && is_leader) {
+        // the sends to s that s's records cause (raft.go:1878-1923,
+        // 1955-1974): a ReadIndexResp per request of s released (queued or
+        // new), one answer per HeartbeatResp (and, in the raft launch, per
+        // record of another type), and per ReplicateResp a resend only
+        // while s is paused -- an accepted answer from Wait resends once and
+        // leaves s in Replicate, where only a commit broadcast (counted for
+        // every follower below) sends to it; s is paused again only after a
+        // reject or a HeartbeatResp (remote.go:103-213)
+        const uint32_t hb_s = ns - nri_s - nrr_s - ((info & MI_PROP) ? 1u : 0u);
+        const uint32_t w0 =
+            rem_get<R>(L, s).st != DRB_REMOTE_REPLICATE ? 1u : 0u;
+        const uint32_t rr = (info & MI_REJECT) ? nrr_s : umin32(nrr_s, w0 + hb_s);
+        uint32_t riq = 0;
+#pragma unroll
+        for (int d = 0; d < DRB_RI_DEPTH; ++d)
+          riq += ((uint32_t)d < r.ri_count && r.ri_fr[d] == (uint32_t)s + 1u)
+                     ? 1u : 0u;
+        own_packed |= (uint64_t)umin32(riq + nri_s + hb_s + rr, 31u) << (5 * s);
+      }
       if (info & MI_RESP) resp_from |= 1u << s;
       if (info & MI_PROP) {
         prop_from |= 1u << s;
@@ -2870,26 +2852,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
               fb = DRB_FB_CAPACITY;
           }
       }
-      // mailbox: messages the round can send to each follower s.  Each
-      // message from s triggers at most one send back to s (resend,
-      // retry, raft.go:1878-1923); a broadcast to everyone needs a commit
-      // advance (raft.go:1885), so there are at most min(#ReplicateResp,
-      // last - committed) of them; plus the ReadIndex / tick heartbeats,
-      // the proposal broadcast and ReadIndexResps of queued requests.
+      // mailbox: messages the round can send to each follower s: the
+      // broadcasts every follower gets -- the tick's heartbeat, one
+      // heartbeat per ReadIndex (staged or from any follower), one
+      // Replicate per proposal batch and per Propose, and one per commit
+      // advance (raft.go:1885: at most min(#ReplicateResp, last -
+      // committed), an answer only acknowledges entries the round began
+      // with) -- plus what s's own records cause (own_packed, above).
+      // tools/mailbox_bound.py checks it against the oracle's sends.
       {
         uint64_t adv = r.last > r.committed ? r.last - r.committed : 0;
         uint32_t nb = (uint32_t)umin64((uint64_t)n_rr, adv);
         uint32_t base = (in_lo != 0) + (p.tick ? 1 : 0) + (nprops ? 1 : 0) +
-                        __builtin_popcount(prop_from) + n_ri_msgs * 2 +
-                        r.ri_count + nb + (SLOW ? 1 : 0);
+                        __builtin_popcount(prop_from) + n_ri_msgs + nb +
+                        (SLOW ? 1 : 0);
 #pragma unroll
         for (int s = 0; s < R; ++s) {
           if ((uint32_t)s == slot) continue;
-          // a ReadIndex from s is answered by the broadcast and the
-          // release counted in base, not by a send of its own
-          const uint32_t ns = (uint32_t)((nin_packed >> (5 * s)) & 31u);
-          uint32_t bound = base + ns -
-                           (uint32_t)((nri_packed >> (5 * s)) & 31u);
+          uint32_t bound = base + (uint32_t)((own_packed >> (5 * s)) & 31u);
           // a transfer: one TimeoutNow from the ReplicateResps (it needs
           // match == lastIndex after a successful tryUpdate, and match only
           // grows while lastIndex stands: raft.go:1883-1895), plus a
@@ -3257,14 +3237,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       if (apply_hi >= apply_lo && apply_lo != 0) {
         uint64_t from = umax64(apply_lo, r.sm_index + 1);
         for (uint64_t idx = from; idx <= apply_hi; ++idx) {
-          int rc;
-          if (DRB_ABLATE & 1) {  // timing only: no state machine access
-            r.sm_index = idx;
-            r.applied_any = true;
-            rc = 1;
-          } else {
-            rc = apply_entry<R, EXT>(L, r, idx);
-          }
+          const int rc = apply_entry<R, EXT>(L, r, idx);
           if (rc < 0) {
             // the rsm apply of this replica leaves the fast path at idx;
             // the raft round itself completed: (sm_index, pushed_index]
@@ -3301,9 +3274,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         }
         last_final = r.last;
       }
-      // DRB_READS_EARLY: the served reads issued before the state store and
-      // the outbox headers (their loads then overlap those stores)
-      if (DRB_READS_EARLY && LEAD && p.n_reads && !(DRB_ABLATE & 2))
+      // the leader's served reads issued before the state store and the
+      // outbox headers, their loads overlapping those stores (0.3-0.8 %
+      // faster at C3 than after them, profiles/r04_reads)
+      if (LEAD && p.n_reads)
         serve_reads_lane<EXT>(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
                               p.key_space, c_served, c_deferred);
       sent_c1 = r.c1mask;
@@ -3384,7 +3358,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     if (p.encode_saves && c_saved == 0) v.save_len[ix(v, slot, g)] = 0;
     DRB_PH(6);  // state store + outbox headers
     // ReadLocalNode of the released reads, against the state just applied
-    if ((!DRB_READS_EARLY || !LEAD) && p.n_reads && !(DRB_ABLATE & 2))
+    if (!LEAD && p.n_reads)
       serve_reads_lane<EXT>(v, slot, g, r.nrtr, r.sm_index, p.n_reads,
                        p.key_space, c_served, c_deferred);
     DRB_PH(7);  // served reads

@@ -9,7 +9,8 @@ import os
 
 from . import abi
 from .abi import (ApplyResult, Config, Entry, Flagged, Message, ReadyToRead, Region, ReplicaState,
-                  RoundIn, RoundOut, WireCfg, WireIn, WireOut, entry_to_tuple,
+                  RoundIn, RoundOut, WireCfg, WireCpu, WireIn, WireOut,
+                  entry_to_tuple,
                   message_to_tuple)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -61,6 +62,13 @@ SIGNATURES = {
     "drb_request_leader_transfer": (C.c_int, [P, U32, PU32, PU64]),
     "drb_ingest": (C.c_int, [P, C.POINTER(Message), SZ, C.POINTER(Entry),
                              PU8, PU64, PU64]),
+    "drb_ingest_ex": (C.c_int, [P, C.POINTER(Message), SZ, C.POINTER(Entry),
+                                PU8, PU8, PU64, PU64, PU64]),
+    "drb_export_inbox": (C.c_int, [P, U64, U32, C.c_int, C.POINTER(Message),
+                                   SZ, C.POINTER(Entry), SZ, PU8, SZ,
+                                   C.POINTER(SZ)]),
+    "drb_ingest_wire_cpu": (C.c_int, [P, C.POINTER(WireCpu), SZ,
+                                      C.POINTER(SZ)]),
     "drb_step_round": (C.c_int, [P, C.POINTER(RoundIn),
                                  C.POINTER(RoundOut)]),
     "drb_step_round_async": (C.c_int, [P, C.POINTER(RoundIn)]),
@@ -324,6 +332,16 @@ class Engine:
                              C.byref(drop)), "drb_ingest")
         return acc.value, drop.value
 
+    def ingest_ex(self, marr, n, earr, pool):
+        """drb_ingest_ex: counts and each message's fate (abi.ING_*)."""
+        acc, drop, div = U64(), U64(), U64()
+        st = (C.c_uint8 * max(1, n))()
+        _ck(lib().drb_ingest_ex(self.h, marr, n, earr, pool, st,
+                                C.byref(acc), C.byref(drop), C.byref(div)),
+            "drb_ingest_ex")
+        return {"accepted": acc.value, "dropped": drop.value,
+                "diverted": div.value, "status": list(st[:n])}
+
     # ---------------------------------------------------------- round
     def step(self, tick=False, prop_slot=abi.DRB_NONE, ri_slot=abi.DRB_NONE,
              reads_per_ctx=0, key_space=0, encode_saves=False, ri_replica=0,
@@ -404,6 +422,19 @@ class Engine:
         _ck(lib().drb_export_outbox(self.h, g, slot, marr, cap, earr, ecap,
                                     pool, pcap, C.byref(n)),
             "drb_export_outbox")
+        return [message_to_tuple(marr[i], earr, pool) for i in range(n.value)]
+
+    def export_inbox(self, g, slot, last_round=False):
+        """drb_export_inbox: the messages in (g, slot)'s inbound planes."""
+        cap, ecap = 32 * self.R, 32 * self.R * self.cfg["window"]
+        pcap = ecap * self.cfg["cmd_cap"] + 16
+        marr = (Message * cap)()
+        earr = (Entry * ecap)()
+        pool = (C.c_uint8 * pcap)()
+        n = SZ()
+        _ck(lib().drb_export_inbox(self.h, g, slot, int(bool(last_round)),
+                                   marr, cap, earr, ecap, pool, pcap,
+                                   C.byref(n)), "drb_export_inbox")
         return [message_to_tuple(marr[i], earr, pool) for i in range(n.value)]
 
     def export_ready(self, g, slot):
@@ -661,6 +692,19 @@ class Engine:
         _ck(lib().drb_ingest_wire(self.h, buf, len(data), deployment_id,
                                   C.byref(res)), "drb_ingest_wire")
         return {f: getattr(res, f) for f, _ in WireIn._fields_}
+
+    def ingest_wire_cpu(self):
+        """drb_ingest_wire_cpu: [(offset, length, fate)] of the last
+        drb_ingest_wire stream's CPU-path messages, in stream order."""
+        n = SZ()
+        rc = lib().drb_ingest_wire_cpu(self.h, None, 0, C.byref(n))
+        if rc not in (abi.DRB_OK, abi.DRB_ERANGE):
+            _ck(rc, "drb_ingest_wire_cpu")
+        arr = (WireCpu * max(1, n.value))()
+        _ck(lib().drb_ingest_wire_cpu(self.h, arr, n.value, C.byref(n)),
+            "drb_ingest_wire_cpu")
+        return [(arr[i].offset, arr[i].length, arr[i].fate)
+                for i in range(n.value)]
 
     def ingest_buffer(self, data):
         """Copies data into the engine's pinned receive buffer

@@ -606,18 +606,68 @@ int drb_request_leader_transfer(drb_engine *e, uint32_t slot,
 /* Inbound boundary: IMessageHandler.HandleMessageBatch
  * (internal/transport/transport.go:86-91, nodehost.go:2072-2122).  Places
  * messages from replicas NOT hosted by this engine into the inbox of the
- * next round.  Messages for unknown shards / unhosted targets, or beyond
- * the mailbox capacity, are dropped (nodehost.go:2112-2114).  With
- * placement (place_world > 1) shard_id names the global group: a message
- * reaches the rank that hosts its receiver ((group + slot) mod N, lane
- * group / N), others are dropped; a sender slot that belongs to another
- * rank is written into the inbound planes, its Replicates' entries into the
- * plane's entry_mbox rows (a Replicate beyond them is dropped: the sender
- * retries).  Call it after the round's plane exchange.  The same holds for
- * drb_ingest_wire. */
+ * next round.
+ *
+ * The reference drops an incoming message only when the receiving node's
+ * MessageQueue already holds ReceiveQueueLength = 1024 messages
+ * (internal/server/message.go:105-120 MessageQueue.Add, settings/soft.go:202,
+ * nodehost.go:2112-2114), and a message for a shard or replica this
+ * NodeHost does not host (nodehost.go:2089-2098).  Here, every message is
+ * one of:
+ *   DRB_ING_PLACED    in the receiver's GPU inbox of the next round;
+ *   DRB_ING_DROPPED   the reference drops it too: an unknown shard, a
+ *                     receiver this engine does not host (with placement:
+ *                     not on this rank), a sender this engine hosts (the
+ *                     transport delivers remote senders only);
+ *   DRB_ING_DIVERTED  the GPU inbox cannot hold it, or its receiver is off
+ *                     the fast path: the message goes to the CPU raft.Peer
+ *                     of its receiver, whose MessageQueue.Add applies the
+ *                     1024 rule.  A GPU capacity -- a (sender, receiver)
+ *                     plane's `mailbox` records, a second Propose of one
+ *                     sender in a round or one the forward rows cannot
+ *                     hold, a Replicate beyond a remote plane's entry_mbox
+ *                     rows, a Cmd longer than cmd_cap -- marks the receiver
+ *                     DRB_F_FALLBACK with DRB_FB_CAPACITY (listed by
+ *                     drb_take_flagged with the engine's current round),
+ *                     and that message and every later one for the
+ *                     receiver in the call are diverted.  The receiver's
+ *                     CPU inbox is then drb_export_inbox(.., 0, ..) (what
+ *                     was placed before, each sender's in order) followed
+ *                     by the diverted messages, in call order.
+ * With placement (place_world > 1) shard_id names the global group: a
+ * message reaches the rank that hosts its receiver ((group + slot) mod N,
+ * lane group / N); a sender slot that belongs to another rank is written
+ * into the inbound planes, its Replicates' entries into the plane's
+ * entry_mbox rows.  Call it after the round's plane exchange.  The same
+ * holds for drb_ingest_wire. */
+enum drb_ingest_fate {
+  DRB_ING_PLACED = 0,
+  DRB_ING_DROPPED = 1,
+  DRB_ING_DIVERTED = 2,
+  DRB_ING_SNAPSHOT = 3  /* drb_ingest_wire: an InstallSnapshot (CPU path) */
+};
+/* status (may be NULL): n bytes, each message's drb_ingest_fate */
+int drb_ingest_ex(drb_engine *e, const drb_message *msgs, size_t n,
+                  const drb_entry *ents, const uint8_t *pool, uint8_t *status,
+                  uint64_t *accepted, uint64_t *dropped, uint64_t *diverted);
+/* drb_ingest_ex without the per-message status and the diverted count */
 int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                const drb_entry *ents, const uint8_t *pool, uint64_t *accepted,
                uint64_t *dropped);
+/* The messages in replica slot `slot` of `group`'s inbound planes:
+ * last_round == 0, the inbox the next round would take (the last round's
+ * co-resident sends and what was ingested since); last_round == 1, the one
+ * the last round took -- which a replica that round marked DRB_F_FALLBACK
+ * left unprocessed (valid until the next round).  Per sender in its send
+ * order (Replicates first, as the reference sends them), senders by slot;
+ * a Quiesce is a message of its own (node.go:993-1005); Replicate entries
+ * and Propose entries with their Cmd bytes in pool.  Hands a replica that
+ * leaves the fast path its pending messages for the CPU raft.Peer
+ * (node.stepNode's MessageQueue, node.go:1139-1159). */
+int drb_export_inbox(drb_engine *e, uint64_t group, uint32_t slot,
+                     int last_round, drb_message *out, size_t cap,
+                     drb_entry *ents, size_t ent_cap, uint8_t *pool,
+                     size_t pool_cap, size_t *n_msgs);
 
 /* --- the step round ---------------------------------------------------- */
 
@@ -1091,7 +1141,17 @@ typedef struct drb_wire_in {
   uint64_t snapshots;  /* snapshot chunks / InstallSnapshot (CPU path) */
   uint64_t consumed;   /* stream bytes consumed */
   uint64_t bad;        /* 1: stopped at a bad frame (ErrBadMessage) */
+  uint64_t diverted;   /* DRB_ING_DIVERTED (drb_ingest_ex) */
 } drb_wire_in;
+
+/* A message of the last drb_ingest_wire stream that goes to the CPU path:
+ * its Requests element (a marshalled pb.Message) at stream[offset, offset +
+ * length), for pb.Message.Unmarshal and the receiver's raft.Peer. */
+typedef struct drb_wire_cpu {
+  uint64_t offset;
+  uint32_t length;
+  uint32_t fate;  /* DRB_ING_DIVERTED or DRB_ING_SNAPSHOT */
+} drb_wire_cpu;
 
 /* The receiving end of that connection, for replicas hosted here whose
  * peers are elsewhere: readMessage (tcp.go:180-237: header and payload
@@ -1102,10 +1162,16 @@ typedef struct drb_wire_in {
  * the stream as ErrBadMessage closes the connection.  The stream is
  * uploaded once: payload CRCs, message decode and placement run on the
  * GPU (drb_ingest.hpp); the host reads the 20 B frame headers and walks
- * each batch's top-level fields.  DRB_ERANGE (nothing placed) when a
- * delivered entry's Cmd exceeds cmd_cap. */
+ * each batch's top-level fields.  Messages are placed, dropped or diverted
+ * as by drb_ingest_ex (a delivered entry's Cmd longer than cmd_cap is a
+ * capacity divert); the diverted ones and the InstallSnapshot messages are
+ * listed, in stream order, by drb_ingest_wire_cpu. */
 int drb_ingest_wire(drb_engine *e, const uint8_t *stream, size_t len,
                     uint64_t deployment_id, drb_wire_in *out);
+/* The CPU path's messages of the last drb_ingest_wire call (valid until
+ * the next one): *n_out is the count, DRB_ERANGE when it exceeds cap. */
+int drb_ingest_wire_cpu(drb_engine *e, drb_wire_cpu *out, size_t cap,
+                        size_t *n_out);
 /* A receive buffer of at least `cap` bytes in pinned (page-locked) host
  * memory, owned by the engine (grow-only; valid until the next call or
  * drb_engine_destroy).  A transport that reads its connection into it

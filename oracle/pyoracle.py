@@ -335,6 +335,12 @@ def build_messages(msgs):
     return marr, len(out), earr, pool
 
 
+def msg_tuple(m):
+    """The canonical tuple (abi.message_to_tuple) of a msg() dict."""
+    marr, n, earr, pool = build_messages([m])
+    return message_to_tuple(marr[0], earr, pool)
+
+
 def _unpack_messages(marr, n, earr, pool):
     res = []
     for i in range(n):

@@ -298,6 +298,7 @@ class DistPair:
         for e in self.engs:
             e.init_steady(term=2, leader_slot=0, seed=seed)
         self.rounds = 0
+        self.cpu = set()  # groups handed to the CPU path (the oracle)
 
     def set_hosted(self, g, s, hosted):
         """Replica slot s of group g stops (or returns) on both sides."""
@@ -332,12 +333,64 @@ class DistPair:
     def lane_group(self, r, s, j):
         return self.N * j + (r - s) % self.N
 
+    # ---------------------------------------------- fallback round trip
+    # (Pair.to_cpu / settled / from_cpu over the ranks that hold a group)
+    def to_cpu(self, g):
+        for s in range(self.R):
+            r, j = self.where(g, s)
+            sts = self.engs[r].export_replicas(j, 1)
+            sts[s].flags |= abi.F_FALLBACK
+            self.engs[r].import_replicas(j, sts)
+        self.cpu.add(g)
+
+    def settled(self, g):
+        lead = 0
+        for s in range(self.R):
+            st = self.orc.export(g, s)
+            if not st.flags & abi.F_HOSTED:
+                continue
+            if st.role == abi.LEADER:
+                lead += 1
+            elif st.role not in (abi.FOLLOWER, abi.NONVOTING, abi.WITNESS):
+                return False
+            if self.orc.export_outbox(g, s) or st.ri_count:
+                return False
+            if not (st.committed == st.last_index == st.processed ==
+                    st.sm_index):
+                return False
+        return lead == 1
+
+    def from_cpu(self, g, W=32):
+        """Group g back from the oracle into the replicas the engines host
+        (a slot on a CPU NodeHost stays unhosted)."""
+        for s in range(self.R):
+            r, j = self.where(g, s)
+            e = self.engs[r]
+            sts = e.export_replicas(j, 1)
+            hosted = sts[s].flags & abi.F_HOSTED
+            st = self.orc.export(g, s)
+            if hosted:
+                lo = max(1, st.last_index - W + 1)
+                ents = self.orc.export_log(g, s, lo, st.last_index)
+                ep = po.EntryPool([po._etuple_to_dict(t) for t in ents])
+                arr, pool, n = ep.arrays()
+                e.import_log(j, s, arr, pool)
+                e.kv_import(j, s, self.orc.export_kv(g, s))
+            st.flags = hosted
+            st.fallback_reason = 0
+            sts[s] = st
+            e.import_replicas(j, sts)
+        self.cpu.discard(g)
+
     def exchange(self):
         Engine.exchange_local(self.engs, counted=self.counted)
 
     def round(self, k=1, tick=False, read_index=False, groups=None,
               exchange=True):
         salt = self.rounds
+        if self.cpu:  # no client input for groups on the CPU path
+            groups = [g for g in (range(self.G) if groups is None else groups)
+                      if g not in self.cpu]
         pin = ri_in = abi.DRB_NONE
         if k:
             counts, ents, pool = workload.build_batch(
@@ -385,6 +438,8 @@ class DistPair:
     def check(self, groups=None, logs=True, kv=True, msgs=True, slots=None):
         errs = []
         for g in (range(self.G) if groups is None else groups):
+            if g in self.cpu:
+                continue
             for s in (range(self.R) if slots is None else slots):
                 r, j = self.where(g, s)
                 e = self.engs[r]

@@ -138,3 +138,64 @@ def test_ingest_waits_for_the_exchange(via):
     assert refused > 0
     assert all(p.replica(g, s).sm_index == p.orc.export(g, s).sm_index > 3
                for g in range(G) for s in mine)
+
+
+@pytest.mark.parametrize("via", ["ingest", "wire"])
+def test_entry_rows_overflow_goes_to_the_cpu_path(via):
+    """The CPU NodeHost's leader sends Replicates whose entries a remote
+    plane's entry rows cannot hold (entry_mbox = 1 row, two-entry rounds).
+    The reference's inbox takes them (message.go:105-120); the engine hands
+    each receiver's group to the CPU path (DRB_FB_CAPACITY) with the
+    message instead of dropping it, the oracle -- which received exactly
+    the engine's stream -- steps the group until it settles, and it comes
+    back (drb_import_*).  The other groups stay bit-exact every round."""
+    G, N, R = 16, 2, 3
+    p = DistPair(G=G, R=R, N=N, E=1, max_props=2)
+    _host_elsewhere(p, 0)  # the CPU NodeHost holds the leaders
+    mine = [1, 2]
+    went, came, diverted = set(), set(), 0
+    for r in range(18):
+        now = set()
+        # (the last rounds without ticks: the CPU groups settle and return)
+        o, e = p.round(k=2 if r in (2, 5) else 1, tick=(r % 2 == 0 and r < 14))
+        assert e["fallbacks"] == 0 and e["errors"] == 0, (r, e, p.why())
+        for rank, msgs in _cpu_sends(p, 0).items():
+            if not msgs:
+                continue
+            eng = p.engs[rank]
+            if via == "ingest":
+                got = eng.ingest_ex(*po.build_messages(msgs))
+                div = [po.msg_tuple(m) for m, f in zip(msgs, got["status"])
+                       if f == abi.ING_DIVERTED]
+            else:
+                data = wr.expected_stream(msgs, DID, b"cpu:1")
+                got = eng.ingest_wire(data, DID)
+                div = [wr.message_tuple(data[o:o + n])
+                       for o, n, f in eng.ingest_wire_cpu()]
+            assert got["dropped"] == 0, (r, rank, got)
+            assert got["accepted"] + got["diverted"] == len(msgs), got
+            assert len(div) == got["diverted"]
+            diverted += got["diverted"]
+            for (j, s, reason, flags, _, _) in eng.take_flagged()[0]:
+                assert reason == abi.FB["CAPACITY"], (j, s, reason)
+                g = p.lane_group(rank, s, j)
+                # the receiver's CPU inbox: what was placed, then the
+                # diverted messages -- the CPU leader's sends to it
+                inbox = [m for m in eng.export_inbox(j, s) if m[1] == 1] + \
+                    [d for d in div if d[0] == g + 1 and d[2] == s + 1]
+                want = [t for t in p.orc.export_outbox(g, 0) if t[2] == s + 1]
+                assert inbox == want, (r, g, s)
+                now.add(g)
+        for g in sorted(now - p.cpu):
+            p.to_cpu(g)
+        went |= now
+        errs = p.check(slots=mine)
+        assert not errs, (r, errs[:2])
+        for g in sorted(p.cpu):
+            if p.settled(g):
+                p.from_cpu(g)
+                came.add(g)
+    assert diverted and went and came == went and not p.cpu, \
+        (diverted, went, came, p.cpu)
+    assert all(p.replica(g, s).sm_index == p.orc.export(g, s).sm_index > 3
+               for g in range(G) for s in mine)

@@ -32,9 +32,10 @@ def _round(p, stats=None, **kw):
     o, e = p.round(**kw)
     assert e.fallbacks == 0 and e.errors == 0, (p.rounds, e.to_dict(),
                                                  p.why())
-    assert (e.committed_entries, e.messages, e.dropped_proposals) == \
-        (o.committed_entries, o.messages, o.dropped_proposals), \
-        (p.rounds, e.to_dict(), o.to_dict())
+    if not p.cpu:  # (the oracle's counters include the CPU path's groups)
+        assert (e.committed_entries, e.messages, e.dropped_proposals) == \
+            (o.committed_entries, o.messages, o.dropped_proposals), \
+            (p.rounds, e.to_dict(), o.to_dict())
     errs = p.check()
     assert not errs, (p.rounds, errs[:2])
     if stats is not None:
@@ -109,14 +110,29 @@ def _unhost(p, groups, slot):
         p.eng.import_replicas(g, sts)
 
 
+def _cpu_inbox(p, g, slot, diverted):
+    """What the receiver's CPU raft.Peer gets once its group leaves the
+    GPU at ingest: drb_export_inbox (placed before) then the diverted
+    messages, per sender (include/drb_engine.h drb_ingest_ex)."""
+    out = {}
+    for m in p.eng.export_inbox(g, slot) + diverted:
+        out.setdefault(m[1], []).append(m)
+    return out.get(3, [])  # (replica 3: the other NodeHost)
+
+
 @pytest.mark.parametrize("via", ["ingest", "wire"])
 def test_proposals_from_another_nodehost(via):
     """Replica 3 lives on another NodeHost: its clients' proposals come in
     as that node's Propose messages (with entries of 16 B, 60 B and
     NoOP-session empty Cmds), through drb_ingest or as TCP bytes through
-    drb_ingest_wire, and the GPU leader appends them.  A second Propose of
-    the same sender in one round is dropped as by a full queue, on both
-    sides alike (the oracle receives only the first)."""
+    drb_ingest_wire, and the GPU leader appends them.  Now and then a second
+    Propose of the same sender arrives in one round: the reference's inbox
+    (1024 messages, message.go:105-120) takes it, the GPU inbox (one
+    Propose per plane and round) cannot -- the engine hands the receiver's
+    group to the CPU path (DRB_FB_CAPACITY) with that message, and the
+    oracle, which received exactly the same stream, steps it there until it
+    settles and comes back (drb_import_*).  Every GPU group stays bit-exact
+    with the oracle."""
     G, R = 30, 3
     p = Pair(G=G, R=R, forward_proposals=1, max_props=3, mailbox=16,
              kv_val_cap=64, cmd_cap=96)
@@ -125,9 +141,13 @@ def test_proposals_from_another_nodehost(via):
         _round(p, st, k=1, tick=True)
     _unhost(p, range(G), 2)
     _round(p, st, k=1, tick=True)
-    for r in range(6):
-        msgs = []
-        for g in range(G):
+    went, came = set(), set()
+    for r in range(10):
+        msgs, extra = [], []
+        # (the other NodeHost's clients stop proposing to a group on the
+        # CPU path, so that it settles and returns)
+        live = [g for g in range(G) if g not in p.cpu]
+        for g in live:
             n = 1 + (g + r) % 3
             vl = [4, 60, 0][(g + r) % 3]
             es = []
@@ -140,19 +160,53 @@ def test_proposals_from_another_nodehost(via):
                                  type=d["type"], cmd=d["cmd"]))
             msgs.append(po.msg(MSG["Propose"], from_=3, to=1, shard_id=g + 1,
                                entries=es))
-        p.orc.ingest(msgs)
-        extra = [po.msg(MSG["Propose"], from_=3, to=1, shard_id=g + 1,
-                        entries=[po.ent(key=7)]) for g in range(0, G, 7)]
+        if r < 6:
+            extra = [po.msg(MSG["Propose"], from_=3, to=1, shard_id=g + 1,
+                            entries=[po.ent(key=7 + r)])
+                     for g in live if (g + r) % 7 == 0]
+        stream = msgs + extra
+        p.orc.ingest(stream)  # the oracle gets the whole stream
         if via == "ingest":
-            marr, n, earr, pool = po.build_messages(msgs + extra)
-            acc, drop = p.eng.ingest(marr, n, earr, pool)
+            got = p.eng.ingest_ex(*po.build_messages(stream))
+            div = [m for m, f in zip(stream, got["status"])
+                   if f == abi.ING_DIVERTED]
+            div = [po.msg_tuple(m) for m in div]
         else:
-            data = wr.expected_stream(msgs + extra, DID, b"10.0.0.9:26001")
+            data = wr.expected_stream(stream, DID, b"10.0.0.9:26001")
             got = p.eng.ingest_wire(data, DID)
-            acc, drop = got["accepted"], got["dropped"]
-        assert (acc, drop) == (len(msgs), len(extra)), (acc, drop)
+            cpu = p.eng.ingest_wire_cpu()
+            assert all(f == abi.ING_DIVERTED for _, _, f in cpu)
+            div = [wr.message_tuple(data[o:o + n]) for o, n, _ in cpu]
+        assert (got["accepted"], got["dropped"], got["diverted"]) == \
+            (len(msgs), 0, len(extra)), got
+        # the diverted ones are exactly the second Proposes, and each
+        # flagged receiver's CPU inbox is what the oracle's node received
+        assert sorted(div) == sorted(po.msg_tuple(m) for m in extra)
+        recs, lost = p.eng.take_flagged()
+        assert lost == 0
+        flagged = {(g, s) for (g, s, reason, *_x) in recs
+                   if reason == abi.FB["CAPACITY"]}
+        assert flagged == {(m["shard_id"] - 1, 0) for m in extra}, flagged
+        for (g, s) in flagged:
+            want = [po.msg_tuple(m) for m in stream
+                    if m["shard_id"] == g + 1]
+            assert _cpu_inbox(p, g, s, [d for d in div if d[0] == g + 1]) \
+                == want, g
+            p.to_cpu(g)
+            went.add(g)
         _round(p, st, k=1, tick=(r % 2 == 0))
-    _round(p, st, k=1, tick=True)
+        for g in sorted(p.cpu):
+            if p.settled(g):
+                p.from_cpu(g)
+                came.add(g)
+    for _ in range(6):  # (quiet rounds: no heartbeats, the CPU groups settle)
+        _round(p, st, k=1, tick=False)
+        for g in sorted(p.cpu):
+            if p.settled(g):
+                p.from_cpu(g)
+                came.add(g)
+    assert went and came == went and not p.cpu, (went, came, p.cpu)
+    assert not p.check(), p.check()[:2]
     assert st["committed"] > G * 6, st
 
 

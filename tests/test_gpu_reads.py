@@ -29,14 +29,9 @@ def _read_key(low, j, key_space):
     return x % key_space
 
 
-@pytest.mark.parametrize("ri_replica,read_lanes", [(0, "0"), (2, "0"),
-                                                   (0, "1"), (2, "1")])
-def test_batched_ready_to_reads_and_read_results(ri_replica, read_lanes,
-                                                 monkeypatch):
-    """read_lanes "1": the leaders' reads served one thread per read
-    (k_read_lanes, DRB_READ_LANES) instead of inside the leader kernel."""
+@pytest.mark.parametrize("ri_replica", [0, 2])
+def test_batched_ready_to_reads_and_read_results(ri_replica):
     G, R = 300, 3
-    monkeypatch.setenv("DRB_READ_LANES", read_lanes)
     p = Pair(G=G, R=R, max_reads_per_ctx=READS)
     slot = 0 if ri_replica == 0 else ri_replica - 1
     n_rtr = n_res = found = 0

@@ -53,12 +53,11 @@ def test_random_rounds(case, seed):
     kw = {}
     if case != "voters":
         kw[case + "_slots"] = 1 << 3
-    # (the mailbox bound the pre-pass checks is an upper bound of a
-    # round's sends per follower -- tick, proposals, ReadIndex broadcasts,
-    # commit notifications, one answer per message in -- which this mix
-    # drives past 16 at R = 4 now and then; 24 is the mailbox's maximum)
+    # (the pre-pass's per-follower mailbox bound -- the broadcasts every
+    # follower gets plus what that follower's own records cause -- stays
+    # within 16 on this mix: tools/mailbox_bound.py against the oracle)
     p = Pair(G=G, R=R, elections=1, forward_proposals=1, max_props=2,
-             mailbox=24, **kw)
+             mailbox=16, **kw)
     # replica IDs (0: the leader); a witness neither proposes nor reads
     ids = [0, 1, 2, 3] + ([4] if case != "witness" else [])
     stopped = {}  # slot -> groups
@@ -114,6 +113,10 @@ def test_random_rounds(case, seed):
                 p.from_cpu(g)
         committed += e.committed_entries
     assert committed > G * 10
+    # the default seeds run without a single capacity fallback; wider runs
+    # (DRB_SOAK_SEEDS) may meet the ReadIndex queue's depth now and then
+    if not os.environ.get("DRB_SOAK_SEEDS"):
+        assert fallbacks == 0, fallbacks
     assert fallbacks <= G, fallbacks  # the GPU path stays the main one
     print("soak %s/%d: %d capacity fallbacks, %d at a full ReadIndex queue"
           % (case, seed, fallbacks, ri_full))

@@ -70,6 +70,48 @@ def expected_stream(msgs, deployment_id, source, max_batch=MAX_MSG_BATCH,
         for b in split_batches(msgs, max_batch))
 
 
+def _varint(d, i):
+    v = s = 0
+    while True:
+        b = d[i]
+        i += 1
+        v |= (b & 0x7f) << s
+        s += 7
+        if b < 0x80:
+            return v, i
+
+
+def message_tuple(data):
+    """pb.Message.Unmarshal (raft.pb.go field numbers, message.go:6-20) of
+    one marshalled Requests element, as abi.message_to_tuple: an
+    independent proto2 walk, colfer entries through the oracle codec."""
+    f = dict(type=0, to=0, from_=0, shard_id=0, term=0, log_term=0,
+             log_index=0, commit=0, reject=0, hint=0, hint_high=0)
+    names = {1: "type", 2: "to", 3: "from_", 4: "shard_id", 5: "term",
+             6: "log_term", 7: "log_index", 8: "commit", 9: "reject",
+             10: "hint", 13: "hint_high"}
+    ents, i = [], 0
+    while i < len(data):
+        key, i = _varint(data, i)
+        fn, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _varint(data, i)
+            f[names[fn]] = v
+        else:
+            assert wt == 2, (fn, wt)
+            n, i = _varint(data, i)
+            if fn == 11:
+                e, used = po.entry_unmarshal(data[i:i + n])
+                assert used == n
+                ents.append(e)
+            i += n
+    m = po.msg(f["type"], from_=f["from_"], to=f["to"], term=f["term"],
+               log_term=f["log_term"], log_index=f["log_index"],
+               commit=f["commit"], reject=bool(f["reject"]), hint=f["hint"],
+               hint_high=f["hint_high"], entries=ents, shard_id=f["shard_id"])
+    return po.msg_tuple(m)
+
+
 def parse_stream(data):
     """Splits a stream into payloads, checking magic, the header CRC and
     the payload CRC with zlib (independent of the oracle)."""
