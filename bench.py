@@ -193,14 +193,30 @@ def c5_pool_blocks(G, R, rounds, active_ppm):
     return int(mean + 8 * mean ** 0.5) + R * 65536
 
 
+def host_cores():
+    """(cores this process may run on, CPUs the host shows): the affinity
+    set, capped by the cgroup's CPU quota (cpu.max) where one is set -- a
+    GPU box's share of its machine."""
+    visible = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n), visible
+
+
 def cpu_baseline(args, seconds):
     """The CPU oracle (C restatement of the reference path) on the host:
-    a bounded sample of the same workload, groups split over threads."""
+    a bounded sample of the same workload, groups split over one thread per
+    core this process may use."""
     from dragonboat_amd import workload
     from oracle import pyoracle as po
     import ctypes as C
     from dragonboat_amd.abi import RoundOut
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    cores, visible = host_cores()
     G = 1000 * cores  # C1 scale per core
     c = po.Cluster(G, args.replicas, logdb_keep=64)
     c.setup_steady(0)
@@ -249,7 +265,8 @@ def cpu_baseline(args, seconds):
         committed += sum(o.committed_entries for o in outs)
         rounds += 1
     return dict(value=committed / t_run if t_run else 0.0,
-                unit="committed entries/s", cores=cores, kind="port",
+                unit="committed entries/s", cores=cores,
+                host_cpus_visible=visible, kind="port",
                 sample="%d groups x %d replicas, %d rounds of the same "
                        "workload (k=%d, %s, a LocalTick every round), CPU "
                        "restatement (oracle/), not dragonboat" % (
@@ -809,8 +826,11 @@ def main():
             for bw in wb:
                 eng.free_worker_bufs(bw)
             import ctypes as _C
-            dbytes = (down[0] * _C.sizeof(_abi.WorkerRead) + down[1] * 8 +
-                      down[2] * _C.sizeof(_abi.WorkerApplied)) / KW
+            # the lean records (include/drb_engine.h): a word per lane,
+            # 16 B per ReadyToRead, 4 B + a nibble per served read, 4 B per
+            # applied entry
+            dbytes = (KW * G * 4 + down[0] * _C.sizeof(_abi.WorkerRead) +
+                      down[1] * 4 + (down[1] + KW) // 2 + down[2] * 4) / KW
             step_worker = {
                 "ms_per_step": wms, "steps": KW,
                 "committed_entries_per_s": wout.committed_entries /

@@ -161,25 +161,26 @@ class ApplyResult(C.Structure):
 
 
 class WorkerRead(C.Structure):
-    """drb_worker_read: a ReadyToRead and where its served reads start
-    (values[first, next record's first))."""
-    _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64),
-                ("ctx_high", C.c_uint64), ("group", C.c_uint32),
-                ("first", C.c_uint32)]
+    """drb_worker_read: a ReadyToRead (its Index and SystemCtx.Low)."""
+    _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64)]
 
 
-class WorkerApplied(C.Structure):
-    """drb_worker_applied: one applied entry (pendingProposals.applied)."""
-    _fields_ = [("key", C.c_uint64), ("value", C.c_uint64),
-                ("group", C.c_uint32), ("ignored", C.c_uint32)]
+WORKER_FOUND, WORKER_LONG, WORKER_IGNORED = 8, 5, 0x80000000
+
+
+def worker_lane(w):
+    """(ReadyToReads, served mask, applied entries) of a lanes[] word."""
+    return w & 0xF, (w >> 4) & 0xFF, (w >> 12) & 0xFFFF
 
 
 class WorkerBufs(C.Structure):
     """drb_worker_bufs: pinned host buffers of one step-worker export."""
-    _fields_ = [("reads", C.POINTER(WorkerRead)), ("reads_cap", C.c_uint64),
-                ("values", C.POINTER(C.c_uint64)),
+    _fields_ = [("lanes", C.POINTER(C.c_uint32)), ("lanes_cap", C.c_uint64),
+                ("reads", C.POINTER(WorkerRead)), ("reads_cap", C.c_uint64),
+                ("values", C.POINTER(C.c_uint32)),
+                ("value_meta", C.POINTER(C.c_uint8)),
                 ("values_cap", C.c_uint64),
-                ("applied", C.POINTER(WorkerApplied)),
+                ("applied", C.POINTER(C.c_uint32)),
                 ("applied_cap", C.c_uint64),
                 ("n_reads", C.c_uint64), ("n_values", C.c_uint64),
                 ("n_applied", C.c_uint64)]

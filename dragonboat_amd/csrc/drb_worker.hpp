@@ -9,7 +9,9 @@
 // 243-257).  Here one export covers every group of a replica slot:
 //   1. on the engine stream, behind the round: per lane the three record
 //      counts, one exclusive scan of {reads, values, applied} (hipCUB), and
-//      a compaction of the records into device staging[parity];
+//      a compaction of the lean records (include/drb_engine.h: a word per
+//      lane, 16 B per ReadyToRead, 4 B + a nibble per served read, 4 B per
+//      applied entry) into device staging[parity];
 //   2. on a copy stream of its own: a drain kernel moves staging[parity]
 //      into the caller's pinned host buffers (PCIe writes from the device,
 //      the counts to a mapped header), so the transfer overlaps the next
@@ -23,9 +25,11 @@ struct WorkerState {
   hipEvent_t ev_staged[2] = {nullptr, nullptr};
   hipEvent_t ev_drained[2] = {nullptr, nullptr};
   bool drained_valid[2] = {false, false};
+  uint32_t *lanes[2] = {nullptr, nullptr};  // [G]
   drb_worker_read *rd[2] = {nullptr, nullptr};
-  uint64_t *val[2] = {nullptr, nullptr};
-  drb_worker_applied *ap[2] = {nullptr, nullptr};
+  uint32_t *val[2] = {nullptr, nullptr};
+  uint32_t *meta[2] = {nullptr, nullptr};  // nibbles, 8 per word
+  uint32_t *ap[2] = {nullptr, nullptr};
   uint64_t cap_rd = 0, cap_val = 0, cap_ap = 0;  // staging capacity
   uint4 *cnt = nullptr, *off = nullptr;          // [G + 1]
   void *tmp = nullptr;
@@ -33,6 +37,7 @@ struct WorkerState {
   unsigned long long *tot = nullptr;  // device [2][4]
   unsigned long long *hdr = nullptr;  // pinned, mapped [2][4]
   unsigned long long *hdr_dev = nullptr;  // ... its device address
+  // the buffers of the exports in flight (waited for or not), by parity
   const drb_worker_bufs *owner[2] = {nullptr, nullptr};
   uint64_t seq = 0;
 };
@@ -74,16 +79,25 @@ __global__ void k_worker_count(const View v, uint32_t slot, uint32_t n_reads,
     }
     uint64_t lo, hi;
     worker_apply_range(v, slot, g, &lo, &hi);
-    c.z = hi > lo ? (uint32_t)(hi - lo) : 0u;
+    c.z = hi > lo ? (uint32_t)min(hi - lo, (uint64_t)0xffffu) : 0u;
   }
   cnt[g] = c;  // cnt[G] = 0: the scan's last element is the total
 }
 
+// a served read's value-meta nibble (include/drb_engine.h): read_res.y is
+// vlen | found << 31 (serve_reads_lane)
+__device__ inline uint32_t worker_nibble(uint32_t y) {
+  if (!(y >> 31)) return 0u;
+  const uint32_t vlen = y & 0x7fffffffu;
+  return DRB_WORKER_FOUND | (vlen > 4 ? (uint32_t)DRB_WORKER_LONG : vlen);
+}
+
 __global__ void k_worker_compact(const View v, uint32_t slot,
                                  uint32_t n_reads, const uint4 *off,
-                                 drb_worker_read *rd, uint64_t cap_rd,
-                                 uint64_t *val, uint64_t cap_val,
-                                 drb_worker_applied *ap, uint64_t cap_ap,
+                                 uint32_t *lanes, drb_worker_read *rd,
+                                 uint64_t cap_rd, uint32_t *val,
+                                 uint32_t *meta, uint64_t cap_val,
+                                 uint32_t *ap, uint64_t cap_ap,
                                  unsigned long long *tot) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g == v.G) {  // the totals
@@ -96,47 +110,61 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
   const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
   const uint32_t m =
       nr && n_reads ? v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u) : 0u;
+  uint64_t lo, hi;
+  worker_apply_range(v, slot, g, &lo, &hi);
+  const uint32_t na = hi > lo ? (uint32_t)min(hi - lo, (uint64_t)0xffffu) : 0u;
+  lanes[g] = nr | (m << 4) | (na << 12);
   uint64_t vo = o.y;
+  // the nibbles of this lane's reads, one word (8 nibbles) at a time; the
+  // first and last words may be shared with the neighbouring lanes (the
+  // staging words start zeroed, shared ones take an atomicOr)
+  uint32_t word = 0;
+  uint64_t wi = vo / 8;
+  auto flush = [&](bool last) {
+    if (!word) return;
+    const uint64_t first_w = o.y / 8;
+    const bool shared = wi == first_w || last;
+    if (wi * 8 < cap_val) {
+      if (shared)
+        atomicOr(&meta[wi], word);
+      else
+        meta[wi] = word;
+    }
+    word = 0;
+  };
   for (uint32_t k = 0; k < nr; ++k) {
-    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
-    const uint4 c1 = v.rtr[rtr_ix(v, slot, k, 1, g)];
-    const bool served = (m >> k) & 1u;
     if (o.x + k < cap_rd) {
+      const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
       drb_worker_read r;
       r.index = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
       r.ctx_low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
-      r.ctx_high = (uint64_t)c1.x | ((uint64_t)c1.y << 32);
-      r.group = (uint32_t)g;
-      r.first = (uint32_t)vo;  // (its n_reads results follow when served)
       rd[o.x + k] = r;
     }
-    if (!served) continue;
+    if (!((m >> k) & 1u)) continue;
     for (uint32_t j = 0; j < n_reads; ++j, ++vo) {
-      if (vo >= cap_val) continue;
       const uint2 w = v.read_res[rres_ix(v, slot, k, j, g)];
-      val[vo] = (uint64_t)w.x | ((uint64_t)w.y << 32);
+      if (vo < cap_val) val[vo] = w.x;
+      if (vo / 8 != wi) {
+        flush(false);
+        wi = vo / 8;
+      }
+      word |= worker_nibble(w.y) << (4 * (vo & 7));
     }
   }
-  uint64_t lo, hi;
-  worker_apply_range(v, slot, g, &lo, &hi);
+  flush(true);
   for (uint64_t idx = lo + 1, a = o.z; idx <= hi && a < cap_ap; ++idx, ++a) {
-    const uint4 m0 = v.ring[ring_ix(v, slot, idx, 0, g)];
     const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
     const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
-    drb_worker_applied r;
-    r.key = hi64(m0);
     const uint64_t client = lo64(m1);
     const uint32_t type = m2.z, clen = m2.w;
-    r.ignored = client == 0 ? 1u : 0u;
-    // KVTest.Update's Result.Value: the payload length (kvtest.go:161)
-    r.value = r.ignored ? 0
+    // KVTest.Update's Result.Value: the payload length (kvtest.go:161); an
+    // empty no-op entry is ignored by the rsm (statemachine.go:939)
+    ap[a] = client == 0 ? DRB_WORKER_IGNORED
                         : (type == DRB_ENTRY_ENCODED && clen ? clen - 1 : clen);
-    r.group = (uint32_t)g;
-    ap[a] = r;
   }
 }
 
-// bytes [0, n) of src into dst (16-byte aligned, n a multiple of 8), a
+// bytes [0, n) of src into dst (16-byte aligned, n a multiple of 4), a
 // grid-stride walk of 16 B words
 __device__ inline void worker_drain_copy(uint8_t *dst, const uint8_t *src,
                                          uint64_t n, uint64_t t,
@@ -144,28 +172,36 @@ __device__ inline void worker_drain_copy(uint8_t *dst, const uint8_t *src,
   const uint64_t n16 = n / 16;
   for (uint64_t i = t; i < n16; i += nt)
     ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
-  if ((n & 15) && t == 0)
-    *(uint2 *)(dst + n16 * 16) = *(const uint2 *)(src + n16 * 16);
+  for (uint64_t i = n16 * 4 + t; i < n / 4; i += nt)
+    ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
 }
 
-__global__ void k_worker_drain(const unsigned long long *tot,
+__global__ void k_worker_drain(const unsigned long long *tot, uint64_t G,
+                               const uint32_t *lanes, uint32_t *hlanes,
                                const drb_worker_read *rd, uint64_t cap_rd,
-                               drb_worker_read *hrd, const uint64_t *val,
-                               uint64_t cap_val, uint64_t *hval,
-                               const drb_worker_applied *ap, uint64_t cap_ap,
-                               drb_worker_applied *hap,
-                               unsigned long long *hdr) {
+                               drb_worker_read *hrd, const uint32_t *val,
+                               const uint32_t *meta, uint64_t cap_val,
+                               uint32_t *hval, uint8_t *hmeta,
+                               const uint32_t *ap, uint64_t cap_ap,
+                               uint32_t *hap, unsigned long long *hdr) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t nrd = min((uint64_t)tot[0], cap_rd);
   const uint64_t nval = min((uint64_t)tot[1], cap_val);
   const uint64_t nap = min((uint64_t)tot[2], cap_ap);
+  worker_drain_copy((uint8_t *)hlanes, (const uint8_t *)lanes, G * 4, t, nt);
   if (hrd) worker_drain_copy((uint8_t *)hrd, (const uint8_t *)rd,
                              nrd * sizeof(drb_worker_read), t, nt);
-  if (hval) worker_drain_copy((uint8_t *)hval, (const uint8_t *)val,
-                              nval * sizeof(uint64_t), t, nt);
-  if (hap) worker_drain_copy((uint8_t *)hap, (const uint8_t *)ap,
-                             nap * sizeof(drb_worker_applied), t, nt);
+  if (hval) {
+    worker_drain_copy((uint8_t *)hval, (const uint8_t *)val, nval * 4, t, nt);
+    // the nibbles: whole words, then the last partial word's bytes
+    const uint64_t nb = (nval + 1) / 2, nw = nb / 4;
+    worker_drain_copy(hmeta, (const uint8_t *)meta, nw * 4, t, nt);
+    if (t < nb - nw * 4)
+      hmeta[nw * 4 + t] = (uint8_t)(meta[nw] >> (8 * t));
+  }
+  if (hap) worker_drain_copy((uint8_t *)hap, (const uint8_t *)ap, nap * 4, t,
+                             nt);
   if (t == 0) {
     hdr[0] = tot[0];
     hdr[1] = tot[1];
@@ -182,8 +218,10 @@ static void worker_free(drb_engine *e) {
   for (int k = 0; k < 2; ++k) {
     if (w->ev_staged[k]) (void)hipEventDestroy(w->ev_staged[k]);
     if (w->ev_drained[k]) (void)hipEventDestroy(w->ev_drained[k]);
+    if (w->lanes[k]) (void)hipFree(w->lanes[k]);
     if (w->rd[k]) (void)hipFree(w->rd[k]);
     if (w->val[k]) (void)hipFree(w->val[k]);
+    if (w->meta[k]) (void)hipFree(w->meta[k]);
     if (w->ap[k]) (void)hipFree(w->ap[k]);
   }
   if (w->cnt) (void)hipFree(w->cnt);
@@ -210,15 +248,17 @@ static int worker_reserve(drb_engine *e, uint64_t crd, uint64_t cval,
   for (int k = 0; k < 2; ++k) {
     if (w.rd[k]) HIPCHK(hipFree(w.rd[k]));
     if (w.val[k]) HIPCHK(hipFree(w.val[k]));
+    if (w.meta[k]) HIPCHK(hipFree(w.meta[k]));
     if (w.ap[k]) HIPCHK(hipFree(w.ap[k]));
     w.rd[k] = nullptr;
     w.val[k] = nullptr;
+    w.meta[k] = nullptr;
     w.ap[k] = nullptr;
     HIPCHK(hipMalloc(&w.rd[k], std::max<uint64_t>(crd, 1) *
                                    sizeof(drb_worker_read)));
-    HIPCHK(hipMalloc(&w.val[k], std::max<uint64_t>(cval, 1) * 8 + 16));
-    HIPCHK(hipMalloc(&w.ap[k], std::max<uint64_t>(cap, 1) *
-                                   sizeof(drb_worker_applied)));
+    HIPCHK(hipMalloc(&w.val[k], std::max<uint64_t>(cval, 1) * 4 + 16));
+    HIPCHK(hipMalloc(&w.meta[k], (std::max<uint64_t>(cval, 1) / 8 + 2) * 4));
+    HIPCHK(hipMalloc(&w.ap[k], std::max<uint64_t>(cap, 1) * 4 + 16));
   }
   w.cap_rd = crd;
   w.cap_val = cval;
@@ -237,6 +277,8 @@ static int worker_init(drb_engine *e) {
     HIPCHK(hipEventCreateWithFlags(&w->ev_staged[k], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&w->ev_drained[k], hipEventDisableTiming));
   }
+  for (int k = 0; k < 2; ++k)
+    HIPCHK(hipMalloc(&w->lanes[k], std::max<uint64_t>(G, 1) * 4 + 16));
   HIPCHK(hipMalloc(&w->cnt, (G + 1) * sizeof(uint4)));
   HIPCHK(hipMalloc(&w->off, (G + 1) * sizeof(uint4)));
   HIPCHK(hipcub::DeviceScan::ExclusiveScan(nullptr, w->tmp_bytes, w->cnt,
@@ -279,18 +321,20 @@ static int worker_dev_ptr(void *h, void **d) {
 extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
                                  const drb_worker_bufs *b) {
   if (!e || !b || slot >= e->v.R) return DRB_EINVAL;
-  if ((b->reads_cap && !b->reads) || (b->values_cap && !b->values) ||
+  if (!b->lanes || b->lanes_cap < e->v.G || (b->reads_cap && !b->reads) ||
+      (b->values_cap && (!b->values || !b->value_meta)) ||
       (b->applied_cap && !b->applied))
     return DRB_EINVAL;
-  // (the records hold the lane and the value offset in 32 bits)
-  if (e->v.G > 0xffffffffull || b->values_cap > 0xffffffffull)
-    return DRB_ERANGE;
   if (int rc = worker_init(e)) return rc;
   WorkerState &w = *e->worker;
+  // one export in flight per buffer set (the two parities may hold two)
+  if (w.owner[0] == b || w.owner[1] == b) return DRB_EAGAIN;
   if (int rc = worker_reserve(e, b->reads_cap, b->values_cap, b->applied_cap))
     return rc;
-  void *hrd, *hval, *hap;
-  if (worker_dev_ptr(b->reads, &hrd) || worker_dev_ptr(b->values, &hval) ||
+  void *hl, *hrd, *hval, *hmeta, *hap;
+  if (worker_dev_ptr(b->lanes, &hl) || worker_dev_ptr(b->reads, &hrd) ||
+      worker_dev_ptr(b->values, &hval) ||
+      worker_dev_ptr(b->value_meta, &hmeta) ||
       worker_dev_ptr(b->applied, &hap))
     return DRB_EINVAL;
   const View &v = e->v;
@@ -298,7 +342,9 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
   const uint32_t n_reads =
       v.read_res && e->reads_round == e->round ? e->reads_n : 0u;
   const int k = (int)(w.seq & 1);
-  // staging[k] is free once the drain two exports back is done
+  // staging[k] and its owner slot are free once the export two back was
+  // waited for (its drain is then done)
+  if (w.owner[k]) return DRB_EAGAIN;
   if (w.drained_valid[k])
     HIPCHK(hipStreamWaitEvent(e->stream, w.ev_drained[k], 0));
   const unsigned blocks = (unsigned)((v.G + 1 + 255) / 256);
@@ -308,17 +354,20 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
   HIPCHK(hipcub::DeviceScan::ExclusiveScan(w.tmp, tb, w.cnt, w.off, U4Sum(),
                                            make_uint4(0, 0, 0, 0),
                                            (int)(v.G + 1), e->stream));
+  HIPCHK(hipMemsetAsync(w.meta[k], 0, (std::max<uint64_t>(w.cap_val, 1) / 8 + 2) * 4,
+                        e->stream));
   k_worker_compact<<<blocks, 256, 0, e->stream>>>(
-      v, slot, n_reads, w.off, w.rd[k], b->reads_cap, w.val[k],
-      b->values_cap, w.ap[k], b->applied_cap, w.tot + 4 * k);
+      v, slot, n_reads, w.off, w.lanes[k], w.rd[k], b->reads_cap, w.val[k],
+      w.meta[k], b->values_cap, w.ap[k], b->applied_cap, w.tot + 4 * k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(w.ev_staged[k], e->stream));
   // the transfer, on the copy stream: PCIe-bound, a few workgroups
   HIPCHK(hipStreamWaitEvent(w.sx, w.ev_staged[k], 0));
   k_worker_drain<<<256, 256, 0, w.sx>>>(
-      w.tot + 4 * k, w.rd[k], b->reads_cap, (drb_worker_read *)hrd, w.val[k],
-      b->values_cap, (uint64_t *)hval, w.ap[k], b->applied_cap,
-      (drb_worker_applied *)hap, w.hdr_dev + 4 * k);
+      w.tot + 4 * k, v.G, w.lanes[k], (uint32_t *)hl, w.rd[k], b->reads_cap,
+      (drb_worker_read *)hrd, w.val[k], w.meta[k], b->values_cap,
+      (uint32_t *)hval, (uint8_t *)hmeta, w.ap[k], b->applied_cap,
+      (uint32_t *)hap, w.hdr_dev + 4 * k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(w.ev_drained[k], w.sx));
   w.drained_valid[k] = true;
@@ -330,6 +379,7 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
 extern "C" int drb_worker_wait(drb_engine *e, drb_worker_bufs *b) {
   if (!e || !b || !e->worker) return DRB_EINVAL;
   WorkerState &w = *e->worker;
+  // (drb_worker_export keeps at most one export in flight per buffer set)
   int k = -1;
   for (int q = 0; q < 2; ++q)
     if (w.owner[q] == b && w.drained_valid[q]) k = q;

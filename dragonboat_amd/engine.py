@@ -740,18 +740,22 @@ class Engine:
         """A drb_worker_bufs over fresh pinned host buffers (drb_host_alloc);
         free them with free_worker_bufs."""
         b = abi.WorkerBufs()
-        for name, typ, cap in (("reads", abi.WorkerRead, reads_cap),
-                               ("values", C.c_uint64, values_cap),
-                               ("applied", abi.WorkerApplied, applied_cap)):
+        for name, typ, n, cap in (
+                ("lanes", C.c_uint32, self.G, self.G),
+                ("reads", abi.WorkerRead, reads_cap, reads_cap),
+                ("values", C.c_uint32, values_cap, values_cap),
+                ("value_meta", C.c_uint8, (values_cap + 1) // 2, None),
+                ("applied", C.c_uint32, applied_cap, applied_cap)):
             p = P()
-            _ck(lib().drb_host_alloc(self.h, max(1, cap) * C.sizeof(typ),
+            _ck(lib().drb_host_alloc(self.h, max(1, n) * C.sizeof(typ),
                                      C.byref(p)), "drb_host_alloc")
             setattr(b, name, C.cast(p, C.POINTER(typ)))
-            setattr(b, name + "_cap", cap)
+            if cap is not None:
+                setattr(b, name + "_cap", cap)
         return b
 
     def free_worker_bufs(self, b):
-        for name in ("reads", "values", "applied"):
+        for name in ("lanes", "reads", "values", "value_meta", "applied"):
             _ck(lib().drb_host_free(self.h, C.cast(getattr(b, name), P)),
                 "drb_host_free")
 

@@ -748,39 +748,59 @@ int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
  * into device staging (two buffers, by export parity) and, on a copy
  * stream, their transfer into the caller's host buffers (drb_host_alloc):
  * the transfer overlaps the next rounds.  drb_worker_wait blocks until
- * that export's bytes are in its buffers and fills the counts.  Records in
- * group order, each group's in release / index order.
+ * that export's bytes are in its buffers and fills the counts.
+ *
+ * The records carry only what the host cannot rebuild from what it staged
+ * (about 64 B per C3 group-round):
+ *   lanes[g]   one word per lane (every lane of the engine, g < num_groups):
+ *              bits 0-3 its ReadyToReads this round, bits 4-11 which of
+ *              them had their reads served (bit k: the k-th; its
+ *              reads_per_ctx results follow in values), bits 12-27 its
+ *              applied entries;
+ *   reads      per ReadyToRead, lanes in order, each lane's in release
+ *              order: its Index and SystemCtx.Low (the host issued the ctx:
+ *              Low is its random part, High its own tick + 30,
+ *              request.go:864-875);
+ *   values     per served read, in ReadyToRead and read order: the value's
+ *              first 4 bytes, little endian;
+ *   value_meta a nibble per served read (read i: byte i / 2, low nibble
+ *              for even i): bit 3 found, bits 0-2 the value's length, or 5
+ *              when it is longer than 4 bytes (drb_export_read_values has
+ *              it whole);
+ *   applied    per applied entry, lanes in order, each lane's in index
+ *              order: KVTest's sm.Result.Value (kvtest.go:161) in bits
+ *              0-30, bit 31 set for an empty no-op entry the rsm ignores
+ *              (statemachine.go:939).  The entries are the host's own
+ *              proposals in the order it staged them (Key, ClientID and
+ *              SeriesID are the host's: node.go:243-257 matches on them).
  */
-typedef struct drb_worker_read {  /* one ReadyToRead, 32 B */
-  uint64_t index;      /* its read index */
+typedef struct drb_worker_read {  /* one ReadyToRead, 16 B */
+  uint64_t index;
   uint64_t ctx_low;
-  uint64_t ctx_high;
-  uint32_t group;      /* lane (ShardID = first_shard_id + group) */
-  uint32_t first;      /* its served reads' results: values[first, end),
-                        * end = the next record's first (n_values after
-                        * the last); empty when the ctx was deferred until
-                        * its index is applied, or no reads ran */
 } drb_worker_read;
 
-typedef struct drb_worker_applied {  /* one applied entry, 24 B */
-  uint64_t key;        /* pb.Entry.Key: the proposal's RequestState */
-  uint64_t value;      /* sm.Result.Value (kvtest.go:161) */
-  uint32_t group;
-  uint32_t ignored;    /* 1: an empty no-op entry (statemachine.go:939) */
-} drb_worker_applied;
+#define DRB_WORKER_LANE_READS(w) ((w) & 0xfu)
+#define DRB_WORKER_LANE_SERVED(w) (((w) >> 4) & 0xffu)
+#define DRB_WORKER_LANE_APPLIED(w) (((w) >> 12) & 0xffffu)
+#define DRB_WORKER_FOUND 8u
+#define DRB_WORKER_LONG 5u
+#define DRB_WORKER_IGNORED 0x80000000u
 
 typedef struct drb_worker_bufs {
-  drb_worker_read *reads;      /* host buffers from drb_host_alloc */
+  uint32_t *lanes;             /* host buffers from drb_host_alloc */
+  uint64_t lanes_cap;          /* >= num_groups */
+  drb_worker_read *reads;
   uint64_t reads_cap;
-  /* per served read: LE32 value | (vlen | found << 31) << 32 (the value's
-   * first 4 bytes; all of it at C3's 4-byte values) */
-  uint64_t *values;
+  uint32_t *values;
+  uint8_t *value_meta;         /* (values_cap + 1) / 2 bytes */
   uint64_t values_cap;
-  drb_worker_applied *applied;
+  uint32_t *applied;
   uint64_t applied_cap;
   uint64_t n_reads, n_values, n_applied;  /* set by drb_worker_wait */
 } drb_worker_bufs;
 
+/* DRB_EAGAIN: b already has an export in flight (drb_worker_wait it
+ * first); two drb_worker_bufs alternate in a step worker's loop */
 int drb_worker_export(drb_engine *e, uint32_t slot, const drb_worker_bufs *b);
 /* DRB_ERANGE when a count exceeded its cap (the counts are the full ones,
  * the buffers hold the first cap records) */
@@ -1017,13 +1037,20 @@ int drb_exchange_bytes(drb_engine *e, uint64_t *bytes, int reset);
  * engine, i.e. one stream synchronisation each, then the copies and a
  * synchronisation of every stream): fewer bytes, host round trips. */
 int drb_exchange_local_counted(drb_engine *const *engines, uint32_t n);
-/* A process-per-GPU host (RCCL send/recv of drb_plane_regions on the
- * engine stream) tells the engine its exchange of the last round is
- * enqueued.  With replicas spread over ranks, drb_ingest / drb_ingest_wire
- * return DRB_EAGAIN between a round's launch and its exchange: a message
- * for a remote plane written then would be overwritten by the exchange's
- * copy of that plane (the receiver's inbound header), so the transport
- * retries after the exchange.  drb_exchange_local marks it itself. */
+/* A process-per-GPU host (RCCL send/recv of drb_plane_regions) tells the
+ * engine its exchange of the last round is enqueued.  With replicas spread
+ * over ranks, drb_ingest / drb_ingest_wire return DRB_EAGAIN between a
+ * round's launch and its exchange: a message for a remote plane written
+ * then would be overwritten by the exchange's copy of that plane (the
+ * receiver's inbound header), so the transport retries after the exchange.
+ * Ordering contract: the exchange's receives must be enqueued on the
+ * engine stream (drb_engine_stream; ncclGroupStart ... ncclGroupEnd on it,
+ * as dragonboat_amd/exchange.py does) or have completed before this call
+ * -- drb_ingest's placement is ordered behind them only on that stream.  A
+ * host whose collectives run on a stream of its own makes the engine
+ * stream wait on an event recorded after them (hipStreamWaitEvent), or
+ * synchronises that stream, before drb_exchange_mark.
+ * drb_exchange_local marks it itself. */
 int drb_exchange_mark(drb_engine *e);
 
 /*

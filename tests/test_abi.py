@@ -67,7 +67,7 @@ STRUCTS = {
     "drb_tan_state": abi.TanState,
     "drb_tan_log": abi.TanLog,
     "drb_worker_read": abi.WorkerRead,
-    "drb_worker_applied": abi.WorkerApplied,
+    "drb_wire_cpu": abi.WireCpu,
     "drb_worker_bufs": abi.WorkerBufs,
 }
 # ctypes field names that differ from the C member name
