@@ -164,6 +164,11 @@ def parse():
                     help="after the timed region, also time rounds whose "
                          "proposals come from host memory through "
                          "drb_stage_proposals (default: on for c2/c3, N=1)")
+    ap.add_argument("--chunk-ab", default="",
+                    help="c3, after the timed region: A/B of drb_step_rounds "
+                         "(k rounds chunk by chunk of the groups) against "
+                         "plain rounds, specs CHUNK_GROUPS:K,... (e.g. "
+                         "65536:4,262144:2); reported as chunk_ab, not value")
     ap.add_argument("--step-worker", type=int, default=-1,
                     help="after the timed region, also time whole step-"
                          "worker rounds: host-staged proposals, the round, "
@@ -634,6 +639,50 @@ def main():
     achieved = alg / (kern_ms * 1e-3) / 1e9
     traffic = (None, None) if (c2 or c4 or c5 or args.kv_fill == 0) else \
         pmc_traffic(G, R)
+    chunk_ab = None
+    if args.chunk_ab and not (c4 or c5):
+        # the same rounds (the timed batches again, slot b = i % NP) as K
+        # plain rounds and as K / k drb_step_rounds calls, alternated twice
+        fused = reads and args.reads_mode == "fused"
+
+        def rin(i):
+            return dict(tick=True, prop_slot=i % NP,
+                        ri_slot=i % NP if reads else 0xFFFFFFFF,
+                        reads_per_ctx=READS_PER_CTX if fused else 0,
+                        key_space=KEY_SPACE)
+
+        def plain():
+            eng.sync()
+            a = time.perf_counter()
+            for i in range(K):
+                eng.step_async(**rin(i))
+            eng.sync()
+            return (time.perf_counter() - a) * 1e3 / K
+
+        def chunked(cg, kk):
+            eng.sync()
+            a = time.perf_counter()
+            for i in range(0, K, kk):
+                eng.step_rounds([rin(i + t) for t in range(min(kk, K - i))],
+                                cg)
+            eng.sync()
+            return (time.perf_counter() - a) * 1e3 / K
+
+        chunk_ab = {"plain_ms": [], "note": "K rounds of the timed batches "
+                    "(LocalTick every round) as plain rounds and as "
+                    "drb_step_rounds(k) over chunks of chunk_groups groups "
+                    "(two streams alternating chunks), alternated twice, "
+                    "ms per round; not value"}
+        specs = [tuple(int(x) for x in sp.split(":"))
+                 for sp in args.chunk_ab.split(",") if sp]
+        for rep in range(2):
+            chunk_ab["plain_ms"].append(plain())
+            for cg, kk in specs:
+                chunk_ab.setdefault("%d:%d" % (cg, kk), []).append(
+                    chunked(cg, kk))
+        out2 = eng.read_counters(reset=True)
+        chunk_ab["fallbacks"] = out2.fallbacks
+        chunk_ab["errors"] = out2.errors
     wire = None
     if not (c4 or c5 or args.no_wire):
         # after the timed region: the last round's leader -> follower-slot-1
@@ -809,18 +858,23 @@ def main():
             eng.read_counters(reset=True)
             eng.sync()
             w0 = time.perf_counter()
+            # a step worker's iteration: the round (its proposals staged
+            # one iteration ahead), the export behind it, the next round's
+            # entry queue up while it runs, then the outputs of the round
+            # before it (their copy ran beside this round)
+            eng.stage_proposals_packed(0, _abi.ENTRY_ENCODED, *hp[0])
             for i in range(KW):
-                b = i % HB
-                bw = wb[i % 2]
-                if i >= 2:  # the worker consumed export i - 2's buffers
-                    n3 = eng.worker_wait(bw)
+                step(2 * args.warmup + K + KH + i, i % HB)
+                eng.worker_export(0, wb[i % 2])
+                if i + 1 < KW:
+                    b1 = (i + 1) % HB
+                    eng.stage_proposals_packed(b1, _abi.ENTRY_ENCODED,
+                                               *hp[b1])
+                if i >= 1:
+                    n3 = eng.worker_wait(wb[(i - 1) % 2])
                     down = [d + x for d, x in zip(down, n3)]
-                eng.stage_proposals_packed(b, _abi.ENTRY_ENCODED, *hp[b])
-                step(2 * args.warmup + K + KH + i, b)
-                eng.worker_export(0, bw)
-            for i in range(max(0, KW - 2), KW):
-                n3 = eng.worker_wait(wb[i % 2])
-                down = [d + x for d, x in zip(down, n3)]
+            n3 = eng.worker_wait(wb[(KW - 1) % 2])
+            down = [d + x for d, x in zip(down, n3)]
             wms = (time.perf_counter() - w0) * 1e3 / KW
             wout = eng.read_counters(reset=True)
             for bw in wb:
@@ -842,14 +896,15 @@ def main():
                 "read_results_per_round": down[1] / KW,
                 "applied_per_round": down[2] / KW,
                 "note": "whole step-worker rounds timed around the loop: "
-                        "packed proposals from pinned host memory, the "
-                        "round with its 9 reads per released ctx, then "
-                        "drb_worker_export of slot 0's ReadyToReads, "
-                        "read results and applied entries into pinned "
-                        "host buffers (compaction behind the round, the "
-                        "transfer on a copy stream overlapping the next "
-                        "round; drb_worker_wait before a buffer set is "
-                        "reused); not `value`"}
+                        "packed proposals from pinned host memory (staged "
+                        "one round ahead), the round with its 9 reads per "
+                        "released ctx, then drb_worker_export of slot 0's "
+                        "ReadyToReads, read results and applied entries "
+                        "in the lean records (compaction behind the "
+                        "round, exact-size copy-engine transfers into "
+                        "pinned host buffers beside the next round); "
+                        "drb_worker_wait of the previous round's export "
+                        "every iteration; not `value`"}
         del hb, hp
     # the replicas that left the fast path during the run, by reason
     # (drb_take_flagged): a run with any is not a pure fast-path number
@@ -996,6 +1051,8 @@ def main():
             res["host_staged"] = host_staged
         if step_worker is not None:
             res["step_worker"] = step_worker
+        if chunk_ab is not None:
+            res["chunk_ab"] = chunk_ab
         if failover is not None:
             res["failover"] = failover
         if args.elections:

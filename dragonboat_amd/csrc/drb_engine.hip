@@ -1951,15 +1951,23 @@ __global__ __launch_bounds__(256) void k_active_scatter(const View v) {
   }
 }
 
+// blk0 / nblk: a chunk of group blocks (drb_step_rounds; nblk 0: all), on
+// stream st
 template <int R>
-static void launch_step(drb_engine *e, const RoundParams &p0) {
-  const unsigned gx = (unsigned)((e->v.G + 255) / 256);
+static void launch_step(drb_engine *e, const RoundParams &p0,
+                        hipStream_t st = nullptr, uint32_t blk0 = 0,
+                        uint32_t nblk = 0) {
+  const unsigned gx_all = (unsigned)((e->v.G + 255) / 256);
+  const unsigned gx = nblk ? nblk : gx_all;
+  if (!st) st = e->stream;
   if (p0.listed) {
     k_active_scan<R><<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v, p0);
     k_active_prefix<<<4 * e->v.R, 1024, 0, e->stream>>>(e->v, gx);
     k_active_scatter<<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v);
   }
   RoundParams pl = p0, pf = p0;
+  pl.blk0 = pf.blk0 = blk0;
+  pl.gx_all = pf.gx_all = nblk ? gx_all : 0u;
   uint32_t nl = 0, nf = 0;
   pl.slots = slot_list(e->role_slots[0], &nl);
   pf.slots = slot_list(e->role_slots[1], &nf);
@@ -1978,8 +1986,8 @@ static void launch_step(drb_engine *e, const RoundParams &p0) {
   const bool fwd = e->v.fwd_props || e->v.nv_mask || e->v.wt_mask;
   const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
   const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
-  if (nl) launch[kl](e->v, pl, gx * nl, e->stream);
-  if (nf) launch[kf](e->v, pf, gx * nf, e->stream);
+  if (nl) launch[kl](e->v, pl, gx * nl, st);
+  if (nf) launch[kf](e->v, pf, gx * nf, st);
   if (e->v.elections) {  // the replicas the two launches routed (F_SLOW)
     RoundParams ps = p0;
     ps.slots = 0;
@@ -2060,23 +2068,20 @@ extern "C" int drb_role_slots(const drb_engine *e, uint32_t *leader_slots,
   return DRB_OK;
 }
 
-extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
-  if (!e || !in) return DRB_EINVAL;
-  // transport threads stage the next round's inbox under this lock: a
-  // round launches and advances e->round atomically with respect to them
-  std::lock_guard<std::mutex> ingest_lock(e->ingest_mu);
-  // a durable LogDB: the last round's messages wait for its persistence
-  if (e->cfg.durable_log && e->committed_round < e->round) return DRB_EINVAL;
+// a round's parameters from its drb_round_in (round t = e->round + 1 + ahead)
+static int round_params(drb_engine *e, const drb_round_in *in, uint64_t ahead,
+                        uint64_t ticks_before, RoundParams *out) {
   if (in->prop_slot != DRB_NONE && in->prop_slot >= e->cfg.prop_slots)
     return DRB_ERANGE;
   if (in->ri_slot != DRB_NONE && in->ri_slot >= e->cfg.ri_slots)
     return DRB_ERANGE;
   RoundParams p;
+  memset(&p, 0, sizeof(p));
   p.slots = 0;
   p.nrows = 1;
-  p.round = e->round + 1;
+  p.round = e->round + 1 + ahead;
   p.tick = in->tick ? 1 : 0;
-  p.tick_no = e->ticks + p.tick;
+  p.tick_no = ticks_before + p.tick;
   p.prop_slot = in->prop_slot;
   p.ri_slot = in->ri_slot;
   p.n_reads = in->reads_per_ctx;
@@ -2099,6 +2104,48 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   if ((p.prop_replica && ((e->v.wt_mask >> (p.prop_replica - 1)) & 1u)) ||
       (p.ri_replica && ((e->v.wt_mask >> (p.ri_replica - 1)) & 1u)))
     return DRB_EINVAL;
+  *out = p;
+  return DRB_OK;
+}
+
+static int launch_any(drb_engine *e, const RoundParams &p,
+                      hipStream_t st = nullptr, uint32_t blk0 = 0,
+                      uint32_t nblk = 0) {
+  switch (e->v.R) {
+    case 1: launch_step<1>(e, p, st, blk0, nblk); break;
+    case 2: launch_step<2>(e, p, st, blk0, nblk); break;
+    case 3: launch_step<3>(e, p, st, blk0, nblk); break;
+    case 4: launch_step<4>(e, p, st, blk0, nblk); break;
+    case 5: launch_step<5>(e, p, st, blk0, nblk); break;
+    case 6: launch_step<6>(e, p, st, blk0, nblk); break;
+    case 7: launch_step<7>(e, p, st, blk0, nblk); break;
+    case 8: launch_step<8>(e, p, st, blk0, nblk); break;
+    default: return DRB_EINVAL;
+  }
+  HIPCHK(hipGetLastError());
+  return DRB_OK;
+}
+
+// the host's bookkeeping after round p was enqueued
+static void round_done(drb_engine *e, const RoundParams &p) {
+  e->round++;
+  e->ticks += p.tick;
+  if (p.n_reads) {
+    e->reads_round = e->round;
+    e->reads_n = p.n_reads;
+    e->reads_ks = p.key_space;
+  }
+}
+
+extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
+  if (!e || !in) return DRB_EINVAL;
+  // transport threads stage the next round's inbox under this lock: a
+  // round launches and advances e->round atomically with respect to them
+  std::lock_guard<std::mutex> ingest_lock(e->ingest_mu);
+  // a durable LogDB: the last round's messages wait for its persistence
+  if (e->cfg.durable_log && e->committed_round < e->round) return DRB_EINVAL;
+  RoundParams p;
+  if (int rc = round_params(e, in, 0, e->ticks, &p)) return rc;
   if (e->v.elections)  // this round's slow list
     HIPCHK(hipMemsetAsync(e->v.slow_n, 0, 8, e->stream));
   // plane summaries of this round only -- once a host reads them
@@ -2112,30 +2159,57 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
     HIPCHK(hipMemsetAsync(e->v.xslow, 0,
                           4ull * e->v.R * e->v.R * ((e->v.G + 255) / 256) * 4,
                           e->stream));
-  switch (e->v.R) {
-    case 1: launch_step<1>(e, p); break;
-    case 2: launch_step<2>(e, p); break;
-    case 3: launch_step<3>(e, p); break;
-    case 4: launch_step<4>(e, p); break;
-    case 5: launch_step<5>(e, p); break;
-    case 6: launch_step<6>(e, p); break;
-    case 7: launch_step<7>(e, p); break;
-    case 8: launch_step<8>(e, p); break;
-    default: return DRB_EINVAL;
-  }
-  HIPCHK(hipGetLastError());
+  if (int rc = launch_any(e, p)) return rc;
   if (p.encode_saves && e->v.save_tan) {
     int rc = launch_tan(e, (uint32_t)p.round);
     if (rc) return rc;
   }
   if (p.prop_slot != DRB_NONE)
     HIPCHK(hipEventRecord(e->ev_prop[p.prop_slot], e->stream));
-  e->round++;
-  e->ticks += p.tick;
-  if (p.n_reads) {
-    e->reads_round = e->round;
-    e->reads_n = p.n_reads;
-    e->reads_ks = p.key_space;
+  round_done(e, p);
+  return DRB_OK;
+}
+
+// k rounds, chunk by chunk of the groups: each chunk of chunk_groups
+// groups (a multiple of 256) runs all k rounds before the next chunk starts
+// -- groups are independent (the reference steps each shard on its own,
+// engine.go:1316-1328), so every group sees exactly the rounds of
+// drb_step_round_async, and a chunk's rounds can find its mailbox, state
+// and window rows still on-die.  Chunks alternate between two streams
+// (joined back into the engine stream at the end).  Co-resident replicas,
+// no elections, no listed rounds, no tan records, no durable LogDB.
+extern "C" int drb_step_rounds(drb_engine *e, const drb_round_in *in,
+                               uint32_t k, uint64_t chunk_groups) {
+  if (!e || !in || !k) return DRB_EINVAL;
+  std::lock_guard<std::mutex> ingest_lock(e->ingest_mu);
+  if (e->v.elections || e->v.remote_mask || e->v.save_tan ||
+      e->cfg.durable_log)
+    return DRB_EINVAL;
+  const uint64_t gx = (e->v.G + 255) / 256;
+  if (!chunk_groups || chunk_groups % 256) return DRB_EINVAL;
+  const uint64_t cb = chunk_groups / 256;
+  std::vector<RoundParams> ps(k);
+  uint64_t ticks = e->ticks;
+  for (uint32_t t = 0; t < k; ++t) {
+    if (in[t].listed) return DRB_EINVAL;
+    if (int rc = round_params(e, &in[t], t, ticks, &ps[t])) return rc;
+    ticks += ps[t].tick;
+  }
+  // both streams start behind the engine stream's work
+  HIPCHK(hipEventRecord(e->ev_fork, e->stream));
+  HIPCHK(hipStreamWaitEvent(e->stream2, e->ev_fork, 0));
+  for (uint64_t c0 = 0, c = 0; c0 < gx; c0 += cb, ++c) {
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, gx - c0);
+    hipStream_t st = (c & 1) ? e->stream2 : e->stream;
+    for (uint32_t t = 0; t < k; ++t)
+      if (int rc = launch_any(e, ps[t], st, (uint32_t)c0, nb)) return rc;
+  }
+  HIPCHK(hipEventRecord(e->ev_join, e->stream2));
+  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+  for (uint32_t t = 0; t < k; ++t) {
+    if (ps[t].prop_slot != DRB_NONE)
+      HIPCHK(hipEventRecord(e->ev_prop[ps[t].prop_slot], e->stream));
+    round_done(e, ps[t]);
   }
   return DRB_OK;
 }

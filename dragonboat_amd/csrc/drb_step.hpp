@@ -2252,6 +2252,10 @@ struct RoundParams {
   uint32_t ri_replica;  // staged ReadIndex at: 0 the leader, else ID
   uint32_t listed;      // 1: step the active list (k_active_*), see below
   uint32_t prop_replica;  // staged proposals at: 0 the leader, else ID
+  // a launch over a chunk of the groups (drb_step_rounds): its first group
+  // block, and the engine's group blocks (0: the launch covers them all)
+  uint32_t blk0;
+  uint32_t gx_all;
 };
 
 // Whether this replica takes the lane's staged proposals / ReadIndex
@@ -2320,9 +2324,11 @@ DRB_DEV BlockPos block_pos(const RoundParams &p) {
   const uint32_t n = p.nrows ? p.nrows : 1u;
   const uint32_t b = blockIdx.x, gx = gridDim.x / n;
   BlockPos bp;
-  bp.gx = gx;
+  // (a chunk's launch: its blocks are group blocks blk0.. of the engine's
+  // gx_all, so lanes and counter rows are the full launch's)
+  bp.gx = p.gx_all ? p.gx_all : gx;
   bp.y = b / gx;
-  bp.x = b % gx;
+  bp.x = p.blk0 + b % gx;
   return bp;
 }
 

@@ -11,20 +11,25 @@
 //      counts, one exclusive scan of {reads, values, applied} (hipCUB), and
 //      a compaction of the lean records (include/drb_engine.h: a word per
 //      lane, 16 B per ReadyToRead, 4 B + a nibble per served read, 4 B per
-//      applied entry) into device staging[parity];
-//   2. on a copy stream of its own: a drain kernel moves staging[parity]
-//      into the caller's pinned host buffers (PCIe writes from the device,
-//      the counts to a mapped header), so the transfer overlaps the next
-//      rounds on the engine stream; staging[parity] is reused two exports
-//      later, behind that drain.
-// No host synchronisation until drb_worker_wait.
+//      applied entry) into device staging[parity]; the totals go straight
+//      to mapped host memory;
+//   2. the engine's drain thread waits for that compaction and copies
+//      exactly those bytes into the caller's pinned buffers with the copy
+//      engines (hipMemcpyAsync on a stream of its own): the transfer
+//      overlaps the next rounds and takes no CU.  (A drain kernel writing
+//      host memory from 256 workgroups slowed the concurrent leader kernel
+//      from 0.72 to 1.76 ms: profiles/r05_worker.)
+// No host synchronisation in the caller until drb_worker_wait.
 #pragma once
 
+#include <condition_variable>
+#include <deque>
+#include <thread>
+
 struct WorkerState {
-  hipStream_t sx = nullptr;
+  hipStream_t sx = nullptr;  // the drain thread's copies
   hipEvent_t ev_staged[2] = {nullptr, nullptr};
   hipEvent_t ev_drained[2] = {nullptr, nullptr};
-  bool drained_valid[2] = {false, false};
   uint32_t *lanes[2] = {nullptr, nullptr};  // [G]
   drb_worker_read *rd[2] = {nullptr, nullptr};
   uint32_t *val[2] = {nullptr, nullptr};
@@ -34,12 +39,23 @@ struct WorkerState {
   uint4 *cnt = nullptr, *off = nullptr;          // [G + 1]
   void *tmp = nullptr;
   size_t tmp_bytes = 0;
-  unsigned long long *tot = nullptr;  // device [2][4]
-  unsigned long long *hdr = nullptr;  // pinned, mapped [2][4]
+  unsigned long long *hdr = nullptr;      // pinned, mapped [2][4]: totals
   unsigned long long *hdr_dev = nullptr;  // ... its device address
   // the buffers of the exports in flight (waited for or not), by parity
   const drb_worker_bufs *owner[2] = {nullptr, nullptr};
   uint64_t seq = 0;
+  // the drain thread: one job per export, in order
+  struct Job {
+    int k;
+    drb_worker_bufs b;  // (the pointers and capacities at export time)
+  };
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Job> jobs;
+  bool issued[2] = {false, false};  // ev_drained[k] recorded for its job
+  int err = 0;                      // a failed copy (reported by wait)
+  bool stop = false;
 };
 
 namespace {
@@ -100,10 +116,11 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
                                  uint32_t *ap, uint64_t cap_ap,
                                  unsigned long long *tot) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g == v.G) {  // the totals
+  if (g == v.G) {  // the totals, into mapped host memory
     tot[0] = off[g].x;
     tot[1] = off[g].y;
     tot[2] = off[g].z;
+    __threadfence_system();
   }
   if (g >= v.G) return;
   const uint4 o = off[g];
@@ -164,56 +181,19 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
   }
 }
 
-// bytes [0, n) of src into dst (16-byte aligned, n a multiple of 4), a
-// grid-stride walk of 16 B words
-__device__ inline void worker_drain_copy(uint8_t *dst, const uint8_t *src,
-                                         uint64_t n, uint64_t t,
-                                         uint64_t nt) {
-  const uint64_t n16 = n / 16;
-  for (uint64_t i = t; i < n16; i += nt)
-    ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
-  for (uint64_t i = n16 * 4 + t; i < n / 4; i += nt)
-    ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
-}
-
-__global__ void k_worker_drain(const unsigned long long *tot, uint64_t G,
-                               const uint32_t *lanes, uint32_t *hlanes,
-                               const drb_worker_read *rd, uint64_t cap_rd,
-                               drb_worker_read *hrd, const uint32_t *val,
-                               const uint32_t *meta, uint64_t cap_val,
-                               uint32_t *hval, uint8_t *hmeta,
-                               const uint32_t *ap, uint64_t cap_ap,
-                               uint32_t *hap, unsigned long long *hdr) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t nrd = min((uint64_t)tot[0], cap_rd);
-  const uint64_t nval = min((uint64_t)tot[1], cap_val);
-  const uint64_t nap = min((uint64_t)tot[2], cap_ap);
-  worker_drain_copy((uint8_t *)hlanes, (const uint8_t *)lanes, G * 4, t, nt);
-  if (hrd) worker_drain_copy((uint8_t *)hrd, (const uint8_t *)rd,
-                             nrd * sizeof(drb_worker_read), t, nt);
-  if (hval) {
-    worker_drain_copy((uint8_t *)hval, (const uint8_t *)val, nval * 4, t, nt);
-    // the nibbles: whole words, then the last partial word's bytes
-    const uint64_t nb = (nval + 1) / 2, nw = nb / 4;
-    worker_drain_copy(hmeta, (const uint8_t *)meta, nw * 4, t, nt);
-    if (t < nb - nw * 4)
-      hmeta[nw * 4 + t] = (uint8_t)(meta[nw] >> (8 * t));
-  }
-  if (hap) worker_drain_copy((uint8_t *)hap, (const uint8_t *)ap, nap * 4, t,
-                             nt);
-  if (t == 0) {
-    hdr[0] = tot[0];
-    hdr[1] = tot[1];
-    hdr[2] = tot[2];
-  }
-}
-
 }  // namespace
 
 static void worker_free(drb_engine *e) {
   WorkerState *w = e->worker;
   if (!w) return;
+  if (w->th.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(w->mu);
+      w->stop = true;
+    }
+    w->cv.notify_all();
+    w->th.join();
+  }
   if (w->sx) (void)hipStreamSynchronize(w->sx);
   for (int k = 0; k < 2; ++k) {
     if (w->ev_staged[k]) (void)hipEventDestroy(w->ev_staged[k]);
@@ -227,11 +207,59 @@ static void worker_free(drb_engine *e) {
   if (w->cnt) (void)hipFree(w->cnt);
   if (w->off) (void)hipFree(w->off);
   if (w->tmp) (void)hipFree(w->tmp);
-  if (w->tot) (void)hipFree(w->tot);
   if (w->hdr) (void)hipHostFree(w->hdr);
   if (w->sx) (void)hipStreamDestroy(w->sx);
   delete w;
   e->worker = nullptr;
+}
+
+// the drain thread's copies of one export: exactly the compacted bytes
+// (totals from the mapped header, capped by the caller's capacities)
+static hipError_t worker_copy(drb_engine *e, WorkerState &w,
+                              const WorkerState::Job &j) {
+  const int k = j.k;
+  hipError_t r = hipEventSynchronize(w.ev_staged[k]);
+  if (r != hipSuccess) return r;
+  const unsigned long long *t = w.hdr + 4 * k;
+  const uint64_t nrd = std::min<uint64_t>(t[0], j.b.reads_cap);
+  const uint64_t nval = std::min<uint64_t>(t[1], j.b.values_cap);
+  const uint64_t nap = std::min<uint64_t>(t[2], j.b.applied_cap);
+  struct {
+    void *dst;
+    const void *src;
+    size_t n;
+  } cp[5] = {{j.b.lanes, w.lanes[k], (size_t)e->v.G * 4},
+             {j.b.reads, w.rd[k], nrd * sizeof(drb_worker_read)},
+             {j.b.values, w.val[k], nval * 4},
+             {j.b.value_meta, w.meta[k], (nval + 1) / 2},
+             {j.b.applied, w.ap[k], nap * 4}};
+  for (auto &c : cp)
+    if (c.n && c.dst && r == hipSuccess)
+      r = hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, w.sx);
+  if (r == hipSuccess) r = hipEventRecord(w.ev_drained[k], w.sx);
+  return r;
+}
+
+static void worker_thread(drb_engine *e) {
+  WorkerState &w = *e->worker;
+  (void)hipSetDevice(e->cfg.device);  // (the current device is per thread)
+  for (;;) {
+    WorkerState::Job j;
+    {
+      std::unique_lock<std::mutex> g(w.mu);
+      w.cv.wait(g, [&] { return w.stop || !w.jobs.empty(); });
+      if (w.jobs.empty()) return;  // stop, nothing left
+      j = w.jobs.front();
+      w.jobs.pop_front();
+    }
+    const hipError_t r = worker_copy(e, w, j);
+    {
+      std::lock_guard<std::mutex> g(w.mu);
+      if (r != hipSuccess) w.err = DRB_EDEVICE;
+      w.issued[j.k] = true;
+    }
+    w.cv.notify_all();
+  }
 }
 
 // device staging of at least these capacities (grow-only; growing waits
@@ -286,11 +314,11 @@ static int worker_init(drb_engine *e) {
                                            make_uint4(0, 0, 0, 0),
                                            (int)(G + 1), e->stream));
   HIPCHK(hipMalloc(&w->tmp, std::max<size_t>(w->tmp_bytes, 16)));
-  HIPCHK(hipMalloc(&w->tot, 8 * sizeof(unsigned long long)));
   HIPCHK(hipHostMalloc((void **)&w->hdr, 8 * sizeof(unsigned long long),
                        hipHostMallocMapped));
   memset(w->hdr, 0, 8 * sizeof(unsigned long long));
   HIPCHK(hipHostGetDevicePointer((void **)&w->hdr_dev, w->hdr, 0));
+  w->th = std::thread(worker_thread, e);
   return DRB_OK;
 }
 
@@ -327,26 +355,19 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
     return DRB_EINVAL;
   if (int rc = worker_init(e)) return rc;
   WorkerState &w = *e->worker;
-  // one export in flight per buffer set (the two parities may hold two)
-  if (w.owner[0] == b || w.owner[1] == b) return DRB_EAGAIN;
+  const int k = (int)(w.seq & 1);
+  {
+    // one export in flight per buffer set, and staging[k] free (its
+    // export, two back, waited for: its copies are done)
+    std::lock_guard<std::mutex> g(w.mu);
+    if (w.owner[0] == b || w.owner[1] == b || w.owner[k]) return DRB_EAGAIN;
+  }
   if (int rc = worker_reserve(e, b->reads_cap, b->values_cap, b->applied_cap))
     return rc;
-  void *hl, *hrd, *hval, *hmeta, *hap;
-  if (worker_dev_ptr(b->lanes, &hl) || worker_dev_ptr(b->reads, &hrd) ||
-      worker_dev_ptr(b->values, &hval) ||
-      worker_dev_ptr(b->value_meta, &hmeta) ||
-      worker_dev_ptr(b->applied, &hap))
-    return DRB_EINVAL;
   const View &v = e->v;
   // the reads of the last round, if it served them with results
   const uint32_t n_reads =
       v.read_res && e->reads_round == e->round ? e->reads_n : 0u;
-  const int k = (int)(w.seq & 1);
-  // staging[k] and its owner slot are free once the export two back was
-  // waited for (its drain is then done)
-  if (w.owner[k]) return DRB_EAGAIN;
-  if (w.drained_valid[k])
-    HIPCHK(hipStreamWaitEvent(e->stream, w.ev_drained[k], 0));
   const unsigned blocks = (unsigned)((v.G + 1 + 255) / 256);
   k_worker_count<<<blocks, 256, 0, e->stream>>>(v, slot, n_reads, w.cnt);
   HIPCHK(hipGetLastError());
@@ -354,24 +375,21 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
   HIPCHK(hipcub::DeviceScan::ExclusiveScan(w.tmp, tb, w.cnt, w.off, U4Sum(),
                                            make_uint4(0, 0, 0, 0),
                                            (int)(v.G + 1), e->stream));
-  HIPCHK(hipMemsetAsync(w.meta[k], 0, (std::max<uint64_t>(w.cap_val, 1) / 8 + 2) * 4,
+  HIPCHK(hipMemsetAsync(w.meta[k], 0,
+                        (std::max<uint64_t>(w.cap_val, 1) / 8 + 2) * 4,
                         e->stream));
   k_worker_compact<<<blocks, 256, 0, e->stream>>>(
       v, slot, n_reads, w.off, w.lanes[k], w.rd[k], b->reads_cap, w.val[k],
-      w.meta[k], b->values_cap, w.ap[k], b->applied_cap, w.tot + 4 * k);
+      w.meta[k], b->values_cap, w.ap[k], b->applied_cap, w.hdr_dev + 4 * k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(w.ev_staged[k], e->stream));
-  // the transfer, on the copy stream: PCIe-bound, a few workgroups
-  HIPCHK(hipStreamWaitEvent(w.sx, w.ev_staged[k], 0));
-  k_worker_drain<<<256, 256, 0, w.sx>>>(
-      w.tot + 4 * k, v.G, w.lanes[k], (uint32_t *)hl, w.rd[k], b->reads_cap,
-      (drb_worker_read *)hrd, w.val[k], w.meta[k], b->values_cap,
-      (uint32_t *)hval, (uint8_t *)hmeta, w.ap[k], b->applied_cap,
-      (uint32_t *)hap, w.hdr_dev + 4 * k);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(w.ev_drained[k], w.sx));
-  w.drained_valid[k] = true;
-  w.owner[k] = b;
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    w.owner[k] = b;
+    w.issued[k] = false;
+    w.jobs.push_back(WorkerState::Job{k, *b});
+  }
+  w.cv.notify_all();
   w.seq++;
   return DRB_OK;
 }
@@ -379,16 +397,23 @@ extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
 extern "C" int drb_worker_wait(drb_engine *e, drb_worker_bufs *b) {
   if (!e || !b || !e->worker) return DRB_EINVAL;
   WorkerState &w = *e->worker;
-  // (drb_worker_export keeps at most one export in flight per buffer set)
   int k = -1;
-  for (int q = 0; q < 2; ++q)
-    if (w.owner[q] == b && w.drained_valid[q]) k = q;
-  if (k < 0) return DRB_EINVAL;
+  {
+    std::unique_lock<std::mutex> g(w.mu);
+    for (int q = 0; q < 2; ++q)
+      if (w.owner[q] == b) k = q;
+    if (k < 0) return DRB_EINVAL;
+    w.cv.wait(g, [&] { return w.issued[k]; });
+    if (w.err) return w.err;
+  }
   HIPCHK(hipEventSynchronize(w.ev_drained[k]));
   b->n_reads = w.hdr[4 * k];
   b->n_values = w.hdr[4 * k + 1];
   b->n_applied = w.hdr[4 * k + 2];
-  w.owner[k] = nullptr;
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    w.owner[k] = nullptr;
+  }
   return b->n_reads > b->reads_cap || b->n_values > b->values_cap ||
                  b->n_applied > b->applied_cap
              ? DRB_ERANGE

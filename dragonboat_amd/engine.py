@@ -72,6 +72,7 @@ SIGNATURES = {
     "drb_step_round": (C.c_int, [P, C.POINTER(RoundIn),
                                  C.POINTER(RoundOut)]),
     "drb_step_round_async": (C.c_int, [P, C.POINTER(RoundIn)]),
+    "drb_step_rounds": (C.c_int, [P, C.POINTER(RoundIn), U32, U64]),
     "drb_read_counters": (C.c_int, [P, C.POINTER(RoundOut), C.c_int]),
     "drb_debug_phase": (C.c_int, [P, C.POINTER(U64), C.c_int]),
     "drb_take_flagged": (C.c_int, [P, C.POINTER(Flagged), SZ, C.POINTER(SZ),
@@ -366,6 +367,22 @@ class Engine:
                       int(bool(listed)), prop_replica)
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
+
+    def step_rounds(self, rounds, chunk_groups):
+        """drb_step_rounds: len(rounds) rounds chunk by chunk of the groups;
+        rounds: [dict(tick=, prop_slot=, ri_slot=, reads_per_ctx=,
+        key_space=, encode_saves=)]."""
+        arr = (RoundIn * len(rounds))()
+        for i, r in enumerate(rounds):
+            arr[i] = RoundIn(int(bool(r.get("tick"))),
+                             r.get("prop_slot", abi.DRB_NONE),
+                             r.get("ri_slot", abi.DRB_NONE),
+                             r.get("reads_per_ctx", 0), r.get("key_space", 0),
+                             int(bool(r.get("encode_saves"))),
+                             r.get("ri_replica", 0), 0,
+                             r.get("prop_replica", 0))
+        _ck(lib().drb_step_rounds(self.h, arr, len(rounds), chunk_groups),
+            "drb_step_rounds")
 
     def read_counters(self, reset=True):
         out = RoundOut()

@@ -680,6 +680,17 @@ int drb_step_round(drb_engine *e, const drb_round_in *in, drb_round_out *out);
 /* Same, without the host synchronisation; counters accumulate on device
  * and are read by drb_read_counters(). */
 int drb_step_round_async(drb_engine *e, const drb_round_in *in);
+/* k rounds (in[0..k)) at once, chunk by chunk of the groups: each chunk of
+ * chunk_groups groups (a multiple of 256) runs all k rounds before the
+ * next starts.  Groups are independent -- the reference steps each shard on
+ * its own when it is ready (engine.go:1316-1328, workReady :128-226) -- so
+ * every group goes through exactly the rounds k drb_step_round_async calls
+ * would give it; a chunk's mailbox, state and window rows may stay on-die
+ * between its rounds.  No host synchronisation.  Co-resident replicas only,
+ * without elections, listed rounds, tan records or durable_log
+ * (DRB_EINVAL): those step round by round. */
+int drb_step_rounds(drb_engine *e, const drb_round_in *in, uint32_t k,
+                    uint64_t chunk_groups);
 int drb_read_counters(drb_engine *e, drb_round_out *out, int reset);
 /* Timing builds only: per-phase cycle sums of the step kernels' lanes,
  * out[16] = [follower, leader] x {lanes stepped, load + pre-pass, inbox
