@@ -100,13 +100,16 @@ def test_nonvoting_replication_proposals_and_reads():
     assert p.eng.kv_export(0, NV) == p.eng.kv_export(0, 0)
 
 
-def test_nonvoting_not_in_the_quorum():
+@pytest.mark.parametrize("pre_vote", [0, 1])
+def test_nonvoting_not_in_the_quorum(pre_vote):
     """A stopped voter: the leader, one voter and the nonVoting -- 2 of 3
     voters still commit.  Then a second voter stops: the nonVoting's
     acknowledgements do not make a quorum, nothing commits, and CheckQuorum
-    steps the leader down (raft launch)."""
+    steps the leader down (raft launch); with PreVote the remaining voters'
+    pre-vote campaigns find no quorum either."""
     G, R = 32, 4
-    p = Pair(G=G, R=R, nonvoting_slots=1 << NV, elections=1)
+    p = Pair(G=G, R=R, nonvoting_slots=1 << NV, elections=1,
+             pre_vote=pre_vote)
     st = {"committed": 0, "slow": 0}
     for r in range(3):
         _round(p, st, k=1, tick=True)
@@ -130,13 +133,16 @@ def test_nonvoting_not_in_the_quorum():
     assert sts[NV].role == abi.NONVOTING and sts[0].role != abi.LEADER
 
 
+@pytest.mark.parametrize("pre_vote", [0, 1])
 @pytest.mark.parametrize("kind", ["witness", "nonvoting"])
-def test_member_never_campaigns(kind):
+def test_member_never_campaigns(kind, pre_vote):
     """The leader stops: a voter is elected; the member keeps its role (a
-    witness votes, a nonVoting does not) and follows the new leader."""
+    witness votes and grants pre-votes -- the any-state RequestPreVote
+    branch of the passive roles, raft.go:1670-1695 --, a nonVoting does
+    neither) and follows the new leader."""
     G, R = 24, 4
     kw = {kind + "_slots": 1 << NV}
-    p = Pair(G=G, R=R, elections=1, **kw)
+    p = Pair(G=G, R=R, elections=1, pre_vote=pre_vote, **kw)
     want = abi.WITNESS if kind == "witness" else abi.NONVOTING
     st = {"committed": 0, "slow": 0}
     for r in range(3):
@@ -156,6 +162,36 @@ def test_member_never_campaigns(kind):
     for r in range(6):
         _round(p, st, k=1, tick=(r % 2 == 0), read_index=True,
                ri_replica=0)
+
+
+@pytest.mark.parametrize("pre_vote", [0, 1])
+def test_witness_vote_makes_the_quorum(pre_vote):
+    """Two voters and a witness (quorum 2 of 3): when the leader stops, the
+    remaining voter wins only with the witness's pre-vote (PreVote) and
+    vote -- the witness's term gate and vote handlers decide the election
+    (raft.go:1507-1590, 1670-1722), bit-exact with the oracle."""
+    G, R = 24, 3
+    p = Pair(G=G, R=R, elections=1, witness_slots=1 << 2, pre_vote=pre_vote)
+    st = {"committed": 0, "slow": 0}
+    for r in range(3):
+        _round(p, st, k=1, tick=True)
+    for g in range(G):
+        p.orc.set_hosted(g, 0, False)
+    p.eng.host_slot(0, False)
+    elected = False
+    for r in range(80):
+        _round(p, st, k=0, tick=True)
+        roles = [_roles(p, g) for g in range(G)]
+        assert all(rs[2] == abi.WITNESS for rs in roles)
+        if all(rs[1] == abi.LEADER for rs in roles):
+            elected = True
+            break
+    assert elected and st["slow"] > 0, st
+    c0 = st["committed"]
+    for r in range(6):
+        _round(p, st, k=1, tick=(r % 2 == 0), read_index=True,
+               ri_replica=0)
+    assert st["committed"] - c0 >= G * 3, st
 
 
 @pytest.mark.parametrize("kind,N", [("witness", 2), ("nonvoting", 3)])

@@ -9,6 +9,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <thread>
+
 #define CK(x)                                                          \
   do {                                                                 \
     hipError_t e_ = (x);                                               \
@@ -95,6 +97,70 @@ int main() {
       free(h);
     } else {
       CK(hipHostFree(h));
+    }
+  }
+  // the step worker's situation: pinned mapped host buffers, several
+  // streams, an H2D upload in flight, copies issued from another thread
+  {
+    void *h, *hu;
+    CK(hipHostMalloc(&h, B, hipHostMallocMapped));
+    CK(hipHostMalloc(&hu, B, hipHostMallocDefault));
+    void *du;
+    CK(hipMalloc(&du, B));
+    hipStream_t ss[4];
+    for (auto &x : ss) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (int nstr : {1, 2, 4}) {
+      for (int rep = 0; rep < 3; ++rep) {
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a0, ss[0]));
+        for (int q = 1; q < nstr; ++q) CK(hipStreamWaitEvent(ss[q], a0, 0));
+        const size_t part = B / nstr;
+        for (int q = 0; q < nstr; ++q)
+          CK(hipMemcpyAsync((char *)h + q * part, (char *)dsrc + q * part,
+                            part, hipMemcpyDeviceToHost, ss[q]));
+        for (int q = 1; q < nstr; ++q) {
+          CK(hipEventRecord(b0, ss[q]));
+          CK(hipStreamWaitEvent(ss[0], b0, 0));
+        }
+        CK(hipEventRecord(a1, ss[0]));
+        CK(hipEventSynchronize(a1));
+        float t;
+        CK(hipEventElapsedTime(&t, a0, a1));
+        if (rep == 2)
+          printf("d2h on %d streams: %.3f ms (%.1f GB/s)\n", nstr, t,
+                 B / t / 1e6);
+      }
+    }
+    // with a 64 MiB H2D on another stream at the same time
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(a0, ss[0]));
+      CK(hipStreamWaitEvent(ss[1], a0, 0));
+      CK(hipMemcpyAsync(du, hu, B, hipMemcpyHostToDevice, ss[1]));
+      CK(hipMemcpyAsync(h, dsrc, B, hipMemcpyDeviceToHost, ss[0]));
+      CK(hipEventRecord(a1, ss[0]));
+      CK(hipEventRecord(b1, ss[1]));
+      CK(hipDeviceSynchronize());
+      float t1, t2;
+      CK(hipEventElapsedTime(&t1, a0, a1));
+      CK(hipEventElapsedTime(&t2, a0, b1));
+      if (rep == 2)
+        printf("d2h beside h2d: d2h %.3f ms, h2d done at %.3f ms\n", t1, t2);
+    }
+    // issued from another host thread
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipDeviceSynchronize());
+      float t = 0;
+      std::thread th([&]() {
+        CK(hipSetDevice(0));
+        CK(hipEventRecord(a0, ss[2]));
+        CK(hipMemcpyAsync(h, dsrc, B, hipMemcpyDeviceToHost, ss[2]));
+        CK(hipEventRecord(a1, ss[2]));
+        CK(hipEventSynchronize(a1));
+        CK(hipEventElapsedTime(&t, a0, a1));
+      });
+      th.join();
+      if (rep == 2) printf("d2h from another thread: %.3f ms\n", t);
     }
   }
   return 0;
