@@ -45,10 +45,17 @@ def alg_bytes_per_group_round(R=3, k=1, P=16, reads=True, spread=False):
     return b_round + b_entries + b_apply + b_read + b_msg
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_current.json")
+PMC_DIR = os.path.join(ROOT, "profiles")
 
 
-def pmc_traffic(G, R):
+def pmc_file(key):
+    """the committed PMC summary of a workload: C3's is pmc_current.json,
+    the others pmc_<workload>.json (tools/prof_workloads.sh)"""
+    return os.path.join(PMC_DIR, "pmc_current.json" if key == "c3" else
+                        "pmc_%s.json" % key)
+
+
+def pmc_traffic(key, G, R):
     """HBM bytes per round from the committed rocprofv3 PMC passes of this
     workload (tools/pmc_summary.py over the timed rounds' step kernels):
     (FETCH_SIZE x2 + WRITE_SIZE, FETCH_SIZE + WRITE_SIZE).  The first is an
@@ -57,7 +64,7 @@ def pmc_traffic(G, R):
     second the matching lower bound.  (None, None) when no summary matches
     this configuration."""
     try:
-        s = json.load(open(PMC_SUMMARY))
+        s = json.load(open(pmc_file(key)))
     except (OSError, ValueError):
         return None, None
     if s.get("groups") != G or s.get("replicas") != R:
@@ -119,6 +126,11 @@ def parse():
                          "(drb_round_in.listed; default: on for c5)")
     ap.add_argument("--quiesce", type=int, default=-1,
                     help="Config.Quiesce (default: on for c5, SURVEY 8d)")
+    ap.add_argument("--c5-warm", type=int, default=400,
+                    help="c5: rounds run before the warmup, ticking every "
+                         "round, so the timed rounds see the quiesced "
+                         "steady state (quiesceState: 20 x ElectionRTT = 200 "
+                         "idle ticks, quiesce.go:44-82)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--save", default="",
                     choices=["", "none", "entrybatch", "tan", "tanmux"],
@@ -188,6 +200,7 @@ C5_VAL = {128: 116, 1024: 1011}
 # (put_value_long: a block per distinct key, bump-allocated)
 C5_KEYS = KEY_SPACE
 C5_SLOTS = 32
+C5_WARM_BASE = 1 << 23  # the pre-warm rounds' draws (salt = round)
 C5_OVF_PER = 1 / 64
 
 
@@ -423,6 +436,7 @@ def main():
     c4 = args.workload == "c4"
     c5 = args.workload == "c5"
     c2 = args.workload == "c2"
+    c3 = args.workload == "c3"
     if c2:  # 64k groups, 16 B writes, replicas co-resident
         args.no_read_index = True
         if args.groups == 1 << 20:
@@ -473,7 +487,7 @@ def main():
         # the KV: C5_SLOTS keys per replica, the values in one shared pool
         # sized for the keys the run writes (c5_pool_blocks)
         ks = C5_SLOTS
-        c5_rounds = 2 * args.warmup + args.steps + 8
+        c5_rounds = args.c5_warm + 2 * args.warmup + args.steps + 8
         eng = Engine(num_groups=G, num_replicas=R, window=8, cmd_cap=cmd_cap,
                      max_props=max(1, k), prop_slots=NP, ri_slots=1,
                      mailbox=8, kv_slots=ks, kv_val_cap=vlen + 13 & ~15,
@@ -555,6 +569,26 @@ def main():
             stage(0, WARM_SALT + i)
         step(i, 0 if not c5 else None)
 
+    quiesce_info = None
+    if c5 and args.c5_warm > 0:
+        # C5's steady state: at 1 % of the groups proposing per round, a
+        # group stays idle for the 200 ticks quiesceState needs with
+        # probability ~0.99^200 = 13 %; these rounds (their own draws, a
+        # tick each) get the timed rounds past that threshold
+        for j in range(args.c5_warm):
+            step(C5_WARM_BASE + j)
+            if j % 128 == 127:
+                eng.sync()
+        eng.sync()
+        # the quiesced replicas on a sample of 64 runs of 64 groups
+        n_q = n_s = 0
+        for r0 in range(0, G - 64 + 1, max(64, G // 64))[:64]:
+            for st in eng.export_replicas(r0, 64):
+                n_s += 1
+                n_q += st.qs_quiesced_since > 0
+        quiesce_info = {"warm_rounds": args.c5_warm,
+                        "quiesced_fraction": n_q / max(1, n_s),
+                        "sampled_replicas": n_s}
     tw0 = time.perf_counter()
     for i in range(args.warmup):
         warm_step(i)
@@ -637,8 +671,13 @@ def main():
         if saves:  # + the save bytes the round writes
             alg += out.saved_bytes / K
     achieved = alg / (kern_ms * 1e-3) / 1e9
-    traffic = (None, None) if (c2 or c4 or c5 or args.kv_fill == 0) else \
-        pmc_traffic(G, R)
+    # the workload's committed PMC summary (C3 at the KV steady state; C4
+    # at N = 1 only, its per-GPU share differs with N)
+    pmc_key = ("c5_%d" % args.payload if c5 else "c4" if c4 else
+               "c2" if c2 else "c3")
+    traffic = (None, None) if ((c3 and args.kv_fill == 0) or
+                               (c4 and world > 1)) else \
+        pmc_traffic(pmc_key, G, R)
     chunk_ab = None
     if args.chunk_ab and not (c4 or c5):
         # the same rounds (the timed batches again, slot b = i % NP) as K
@@ -826,9 +865,10 @@ def main():
         h0 = time.perf_counter()
         for i in range(KH):
             b = i % HB
-            eng.stage_proposals_packed(b, _abi.ENTRY_ENCODED, *hp[b])
+            eng.stage_proposals_packed_async(b, _abi.ENTRY_ENCODED, *hp[b])
             step(2 * args.warmup + K + i, b)
         eng.sync()
+        eng.stage_wait_upload()
         hms = (time.perf_counter() - h0) * 1e3 / KH
         hout = eng.read_counters(reset=True)
         host_staged = {
@@ -837,10 +877,11 @@ def main():
                                                                  1e-3),
             "upload_bytes_per_round": int(sum(x.numel() for x in hb[0])),
             "note": "proposals staged from pinned host memory every round "
-                    "in the packed form (drb_stage_proposals_packed: Key, "
-                    "ClientID, Cmd length and bytes per entry, one H2D per "
-                    "array on a copy stream overlapping the previous round, "
-                    "+ scans and a layout kernel), timed around the whole "
+                    "in the packed form (drb_stage_proposals_packed_async: "
+                    "Key, ClientID, Cmd length and bytes per entry, one H2D "
+                    "per array on a copy stream overlapping the previous "
+                    "round, + scans and a layout kernel; the host waits for "
+                    "an upload at the next call), timed around the whole "
                     "loop; not `value`"}
         if args.step_worker < 0:
             args.step_worker = int(reads and not c2 and args.read_results)
@@ -854,28 +895,50 @@ def main():
             wb = [eng.worker_bufs(2 * G, 2 * G * READS_PER_CTX, 4 * G * k)
                   for _ in range(2)]
             KW = max(5, K)
-            down = [0, 0, 0]
+            WW = max(2, args.warmup)
+
+            def worker_loop(n, r0):
+                # a step worker's iteration: the round (its proposals
+                # staged one iteration ahead), the export behind it, the
+                # next round's entry queue up while it runs, then the
+                # outputs of the round before it (their copy ran beside
+                # this round)
+                got = [0, 0, 0]
+                marks = []
+                eng.stage_proposals_packed_async(0, _abi.ENTRY_ENCODED,
+                                                 *hp[0])
+                pc = time.perf_counter
+                for i in range(n):
+                    t = [pc()]
+                    step(r0 + i, i % HB)
+                    t.append(pc())
+                    eng.worker_export(0, wb[i % 2])
+                    t.append(pc())
+                    if i + 1 < n:
+                        b1 = (i + 1) % HB
+                        eng.stage_proposals_packed_async(
+                            b1, _abi.ENTRY_ENCODED, *hp[b1])
+                    t.append(pc())
+                    if i >= 1:
+                        n3 = eng.worker_wait(wb[(i - 1) % 2])
+                        got = [d + x for d, x in zip(got, n3)]
+                    t.append(pc())
+                    marks.append(t[-1])
+                    phases.append([b - a for a, b in zip(t, t[1:])])
+                n3 = eng.worker_wait(wb[(n - 1) % 2])
+                eng.stage_wait_upload()
+                return [d + x for d, x in zip(got, n3)], marks
+
+            r0 = 2 * args.warmup + K + KH
+            phases = []
+            worker_loop(WW, r0)  # untimed: first copies, host pages
+            phases = []
             eng.read_counters(reset=True)
             eng.sync()
             w0 = time.perf_counter()
-            # a step worker's iteration: the round (its proposals staged
-            # one iteration ahead), the export behind it, the next round's
-            # entry queue up while it runs, then the outputs of the round
-            # before it (their copy ran beside this round)
-            eng.stage_proposals_packed(0, _abi.ENTRY_ENCODED, *hp[0])
-            for i in range(KW):
-                step(2 * args.warmup + K + KH + i, i % HB)
-                eng.worker_export(0, wb[i % 2])
-                if i + 1 < KW:
-                    b1 = (i + 1) % HB
-                    eng.stage_proposals_packed(b1, _abi.ENTRY_ENCODED,
-                                               *hp[b1])
-                if i >= 1:
-                    n3 = eng.worker_wait(wb[(i - 1) % 2])
-                    down = [d + x for d, x in zip(down, n3)]
-            n3 = eng.worker_wait(wb[(KW - 1) % 2])
-            down = [d + x for d, x in zip(down, n3)]
+            down, marks = worker_loop(KW, r0 + WW)
             wms = (time.perf_counter() - w0) * 1e3 / KW
+            its = sorted((b - a) * 1e3 for a, b in zip([w0] + marks, marks))
             wout = eng.read_counters(reset=True)
             for bw in wb:
                 eng.free_worker_bufs(bw)
@@ -886,7 +949,16 @@ def main():
             dbytes = (KW * G * 4 + down[0] * _C.sizeof(_abi.WorkerRead) +
                       down[1] * 4 + (down[1] + KW) // 2 + down[2] * 4) / KW
             step_worker = {
-                "ms_per_step": wms, "steps": KW,
+                "ms_per_step": wms, "steps": KW, "warmup": WW,
+                "iteration_ms_median": its[len(its) // 2],
+                "iteration_ms_max": its[-1],
+                # host time per call, medians: the round's launches, the
+                # export, the next round's staging (waits for its upload),
+                # the wait for the previous export's copies
+                "host_ms": dict(zip(
+                    ("round", "export", "stage", "wait"),
+                    (round(sorted(x)[len(x) // 2] * 1e3, 4)
+                     for x in zip(*phases)))),
                 "committed_entries_per_s": wout.committed_entries /
                 (wms * KW * 1e-3),
                 "upload_bytes_per_round": int(sum(x.numel()
@@ -992,7 +1064,8 @@ def main():
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic[0],
                 "traffic_lower": traffic[1],
-                "traffic_source": "profiles/pmc_current.json (rocprofv3, "
+                "traffic_source": os.path.relpath(pmc_file(pmc_key), ROOT) +
+                                  " (rocprofv3, "
                                   "the timed rounds' step kernels, bytes per "
                                   "round): traffic = FETCH_SIZE x2 + "
                                   "WRITE_SIZE, an upper bound (the x2 is for "
@@ -1017,10 +1090,14 @@ def main():
                          "saved_bytes": out.saved_bytes},
         }
         if c5:
+            if quiesce_info is not None:
+                quiesce_info["stepped_fraction"] = \
+                    out.replicas_stepped / K / (G * R)
+                res["quiesce"] = quiesce_info
             # C5's rounds are mostly heartbeats of the groups that do not
-            # propose (no group reaches the quiesce threshold with a tick
-            # every round): a second figure counts, on top of the entry
-            # bytes, each stepped replica's 64 B state record read + write
+            # propose (past the pre-warm ~13 % of them are quiesced and
+            # skipped by the listed rounds): a second figure counts, on top
+            # of the entry bytes, each stepped replica's 64 B state record read + write
             # and each message's 16 B record written + read
             hb = (out.replicas_stepped * 128 + out.messages * 32) / K
             ach2 = (alg + hb) / (kern_ms * 1e-3) / 1e9

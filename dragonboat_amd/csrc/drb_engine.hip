@@ -1171,10 +1171,13 @@ __global__ void k_stage_packed(View v, uint32_t slot, uint32_t type,
   }
 }
 
-extern "C" int drb_stage_proposals_packed(
-    drb_engine *e, uint32_t slot, uint32_t type, const uint8_t *counts,
-    uint64_t n_entries, const uint64_t *keys, const uint64_t *client_ids,
-    const uint16_t *cmd_lens, const uint8_t *pool, size_t pool_len) {
+// drb_stage_proposals_packed(_async): `async` returns with the upload
+// queued, once the previous call's upload is done (its arrays free)
+static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
+                        const uint8_t *counts, uint64_t n_entries,
+                        const uint64_t *keys, const uint64_t *client_ids,
+                        const uint16_t *cmd_lens, const uint8_t *pool,
+                        size_t pool_len, bool async) {
   if (!e || slot >= e->cfg.prop_slots) return DRB_ERANGE;
   if (!counts || (n_entries && (!keys || !client_ids || !cmd_lens)) ||
       (pool_len && !pool))
@@ -1220,6 +1223,8 @@ extern "C" int drb_stage_proposals_packed(
     e->stage_bytes = need;
   }
   uint8_t *d = (uint8_t *)e->stage_buf;
+  // the previous call's arrays are read once its upload is done
+  if (async) HIPCHK(hipEventSynchronize(e->ev_uploaded));
   // the upload and the layout on the copy stream: the upload overlaps the
   // running round; the layout waits only for the engine-stream work on
   // this slot (ev_prop), so it runs beside a round that reads another
@@ -1269,6 +1274,28 @@ extern "C" int drb_stage_proposals_packed(
   HIPCHK(hipEventRecord(e->ev_staged, ls));
   HIPCHK(hipEventRecord(e->ev_stage_free, ls));
   HIPCHK(hipStreamWaitEvent(e->stream, e->ev_staged, 0));
+  if (!async) HIPCHK(hipEventSynchronize(e->ev_uploaded));
+  return DRB_OK;
+}
+
+extern "C" int drb_stage_proposals_packed(
+    drb_engine *e, uint32_t slot, uint32_t type, const uint8_t *counts,
+    uint64_t n_entries, const uint64_t *keys, const uint64_t *client_ids,
+    const uint16_t *cmd_lens, const uint8_t *pool, size_t pool_len) {
+  return stage_packed(e, slot, type, counts, n_entries, keys, client_ids,
+                      cmd_lens, pool, pool_len, false);
+}
+
+extern "C" int drb_stage_proposals_packed_async(
+    drb_engine *e, uint32_t slot, uint32_t type, const uint8_t *counts,
+    uint64_t n_entries, const uint64_t *keys, const uint64_t *client_ids,
+    const uint16_t *cmd_lens, const uint8_t *pool, size_t pool_len) {
+  return stage_packed(e, slot, type, counts, n_entries, keys, client_ids,
+                      cmd_lens, pool, pool_len, true);
+}
+
+extern "C" int drb_stage_wait_upload(drb_engine *e) {
+  if (!e) return DRB_EINVAL;
   HIPCHK(hipEventSynchronize(e->ev_uploaded));
   return DRB_OK;
 }

@@ -54,6 +54,10 @@ SIGNATURES = {
     "drb_stage_proposals_packed": (C.c_int, [P, U32, U32, PU8, U64, PU64,
                                              PU64, C.POINTER(C.c_uint16),
                                              PU8, SZ]),
+    "drb_stage_proposals_packed_async": (C.c_int, [P, U32, U32, PU8, U64, PU64,
+                                             PU64, C.POINTER(C.c_uint16),
+                                             PU8, SZ]),
+    "drb_stage_wait_upload": (C.c_int, [P]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
     "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
                                               U64, U32]),
@@ -300,6 +304,17 @@ class Engine:
                                              keys, clients, lens, pool,
                                              pool_len),
             "drb_stage_proposals_packed")
+
+    def stage_proposals_packed_async(self, slot, type, counts, n, keys,
+                                     clients, lens, pool, pool_len):
+        """drb_stage_proposals_packed_async: the arrays stay in use until
+        the next call (or stage_wait_upload) returns."""
+        _ck(lib().drb_stage_proposals_packed_async(
+            self.h, slot, type, counts, n, keys, clients, lens, pool,
+            pool_len), "drb_stage_proposals_packed_async")
+
+    def stage_wait_upload(self):
+        _ck(lib().drb_stage_wait_upload(self.h), "drb_stage_wait_upload")
 
     def gen_kv_proposals(self, slot, k, key_space, val_len, seed, salt,
                          active_ppm=1000000):

@@ -563,6 +563,20 @@ int drb_stage_proposals_packed(drb_engine *e, uint32_t slot, uint32_t type,
                                const uint64_t *client_ids,
                                const uint16_t *cmd_lens, const uint8_t *pool,
                                size_t pool_len);
+/* The same, pipelined one call deep for a step worker that stages round
+ * t + 1 while round t runs: returns once the previous call's upload is done
+ * (that call's arrays are then the caller's again) and this call's upload
+ * is queued.  The arrays stay in use until the next call, or
+ * drb_stage_wait_upload, returns; pinned host memory required.  Replaces
+ * the same entryQueue.add (queue.go:60) as drb_stage_proposals_packed. */
+int drb_stage_proposals_packed_async(drb_engine *e, uint32_t slot,
+                                     uint32_t type, const uint8_t *counts,
+                                     uint64_t n_entries, const uint64_t *keys,
+                                     const uint64_t *client_ids,
+                                     const uint16_t *cmd_lens,
+                                     const uint8_t *pool, size_t pool_len);
+/* Until the last staged upload is done (its host arrays free). */
+int drb_stage_wait_upload(drb_engine *e);
 /* Device-side synthetic proposal generator (bench / SURVEY 8d inputs):
  * k KVTest PBKV writes per group, NoOP session, EncodedEntry v0. */
 int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,

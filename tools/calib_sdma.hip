@@ -133,6 +133,38 @@ int main() {
     printf("beside the kernel, %d engine(s): copy %.3f ms, kernel %.3f ms "
            "(alone %.3f)\n", n, tc, tk2, tk);
   }
+  // a hipMemcpyAsync H2D (the staged proposals' upload) beside a D2H on
+  // each of the first engines: does HIP's engine choice collide with it?
+  {
+    void *hu, *du;
+    CK(hipHostMalloc(&hu, B, hipHostMallocDefault));
+    CK(hipMalloc(&du, B));
+    const double tu0 = now_ms();
+    CK(hipMemcpyAsync(du, hu, B, hipMemcpyHostToDevice, s2));
+    CK(hipStreamSynchronize(s2));
+    printf("h2d alone: %.3f ms\n", now_ms() - tu0);
+    for (size_t i = 0; i < eng.size() && i < 4; ++i) {
+      std::swap(eng[0], eng[i]);
+      double tc = 0, tu = 0;
+      for (int rep = 0; rep < 3; ++rep) {
+        const double t0 = now_ms();
+        hsa_signal_store_relaxed(sig[0], 1);
+        HK(hsa_amd_memory_async_copy_on_engine(
+            h, g_cpu, dsrc, g_gpu, B, 0, nullptr, sig[0],
+            (hsa_amd_sdma_engine_id_t)(1u << eng[0]), true));
+        CK(hipMemcpyAsync(du, hu, B, hipMemcpyHostToDevice, s2));
+        CK(hipStreamSynchronize(s2));
+        tu = now_ms() - t0;
+        while (hsa_signal_wait_scacquire(sig[0], HSA_SIGNAL_CONDITION_LT, 1,
+                                         UINT64_MAX, HSA_WAIT_STATE_ACTIVE))
+          ;
+        tc = now_ms() - t0;
+      }
+      printf("d2h on engine %d beside a hip h2d: d2h done %.3f ms, h2d done "
+             "%.3f ms\n", eng[0], tc, tu);
+      std::swap(eng[0], eng[i]);
+    }
+  }
   for (auto &s : sig) hsa_signal_destroy(s);
   HK(hsa_shut_down());
   return 0;

@@ -1,10 +1,9 @@
 """The step-worker loop as rocprofv3 saw it (--kernel-trace
---memory-copy-trace): for the last N rounds of the loop (each ends with a
-k_worker_drain), every kernel and copy relative to the round's first
-dispatch, with its queue, and per round the spans of the step kernels, the
-export's compaction, the drain (device writes into pinned host memory) and
-the proposal upload (H2D copies).  Shows whether the drain of round t
-overlaps round t + 1.
+--memory-copy-trace): for the last N rounds of the loop (each starts with
+the export's k_worker_count), every kernel and copy relative to the round's
+first dispatch, with its queue, then the period between exports, the
+exports' D2H copy time per round and the mean step kernel.  Shows whether
+the copies of round t overlap round t + 1 and what they cost its kernels.
 
 usage: python tools/worker_timeline.py <trace dir> [N] [out.txt]
 """
@@ -43,7 +42,6 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     out = open(sys.argv[3], "w") if len(sys.argv) > 3 else sys.stdout
     ev = load(d)
-    drains = [i for i, e in enumerate(ev) if e[3].startswith("k_worker_drain")]
     counts = [i for i, e in enumerate(ev) if e[3].startswith("k_worker_count")]
     if len(counts) < n + 1:
         print("no step-worker loop in the trace", file=out)
@@ -66,13 +64,16 @@ def main():
     for i in range(len(counts) - n, len(counts)):
         per.append(ev[counts[i]][0])
     periods = [(b - a) / 1e3 for a, b in zip(per, per[1:])]
-    dr = [(ev[i][1] - ev[i][0]) / 1e3 for i in drains[-n:]]
+    d2h = []
+    for a, b in zip(per, per[1:]):
+        d2h.append(sum(e[1] - e[0] for e in ev if a <= e[0] < b and
+                       e[2] == "C" and "DEVICE_TO_HOST" in e[3]) / 1e3)
     steps = [(e[1] - e[0]) / 1e3 for e in ev[-4 * n * 40:]
              if e[3].startswith("step_kernel")]
     print("period between exports (us): %s" %
           ", ".join("%.0f" % p for p in periods), file=out)
-    print("drain kernel durations (us): %s" %
-          ", ".join("%.0f" % x for x in dr), file=out)
+    print("D2H copy time per period (us): %s" %
+          ", ".join("%.0f" % x for x in d2h), file=out)
     if steps:
         print("step kernels in the window: %d, mean %.0f us" %
               (len(steps), sum(steps) / len(steps)), file=out)
