@@ -313,3 +313,27 @@ def test_ingest_wire_wide_steps_and_warm_reruns():
         t.round(k=1, tick=True, read_index=r == 1)
     errs = t.check()
     assert not errs, errs[:2]
+
+
+def test_ingest_wire_first_call_without_a_whole_frame():
+    """A fresh receiver's first drb_ingest_wire calls hold no whole frame:
+    an empty stream, then a cut inside the first request header, then one
+    inside the first payload (the call the round-4 crash came from: the
+    upload pipeline's first event recorded before any piece existed,
+    DESIGN §7a).  Nothing is consumed; the whole stream then goes in and
+    the round after it stays bit-exact with the oracle cluster."""
+    from dragonboat_amd import abi
+    t = TwoNodes(G=16)
+    hb = po.msg(abi.MSG["Heartbeat"], from_=1, to=2, term=2, shard_id=1)
+    data = po.wire_frame(po.messagebatch_marshal([hb] * 4, t.did, SRC))
+    assert len(data) > 40
+    for cut in (0, 9, 40):
+        got = t.foll.ingest_wire(data[:cut], t.did)
+        assert got["consumed"] == 0 and got["messages"] == 0, (cut, got)
+        assert got["bad"] == 0 and got["accepted"] == 0, (cut, got)
+    o, a, b = t.round(k=1, tick=True)
+    errs = t.check()
+    assert not errs, errs[:2]
+    got = t.foll.ingest_wire_pinned(t.foll.ingest_buffer(data[:30]), 30,
+                                    t.did)
+    assert got["consumed"] == 0 and got["messages"] == 0, got
