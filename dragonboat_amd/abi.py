@@ -230,6 +230,12 @@ class Region(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
 
 
+class Xfer(C.Structure):
+    """drb_xfer: one transfer of the fixed exchange (drb_exchange_plan)."""
+    _fields_ = [("peer", C.c_uint32), ("recv", C.c_uint32),
+                ("ptr", C.c_void_p), ("bytes", C.c_uint64)]
+
+
 PLANE_REGIONS = 10
 PLANE_C1 = 1 << 18
 

@@ -124,7 +124,7 @@ def build(force=False, verbose=False, out=None, defines=(), jobs=None,
             list(ex.map(_compile, todo))
     tmp = target + ".tmp"
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", tmp] + \
-        objs + ["-lhsa-runtime64"]
+        objs + ["-lhsa-runtime64", "-lrccl"]
     if verbose:
         print(" ".join(cmd[:6]) + " <%d objects>" % len(objs), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -24,7 +24,9 @@
 // Error behaviour follows the host transport: a frame whose header or
 // payload CRC fails, or whose batch does not decode, is ErrBadMessage --
 // the frames before it are delivered, it and the rest are not
-// (drb_wire_in.bad, .consumed); a snapshot chunk frame (method 200) and an
+// (drb_wire_in.bad, .consumed); a stream that ends inside a sound frame is
+// not bad: .consumed stops before it, for the transport to hand in again
+// with the bytes that follow; a snapshot chunk frame (method 200) and an
 // InstallSnapshot message are counted for the CPU path.
 #pragma once
 

@@ -159,13 +159,22 @@ struct Frame {
 // the whole frames of a stream (tcp.go:64-112, 180-237), reusing fr's
 // vectors (a warm call neither faults nor frees); returns the bytes of the
 // whole frames, *bad set when a header is malformed or its CRC fails (the
-// frames before it are kept: ErrBadMessage closes the connection there)
+// frames before it are kept: ErrBadMessage closes the connection there).
+// A stream that ends inside a frame whose bytes so far are sound -- the
+// magic's first bytes, or a whole header whose payload has not all arrived
+// -- is not bad: readMessage would still be waiting for the rest
+// (io.ReadFull), so the walk stops before it and the transport hands those
+// bytes in again with what follows.
 static size_t walk_frames(const uint8_t *stream, size_t len,
                           std::vector<Frame> &fr, bool *bad) {
   size_t nfr = 0, i = 0;
   *bad = false;
   while (i < len) {
-    if (len - i < 20 || stream[i] != 0xAE || stream[i + 1] != 0x7D) {
+    if (len - i < 20) {  // a header still arriving, if its magic is sound
+      *bad = stream[i] != 0xAE || (len - i > 1 && stream[i + 1] != 0x7D);
+      break;
+    }
+    if (stream[i] != 0xAE || stream[i + 1] != 0x7D) {
       *bad = true;
       break;
     }
@@ -176,10 +185,11 @@ static size_t walk_frames(const uint8_t *stream, size_t len,
     const uint32_t method = (uint32_t)be(h, 2);
     const uint64_t size = be(h + 2, 8);
     if (crc32_small(h, 18) != hcrc || (method != 100 && method != 200) ||
-        size == 0 || size > len - i - 20) {
+        size == 0) {
       *bad = true;
       break;
     }
+    if (size > len - i - 20) break;  // its payload still arriving
     if (nfr == fr.size()) fr.emplace_back();
     Frame &f = fr[nfr++];
     f.off = i + 20;

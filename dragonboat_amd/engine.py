@@ -126,6 +126,10 @@ SIGNATURES = {
     "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
     "drb_exchange_local_counted": (C.c_int, [C.POINTER(P), U32]),
     "drb_exchange_mark": (C.c_int, [P]),
+    "drb_exchange_plan": (C.c_int, [P, U32, C.POINTER(abi.Xfer), SZ,
+                                    C.POINTER(SZ)]),
+    "drb_exchange_rccl": (C.c_int, [P, P, U32]),
+    "drb_exchange_rccl_roles": (C.c_int, [P, P, PU32]),
     "drb_exchange_bytes": (C.c_int, [P, C.POINTER(U64), C.c_int]),
     "drb_encode_wire": (C.c_int, [P, U32, U32, C.POINTER(WireCfg),
                                   C.POINTER(WireOut)]),
@@ -674,6 +678,29 @@ class Engine:
         _ck(lib().drb_exchange_bytes(self.h, C.byref(b), int(bool(reset))),
             "drb_exchange_bytes")
         return b.value
+
+    def exchange_plan(self, leader_mask):
+        """drb_exchange_plan: [(peer, recv, device address, bytes)] of this
+        rank's fixed-capacity exchange step, in posting order."""
+        n = SZ()
+        _ck(lib().drb_exchange_plan(self.h, leader_mask, None, 0,
+                                    C.byref(n)), "drb_exchange_plan")
+        arr = (abi.Xfer * max(1, n.value))()
+        _ck(lib().drb_exchange_plan(self.h, leader_mask, arr, n.value,
+                                    C.byref(n)), "drb_exchange_plan")
+        return [(arr[i].peer, arr[i].recv, arr[i].ptr, arr[i].bytes)
+                for i in range(n.value)]
+
+    def exchange_rccl(self, comm, leader_mask):
+        """drb_exchange_rccl over an ncclComm_t (an address)."""
+        _ck(lib().drb_exchange_rccl(self.h, comm, leader_mask),
+            "drb_exchange_rccl")
+
+    def exchange_rccl_roles(self, comm):
+        m = U32()
+        _ck(lib().drb_exchange_rccl_roles(self.h, comm, C.byref(m)),
+            "drb_exchange_rccl_roles")
+        return m.value
 
     def exchange_mark(self):
         """This rank's own exchange of the last round is enqueued (RCCL):

@@ -1054,6 +1054,39 @@ int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
  *    bounds) by peer copies, so no counts are read.
  * The receivers read only what the plane headers count. */
 int drb_exchange_local(drb_engine *const *engines, uint32_t n);
+/* The fixed-capacity exchange step of a process-per-GPU host as a list of
+ * point-to-point transfers: every remote plane that can carry fast-path
+ * messages -- a leader slot at either end on some rank (leader_mask: the
+ * OR over the ranks of drb_role_slots' leader_slots; every plane with
+ * drb_config.elections) -- at its full capacity (what the step pre-pass
+ * bounds), its drb_plane_regions sent to the rank the plane goes to and
+ * received from the rank it comes from.  Every rank lists its transfers in
+ * the same (from, to, region) order, so each pair of ranks posts matching
+ * sends and receives (dragonboat_amd/exchange.py plan(), fixed mode).
+ * *n_xfers = the count; DRB_ERANGE when it exceeds cap (xfers may be NULL
+ * with cap 0 to size the list).  Empty before the first round and with
+ * place_world < 2. */
+typedef struct drb_xfer {
+  uint32_t peer;  /* the other rank */
+  uint32_t recv;  /* 0: send this region, 1: receive into it */
+  void *ptr;      /* device address */
+  uint64_t bytes;
+} drb_xfer;
+int drb_exchange_plan(drb_engine *e, uint32_t leader_mask, drb_xfer *xfers,
+                      size_t cap, size_t *n_xfers);
+/* The same step over RCCL (xGMI between the GPUs of a node): the transfers
+ * as ncclSend / ncclRecv in one ncclGroupStart .. ncclGroupEnd on the
+ * engine stream -- behind the round that wrote the outbox planes, ahead of
+ * the next one, no host synchronisation -- then drb_exchange_mark.  comm is
+ * the rank's ncclComm_t over the placement's ranks (rank place_rank of
+ * place_world; DRB_EINVAL otherwise); RCCL errors are DRB_EDEVICE.
+ * Replaces Transport.Send -> handleRequest (transport.go:346, :305) for
+ * GPU-resident replicas, with no Python in the host process. */
+int drb_exchange_rccl(drb_engine *e, void *comm, uint32_t leader_mask);
+/* leader_mask for drb_exchange_rccl / drb_exchange_plan: the OR over comm's
+ * ranks of each engine's leader slots (an ncclAllReduce; synchronises the
+ * engine stream).  Collective: every rank calls it after its imports. */
+int drb_exchange_rccl_roles(drb_engine *e, void *comm, uint32_t *leader_mask);
 /* Inbound plane bytes the exchanges moved into this engine since the last
  * reset (the device pull's own count plus region copies); synchronises the
  * engine stream. */
@@ -1211,7 +1244,10 @@ typedef struct drb_wire_cpu {
  * (raft_optimized.go:308-656, 659-983, 1056-1207), the DeploymentId /
  * BinVer filter of Transport.handleRequest (transport.go:305-316), then
  * drb_ingest's placement.  Frames are consumed in order; a bad frame stops
- * the stream as ErrBadMessage closes the connection.  The stream is
+ * the stream as ErrBadMessage closes the connection.  A stream that ends
+ * inside a frame whose bytes so far are sound is not bad: `consumed` stops
+ * before that frame, and the transport passes its bytes again with the
+ * ones that follow (readMessage's io.ReadFull would still be waiting).  The stream is
  * uploaded once: payload CRCs, message decode and placement run on the
  * GPU (drb_ingest.hpp); the host reads the 20 B frame headers and walks
  * each batch's top-level fields.  Messages are placed, dropped or diverted

@@ -69,6 +69,8 @@ STRUCTS = {
     "drb_worker_read": abi.WorkerRead,
     "drb_wire_cpu": abi.WireCpu,
     "drb_worker_bufs": abi.WorkerBufs,
+    "drb_region": abi.Region,
+    "drb_xfer": abi.Xfer,
 }
 # ctypes field names that differ from the C member name
 RENAMED = {"from_": "from"}
