@@ -1128,20 +1128,21 @@ extern "C" int drb_stage_proposals(drb_engine *e, uint32_t slot,
 
 // The packed form of a NoOP-session batch (drb_stage_proposals_packed):
 // counts u8 per group, Key / ClientID / Cmd length per entry, the Cmd bytes
-// back to back.  ent0[g] / coff[i]: exclusive scans of counts / lengths.
-__global__ void k_widen_u8(const uint8_t *in, uint32_t *out, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = in[i];
-}
-__global__ void k_widen_u16(const uint16_t *in, uint32_t *out, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = in[i];
-}
+// back to back.  ent0[g] / coff[i]: exclusive scans of counts / lengths,
+// read through widening iterators (no widened copies, no extra launches).
+struct WidenU32 {
+  __host__ __device__ uint32_t operator()(uint8_t x) const { return x; }
+  __host__ __device__ uint32_t operator()(uint16_t x) const { return x; }
+};
+using WidenU8 = hipcub::TransformInputIterator<uint32_t, WidenU32,
+                                               const uint8_t *>;
+using WidenU16 = hipcub::TransformInputIterator<uint32_t, WidenU32,
+                                                const uint16_t *>;
 
 __global__ void k_stage_packed(View v, uint32_t slot, uint32_t type,
-                               const uint32_t *counts, const uint32_t *ent0,
+                               const uint8_t *counts, const uint32_t *ent0,
                                const uint64_t *keys, const uint64_t *clients,
-                               const uint32_t *lens, const uint32_t *coff,
+                               const uint16_t *lens, const uint32_t *coff,
                                const uint8_t *pool, uint64_t pool_len) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= v.G) return;
@@ -1171,6 +1172,28 @@ __global__ void k_stage_packed(View v, uint32_t slot, uint32_t type,
   }
 }
 
+// the packed batch's block layout (drb_stage_packed_layout): counts at 0,
+// then keys, client ids, lengths and the pool, each 256-aligned; *bytes =
+// the block's length
+static void stage_layout(uint64_t G, uint64_t n, size_t pool_len,
+                         uint64_t off[4], size_t *bytes) {
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const uint64_t n1 = n ? n : 1;
+  off[0] = al(G);
+  off[1] = off[0] + al(8 * n1);
+  off[2] = off[1] + al(8 * n1);
+  off[3] = off[2] + al(2 * n1);
+  *bytes = off[3] + pool_len;
+}
+
+extern "C" int drb_stage_packed_layout(const drb_engine *e, uint64_t n_entries,
+                                       size_t pool_len, uint64_t *offsets,
+                                       size_t *bytes) {
+  if (!e || !offsets || !bytes) return DRB_EINVAL;
+  stage_layout(e->v.G, n_entries, pool_len, offsets, bytes);
+  return DRB_OK;
+}
+
 // drb_stage_proposals_packed(_async): `async` returns with the upload
 // queued, once the previous call's upload is done (its arrays free)
 static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
@@ -1196,23 +1219,24 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
   }
   if (cmax > v.max_props) return DRB_ERANGE;
   if (tsum != n) return DRB_EINVAL;
-  // upload: counts | keys | client ids | lengths | pool, then device-side
-  // u32 counts, lengths, their scans and the scans' temp storage
+  // upload: counts | keys | client ids | lengths | pool (stage_layout),
+  // then device-side the two scans and their temp storage
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const uint64_t n1 = n ? n : 1;
   size_t tb1 = 0, tb2 = 0;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, (uint32_t *)nullptr,
-                                          (uint32_t *)nullptr, (int)G,
-                                          e->stream));
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (uint32_t *)nullptr,
-                                          (uint32_t *)nullptr, (int)n1,
-                                          e->stream));
-  const size_t o_cnt = 0, o_key = al(G), o_cid = o_key + al(8 * n1),
-               o_len = o_cid + al(8 * n1), o_pool = o_len + al(2 * n1),
-               up = o_pool + std::max<size_t>(pool_len, 16);
-  const size_t o_c32 = al(up), o_e0 = o_c32 + al(4 * G),
-               o_l32 = o_e0 + al(4 * G), o_off = o_l32 + al(4 * n1),
-               o_tmp = o_off + al(4 * n1),
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(
+      nullptr, tb1, WidenU8((const uint8_t *)nullptr, WidenU32()),
+      (uint32_t *)nullptr, (int)G, e->stream));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(
+      nullptr, tb2, WidenU16((const uint16_t *)nullptr, WidenU32()),
+      (uint32_t *)nullptr, (int)n1, e->stream));
+  uint64_t lo[4];
+  size_t up = 0;
+  stage_layout(G, n, pool_len, lo, &up);
+  const size_t o_cnt = 0, o_key = lo[0], o_cid = lo[1], o_len = lo[2],
+               o_pool = lo[3];
+  const size_t o_e0 = al(std::max<size_t>(up, o_pool + 16)),
+               o_off = o_e0 + al(4 * G), o_tmp = o_off + al(4 * n1),
                need = o_tmp + al(std::max(tb1, tb2));
   if (need > e->stage_bytes) {
     HIPCHK(hipStreamSynchronize(e->stream));  // the buffer may be in use
@@ -1230,19 +1254,32 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
   // this slot (ev_prop), so it runs beside a round that reads another
   // slot, and the engine stream waits for it before its next round
   HIPCHK(hipStreamWaitEvent(e->stream_h2d, e->ev_stage_free, 0));
-  HIPCHK(hipMemcpyAsync(d + o_cnt, counts, G, hipMemcpyHostToDevice,
-                        e->stream_h2d));
-  if (n) {
-    HIPCHK(hipMemcpyAsync(d + o_key, keys, 8 * n, hipMemcpyHostToDevice,
+  // the arrays in one block at stage_layout's offsets (a host that builds
+  // its batch in place, drb_stage_packed_layout): one DMA
+  const uint8_t *c8 = counts;
+  const bool one_block =
+      (const uint8_t *)keys == c8 + o_key &&
+      (const uint8_t *)client_ids == c8 + o_cid &&
+      (const uint8_t *)cmd_lens == c8 + o_len &&
+      (!pool_len || pool == c8 + o_pool);
+  if (one_block) {
+    HIPCHK(hipMemcpyAsync(d, counts, up, hipMemcpyHostToDevice,
                           e->stream_h2d));
-    HIPCHK(hipMemcpyAsync(d + o_cid, client_ids, 8 * n,
-                          hipMemcpyHostToDevice, e->stream_h2d));
-    HIPCHK(hipMemcpyAsync(d + o_len, cmd_lens, 2 * n, hipMemcpyHostToDevice,
+  } else {
+    HIPCHK(hipMemcpyAsync(d + o_cnt, counts, G, hipMemcpyHostToDevice,
                           e->stream_h2d));
+    if (n) {
+      HIPCHK(hipMemcpyAsync(d + o_key, keys, 8 * n, hipMemcpyHostToDevice,
+                            e->stream_h2d));
+      HIPCHK(hipMemcpyAsync(d + o_cid, client_ids, 8 * n,
+                            hipMemcpyHostToDevice, e->stream_h2d));
+      HIPCHK(hipMemcpyAsync(d + o_len, cmd_lens, 2 * n,
+                            hipMemcpyHostToDevice, e->stream_h2d));
+    }
+    if (pool_len)
+      HIPCHK(hipMemcpyAsync(d + o_pool, pool, pool_len,
+                            hipMemcpyHostToDevice, e->stream_h2d));
   }
-  if (pool_len)
-    HIPCHK(hipMemcpyAsync(d + o_pool, pool, pool_len, hipMemcpyHostToDevice,
-                          e->stream_h2d));
   HIPCHK(hipEventRecord(e->ev_uploaded, e->stream_h2d));
   // the lengths' sum while the upload runs; a batch that fails it is not
   // laid out, the slot stays as it was
@@ -1255,20 +1292,16 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
   }
   HIPCHK(hipStreamWaitEvent(e->stream_h2d, e->ev_prop[slot], 0));
   hipStream_t ls = e->stream_h2d;
-  uint32_t *c32 = (uint32_t *)(d + o_c32), *e0 = (uint32_t *)(d + o_e0);
-  uint32_t *l32 = (uint32_t *)(d + o_l32), *off = (uint32_t *)(d + o_off);
-  k_widen_u8<<<(unsigned)((G + 255) / 256), 256, 0, ls>>>(d + o_cnt, c32, G);
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(d + o_tmp, tb1, c32, e0, (int)G,
-                                          ls));
-  if (n) {
-    k_widen_u16<<<(unsigned)((n + 255) / 256), 256, 0, ls>>>(
-        (const uint16_t *)(d + o_len), l32, n);
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(d + o_tmp, tb2, l32, off, (int)n,
-                                            ls));
-  }
+  uint32_t *e0 = (uint32_t *)(d + o_e0), *off = (uint32_t *)(d + o_off);
+  const uint16_t *l16 = (const uint16_t *)(d + o_len);
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(
+      d + o_tmp, tb1, WidenU8(d + o_cnt, WidenU32()), e0, (int)G, ls));
+  if (n)
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(
+        d + o_tmp, tb2, WidenU16(l16, WidenU32()), off, (int)n, ls));
   k_stage_packed<<<(unsigned)((G + 255) / 256), 256, 0, ls>>>(
-      v, slot, type, c32, e0, (const uint64_t *)(d + o_key),
-      (const uint64_t *)(d + o_cid), l32, off, d + o_pool,
+      v, slot, type, d + o_cnt, e0, (const uint64_t *)(d + o_key),
+      (const uint64_t *)(d + o_cid), l16, off, d + o_pool,
       (uint64_t)pool_len);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e->ev_staged, ls));

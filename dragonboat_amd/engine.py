@@ -58,6 +58,7 @@ SIGNATURES = {
                                              PU64, C.POINTER(C.c_uint16),
                                              PU8, SZ]),
     "drb_stage_wait_upload": (C.c_int, [P]),
+    "drb_stage_packed_layout": (C.c_int, [P, U64, SZ, PU64, C.POINTER(SZ)]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
     "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
                                               U64, U32]),
@@ -316,6 +317,16 @@ class Engine:
         _ck(lib().drb_stage_proposals_packed_async(
             self.h, slot, type, counts, n, keys, clients, lens, pool,
             pool_len), "drb_stage_proposals_packed_async")
+
+    def stage_packed_layout(self, n_entries, pool_len):
+        """drb_stage_packed_layout: ([keys, client ids, lengths, pool]
+        offsets, block bytes) of a one-block packed batch."""
+        off = (U64 * 4)()
+        nb = SZ()
+        _ck(lib().drb_stage_packed_layout(self.h, n_entries, pool_len, off,
+                                          C.byref(nb)),
+            "drb_stage_packed_layout")
+        return list(off), nb.value
 
     def stage_wait_upload(self):
         _ck(lib().drb_stage_wait_upload(self.h), "drb_stage_wait_upload")

@@ -577,6 +577,14 @@ int drb_stage_proposals_packed_async(drb_engine *e, uint32_t slot,
                                      const uint8_t *pool, size_t pool_len);
 /* Until the last staged upload is done (its host arrays free). */
 int drb_stage_wait_upload(drb_engine *e);
+/* Where a host builds a packed batch of n_entries entries and pool_len Cmd
+ * bytes in one pinned block so that either call uploads it in one DMA:
+ * counts at offset 0, then keys, client ids, lengths and the pool at
+ * offsets[0..3] (256-aligned); *bytes = the block's length.  Arrays
+ * elsewhere are uploaded one copy each. */
+int drb_stage_packed_layout(const drb_engine *e, uint64_t n_entries,
+                            size_t pool_len, uint64_t *offsets,
+                            size_t *bytes);
 /* Device-side synthetic proposal generator (bench / SURVEY 8d inputs):
  * k KVTest PBKV writes per group, NoOP session, EncodedEntry v0. */
 int drb_gen_kv_proposals(drb_engine *e, uint32_t slot, uint32_t k,

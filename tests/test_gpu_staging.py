@@ -16,12 +16,33 @@ from tests.gpu_harness import Pair
 pytestmark = pytest.mark.gpu
 
 
+def _one_block(eng, arrs):
+    """The packed arrays copied into one block at drb_stage_packed_layout's
+    offsets (the one-DMA upload)."""
+    cnt, n, keys, cids, lens, pb, plen = arrs
+    off, nbytes = eng.stage_packed_layout(n, plen)
+    blk = (C.c_uint8 * max(1, nbytes))()
+    base = C.addressof(blk)
+    C.memmove(base, cnt, C.sizeof(cnt))
+    for o, a, sz in ((off[0], keys, 8 * n), (off[1], cids, 8 * n),
+                     (off[2], lens, 2 * n), (off[3], pb, plen)):
+        C.memmove(base + o, a, sz)
+
+    def at(o, t):
+        return C.cast(base + o, C.POINTER(t))
+    return blk, (at(0, C.c_uint8), n, at(off[0], C.c_uint64),
+                 at(off[1], C.c_uint64), at(off[2], C.c_uint16),
+                 at(off[3], C.c_uint8), plen)
+
+
 def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4,
-                  slot=0, pipelined=False):
+                  slot=0, pipelined=False, one_block=False):
     counts, ents, pool = workload.build_batch(p.G, k, p.seed, salt,
                                               key_space, val_len, groups)
     p.orc.stage_proposals(counts, k, ents, pool)
     arrs = workload.pack_batch(p.G, k, counts, ents, pool)
+    if one_block:  # (the block stays alive with p until the next batch)
+        p._keep, arrs = _one_block(p.eng, arrs)
     if pipelined:
         # drb_stage_proposals_packed_async: these arrays stay in use until
         # the next call returns (the caller keeps them)
@@ -31,10 +52,12 @@ def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4,
     return arrs
 
 
-@pytest.mark.parametrize("k,val_len,pipelined", [(1, 4, False), (3, 4, False),
-                                                 (2, 16, False), (1, 4, True),
-                                                 (3, 16, True)])
-def test_packed_staging_matches_oracle(k, val_len, pipelined):
+@pytest.mark.parametrize("k,val_len,pipelined,one_block",
+                         [(1, 4, False, False), (3, 4, False, False),
+                          (2, 16, False, False), (1, 4, True, False),
+                          (3, 16, True, False), (2, 4, False, True),
+                          (3, 16, True, True)])
+def test_packed_staging_matches_oracle(k, val_len, pipelined, one_block):
     G = 96
     p = Pair(G=G, R=3, max_props=4, cmd_cap=32, kv_val_cap=16, prop_slots=2)
     held = None
@@ -42,7 +65,8 @@ def test_packed_staging_matches_oracle(k, val_len, pipelined):
         groups = None if rnd % 3 else [g for g in range(G) if g % 4]
         cur = _stage_packed(p, k, rnd, groups, val_len=val_len,
                             slot=rnd % 2 if pipelined else 0,
-                            pipelined=pipelined)
+                            pipelined=pipelined, one_block=one_block)
+        cur = (cur, getattr(p, "_keep", None))
         held = (held, cur)[1]  # the previous call's arrays are free now
         o = p.orc.round(tick=rnd % 2 == 0)
         e = p.eng.step(tick=rnd % 2 == 0,
