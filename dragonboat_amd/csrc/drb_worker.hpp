@@ -14,22 +14,20 @@
 //      applied entry) into device staging[parity]; the totals go straight
 //      to mapped host memory;
 //   2. the engine's drain thread waits for that compaction and copies
-//      exactly those bytes into the caller's pinned buffers on an SDMA
-//      engine HIP's own copies do not use (hsa_amd_memory_async_copy_on_engine,
-//      a completion signal per buffer set): the transfer overlaps the next
-//      rounds at PCIe rate (~56 GB/s) and takes no CU.  Measured
-//      (tools/calib_sdma, tools/calib_d2h, profiles/r05_worker): a drain
-//      kernel writing host memory from 256 workgroups slowed the concurrent
-//      leader kernel from 0.72 to 1.76 ms; hipMemcpyAsync D2H runs either
-//      on one SDMA queue at ~29 GB/s or, inside a PyTorch process, as
-//      __amd_rocclr_copyBuffer blit kernels that take CUs from the round;
-//      one chosen engine moves 56 GB/s beside an HBM-bound kernel without
-//      slowing it, and beside HIP's H2D on another engine.
+//      exactly those bytes into the caller's pinned buffers on the
+//      engine's download SDMA engine (drb_hsa.hpp: a completion signal per
+//      buffer set): the transfer overlaps the next rounds at PCIe rate
+//      (~56 GB/s) and takes no CU, and the staged proposals go up on
+//      another engine.  Measured (tools/calib_sdma, tools/calib_d2h,
+//      profiles/r05_worker): a drain kernel writing host memory from 256
+//      workgroups slowed the concurrent leader kernel from 0.72 to 1.76 ms;
+//      hipMemcpyAsync D2H runs either on one SDMA queue at ~29 GB/s or,
+//      inside a PyTorch process, as __amd_rocclr_copyBuffer blit kernels
+//      that take CUs from the round; one engine moves 56 GB/s beside an
+//      HBM-bound kernel without slowing it, and an upload and a download on
+//      the same engine run one after the other.
 // No host synchronisation in the caller until drb_worker_wait.
 #pragma once
-
-#include <hsa/hsa.h>
-#include <hsa/hsa_ext_amd.h>
 
 #include <condition_variable>
 #include <deque>
@@ -65,96 +63,11 @@ struct WorkerState {
   bool issued[2] = {false, false};  // the copies of its job issued
   int err = 0;                      // a failed copy (reported by wait)
   bool stop = false;
-  // the SDMA engine the copies go to (0: none found, hipMemcpyAsync on sx)
+  // the copies on the engine's download SDMA engine (drb_hsa.hpp;
+  // hipMemcpyAsync on sx when HSA is unavailable)
   bool hsa = false;
-  hsa_agent_t cpu{}, gpu{};
-  uint32_t engine = 0;
   hsa_signal_t done[2] = {{0}, {0}};  // copies outstanding, by parity
 };
-
-// the HSA agents of the engine's device and of host memory, and the SDMA
-// engine for device -> host copies (the preferred one, else the first)
-static void worker_pick_engine(drb_engine *e, WorkerState &w) {
-  int bus = -1, dev = -1, dom = -1;
-  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId,
-                            e->cfg.device) != hipSuccess ||
-      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId,
-                            e->cfg.device) != hipSuccess ||
-      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID,
-                            e->cfg.device) != hipSuccess)
-    return;
-  if (hsa_init() != HSA_STATUS_SUCCESS) return;
-  struct Find {
-    int bus, dev, dom;
-    bool cpu_ok, gpu_ok;
-    hsa_agent_t cpu, gpu;
-  } f{bus, dev, dom, false, false, {}, {}};
-  (void)hsa_iterate_agents(
-      [](hsa_agent_t a, void *p) {
-        Find &f = *(Find *)p;
-        hsa_device_type_t t;
-        if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) !=
-            HSA_STATUS_SUCCESS)
-          return HSA_STATUS_SUCCESS;
-        if (t == HSA_DEVICE_TYPE_CPU && !f.cpu_ok) {
-          f.cpu = a;
-          f.cpu_ok = true;
-        } else if (t == HSA_DEVICE_TYPE_GPU && !f.gpu_ok) {
-          uint32_t bdf = 0, dom = 0;
-          (void)hsa_agent_get_info(
-              a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
-          (void)hsa_agent_get_info(
-              a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
-          if ((int)(bdf >> 8) == f.bus && (int)((bdf >> 3) & 31) == f.dev &&
-              (int)dom == f.dom) {
-            f.gpu = a;
-            f.gpu_ok = true;
-          }
-        }
-        return HSA_STATUS_SUCCESS;
-      },
-      &f);
-  uint32_t avail = 0, pref = 0;
-  if (!f.cpu_ok || !f.gpu_ok ||
-      hsa_amd_memory_copy_engine_status(f.cpu, f.gpu, &avail) !=
-          HSA_STATUS_SUCCESS ||
-      !avail) {
-    (void)hsa_shut_down();
-    return;
-  }
-  // HIP's own copies (the staged proposals' H2D upload) take the lowest
-  // preferred engine, or engine 0 without a preference; a D2H on that
-  // engine queues behind them (64 MiB each way: 2.37 ms for both on one
-  // engine against 1.2-1.5 ms on two, tools/calib_sdma; the step-worker
-  // round 2.12 ms on HIP's engine, 1.50 on any of engines 1-3,
-  // profiles/r05_worker), so the next preferred engine, else the lowest
-  // of the first four (the fast ones: 4-15 move 7-13 GB/s) that is not it
-  (void)hsa_amd_memory_get_preferred_copy_engine(f.cpu, f.gpu, &pref);
-  const uint32_t hip_eng = pref ? (pref & (~pref + 1)) : 1u;
-  uint32_t m = pref & avail & ~hip_eng;
-  if (!m) m = avail & 0xfu & ~hip_eng;
-  if (!m) m = avail;
-  for (int k = 0; k < 2; ++k)
-    if (hsa_signal_create(0, 0, nullptr, &w.done[k]) != HSA_STATUS_SUCCESS) {
-      for (int q = 0; q < k; ++q) (void)hsa_signal_destroy(w.done[q]);
-      w.done[0].handle = w.done[1].handle = 0;
-      (void)hsa_shut_down();
-      return;
-    }
-  w.cpu = f.cpu;
-  w.gpu = f.gpu;
-  w.engine = m & (~m + 1);  // the lowest engine of the mask
-  if (getenv("DRB_WORKER_LOG")) {
-    uint32_t up = 0, up_pref = 0;
-    (void)hsa_amd_memory_copy_engine_status(f.gpu, f.cpu, &up);
-    (void)hsa_amd_memory_get_preferred_copy_engine(f.gpu, f.cpu, &up_pref);
-    fprintf(stderr,
-            "drb worker: D2H engines 0x%x preferred 0x%x, H2D engines 0x%x "
-            "preferred 0x%x; D2H on 0x%x\n",
-            avail, pref, up, up_pref, w.engine);
-  }
-  w.hsa = true;
-}
 
 // until the copies of buffer set k are done
 static void worker_wait_copies(WorkerState &w, int k) {
@@ -301,13 +214,11 @@ static void worker_free(drb_engine *e) {
     w->th.join();
   }
   if (w->sx) (void)hipStreamSynchronize(w->sx);
-  if (w->hsa) {
+  if (w->hsa)
     for (int k = 0; k < 2; ++k) {
       worker_wait_copies(*w, k);
       (void)hsa_signal_destroy(w->done[k]);
     }
-    (void)hsa_shut_down();
-  }
   for (int k = 0; k < 2; ++k) {
     if (w->ev_staged[k]) (void)hipEventDestroy(w->ev_staged[k]);
     if (w->ev_drained[k]) (void)hipEventDestroy(w->ev_drained[k]);
@@ -347,14 +258,15 @@ static hipError_t worker_copy(drb_engine *e, WorkerState &w,
              {j.b.value_meta, w.meta[k], (nval + 1) / 2},
              {j.b.applied, w.ap[k], nap * 4}};
   if (w.hsa) {
+    const HsaXfer &x = e->xfer;
     int n = 0;
     for (auto &c : cp) n += c.n && c.dst;
     hsa_signal_store_screlease(w.done[k], n);
     for (auto &c : cp) {
       if (!(c.n && c.dst)) continue;
       if (hsa_amd_memory_async_copy_on_engine(
-              c.dst, w.cpu, c.src, w.gpu, c.n, 0, nullptr, w.done[k],
-              (hsa_amd_sdma_engine_id_t)w.engine, true) != HSA_STATUS_SUCCESS) {
+              c.dst, x.cpu, c.src, x.gpu, c.n, 0, nullptr, w.done[k],
+              (hsa_amd_sdma_engine_id_t)x.down, true) != HSA_STATUS_SUCCESS) {
         hsa_signal_subtract_screlease(w.done[k], 1);
         r = hipErrorUnknown;
       }
@@ -455,7 +367,16 @@ static int worker_init(drb_engine *e) {
                        hipHostMallocMapped));
   memset(w->hdr, 0, 8 * sizeof(unsigned long long));
   HIPCHK(hipHostGetDevicePointer((void **)&w->hdr_dev, w->hdr, 0));
-  worker_pick_engine(e, *w);
+  // the copies on the engine's download SDMA engine (drb_hsa.hpp)
+  if (hsa_xfer_init(e->cfg.device, &e->xfer)) {
+    w->hsa = hsa_signal_create(0, 0, nullptr, &w->done[0]) ==
+             HSA_STATUS_SUCCESS;
+    if (w->hsa && hsa_signal_create(0, 0, nullptr, &w->done[1]) !=
+                      HSA_STATUS_SUCCESS) {
+      (void)hsa_signal_destroy(w->done[0]);
+      w->hsa = false;
+    }
+  }
   w->th = std::thread(worker_thread, e);
   return DRB_OK;
 }

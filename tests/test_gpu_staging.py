@@ -16,13 +16,33 @@ from tests.gpu_harness import Pair
 pytestmark = pytest.mark.gpu
 
 
-def _one_block(eng, arrs):
+class _Pinned:
+    """A pinned host block (drb_host_alloc): the staged upload then runs on
+    the engine's own SDMA engine (drb_hsa.hpp)."""
+
+    def __init__(self, eng, nbytes):
+        from dragonboat_amd.engine import lib
+        self.eng, self.p = eng, C.c_void_p()
+        assert lib().drb_host_alloc(eng.h, max(1, nbytes),
+                                    C.byref(self.p)) == 0
+        self.addr = self.p.value
+
+    def __del__(self):
+        from dragonboat_amd.engine import lib
+        lib().drb_host_free(self.eng.h, self.p)
+
+
+def _one_block(eng, arrs, pinned=False):
     """The packed arrays copied into one block at drb_stage_packed_layout's
     offsets (the one-DMA upload)."""
     cnt, n, keys, cids, lens, pb, plen = arrs
     off, nbytes = eng.stage_packed_layout(n, plen)
-    blk = (C.c_uint8 * max(1, nbytes))()
-    base = C.addressof(blk)
+    if pinned:
+        blk = _Pinned(eng, nbytes)
+        base = blk.addr
+    else:
+        blk = (C.c_uint8 * max(1, nbytes))()
+        base = C.addressof(blk)
     C.memmove(base, cnt, C.sizeof(cnt))
     for o, a, sz in ((off[0], keys, 8 * n), (off[1], cids, 8 * n),
                      (off[2], lens, 2 * n), (off[3], pb, plen)):
@@ -42,7 +62,7 @@ def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4,
     p.orc.stage_proposals(counts, k, ents, pool)
     arrs = workload.pack_batch(p.G, k, counts, ents, pool)
     if one_block:  # (the block stays alive with p until the next batch)
-        p._keep, arrs = _one_block(p.eng, arrs)
+        p._keep, arrs = _one_block(p.eng, arrs, one_block == "pinned")
     if pipelined:
         # drb_stage_proposals_packed_async: these arrays stay in use until
         # the next call returns (the caller keeps them)
@@ -55,8 +75,9 @@ def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4,
 @pytest.mark.parametrize("k,val_len,pipelined,one_block",
                          [(1, 4, False, False), (3, 4, False, False),
                           (2, 16, False, False), (1, 4, True, False),
-                          (3, 16, True, False), (2, 4, False, True),
-                          (3, 16, True, True)])
+                          (3, 16, True, False), (2, 4, False, "pageable"),
+                          (3, 16, True, "pageable"), (2, 4, False, "pinned"),
+                          (3, 16, True, "pinned")])
 def test_packed_staging_matches_oracle(k, val_len, pipelined, one_block):
     G = 96
     p = Pair(G=G, R=3, max_props=4, cmd_cap=32, kv_val_cap=16, prop_slots=2)
@@ -96,3 +117,56 @@ def test_packed_staging_rejects_bad_sums():
     with pytest.raises(DrbError):
         p.eng.stage_proposals_packed(0, abi.ENTRY_ENCODED, cnt, 16, keys,
                                      keys, lens, pool, 32)
+
+
+def test_sdma_upload_lays_out_the_same_batch():
+    """A batch of ≥ 8 MB built in one pinned block goes up on the engine's
+    own SDMA engine (hsa_amd_memory_async_copy_on_engine, drb_hsa.hpp); the
+    same batch in a pageable block goes through hipMemcpyAsync, the path
+    the oracle tests above pin.  Two engines from the same state, one round
+    each: the same commits, and every sampled replica's state and log
+    equal."""
+    import numpy as np
+    from dragonboat_amd.engine import Engine
+    from tests.gpu_harness import state_diff
+    G, R, seed = 262144, 3, 0x5EEDD8B0
+    arrs = [x.view("u1") for x in workload.build_packed_np(G, seed, 7)]
+    n, plen = arrs[1].size // 8, arrs[4].size
+    engs, keep = [], []
+    for pinned in (True, False):
+        e = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
+                   max_props=1, prop_slots=2)
+        e.init_steady(term=2, leader_slot=0, seed=seed)
+        off, nbytes = e.stage_packed_layout(n, plen)
+        assert nbytes >= 8 << 20
+        if pinned:
+            blk = _Pinned(e, nbytes)
+            base = blk.addr
+        else:
+            blk = np.zeros(nbytes, dtype=np.uint8)
+            base = blk.ctypes.data
+        view = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(base))
+        for o, x in zip([0] + off, arrs):
+            view[o:o + x.size] = x
+        ptr = [C.cast(base + o, t) for o, t in zip(
+            [0] + off, [C.POINTER(C.c_uint8), C.POINTER(C.c_uint64),
+                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint16),
+                        C.POINTER(C.c_uint8)])]
+        e.stage_proposals_packed(0, abi.ENTRY_ENCODED, ptr[0], n, ptr[1],
+                                 ptr[2], ptr[3], ptr[4], plen)
+        committed = 0
+        for r in range(3):  # the batch, then rounds that commit it
+            out = e.step(tick=r == 0, prop_slot=0 if r == 0 else abi.DRB_NONE)
+            assert out.fallbacks == 0 and out.errors == 0
+            committed += out.committed_entries
+        engs.append((e, committed))
+        keep.append(blk)
+    (a, ca), (b, cb) = engs
+    assert ca == cb and ca > 0
+    for g0 in range(0, G, 8191):
+        sa, sb = a.export_replicas(g0, 1), b.export_replicas(g0, 1)
+        for s in range(R):
+            assert not state_diff(sa[s], sb[s], R), (g0, s)
+            li = sa[s].last_index
+            assert a.export_log(g0, s, max(1, li - 2), li) == \
+                b.export_log(g0, s, max(1, li - 2), li), (g0, s)
