@@ -578,7 +578,10 @@ int drb_stage_proposals_packed_async(drb_engine *e, uint32_t slot,
 /* Until the last staged upload is done (its host arrays free). */
 int drb_stage_wait_upload(drb_engine *e);
 /* Where a host builds a packed batch of n_entries entries and pool_len Cmd
- * bytes in one pinned block so that either call uploads it in one DMA:
+ * bytes in one pinned block so that either call uploads it in one DMA (of
+ * 8 MB and more, on the engine's own upload SDMA engine -- the one its
+ * step-worker downloads do not use -- with the call returning once it is
+ * up):
  * counts at offset 0, then keys, client ids, lengths and the pool at
  * offsets[0..3] (256-aligned); *bytes = the block's length.  Arrays
  * elsewhere are uploaded one copy each. */
