@@ -10,6 +10,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <numaif.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <vector>
 
@@ -66,6 +71,40 @@ int main() {
   CK(hipMemset(sa, 2, S));
   CK(hipHostMalloc(&h, B, hipHostMallocMapped));
   CK(hipDeviceSynchronize());
+  {
+    // NUMA placement: the GPU's node, the nodes of the CPUs this process
+    // may run on, and the node of the pinned buffer's first page
+    int bus = 0, devn = 0, dom = 0;
+    CK(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, 0));
+    CK(hipDeviceGetAttribute(&devn, hipDeviceAttributePciDeviceId, 0));
+    CK(hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, 0));
+    char path[128];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%04x:%02x:%02x.0/numa_node",
+             dom, bus, devn);
+    int gnode = -9;
+    if (FILE *f = fopen(path, "r")) {
+      if (fscanf(f, "%d", &gnode) != 1) gnode = -8;
+      fclose(f);
+    }
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    sched_getaffinity(0, sizeof(cs), &cs);
+    int counts[8] = {0};
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+      if (!CPU_ISSET(c, &cs)) continue;
+      for (int n = 0; n < 8; ++n) {
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", c, n);
+        if (access(path, F_OK) == 0) counts[n]++;
+      }
+    }
+    void *pg = h;
+    int status = -99;
+    syscall(SYS_move_pages, 0, 1UL, &pg, nullptr, &status, 0);
+    printf("numa: gpu node %d; allowed cpus per node:", gnode);
+    for (int n = 0; n < 8; ++n)
+      if (counts[n]) printf(" n%d=%d", n, counts[n]);
+    printf("; pinned buffer page on node %d\n", status);
+  }
   HK(hsa_init());
   HK(hsa_iterate_agents(pick, nullptr));
   if (!have_cpu || !have_gpu) return 1;
