@@ -781,10 +781,11 @@ int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
  * ReadLocalNode, nodehost.go:849; the applied entries,
  * pendingProposals.applied, node.go:243-257).  drb_worker_export enqueues,
  * behind the last round, a compaction of replica slot `slot`'s outputs
- * into device staging (two buffers, by export parity) and, on a copy
- * stream, their transfer into the caller's host buffers (drb_host_alloc):
- * the transfer overlaps the next rounds.  drb_worker_wait blocks until
- * that export's bytes are in its buffers and fills the counts.
+ * into device staging (two buffers, by export parity) and their transfer
+ * into the caller's host buffers (drb_host_alloc) on the engine's download
+ * SDMA engine (no CU time; the staged proposals go up on another one): the
+ * transfer overlaps the next rounds.  drb_worker_wait blocks until that
+ * export's bytes are in its buffers and fills the counts.
  *
  * The records carry only what the host cannot rebuild from what it staged
  * (about 64 B per C3 group-round):
