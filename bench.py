@@ -181,6 +181,15 @@ def parse():
                          "(k rounds chunk by chunk of the groups) against "
                          "plain rounds, specs CHUNK_GROUPS:K,... (e.g. "
                          "65536:4,262144:2); reported as chunk_ab, not value")
+    ap.add_argument("--c4-cross", type=int, default=-1,
+                    help="with --gpus N > 1 and a co-resident workload, also "
+                         "time C4 across the ranks through the C ABI's RCCL "
+                         "exchange (drb_exchange_rccl*; gloo: a rehearsal "
+                         "through host memory); default on")
+    ap.add_argument("--c4-groups", type=int, default=1 << 20,
+                    help="groups of that C4 run (in total)")
+    ap.add_argument("--c4-timeout", type=int, default=240,
+                    help="seconds the C4 cross-GPU phase may take")
     ap.add_argument("--step-worker", type=int, default=-1,
                     help="after the timed region, also time whole step-"
                          "worker rounds: host-staged proposals, the round, "
@@ -386,6 +395,124 @@ def run_c4_local(args):
     for e in engs:
         e.close()
     return 0
+
+
+def run_c4_cross(args, world, rank, local, gloo):
+    """C4 across the process group's ranks through the C ABI, beside a
+    multi-GPU run of another workload: --c4-groups groups x 5 replicas,
+    replica slot s of group g on rank (g + s) mod world at lane g // world,
+    bench.py's C4 engine, the planes moved after every round by
+    drb_exchange_rccl_counted (drb_plane_counts, an ncclAllGather of the
+    words, ncclSend / ncclRecv at those sizes) and by drb_exchange_rccl (the
+    fixed full-capacity step, no host round trip) -- RCCL over xGMI, what a
+    Go NodeHost per GPU would call.  With the gloo backend
+    (a rehearsal with the ranks on one GPU: RCCL refuses two ranks on one
+    device) the same C-ABI transfer lists (drb_exchange_plan_words /
+    drb_exchange_plan) move through host memory instead."""
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    from dragonboat_amd import dist as ddist
+    from dragonboat_amd import exchange as X
+    from dragonboat_amd.engine import Engine
+    G, R, k = args.c4_groups, 5, 1
+    lanes = (G + world - 1) // world
+    NP = max(8, args.steps)
+    seed = ddist.BASE_SEED
+    red = "cpu" if gloo else "cuda"
+    dev = torch.device("cuda", local)
+    eng = Engine(num_groups=lanes, num_replicas=R, window=32, cmd_cap=32,
+                 max_props=k, prop_slots=NP, ri_slots=NP, mailbox=8,
+                 kv_slots=512, kv_val_cap=4, total_groups=G,
+                 place_world=world, place_rank=rank, entry_mbox=k + 2,
+                 device=local)
+    comm = None
+    try:
+        eng.init_steady(term=2, leader_slot=0, seed=seed)
+        if gloo:
+            t = torch.tensor([eng.role_slots()[0]], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.BOR)
+            mask = int(t.item())
+        else:
+            comm = ddist.RcclComm(world, rank)
+            mask = eng.exchange_rccl_roles(comm.handle)
+
+        def xchg(mode):
+            if not gloo:
+                if mode == "counted":
+                    eng.exchange_rccl_counted(comm.handle)
+                else:
+                    eng.exchange_rccl(comm.handle, mask)
+                return
+            if mode == "counted":
+                mine = torch.tensor(eng.plane_counts(), dtype=torch.int64)
+                allw = torch.empty(world * R * R, dtype=torch.int64)
+                dist.all_gather_into_tensor(allw, mine)
+                flat = allw.tolist()
+                ops = eng.exchange_plan_words(
+                    [flat[q * R * R:(q + 1) * R * R] for q in range(world)])
+            else:
+                eng.sync()
+                ops = eng.exchange_plan(mask)
+            X.run_ops_staged([("recv" if rv else "send", peer, (ptr, n))
+                              for peer, rv, ptr, n in ops], dev)
+            staged[0] += sum(n for _, rv, _, n in ops if rv)
+            torch.cuda.current_stream(dev).synchronize()
+            eng.exchange_mark()
+
+        out = {"groups": G, "replicas": R, "lanes_per_rank": lanes,
+               "world": world,
+               "transport": ("gloo rehearsal: the C-ABI transfer lists "
+                             "through host memory (ranks sharing one GPU)"
+                             if gloo else "RCCL ncclSend / ncclRecv over "
+                             "xGMI, drb_exchange_rccl_counted / "
+                             "drb_exchange_rccl on the engine stream")}
+        r0, WARM, TIMED = 0, 1 << 21, 1 << 22
+        staged = [0]  # (gloo: the bytes received through host memory)
+        for mode in ("counted", "fixed"):
+            for i in range(args.warmup):
+                eng.gen_kv_proposals(0, k, KEY_SPACE, 4, seed, WARM + r0 + i)
+                eng.step_async(tick=True, prop_slot=0)
+                xchg(mode)
+            r0 += args.warmup
+            K = args.steps
+            for b in range(K):
+                eng.gen_kv_proposals(b, k, KEY_SPACE, 4, seed, TIMED + r0 + b)
+            eng.sync()
+            eng.read_counters(reset=True)
+            eng.exchange_bytes(reset=True)
+            staged[0] = 0
+            ddist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(K):
+                eng.step_async(tick=True, prop_slot=i)
+                xchg(mode)
+            eng.sync()
+            torch.cuda.synchronize()
+            ddist.barrier()
+            el = ddist.reduce_max(time.perf_counter() - t0, red)
+            r0 += K
+            o = eng.read_counters(reset=True)
+            xb = ddist.reduce_max((eng.exchange_bytes(reset=True) +
+                                   staged[0]) / K, red)
+            committed = ddist.reduce_sum(o.committed_entries, red)
+            fb = ddist.reduce_sum(o.fallbacks + o.errors, red)
+            out[mode] = {
+                "value": committed / el, "unit": "committed entries/s",
+                "ms_per_step": el * 1e3 / K, "steps": K,
+                "committed_per_round": committed / K,
+                "xchg_bytes_per_round_per_rank": xb,
+                "fallbacks_and_errors": fb}
+        out["note"] = ("C4 beside the main workload, timed around the whole "
+                       "job (the exchange included), max over ranks; "
+                       "xchg_bytes: inbound plane bytes per round of the "
+                       "busiest rank (drb_exchange_bytes); not `value`")
+        return out
+    finally:
+        if comm is not None:
+            comm.close()
+        eng.close()
 
 
 def self_launch(args):
@@ -854,19 +981,23 @@ def main():
         u8p, u64p, u16p = (C.POINTER(C.c_uint8), C.POINTER(C.c_uint64),
                            C.POINTER(C.c_uint16))
         hb, hp = [], []
+        # one NoOP session per group (client.NewNoOPSession): registered
+        # once (drb_set_session_clients), so the batches leave ClientID out
+        eng.set_session_clients(workload.build_packed_np(G, seed, 0)[2])
         for b in range(HB):
             arrs = [x.view("u1") for x in workload.build_packed_np(G, seed, b)]
             n_e, plen = arrs[1].size // 8, arrs[4].size
-            off, nbytes = eng.stage_packed_layout(n_e, plen)
+            off, _ = eng.stage_packed_layout(n_e, plen)
+            nbytes = off[3] + plen  # (no client ids: the block ends here)
             blk = torch.zeros(max(1, nbytes), dtype=torch.uint8).pin_memory()
             view = blk.numpy()
             for o, x in zip([0] + off, arrs):
-                view[o:o + x.size] = x
+                if x is not arrs[2]:
+                    view[o:o + x.size] = x
             base = blk.data_ptr()
-            hb.append((blk, sum(x.size for x in arrs)))
+            hb.append((blk, sum(x.size for x in arrs) - arrs[2].size))
             hp.append((C.cast(base, u8p), n_e, C.cast(base + off[0], u64p),
-                       C.cast(base + off[1], u64p),
-                       C.cast(base + off[2], u16p),
+                       None, C.cast(base + off[2], u16p),
                        C.cast(base + off[3], u8p), plen))
         KH = max(5, K)
         eng.read_counters(reset=True)
@@ -887,11 +1018,12 @@ def main():
             "upload_bytes_per_round": int(hb[0][1]),
             "note": "proposals staged from pinned host memory every round "
                     "in the packed form (drb_stage_proposals_packed_async: "
-                    "Key, ClientID, Cmd length and bytes per entry, one H2D "
-                    "per array on a copy stream overlapping the previous "
-                    "round, + scans and a layout kernel; the host waits for "
-                    "an upload at the next call), timed around the whole "
-                    "loop; not `value`"}
+                    "per group a count, per entry Key, Cmd length and bytes "
+                    "-- ClientID is the group's session client, registered "
+                    "once by drb_set_session_clients -- one DMA on a copy "
+                    "engine overlapping the previous round, + scans and a "
+                    "layout kernel; the host waits for an upload at the "
+                    "next call), timed around the whole loop; not `value`"}
         if args.step_worker < 0:
             args.step_worker = int(reads and not c2 and args.read_results)
         if args.step_worker:
@@ -901,7 +1033,7 @@ def main():
             # reads' results, pendingProposals.applied -- exported behind
             # each round and drained on a copy stream into pinned host
             # buffers while the next round runs (two buffer sets)
-            wb = [eng.worker_bufs(2 * G, 2 * G * READS_PER_CTX, 4 * G * k)
+            wb = [eng.worker_bufs(2 * G, 2 * G * READS_PER_CTX, 2 * G)
                   for _ in range(2)]
             KW = max(5, K)
             WW = max(2, args.warmup)
@@ -912,7 +1044,7 @@ def main():
                 # next round's entry queue up while it runs, then the
                 # outputs of the round before it (their copy ran beside
                 # this round)
-                got = [0, 0, 0]
+                got = [0, 0, 0, 0]
                 marks = []
                 eng.stage_proposals_packed_async(0, _abi.ENTRY_ENCODED,
                                                  *hp[0])
@@ -930,13 +1062,13 @@ def main():
                     t.append(pc())
                     if i >= 1:
                         n3 = eng.worker_wait(wb[(i - 1) % 2])
-                        got = [d + x for d, x in zip(got, n3)]
+                        got = [d + x for d, x in zip(got, n3 + (1,))]
                     t.append(pc())
                     marks.append(t[-1])
                     phases.append([b - a for a, b in zip(t, t[1:])])
                 n3 = eng.worker_wait(wb[(n - 1) % 2])
                 eng.stage_wait_upload()
-                return [d + x for d, x in zip(got, n3)], marks
+                return [d + x for d, x in zip(got, n3 + (1,))], marks
 
             r0 = 2 * args.warmup + K + KH
             phases = []
@@ -951,12 +1083,11 @@ def main():
             wout = eng.read_counters(reset=True)
             for bw in wb:
                 eng.free_worker_bufs(bw)
-            import ctypes as _C
-            # the lean records (include/drb_engine.h): a word per lane,
-            # 16 B per ReadyToRead, 4 B + a nibble per served read, 4 B per
-            # applied entry
-            dbytes = (KW * G * 4 + down[0] * _C.sizeof(_abi.WorkerRead) +
-                      down[1] * 4 + (down[1] + KW) // 2 + down[2] * 4) / KW
+            # the lean records (include/drb_engine.h): a word per lane, a
+            # 4 B ctx tag per ReadyToRead, 4 B + 2 bits per served read, 8 B
+            # per ReadyToRead not served (over the exports waited for)
+            dbytes = (down[3] * G * 4 + down[0] * 4 + down[1] * 4 +
+                      (down[1] + 3 * down[3]) // 4 + down[2] * 8) / down[3]
             step_worker = {
                 "ms_per_step": wms, "steps": KW, "warmup": WW,
                 "iteration_ms_median": its[len(its) // 2],
@@ -974,12 +1105,12 @@ def main():
                 "download_bytes_per_round": int(dbytes),
                 "ready_to_reads_per_round": down[0] / KW,
                 "read_results_per_round": down[1] / KW,
-                "applied_per_round": down[2] / KW,
+                "deferred_per_round": down[2] / KW,
                 "note": "whole step-worker rounds timed around the loop: "
                         "packed proposals from pinned host memory (staged "
                         "one round ahead), the round with its 9 reads per "
                         "released ctx, then drb_worker_export of slot 0's "
-                        "ReadyToReads, read results and applied entries "
+                        "ReadyToReads, read results and applied counts "
                         "in the lean records (compaction behind the "
                         "round, exact-size copy-engine transfers into "
                         "pinned host buffers beside the next round); "
@@ -1155,6 +1286,33 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             # (rank 0 at N = 1 only: the scaling runs keep their ranks' time)
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    if args.c4_cross < 0:
+        args.c4_cross = int(world > 1 and not c4)
+    if args.c4_cross and world > 1:
+        # C4 through the C ABI's cross-GPU exchange, after the timed run.
+        # A watchdog ends the phase if the exchange hangs (ncclCommAbort,
+        # then the line without it), so the main measurement still lands.
+        done = threading.Event()
+        cross = {}
+
+        def watchdog():
+            if done.wait(args.c4_timeout):
+                return
+            if rank == 0:
+                res["c4_cross"] = {"error": "timed out after %d s" %
+                                   args.c4_timeout}
+                print(json.dumps(res), flush=True)
+            os._exit(0 if rank == 0 else 3)
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            cross = run_c4_cross(args, world, rank, local,
+                                 args.dist_backend == "gloo")
+        except Exception as ex:  # (reported in the line, not fatal to it)
+            cross = {"error": "%s: %s" % (type(ex).__name__, ex)}
+        done.set()
+        if rank == 0:
+            res["c4_cross"] = cross
+    if rank == 0:
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -17,6 +17,7 @@ DRB_ENOMEM = -3
 DRB_ENOSYS = -4
 DRB_ERANGE = -5
 DRB_EAGAIN = -6  # retry: ingest between a round and its exchange
+DRB_EDIVERTED = -7  # drb_ingest: some messages went to the CPU path
 
 # raftpb.MessageType (raftpb/types.go:8-37)
 MSG = dict(
@@ -139,7 +140,8 @@ class Config(C.Structure):
                 ("kv_overflow_buckets", C.c_uint64),
                 ("forward_proposals", C.c_uint32),
                 ("nonvoting_slots", C.c_uint32),
-                ("witness_slots", C.c_uint32)]
+                ("witness_slots", C.c_uint32),
+                ("host_copies", C.c_uint32)]
 
 
 class ReadResult(C.Structure):
@@ -160,30 +162,39 @@ class ApplyResult(C.Structure):
                 ("slot", C.c_uint32), ("ignored", C.c_uint32)]
 
 
-class WorkerRead(C.Structure):
-    """drb_worker_read: a ReadyToRead (its Index and SystemCtx.Low)."""
-    _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64)]
-
-
-WORKER_FOUND, WORKER_LONG, WORKER_IGNORED = 8, 5, 0x80000000
+# drb_worker_bufs value_meta codes (include/drb_engine.h)
+WORKER_MISS, WORKER_V4, WORKER_SHORT, WORKER_LONG = 0, 1, 2, 3
 
 
 def worker_lane(w):
-    """(ReadyToReads, served mask, applied entries) of a lanes[] word."""
+    """(ReadyToReads, served mask, applied own proposals) of a lanes[]
+    word."""
     return w & 0xF, (w >> 4) & 0xFF, (w >> 12) & 0xFFFF
+
+
+def worker_value(code, word):
+    """A served read's result from its 2-bit code and value word: None (not
+    found), the value bytes, or (first 4 bytes, True) for a longer one."""
+    if code == WORKER_MISS:
+        return None
+    if code == WORKER_V4:
+        return word.to_bytes(4, "little")
+    if code == WORKER_SHORT:
+        return (word & 0xFFFFFF).to_bytes(3, "little")[:word >> 24]
+    return (word.to_bytes(4, "little"), True)
 
 
 class WorkerBufs(C.Structure):
     """drb_worker_bufs: pinned host buffers of one step-worker export."""
     _fields_ = [("lanes", C.POINTER(C.c_uint32)), ("lanes_cap", C.c_uint64),
-                ("reads", C.POINTER(WorkerRead)), ("reads_cap", C.c_uint64),
+                ("reads", C.POINTER(C.c_uint32)), ("reads_cap", C.c_uint64),
                 ("values", C.POINTER(C.c_uint32)),
                 ("value_meta", C.POINTER(C.c_uint8)),
                 ("values_cap", C.c_uint64),
-                ("applied", C.POINTER(C.c_uint32)),
-                ("applied_cap", C.c_uint64),
+                ("deferred", C.POINTER(C.c_uint64)),
+                ("deferred_cap", C.c_uint64),
                 ("n_reads", C.c_uint64), ("n_values", C.c_uint64),
-                ("n_applied", C.c_uint64)]
+                ("n_deferred", C.c_uint64)]
 
 
 class SaveRecord(C.Structure):

@@ -43,6 +43,13 @@ struct drb_engine {
   hipEvent_t ev_fork, ev_join;    // stream -> stream2 -> stream
   hipStream_t stream_h2d;         // drb_stage_proposals uploads
   HsaXfer xfer;  // the engine's own SDMA transfers (drb_hsa.hpp)
+  // sticky: a multi-round call failed after some of its rounds were
+  // enqueued, so the device ran rounds the host did not account for (round
+  // tags, mailbox parity); every later step call returns it
+  int failed = 0;
+  // drb_set_session_clients: per lane the ClientID of the host's NoOP
+  // session of its group ([G], null until set)
+  uint64_t *sess_client = nullptr;
   hipEvent_t ev_staged;           // upload done -> layout kernel
   hipEvent_t ev_stage_free;       // layout kernel done -> next upload
   hipEvent_t ev_uploaded;         // packed upload done -> host arrays free
@@ -269,6 +276,12 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   e->bytes = 0;
   e->scratch = nullptr;
   e->scratch_bytes = 0;
+  if (cfg->host_copies > 1) {
+    delete e;
+    return DRB_EINVAL;
+  }
+  // (host_copies: HIP copies, as when the SDMA engines are unavailable)
+  if (cfg->host_copies) e->xfer.state = -1;
   if (hipSetDevice(cfg->device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
           hipSuccess ||
@@ -512,6 +525,7 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   wire_free(e);
   ingest_free(e->ingest);
   worker_free(e);
+  if (e->sess_client) (void)hipFree(e->sess_client);
   hsa_xfer_fini(&e->xfer);
   (void)hipEventDestroy(e->ev_fork);
   (void)hipEventDestroy(e->ev_join);
@@ -1142,18 +1156,22 @@ using WidenU8 = hipcub::TransformInputIterator<uint32_t, WidenU32,
 using WidenU16 = hipcub::TransformInputIterator<uint32_t, WidenU32,
                                                 const uint16_t *>;
 
+// clients null: every entry of lane g carries the group's registered
+// session client, sess[g] (drb_set_session_clients)
 __global__ void k_stage_packed(View v, uint32_t slot, uint32_t type,
                                const uint8_t *counts, const uint32_t *ent0,
                                const uint64_t *keys, const uint64_t *clients,
-                               const uint16_t *lens, const uint32_t *coff,
-                               const uint8_t *pool, uint64_t pool_len) {
+                               const uint64_t *sess, const uint16_t *lens,
+                               const uint32_t *coff, const uint8_t *pool,
+                               uint64_t pool_len) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= v.G) return;
   const uint32_t n = counts[g];
   v.prop_count[(uint64_t)slot * v.G + g] = n;
+  const uint64_t sc = clients || !n ? 0ull : sess[g];
   for (uint32_t j = 0; j < n; ++j) {
     const uint64_t i = (uint64_t)ent0[g] + j;
-    const uint64_t key = keys[i], cid = clients[i];
+    const uint64_t key = keys[i], cid = clients ? clients[i] : sc;
     const uint32_t len = lens[i];
     const uint64_t off = coff[i];
     v.props[prop_ix(v, slot, j, 0, g)] = mk4h(key, cid);
@@ -1179,17 +1197,18 @@ __global__ void k_stage_packed(View v, uint32_t slot, uint32_t type,
 constexpr size_t kSdmaMinBytes = 8u << 20;
 
 // the packed batch's block layout (drb_stage_packed_layout): counts at 0,
-// then keys, client ids, lengths and the pool, each 256-aligned; *bytes =
-// the block's length
+// then keys, lengths, the pool and last the client ids, each 256-aligned
+// (off[] = keys, client ids, lengths, pool); *bytes = the block's length.
+// A batch of the registered session clients stops at the pool's end.
 static void stage_layout(uint64_t G, uint64_t n, size_t pool_len,
                          uint64_t off[4], size_t *bytes) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const uint64_t n1 = n ? n : 1;
   off[0] = al(G);
-  off[1] = off[0] + al(8 * n1);
-  off[2] = off[1] + al(8 * n1);
+  off[2] = off[0] + al(8 * n1);
   off[3] = off[2] + al(2 * n1);
-  *bytes = off[3] + pool_len;
+  off[1] = al(off[3] + pool_len);
+  *bytes = off[1] + 8 * n1;
 }
 
 extern "C" int drb_stage_packed_layout(const drb_engine *e, uint64_t n_entries,
@@ -1208,9 +1227,10 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
                         const uint16_t *cmd_lens, const uint8_t *pool,
                         size_t pool_len, bool async) {
   if (!e || slot >= e->cfg.prop_slots) return DRB_ERANGE;
-  if (!counts || (n_entries && (!keys || !client_ids || !cmd_lens)) ||
-      (pool_len && !pool))
+  if (!counts || (n_entries && (!keys || !cmd_lens)) || (pool_len && !pool))
     return DRB_EINVAL;
+  // without client ids: the registered session clients
+  if (n_entries && !client_ids && !e->sess_client) return DRB_EINVAL;
   const View &v = e->v;
   const uint64_t G = v.G, n = n_entries;
   // the counts before anything reads the entry arrays (they bound n); the
@@ -1225,7 +1245,7 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
   }
   if (cmax > v.max_props) return DRB_ERANGE;
   if (tsum != n) return DRB_EINVAL;
-  // upload: counts | keys | client ids | lengths | pool (stage_layout),
+  // upload: counts | keys | lengths | pool | client ids (stage_layout),
   // then device-side the two scans and their temp storage
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const uint64_t n1 = n ? n : 1;
@@ -1241,6 +1261,7 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
   stage_layout(G, n, pool_len, lo, &up);
   const size_t o_cnt = 0, o_key = lo[0], o_cid = lo[1], o_len = lo[2],
                o_pool = lo[3];
+  if (!client_ids) up = o_pool + pool_len;  // (no client region)
   const size_t o_e0 = al(std::max<size_t>(up, o_pool + 16)),
                o_off = o_e0 + al(4 * G), o_tmp = o_off + al(4 * n1),
                need = o_tmp + al(std::max(tb1, tb2));
@@ -1265,7 +1286,7 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
   const uint8_t *c8 = counts;
   const bool one_block =
       (const uint8_t *)keys == c8 + o_key &&
-      (const uint8_t *)client_ids == c8 + o_cid &&
+      (!client_ids || (const uint8_t *)client_ids == c8 + o_cid) &&
       (const uint8_t *)cmd_lens == c8 + o_len &&
       (!pool_len || pool == c8 + o_pool);
   // a large pinned one-block batch goes up on the engine's upload SDMA
@@ -1292,8 +1313,9 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
     if (n) {
       HIPCHK(hipMemcpyAsync(d + o_key, keys, 8 * n, hipMemcpyHostToDevice,
                             e->stream_h2d));
-      HIPCHK(hipMemcpyAsync(d + o_cid, client_ids, 8 * n,
-                            hipMemcpyHostToDevice, e->stream_h2d));
+      if (client_ids)
+        HIPCHK(hipMemcpyAsync(d + o_cid, client_ids, 8 * n,
+                              hipMemcpyHostToDevice, e->stream_h2d));
       HIPCHK(hipMemcpyAsync(d + o_len, cmd_lens, 2 * n,
                             hipMemcpyHostToDevice, e->stream_h2d));
     }
@@ -1323,8 +1345,8 @@ static int stage_packed(drb_engine *e, uint32_t slot, uint32_t type,
         d + o_tmp, tb2, WidenU16(l16, WidenU32()), off, (int)n, ls));
   k_stage_packed<<<(unsigned)((G + 255) / 256), 256, 0, ls>>>(
       v, slot, type, d + o_cnt, e0, (const uint64_t *)(d + o_key),
-      (const uint64_t *)(d + o_cid), l16, off, d + o_pool,
-      (uint64_t)pool_len);
+      client_ids ? (const uint64_t *)(d + o_cid) : nullptr, e->sess_client,
+      l16, off, d + o_pool, (uint64_t)pool_len);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e->ev_staged, ls));
   HIPCHK(hipEventRecord(e->ev_stage_free, ls));
@@ -1347,6 +1369,24 @@ extern "C" int drb_stage_proposals_packed_async(
     const uint16_t *cmd_lens, const uint8_t *pool, size_t pool_len) {
   return stage_packed(e, slot, type, counts, n_entries, keys, client_ids,
                       cmd_lens, pool, pool_len, true);
+}
+
+extern "C" int drb_set_session_clients(drb_engine *e,
+                                       const uint64_t *client_ids) {
+  if (!e || !client_ids) return DRB_EINVAL;
+  const uint64_t G = e->v.G;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  if (!e->sess_client) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMalloc(&e->sess_client, std::max<uint64_t>(G, 1) * 8));
+    e->bytes += G * 8;
+  }
+  // ordered before every later staging and export (both streams wait)
+  HIPCHK(hipStreamSynchronize(e->stream_h2d));
+  HIPCHK(hipMemcpyAsync(e->sess_client, client_ids, G * 8,
+                        hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return DRB_OK;
 }
 
 extern "C" int drb_stage_wait_upload(drb_engine *e) {
@@ -1898,8 +1938,11 @@ extern "C" int drb_ingest_ex(drb_engine *e, const drb_message *msgs, size_t n,
 extern "C" int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                           const drb_entry *ents, const uint8_t *pool,
                           uint64_t *accepted, uint64_t *dropped) {
-  return drb_ingest_ex(e, msgs, n, ents, pool, nullptr, accepted, dropped,
-                       nullptr);
+  uint64_t div = 0;
+  const int rc = drb_ingest_ex(e, msgs, n, ents, pool, nullptr, accepted,
+                               dropped, &div);
+  // (a caller without the fates must not lose the diverted messages)
+  return rc == DRB_OK && div ? DRB_EDIVERTED : rc;
 }
 
 // ---------------------------------------------------------------- step
@@ -2243,6 +2286,7 @@ extern "C" int drb_step_round_async(drb_engine *e, const drb_round_in *in) {
   // transport threads stage the next round's inbox under this lock: a
   // round launches and advances e->round atomically with respect to them
   std::lock_guard<std::mutex> ingest_lock(e->ingest_mu);
+  if (e->failed) return e->failed;
   // a durable LogDB: the last round's messages wait for its persistence
   if (e->cfg.durable_log && e->committed_round < e->round) return DRB_EINVAL;
   RoundParams p;
@@ -2283,6 +2327,7 @@ extern "C" int drb_step_rounds(drb_engine *e, const drb_round_in *in,
                                uint32_t k, uint64_t chunk_groups) {
   if (!e || !in || !k) return DRB_EINVAL;
   std::lock_guard<std::mutex> ingest_lock(e->ingest_mu);
+  if (e->failed) return e->failed;
   if (e->v.elections || e->v.remote_mask || e->v.save_tan ||
       e->cfg.durable_log)
     return DRB_EINVAL;
@@ -2299,14 +2344,22 @@ extern "C" int drb_step_rounds(drb_engine *e, const drb_round_in *in,
   // both streams start behind the engine stream's work
   HIPCHK(hipEventRecord(e->ev_fork, e->stream));
   HIPCHK(hipStreamWaitEvent(e->stream2, e->ev_fork, 0));
-  for (uint64_t c0 = 0, c = 0; c0 < gx; c0 += cb, ++c) {
+  int rc = DRB_OK;
+  for (uint64_t c0 = 0, c = 0; c0 < gx && !rc; c0 += cb, ++c) {
     const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, gx - c0);
     hipStream_t st = (c & 1) ? e->stream2 : e->stream;
-    for (uint32_t t = 0; t < k; ++t)
-      if (int rc = launch_any(e, ps[t], st, (uint32_t)c0, nb)) return rc;
+    for (uint32_t t = 0; t < k && !rc; ++t)
+      rc = launch_any(e, ps[t], st, (uint32_t)c0, nb);
   }
-  HIPCHK(hipEventRecord(e->ev_join, e->stream2));
-  HIPCHK(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+  // the second stream joins the engine stream whatever happened
+  const hipError_t j1 = hipEventRecord(e->ev_join, e->stream2);
+  const hipError_t j2 = hipStreamWaitEvent(e->stream, e->ev_join, 0);
+  if (rc || j1 != hipSuccess || j2 != hipSuccess) {
+    // some chunks ran some of the rounds: the engine's round count no
+    // longer matches the device, so it stops stepping
+    e->failed = rc ? rc : DRB_EDEVICE;
+    return e->failed;
+  }
   for (uint32_t t = 0; t < k; ++t) {
     if (ps[t].prop_slot != DRB_NONE)
       HIPCHK(hipEventRecord(e->ev_prop[ps[t].prop_slot], e->stream));

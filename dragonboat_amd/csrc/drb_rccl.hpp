@@ -31,15 +31,16 @@ static void xplan_words(const drb_engine *e, uint32_t leader_mask,
         (*row)[a * R + b] = full_word(v, (leader_mask >> a) & 1u);
 }
 
-extern "C" int drb_exchange_plan(drb_engine *e, uint32_t leader_mask,
-                                 drb_xfer *ops, size_t cap, size_t *n_ops) {
-  if (!e || !n_ops || (cap && !ops)) return DRB_EINVAL;
+// the transfers of one exchange step from every rank's plane words
+// (words[q * R * R + a * R + b]: rank q's word of plane (a, b)): this rank
+// sends plane (a, b) at its own word and receives it at its sender's, in
+// the same (from, to, region) order on every rank
+static int xplan_ops(drb_engine *e, const uint32_t *words, drb_xfer *ops,
+                     size_t cap, size_t *n_ops) {
   *n_ops = 0;
   const View &v = e->v;
   const uint32_t R = v.R;
   if (v.place_world < 2) return DRB_OK;
-  std::vector<uint32_t> row;
-  xplan_words(e, leader_mask, &row);
   size_t n = 0;
   auto put = [&](uint32_t peer, uint32_t recv, const drb_region &r) {
     if (n < cap) ops[n] = drb_xfer{peer, recv, r.ptr, r.bytes};
@@ -52,40 +53,49 @@ extern "C" int drb_exchange_plan(drb_engine *e, uint32_t leader_mask,
       const int dst = drb_place_peer(v.place_world, v.place_rank, a, b, 0);
       if (dst < 0) continue;
       const int src = drb_place_peer(v.place_world, v.place_rank, a, b, 1);
-      const uint32_t w = row[a * R + b];  // the same word on every rank
-      if (!w) continue;
-      int k = drb_plane_regions(e, a, b, w, 0, reg);
-      if (k < 0) return k;
-      for (int i = 0; i < k; ++i) put((uint32_t)dst, 0, reg[i]);
-      k = drb_plane_regions(e, a, b, w, 1, reg);
-      if (k < 0) return k;
-      for (int i = 0; i < k; ++i) put((uint32_t)src, 1, reg[i]);
+      const uint32_t ws = words[(uint64_t)v.place_rank * R * R + a * R + b];
+      const uint32_t wr = words[(uint64_t)src * R * R + a * R + b];
+      if (ws) {
+        const int k = drb_plane_regions(e, a, b, ws, 0, reg);
+        if (k < 0) return k;
+        for (int i = 0; i < k; ++i) put((uint32_t)dst, 0, reg[i]);
+      }
+      if (wr) {
+        const int k = drb_plane_regions(e, a, b, wr, 1, reg);
+        if (k < 0) return k;
+        for (int i = 0; i < k; ++i) put((uint32_t)src, 1, reg[i]);
+      }
     }
   *n_ops = n;
   return n > cap && ops ? DRB_ERANGE : DRB_OK;
 }
 
-extern "C" int drb_exchange_rccl(drb_engine *e, void *comm,
-                                 uint32_t leader_mask) {
-  if (!e || !comm) return DRB_EINVAL;
-  if (e->v.place_world < 2) return drb_exchange_mark(e);
-  int nranks = 0, me = -1;
-  ncclComm_t c = (ncclComm_t)comm;
-  if (ncclCommCount(c, &nranks) != ncclSuccess ||
-      ncclCommUserRank(c, &me) != ncclSuccess)
-    return DRB_EDEVICE;
-  if ((uint32_t)nranks != e->v.place_world ||
-      (uint32_t)me != e->v.place_rank)
-    return DRB_EINVAL;
-  size_t n = 0;
-  if (int rc = drb_exchange_plan(e, leader_mask, nullptr, 0, &n)) return rc;
-  std::vector<drb_xfer> ops(n);
-  if (int rc = drb_exchange_plan(e, leader_mask, ops.data(), n, &n)) return rc;
-  HIPCHK(hipSetDevice(e->cfg.device));
-  // one group on the engine stream: RCCL's kernels run behind the round
-  // that wrote the outbox planes, and the next round behind them
+extern "C" int drb_exchange_plan(drb_engine *e, uint32_t leader_mask,
+                                 drb_xfer *ops, size_t cap, size_t *n_ops) {
+  if (!e || !n_ops || (cap && !ops)) return DRB_EINVAL;
+  *n_ops = 0;
+  const View &v = e->v;
+  if (v.place_world < 2) return DRB_OK;
+  // the fixed step: the same full-capacity row on every rank
+  std::vector<uint32_t> row, all;
+  xplan_words(e, leader_mask, &row);
+  for (uint32_t q = 0; q < v.place_world; ++q)
+    all.insert(all.end(), row.begin(), row.end());
+  return xplan_ops(e, all.data(), ops, cap, n_ops);
+}
+
+extern "C" int drb_exchange_plan_words(drb_engine *e, const uint32_t *words,
+                                       drb_xfer *ops, size_t cap,
+                                       size_t *n_ops) {
+  if (!e || !words || !n_ops || (cap && !ops)) return DRB_EINVAL;
+  return xplan_ops(e, words, ops, cap, n_ops);
+}
+
+// the transfers as ncclSend / ncclRecv in one group on the engine stream
+static int xpost_rccl(drb_engine *e, ncclComm_t c,
+                      const std::vector<drb_xfer> &ops) {
   bool ok = ncclGroupStart() == ncclSuccess;
-  for (size_t i = 0; ok && i < n; ++i) {
+  for (size_t i = 0; ok && i < ops.size(); ++i) {
     const drb_xfer &x = ops[i];
     ok = (x.recv ? ncclRecv(x.ptr, x.bytes, ncclUint8, (int)x.peer, c,
                             e->stream)
@@ -96,6 +106,65 @@ extern "C" int drb_exchange_rccl(drb_engine *e, void *comm,
   if (!ok) return DRB_EDEVICE;
   for (const drb_xfer &x : ops)
     if (x.recv) e->xcopy_bytes += x.bytes;  // (drb_exchange_bytes: inbound)
+  return DRB_OK;
+}
+
+// comm must be the placement's: rank place_rank of place_world
+static int xcomm_check(const drb_engine *e, ncclComm_t c) {
+  int nranks = 0, me = -1;
+  if (ncclCommCount(c, &nranks) != ncclSuccess ||
+      ncclCommUserRank(c, &me) != ncclSuccess)
+    return DRB_EDEVICE;
+  if ((uint32_t)nranks != e->v.place_world ||
+      (uint32_t)me != e->v.place_rank)
+    return DRB_EINVAL;
+  return DRB_OK;
+}
+
+extern "C" int drb_exchange_rccl_counted(drb_engine *e, void *comm) {
+  if (!e || !comm) return DRB_EINVAL;
+  if (e->v.place_world < 2) return drb_exchange_mark(e);
+  ncclComm_t c = (ncclComm_t)comm;
+  if (int rc = xcomm_check(e, c)) return rc;
+  const uint32_t R = e->v.R, W = e->v.place_world;
+  const size_t rr = (size_t)R * R;
+  // this rank's words (a synchronisation of the engine stream), then every
+  // rank's (an all-gather on the engine stream, read back)
+  std::vector<uint32_t> mine(rr), all(rr * W);
+  if (int rc = drb_plane_counts(e, mine.data())) return rc;
+  void *d = nullptr;
+  if (scratch(e, 4 * rr * (W + 1), &d)) return DRB_ENOMEM;
+  uint32_t *dm = (uint32_t *)d, *da = dm + rr;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  HIPCHK(hipMemcpyAsync(dm, mine.data(), 4 * rr, hipMemcpyHostToDevice,
+                        e->stream));
+  if (ncclAllGather(dm, da, rr, ncclUint32, c, e->stream) != ncclSuccess)
+    return DRB_EDEVICE;
+  HIPCHK(hipMemcpyAsync(all.data(), da, 4 * rr * W, hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  size_t n = 0;
+  if (int rc = xplan_ops(e, all.data(), nullptr, 0, &n)) return rc;
+  std::vector<drb_xfer> ops(n);
+  if (int rc = xplan_ops(e, all.data(), ops.data(), n, &n)) return rc;
+  if (int rc = xpost_rccl(e, c, ops)) return rc;
+  return drb_exchange_mark(e);
+}
+
+extern "C" int drb_exchange_rccl(drb_engine *e, void *comm,
+                                 uint32_t leader_mask) {
+  if (!e || !comm) return DRB_EINVAL;
+  if (e->v.place_world < 2) return drb_exchange_mark(e);
+  ncclComm_t c = (ncclComm_t)comm;
+  if (int rc = xcomm_check(e, c)) return rc;
+  size_t n = 0;
+  if (int rc = drb_exchange_plan(e, leader_mask, nullptr, 0, &n)) return rc;
+  std::vector<drb_xfer> ops(n);
+  if (int rc = drb_exchange_plan(e, leader_mask, ops.data(), n, &n)) return rc;
+  HIPCHK(hipSetDevice(e->cfg.device));
+  // one group on the engine stream: RCCL's kernels run behind the round
+  // that wrote the outbox planes, and the next round behind them
+  if (int rc = xpost_rccl(e, c, ops)) return rc;
   return drb_exchange_mark(e);
 }
 

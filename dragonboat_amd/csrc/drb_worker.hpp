@@ -8,11 +8,12 @@
 // 930-953) and the applied entries (pendingProposals.applied, node.go:
 // 243-257).  Here one export covers every group of a replica slot:
 //   1. on the engine stream, behind the round: per lane the three record
-//      counts, one exclusive scan of {reads, values, applied} (hipCUB), and
-//      a compaction of the lean records (include/drb_engine.h: a word per
-//      lane, 16 B per ReadyToRead, 4 B + a nibble per served read, 4 B per
-//      applied entry) into device staging[parity]; the totals go straight
-//      to mapped host memory;
+//      counts, one exclusive scan of {ReadyToReads, values, deferred}
+//      (hipCUB), and a compaction of the lean records (include/drb_engine.h:
+//      a word per lane -- its applied count included --, a 4 B ctx tag per
+//      ReadyToRead, 4 B + 2 bits per served read, 8 B per ReadyToRead whose
+//      reads were not served) into device staging[parity]; the totals go
+//      straight to mapped host memory;
 //   2. the engine's drain thread waits for that compaction and copies
 //      exactly those bytes into the caller's pinned buffers on the
 //      engine's download SDMA engine (drb_hsa.hpp: a completion signal per
@@ -33,48 +34,69 @@
 #include <deque>
 #include <thread>
 
+// staging sets: an export takes a free one and holds it until its wait
+// (two per step worker, one per partition and parity)
+constexpr int kWorkerSets = 16;
+
+struct WorkerSet {
+  hipEvent_t ev_staged = nullptr, ev_drained = nullptr;
+  uint32_t *lanes = nullptr;  // [G]
+  uint32_t *rd = nullptr;     // ctx tags
+  uint32_t *val = nullptr;
+  uint32_t *meta = nullptr;   // 2-bit codes, 16 per word
+  uint64_t *dfr = nullptr;    // deferred ReadyToReads' Index
+  uint64_t cap_rd = 0, cap_val = 0, cap_df = 0;  // staging capacity
+  // the buffers of the export in flight (waited for or not)
+  const drb_worker_bufs *owner = nullptr;
+  bool issued = false;  // the copies of its job issued
+  int err = 0;          // a failed copy (reported and cleared by its wait)
+  hsa_signal_t done{0};  // copies outstanding (HSA)
+};
+
 struct WorkerState {
   hipStream_t sx = nullptr;  // the drain thread's copies
-  hipEvent_t ev_staged[2] = {nullptr, nullptr};
-  hipEvent_t ev_drained[2] = {nullptr, nullptr};
-  uint32_t *lanes[2] = {nullptr, nullptr};  // [G]
-  drb_worker_read *rd[2] = {nullptr, nullptr};
-  uint32_t *val[2] = {nullptr, nullptr};
-  uint32_t *meta[2] = {nullptr, nullptr};  // nibbles, 8 per word
-  uint32_t *ap[2] = {nullptr, nullptr};
-  uint64_t cap_rd = 0, cap_val = 0, cap_ap = 0;  // staging capacity
-  uint4 *cnt = nullptr, *off = nullptr;          // [G + 1]
+  WorkerSet set[kWorkerSets];
+  uint4 *cnt = nullptr, *off = nullptr;  // [G + 1]
   void *tmp = nullptr;
   size_t tmp_bytes = 0;
-  unsigned long long *hdr = nullptr;      // pinned, mapped [2][4]: totals
+  unsigned long long *hdr = nullptr;      // pinned, mapped [sets][4]: totals
   unsigned long long *hdr_dev = nullptr;  // ... its device address
-  // the buffers of the exports in flight (waited for or not), by parity
-  const drb_worker_bufs *owner[2] = {nullptr, nullptr};
-  uint64_t seq = 0;
   // the drain thread: one job per export, in order
   struct Job {
     int k;
     drb_worker_bufs b;  // (the pointers and capacities at export time)
+    uint64_t np;        // lanes exported
   };
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;
   std::deque<Job> jobs;
-  bool issued[2] = {false, false};  // the copies of its job issued
-  int err = 0;                      // a failed copy (reported by wait)
   bool stop = false;
   // the copies on the engine's download SDMA engine (drb_hsa.hpp;
   // hipMemcpyAsync on sx when HSA is unavailable)
   bool hsa = false;
-  hsa_signal_t done[2] = {{0}, {0}};  // copies outstanding, by parity
 };
 
-// until the copies of buffer set k are done
+// until the copies of staging set k are done
 static void worker_wait_copies(WorkerState &w, int k) {
   if (!w.hsa) return;
-  while (hsa_signal_wait_scacquire(w.done[k], HSA_SIGNAL_CONDITION_LT, 1,
+  while (hsa_signal_wait_scacquire(w.set[k].done, HSA_SIGNAL_CONDITION_LT, 1,
                                    UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
   }
+}
+
+// every export's copies issued and done (the drain thread idle)
+static void worker_quiesce(WorkerState &w) {
+  {
+    std::unique_lock<std::mutex> g(w.mu);
+    w.cv.wait(g, [&] {
+      if (!w.jobs.empty()) return false;
+      for (const WorkerSet &s : w.set)
+        if (s.owner && !s.issued) return false;
+      return true;
+    });
+  }
+  for (int k = 0; k < kWorkerSets; ++k) worker_wait_copies(w, k);
 }
 
 namespace {
@@ -100,67 +122,92 @@ __device__ inline void worker_apply_range(const View &v, uint32_t slot,
   }
 }
 
-__global__ void k_worker_count(const View v, uint32_t slot, uint32_t n_reads,
-                               uint4 *cnt) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g > v.G) return;
-  uint4 c = make_uint4(0, 0, 0, 0);
-  if (g < v.G) {
-    const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
-    c.x = nr;
-    if (nr && n_reads) {
-      const uint32_t m = v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u);
-      c.y = (uint32_t)__popc(m) * n_reads;
-    }
-    uint64_t lo, hi;
-    worker_apply_range(v, slot, g, &lo, &hi);
-    c.z = hi > lo ? (uint32_t)min(hi - lo, (uint64_t)0xffffu) : 0u;
+// the host's own entries among the applied ones (include/drb_engine.h):
+// those of its registered session client (sess), else every entry with a
+// ClientID -- raft's own empty entries have none (statemachine.go:939)
+__device__ inline uint32_t worker_applied(const View &v, uint32_t slot,
+                                          uint64_t g, const uint64_t *sess) {
+  uint64_t lo, hi;
+  worker_apply_range(v, slot, g, &lo, &hi);
+  const uint64_t sc = sess ? sess[g] : 0ull;
+  uint32_t n = 0;
+  for (uint64_t idx = lo + 1; idx <= hi; ++idx) {
+    const uint64_t client = lo64(v.ring[ring_ix(v, slot, idx, 1, g)]);
+    n += client != 0 && (sess == nullptr || client == sc);
   }
-  cnt[g] = c;  // cnt[G] = 0: the scan's last element is the total
+  return min(n, 0xffffu);
 }
 
-// a served read's value-meta nibble (include/drb_engine.h): read_res.y is
-// vlen | found << 31 (serve_reads_lane)
-__device__ inline uint32_t worker_nibble(uint32_t y) {
-  if (!(y >> 31)) return 0u;
-  const uint32_t vlen = y & 0x7fffffffu;
-  return DRB_WORKER_FOUND | (vlen > 4 ? (uint32_t)DRB_WORKER_LONG : vlen);
+// lanes g0, g0 + stride, ... (np of them): one step worker's partition
+__global__ void k_worker_count(const View v, uint32_t slot, uint32_t n_reads,
+                               uint64_t g0, uint64_t stride, uint64_t np,
+                               uint4 *cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > np) return;
+  const uint64_t g = g0 + i * stride;
+  uint4 c = make_uint4(0, 0, 0, 0);
+  if (i < np) {
+    const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
+    const uint32_t m =
+        nr && n_reads ? v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u) : 0u;
+    c.x = nr;
+    c.y = (uint32_t)__popc(m) * n_reads;
+    c.z = nr - (uint32_t)__popc(m);
+  }
+  cnt[i] = c;  // cnt[np] = 0: the scan's last element is the total
+}
+
+// a served read's 2-bit code and value word (include/drb_engine.h):
+// read_res.y is vlen | found << 31 (serve_reads_lane), .x the value's first
+// 4 bytes
+__device__ inline uint32_t worker_code(uint2 w, uint32_t *word) {
+  *word = w.x;
+  if (!(w.y >> 31)) {
+    *word = 0;
+    return DRB_WORKER_MISS;
+  }
+  const uint32_t vlen = w.y & 0x7fffffffu;
+  if (vlen == 4) return DRB_WORKER_V4;
+  if (vlen > 4) return DRB_WORKER_LONG;
+  *word = (w.x & ((1u << (8 * vlen)) - 1u)) | (vlen << 24);
+  return DRB_WORKER_SHORT;
 }
 
 __global__ void k_worker_compact(const View v, uint32_t slot,
-                                 uint32_t n_reads, const uint4 *off,
-                                 uint32_t *lanes, drb_worker_read *rd,
+                                 uint32_t n_reads, uint64_t g0,
+                                 uint64_t stride, uint64_t np,
+                                 const uint64_t *sess, const uint4 *off,
+                                 uint32_t *lanes, uint32_t *rd,
                                  uint64_t cap_rd, uint32_t *val,
                                  uint32_t *meta, uint64_t cap_val,
-                                 uint32_t *ap, uint64_t cap_ap,
+                                 uint64_t *dfr, uint64_t cap_df,
                                  unsigned long long *tot) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g == v.G) {  // the totals, into mapped host memory
-    tot[0] = off[g].x;
-    tot[1] = off[g].y;
-    tot[2] = off[g].z;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == np) {  // the totals, into mapped host memory
+    tot[0] = off[i].x;
+    tot[1] = off[i].y;
+    tot[2] = off[i].z;
     __threadfence_system();
   }
-  if (g >= v.G) return;
-  const uint4 o = off[g];
+  if (i >= np) return;
+  const uint64_t g = g0 + i * stride;
+  const uint4 o = off[i];
   const uint32_t nr = min(v.rtr_count[ix(v, slot, g)], (uint32_t)RTR_CAP);
   const uint32_t m =
       nr && n_reads ? v.read_served[ix(v, slot, g)] & ((1u << nr) - 1u) : 0u;
-  uint64_t lo, hi;
-  worker_apply_range(v, slot, g, &lo, &hi);
-  const uint32_t na = hi > lo ? (uint32_t)min(hi - lo, (uint64_t)0xffffu) : 0u;
-  lanes[g] = nr | (m << 4) | (na << 12);
-  uint64_t vo = o.y;
-  // the nibbles of this lane's reads, one word (8 nibbles) at a time; the
+  const uint32_t na = worker_applied(v, slot, g, sess);
+  lanes[i] = nr | (m << 4) | (na << 12);
+  uint64_t vo = o.y, di = o.z;
+  // the codes of this lane's reads, one word (16 codes) at a time; the
   // first and last words may be shared with the neighbouring lanes (the
   // staging words start zeroed, shared ones take an atomicOr)
   uint32_t word = 0;
-  uint64_t wi = vo / 8;
+  uint64_t wi = vo / 16;
   auto flush = [&](bool last) {
     if (!word) return;
-    const uint64_t first_w = o.y / 8;
+    const uint64_t first_w = o.y / 16;
     const bool shared = wi == first_w || last;
-    if (wi * 8 < cap_val) {
+    if (wi * 16 < cap_val) {
       if (shared)
         atomicOr(&meta[wi], word);
       else
@@ -169,35 +216,26 @@ __global__ void k_worker_compact(const View v, uint32_t slot,
     word = 0;
   };
   for (uint32_t k = 0; k < nr; ++k) {
-    if (o.x + k < cap_rd) {
-      const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
-      drb_worker_read r;
-      r.index = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
-      r.ctx_low = (uint64_t)c0.z | ((uint64_t)c0.w << 32);
-      rd[o.x + k] = r;
+    const uint4 c0 = v.rtr[rtr_ix(v, slot, k, 0, g)];
+    if (o.x + k < cap_rd) rd[o.x + k] = c0.z;  // the ctx tag: Low's low word
+    if (!((m >> k) & 1u)) {  // not served: the host needs its Index
+      if (di < cap_df) dfr[di] = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+      ++di;
+      continue;
     }
-    if (!((m >> k) & 1u)) continue;
     for (uint32_t j = 0; j < n_reads; ++j, ++vo) {
-      const uint2 w = v.read_res[rres_ix(v, slot, k, j, g)];
-      if (vo < cap_val) val[vo] = w.x;
-      if (vo / 8 != wi) {
+      uint32_t x;
+      const uint32_t code =
+          worker_code(v.read_res[rres_ix(v, slot, k, j, g)], &x);
+      if (vo < cap_val) val[vo] = x;
+      if (vo / 16 != wi) {
         flush(false);
-        wi = vo / 8;
+        wi = vo / 16;
       }
-      word |= worker_nibble(w.y) << (4 * (vo & 7));
+      word |= code << (2 * (vo & 15));
     }
   }
   flush(true);
-  for (uint64_t idx = lo + 1, a = o.z; idx <= hi && a < cap_ap; ++idx, ++a) {
-    const uint4 m1 = v.ring[ring_ix(v, slot, idx, 1, g)];
-    const uint4 m2 = v.ring[ring_ix(v, slot, idx, 2, g)];
-    const uint64_t client = lo64(m1);
-    const uint32_t type = m2.z, clen = m2.w;
-    // KVTest.Update's Result.Value: the payload length (kvtest.go:161); an
-    // empty no-op entry is ignored by the rsm (statemachine.go:939)
-    ap[a] = client == 0 ? DRB_WORKER_IGNORED
-                        : (type == DRB_ENTRY_ENCODED && clen ? clen - 1 : clen);
-  }
 }
 
 }  // namespace
@@ -214,19 +252,19 @@ static void worker_free(drb_engine *e) {
     w->th.join();
   }
   if (w->sx) (void)hipStreamSynchronize(w->sx);
-  if (w->hsa)
-    for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kWorkerSets; ++k) {
+    WorkerSet &s = w->set[k];
+    if (w->hsa) {
       worker_wait_copies(*w, k);
-      (void)hsa_signal_destroy(w->done[k]);
+      if (s.done.handle) (void)hsa_signal_destroy(s.done);
     }
-  for (int k = 0; k < 2; ++k) {
-    if (w->ev_staged[k]) (void)hipEventDestroy(w->ev_staged[k]);
-    if (w->ev_drained[k]) (void)hipEventDestroy(w->ev_drained[k]);
-    if (w->lanes[k]) (void)hipFree(w->lanes[k]);
-    if (w->rd[k]) (void)hipFree(w->rd[k]);
-    if (w->val[k]) (void)hipFree(w->val[k]);
-    if (w->meta[k]) (void)hipFree(w->meta[k]);
-    if (w->ap[k]) (void)hipFree(w->ap[k]);
+    if (s.ev_staged) (void)hipEventDestroy(s.ev_staged);
+    if (s.ev_drained) (void)hipEventDestroy(s.ev_drained);
+    if (s.lanes) (void)hipFree(s.lanes);
+    if (s.rd) (void)hipFree(s.rd);
+    if (s.val) (void)hipFree(s.val);
+    if (s.meta) (void)hipFree(s.meta);
+    if (s.dfr) (void)hipFree(s.dfr);
   }
   if (w->cnt) (void)hipFree(w->cnt);
   if (w->off) (void)hipFree(w->off);
@@ -242,32 +280,33 @@ static void worker_free(drb_engine *e) {
 static hipError_t worker_copy(drb_engine *e, WorkerState &w,
                               const WorkerState::Job &j) {
   const int k = j.k;
-  hipError_t r = hipEventSynchronize(w.ev_staged[k]);
+  WorkerSet &s = w.set[k];
+  hipError_t r = hipEventSynchronize(s.ev_staged);
   if (r != hipSuccess) return r;
   const unsigned long long *t = w.hdr + 4 * k;
   const uint64_t nrd = std::min<uint64_t>(t[0], j.b.reads_cap);
   const uint64_t nval = std::min<uint64_t>(t[1], j.b.values_cap);
-  const uint64_t nap = std::min<uint64_t>(t[2], j.b.applied_cap);
+  const uint64_t ndf = std::min<uint64_t>(t[2], j.b.deferred_cap);
   struct {
     void *dst;
     const void *src;
     size_t n;
-  } cp[5] = {{j.b.lanes, w.lanes[k], (size_t)e->v.G * 4},
-             {j.b.reads, w.rd[k], nrd * sizeof(drb_worker_read)},
-             {j.b.values, w.val[k], nval * 4},
-             {j.b.value_meta, w.meta[k], (nval + 1) / 2},
-             {j.b.applied, w.ap[k], nap * 4}};
+  } cp[5] = {{j.b.lanes, s.lanes, (size_t)j.np * 4},
+             {j.b.reads, s.rd, nrd * 4},
+             {j.b.values, s.val, nval * 4},
+             {j.b.value_meta, s.meta, (nval + 3) / 4},
+             {j.b.deferred, s.dfr, ndf * 8}};
   if (w.hsa) {
     const HsaXfer &x = e->xfer;
     int n = 0;
     for (auto &c : cp) n += c.n && c.dst;
-    hsa_signal_store_screlease(w.done[k], n);
+    hsa_signal_store_screlease(s.done, n);
     for (auto &c : cp) {
       if (!(c.n && c.dst)) continue;
       if (hsa_amd_memory_async_copy_on_engine(
-              c.dst, x.cpu, c.src, x.gpu, c.n, 0, nullptr, w.done[k],
+              c.dst, x.cpu, c.src, x.gpu, c.n, 0, nullptr, s.done,
               (hsa_amd_sdma_engine_id_t)x.down, true) != HSA_STATUS_SUCCESS) {
-        hsa_signal_subtract_screlease(w.done[k], 1);
+        hsa_signal_subtract_screlease(s.done, 1);
         r = hipErrorUnknown;
       }
     }
@@ -276,7 +315,7 @@ static hipError_t worker_copy(drb_engine *e, WorkerState &w,
   for (auto &c : cp)
     if (c.n && c.dst && r == hipSuccess)
       r = hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, w.sx);
-  if (r == hipSuccess) r = hipEventRecord(w.ev_drained[k], w.sx);
+  if (r == hipSuccess) r = hipEventRecord(s.ev_drained, w.sx);
   return r;
 }
 
@@ -295,51 +334,53 @@ static void worker_thread(drb_engine *e) {
     const hipError_t r = worker_copy(e, w, j);
     {
       std::lock_guard<std::mutex> g(w.mu);
-      if (r != hipSuccess) w.err = DRB_EDEVICE;
-      w.issued[j.k] = true;
+      if (r != hipSuccess) w.set[j.k].err = DRB_EDEVICE;
+      w.set[j.k].issued = true;
     }
     w.cv.notify_all();
   }
 }
 
-// device staging of at least these capacities (grow-only; growing waits
-// for the exports in flight)
-static int worker_reserve(drb_engine *e, uint64_t crd, uint64_t cval,
-                          uint64_t cap) {
-  WorkerState &w = *e->worker;
-  if (crd <= w.cap_rd && cval <= w.cap_val && cap <= w.cap_ap) return DRB_OK;
-  {
-    // every export's copies issued (the drain thread done with its jobs)
-    std::unique_lock<std::mutex> g(w.mu);
-    w.cv.wait(g, [&] {
-      return w.jobs.empty() && (!w.owner[0] || w.issued[0]) &&
-             (!w.owner[1] || w.issued[1]);
-    });
+// the 2-bit code words of cval reads (+ slack for the last shared word)
+static uint64_t worker_meta_words(uint64_t cval) {
+  return std::max<uint64_t>(cval, 1) / 16 + 2;
+}
+
+// staging set k (free: no export holds it, its copies done) of at least
+// these capacities (grow-only)
+static int worker_reserve(drb_engine *e, int k, uint64_t crd, uint64_t cval,
+                          uint64_t cdf) {
+  WorkerSet &s = e->worker->set[k];
+  if (!s.lanes) {
+    HIPCHK(hipEventCreateWithFlags(&s.ev_staged, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_drained, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&s.lanes, std::max<uint64_t>(e->v.G, 1) * 4 + 16));
+    if (e->worker->hsa &&
+        hsa_signal_create(0, 0, nullptr, &s.done) != HSA_STATUS_SUCCESS)
+      return DRB_EDEVICE;
   }
-  for (int k = 0; k < 2; ++k) worker_wait_copies(w, k);
-  HIPCHK(hipStreamSynchronize(w.sx));
+  if (s.rd && crd <= s.cap_rd && cval <= s.cap_val && cdf <= s.cap_df)
+    return DRB_OK;
+  // (the engine stream's earlier exports may still read the old staging)
   HIPCHK(hipStreamSynchronize(e->stream));
-  crd = std::max(crd, w.cap_rd);
-  cval = std::max(cval, w.cap_val);
-  cap = std::max(cap, w.cap_ap);
-  for (int k = 0; k < 2; ++k) {
-    if (w.rd[k]) HIPCHK(hipFree(w.rd[k]));
-    if (w.val[k]) HIPCHK(hipFree(w.val[k]));
-    if (w.meta[k]) HIPCHK(hipFree(w.meta[k]));
-    if (w.ap[k]) HIPCHK(hipFree(w.ap[k]));
-    w.rd[k] = nullptr;
-    w.val[k] = nullptr;
-    w.meta[k] = nullptr;
-    w.ap[k] = nullptr;
-    HIPCHK(hipMalloc(&w.rd[k], std::max<uint64_t>(crd, 1) *
-                                   sizeof(drb_worker_read)));
-    HIPCHK(hipMalloc(&w.val[k], std::max<uint64_t>(cval, 1) * 4 + 16));
-    HIPCHK(hipMalloc(&w.meta[k], (std::max<uint64_t>(cval, 1) / 8 + 2) * 4));
-    HIPCHK(hipMalloc(&w.ap[k], std::max<uint64_t>(cap, 1) * 4 + 16));
-  }
-  w.cap_rd = crd;
-  w.cap_val = cval;
-  w.cap_ap = cap;
+  crd = std::max(crd, s.cap_rd);
+  cval = std::max(cval, s.cap_val);
+  cdf = std::max(cdf, s.cap_df);
+  if (s.rd) HIPCHK(hipFree(s.rd));
+  if (s.val) HIPCHK(hipFree(s.val));
+  if (s.meta) HIPCHK(hipFree(s.meta));
+  if (s.dfr) HIPCHK(hipFree(s.dfr));
+  s.rd = nullptr;
+  s.val = nullptr;
+  s.meta = nullptr;
+  s.dfr = nullptr;
+  HIPCHK(hipMalloc(&s.rd, std::max<uint64_t>(crd, 1) * 4 + 16));
+  HIPCHK(hipMalloc(&s.val, std::max<uint64_t>(cval, 1) * 4 + 16));
+  HIPCHK(hipMalloc(&s.meta, worker_meta_words(cval) * 4));
+  HIPCHK(hipMalloc(&s.dfr, std::max<uint64_t>(cdf, 1) * 8 + 16));
+  s.cap_rd = crd;
+  s.cap_val = cval;
+  s.cap_df = cdf;
   return DRB_OK;
 }
 
@@ -350,12 +391,6 @@ static int worker_init(drb_engine *e) {
   const uint64_t G = e->v.G;
   HIPCHK(hipSetDevice(e->cfg.device));
   HIPCHK(hipStreamCreateWithFlags(&w->sx, hipStreamNonBlocking));
-  for (int k = 0; k < 2; ++k) {
-    HIPCHK(hipEventCreateWithFlags(&w->ev_staged[k], hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&w->ev_drained[k], hipEventDisableTiming));
-  }
-  for (int k = 0; k < 2; ++k)
-    HIPCHK(hipMalloc(&w->lanes[k], std::max<uint64_t>(G, 1) * 4 + 16));
   HIPCHK(hipMalloc(&w->cnt, (G + 1) * sizeof(uint4)));
   HIPCHK(hipMalloc(&w->off, (G + 1) * sizeof(uint4)));
   HIPCHK(hipcub::DeviceScan::ExclusiveScan(nullptr, w->tmp_bytes, w->cnt,
@@ -363,20 +398,12 @@ static int worker_init(drb_engine *e) {
                                            make_uint4(0, 0, 0, 0),
                                            (int)(G + 1), e->stream));
   HIPCHK(hipMalloc(&w->tmp, std::max<size_t>(w->tmp_bytes, 16)));
-  HIPCHK(hipHostMalloc((void **)&w->hdr, 8 * sizeof(unsigned long long),
-                       hipHostMallocMapped));
-  memset(w->hdr, 0, 8 * sizeof(unsigned long long));
+  const size_t hb = 4 * kWorkerSets * sizeof(unsigned long long);
+  HIPCHK(hipHostMalloc((void **)&w->hdr, hb, hipHostMallocMapped));
+  memset(w->hdr, 0, hb);
   HIPCHK(hipHostGetDevicePointer((void **)&w->hdr_dev, w->hdr, 0));
   // the copies on the engine's download SDMA engine (drb_hsa.hpp)
-  if (hsa_xfer_init(e->cfg.device, &e->xfer)) {
-    w->hsa = hsa_signal_create(0, 0, nullptr, &w->done[0]) ==
-             HSA_STATUS_SUCCESS;
-    if (w->hsa && hsa_signal_create(0, 0, nullptr, &w->done[1]) !=
-                      HSA_STATUS_SUCCESS) {
-      (void)hsa_signal_destroy(w->done[0]);
-      w->hsa = false;
-    }
-  }
+  w->hsa = hsa_xfer_init(e->cfg.device, &e->xfer);
   w->th = std::thread(worker_thread, e);
   return DRB_OK;
 }
@@ -394,14 +421,7 @@ extern "C" int drb_host_free(drb_engine *e, void *p) {
   if (p) {
     if (WorkerState *w = e->worker) {
       // no copy of an export in flight may still write into it
-      {
-        std::unique_lock<std::mutex> g(w->mu);
-        w->cv.wait(g, [&] {
-          return w->jobs.empty() && (!w->owner[0] || w->issued[0]) &&
-                 (!w->owner[1] || w->issued[1]);
-        });
-      }
-      for (int k = 0; k < 2; ++k) worker_wait_copies(*w, k);
+      worker_quiesce(*w);
       if (w->sx) HIPCHK(hipStreamSynchronize(w->sx));
     }
     HIPCHK(hipHostFree(p));
@@ -409,59 +429,94 @@ extern "C" int drb_host_free(drb_engine *e, void *p) {
   return DRB_OK;
 }
 
-static int worker_dev_ptr(void *h, void **d) {
-  *d = nullptr;
-  if (!h) return DRB_OK;
-  HIPCHK(hipHostGetDevicePointer(d, h, 0));
+// the SDMA engine writes the caller's buffers directly: every byte of each
+// must be pinned host memory (its first and its last byte checked, as
+// drb_stage_proposals_packed checks its upload)
+static bool worker_pinned(const void *p, uint64_t bytes) {
+  if (!p || !bytes) return true;
+  return hsa_host_pinned(p) &&
+         hsa_host_pinned((const uint8_t *)p + (bytes - 1));
+}
+
+extern "C" int drb_worker_export_part(drb_engine *e, uint32_t slot,
+                                      uint32_t n_parts, uint32_t part,
+                                      const drb_worker_bufs *b) {
+  if (!e || !b || slot >= e->v.R || !n_parts || part >= n_parts)
+    return DRB_EINVAL;
+  const View &v = e->v;
+  // the partition's lanes: ShardID % n_parts == part (FixedPartitioner,
+  // internal/server/partition.go:38), i.e. every n_parts-th lane from g0
+  // (co-resident placement: lane g is ShardID first_shard_id + g)
+  if (n_parts > 1 && v.place_world > 1) return DRB_EINVAL;
+  const uint64_t g0 =
+      (part + n_parts - (uint32_t)(e->cfg.first_shard_id % n_parts)) % n_parts;
+  const uint64_t np = v.G > g0 ? (v.G - g0 + n_parts - 1) / n_parts : 0;
+  if (!b->lanes || b->lanes_cap < np || (b->reads_cap && !b->reads) ||
+      (b->values_cap && (!b->values || !b->value_meta)) ||
+      (b->deferred_cap && !b->deferred))
+    return DRB_EINVAL;
+  if (!worker_pinned(b->lanes, np * 4) ||
+      !worker_pinned(b->reads, b->reads_cap * 4) ||
+      !worker_pinned(b->values, b->values_cap * 4) ||
+      !worker_pinned(b->value_meta, (b->values_cap + 3) / 4) ||
+      !worker_pinned(b->deferred, b->deferred_cap * 8))
+    return DRB_EINVAL;
+  if (int rc = worker_init(e)) return rc;
+  WorkerState &w = *e->worker;
+  int k = -1;
+  {
+    // one export in flight per buffer set, and a free staging set (its
+    // last export waited for: its copies are done)
+    std::lock_guard<std::mutex> g(w.mu);
+    for (int q = 0; q < kWorkerSets; ++q) {
+      if (w.set[q].owner == b) return DRB_EAGAIN;
+      if (k < 0 && !w.set[q].owner) k = q;
+    }
+    if (k < 0) return DRB_EAGAIN;
+    w.set[k].owner = b;  // (held from here; released on failure below)
+    w.set[k].issued = false;
+  }
+  auto release = [&](int rc) {
+    std::lock_guard<std::mutex> g(w.mu);
+    w.set[k].owner = nullptr;
+    return rc;
+  };
+  WorkerSet &s = w.set[k];
+  if (int rc = worker_reserve(e, k, b->reads_cap, b->values_cap,
+                              b->deferred_cap))
+    return release(rc);
+  // the reads of the last round, if it served them with results
+  const uint32_t n_reads =
+      v.read_res && e->reads_round == e->round ? e->reads_n : 0u;
+  const unsigned blocks = (unsigned)((np + 1 + 255) / 256);
+  k_worker_count<<<blocks, 256, 0, e->stream>>>(v, slot, n_reads, g0,
+                                                n_parts, np, w.cnt);
+  size_t tb = w.tmp_bytes;
+  if (hipGetLastError() != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveScan(w.tmp, tb, w.cnt, w.off, U4Sum(),
+                                        make_uint4(0, 0, 0, 0), (int)(np + 1),
+                                        e->stream) != hipSuccess ||
+      hipMemsetAsync(s.meta, 0, worker_meta_words(s.cap_val) * 4,
+                     e->stream) != hipSuccess)
+    return release(DRB_EDEVICE);
+  k_worker_compact<<<blocks, 256, 0, e->stream>>>(
+      v, slot, n_reads, g0, n_parts, np, e->sess_client, w.off, s.lanes, s.rd,
+      b->reads_cap, s.val, s.meta, b->values_cap, s.dfr, b->deferred_cap,
+      w.hdr_dev + 4 * k);
+  if (hipGetLastError() != hipSuccess ||
+      hipEventRecord(s.ev_staged, e->stream) != hipSuccess)
+    return release(DRB_EDEVICE);
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    w.jobs.push_back(WorkerState::Job{k, *b, np});
+  }
+  w.cv.notify_all();
   return DRB_OK;
 }
 
 extern "C" int drb_worker_export(drb_engine *e, uint32_t slot,
                                  const drb_worker_bufs *b) {
-  if (!e || !b || slot >= e->v.R) return DRB_EINVAL;
-  if (!b->lanes || b->lanes_cap < e->v.G || (b->reads_cap && !b->reads) ||
-      (b->values_cap && (!b->values || !b->value_meta)) ||
-      (b->applied_cap && !b->applied))
-    return DRB_EINVAL;
-  if (int rc = worker_init(e)) return rc;
-  WorkerState &w = *e->worker;
-  const int k = (int)(w.seq & 1);
-  {
-    // one export in flight per buffer set, and staging[k] free (its
-    // export, two back, waited for: its copies are done)
-    std::lock_guard<std::mutex> g(w.mu);
-    if (w.owner[0] == b || w.owner[1] == b || w.owner[k]) return DRB_EAGAIN;
-  }
-  if (int rc = worker_reserve(e, b->reads_cap, b->values_cap, b->applied_cap))
-    return rc;
-  const View &v = e->v;
-  // the reads of the last round, if it served them with results
-  const uint32_t n_reads =
-      v.read_res && e->reads_round == e->round ? e->reads_n : 0u;
-  const unsigned blocks = (unsigned)((v.G + 1 + 255) / 256);
-  k_worker_count<<<blocks, 256, 0, e->stream>>>(v, slot, n_reads, w.cnt);
-  HIPCHK(hipGetLastError());
-  size_t tb = w.tmp_bytes;
-  HIPCHK(hipcub::DeviceScan::ExclusiveScan(w.tmp, tb, w.cnt, w.off, U4Sum(),
-                                           make_uint4(0, 0, 0, 0),
-                                           (int)(v.G + 1), e->stream));
-  HIPCHK(hipMemsetAsync(w.meta[k], 0,
-                        (std::max<uint64_t>(w.cap_val, 1) / 8 + 2) * 4,
-                        e->stream));
-  k_worker_compact<<<blocks, 256, 0, e->stream>>>(
-      v, slot, n_reads, w.off, w.lanes[k], w.rd[k], b->reads_cap, w.val[k],
-      w.meta[k], b->values_cap, w.ap[k], b->applied_cap, w.hdr_dev + 4 * k);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(w.ev_staged[k], e->stream));
-  {
-    std::lock_guard<std::mutex> g(w.mu);
-    w.owner[k] = b;
-    w.issued[k] = false;
-    w.jobs.push_back(WorkerState::Job{k, *b});
-  }
-  w.cv.notify_all();
-  w.seq++;
-  return DRB_OK;
+  return drb_worker_export_part(e, slot, 1, 0, b);
 }
 
 extern "C" int drb_worker_wait(drb_engine *e, drb_worker_bufs *b) {
@@ -470,25 +525,36 @@ extern "C" int drb_worker_wait(drb_engine *e, drb_worker_bufs *b) {
   int k = -1;
   {
     std::unique_lock<std::mutex> g(w.mu);
-    for (int q = 0; q < 2; ++q)
-      if (w.owner[q] == b) k = q;
+    for (int q = 0; q < kWorkerSets; ++q)
+      if (w.set[q].owner == b) k = q;
     if (k < 0) return DRB_EINVAL;
-    w.cv.wait(g, [&] { return w.issued[k]; });
-    if (w.err) return w.err;
+    w.cv.wait(g, [&] { return w.set[k].issued; });
   }
+  WorkerSet &s = w.set[k];
+  // (the copies that were issued finish before the set is released)
+  hipError_t r = hipSuccess;
   if (w.hsa)
     worker_wait_copies(w, k);
   else
-    HIPCHK(hipEventSynchronize(w.ev_drained[k]));
-  b->n_reads = w.hdr[4 * k];
-  b->n_values = w.hdr[4 * k + 1];
-  b->n_applied = w.hdr[4 * k + 2];
+    r = hipEventSynchronize(s.ev_drained);
   {
     std::lock_guard<std::mutex> g(w.mu);
-    w.owner[k] = nullptr;
+    const int err = s.err ? s.err : r != hipSuccess ? DRB_EDEVICE : 0;
+    if (err) {  // reported once; the buffer set and the staging are free
+      s.err = 0;
+      s.owner = nullptr;
+      return err;
+    }
+  }
+  b->n_reads = w.hdr[4 * k];
+  b->n_values = w.hdr[4 * k + 1];
+  b->n_deferred = w.hdr[4 * k + 2];
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    s.owner = nullptr;
   }
   return b->n_reads > b->reads_cap || b->n_values > b->values_cap ||
-                 b->n_applied > b->applied_cap
+                 b->n_deferred > b->deferred_cap
              ? DRB_ERANGE
              : DRB_OK;
 }

@@ -61,3 +61,57 @@ def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
+
+
+class RcclComm:
+    """An RCCL communicator over the process group's ranks for the C ABI's
+    exchange (drb_exchange_rccl*, include/drb_engine.h): what a Go NodeHost
+    per GPU would hold (cgo).  Rank 0's ncclUniqueId travels
+    over the torch.distributed group; ncclCommInitRank is collective.
+    abort() (ncclCommAbort) may be called from another thread to end
+    operations that hang."""
+
+    def __init__(self, world, rank):
+        import ctypes as C
+        import torch.distributed as dist
+
+        class UniqueId(C.Structure):
+            _fields_ = [("internal", C.c_char * 128)]  # NCCL_UNIQUE_ID_BYTES
+        lib = None
+        for name in ("librccl.so.1", "/opt/rocm/lib/librccl.so.1"):
+            try:
+                lib = C.CDLL(name)
+                break
+            except OSError:
+                pass
+        if lib is None:
+            raise RuntimeError("librccl not loadable")
+        lib.ncclGetUniqueId.argtypes = [C.POINTER(UniqueId)]
+        lib.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int,
+                                         UniqueId, C.c_int]
+        lib.ncclCommDestroy.argtypes = [C.c_void_p]
+        lib.ncclCommAbort.argtypes = [C.c_void_p]
+        uid = UniqueId()
+        if rank == 0 and lib.ncclGetUniqueId(C.byref(uid)) != 0:
+            raise RuntimeError("ncclGetUniqueId failed")
+        box = [C.string_at(C.addressof(uid), 128) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        C.memmove(C.addressof(uid), box[0], 128)
+        self.lib, self.comm = lib, C.c_void_p()
+        rc = lib.ncclCommInitRank(C.byref(self.comm), world, uid, rank)
+        if rc != 0:
+            raise RuntimeError("ncclCommInitRank failed: %d" % rc)
+
+    @property
+    def handle(self):
+        return self.comm.value
+
+    def abort(self):
+        if self.comm.value:
+            self.lib.ncclCommAbort(self.comm)
+            self.comm.value = None
+
+    def close(self):
+        if self.comm.value:
+            self.lib.ncclCommDestroy(self.comm)
+            self.comm.value = None

@@ -58,6 +58,7 @@ SIGNATURES = {
                                              PU64, C.POINTER(C.c_uint16),
                                              PU8, SZ]),
     "drb_stage_wait_upload": (C.c_int, [P]),
+    "drb_set_session_clients": (C.c_int, [P, PU64]),
     "drb_stage_packed_layout": (C.c_int, [P, U64, SZ, PU64, C.POINTER(SZ)]),
     "drb_gen_kv_proposals": (C.c_int, [P, U32, U32, U32, U32, U64, U64]),
     "drb_gen_kv_proposals_active": (C.c_int, [P, U32, U32, U32, U32, U64,
@@ -130,6 +131,9 @@ SIGNATURES = {
     "drb_exchange_plan": (C.c_int, [P, U32, C.POINTER(abi.Xfer), SZ,
                                     C.POINTER(SZ)]),
     "drb_exchange_rccl": (C.c_int, [P, P, U32]),
+    "drb_exchange_plan_words": (C.c_int, [P, PU32, C.POINTER(abi.Xfer), SZ,
+                                          C.POINTER(SZ)]),
+    "drb_exchange_rccl_counted": (C.c_int, [P, P]),
     "drb_exchange_rccl_roles": (C.c_int, [P, P, PU32]),
     "drb_exchange_bytes": (C.c_int, [P, C.POINTER(U64), C.c_int]),
     "drb_encode_wire": (C.c_int, [P, U32, U32, C.POINTER(WireCfg),
@@ -141,6 +145,8 @@ SIGNATURES = {
     "drb_ingest_buffer_alloc": (C.c_int, [P, SZ, C.POINTER(PU8)]),
     "drb_ingest_buffer_free": (C.c_int, [P, PU8]),
     "drb_worker_export": (C.c_int, [P, U32, C.POINTER(abi.WorkerBufs)]),
+    "drb_worker_export_part": (C.c_int, [P, U32, U32, U32,
+                                         C.POINTER(abi.WorkerBufs)]),
     "drb_worker_wait": (C.c_int, [P, C.POINTER(abi.WorkerBufs)]),
     "drb_host_alloc": (C.c_int, [P, SZ, C.POINTER(P)]),
     "drb_host_free": (C.c_int, [P, P]),
@@ -190,7 +196,7 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
                 tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0,
                 kv_overflow_buckets=0, forward_proposals=0,
-                nonvoting_slots=0, witness_slots=0)
+                nonvoting_slots=0, witness_slots=0, host_copies=0)
 
 
 class Engine:
@@ -214,7 +220,7 @@ class Engine:
                    cfg["tan_multiplexed"], cfg["pre_vote"],
                    cfg["max_reads_per_ctx"], cfg["kv_overflow_buckets"],
                    cfg["forward_proposals"], cfg["nonvoting_slots"],
-                   cfg["witness_slots"])
+                   cfg["witness_slots"], cfg["host_copies"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")
@@ -328,6 +334,20 @@ class Engine:
             "drb_stage_packed_layout")
         return list(off), nb.value
 
+    def set_session_clients(self, client_ids):
+        """drb_set_session_clients: the ClientID of the host's NoOP session
+        of every lane's group (a sequence of G ints or a u64 array)."""
+        if hasattr(client_ids, "ctypes"):  # a numpy array
+            import numpy as np
+            arr = np.ascontiguousarray(client_ids, dtype=np.uint64)
+            assert arr.size >= self.G
+            ptr = arr.ctypes.data_as(PU64)
+        else:
+            arr = (U64 * self.G)(*client_ids)
+            ptr = C.cast(arr, PU64)
+        _ck(lib().drb_set_session_clients(self.h, ptr),
+            "drb_set_session_clients")
+
     def stage_wait_upload(self):
         _ck(lib().drb_stage_wait_upload(self.h), "drb_stage_wait_upload")
 
@@ -358,6 +378,8 @@ class Engine:
         return busy.value
 
     def ingest(self, marr, n, earr, pool):
+        """drb_ingest: (accepted, dropped); raises DrbError (DRB_EDIVERTED)
+        when a message had to go to the CPU path -- use ingest_ex there."""
         acc, drop = U64(), U64()
         _ck(lib().drb_ingest(self.h, marr, n, earr, pool, C.byref(acc),
                              C.byref(drop)), "drb_ingest")
@@ -702,6 +724,26 @@ class Engine:
         return [(arr[i].peer, arr[i].recv, arr[i].ptr, arr[i].bytes)
                 for i in range(n.value)]
 
+    def exchange_plan_words(self, words):
+        """drb_exchange_plan_words: the transfer list from every rank's
+        plane words (a list of world rows of R * R words)."""
+        flat = [w for row in words for w in row]
+        arr = (U32 * max(1, len(flat)))(*flat)
+        n = SZ()
+        _ck(lib().drb_exchange_plan_words(self.h, arr, None, 0, C.byref(n)),
+            "drb_exchange_plan_words")
+        ops = (abi.Xfer * max(1, n.value))()
+        _ck(lib().drb_exchange_plan_words(self.h, arr, ops, n.value,
+                                          C.byref(n)),
+            "drb_exchange_plan_words")
+        return [(ops[i].peer, ops[i].recv, ops[i].ptr, ops[i].bytes)
+                for i in range(n.value)]
+
+    def exchange_rccl_counted(self, comm):
+        """drb_exchange_rccl_counted over an ncclComm_t (an address)."""
+        _ck(lib().drb_exchange_rccl_counted(self.h, comm),
+            "drb_exchange_rccl_counted")
+
     def exchange_rccl(self, comm, leader_mask):
         """drb_exchange_rccl over an ncclComm_t (an address)."""
         _ck(lib().drb_exchange_rccl(self.h, comm, leader_mask),
@@ -806,16 +848,18 @@ class Engine:
         return {f: getattr(res, f) for f, _ in WireIn._fields_}
 
     # ---------------------------------------------------------- step worker
-    def worker_bufs(self, reads_cap, values_cap, applied_cap):
+    def worker_bufs(self, reads_cap, values_cap, deferred_cap, lanes=None):
         """A drb_worker_bufs over fresh pinned host buffers (drb_host_alloc);
-        free them with free_worker_bufs."""
+        free them with free_worker_bufs.  lanes: the lanes word capacity
+        (default: every lane)."""
         b = abi.WorkerBufs()
+        nl = self.G if lanes is None else lanes
         for name, typ, n, cap in (
-                ("lanes", C.c_uint32, self.G, self.G),
-                ("reads", abi.WorkerRead, reads_cap, reads_cap),
+                ("lanes", C.c_uint32, nl, nl),
+                ("reads", C.c_uint32, reads_cap, reads_cap),
                 ("values", C.c_uint32, values_cap, values_cap),
-                ("value_meta", C.c_uint8, (values_cap + 1) // 2, None),
-                ("applied", C.c_uint32, applied_cap, applied_cap)):
+                ("value_meta", C.c_uint8, (values_cap + 3) // 4, None),
+                ("deferred", C.c_uint64, deferred_cap, deferred_cap)):
             p = P()
             _ck(lib().drb_host_alloc(self.h, max(1, n) * C.sizeof(typ),
                                      C.byref(p)), "drb_host_alloc")
@@ -825,21 +869,27 @@ class Engine:
         return b
 
     def free_worker_bufs(self, b):
-        for name in ("lanes", "reads", "values", "value_meta", "applied"):
+        for name in ("lanes", "reads", "values", "value_meta", "deferred"):
             _ck(lib().drb_host_free(self.h, C.cast(getattr(b, name), P)),
                 "drb_host_free")
 
-    def worker_export(self, slot, b):
-        """drb_worker_export: enqueue the last round's outputs of replica
-        slot `slot` into b (returns at once)."""
-        _ck(lib().drb_worker_export(self.h, slot, C.byref(b)),
-            "drb_worker_export")
+    def worker_export(self, slot, b, n_parts=1, part=0):
+        """drb_worker_export(_part): enqueue the last round's outputs of
+        replica slot `slot` (of one step worker's partition of the shards)
+        into b (returns at once)."""
+        if n_parts == 1:
+            _ck(lib().drb_worker_export(self.h, slot, C.byref(b)),
+                "drb_worker_export")
+        else:
+            _ck(lib().drb_worker_export_part(self.h, slot, n_parts, part,
+                                             C.byref(b)),
+                "drb_worker_export_part")
 
     def worker_wait(self, b):
-        """drb_worker_wait: (n_reads, n_values, n_applied); raises when a
+        """drb_worker_wait: (n_reads, n_values, n_deferred); raises when a
         count exceeded its buffer."""
         _ck(lib().drb_worker_wait(self.h, C.byref(b)), "drb_worker_wait")
-        return b.n_reads, b.n_values, b.n_applied
+        return b.n_reads, b.n_values, b.n_deferred
 
     def crc32_batch(self, buffers):
         data = b"".join(buffers)

@@ -66,6 +66,8 @@ extern "C" {
 #define DRB_ERANGE (-5)
 #define DRB_EAGAIN (-6)  /* retry later: the call would race a step in
                           * flight (drb_ingest before drb_exchange_*) */
+#define DRB_EDIVERTED (-7) /* drb_ingest: messages were diverted to the CPU
+                            * path; only drb_ingest_ex says which */
 
 /* raftpb.MessageType (raftpb/types.go:8-37) */
 enum drb_message_type {
@@ -414,6 +416,13 @@ typedef struct drb_config {
    * their roles; the leader slot must be a voting member. */
   uint32_t nonvoting_slots;
   uint32_t witness_slots;
+  /* 1: the engine's large host transfers -- the step worker's download
+   * (drb_worker_export) and a pinned one-block proposal upload
+   * (drb_stage_proposals_packed*) -- go through hipMemcpyAsync on the
+   * engine's copy streams instead of its own SDMA engines (drb_hsa.hpp):
+   * the path every engine takes when the HSA copy engines are unavailable,
+   * selectable so that it can be tested.  0: SDMA when available. */
+  uint32_t host_copies;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */
@@ -553,7 +562,9 @@ int drb_stage_proposals(drb_engine *e, uint32_t slot, const uint32_t *counts,
  * -- group by group, in queue order -- its Key, ClientID and Cmd length,
  * the Cmd bytes back to back in pool (pool_len = the sum of the lengths).
  * 1 + n x 18 + pool bytes cross the host link instead of drb_entry rows:
- * 36 B per group at C3 (16 B PBKV writes) against 85 B.  Offsets are
+ * 36 B per group at C3 (16 B PBKV writes) against 85 B; client_ids NULL
+ * takes each group's registered session client (drb_set_session_clients,
+ * DRB_EINVAL without one), 28 B per C3 group.  Offsets are
  * scanned and the entries laid out on the device, ordered and overlapped
  * as drb_stage_proposals; DRB_EINVAL when the counts or lengths do not add
  * up. */
@@ -575,6 +586,13 @@ int drb_stage_proposals_packed_async(drb_engine *e, uint32_t slot,
                                      const uint64_t *client_ids,
                                      const uint16_t *cmd_lens,
                                      const uint8_t *pool, size_t pool_len);
+/* The ClientID of the host's NoOP session of every group (client.go
+ * NewNoOPSession: one per shard, request.go:1085-1096), client_ids[g] for
+ * lane g.  A packed batch may then leave client_ids NULL -- each entry
+ * carries its group's -- and 8 B per entry stay off the host link; the
+ * step-worker export counts a lane's applied entries of that client
+ * (drb_worker_bufs).  Synchronous; set again to change them. */
+int drb_set_session_clients(drb_engine *e, const uint64_t *client_ids);
 /* Until the last staged upload is done (its host arrays free). */
 int drb_stage_wait_upload(drb_engine *e);
 /* Where a host builds a packed batch of n_entries entries and pool_len Cmd
@@ -582,8 +600,10 @@ int drb_stage_wait_upload(drb_engine *e);
  * 8 MB and more, on the engine's own upload SDMA engine -- the one its
  * step-worker downloads do not use -- with the call returning once it is
  * up):
- * counts at offset 0, then keys, client ids, lengths and the pool at
- * offsets[0..3] (256-aligned); *bytes = the block's length.  Arrays
+ * counts at offset 0, then keys, lengths, the pool and the client ids
+ * (256-aligned); offsets[0..3] = keys, client ids, lengths, pool; *bytes =
+ * the block's length.  A batch without client ids (drb_set_session_clients)
+ * ends at offsets[3] + pool_len, and only that much goes up.  Arrays
  * elsewhere are uploaded one copy each. */
 int drb_stage_packed_layout(const drb_engine *e, uint64_t n_entries,
                             size_t pool_len, uint64_t *offsets,
@@ -664,7 +684,13 @@ int drb_request_leader_transfer(drb_engine *e, uint32_t slot,
  * lane group / N); a sender slot that belongs to another rank is written
  * into the inbound planes, its Replicates' entries into the plane's
  * entry_mbox rows.  Call it after the round's plane exchange.  The same
- * holds for drb_ingest_wire. */
+ * holds for drb_ingest_wire, with one difference of scope: its placement
+ * runs one lane per (group, sender, receiver) plane, so a capacity divert
+ * diverts that plane's later messages in the call, while other senders'
+ * planes to the same receiver keep placing theirs (the receiver is flagged
+ * either way, and its CPU inbox -- drb_export_inbox(.., 0, ..) then the
+ * diverted messages per sender in stream order -- keeps every sender's
+ * order, which is all MessageQueue order promises across senders). */
 enum drb_ingest_fate {
   DRB_ING_PLACED = 0,
   DRB_ING_DROPPED = 1,
@@ -675,7 +701,13 @@ enum drb_ingest_fate {
 int drb_ingest_ex(drb_engine *e, const drb_message *msgs, size_t n,
                   const drb_entry *ents, const uint8_t *pool, uint8_t *status,
                   uint64_t *accepted, uint64_t *dropped, uint64_t *diverted);
-/* drb_ingest_ex without the per-message status and the diverted count */
+/* drb_ingest_ex without the per-message status and the diverted count.
+ * Deprecated: a caller that cannot see which messages were diverted would
+ * lose them, so when any was (a GPU capacity, or a receiver already off the
+ * fast path) it returns DRB_EDIVERTED -- the placed ones are in the inbox,
+ * the counts are set, and the caller must replay the call's messages for
+ * the flagged receivers (drb_take_flagged) through the CPU path or use
+ * drb_ingest_ex. */
 int drb_ingest(drb_engine *e, const drb_message *msgs, size_t n,
                const drb_entry *ents, const uint8_t *pool, uint64_t *accepted,
                uint64_t *dropped);
@@ -788,57 +820,76 @@ int drb_export_ready_to_reads_batch(drb_engine *e, uint32_t slot,
  * export's bytes are in its buffers and fills the counts.
  *
  * The records carry only what the host cannot rebuild from what it staged
- * (about 64 B per C3 group-round):
- *   lanes[g]   one word per lane (every lane of the engine, g < num_groups):
- *              bits 0-3 its ReadyToReads this round, bits 4-11 which of
- *              them had their reads served (bit k: the k-th; its
- *              reads_per_ctx results follow in values), bits 12-27 its
- *              applied entries;
- *   reads      per ReadyToRead, lanes in order, each lane's in release
- *              order: its Index and SystemCtx.Low (the host issued the ctx:
- *              Low is its random part, High its own tick + 30,
- *              request.go:864-875);
- *   values     per served read, in ReadyToRead and read order: the value's
- *              first 4 bytes, little endian;
- *   value_meta a nibble per served read (read i: byte i / 2, low nibble
- *              for even i): bit 3 found, bits 0-2 the value's length, or 5
- *              when it is longer than 4 bytes (drb_export_read_values has
- *              it whole);
- *   applied    per applied entry, lanes in order, each lane's in index
- *              order: KVTest's sm.Result.Value (kvtest.go:161) in bits
- *              0-30, bit 31 set for an empty no-op entry the rsm ignores
- *              (statemachine.go:939).  The entries are the host's own
- *              proposals in the order it staged them (Key, ClientID and
- *              SeriesID are the host's: node.go:243-257 matches on them).
+ * and what it issued (about 46 B per C3 group-round):
+ *   lanes[g]    one word per lane (every lane of the engine, g < num_groups):
+ *               bits 0-3 its ReadyToReads this round, bits 4-11 which of
+ *               them had their reads served (bit k: the k-th; its
+ *               reads_per_ctx results follow in values), bits 12-27 how
+ *               many of the host's own proposals it applied -- the entries
+ *               carrying the group's session ClientID
+ *               (drb_set_session_clients), or, with none registered, every
+ *               entry with a ClientID (raft's own empty entries have none,
+ *               statemachine.go:939).  They complete the host's pending
+ *               proposals in the order it staged them; KVTest's
+ *               sm.Result.Value is the length of each one's payload
+ *               (kvtest.go:161), known to the host (drb_apply_results has
+ *               the per-entry form);
+ *   reads       per ReadyToRead, lanes in order, each lane's in release
+ *               order: the low 32 bits of its SystemCtx.Low.  The host
+ *               issued the ctx (request.go:864-875: Low random, High its
+ *               own tick + 30) and a replica releases its requests in the
+ *               order they were queued (readindex.go:77-115), so the tag
+ *               picks the ctx out of the group's pending ones; a pending
+ *               ctx older than a released one was dropped (a host keeps the
+ *               low words of a group's pending ctxs distinct);
+ *   values      per served read, in ReadyToRead and read order: a word whose
+ *               meaning its 2-bit code gives;
+ *   value_meta  a 2-bit code per served read (read i: byte i / 4, bits
+ *               2 * (i % 4)): DRB_WORKER_MISS the key is not in the KV
+ *               (word 0); DRB_WORKER_V4 a 4-byte value, the word; 
+ *               DRB_WORKER_SHORT a shorter one, its bytes in the word's low
+ *               bytes and its length in bits 24-31; DRB_WORKER_LONG a
+ *               longer one, its first 4 bytes (drb_export_read_values has
+ *               it whole);
+ *   deferred    per ReadyToRead whose reads were not served (reads_per_ctx
+ *               0, or its index not yet applied), lanes in order: its
+ *               Index, for pendingReadIndex.applied (request.go:930-953).
  */
-typedef struct drb_worker_read {  /* one ReadyToRead, 16 B */
-  uint64_t index;
-  uint64_t ctx_low;
-} drb_worker_read;
-
 #define DRB_WORKER_LANE_READS(w) ((w) & 0xfu)
 #define DRB_WORKER_LANE_SERVED(w) (((w) >> 4) & 0xffu)
 #define DRB_WORKER_LANE_APPLIED(w) (((w) >> 12) & 0xffffu)
-#define DRB_WORKER_FOUND 8u
-#define DRB_WORKER_LONG 5u
-#define DRB_WORKER_IGNORED 0x80000000u
+#define DRB_WORKER_MISS 0u
+#define DRB_WORKER_V4 1u
+#define DRB_WORKER_SHORT 2u
+#define DRB_WORKER_LONG 3u
 
 typedef struct drb_worker_bufs {
   uint32_t *lanes;             /* host buffers from drb_host_alloc */
   uint64_t lanes_cap;          /* >= num_groups */
-  drb_worker_read *reads;
+  uint32_t *reads;
   uint64_t reads_cap;
   uint32_t *values;
-  uint8_t *value_meta;         /* (values_cap + 1) / 2 bytes */
+  uint8_t *value_meta;         /* (values_cap + 3) / 4 bytes */
   uint64_t values_cap;
-  uint32_t *applied;
-  uint64_t applied_cap;
-  uint64_t n_reads, n_values, n_applied;  /* set by drb_worker_wait */
+  uint64_t *deferred;
+  uint64_t deferred_cap;
+  uint64_t n_reads, n_values, n_deferred;  /* set by drb_worker_wait */
 } drb_worker_bufs;
 
 /* DRB_EAGAIN: b already has an export in flight (drb_worker_wait it
- * first); two drb_worker_bufs alternate in a step worker's loop */
+ * first), or 16 exports are in flight; two drb_worker_bufs alternate in a
+ * step worker's loop */
 int drb_worker_export(drb_engine *e, uint32_t slot, const drb_worker_bufs *b);
+/* The same for one step worker's partition of the shards: the lanes whose
+ * ShardID % n_parts == part (engine.go:1036-1049 processSteps over
+ * workerID's shards; FixedPartitioner, internal/server/partition.go:28-41),
+ * i.e. lanes g0, g0 + n_parts, ... with g0 = (part - first_shard_id) mod
+ * n_parts; lanes[i] is lane g0 + i * n_parts's word (lanes_cap >= that
+ * partition's lane count) and the other records follow those lanes only.
+ * Each worker exports into its own buffer sets, concurrently with the
+ * others.  Co-resident placement only (n_parts 1 is drb_worker_export). */
+int drb_worker_export_part(drb_engine *e, uint32_t slot, uint32_t n_parts,
+                           uint32_t part, const drb_worker_bufs *b);
 /* DRB_ERANGE when a count exceeded its cap (the counts are the full ones,
  * the buffers hold the first cap records) */
 int drb_worker_wait(drb_engine *e, drb_worker_bufs *b);
@@ -1095,6 +1146,21 @@ int drb_exchange_plan(drb_engine *e, uint32_t leader_mask, drb_xfer *xfers,
  * Replaces Transport.Send -> handleRequest (transport.go:346, :305) for
  * GPU-resident replicas, with no Python in the host process. */
 int drb_exchange_rccl(drb_engine *e, void *comm, uint32_t leader_mask);
+/* The transfer list of an exchange step from every rank's plane words:
+ * words[q * R * R + from * R + to] is rank q's summary word of plane
+ * (from, to) -- drb_plane_counts' on each rank for the counted step, the
+ * full-capacity row for the fixed one (drb_exchange_plan) -- this rank
+ * sending each plane at its own word and receiving it at its sender's, in
+ * the same order on every rank (dragonboat_amd/exchange.py plan()). */
+int drb_exchange_plan_words(drb_engine *e, const uint32_t *words,
+                            drb_xfer *xfers, size_t cap, size_t *n_xfers);
+/* The counted step over RCCL: drb_plane_counts (a synchronisation of the
+ * engine stream), an ncclAllGather of every rank's words, then the planes
+ * at those sizes as ncclSend / ncclRecv in one group on the engine stream
+ * and drb_exchange_mark.  At C4's steady state about half the fixed step's
+ * bytes, for one host round trip per round.
+ * Collective: every rank calls it after the same round. */
+int drb_exchange_rccl_counted(drb_engine *e, void *comm);
 /* leader_mask for drb_exchange_rccl / drb_exchange_plan: the OR over comm's
  * ranks of each engine's leader slots (an ncclAllReduce; synchronises the
  * engine stream).  Collective: every rank calls it after its imports. */

@@ -66,7 +66,6 @@ STRUCTS = {
     "drb_tan_record": abi.TanRecord,
     "drb_tan_state": abi.TanState,
     "drb_tan_log": abi.TanLog,
-    "drb_worker_read": abi.WorkerRead,
     "drb_wire_cpu": abi.WireCpu,
     "drb_worker_bufs": abi.WorkerBufs,
     "drb_region": abi.Region,
@@ -147,6 +146,7 @@ def test_engine_without_gpu_fails_loudly():
     dict(num_groups=64, num_replicas=3, forward_proposals=1, max_props=16),
     dict(num_groups=64, num_replicas=3, forward_proposals=1, place_world=2,
          place_rank=0, entry_mbox=4),
+    dict(num_groups=64, num_replicas=3, host_copies=2),  # a 0/1 switch
 ])
 def test_create_rejects_invalid_config(kw):
     """drb_engine_create validates the configuration before it touches a

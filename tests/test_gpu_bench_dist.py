@@ -33,7 +33,11 @@ def _bench(*extra, env=None):
 
 @pytest.mark.gpu
 def test_bench_gpus_2_launches_two_ranks():
-    p = _bench("--gpus", "2", "--dist-backend", "gloo")
+    """... and, after the timed run, C4 across the two ranks through the C
+    ABI's exchange lists (c4_cross: over RCCL on a node, here the gloo
+    rehearsal through host memory), both the counted and the fixed step."""
+    p = _bench("--gpus", "2", "--dist-backend", "gloo", "--c4-groups",
+               str(G))
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
@@ -48,6 +52,17 @@ def test_bench_gpus_2_launches_two_ranks():
     assert abs(res["value"] * res["ms_per_step"] * K / 1e3 - total) <= \
         1e-6 * total + 1
     assert c["fast_path_only"], c
+    x = res["c4_cross"]
+    assert "error" not in x, x
+    assert x["world"] == 2 and x["groups"] == G
+    for mode in ("counted", "fixed"):
+        m = x[mode]
+        assert m["committed_per_round"] == G, (mode, m)
+        assert m["fallbacks_and_errors"] == 0, (mode, m)
+        assert m["xchg_bytes_per_round_per_rank"] > 0, (mode, m)
+    # the counted step ships what the round sent, the fixed one every slot
+    assert x["counted"]["xchg_bytes_per_round_per_rank"] < \
+        x["fixed"]["xchg_bytes_per_round_per_rank"]
 
 
 def test_bench_rejects_gpus_unlike_world_size():

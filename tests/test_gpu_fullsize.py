@@ -373,3 +373,125 @@ def test_fullsize_c5_tan_sampled():
                 assert eng.tan_get(g, s)[0] == want["offset"], where
                 checked += 1
     assert checked > 0
+
+
+def _compare_spread(engs, orc, gids, R, N):
+    """_compare for C4's placement: replica slot s of global group g lives on
+    rank (g + s) mod N at lane g // N."""
+    errs = []
+    for i, g in enumerate(gids):
+        for s in range(R):
+            e, j = engs[(g + s) % N], g // N
+            a, b = e.export_replicas(j, 1)[s], orc.export(i, s)
+            d = state_diff(a, b, R)
+            if a.shard_id != b.shard_id or a.flags != b.flags:
+                d["ids"] = ((a.shard_id, a.flags), (b.shard_id, b.flags))
+            if d:
+                errs.append((g, s, "state", d))
+                continue
+            lo = max(1, b.last_index - 6)
+            if e.export_log(j, s, lo, b.last_index) != \
+                    orc.export_log(i, s, lo, b.last_index):
+                errs.append((g, s, "log"))
+            if e.kv_export(j, s) != orc.export_kv(i, s):
+                errs.append((g, s, "kv"))
+            if by_dest(e.export_outbox(j, s)) != \
+                    by_dest(orc.export_outbox(i, s)):
+                errs.append((g, s, "msgs"))
+        if len(errs) > 4:
+            break
+    return errs
+
+
+def _exchange_by_plan(engs, mask, counted=False):
+    """drb_exchange_plan's transfers of every rank (counted: drb_exchange_
+    plan_words over every rank's drb_plane_counts, the step of
+    drb_exchange_rccl_counted), each send copied into its paired receive
+    (what RCCL's send / recv do between GPUs)."""
+    import torch
+    from dragonboat_amd import exchange as X
+    dev = torch.device("cuda", 0)
+    for e in engs:
+        e.sync()
+    if counted:
+        words = [e.plane_counts() for e in engs]
+        plans = [e.exchange_plan_words(words) for e in engs]
+    else:
+        plans = [e.exchange_plan(mask) for e in engs]
+    moved = 0
+    for r, pr in enumerate(plans):
+        for q, pq in enumerate(plans):
+            if q == r:
+                continue
+            sends = [(p, n) for peer, rv, p, n in pr if peer == q and not rv]
+            recvs = [(p, n) for peer, rv, p, n in pq if peer == r and rv]
+            assert [n for _, n in sends] == [n for _, n in recvs], (r, q)
+            for (sp, n), (dp, _) in zip(sends, recvs):
+                X.device_bytes(dp, n, dev).copy_(X.device_bytes(sp, n, dev))
+                moved += n
+    torch.cuda.synchronize()
+    for e in engs:
+        e.exchange_mark()
+    return moved
+
+
+@pytest.mark.parametrize("mode", ["local", "plan", "counted"])
+def test_fullsize_c4_spread_sampled(mode):
+    """C4 at its configured size and placement: 1,048,576 groups x 5
+    replicas over 8 ranks -- replica slot s of group g on rank (g + s) mod
+    8 at lane g // 8 -- as 8 engines of one process on the one GPU, with
+    bench.py's C4 engine arguments (mailbox 8, entry_mbox k + 2, the device
+    input generators).  After every round the planes move either by
+    drb_exchange_local (the device pull), by drb_exchange_plan's transfer
+    list (the fixed-capacity step of drb_exchange_rccl) or by
+    drb_exchange_plan_words over every rank's counts (the counted step of
+    drb_exchange_rccl_counted), each send copied into its paired receive as
+    RCCL would.  ~1000 sampled groups match one oracle cluster every few
+    rounds: every replica field, log, KV and outbox.  The counted step ships
+    at most 230 MB per rank per round (the fixed one 419 MB)."""
+    G, R, N, NP, k = 1 << 20, 5, 8, 8, 1
+    lanes = G // N
+    engs = [Engine(num_groups=lanes, num_replicas=R, window=32, cmd_cap=32,
+                   max_props=k, prop_slots=NP, ri_slots=NP, mailbox=8,
+                   kv_slots=512, kv_val_cap=4, total_groups=G,
+                   place_world=N, place_rank=r, entry_mbox=k + 2)
+            for r in range(N)]
+    try:
+        for e in engs:
+            e.init_steady(term=2, leader_slot=0, seed=SEED)
+        mask = 0
+        for e in engs:
+            mask |= e.role_slots()[0]
+        gids = _sample(G, 1000)
+        n = len(gids)
+        orc = po.Cluster(n, R, seed=SEED, gids=gids)
+        orc.setup_steady(0)
+        moved = 0
+        for r in range(16):
+            b, salt = r % NP, (1 << 22) + r
+            counts, ents, pool = workload.build_batch(n, k, SEED, salt,
+                                                      gids=gids)
+            orc.stage_proposals(counts, k, ents, pool)
+            for e in engs:
+                e.gen_kv_proposals(b, k, 256, 4, SEED, salt)
+            tick = r % 3 != 2
+            orc.round(tick=tick)
+            outs = [e.step(tick=tick, prop_slot=b) for e in engs]
+            assert sum(o.fallbacks + o.errors for o in outs) == 0, \
+                (r, [o.to_dict() for o in outs if o.fallbacks or o.errors])
+            if r >= 3:
+                assert sum(o.committed_entries for o in outs) == G, r
+            if mode == "local":
+                Engine.exchange_local(engs)
+            else:
+                m = _exchange_by_plan(engs, mask, counted=mode == "counted")
+                if mode == "counted" and r >= 3:
+                    assert m / N <= 230e6, (r, m / N)
+                moved += m
+            if r % 5 == 4 or r == 15:
+                errs = _compare_spread(engs, orc, gids, R, N)
+                assert not errs, (r, errs[:3])
+        assert mode == "local" or moved > 0
+    finally:
+        for e in engs:
+            e.close()

@@ -240,3 +240,33 @@ def test_stepped_down_leader_forwards_its_queue():
     for g in E:
         roles = [x.role for x in p.eng.export_replicas(g, 1)]
         assert roles[0] == abi.FOLLOWER and roles.count(abi.LEADER) == 1
+
+
+def test_legacy_ingest_reports_diversion():
+    """drb_ingest has no per-message fates, so a call that had to divert a
+    message to the CPU path must say so: DRB_EDIVERTED, with the
+    placed messages in the inbox and the counts set; Engine.ingest raises.
+    The engine's state is the one drb_ingest_ex leaves (the receiver
+    flagged CAPACITY)."""
+    import ctypes as C
+    from dragonboat_amd.engine import lib, DrbError
+    G, R = 8, 3
+    p = Pair(G=G, R=R, forward_proposals=1, max_props=3, mailbox=16,
+             kv_val_cap=64, cmd_cap=96)
+    for _ in range(2):
+        _round(p, k=1, tick=True)
+    _unhost(p, range(G), 2)
+    _round(p, k=1, tick=True)
+    two = [po.msg(MSG["Propose"], from_=3, to=1, shard_id=1,
+                  entries=[po.ent(key=5 + j)]) for j in range(2)]
+    acc, drop = C.c_uint64(), C.c_uint64()
+    marr, n, earr, pool = po.build_messages(two)
+    rc = lib().drb_ingest(p.eng.h, marr, n, earr, pool, C.byref(acc),
+                          C.byref(drop))
+    assert rc == abi.DRB_EDIVERTED and (acc.value, drop.value) == (1, 0)
+    recs, _ = p.eng.take_flagged()
+    assert {(g, s, reason) for (g, s, reason, *_x) in recs} == \
+        {(0, 0, abi.FB["CAPACITY"])}
+    # the receiver is off the fast path now: everything for it diverts
+    with pytest.raises(DrbError, match="status -7"):
+        p.eng.ingest(*po.build_messages(two[:1]))

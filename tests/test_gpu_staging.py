@@ -46,21 +46,24 @@ def _one_block(eng, arrs, pinned=False):
     C.memmove(base, cnt, C.sizeof(cnt))
     for o, a, sz in ((off[0], keys, 8 * n), (off[1], cids, 8 * n),
                      (off[2], lens, 2 * n), (off[3], pb, plen)):
-        C.memmove(base + o, a, sz)
+        if a is not None:  # (no client ids: the session clients')
+            C.memmove(base + o, a, sz)
 
     def at(o, t):
         return C.cast(base + o, C.POINTER(t))
     return blk, (at(0, C.c_uint8), n, at(off[0], C.c_uint64),
-                 at(off[1], C.c_uint64), at(off[2], C.c_uint16),
-                 at(off[3], C.c_uint8), plen)
+                 None if cids is None else at(off[1], C.c_uint64),
+                 at(off[2], C.c_uint16), at(off[3], C.c_uint8), plen)
 
 
 def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4,
-                  slot=0, pipelined=False, one_block=False):
+                  slot=0, pipelined=False, one_block=False, sess=False):
     counts, ents, pool = workload.build_batch(p.G, k, p.seed, salt,
                                               key_space, val_len, groups)
     p.orc.stage_proposals(counts, k, ents, pool)
     arrs = workload.pack_batch(p.G, k, counts, ents, pool)
+    if sess:  # each group's entries carry its registered session client
+        arrs = arrs[:3] + (None,) + arrs[4:]
     if one_block:  # (the block stays alive with p until the next batch)
         p._keep, arrs = _one_block(p.eng, arrs, one_block == "pinned")
     if pipelined:
@@ -72,21 +75,34 @@ def _stage_packed(p, k, salt, groups=None, key_space=256, val_len=4,
     return arrs
 
 
-@pytest.mark.parametrize("k,val_len,pipelined,one_block",
-                         [(1, 4, False, False), (3, 4, False, False),
-                          (2, 16, False, False), (1, 4, True, False),
-                          (3, 16, True, False), (2, 4, False, "pageable"),
-                          (3, 16, True, "pageable"), (2, 4, False, "pinned"),
-                          (3, 16, True, "pinned")])
-def test_packed_staging_matches_oracle(k, val_len, pipelined, one_block):
+@pytest.mark.parametrize("k,val_len,pipelined,one_block,sess",
+                         [(1, 4, False, False, False),
+                          (3, 4, False, False, False),
+                          (2, 16, False, False, False),
+                          (1, 4, True, False, False),
+                          (3, 16, True, False, False),
+                          (2, 4, False, "pageable", False),
+                          (3, 16, True, "pageable", False),
+                          (2, 4, False, "pinned", False),
+                          (3, 16, True, "pinned", False),
+                          # client ids left out: drb_set_session_clients
+                          (1, 4, False, False, True),
+                          (3, 16, True, "pageable", True),
+                          (2, 4, True, "pinned", True)])
+def test_packed_staging_matches_oracle(k, val_len, pipelined, one_block,
+                                       sess):
     G = 96
     p = Pair(G=G, R=3, max_props=4, cmd_cap=32, kv_val_cap=16, prop_slots=2)
+    if sess:  # (workload.proposal: one NoOP session per group)
+        p.eng.set_session_clients([workload.client_id(p.seed, g)
+                                   for g in range(G)])
     held = None
     for rnd in range(10):
         groups = None if rnd % 3 else [g for g in range(G) if g % 4]
         cur = _stage_packed(p, k, rnd, groups, val_len=val_len,
                             slot=rnd % 2 if pipelined else 0,
-                            pipelined=pipelined, one_block=one_block)
+                            pipelined=pipelined, one_block=one_block,
+                            sess=sess)
         cur = (cur, getattr(p, "_keep", None))
         held = (held, cur)[1]  # the previous call's arrays are free now
         o = p.orc.round(tick=rnd % 2 == 0)
@@ -103,6 +119,12 @@ def test_packed_staging_matches_oracle(k, val_len, pipelined, one_block):
 
 def test_packed_staging_rejects_bad_sums():
     p = Pair(G=8, R=3)
+    cnt0 = (C.c_uint8 * 8)(*([1] * 8))
+    keys0 = (C.c_uint64 * 8)(*range(1, 9))
+    lens0 = (C.c_uint16 * 8)(*([4] * 8))
+    with pytest.raises(DrbError):  # no client ids, no session clients
+        p.eng.stage_proposals_packed(0, abi.ENTRY_ENCODED, cnt0, 8, keys0,
+                                     None, lens0, (C.c_uint8 * 32)(), 32)
     cnt = (C.c_uint8 * 8)(*([1] * 8))
     keys = (C.c_uint64 * 8)(*range(1, 9))
     lens = (C.c_uint16 * 8)(*([4] * 8))
@@ -133,9 +155,11 @@ def test_sdma_upload_lays_out_the_same_batch():
     arrs = [x.view("u1") for x in workload.build_packed_np(G, seed, 7)]
     n, plen = arrs[1].size // 8, arrs[4].size
     engs, keep = [], []
-    for pinned in (True, False):
+    # (pinned on SDMA, pageable, pinned with host_copies: hipMemcpyAsync,
+    # the path without the HSA copy engines)
+    for pinned, hc in ((True, 0), (False, 0), (True, 1)):
         e = Engine(num_groups=G, num_replicas=R, window=32, cmd_cap=32,
-                   max_props=1, prop_slots=2)
+                   max_props=1, prop_slots=2, host_copies=hc)
         e.init_steady(term=2, leader_slot=0, seed=seed)
         off, nbytes = e.stage_packed_layout(n, plen)
         assert nbytes >= 8 << 20
@@ -161,12 +185,13 @@ def test_sdma_upload_lays_out_the_same_batch():
             committed += out.committed_entries
         engs.append((e, committed))
         keep.append(blk)
-    (a, ca), (b, cb) = engs
-    assert ca == cb and ca > 0
-    for g0 in range(0, G, 8191):
-        sa, sb = a.export_replicas(g0, 1), b.export_replicas(g0, 1)
-        for s in range(R):
-            assert not state_diff(sa[s], sb[s], R), (g0, s)
-            li = sa[s].last_index
-            assert a.export_log(g0, s, max(1, li - 2), li) == \
-                b.export_log(g0, s, max(1, li - 2), li), (g0, s)
+    (a, ca) = engs[0]
+    for (b, cb) in engs[1:]:
+        assert ca == cb and ca > 0
+        for g0 in range(0, G, 8191):
+            sa, sb = a.export_replicas(g0, 1), b.export_replicas(g0, 1)
+            for s in range(R):
+                assert not state_diff(sa[s], sb[s], R), (g0, s)
+                li = sa[s].last_index
+                assert a.export_log(g0, s, max(1, li - 2), li) == \
+                    b.export_log(g0, s, max(1, li - 2), li), (g0, s)

@@ -43,12 +43,21 @@ def _python_plan(e, world, rank, mask):
             X.plan(R, world, rank, words, e.plane_regions)]
 
 
-def _exchange_by_plan(p, mask):
-    """Every rank's sends copied into the paired receives (one GPU)."""
+def _exchange_by_plan(p, mask, counted=False):
+    """Every rank's sends copied into the paired receives (one GPU); counted:
+    the lists drb_exchange_plan_words makes of every rank's plane counts."""
     dev = torch.device("cuda", 0)
     for e in p.engs:
         e.sync()
-    plans = [e.exchange_plan(mask) for e in p.engs]
+    if counted:
+        words = [e.plane_counts() for e in p.engs]
+        plans = [e.exchange_plan_words(words) for e in p.engs]
+        for r, e in enumerate(p.engs):  # the same list exchange.py builds
+            assert plans[r] == [
+                (peer, int(op == "recv"), ptr, n) for op, peer, (ptr, n) in
+                X.plan(e.R, p.N, r, words, e.plane_regions)], r
+    else:
+        plans = [e.exchange_plan(mask) for e in p.engs]
     moved = 0
     for r, pr in enumerate(plans):
         for q, pq in enumerate(plans):
@@ -81,8 +90,10 @@ def test_plan_matches_exchange_py_and_pairs_up(N, R):
     assert not errs, errs[:2]
 
 
-@pytest.mark.parametrize("N,R", [(2, 3), (3, 5)])
-def test_rounds_through_the_plan_stay_bit_exact(N, R):
+@pytest.mark.parametrize("N,R,counted", [(2, 3, False), (3, 5, False),
+                                         (2, 3, True), (3, 5, True),
+                                         (8, 5, True)])
+def test_rounds_through_the_plan_stay_bit_exact(N, R, counted):
     G = 10 * N + 1  # ragged: the last rank holds fewer lanes
     p = DistPair(G=G, R=R, N=N, E=4, max_props=2)
     mask = _leader_mask(p)
@@ -91,7 +102,7 @@ def test_rounds_through_the_plan_stay_bit_exact(N, R):
                          read_index=rnd % 3 == 1, exchange=False)
         assert tot["fallbacks"] == 0 and tot["errors"] == 0, (rnd, tot)
         assert tot["committed_entries"] == o.committed_entries, rnd
-        assert _exchange_by_plan(p, mask) > 0
+        assert _exchange_by_plan(p, mask, counted) > 0
         errs = p.check()
         assert not errs, (rnd, errs[:2])
 
@@ -119,6 +130,8 @@ def test_rccl_entry_points_on_a_one_rank_communicator():
         e.step(tick=True)
         e.exchange_rccl(comm.value, 1 << 1)  # one rank: nothing moves
         e.step(tick=True)
+        e.exchange_rccl_counted(comm.value)
+        e.step(tick=True)
         assert e.read_counters().errors == 0
         # a placement of two ranks does not match a one-rank communicator
         e2 = Engine(num_groups=32, num_replicas=3, total_groups=64,
@@ -127,6 +140,8 @@ def test_rccl_entry_points_on_a_one_rank_communicator():
         e2.step(tick=True)
         with pytest.raises(DrbError):
             e2.exchange_rccl(comm.value, 1)
+        with pytest.raises(DrbError):
+            e2.exchange_rccl_counted(comm.value)
         assert e2.exchange_rccl_roles(comm.value) == 1
     finally:
         L.ncclCommDestroy(comm)
