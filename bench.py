@@ -131,6 +131,10 @@ def parse():
                          "round, so the timed rounds see the quiesced "
                          "steady state (quiesceState: 20 x ElectionRTT = 200 "
                          "idle ticks, quiesce.go:44-82)")
+    ap.add_argument("--no-lean", action="store_true",
+                    help="c5: step every listed replica through the full "
+                         "step kernel (drb_config.no_lean; A/B of the lean "
+                         "kernel of heartbeat rounds, drb_lean.hpp)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--save", default="",
                     choices=["", "none", "entrybatch", "tan", "tanmux"],
@@ -626,7 +630,7 @@ def main():
                      save_tan=int(args.save in ("tan", "tanmux")),
                      tan_multiplexed=int(args.save == "tanmux"),
                      quiesce=args.quiesce, first_shard_id=first_shard,
-                     device=local)
+                     no_lean=int(args.no_lean), device=local)
     else:
         first_shard, seed = ddist.shard_plan(rank, G)
         # with --save: room for the round's EntriesToSave (a follower may

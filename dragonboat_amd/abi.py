@@ -141,7 +141,7 @@ class Config(C.Structure):
                 ("forward_proposals", C.c_uint32),
                 ("nonvoting_slots", C.c_uint32),
                 ("witness_slots", C.c_uint32),
-                ("host_copies", C.c_uint32)]
+                ("host_copies", C.c_uint32), ("no_lean", C.c_uint32)]
 
 
 class ReadResult(C.Structure):

@@ -3,8 +3,8 @@
 hipcc cross-compiles for gfx950 without a GPU; the .so is built in-tree so
 it travels to the GPU box with the repository snapshot.
 
-The step kernel has 56 instantiations (R = 1..8 replicas per group x seven
-kinds, drb_launch.hpp).  Each is its own translation unit
+The step kernel has 72 instantiations (R = 1..8 replicas per group x nine
+kinds, drb_launch.hpp, the lean kernel's two among them).  Each is its own translation unit
 (drb_step_inst.hip compiled with -DDRB_INST_R / -DDRB_INST_KIND), so the
 objects build in parallel and only the ones whose sources changed rebuild;
 the engine's host code and auxiliary kernels are drb_engine.hip.
@@ -24,9 +24,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
          "-Wno-pass-failed"]
-NUM_KINDS = 7
+NUM_KINDS = 9
 # the headers a step-kernel instantiation includes
-STEP_DEPS = ["drb_step_inst.hip", "drb_step.hpp", "drb_launch.hpp",
+STEP_DEPS = ["drb_step_inst.hip", "drb_step.hpp", "drb_lean.hpp",
+             "drb_launch.hpp",
              "drb_layout.hpp", "drb_msg.hpp", "drb_codec.hpp", "drb_ring.hpp"]
 # the tan record kernels' (drb_tan_inst.hip)
 TAN_DEPS = ["drb_tan_inst.hip", "drb_tan.hpp", "drb_launch.hpp",

@@ -50,6 +50,8 @@ struct drb_engine {
   // drb_set_session_clients: per lane the ClientID of the host's NoOP
   // session of its group ([G], null until set)
   uint64_t *sess_client = nullptr;
+  // the lean kernel of listed rounds off (drb_config.no_lean: A/B only)
+  bool no_lean = false;
   hipEvent_t ev_staged;           // upload done -> layout kernel
   hipEvent_t ev_stage_free;       // layout kernel done -> next upload
   hipEvent_t ev_uploaded;         // packed upload done -> host arrays free
@@ -282,6 +284,7 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
   }
   // (host_copies: HIP copies, as when the SDMA engines are unavailable)
   if (cfg->host_copies) e->xfer.state = -1;
+  e->no_lean = cfg->no_lean != 0;
   if (hipSetDevice(cfg->device) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) !=
           hipSuccess ||
@@ -495,6 +498,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.act_cnt, 4 * R * nb);
     rc |= dalloc(e, &v.act_off, 4 * R * nb);
     rc |= dalloc(e, &v.act_mask, 4 * R * nb * 4);
+    rc |= dalloc(e, &v.esc_list, 2 * R * G);
+    rc |= dalloc(e, &v.esc_n, 2 * R);
   }
   rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
@@ -2054,6 +2059,8 @@ __global__ __launch_bounds__(1024) void k_active_prefix(const View v,
     run += cnt[i];
   }
   if (threadIdx.x == 1023) v.act_total[row] = part[1023];
+  // (a lean round's escalation counts, per list row, start at zero)
+  if (threadIdx.x == 0 && row < 2ull * v.R) v.esc_n[row] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_active_scatter(const View v) {
@@ -2126,8 +2133,18 @@ static void launch_step(drb_engine *e, const RoundParams &p0,
     (void)hipEventRecord(e->ev_fork, st);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
   }
+  // listed rounds of a plain EXT engine: the light lanes' heartbeat rounds
+  // through the lean kernel first (drb_lean.hpp), the full kernel then
+  // over the heavy lanes and the ones the lean kernel escalated
+  const bool lean = p0.listed && ext && kl == SK_LEAD_EXT && !nblk &&
+                    !e->v.elections && !e->v.remote_mask &&
+                    !e->v.save_tan && !e->v.save_batched && !e->no_lean;
+  pl.lean = pf.lean = lean ? 1u : 0u;
+  hipStream_t sf = split ? e->stream2 : st;
+  if (nl && lean) launch[SK_LEAD_LEAN](e->v, pl, gx * nl, st);
   if (nl) launch[kl](e->v, pl, gx * nl, st);
-  if (nf) launch[kf](e->v, pf, gx * nf, split ? e->stream2 : st);
+  if (nf && lean) launch[SK_FOLLOW_LEAN](e->v, pf, gx * nf, sf);
+  if (nf) launch[kf](e->v, pf, gx * nf, sf);
   if (split) {
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(st, e->ev_join, 0);

@@ -19,6 +19,9 @@ enum StepKind : int {
   SK_LEAD_FWD = 5,    // step_kernel<R, true, true, false, true>: EXT with
                       //   forwarded proposals (drb_config.forward_proposals)
   SK_FOLLOW_FWD = 6,  // step_kernel<R, false, true, false, true>
+  SK_LEAD_LEAN = 7,   // lean_kernel<R, true>: a listed round's heartbeat-
+                      //   only leaders (drb_lean.hpp)
+  SK_FOLLOW_LEAN = 8,  // lean_kernel<R, false>
   NUM_STEP_KINDS
 };
 
@@ -38,7 +41,9 @@ typedef void (*StepLaunchFn)(const View &v, const RoundParams &p,
   DRB_DECLARE_STEP_LAUNCH(R, 3)                                           \
   DRB_DECLARE_STEP_LAUNCH(R, 4)                                           \
   DRB_DECLARE_STEP_LAUNCH(R, 5)                                           \
-  DRB_DECLARE_STEP_LAUNCH(R, 6)
+  DRB_DECLARE_STEP_LAUNCH(R, 6)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 7)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 8)
 DRB_DECLARE_STEP_LAUNCH_R(1)
 DRB_DECLARE_STEP_LAUNCH_R(2)
 DRB_DECLARE_STEP_LAUNCH_R(3)
@@ -64,7 +69,8 @@ void tan_launch_write(const View &v, uint32_t round, uint64_t max_log,
   {DRB_STEP_LAUNCH_NAME(R, 0), DRB_STEP_LAUNCH_NAME(R, 1),                \
    DRB_STEP_LAUNCH_NAME(R, 2), DRB_STEP_LAUNCH_NAME(R, 3),                \
    DRB_STEP_LAUNCH_NAME(R, 4), DRB_STEP_LAUNCH_NAME(R, 5),                \
-   DRB_STEP_LAUNCH_NAME(R, 6)}
+   DRB_STEP_LAUNCH_NAME(R, 6), DRB_STEP_LAUNCH_NAME(R, 7),                \
+   DRB_STEP_LAUNCH_NAME(R, 8)}
 static const StepLaunchFn kStepLaunch[8][NUM_STEP_KINDS] = {
     DRB_STEP_LAUNCH_ROW(1), DRB_STEP_LAUNCH_ROW(2), DRB_STEP_LAUNCH_ROW(3),
     DRB_STEP_LAUNCH_ROW(4), DRB_STEP_LAUNCH_ROW(5), DRB_STEP_LAUNCH_ROW(6),

@@ -426,6 +426,10 @@ struct View {
   unsigned long long *act_total;    // [2][R][2 (heavy, light)]
   uint32_t *act_cnt, *act_off;      // [2][R][2][blocks]
   uint64_t *act_mask;               // [2][R][2][blocks][4] (a word a wave)
+  // lean listed rounds (drb_lean.hpp): per row the light lanes the lean
+  // kernel left to the full one, and their count
+  uint32_t *esc_list;               // [2][R][G]
+  uint32_t *esc_n;                  // [2][R]
 };
 
 __host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,

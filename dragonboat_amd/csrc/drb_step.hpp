@@ -2256,6 +2256,10 @@ struct RoundParams {
   // block, and the engine's group blocks (0: the launch covers them all)
   uint32_t blk0;
   uint32_t gx_all;
+  // listed rounds with the lean kernel (drb_lean.hpp): the full EXT kernel
+  // steps the heavy part of its row's list and the lanes the lean kernel
+  // escalated
+  uint32_t lean;
 };
 
 // Whether this replica takes the lane's staged proposals / ReadIndex
@@ -2443,16 +2447,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   // past the list's end have nothing to do.
   const uint64_t lrow = ((uint64_t)(LEAD ? 0 : 1) * v.R + slot);
   const uint64_t li = (uint64_t)bp.x * blockDim.x + threadIdx.x;
-  uint64_t nlisted = 0;
+  uint64_t nlisted = 0, nheavy = 0;
+  const bool lean = EXT && !SLOW && p.lean;
   // (the raft launch takes its lanes from the slow list, listed or not)
   if (!SLOW && p.listed) {  // the heavy part of the row's list, then light
-    nlisted = v.act_total[2 * lrow] + v.act_total[2 * lrow + 1];
+    nheavy = v.act_total[2 * lrow];
+    // (lean: the light lanes the lean kernel escalated, instead)
+    nlisted = nheavy + (lean ? v.esc_n[lrow] : v.act_total[2 * lrow + 1]);
     if ((uint64_t)bp.x * blockDim.x >= nlisted) return;  // uniform
   }
-  const uint64_t g = SLOW ? lo64(slow_e)
-                   : p.listed ? (li < nlisted ? v.act_list[lrow * v.G + li]
-                                              : v.G)
-                              : li;
+  const uint64_t g =
+      SLOW ? lo64(slow_e)
+      : p.listed
+          ? (li >= nlisted ? v.G
+             : lean && li >= nheavy ? v.esc_list[lrow * v.G + li - nheavy]
+                                    : v.act_list[lrow * v.G + li])
+          : li;
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[EXT ? 256 : 1];
@@ -3433,3 +3443,5 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
 }
 
 }  // namespace drb
+
+#include "drb_lean.hpp"

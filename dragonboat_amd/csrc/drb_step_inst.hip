@@ -1,6 +1,7 @@
 // drb_step_inst.hip -- one instantiation of the step kernel (drb_step.hpp)
 // and its launcher, compiled once per (R, kind) with -DDRB_INST_R and
-// -DDRB_INST_KIND (dragonboat_amd/build.py).  The 56 instantiations are
+// -DDRB_INST_KIND (dragonboat_amd/build.py).  The 72 instantiations (the
+// lean kernel of drb_lean.hpp among them) are
 // independent translation units so the build runs them in parallel; the
 // engine (drb_engine.hip) calls them through kStepLaunch (drb_launch.hpp).
 //
@@ -24,14 +25,19 @@ void DRB_STEP_LAUNCH_NAME(DRB_INST_R, DRB_INST_KIND)(const View &v,
                                                      unsigned grid,
                                                      hipStream_t s) {
   constexpr int K = DRB_INST_KIND;
-  constexpr bool LEAD =
-      K == SK_LEAD || K == SK_LEAD_EXT || K == SK_SLOW || K == SK_LEAD_FWD;
-  constexpr bool FWD = K == SK_SLOW || K == SK_LEAD_FWD || K == SK_FOLLOW_FWD;
-  constexpr bool EXT = K == SK_LEAD_EXT || K == SK_FOLLOW_EXT || FWD;
-  constexpr bool SLOW = K == SK_SLOW;
-  // the leader's per-remote entry-row floors (LDS) exist with placement C4
-  const size_t dyn = LEAD && v.remote_mask ? DRB_INST_R * 256 * 8 : 0;
-  step_kernel<DRB_INST_R, LEAD, EXT, SLOW, FWD><<<grid, 256, dyn, s>>>(v, p);
+  if constexpr (K == SK_LEAD_LEAN || K == SK_FOLLOW_LEAN) {
+    lean_kernel<DRB_INST_R, K == SK_LEAD_LEAN><<<grid, 256, 0, s>>>(v, p);
+  } else {
+    constexpr bool LEAD =
+        K == SK_LEAD || K == SK_LEAD_EXT || K == SK_SLOW || K == SK_LEAD_FWD;
+    constexpr bool FWD =
+        K == SK_SLOW || K == SK_LEAD_FWD || K == SK_FOLLOW_FWD;
+    constexpr bool EXT = K == SK_LEAD_EXT || K == SK_FOLLOW_EXT || FWD;
+    constexpr bool SLOW = K == SK_SLOW;
+    // the leader's per-remote entry-row floors (LDS) exist with placement C4
+    const size_t dyn = LEAD && v.remote_mask ? DRB_INST_R * 256 * 8 : 0;
+    step_kernel<DRB_INST_R, LEAD, EXT, SLOW, FWD><<<grid, 256, dyn, s>>>(v, p);
+  }
 }
 
 }  // namespace drb

@@ -79,7 +79,8 @@ struct WorkerState {
 
 // until the copies of staging set k are done
 static void worker_wait_copies(WorkerState &w, int k) {
-  if (!w.hsa) return;
+  // (a set never used has no signal yet: nothing to wait for)
+  if (!w.hsa || !w.set[k].done.handle) return;
   while (hsa_signal_wait_scacquire(w.set[k].done, HSA_SIGNAL_CONDITION_LT, 1,
                                    UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
   }
@@ -351,13 +352,16 @@ static uint64_t worker_meta_words(uint64_t cval) {
 static int worker_reserve(drb_engine *e, int k, uint64_t crd, uint64_t cval,
                           uint64_t cdf) {
   WorkerSet &s = e->worker->set[k];
-  if (!s.lanes) {
+  if (!s.ev_staged)
     HIPCHK(hipEventCreateWithFlags(&s.ev_staged, hipEventDisableTiming));
+  if (!s.ev_drained)
     HIPCHK(hipEventCreateWithFlags(&s.ev_drained, hipEventDisableTiming));
+  if (!s.lanes)
     HIPCHK(hipMalloc(&s.lanes, std::max<uint64_t>(e->v.G, 1) * 4 + 16));
-    if (e->worker->hsa &&
-        hsa_signal_create(0, 0, nullptr, &s.done) != HSA_STATUS_SUCCESS)
-      return DRB_EDEVICE;
+  if (e->worker->hsa && !s.done.handle &&
+      hsa_signal_create(0, 0, nullptr, &s.done) != HSA_STATUS_SUCCESS) {
+    s.done.handle = 0;
+    return DRB_EDEVICE;
   }
   if (s.rd && crd <= s.cap_rd && cval <= s.cap_val && cdf <= s.cap_df)
     return DRB_OK;

@@ -196,7 +196,8 @@ DEFAULTS = dict(num_groups=1, first_shard_id=1, num_replicas=3, window=32,
                 save_batched=0, save_tan=0, tan_max_log=0, elections=0,
                 tan_multiplexed=0, pre_vote=0, max_reads_per_ctx=0,
                 kv_overflow_buckets=0, forward_proposals=0,
-                nonvoting_slots=0, witness_slots=0, host_copies=0)
+                nonvoting_slots=0, witness_slots=0, host_copies=0,
+                no_lean=0)
 
 
 class Engine:
@@ -220,7 +221,8 @@ class Engine:
                    cfg["tan_multiplexed"], cfg["pre_vote"],
                    cfg["max_reads_per_ctx"], cfg["kv_overflow_buckets"],
                    cfg["forward_proposals"], cfg["nonvoting_slots"],
-                   cfg["witness_slots"], cfg["host_copies"])
+                   cfg["witness_slots"], cfg["host_copies"],
+                   cfg["no_lean"])
         h = P()
         _ck(lib().drb_engine_create(C.byref(c), C.byref(h)),
             "drb_engine_create")

@@ -423,6 +423,10 @@ typedef struct drb_config {
    * the path every engine takes when the HSA copy engines are unavailable,
    * selectable so that it can be tested.  0: SDMA when available. */
   uint32_t host_copies;
+  /* 1: listed rounds step every listed replica through the full step
+   * kernel; 0: the heartbeat-only rounds of quiet groups go through the
+   * lean kernel first (drb_lean.hpp; for A/B measurements) */
+  uint32_t no_lean;
 } drb_config;
 
 /* One step round (engine.processSteps, engine.go:1304). */

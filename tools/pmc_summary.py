@@ -16,7 +16,7 @@ import json
 import os
 from collections import defaultdict
 
-ROUND_KERNELS = ("step_kernel", "k_serve_reads")
+ROUND_KERNELS = ("step_kernel", "lean_kernel", "k_serve_reads")
 
 
 def load(d):
