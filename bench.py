@@ -1229,6 +1229,7 @@ def main():
                          "flagged_in_warmup": warm_flagged,
                          "replicas_stepped_per_round":
                              out.replicas_stepped / K,
+                         "lean_stepped_per_round": out.lean_stepped / K,
                          "saved_entries": out.saved_entries,
                          "saved_bytes": out.saved_bytes},
         }

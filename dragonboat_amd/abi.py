@@ -311,7 +311,8 @@ class RoundOut(C.Structure):
                 ("log_new", C.c_uint64),
                 ("elections_stepped", C.c_uint64),
                 ("role_changes", C.c_uint64),
-                ("dropped_proposals", C.c_uint64)]
+                ("dropped_proposals", C.c_uint64),
+                ("lean_stepped", C.c_uint64)]
 
     def to_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

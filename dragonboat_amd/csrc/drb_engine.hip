@@ -498,8 +498,8 @@ extern "C" int drb_engine_create(const drb_config *cfg, drb_engine **out) {
     rc |= dalloc(e, &v.act_cnt, 4 * R * nb);
     rc |= dalloc(e, &v.act_off, 4 * R * nb);
     rc |= dalloc(e, &v.act_mask, 4 * R * nb * 4);
-    rc |= dalloc(e, &v.esc_list, 2 * R * G);
-    rc |= dalloc(e, &v.esc_n, 2 * R);
+    rc |= dalloc(e, &v.esc_list, 2ull * R * ESC_SPLIT * esc_seg(G));
+    rc |= dalloc(e, &v.esc_n, 2ull * R * ESC_SPLIT);
   }
   rc |= dalloc(e, &e->role_dev, 2);
   rc |= dalloc(e, &e->dview, 1);
@@ -2060,7 +2060,8 @@ __global__ __launch_bounds__(1024) void k_active_prefix(const View v,
   }
   if (threadIdx.x == 1023) v.act_total[row] = part[1023];
   // (a lean round's escalation counts, per list row, start at zero)
-  if (threadIdx.x == 0 && row < 2ull * v.R) v.esc_n[row] = 0;
+  if (threadIdx.x < ESC_SPLIT && row < 2ull * v.R)
+    v.esc_n[row * ESC_SPLIT + threadIdx.x] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_active_scatter(const View v) {
@@ -2138,12 +2139,26 @@ static void launch_step(drb_engine *e, const RoundParams &p0,
   // over the heavy lanes and the ones the lean kernel escalated
   const bool lean = p0.listed && ext && kl == SK_LEAD_EXT && !nblk &&
                     !e->v.elections && !e->v.remote_mask &&
-                    !e->v.save_tan && !e->v.save_batched && !e->no_lean;
-  pl.lean = pf.lean = lean ? 1u : 0u;
+                    !e->v.save_tan && !e->v.save_batched && !e->no_lean &&
+                    st == e->stream;
+  if (lean) {
+    // the lean kernels, then the full ones over the heavy and the
+    // escalated lanes, one stream.  (The heavy lanes' full launches on the
+    // second stream beside the lean kernels measured no faster: 2.02
+    // against 1.97 ms a C5 round, profiles/r06_lean.)
+    if (split) {
+      (void)hipEventRecord(e->ev_join, e->stream2);
+      (void)hipStreamWaitEvent(st, e->ev_join, 0);
+    }
+    if (nl) launch[SK_LEAD_LEAN](e->v, pl, gx * nl, st);
+    if (nf) launch[SK_FOLLOW_LEAN](e->v, pf, gx * nf, st);
+    pl.lean = pf.lean = LEAN_ALL;
+    if (nl) launch[kl](e->v, pl, gx * nl, st);
+    if (nf) launch[kf](e->v, pf, gx * nf, st);
+    return;
+  }
   hipStream_t sf = split ? e->stream2 : st;
-  if (nl && lean) launch[SK_LEAD_LEAN](e->v, pl, gx * nl, st);
   if (nl) launch[kl](e->v, pl, gx * nl, st);
-  if (nf && lean) launch[SK_FOLLOW_LEAN](e->v, pf, gx * nf, sf);
   if (nf) launch[kf](e->v, pf, gx * nf, sf);
   if (split) {
     (void)hipEventRecord(e->ev_join, e->stream2);
@@ -2446,6 +2461,7 @@ extern "C" int drb_read_counters(drb_engine *e, drb_round_out *out,
   out->elections_stepped = c[C_ELECT];
   out->role_changes = c[C_ROLE];
   out->dropped_proposals = c[C_DPROP];
+  out->lean_stepped = c[C_LEAN];
   out->log_records = 0;
   out->log_syncs = 0;
   out->log_new = 0;

@@ -427,10 +427,19 @@ struct View {
   uint32_t *act_cnt, *act_off;      // [2][R][2][blocks]
   uint64_t *act_mask;               // [2][R][2][blocks][4] (a word a wave)
   // lean listed rounds (drb_lean.hpp): per row the light lanes the lean
-  // kernel left to the full one, and their count
-  uint32_t *esc_list;               // [2][R][G]
-  uint32_t *esc_n;                  // [2][R]
+  // kernel left to the full one, in ESC_SPLIT segments (a workgroup's by
+  // its block index mod ESC_SPLIT), and their counts
+  uint32_t *esc_list;               // [2][R][ESC_SPLIT][esc_seg(G)]
+  uint32_t *esc_n;                  // [2][R][ESC_SPLIT]
 };
+
+// The escalation list of a row is split so that no one counter takes every
+// wave's atomic: a lean round escalates a few lanes of nearly every wave,
+// and atomics on one address serialise at ~14 ns each (profiles/r06_lean).
+constexpr uint32_t ESC_SPLIT = 64;
+__host__ __device__ inline uint64_t esc_seg(uint64_t G) {
+  return ((((G + 255) / 256) + ESC_SPLIT - 1) / ESC_SPLIT) * 256;
+}
 
 __host__ __device__ inline uint64_t ix(const View &v, uint32_t slot,
                                        uint64_t g) {

@@ -44,16 +44,20 @@
 
 namespace drb {
 
-// 4 waves per SIMD: 112 / 119 VGPRs (follower / leader at R = 3) and no
-// spills, where the full EXT kernels spill 37 / 25 at 4 / 3 waves; at 5 or
-// 6 waves the lean kernel itself spills 50-95 VGPRs
+// waves per SIMD: the follower at 5 up to R = 3 (96 VGPRs, 4 spilled; at
+// R = 5 five waves would spill 149), the leader at 4 (113 VGPRs), where
+// the full EXT kernels spill 37 / 25 VGPRs at 4 / 3 waves
 #ifndef DRB_LEAN_WAVES
 #define DRB_LEAN_WAVES 4
+#endif
+#ifndef DRB_LEAN_FOLLOW_WAVES
+#define DRB_LEAN_FOLLOW_WAVES 5
 #endif
 
 template <int R, bool LEAD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    DRB_LEAN_WAVES))) void lean_kernel(const View v, RoundParams p) {
+    LEAD || R > 3 ? DRB_LEAN_WAVES : DRB_LEAN_FOLLOW_WAVES))) void lean_kernel(
+    const View v, RoundParams p) {
   const View *vp = &v;
   const BlockPos bp = block_pos(p);
   const uint32_t slot = (p.slots >> (4 * bp.y)) & 0xfu;
@@ -82,25 +86,86 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   L.members = false;
   uint32_t c_msgs = 0, c_stepped = 0;
   bool esc = false;  // escalated to the full kernel
-  bool active = g < v.G;
-  const uint32_t flags = active ? v.u32[u32_ix(v, W_FLAGS, slot, g)] : 0;
-  const uint32_t role = active ? v.u32[u32_ix(v, W_ROLE, slot, g)] : 0;
+  // records per sender a heartbeat round holds: the tick's Heartbeat, or
+  // the answer to it (a second one -- a ReadIndex's -- carries a ctx and
+  // escalates anyway)
+  constexpr int NREC = 1;
+  // Every load of the lane first, none depending on another: the flags,
+  // the record, the inbox headers and -- speculatively, before the headers
+  // say how many there are -- the first non-Replicate record of each
+  // sender, the quiesce state and tick counter, the leader's remotes.  A
+  // lane then waits for one memory round trip, where the full kernel's
+  // chain of decisions waits for several.
+  const bool valid = g < v.G;
+  const bool qon = v.quiesce;
+  uint32_t flags = 0, role = 0, fbw = 0, ric = 0, pcount = 0;
+  uint4 pkq[4], meta[R], rec[R][NREC], riq = make_uint4(0, 0, 0, 0);
+  uint64_t qsv[5] = {0, 0, 0, 0, 0}, tick_count = 0;
+  uint64_t rmatch[R];
+  uint32_t rstate[R], ractive[R];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) pkq[c] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int s = 0; s < R; ++s) {
+    meta[s] = make_uint4(0, 0, 0, 0);
+    rmatch[s] = 0;
+    rstate[s] = ractive[s] = 0;
+#pragma unroll
+    for (int j = 0; j < NREC; ++j) rec[s][j] = make_uint4(0, 0, 0, 0);
+  }
+  if (valid) {
+    flags = v.u32[u32_ix(v, W_FLAGS, slot, g)];
+    role = v.u32[u32_ix(v, W_ROLE, slot, g)];
+    fbw = v.u32[u32_ix(v, W_FB_REASON, slot, g)];
+    ric = v.u32[u32_ix(v, W_RI_COUNT, slot, g)];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pkq[c] = v.pk[pk_ix(v, c, slot, g)];
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if ((uint32_t)s == slot) continue;
+      meta[s] = v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)];
+#pragma unroll
+      for (int j = 0; j < NREC; ++j)
+        rec[s][j] = v.mbox[mbox_ix(v, L.rbuf, s, slot,
+                                   rec_pos(false, (uint32_t)j, v.MB), 0, g)];
+    }
+    if (qon) {
+      qsv[0] = v.u64[u64_ix(v, F_QS_TICK, slot, g)];
+      qsv[1] = v.u64[u64_ix(v, F_QS_IDLE, slot, g)];
+      qsv[2] = v.u64[u64_ix(v, F_QS_SINCE, slot, g)];
+      qsv[3] = v.u64[u64_ix(v, F_QS_EXIT, slot, g)];
+      qsv[4] = v.u64[u64_ix(v, F_QS_BASE, slot, g)];
+    }
+    if (p.tick) tick_count = v.u64[u64_ix(v, F_TICK_COUNT, slot, g)];
+    if (LEAD) {
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        if ((uint32_t)s != slot) {
+          rmatch[s] = v.rem_match[rem_ix(v, slot, s, g)];
+          rstate[s] = v.rem_state[rem_ix(v, slot, s, g)];
+        }
+        ractive[s] = v.rem_active[rem_ix(v, slot, s, g)];
+      }
+    }
+    if (prop_here(v, p, slot, LEAD))
+      pcount = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
+    if (ri_here(v, p, slot, LEAD))
+      riq = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
+  }
   // (the list holds hosted replicas on the fast path of this row's role)
-  if (!(flags & DRB_F_HOSTED) || (flags & (DRB_F_FALLBACK | DRB_F_ERROR)) ||
-      ((role == DRB_LEADER) != LEAD))
-    active = false;
+  bool active = valid && (flags & DRB_F_HOSTED) &&
+                !(flags & (DRB_F_FALLBACK | DRB_F_ERROR)) &&
+                ((role == DRB_LEADER) == LEAD);
   if (active) {
     Rep<R> r;
-    // the 64 B record as load_rep decodes it; the remotes and the queue
-    // only as far as a heartbeat round reads them
+    // the 64 B record as load_rep decodes it
     uint32_t pw0[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const uint4 q = v.pk[pk_ix(v, c, slot, g)];
-      r.pw[4 * c] = pw0[4 * c] = q.x;
-      r.pw[4 * c + 1] = pw0[4 * c + 1] = q.y;
-      r.pw[4 * c + 2] = pw0[4 * c + 2] = q.z;
-      r.pw[4 * c + 3] = pw0[4 * c + 3] = q.w;
+      r.pw[4 * c] = pw0[4 * c] = pkq[c].x;
+      r.pw[4 * c + 1] = pw0[4 * c + 1] = pkq[c].y;
+      r.pw[4 * c + 2] = pw0[4 * c + 2] = pkq[c].z;
+      r.pw[4 * c + 3] = pw0[4 * c + 3] = pkq[c].w;
     }
     r.last = (uint64_t)r.pw[0] | ((uint64_t)r.pw[1] << 32);
     r.term = (uint64_t)r.pw[2] | ((uint64_t)r.pw[3] << 32);
@@ -122,8 +187,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     r.applied_any = false;
     r.lid_dirty = false;
     r.flags = flags;
-    r.fb = v.u32[u32_ix(v, W_FB_REASON, slot, g)];
-    r.ri_count = v.u32[u32_ix(v, W_RI_COUNT, slot, g)];
+    r.fb = fbw;
+    r.ri_count = ric;
     r.role = LEAD ? DRB_LEADER : DRB_FOLLOWER;
     r.votes = 0;
 #pragma unroll
@@ -138,22 +203,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
               r.saved_to == r.last && r.sm_index == r.last &&
               r.applied_index == r.last && r.marker > r.last &&
               r.ri_count == 0 && !(flags & (F_XFER | F_XFER_REQ)) &&
-              (LEAD || role == DRB_FOLLOWER);
-    if (ri_here(v, p, slot, LEAD)) {
-      const uint4 c = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
-      if (c.x | c.y | c.z | c.w) ok = false;
-    }
-    if (prop_here(v, p, slot, LEAD) &&
-        v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
-      ok = false;
+              (LEAD || role == DRB_FOLLOWER) && pcount == 0 &&
+              !(riq.x | riq.y | riq.z | riq.w);
     if (LEAD) {  // the remotes: match, state, active (next is not needed)
 #pragma unroll
       for (int s = 0; s < R; ++s) {
         RemoteV x;
-        x.m = (uint32_t)s == slot ? 0 : v.rem_match[rem_ix(v, slot, s, g)];
+        x.m = rmatch[s];
         x.n = 0;
-        x.st = (uint32_t)s == slot ? 0 : v.rem_state[rem_ix(v, slot, s, g)];
-        x.a = v.rem_active[rem_ix(v, slot, s, g)];
+        x.st = rstate[s];
+        x.a = ractive[s];
         if ((uint32_t)s != slot &&
             (x.m != r.last || x.st != DRB_REMOTE_REPLICATE))
           ok = false;
@@ -163,42 +222,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     }
     const uint32_t flags0 = r.flags, fb0 = r.fb;
     const uint32_t tag_prev = (uint32_t)(p.round - 1);
-    const bool qon = v.quiesce;
     uint64_t qs_owed = 0;
     if (qon) {
-      r.qs_tick = over_ld(L, F_QS_TICK);
-      r.qs_idle = over_ld(L, F_QS_IDLE);
-      r.qs_since = over_ld(L, F_QS_SINCE);
-      r.qs_exit = over_ld(L, F_QS_EXIT);
+      r.qs_tick = qsv[0];
+      r.qs_idle = qsv[1];
+      r.qs_since = qsv[2];
+      r.qs_exit = qsv[3];
       r.qs_dirty = 0;
-      qs_owed = p.tick_no - p.tick - over_ld(L, F_QS_BASE);
+      qs_owed = p.tick_no - p.tick - qsv[4];
       r.election_tick += qs_owed;
       r.qs_tick += qs_owed;
     }
-    // the inbox: heartbeats only, at the replica's term; the records kept
-    // (at most two per sender: the tick's heartbeat and its answer)
-    constexpr int NREC = 2;
-    uint4 rec[R][NREC];
+    // the inbox: heartbeats only, at the replica's term
     uint32_t nrec[R];
     uint32_t qz_from = 0, resp_from = 0, total_in = 0;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       nrec[s] = 0;
-#pragma unroll
-      for (int j = 0; j < NREC; ++j) rec[s][j] = make_uint4(0, 0, 0, 0);
       if ((uint32_t)s == slot) continue;
-      const uint4 meta = v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)];
-      const bool cur = tag_is(meta.x, tag_prev);
-      const uint32_t info = cur ? meta.y : 0u;
+      const bool cur = tag_is(meta[s].x, tag_prev);
+      const uint32_t info = cur ? meta[s].y : 0u;
       const uint32_t ns = mi_count(info);
-      if (cur && (meta.x & MQ_QUIESCE)) qz_from |= 1u << s;
+      if (cur && (meta[s].x & MQ_QUIESCE)) qz_from |= 1u << s;
       if (!ns) continue;
       if (mi_nrep(info) || ((info >> MI_NRI) & 0x1fu) ||
           ((info >> MI_NRR) & 0x1fu) ||
           (info & (MI_PROP | MI_REJECT | MI_TERM_OTHER |
                    (LEAD ? MI_OFF_LEADER : MI_OFF_FOLLOWER))) ||
-          ((info & MI_TERM) && hi64(meta) != r.term) || ns > (uint32_t)NREC ||
-          (!LEAD && (uint64_t)s + 1 != r.leader_id))
+          ((info & MI_TERM) && hi64(meta[s]) != r.term) ||
+          ns > (uint32_t)NREC || (!LEAD && (uint64_t)s + 1 != r.leader_id))
         ok = false;
       if (info & MI_RESP) resp_from |= 1u << s;
       total_in += ns;
@@ -206,10 +258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int j = 0; j < NREC; ++j)
         if ((uint32_t)j < nrec[s]) {
-          const uint4 c0 =
-              v.mbox[mbox_ix(v, L.rbuf, s, slot, rec_pos(false, j, v.MB), 0,
-                             g)];
-          rec[s][j] = c0;
+          const uint4 c0 = rec[s][j];
           // (a record with a second chunk carries a ReadIndex ctx; one
           // that repeats the last ctx as well)
           const uint32_t t = c0.x & 0xffu;
@@ -267,8 +316,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       for (int s = 0; s < R; ++s) {
         if ((uint32_t)s == slot) continue;
         if (qon && ((qz_from >> s) & 1)) qs_try_enter(v, r);
-        const uint64_t sterm =
-            hi64(v.mbox_meta[mmeta_ix(v, L.rbuf, s, slot, g)]);
+        const uint64_t sterm = hi64(meta[s]);
 #pragma unroll
         for (int j = 0; j < NREC; ++j) {
           if ((uint32_t)j >= nrec[s]) continue;
@@ -291,7 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       if (p.tick && quiet) {
         r.election_tick++;  // raft.quiescedTick (raft.go:650-656)
       } else if (p.tick) {
-        over_st(L, F_TICK_COUNT, over_ld(L, F_TICK_COUNT) + 1);
+        over_st(L, F_TICK_COUNT, tick_count + 1);
         if (LEAD) {
           r.election_tick++;
           if (r.election_tick >= v.election_rtt) {
@@ -411,19 +459,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
     }
   }
-  // the escalated lanes onto the row's list: one atomic per wave (global
-  // atomics on one address from every lane serialise, ~14 ns each)
+  // the escalated lanes onto the row's list: one atomic per wave, into
+  // the list segment of this block (block index mod ESC_SPLIT; global
+  // atomics on one address serialise, ~14 ns each)
   {
     const uint64_t bal = __ballot(esc);
     if (bal) {
       const uint32_t lane = threadIdx.x & 63u;
       const uint32_t first = (uint32_t)__ffsll((long long)bal) - 1u;
+      const uint32_t k = bp.x % ESC_SPLIT;
+      const uint64_t seg = esc_seg(v.G);
       unsigned base = 0;
       if (lane == first)
-        base = atomicAdd(&v.esc_n[lrow], (unsigned)__popcll(bal));
+        base = atomicAdd(&v.esc_n[lrow * ESC_SPLIT + k],
+                         (unsigned)__popcll(bal));
       base = (unsigned)__shfl((int)base, (int)first, 64);
       if (esc)
-        v.esc_list[lrow * v.G + base +
+        v.esc_list[(lrow * ESC_SPLIT + k) * seg + base +
                    (unsigned)__popcll(bal & ((1ull << lane) - 1ull))] =
             (uint32_t)g;
     }
@@ -431,6 +483,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   uint32_t cnt[NUM_COUNTERS] = {};
   cnt[C_MESSAGES] = c_msgs;
   cnt[C_STEPPED] = c_stepped;
+  cnt[C_LEAN] = c_stepped;
   block_counters<LEAD, 0, NUM_COUNTERS>(v, slot, bp, cnt);
 }
 

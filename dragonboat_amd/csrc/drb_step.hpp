@@ -108,6 +108,7 @@ enum : int {
   C_ELECT,    // elections: replicas the raft launch stepped
   C_ROLE,     // elections: role changes
   C_DPROP,    // elections: proposals a transferring leader dropped
+  C_LEAN,     // replicas the lean kernel of a listed round stepped
   NUM_COUNTERS
 };
 
@@ -2257,10 +2258,16 @@ struct RoundParams {
   uint32_t blk0;
   uint32_t gx_all;
   // listed rounds with the lean kernel (drb_lean.hpp): the full EXT kernel
-  // steps the heavy part of its row's list and the lanes the lean kernel
-  // escalated
+  // steps the heavy part of its row's list (LEAN_HEAVY, concurrently with
+  // the lean kernel) or the lanes the lean kernel escalated (LEAN_ESC,
+  // after it)
   uint32_t lean;
 };
+
+// RoundParams.lean: the full kernel of a lean round steps the heavy part
+// of its row's list and the lanes the lean kernel escalated (LEAN_ALL), or
+// one of the two (LEAN_HEAVY, LEAN_ESC)
+constexpr uint32_t LEAN_HEAVY = 1, LEAN_ESC = 2, LEAN_ALL = 3;
 
 // Whether this replica takes the lane's staged proposals / ReadIndex
 // (co-resident: the leader, or replica ri_replica for reads; replicas
@@ -2365,7 +2372,10 @@ DRB_DEV void block_counters(const View &v, uint32_t slot, BlockPos bp,
     if (s) {
       const uint64_t row =
           ((uint64_t)(LEAD ? 0 : 1) * v.R + slot) * bp.gx + bp.x;
-      v.counters[row * NUM_COUNTERS + FIRST + i] += s;
+      // (an atomic: a lean round's kernels run concurrently, and two of
+      // them may own the same row; rows are per block, so no contention)
+      atomicAdd(&v.counters[row * NUM_COUNTERS + FIRST + i],
+                (unsigned long long)s);
     }
   }
 }
@@ -2447,22 +2457,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   // past the list's end have nothing to do.
   const uint64_t lrow = ((uint64_t)(LEAD ? 0 : 1) * v.R + slot);
   const uint64_t li = (uint64_t)bp.x * blockDim.x + threadIdx.x;
-  uint64_t nlisted = 0, nheavy = 0;
-  const bool lean = EXT && !SLOW && p.lean;
+  uint64_t nlisted = 0, nheavy = 0, nesc = 0;
+  const uint32_t lean = EXT && !SLOW ? p.lean : 0u;
   // (the raft launch takes its lanes from the slow list, listed or not)
   if (!SLOW && p.listed) {  // the heavy part of the row's list, then light
-    nheavy = v.act_total[2 * lrow];
-    // (lean: the light lanes the lean kernel escalated, instead)
-    nlisted = nheavy + (lean ? v.esc_n[lrow] : v.act_total[2 * lrow + 1]);
+    // (a lean round: the heavy part alone, or the light lanes the lean
+    // kernel escalated, from the ESC_SPLIT segments of the row's list)
+    nheavy = lean == LEAN_ESC ? 0 : v.act_total[2 * lrow];
+    if (lean & LEAN_ESC)
+      for (uint32_t k = 0; k < ESC_SPLIT; ++k)
+        nesc += v.esc_n[lrow * ESC_SPLIT + k];
+    nlisted = nheavy + (lean & LEAN_ESC ? nesc
+                        : lean == LEAN_HEAVY ? 0
+                                             : v.act_total[2 * lrow + 1]);
     if ((uint64_t)bp.x * blockDim.x >= nlisted) return;  // uniform
   }
-  const uint64_t g =
-      SLOW ? lo64(slow_e)
-      : p.listed
-          ? (li >= nlisted ? v.G
-             : lean && li >= nheavy ? v.esc_list[lrow * v.G + li - nheavy]
-                                    : v.act_list[lrow * v.G + li])
-          : li;
+  uint64_t g = SLOW ? lo64(slow_e) : li;
+  if (!SLOW && p.listed) {
+    if (li >= nlisted) {
+      g = v.G;
+    } else if ((lean & LEAN_ESC) && li >= nheavy) {  // li's segment
+      uint64_t x = li - nheavy, k = 0;
+      for (; k + 1 < ESC_SPLIT; ++k) {
+        const uint32_t c = v.esc_n[lrow * ESC_SPLIT + k];
+        if (x < c) break;
+        x -= c;
+      }
+      g = v.esc_list[(lrow * ESC_SPLIT + k) * esc_seg(v.G) + x];
+    } else {
+      g = v.act_list[lrow * v.G + li];
+    }
+  }
   __shared__ RemLds<R> rl;
   __shared__ uint32_t oinfo[R * 256];
   __shared__ uint32_t crc_tab[EXT ? 256 : 1];

@@ -486,6 +486,8 @@ typedef struct drb_round_out {
   uint64_t dropped_proposals;     /* entries a leader transferring its
                                    * leadership dropped (raft.go:1796-1800;
                                    * the clients' requests complete Dropped) */
+  uint64_t lean_stepped;          /* listed rounds: of replicas_stepped, the
+                                   * heartbeat rounds the lean kernel took */
 } drb_round_out;
 
 typedef struct drb_engine drb_engine;
