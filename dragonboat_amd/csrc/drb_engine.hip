@@ -1403,18 +1403,12 @@ extern "C" int drb_stage_wait_upload(drb_engine *e) {
 // SURVEY 8(d) synthetic writes; bit-identical to dragonboat_amd/workload.py
 constexpr uint64_t ACTIVE_SALT = 0xAC71BE5EAC71BE5Eull;
 
-__global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
-                         uint32_t val_len, uint64_t seed, uint64_t salt,
-                         uint32_t active_ppm) {
-  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane >= v.G) return;
+// the proposals of one proposing lane
+__device__ static void gen_kv_lane(const View &v, uint32_t ps, uint32_t k,
+                                   uint32_t key_space, uint32_t val_len,
+                                   uint64_t seed, uint64_t salt,
+                                   uint64_t lane) {
   const uint64_t g = gid(v, v.stage_slot, lane);  // the seeded group
-  if (active_ppm < 1000000u &&
-      mix64(seed ^ ACTIVE_SALT ^ (g * 0x9E3779B97F4A7C15ull) ^ (salt << 24)) %
-              1000000u >= active_ppm) {
-    v.prop_count[(uint64_t)ps * v.G + lane] = 0;
-    return;
-  }
   const uint64_t cid = mix64(seed ^ 0xC11E47C11E47C11Eull ^ g) | 1;
   for (uint32_t j = 0; j < k; ++j) {
     uint64_t r0 = mix64(seed ^ (g * 0x9E3779B97F4A7C15ull) ^ (salt << 32) ^
@@ -1458,7 +1452,58 @@ __global__ void k_gen_kv(View v, uint32_t ps, uint32_t k, uint32_t key_space,
         DRB_ENTRY_ENCODED, clen, prop_fast(DRB_ENTRY_ENCODED, cid, 0, clen, 0),
         0);
   }
-  v.prop_count[(uint64_t)ps * v.G + lane] = k;
+}
+
+// Each workgroup draws GEN_ITERS x 256 lanes, 256 at a time, writes every
+// prop_count and gathers the proposing lanes in LDS; a full batch of 256
+// (or the rest, at the end) is then generated one lane per thread.  At C5's
+// 1 % a thread per lane left ~half the waves running the whole byte loop
+// for one or two lanes (117 us a round at 4M groups).
+constexpr uint32_t GEN_ITERS = 16;
+
+__global__ __launch_bounds__(256) void k_gen_kv(
+    View v, uint32_t ps, uint32_t k, uint32_t key_space, uint32_t val_len,
+    uint64_t seed, uint64_t salt, uint32_t active_ppm) {
+  if (active_ppm >= 1000000u) {  // every lane proposes: a thread per lane
+    const uint64_t lane = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (lane >= v.G) return;
+    v.prop_count[(uint64_t)ps * v.G + lane] = k;
+    gen_kv_lane(v, ps, k, key_space, val_len, seed, salt, lane);
+    return;
+  }
+  __shared__ uint32_t list[512];
+  __shared__ uint32_t nlist;
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * GEN_ITERS * 256;
+  for (uint32_t it = 0; it < GEN_ITERS; ++it) {
+    const uint64_t lane = base + (uint64_t)it * 256 + threadIdx.x;
+    if (lane < v.G) {
+      const uint64_t g = gid(v, v.stage_slot, lane);
+      const bool on =
+          mix64(seed ^ ACTIVE_SALT ^ (g * 0x9E3779B97F4A7C15ull) ^
+                (salt << 24)) % 1000000u < active_ppm;
+      v.prop_count[(uint64_t)ps * v.G + lane] = on ? k : 0u;
+      if (on) list[atomicAdd(&nlist, 1u)] = (uint32_t)(lane - base);
+    }
+    __syncthreads();
+    const uint32_t n = nlist;
+    if (n >= 256 || it + 1 == GEN_ITERS) {
+      if (threadIdx.x < n && threadIdx.x < 256)
+        gen_kv_lane(v, ps, k, key_space, val_len, seed, salt,
+                    base + list[threadIdx.x]);
+      __syncthreads();  // (the batch read before the list moves down)
+      if (n > 256 && threadIdx.x < n - 256)
+        list[threadIdx.x] = list[256 + threadIdx.x];
+      if (threadIdx.x == 0) nlist = n > 256 ? n - 256 : 0u;
+      __syncthreads();
+    }
+  }
+  // (at most 255 left after the last batch of 256: one more pass)
+  const uint32_t n = nlist;
+  if (threadIdx.x < n)
+    gen_kv_lane(v, ps, k, key_space, val_len, seed, salt,
+                base + list[threadIdx.x]);
 }
 
 extern "C" int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot,
@@ -1469,7 +1514,8 @@ extern "C" int drb_gen_kv_proposals_active(drb_engine *e, uint32_t slot,
       val_len > 16383 ||
       12 + (val_len < 128 ? 1 : 2) + val_len > e->cfg.cmd_cap)
     return DRB_EINVAL;
-  k_gen_kv<<<(unsigned)((e->v.G + 255) / 256), 256, 0, e->stream>>>(
+  const uint64_t per = active_ppm >= 1000000u ? 256 : GEN_ITERS * 256;
+  k_gen_kv<<<(unsigned)((e->v.G + per - 1) / per), 256, 0, e->stream>>>(
       e->v, slot, k, key_space, val_len, seed, salt, active_ppm);
   HIPCHK(hipGetLastError());  // stream-ordered before the next round
   HIPCHK(hipEventRecord(e->ev_prop[slot], e->stream));
@@ -1980,56 +2026,75 @@ static uint32_t slot_list(uint32_t mask, uint32_t *n) {
 template <int R>
 __global__ __launch_bounds__(256) void k_active_scan(const View v,
                                                      RoundParams p) {
-  const uint32_t s = blockIdx.y;
+  // one thread per group, all R replica slots: every input of the rule
+  // loaded at once (one memory round trip), the group's proposal count and
+  // ReadIndex row once for all slots
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint64_t nb = gridDim.x;
-  bool lead = false, run = false, heavy = false;
-  if (g < v.G) {
-    const uint32_t flags = v.u32[u32_ix(v, W_FLAGS, s, g)];
-    lead = v.u32[u32_ix(v, W_ROLE, s, g)] == DRB_LEADER;
-    if (flags & DRB_F_HOSTED) {
-      if (flags & (DRB_F_FALLBACK | DRB_F_ERROR)) {
+  const bool valid = g < v.G;
+  const uint32_t rbuf = (uint32_t)((p.round - 1) & 1);
+  uint32_t flags[R], role[R], pc = 0;
+  uint64_t tags[R];
+  uint4 ri = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int s = 0; s < R; ++s) {
+    flags[s] = role[s] = 0;
+    tags[s] = 0;
+  }
+  if (valid) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      flags[s] = v.u32[u32_ix(v, W_FLAGS, s, g)];
+      role[s] = v.u32[u32_ix(v, W_ROLE, s, g)];
+      tags[s] = v.inbox_tag[((uint64_t)rbuf * v.R + s) * v.G + g];
+    }
+    if (p.prop_slot != DRB_NONE)
+      pc = v.prop_count[(uint64_t)p.prop_slot * v.G + g];
+    if (p.ri_slot != DRB_NONE) ri = v.ri_in[(uint64_t)p.ri_slot * v.G + g];
+  }
+  __shared__ uint32_t c[R][4][4];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < R; ++s) {
+    const bool lead = role[s] == DRB_LEADER;
+    bool run = false, heavy = false;
+    if (flags[s] & DRB_F_HOSTED) {
+      if (flags[s] & (DRB_F_FALLBACK | DRB_F_ERROR)) {
         v.rtr_count[ix(v, s, g)] = 0;  // no round output (step kernel)
         if (p.encode_saves) v.save_len[ix(v, s, g)] = 0;
       } else {
-        run = !idle_round<R>(v, p, s, g, lead, flags);
+        run = !idle_round_of<R>(v, p, s, lead, flags[s], tags[s], pc, ri);
       }
     }
     if (run) {
-      const uint64_t tags =
-          v.inbox_tag[((uint64_t)((p.round - 1) & 1) * v.R + s) * v.G + g];
 #pragma unroll
       for (int q = 0; q < R; ++q) {
-        const uint32_t b = (uint32_t)(tags >> (8 * q)) & 0xffu;
-        if ((uint32_t)q != s && tag_current(b, p.round - 1) &&
-            (b & TAG_HEAVY))
+        const uint32_t b = (uint32_t)(tags[s] >> (8 * q)) & 0xffu;
+        if (q != s && tag_current(b, p.round - 1) && (b & TAG_HEAVY))
           heavy = true;
       }
-      if (prop_here(v, p, s, lead) &&
-          v.prop_count[(uint64_t)p.prop_slot * v.G + g] != 0)
-        heavy = true;
+      if (prop_here(v, p, s, lead) && pc != 0) heavy = true;
     }
-  }
-  uint64_t bal[4];
-  bal[0] = __ballot(run && lead && heavy);
-  bal[1] = __ballot(run && lead && !heavy);
-  bal[2] = __ballot(run && !lead && heavy);
-  bal[3] = __ballot(run && !lead && !heavy);
-  __shared__ uint32_t c[4][4];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) {
+    uint64_t bal[4];
+    bal[0] = __ballot(run && lead && heavy);
+    bal[1] = __ballot(run && lead && !heavy);
+    bal[2] = __ballot(run && !lead && heavy);
+    bal[3] = __ballot(run && !lead && !heavy);
+    if (lane == 0) {
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const uint64_t row = ((uint64_t)(k >> 1) * v.R + s) * 2 + (k & 1);
-      v.act_mask[(row * nb + blockIdx.x) * 4 + wave] = bal[k];
-      c[k][wave] = (uint32_t)__popcll(bal[k]);
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t row = ((uint64_t)(k >> 1) * v.R + s) * 2 + (k & 1);
+        v.act_mask[(row * nb + blockIdx.x) * 4 + wave] = bal[k];
+        c[s][k][wave] = (uint32_t)__popcll(bal[k]);
+      }
     }
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
-    const uint32_t k = threadIdx.x;
+  if (threadIdx.x < 4 * R) {
+    const uint32_t s = threadIdx.x >> 2, k = threadIdx.x & 3;
     const uint64_t row = ((uint64_t)(k >> 1) * v.R + s) * 2 + (k & 1);
-    v.act_cnt[row * nb + blockIdx.x] = c[k][0] + c[k][1] + c[k][2] + c[k][3];
+    v.act_cnt[row * nb + blockIdx.x] =
+        c[s][k][0] + c[s][k][1] + c[s][k][2] + c[s][k][3];
   }
 }
 
@@ -2099,7 +2164,7 @@ static void launch_step(drb_engine *e, const RoundParams &p0,
   const unsigned gx = nblk ? nblk : gx_all;
   if (!st) st = e->stream;
   if (p0.listed) {
-    k_active_scan<R><<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v, p0);
+    k_active_scan<R><<<gx, 256, 0, e->stream>>>(e->v, p0);
     k_active_prefix<<<4 * e->v.R, 1024, 0, e->stream>>>(e->v, gx);
     k_active_scatter<<<dim3(gx, e->v.R), 256, 0, e->stream>>>(e->v);
   }
@@ -2143,9 +2208,11 @@ static void launch_step(drb_engine *e, const RoundParams &p0,
                     st == e->stream;
   if (lean) {
     // the lean kernels, then the full ones over the heavy and the
-    // escalated lanes, one stream.  (The heavy lanes' full launches on the
-    // second stream beside the lean kernels measured no faster: 2.02
-    // against 1.97 ms a C5 round, profiles/r06_lean.)
+    // escalated lanes, one stream.  Measured slower on two streams: the
+    // heavy lanes' full launches beside the lean kernels (2.02 against 1.97
+    // ms a C5 round), the two full launches side by side (1.92 against
+    // 1.90), the two lean ones (1.93), both pairs (1.96;
+    // profiles/r06_lean/c5_streams_ab.txt).
     if (split) {
       (void)hipEventRecord(e->ev_join, e->stream2);
       (void)hipStreamWaitEvent(st, e->ev_join, 0);

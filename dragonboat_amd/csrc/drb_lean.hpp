@@ -103,16 +103,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   uint64_t qsv[5] = {0, 0, 0, 0, 0}, tick_count = 0;
   uint64_t rmatch[R];
   uint32_t rstate[R], ractive[R];
+  // (meta, rec, rmatch and rstate of the lane's own slot are never loaded
+  // and never read: left undefined, so that the compiler merges the loaded
+  // and the skipped path without a copy -- a copy of a loaded register
+  // waits for the load, which split the follower's loads into two round
+  // trips)
 #pragma unroll
   for (int c = 0; c < 4; ++c) pkq[c] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-  for (int s = 0; s < R; ++s) {
-    meta[s] = make_uint4(0, 0, 0, 0);
-    rmatch[s] = 0;
-    rstate[s] = ractive[s] = 0;
-#pragma unroll
-    for (int j = 0; j < NREC; ++j) rec[s][j] = make_uint4(0, 0, 0, 0);
-  }
+  for (int s = 0; s < R; ++s) ractive[s] = 0;
   if (valid) {
     flags = v.u32[u32_ix(v, W_FLAGS, slot, g)];
     role = v.u32[u32_ix(v, W_ROLE, slot, g)];
@@ -209,9 +208,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int s = 0; s < R; ++s) {
         RemoteV x;
-        x.m = rmatch[s];
+        x.m = (uint32_t)s != slot ? rmatch[s] : 0;
         x.n = 0;
-        x.st = rstate[s];
+        x.st = (uint32_t)s != slot ? rstate[s] : 0;
         x.a = ractive[s];
         if ((uint32_t)s != slot &&
             (x.m != r.last || x.st != DRB_REMOTE_REPLICATE))

@@ -2301,6 +2301,25 @@ DRB_DEV bool prop_here(const View &v, const RoundParams &p, uint32_t slot,
 // without input: a quiesced tick only advances its tick counters
 // (node.tick node.go:1562-1579, raft.quiescedTick raft.go:650-656),
 // which the next round it runs applies at once (F_QS_BASE).
+// idle_round_of is the same rule over preloaded inputs -- the flags, the
+// slot's inbox tag word, the group's staged proposal count and ReadIndex
+// row (looked at only where prop_here / ri_here) -- which k_active_scan
+// loads all at once; idle_round loads them as the rule needs them.
+template <int R>
+DRB_DEV bool idle_round_of(const View &v, const RoundParams &p, uint32_t slot,
+                           bool lead, uint32_t flags, uint64_t tags,
+                           uint32_t pcount, uint4 ri) {
+  if (!(flags & F_AT_REST) || v.remote_mask) return false;
+  if (p.tick && !(v.quiesce && (flags & F_QUIESCED))) return false;
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if ((uint32_t)s != slot &&
+        tag_current((uint32_t)(tags >> (8 * s)) & 0xffu, p.round - 1))
+      return false;
+  if (prop_here(v, p, slot, lead) && pcount != 0) return false;
+  if (ri_here(v, p, slot, lead) && (ri.x | ri.y)) return false;
+  return true;
+}
 template <int R>
 DRB_DEV bool idle_round(const View &v, const RoundParams &p, uint32_t slot,
                         uint64_t g, bool lead, uint32_t flags) {

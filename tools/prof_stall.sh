@@ -12,4 +12,4 @@ P1="SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INS
 P2="SQ_WAVES,SQ_BUSY_CYCLES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_INSTS_LDS,SQ_WAIT_INST_LDS,GRBM_GUI_ACTIVE"
 tools/gpu_step.sh 300 $o/p1.log timeout -s KILL 280 rocprofv3 --pmc $P1 -d $o/p1 -o run --output-format csv -- $B || exit 1
 tools/gpu_step.sh 300 $o/p2.log timeout -s KILL 280 rocprofv3 --pmc $P2 -d $o/p2 -o run --output-format csv -- $B || exit 1
-python tools/stall_summary.py $o/stall.json $o/p1 $o/p2 --last 20 --workload "C3 steady state (bench.py defaults), timed rounds" > $o/stall.txt
+python tools/stall_summary.py $o/stall.json $o/p1 $o/p2 --last 20 --workload "${WL:-C3 steady state (bench.py defaults), timed rounds}" > $o/stall.txt
