@@ -176,6 +176,12 @@ def parse():
                          "the placement) stepped together, their planes "
                          "moved by drb_exchange_local (the device pull, no "
                          "host synchronisation)")
+    ap.add_argument("--local-exchange", choices=("bind", "pull"),
+                    default="bind",
+                    help="--local-ranks: bind = the engines read remote "
+                         "planes in the senders' outboxes (drb_exchange_"
+                         "local_bind, zero-copy); pull = the device pull "
+                         "copies them into the receivers' inbound planes")
     ap.add_argument("--host-staged", type=int, default=-1,
                     help="after the timed region, also time rounds whose "
                          "proposals come from host memory through "
@@ -330,6 +336,9 @@ def run_c4_local(args):
             for r in range(N)]
     for e in engs:
         e.init_steady(term=2, leader_slot=0, seed=seed)
+    bind = args.local_exchange == "bind"
+    if bind:
+        Engine.exchange_local_bind(engs)
 
     def rnd(i, b, tick):
         for e in engs:
@@ -378,13 +387,17 @@ def run_c4_local(args):
                         "every %d round(s)" % (G, R, N, k, te),
             "local_ranks": N, "groups_per_rank": lanes, "replicas": R,
             "parallelism": "replicas spread over %d engines of one process "
-                           "on one GPU; drb_exchange_local (device pull)" % N},
+                           "on one GPU; drb_exchange_local (%s)" % (
+                               N, "zero-copy: bound engines read the senders' "
+                               "outboxes" if bind else "device pull")},
         "exchange": {
             "bytes_per_round": sum(xb) / K,
             "bytes_per_round_per_rank": sum(xb) / K / N,
+            "mode": args.local_exchange,
             "note": "inbound plane bytes the pull kernels moved (headers of "
                     "the round, counted records, entry rows), "
-                    "drb_exchange_bytes"},
+                    "drb_exchange_bytes; 0 when bound: the step kernels "
+                    "read the senders' outbox planes in place"},
         "roofline": {"bound": "hbm", "alg_bytes_per_round": alg,
                      "achieved": alg / (el / K) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s",
@@ -776,6 +789,8 @@ def main():
     out = eng.read_counters(reset=True)
     if phase_dbg:  # cycles per stepped lane of each round phase
         for role, x in eng.debug_phase(reset=True).items():
+            print("phase raw %s per round: %s" % (
+                role, " ".join("%.0f" % (c / K) for c in x)), file=sys.stderr)
             if x[0]:
                 print("phase %s lanes %d: %s" % (
                     role, x[0] // K, " ".join("%.0f" % (c / x[0])

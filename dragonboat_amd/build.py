@@ -25,6 +25,8 @@ ARCH = "gfx950"
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
          "-Wno-pass-failed"]
 NUM_KINDS = 9
+# the LOCAL kinds 9-12 (drb_launch.hpp), for these R only
+LOCAL_KINDS, LOCAL_R = (9, 10, 11, 12), (3, 5)
 # the headers a step-kernel instantiation includes
 STEP_DEPS = ["drb_step_inst.hip", "drb_step.hpp", "drb_lean.hpp",
              "drb_launch.hpp",
@@ -54,7 +56,8 @@ def _units(defines):
              ("tan_select.o", "drb_tan_inst.hip", ["DRB_TAN_KERNELS=1"],
               tan_deps)]
     for r in range(1, 9):
-        for k in range(NUM_KINDS):
+        for k in list(range(NUM_KINDS)) + \
+                (list(LOCAL_KINDS) if r in LOCAL_R else []):
             units.append(("step_r%d_k%d.o" % (r, k), "drb_step_inst.hip",
                           ["DRB_INST_R=%d" % r, "DRB_INST_KIND=%d" % k],
                           step_deps))

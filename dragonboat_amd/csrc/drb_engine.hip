@@ -52,6 +52,10 @@ struct drb_engine {
   uint64_t *sess_client = nullptr;
   // the lean kernel of listed rounds off (drb_config.no_lean: A/B only)
   bool no_lean = false;
+  // drb_exchange_local_bind: the engines of the group, this one included,
+  // and per rank their outbox planes (host copy; v.peers the device one)
+  std::vector<drb_engine *> bound;
+  std::vector<PeerPlanes> peers_host;
   hipEvent_t ev_staged;           // upload done -> layout kernel
   hipEvent_t ev_stage_free;       // layout kernel done -> next upload
   hipEvent_t ev_uploaded;         // packed upload done -> host arrays free
@@ -523,6 +527,15 @@ extern "C" int drb_engine_destroy(drb_engine *e) {
   if (!e) return DRB_EINVAL;
   (void)hipStreamSynchronize(e->stream);
   (void)hipStreamSynchronize(e->stream2);
+  // bound peers read this engine's outbox planes: their work drains first,
+  // and their later rounds fail (their remote planes are gone)
+  for (drb_engine *o : e->bound) {
+    if (o == e) continue;
+    (void)hipStreamSynchronize(o->stream);
+    o->failed = DRB_EINVAL;
+    o->bound.erase(std::remove(o->bound.begin(), o->bound.end(), e),
+                   o->bound.end());
+  }
   for (void *p : e->allocs) (void)hipFree(p);
   if (e->scratch) (void)hipFree(e->scratch);
   if (e->stage_buf) (void)hipFree(e->stage_buf);
@@ -1666,6 +1679,9 @@ extern "C" int drb_ingest_ex(drb_engine *e, const drb_message *msgs, size_t n,
                              uint8_t *status, uint64_t *accepted,
                              uint64_t *dropped, uint64_t *diverted) {
   if (!e || (n && !msgs)) return DRB_EINVAL;
+  // a bound engine's remote planes are its peers' outboxes
+  // (drb_exchange_local_bind): nothing is delivered into them
+  if (!e->bound.empty()) return DRB_EINVAL;
   const View &v = e->v;
   std::lock_guard<std::mutex> lock(e->ingest_mu);
   // replicas spread over ranks: not between a round and its exchange
@@ -2187,8 +2203,15 @@ static void launch_step(drb_engine *e, const RoundParams &p0,
   // forwarded proposals and member kinds: the EXT kernels with the Propose
   // and nonVoting / witness paths
   const bool fwd = e->v.fwd_props || e->v.nv_mask || e->v.wt_mask;
-  const int kl = fwd ? SK_LEAD_FWD : ext ? SK_LEAD_EXT : SK_LEAD;
-  const int kf = fwd ? SK_FOLLOW_FWD : ext ? SK_FOLLOW_EXT : SK_FOLLOW;
+  // without placement (no remote planes) the LOCAL instantiations, which
+  // compile the remote-plane paths out (drb_launch.hpp)
+  const bool local = !e->v.remote_mask;
+  const int kl = fwd ? SK_LEAD_FWD
+                 : ext ? (local ? SK_LEAD_EXT_LOCAL : SK_LEAD_EXT)
+                       : (local ? SK_LEAD_LOCAL : SK_LEAD);
+  const int kf = fwd ? SK_FOLLOW_FWD
+                 : ext ? (local ? SK_FOLLOW_EXT_LOCAL : SK_FOLLOW_EXT)
+                       : (local ? SK_FOLLOW_LOCAL : SK_FOLLOW);
   // a small round (C2: 64k groups, 768 workgroups, one wave per SIMD) runs
   // its two launches side by side on the engine's two streams: they touch
   // disjoint state, and neither fills the chip alone
@@ -2202,7 +2225,7 @@ static void launch_step(drb_engine *e, const RoundParams &p0,
   // listed rounds of a plain EXT engine: the light lanes' heartbeat rounds
   // through the lean kernel first (drb_lean.hpp), the full kernel then
   // over the heavy lanes and the ones the lean kernel escalated
-  const bool lean = p0.listed && ext && kl == SK_LEAD_EXT && !nblk &&
+  const bool lean = p0.listed && ext && !fwd && !nblk &&
                     !e->v.elections && !e->v.remote_mask &&
                     !e->v.save_tan && !e->v.save_batched && !e->no_lean &&
                     st == e->stream;
@@ -2719,6 +2742,24 @@ extern "C" int drb_step_round(drb_engine *e, const drb_round_in *in,
 }
 
 // ---------------------------------------------------------------- outputs
+// a remote plane's arrays as the step reads them (drb_step.hpp in_mbox &
+// co.): the inbound copies, or a bound engine's sender outbox
+struct InPlanes {
+  uint4 *mbox, *meta, *embox;
+  uint64_t *maxapp, *elo, *rterm;
+};
+static InPlanes in_planes(const drb_engine *e, uint32_t from, uint32_t to) {
+  const View &v = e->v;
+  if (v.peers && !e->peers_host.empty()) {
+    const PeerPlanes &p = e->peers_host[plane_sender(v, from, to)];
+    return {const_cast<uint4 *>(p.mbox), const_cast<uint4 *>(p.meta),
+            const_cast<uint4 *>(p.embox), const_cast<uint64_t *>(p.maxapp),
+            const_cast<uint64_t *>(p.elo), const_cast<uint64_t *>(p.rterm)};
+  }
+  return {v.mbox_in, v.meta_in, v.embox_in, v.maxapp_in, v.elo_in,
+          v.rterm_in};
+}
+
 // entries [lo, hi] of a remote plane's entry rows (their first index elo),
 // as drb_export_log writes them
 static int export_entry_rows(drb_engine *e, uint32_t buf, uint64_t g,
@@ -2733,7 +2774,7 @@ static int export_entry_rows(drb_engine *e, uint32_t buf, uint64_t g,
     for (uint32_t c = 0; c < ENT_META + v.C16; ++c)
       idx.push_back(embox_ix(v, buf, from, to, (uint32_t)(i - elo), c, g));
   std::vector<uint4> val;
-  if (gather(e, v.embox_in, idx, val)) return DRB_EDEVICE;
+  if (gather(e, in_planes(e, from, to).embox, idx, val)) return DRB_EDEVICE;
   size_t used = 0, k = 0;
   for (uint64_t i = lo; i <= hi; ++i, ++k) {
     const uint4 *c = &val[k * (ENT_META + v.C16)];
@@ -2766,8 +2807,9 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
                        uint4 meta, uint64_t tag, bool remote = false) {
   const View &v = e->v;
   const bool cur = tag_is(meta.x, tag);
-  uint4 *const mbox = remote ? v.mbox_in : v.mbox;
-  uint64_t *const rterm = remote ? v.rterm_in : v.rterm;
+  const InPlanes ip = in_planes(e, from, to);
+  uint4 *const mbox = remote ? ip.mbox : v.mbox;
+  uint64_t *const rterm = remote ? ip.rterm : v.rterm;
   const uint32_t k = cur ? mi_count(meta.y) : 0;
   if (cur && (meta.x & MQ_QUIESCE)) {  // sendEnterQuiesceMessages
     if (*nm >= cap) return DRB_ERANGE;
@@ -2794,7 +2836,7 @@ static int export_pair(drb_engine *e, uint32_t buf, uint64_t g,
   uint64_t elo = 0;  // remote: the entry rows' first index
   if (remote && mi_nrep(meta.y)) {
     std::vector<uint64_t> li{mmeta_ix(v, buf, from, to, g)}, lv;
-    if (gather(e, v.elo_in, li, lv)) return DRB_EDEVICE;
+    if (gather(e, ip.elo, li, lv)) return DRB_EDEVICE;
     elo = lv[0];
   }
   uint64_t prev_lo = 0, prev_hi = 0;
@@ -2933,7 +2975,7 @@ extern "C" int drb_export_inbox(drb_engine *e, uint64_t group, uint32_t slot,
       const bool rm = pair_remote(v, from, slot);
       std::vector<uint64_t> mi{mmeta_ix(v, buf, from, slot, group)};
       std::vector<uint4> meta;
-      if (gather(e, rm ? v.meta_in : v.mbox_meta, mi, meta))
+      if (gather(e, rm ? in_planes(e, from, slot).meta : v.mbox_meta, mi, meta))
         return DRB_EDEVICE;
       int rc = export_pair(e, buf, group, from, slot, out, cap, &nm, ents,
                            ent_cap, &ne, pool, pool_cap, &np, meta[0], tag, rm);
@@ -3049,6 +3091,7 @@ extern "C" int drb_plane_peer(const drb_engine *e, uint32_t from, uint32_t to,
 extern "C" int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
                                  uint32_t word, int dir, drb_region *out) {
   if (!e || !out || from >= e->v.R || to >= e->v.R) return DRB_EINVAL;
+  if (dir && !e->bound.empty()) return DRB_EINVAL;  // (drb_ingest_ex)
   const View &v = e->v;
   if (!pair_remote(v, from, to) || e->round == 0) return 0;
   const uint32_t buf = (uint32_t)(e->round & 1);  // the last round's outbox
@@ -3296,6 +3339,68 @@ static int exchange_pull(drb_engine *const *engines, uint32_t n) {
   return DRB_OK;
 }
 
+// ---- the zero-copy exchange of one process's engines on one GPU
+// Bound engines read each remote plane straight from the sender rank's
+// outbox (View.peers, drb_step.hpp in_mbox & co.); drb_exchange_local then
+// only orders the rounds: every engine's next round waits for every
+// engine's last one, so a round reads its senders' finished outboxes and a
+// sender overwrites an outbox buffer (two rounds later) only after its
+// receivers read it.
+static bool any_bound(drb_engine *const *engines, uint32_t n) {
+  for (uint32_t r = 0; r < n; ++r)
+    if (!engines[r]->bound.empty()) return true;
+  return false;
+}
+static bool is_bound(drb_engine *const *engines, uint32_t n) {
+  for (uint32_t r = 0; r < n; ++r)
+    if (engines[r]->bound.size() != n || engines[r]->bound[r] != engines[r] ||
+        engines[r]->bound != engines[0]->bound)
+      return false;
+  return n > 0;
+}
+static void exchange_barrier(drb_engine *const *engines, uint32_t n) {
+  for (uint32_t r = 0; r < n; ++r)
+    (void)hipEventRecord(engines[r]->ev_xsend, engines[r]->stream);
+  for (uint32_t d = 0; d < n; ++d)
+    for (uint32_t r = 0; r < n; ++r)
+      if (r != d)
+        (void)hipStreamWaitEvent(engines[d]->stream, engines[r]->ev_xsend, 0);
+}
+
+extern "C" int drb_exchange_local_bind(drb_engine *const *engines,
+                                       uint32_t n) {
+  if (int rc = exchange_check(engines, n)) return rc;
+  if (n < 2 || !pull_ok(engines, n) || any_bound(engines, n))
+    return DRB_EINVAL;
+  for (uint32_t r = 0; r < n; ++r)
+    if (engines[r]->v.place_world != n || engines[r]->v.place_rank != r)
+      return DRB_EINVAL;  // (engines[r] is rank r of the placement)
+  std::vector<PeerPlanes> src(n);
+  for (uint32_t r = 0; r < n; ++r) {
+    const View &v = engines[r]->v;
+    src[r] = {v.mbox, v.mbox_meta, v.embox, v.mbox_maxapp, v.elo, v.rterm};
+  }
+  std::vector<drb_engine *> group(engines, engines + n);
+  for (uint32_t r = 0; r < n; ++r) {
+    drb_engine *e = engines[r];
+    HIPCHK(hipSetDevice(e->cfg.device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    PeerPlanes *d = nullptr;
+    if (dalloc(e, &d, n)) return DRB_ENOMEM;
+    HIPCHK(hipMemcpyAsync(d, src.data(), n * sizeof(PeerPlanes),
+                          hipMemcpyHostToDevice, e->stream));
+    e->v.peers = d;
+    HIPCHK(hipMemcpyAsync(e->dview, &e->v, sizeof(View),
+                          hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  for (uint32_t r = 0; r < n; ++r) {
+    engines[r]->bound = group;
+    engines[r]->peers_host = src;
+  }
+  return DRB_OK;
+}
+
 extern "C" int drb_exchange_bytes(drb_engine *e, uint64_t *bytes, int reset) {
   if (!e || !bytes) return DRB_EINVAL;
   unsigned long long b = 0;
@@ -3315,6 +3420,14 @@ extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
   const View &v = engines[0]->v;
   const uint32_t R = v.R;
   ExchangeLocks locks(engines, n);
+  if (is_bound(engines, n)) {  // zero-copy: the rounds' order alone
+    if (engines[0]->round == 0) return DRB_OK;
+    exchange_barrier(engines, n);
+    for (uint32_t r = 0; r < n; ++r)
+      engines[r]->exchanged_round = engines[r]->round;
+    return DRB_OK;
+  }
+  if (any_bound(engines, n)) return DRB_EINVAL;  // (not the bound group)
   if (pull_ok(engines, n)) {  // one GPU: counted, on the device
     if (engines[0]->round == 0) return DRB_OK;
     if (int rc = exchange_pull(engines, n)) return rc;
@@ -3355,6 +3468,7 @@ extern "C" int drb_exchange_local(drb_engine *const *engines, uint32_t n) {
 extern "C" int drb_exchange_local_counted(drb_engine *const *engines,
                                           uint32_t n) {
   if (int rc = exchange_check(engines, n)) return rc;
+  if (any_bound(engines, n)) return DRB_EINVAL;
   const uint32_t R = engines[0]->v.R;
   ExchangeLocks locks(engines, n);
   std::vector<std::vector<uint32_t>> words(n, std::vector<uint32_t>(R * R));

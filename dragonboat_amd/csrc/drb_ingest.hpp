@@ -838,6 +838,7 @@ extern "C" int drb_ingest_wire(drb_engine *e, const uint8_t *stream,
                                drb_wire_in *out) {
   using namespace drb;
   if (!e || (!stream && len)) return DRB_EINVAL;
+  if (!e->bound.empty()) return DRB_EINVAL;  // (drb_ingest_ex)
   wirehost::crc_init();
   std::lock_guard<std::mutex> lock(e->ingest_mu);
   // replicas spread over ranks: not between a round and its exchange

@@ -22,6 +22,13 @@ enum StepKind : int {
   SK_LEAD_LEAN = 7,   // lean_kernel<R, true>: a listed round's heartbeat-
                       //   only leaders (drb_lean.hpp)
   SK_FOLLOW_LEAN = 8,  // lean_kernel<R, false>
+  // the LOCAL instantiations of kinds 0-3 (no remote planes compiled in:
+  // engines without placement, View.remote_mask 0), built for R = 3 and 5;
+  // other R run the kinds they stand for
+  SK_LEAD_LOCAL = 9,
+  SK_FOLLOW_LOCAL = 10,
+  SK_LEAD_EXT_LOCAL = 11,
+  SK_FOLLOW_EXT_LOCAL = 12,
   NUM_STEP_KINDS
 };
 
@@ -52,6 +59,13 @@ DRB_DECLARE_STEP_LAUNCH_R(5)
 DRB_DECLARE_STEP_LAUNCH_R(6)
 DRB_DECLARE_STEP_LAUNCH_R(7)
 DRB_DECLARE_STEP_LAUNCH_R(8)
+#define DRB_DECLARE_STEP_LAUNCH_LOCAL(R)                                  \
+  DRB_DECLARE_STEP_LAUNCH(R, 9)                                           \
+  DRB_DECLARE_STEP_LAUNCH(R, 10)                                          \
+  DRB_DECLARE_STEP_LAUNCH(R, 11)                                          \
+  DRB_DECLARE_STEP_LAUNCH(R, 12)
+DRB_DECLARE_STEP_LAUNCH_LOCAL(3)
+DRB_DECLARE_STEP_LAUNCH_LOCAL(5)
 
 // the tan record kernels (drb_tan.hpp), compiled in drb_tan_inst.hip
 void tan_launch_select(const View &v, uint32_t round, uint64_t max_log,
@@ -70,11 +84,22 @@ void tan_launch_write(const View &v, uint32_t round, uint64_t max_log,
    DRB_STEP_LAUNCH_NAME(R, 2), DRB_STEP_LAUNCH_NAME(R, 3),                \
    DRB_STEP_LAUNCH_NAME(R, 4), DRB_STEP_LAUNCH_NAME(R, 5),                \
    DRB_STEP_LAUNCH_NAME(R, 6), DRB_STEP_LAUNCH_NAME(R, 7),                \
-   DRB_STEP_LAUNCH_NAME(R, 8)}
+   DRB_STEP_LAUNCH_NAME(R, 8), DRB_STEP_LAUNCH_NAME(R, 0),                \
+   DRB_STEP_LAUNCH_NAME(R, 2), DRB_STEP_LAUNCH_NAME(R, 1),                \
+   DRB_STEP_LAUNCH_NAME(R, 3)}
+#define DRB_STEP_LAUNCH_ROW_LOCAL(R)                                      \
+  {DRB_STEP_LAUNCH_NAME(R, 0), DRB_STEP_LAUNCH_NAME(R, 1),                \
+   DRB_STEP_LAUNCH_NAME(R, 2), DRB_STEP_LAUNCH_NAME(R, 3),                \
+   DRB_STEP_LAUNCH_NAME(R, 4), DRB_STEP_LAUNCH_NAME(R, 5),                \
+   DRB_STEP_LAUNCH_NAME(R, 6), DRB_STEP_LAUNCH_NAME(R, 7),                \
+   DRB_STEP_LAUNCH_NAME(R, 8), DRB_STEP_LAUNCH_NAME(R, 9),                \
+   DRB_STEP_LAUNCH_NAME(R, 10), DRB_STEP_LAUNCH_NAME(R, 11),              \
+   DRB_STEP_LAUNCH_NAME(R, 12)}
 static const StepLaunchFn kStepLaunch[8][NUM_STEP_KINDS] = {
-    DRB_STEP_LAUNCH_ROW(1), DRB_STEP_LAUNCH_ROW(2), DRB_STEP_LAUNCH_ROW(3),
-    DRB_STEP_LAUNCH_ROW(4), DRB_STEP_LAUNCH_ROW(5), DRB_STEP_LAUNCH_ROW(6),
-    DRB_STEP_LAUNCH_ROW(7), DRB_STEP_LAUNCH_ROW(8)};
+    DRB_STEP_LAUNCH_ROW(1),       DRB_STEP_LAUNCH_ROW(2),
+    DRB_STEP_LAUNCH_ROW_LOCAL(3), DRB_STEP_LAUNCH_ROW(4),
+    DRB_STEP_LAUNCH_ROW_LOCAL(5), DRB_STEP_LAUNCH_ROW(6),
+    DRB_STEP_LAUNCH_ROW(7),       DRB_STEP_LAUNCH_ROW(8)};
 #endif
 
 }  // namespace drb

@@ -286,6 +286,12 @@ __host__ __device__ inline uint32_t prop_fast(uint32_t type, uint64_t client_id,
 }
 constexpr int RTR_CAP = 8;  // ReadyToRead records per replica per round
 
+// one engine's outbox planes (drb_exchange_local_bind; the device pull)
+struct PeerPlanes {
+  const uint4 *mbox, *meta, *embox;
+  const uint64_t *maxapp, *elo, *rterm;
+};
+
 struct View {
   uint64_t G;      // groups
   uint32_t R;      // replicas
@@ -414,6 +420,10 @@ struct View {
   // rterm)
   uint32_t *xslow;
   uint64_t *rterm_in;
+  // engines of one process on one device bound for the zero-copy exchange
+  // (drb_exchange_local_bind): per rank its outbox planes, from which the
+  // step kernels read their remote planes in place of the *_in copies
+  const struct PeerPlanes *peers;
   unsigned long long *counters;  // [8] (drb_round_out order from index 1)
   // flagged-replica list (drb_take_flagged): {g lo, g hi, slot | reason
   // << 8 | flags << 16, round}, appended with one atomic per marked lane
@@ -495,6 +505,14 @@ __host__ __device__ inline uint64_t embox_ix(const View &v, uint32_t buf,
 __host__ __device__ inline bool pair_remote(const View &v, uint32_t from,
                                             uint32_t to) {
   return (v.remote_mask >> (from * v.R + to)) & 1ull;
+}
+// the rank whose outbox holds this rank's inbound plane (from, to): slot s
+// of group g lives on rank (g + s) mod N at lane g / N, so every lane of
+// the plane comes from one rank, at the same lane (drb_place_peer, dir 1)
+__host__ __device__ inline uint32_t plane_sender(const View &v,
+                                                 uint32_t from, uint32_t to) {
+  const uint32_t N = v.place_world, d = (to % N + N - from % N) % N;
+  return (v.place_rank + N - d) % N;
 }
 // the global group of replica slot s at lane g (include/drb_engine.h)
 __host__ __device__ inline uint64_t rterm_ix(const View &v, uint32_t buf,

@@ -44,9 +44,13 @@
 
 namespace drb {
 
-// waves per SIMD: the follower at 5 up to R = 3 (96 VGPRs, 4 spilled; at
-// R = 5 five waves would spill 149), the leader at 4 (113 VGPRs), where
-// the full EXT kernels spill 37 / 25 VGPRs at 4 / 3 waves
+// waves per SIMD: the follower at 5 up to R = 3 (85 VGPRs, no spills; 6
+// waves would spill 20, and at R = 5 five would spill 149), the leader at
+// 4 (101 VGPRs; 5 would spill 24), where the full EXT kernels spill
+// 37 / 25 VGPRs at 4 / 3 waves
+#ifndef DRB_LEAN_WHY
+#define DRB_LEAN_WHY 0
+#endif
 #ifndef DRB_LEAN_WAVES
 #define DRB_LEAN_WAVES 4
 #endif
@@ -84,6 +88,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   L.slow = false;
   L.dirty = DRB_REM_DIRTY;
   L.members = false;
+  L.peers = false;  // (lean rounds: no remote planes)
   uint32_t c_msgs = 0, c_stepped = 0;
   bool esc = false;  // escalated to the full kernel
   // records per sender a heartbeat round holds: the tick's Heartbeat, or
@@ -204,6 +209,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
               r.ri_count == 0 && !(flags & (F_XFER | F_XFER_REQ)) &&
               (LEAD || role == DRB_FOLLOWER) && pcount == 0 &&
               !(riq.x | riq.y | riq.z | riq.w);
+#if DRB_LEAN_WHY
+    uint32_t why = 0;  // (timing variant: why a lane escalates)
+    if (r.committed != r.last) why |= 2u;
+    if (r.processed != r.last || r.saved_to != r.last ||
+        r.sm_index != r.last || r.applied_index != r.last)
+      why |= 4u;
+    if (r.marker <= r.last) why |= 8u;
+    if (r.ri_count || (flags & (F_XFER | F_XFER_REQ)) ||
+        !(LEAD || role == DRB_FOLLOWER) || pcount || (riq.x | riq.y | riq.z | riq.w))
+      why |= 16u;
+#define DRB_WHY(b) why |= (b)
+#else
+#define DRB_WHY(b) (void)0
+#endif
     if (LEAD) {  // the remotes: match, state, active (next is not needed)
 #pragma unroll
       for (int s = 0; s < R; ++s) {
@@ -213,8 +232,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         x.st = (uint32_t)s != slot ? rstate[s] : 0;
         x.a = ractive[s];
         if ((uint32_t)s != slot &&
-            (x.m != r.last || x.st != DRB_REMOTE_REPLICATE))
+            (x.m != r.last || x.st != DRB_REMOTE_REPLICATE)) {
           ok = false;
+          DRB_WHY(32u);
+        }
         rem_put<R>(L, s, x);
       }
       rl.dirty[L.tid] = 0;
@@ -249,8 +270,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
           (info & (MI_PROP | MI_REJECT | MI_TERM_OTHER |
                    (LEAD ? MI_OFF_LEADER : MI_OFF_FOLLOWER))) ||
           ((info & MI_TERM) && hi64(meta[s]) != r.term) ||
-          ns > (uint32_t)NREC || (!LEAD && (uint64_t)s + 1 != r.leader_id))
+          ns > (uint32_t)NREC || (!LEAD && (uint64_t)s + 1 != r.leader_id)) {
         ok = false;
+        DRB_WHY(64u);
+      }
       if (info & MI_RESP) resp_from |= 1u << s;
       total_in += ns;
       nrec[s] = ns < (uint32_t)NREC ? ns : (uint32_t)NREC;
@@ -262,11 +285,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
           // that repeats the last ctx as well)
           const uint32_t t = c0.x & 0xffu;
           if ((c0.x & (MF_HAS_C1 | MF_HINT_PREV | MF_TERM_OTHER)) ||
-              t != (LEAD ? DRB_MSG_HEARTBEAT_RESP : DRB_MSG_HEARTBEAT))
+              t != (LEAD ? DRB_MSG_HEARTBEAT_RESP : DRB_MSG_HEARTBEAT)) {
             ok = false;
+            DRB_WHY(128u);
+          }
           // HeartbeatResp: a = Hint; Heartbeat: a = Commit
-          if (LEAD ? (hi64(c0) != 0 || c0.y != 0) : hi64(c0) > r.committed)
+          if (LEAD ? (hi64(c0) != 0 || c0.y != 0) : hi64(c0) > r.committed) {
             ok = false;
+            DRB_WHY(128u);
+          }
         }
     }
     // the tick: no election timeout (follower), the CheckQuorum quorum
@@ -282,13 +309,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             if ((uint32_t)s != slot &&
                 (rl.a[s][L.tid] || ((resp_from >> s) & 1)))
               c++;
-          if (c < (uint32_t)(R / 2 + 1)) ok = false;
+          if (c < (uint32_t)(R / 2 + 1)) {
+            ok = false;
+            DRB_WHY(16u);
+          }
         }
       } else {
         const uint64_t et = (total_in ? 0 : r.election_tick) + 1;
-        if (et >= ld_f(L, r, F_RAND_TIMEOUT)) ok = false;
+        if (et >= ld_f(L, r, F_RAND_TIMEOUT)) {
+          ok = false;
+          DRB_WHY(16u);
+        }
       }
     }
+#undef DRB_WHY
+#if DRB_LEAN_WHY
+    if (!ok && v.phase) {  // per wave: one atomic per reason
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t m = __ballot(b ? ((why >> b) & 1u) : 1u);
+        if ((threadIdx.x & 63) == __builtin_ctzll(m) && m)
+          atomicAdd(&v.phase[(LEAD ? 8 : 0) + b],
+                    (unsigned long long)__popcll(m));
+      }
+    }
+#endif
     if (!ok) {
       esc = true;  // the full step kernel takes it, untouched (below)
     } else {

@@ -123,6 +123,7 @@ static int xcomm_check(const drb_engine *e, ncclComm_t c) {
 
 extern "C" int drb_exchange_rccl_counted(drb_engine *e, void *comm) {
   if (!e || !comm) return DRB_EINVAL;
+  if (!e->bound.empty()) return DRB_EINVAL;  // (drb_exchange_local_bind)
   if (e->v.place_world < 2) return drb_exchange_mark(e);
   ncclComm_t c = (ncclComm_t)comm;
   if (int rc = xcomm_check(e, c)) return rc;
@@ -154,6 +155,7 @@ extern "C" int drb_exchange_rccl_counted(drb_engine *e, void *comm) {
 extern "C" int drb_exchange_rccl(drb_engine *e, void *comm,
                                  uint32_t leader_mask) {
   if (!e || !comm) return DRB_EINVAL;
+  if (!e->bound.empty()) return DRB_EINVAL;  // (drb_exchange_local_bind)
   if (e->v.place_world < 2) return drb_exchange_mark(e);
   ncclComm_t c = (ncclComm_t)comm;
   if (int rc = xcomm_check(e, c)) return rc;

@@ -85,6 +85,10 @@ namespace drb {
 #endif
 // timing only: per-phase cycle sums of the leader / follower lanes
 // (View.phase, drb_debug_phase); 0 in shipped builds
+// the zero-copy exchange's reads (in_mbox & co.; 0: timing variant only)
+#ifndef DRB_PEERS
+#define DRB_PEERS 1
+#endif
 #ifndef DRB_PHASE_PROF
 #define DRB_PHASE_PROF 0
 #endif
@@ -189,6 +193,11 @@ struct Lane {
   // by the FWD instantiations (and the raft launch) only; the C3 and C5
   // kernels compile them out
   bool members = false;
+  // remote planes may be read in bound peers' outboxes (View.peers,
+  // drb_exchange_local_bind): off in the LOCAL instantiations (engines
+  // without placement), which compile that path out -- it costs the C3
+  // kernels ~1-2 % in registers (profiles/r06_bind)
+  bool peers = true;
 };
 
 // ------------------------------------------------------------ helpers
@@ -540,6 +549,39 @@ DRB_DEV bool rem_try_update(const Lane &L, int s, uint64_t index) {
   return u;
 }
 
+// A remote plane (pair_remote) as the step reads it: the inbound copy the
+// exchange wrote, or -- engines bound for the zero-copy exchange
+// (View.peers) -- the sender rank's outbox itself
+DRB_DEV const PeerPlanes *in_peer(const Lane &L, uint32_t from, uint32_t to) {
+  const View &v = *L.v;
+  return DRB_PEERS && L.peers && v.peers ? &v.peers[plane_sender(v, from, to)]
+                                         : nullptr;
+}
+DRB_DEV const uint4 *in_mbox(const Lane &L, uint32_t from, uint32_t to) {
+  const PeerPlanes *q = in_peer(L, from, to);
+  return q ? q->mbox : L.v->mbox_in;
+}
+DRB_DEV const uint4 *in_meta(const Lane &L, uint32_t from, uint32_t to) {
+  const PeerPlanes *q = in_peer(L, from, to);
+  return q ? q->meta : L.v->meta_in;
+}
+DRB_DEV const uint4 *in_embox(const Lane &L, uint32_t from, uint32_t to) {
+  const PeerPlanes *q = in_peer(L, from, to);
+  return q ? q->embox : L.v->embox_in;
+}
+DRB_DEV const uint64_t *in_maxapp(const Lane &L, uint32_t from, uint32_t to) {
+  const PeerPlanes *q = in_peer(L, from, to);
+  return q ? q->maxapp : L.v->maxapp_in;
+}
+DRB_DEV const uint64_t *in_elo(const Lane &L, uint32_t from, uint32_t to) {
+  const PeerPlanes *q = in_peer(L, from, to);
+  return q ? q->elo : L.v->elo_in;
+}
+DRB_DEV const uint64_t *in_rterm(const Lane &L, uint32_t from, uint32_t to) {
+  const PeerPlanes *q = in_peer(L, from, to);
+  return q ? q->rterm : L.v->rterm_in;
+}
+
 // ------------------------------------------------------------ log
 // commitTo (logentry.go:336-349)
 // The lowest next the round's ReplicateResps from remote s can leave it
@@ -553,9 +595,9 @@ DRB_DEV uint64_t resp_floor(const Lane &L, const RemoteV &x, int s,
                             uint32_t ns) {
   const View &v = *L.v;
   const bool rm = pair_remote(v, s, L.slot);
-  const uint4 *mb = rm ? v.mbox_in : v.mbox;
+  const uint4 *mb = rm ? in_mbox(L, s, L.slot) : v.mbox;
   const uint32_t nrp = mi_nrep(
-      (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(v, L.rbuf, s, L.slot, L.g)].y);
+      (rm ? in_meta(L, s, L.slot) : v.mbox_meta)[mmeta_ix(v, L.rbuf, s, L.slot, L.g)].y);
   uint64_t f = x.n;
   for (uint32_t j = nrp; j < ns; ++j) {
     const uint32_t k = rec_pos(false, j - nrp, v.MB);
@@ -962,8 +1004,8 @@ DRB_DEV uint4 ent_chunk(const Lane &L, const EntSrc &src, uint32_t s,
                         uint64_t idx, uint32_t c) {
   const View &v = *L.v;
   if (src.remote)
-    return v.embox_in[embox_ix(v, L.rbuf, s, L.slot, (uint32_t)(idx - src.lo),
-                               c, L.g)];
+    return in_embox(L, s, L.slot)[embox_ix(
+        v, L.rbuf, s, L.slot, (uint32_t)(idx - src.lo), c, L.g)];
   return v.ring[ring_ix(v, s, idx, c, L.g)];
 }
 
@@ -2451,7 +2493,8 @@ DRB_DEV void block_plane_summary(const View &v, BlockPos bp, uint32_t from,
 // machine (el_*, above) as well, whatever their role.
 // FWD: forwarded proposals (drb_config.forward_proposals; an EXT
 // instantiation of its own, so C5's EXT kernels keep their registers)
-template <int R, bool LEAD, bool EXT, bool SLOW = false, bool FWD = false>
+template <int R, bool LEAD, bool EXT, bool SLOW = false, bool FWD = false,
+          bool LOCAL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_SLOW_WAVES : LEAD ? (EXT ? DRB_EXT_LEAD_WAVES : DRB_LEAD_WAVES) : DRB_FOLLOW_WAVES))) void step_kernel(const View v,
                                                    RoundParams p) {
   // the View is a by-value kernel argument: its fields are wave-uniform
@@ -2559,6 +2602,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
   L.slow = SLOW;
   L.dirty = EXT && DRB_REM_DIRTY;
   L.members = FWD;
+  L.peers = !LOCAL;
   uint32_t c_commit = 0, c_applied = 0, c_fb = 0, c_err = 0, c_msgs = 0;
   uint32_t c_rtr = 0, c_drop = 0;
   uint32_t c_served = 0, c_deferred = 0, c_saved = 0, c_saved_bytes = 0;
@@ -2670,7 +2714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
     for (int s = 0; s < R; ++s) {
       if ((uint32_t)s == slot) continue;
       const bool rm = pair_remote(v, s, slot);
-      const uint4 meta = (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(v, L.rbuf, s,
+      const uint4 meta = (rm ? in_meta(L, s, slot) : v.mbox_meta)[mmeta_ix(v, L.rbuf, s,
                                                                  slot, g)];
       const bool cur = tag_is(meta.x, tag_prev);
       const uint32_t info = cur ? meta.y : 0u;
@@ -2681,7 +2725,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         // the types the raft launch handles (el_dispatch); anything else
         // (snapshots, leader transfer, ...) is the CPU path's
         if (info & (MI_OFF_LEADER | MI_OFF_FOLLOWER)) {
-          const uint4 *mb = rm ? v.mbox_in : v.mbox;
+          const uint4 *mb = rm ? in_mbox(L, s, slot) : v.mbox;
           const uint32_t nrp = mi_nrep(info);
           for (uint32_t j = 0; j < ns; ++j) {
             const uint32_t k = rec_pos(j < nrp, j < nrp ? j : j - nrp, v.MB);
@@ -2708,7 +2752,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           // leader that steps down for one learns the new leader, and would
           // forward its queued proposals to it (handleFollowerPropose,
           // raft.go:2103-2116); without one it drops them
-          const uint4 *mb = rm ? v.mbox_in : v.mbox;
+          const uint4 *mb = rm ? in_mbox(L, s, slot) : v.mbox;
           const uint32_t nrp = mi_nrep(info);
           for (uint32_t j = 0; j < ns; ++j) {
             const uint32_t k = rec_pos(j < nrp, j < nrp ? j : j - nrp, v.MB);
@@ -2720,7 +2764,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                              !(x & MF_REJECT));
             const uint64_t rt =
                 (x & MF_TERM_OTHER)
-                    ? (rm ? v.rterm_in : v.rterm)[rterm_ix(v, L.rbuf, s, slot,
+                    ? (rm ? in_rterm(L, s, slot) : v.rterm)[rterm_ix(v, L.rbuf, s, slot,
                                                            k, g)]
                     : (x & MF_TERM_ZERO) ? 0 : hi64(meta);
             if ((x & MF_TERM_OTHER) && !pv && rt > r.term) higher_in = true;
@@ -2771,7 +2815,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       }
       if (info & MI_REJECT) rej_from |= 1u << s;
       if (!is_leader && mi_nrep(info))
-        max_app = umax64(max_app, (rm ? v.maxapp_in : v.mbox_maxapp)[mmeta_ix(
+        max_app = umax64(max_app, (rm ? in_maxapp(L, s, slot) : v.mbox_maxapp)[mmeta_ix(
                                       v, L.rbuf, s, slot, g)]);
       if (FPF && ns && (pf_s[0] < 0 || (PFS > 1 && pf_s[1] < 0))) {
         // the records go to LDS in one batch; the dispatch loop reads them
@@ -2779,7 +2823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         const int q = pf_s[0] < 0 ? 0 : 1;
         pf_s[q] = s;
         pf_nrp[q] = mi_nrep(info);
-        const uint4 *mb = rm ? v.mbox_in : v.mbox;
+        const uint4 *mb = rm ? in_mbox(L, s, slot) : v.mbox;
 #pragma unroll
         for (int j = 0; j < (FPF ? PFN : 1); ++j)
           if ((uint32_t)j < ns) {
@@ -3080,8 +3124,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           if (qon && pass == 1 && ((qz_from >> s) & 1)) qs_try_enter(v, r);
           if (!((nin_packed >> (5 * s)) & 31u)) continue;
           const bool rm = pair_remote(v, s, slot);
-          const uint4 *mb = rm ? v.mbox_in : v.mbox;
-          const uint4 meta = (rm ? v.meta_in : v.mbox_meta)[mmeta_ix(
+          const uint4 *mb = rm ? in_mbox(L, s, slot) : v.mbox;
+          const uint4 meta = (rm ? in_meta(L, s, slot) : v.mbox_meta)[mmeta_ix(
               v, L.rbuf, s, slot, g)];
           const uint64_t sterm = hi64(meta);
           // records of this pass: the Replicates, then the others
@@ -3090,7 +3134,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
           src.remote = rm;
           src.lo = 0;
           if (rm && pass == 0 && cnt)
-            src.lo = v.elo_in[mmeta_ix(v, L.rbuf, s, slot, g)];
+            src.lo = in_elo(L, s, slot)[mmeta_ix(v, L.rbuf, s, slot, g)];
           uint64_t prev_lo = 0, prev_hi = 0;
           // (a window of prefetched records measured slower: the leader
           // spills more, profiles/r02_kvline/README.md)
@@ -3108,7 +3152,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
             // within its round carries its own term (rterm)
             const uint64_t rt =
                 (SLOW && (c0.x & MF_TERM_OTHER))
-                    ? (rm ? v.rterm_in : v.rterm)[rterm_ix(v, L.rbuf, s, slot,
+                    ? (rm ? in_rterm(L, s, slot) : v.rterm)[rterm_ix(v, L.rbuf, s, slot,
                                                            k, g)]
                     : sterm;
             const Msg m = msg_decode(c0, c1, rt, prev_lo, prev_hi);

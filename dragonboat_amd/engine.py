@@ -127,6 +127,7 @@ SIGNATURES = {
                                     C.POINTER(Region)]),
     "drb_exchange_local": (C.c_int, [C.POINTER(P), U32]),
     "drb_exchange_local_counted": (C.c_int, [C.POINTER(P), U32]),
+    "drb_exchange_local_bind": (C.c_int, [C.POINTER(P), U32]),
     "drb_exchange_mark": (C.c_int, [P]),
     "drb_exchange_plan": (C.c_int, [P, U32, C.POINTER(abi.Xfer), SZ,
                                     C.POINTER(SZ)]),
@@ -705,6 +706,16 @@ class Engine:
         fn = lib().drb_exchange_local_counted if counted else \
             lib().drb_exchange_local
         _ck(fn(arr, len(engines)), "drb_exchange_local")
+
+    @staticmethod
+    def exchange_local_bind(engines):
+        """Bind one process's engines on one GPU (rank order) for the
+        zero-copy exchange (drb_exchange_local_bind): their rounds read
+        remote planes from the senders' outboxes, exchange_local then only
+        orders the rounds.  For good: destroy them together."""
+        arr = (P * len(engines))(*[e.h for e in engines])
+        _ck(lib().drb_exchange_local_bind(arr, len(engines)),
+            "drb_exchange_local_bind")
 
     def exchange_bytes(self, reset=False):
         """Inbound plane bytes moved into this engine by the exchanges

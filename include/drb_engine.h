@@ -1121,8 +1121,22 @@ int drb_plane_regions(drb_engine *e, uint32_t from, uint32_t to,
  *    (all mailbox positions, both chunks, the header, the max-append word,
  *    the entry-row base and entry_mbox entry rows: what the pre-pass
  *    bounds) by peer copies, so no counts are read.
- * The receivers read only what the plane headers count. */
+ * The receivers read only what the plane headers count.
+ *  - Engines bound by drb_exchange_local_bind: nothing moves; only the
+ *    rounds' order is enqueued (each engine's next round waits for every
+ *    engine's last one). */
 int drb_exchange_local(drb_engine *const *engines, uint32_t n);
+/* Binds the n engines of one process on one device (engines[r] rank r of
+ * the placement, n >= 2, every engine at the same round) for the zero-copy
+ * exchange: their step kernels read each remote plane straight from the
+ * sender rank's outbox -- every lane of an inbound plane (from, to) comes
+ * from one rank, at the same lane (drb_place_peer) -- so drb_exchange_local
+ * copies nothing.  For the rest of their lives the bound engines take no
+ * other exchange and no delivered messages (drb_ingest_ex, drb_ingest_wire,
+ * drb_exchange_rccl*, drb_exchange_local_counted, drb_plane_regions dir 1:
+ * DRB_EINVAL); they are destroyed together (a peer's destroy waits for the
+ * others' queued work and fails their later rounds). */
+int drb_exchange_local_bind(drb_engine *const *engines, uint32_t n);
 /* The fixed-capacity exchange step of a process-per-GPU host as a list of
  * point-to-point transfers: every remote plane that can carry fast-path
  * messages -- a leader slot at either end on some rank (leader_mask: the

@@ -279,9 +279,10 @@ class DistPair:
     Stepped in lock-step with one oracle cluster of all G groups."""
 
     def __init__(self, G, R=5, N=8, seed=0x5EEDD8B0, window=32, E=4,
-                 counted=False, **engine_kw):
+                 counted=False, bound=False, **engine_kw):
         self.G, self.R, self.N, self.seed = G, R, N, seed
         self.counted = counted  # drb_exchange_local_counted
+        self.bound = bound  # drb_exchange_local_bind: zero-copy planes
         self.lanes = (G + N - 1) // N
         self.engs = [Engine(num_groups=self.lanes, num_replicas=R,
                             window=window, total_groups=G, place_world=N,
@@ -297,6 +298,8 @@ class DistPair:
             self.orc.set_pre_vote(True)
         for e in self.engs:
             e.init_steady(term=2, leader_slot=0, seed=seed)
+        if bound:
+            Engine.exchange_local_bind(self.engs)
         self.rounds = 0
         self.cpu = set()  # groups handed to the CPU path (the oracle)
 

@@ -81,15 +81,23 @@ def test_bench_local_ranks_is_the_c4_run():
 
 
 @pytest.mark.gpu
-def test_bench_c4_local_ranks():
+@pytest.mark.parametrize("mode", ["bind", "pull"])
+def test_bench_c4_local_ranks(mode):
     """bench.py --workload c4 --local-ranks 4: four engines of one process
-    on the one GPU, their planes moved by drb_exchange_local's device pull;
-    every group commits one entry a round and the pull reports its bytes."""
-    p = _bench("--workload", "c4", "--local-ranks", "4")
+    on the one GPU, bound for the zero-copy exchange (the default: the
+    receivers read the senders' outboxes, nothing is pulled) or their
+    planes moved by drb_exchange_local's device pull (which reports its
+    bytes); every group commits one entry a round."""
+    p = _bench("--workload", "c4", "--local-ranks", "4",
+               "--local-exchange", mode)
     assert p.returncode == 0, p.stderr[-3000:]
     res = json.loads([x for x in p.stdout.splitlines()
                       if x.startswith("{")][-1])
     assert res["config"]["local_ranks"] == 4
     assert res["counters"]["committed_per_round"] == G
     assert res["counters"]["fallbacks_and_errors"] == 0
-    assert res["exchange"]["bytes_per_round"] > 0
+    assert res["exchange"]["mode"] == mode
+    if mode == "pull":
+        assert res["exchange"]["bytes_per_round"] > 0
+    else:
+        assert res["exchange"]["bytes_per_round"] == 0

@@ -435,14 +435,16 @@ def _exchange_by_plan(engs, mask, counted=False):
     return moved
 
 
-@pytest.mark.parametrize("mode", ["local", "plan", "counted"])
+@pytest.mark.parametrize("mode", ["local", "plan", "counted", "bound"])
 def test_fullsize_c4_spread_sampled(mode):
     """C4 at its configured size and placement: 1,048,576 groups x 5
     replicas over 8 ranks -- replica slot s of group g on rank (g + s) mod
     8 at lane g // 8 -- as 8 engines of one process on the one GPU, with
     bench.py's C4 engine arguments (mailbox 8, entry_mbox k + 2, the device
     input generators).  After every round the planes move either by
-    drb_exchange_local (the device pull), by drb_exchange_plan's transfer
+    drb_exchange_local (the device pull; "bound": nothing moves, the
+    receivers read the senders' outboxes, drb_exchange_local_bind), by
+    drb_exchange_plan's transfer
     list (the fixed-capacity step of drb_exchange_rccl) or by
     drb_exchange_plan_words over every rank's counts (the counted step of
     drb_exchange_rccl_counted), each send copied into its paired receive as
@@ -459,6 +461,8 @@ def test_fullsize_c4_spread_sampled(mode):
     try:
         for e in engs:
             e.init_steady(term=2, leader_slot=0, seed=SEED)
+        if mode == "bound":
+            Engine.exchange_local_bind(engs)
         mask = 0
         for e in engs:
             mask |= e.role_slots()[0]
@@ -481,7 +485,7 @@ def test_fullsize_c4_spread_sampled(mode):
                 (r, [o.to_dict() for o in outs if o.fallbacks or o.errors])
             if r >= 3:
                 assert sum(o.committed_entries for o in outs) == G, r
-            if mode == "local":
+            if mode in ("local", "bound"):
                 Engine.exchange_local(engs)
             else:
                 m = _exchange_by_plan(engs, mask, counted=mode == "counted")
@@ -491,7 +495,7 @@ def test_fullsize_c4_spread_sampled(mode):
             if r % 5 == 4 or r == 15:
                 errs = _compare_spread(engs, orc, gids, R, N)
                 assert not errs, (r, errs[:3])
-        assert mode == "local" or moved > 0
+        assert mode in ("local", "bound") or moved > 0
     finally:
         for e in engs:
             e.close()

@@ -5,9 +5,12 @@ the same seeded inputs (SURVEY 8d workload) and compares the full
 per-replica state, resident log, KV contents, sent messages and
 ReadyToReads after every round (tests/gpu_harness.py).
 """
+import ctypes as C
+
 import pytest
 
 from dragonboat_amd import abi
+from dragonboat_amd.engine import Engine
 from tests.gpu_harness import Pair
 
 pytestmark = pytest.mark.gpu
@@ -226,17 +229,21 @@ def test_entries_to_save_capacity_falls_back():
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,R,G,counted", [
     (8, 5, 44, False), (2, 3, 30, False), (3, 5, 31, False),
-    (4, 3, 20, False), (8, 5, 44, True), (3, 5, 31, True)])
+    (4, 3, 20, False), (8, 5, 44, True), (3, 5, 31, True),
+    (8, 5, 44, "bound"), (3, 5, 31, "bound"), (2, 3, 30, "bound")])
 def test_replicas_spread_over_ranks_c4(N, R, G, counted):
     """C4 placement: replica slot s of group g on rank
     (g + s) mod N; every cross-rank message and its entries travel in the
     mailbox planes moved between the ranks' engines (drb_plane_regions --
     what RCCL moves between GPUs, here drb_exchange_local on one GPU: the
     full-capacity planes behind cross-stream events, or the counted sizes
-    with host synchronisation).  Bit-exact against one oracle cluster of
-    all G groups."""
+    with host synchronisation) -- or, engines bound for the zero-copy
+    exchange ("bound", drb_exchange_local_bind), read by the receivers in
+    the senders' outboxes.  Bit-exact against one oracle cluster of all G
+    groups."""
     from tests.gpu_harness import DistPair
-    p = DistPair(G=G, R=R, N=N, max_props=4, counted=counted)
+    p = DistPair(G=G, R=R, N=N, max_props=4, counted=counted is True,
+                 bound=counted == "bound")
     assert not p.check(), "init"
     for r in range(12):
         k = 1 if r % 5 != 4 else (3 if r % 2 else 0)
@@ -248,6 +255,37 @@ def test_replicas_spread_over_ranks_c4(N, R, G, counted):
              o.ready_to_reads), (r, e, o.to_dict())
         errs = p.check()
         assert not errs, (r, errs[:3])
+
+
+@pytest.mark.gpu
+def test_bound_engines_take_no_other_exchange():
+    """Engines bound for the zero-copy exchange (drb_exchange_local_bind)
+    read their remote planes in their peers' outboxes: nothing may be
+    delivered into the inbound copies they no longer read -- ingest, the
+    counted local exchange, inbound plane regions are DRB_EINVAL -- a
+    second bind is refused, and rounds stay bit-exact after the refusals."""
+    from dragonboat_amd.engine import DrbError
+    from tests.gpu_harness import DistPair
+    p = DistPair(G=20, R=3, N=2, max_props=4, bound=True)
+    o, e = p.round(k=1, tick=True)
+    assert e["fallbacks"] == 0 and not p.check()
+    eng = p.engs[0]
+    marr = (abi.Message * 1)()
+    earr = (abi.Entry * 1)()
+    pool = (C.c_uint8 * 16)()
+    with pytest.raises(DrbError, match="status -1"):
+        eng.ingest_ex(marr, 0, earr, pool)
+    with pytest.raises(DrbError, match="status -1"):
+        Engine.exchange_local(p.engs, counted=True)
+    with pytest.raises(DrbError, match="status -1"):
+        eng.plane_regions(1, 0, 0xffffffff, 1)
+    with pytest.raises(DrbError, match="status -1"):
+        Engine.exchange_local_bind(p.engs)
+    for r in range(4):
+        o, e = p.round(k=1, tick=r % 2 == 0)
+        assert e["fallbacks"] == 0 and e["errors"] == 0, (r, e)
+        assert e["committed_entries"] == o.committed_entries, r
+    assert not p.check()
 
 
 def _long_payload_rounds(p, val_len, rounds=8, encode=False, device_gen=False):
