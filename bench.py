@@ -161,12 +161,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true",
                     help="skip the receiving-side wire ingest measurement")
-    ap.add_argument("--exchange", default="fixed",
+    ap.add_argument("--exchange", default="counted",
                     choices=["fixed", "counted"],
-                    help="c4 plane exchange: full-capacity planes enqueued "
-                         "behind the round (no host sync) or sized by an "
-                         "all_gather of per-plane counts (dragonboat_amd/"
-                         "exchange.py)")
+                    help="c4 plane exchange: sized by an all_gather of "
+                         "per-plane counts (the default: about half the "
+                         "fixed step's bytes, VERDICT r5) or full-capacity "
+                         "planes enqueued behind the round with no host "
+                         "sync (dragonboat_amd/exchange.py)")
     ap.add_argument("--read-results", type=int, default=1,
                     help="c3: the timed reads write each client's "
                          "ReadLocalNode result (drb_config.max_reads_per_"
