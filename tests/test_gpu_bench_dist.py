@@ -101,3 +101,24 @@ def test_bench_c4_local_ranks(mode):
         assert res["exchange"]["bytes_per_round"] > 0
     else:
         assert res["exchange"]["bytes_per_round"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xmode", ["counted", "fixed"])
+def test_bench_c4_gpus_2(xmode):
+    """bench.py --workload c4 --gpus 2: the replicas of every group spread
+    over the two ranks, the planes moved after every round by exchange.py
+    (counted by default: an all_gather of the plane words, then the planes
+    at those sizes; or the fixed full-capacity step) -- through host memory
+    under gloo here, RCCL on a node.  Every group commits every round and
+    nothing leaves the fast path."""
+    p = _bench("--workload", "c4", "--gpus", "2", "--dist-backend", "gloo",
+               "--exchange", xmode)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([x for x in p.stdout.splitlines()
+                      if x.startswith("{")][-1])
+    assert res["n_gpus"] == 2
+    assert res["exchange"]["mode"] == xmode
+    c = res["counters"]
+    assert c["fallbacks"] == 0 and c["errors"] == 0, c
+    assert c["committed_per_round"] > 0, c
