@@ -48,6 +48,11 @@ namespace drb {
 // waves would spill 20, and at R = 5 five would spill 149), the leader at
 // 4 (101 VGPRs; 5 would spill 24), where the full EXT kernels spill
 // 37 / 25 VGPRs at 4 / 3 waves
+// (timing variant: the round-6 first eligibility -- every entry committed,
+// applied and out of memory)
+#ifndef DRB_LEAN_STRICT
+#define DRB_LEAN_STRICT 0
+#endif
 #ifndef DRB_LEAN_WHY
 #define DRB_LEAN_WHY 0
 #endif
@@ -201,21 +206,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       r.ri_fr[d] = 0;
       r.ri_cf[d] = 0;
     }
-    // a quiet group, nothing staged, no queue, no transfer, the role of
-    // the fast path (the pre-pass's ROLE test)
-    bool ok = r.committed == r.last && r.processed == r.last &&
-              r.saved_to == r.last && r.sm_index == r.last &&
-              r.applied_index == r.last && r.marker > r.last &&
+    // nothing to save (saved_to = last) or apply (processed = committed,
+    // the state machine at it), nothing staged, no queue, no transfer, the
+    // role of the fast path (the pre-pass's ROLE test).  Entries may still
+    // be uncommitted, or applied but held in memory: updateAppliedIndex and
+    // inMemory.appliedLogTo below are all such a round does with them --
+    // where appliedLogTo needs a term the cache does not give, the lane
+    // escalates (log_term would read the ring)
+    const uint64_t la = r.sm_index;  // applied_index after updateAppliedIndex
+    const bool log_to = la > 0 && la >= r.marker && r.last >= r.marker &&
+                        la <= r.last;
+    bool ok = r.saved_to == r.last && r.processed == r.committed &&
+              r.sm_index == r.processed && r.committed <= r.last &&
+              r.applied_index <= r.sm_index &&
+              (!log_to || la >= r.term_start) &&
+              (!DRB_LEAN_STRICT || (r.committed == r.last &&
+                                    r.applied_index == r.last &&
+                                    r.marker > r.last)) &&
               r.ri_count == 0 && !(flags & (F_XFER | F_XFER_REQ)) &&
               (LEAD || role == DRB_FOLLOWER) && pcount == 0 &&
               !(riq.x | riq.y | riq.z | riq.w);
 #if DRB_LEAN_WHY
     uint32_t why = 0;  // (timing variant: why a lane escalates)
-    if (r.committed != r.last) why |= 2u;
-    if (r.processed != r.last || r.saved_to != r.last ||
-        r.sm_index != r.last || r.applied_index != r.last)
+    if (r.committed > r.last || r.applied_index > r.sm_index) why |= 2u;
+    if (r.processed != r.committed || r.saved_to != r.last ||
+        r.sm_index != r.processed)
       why |= 4u;
-    if (r.marker <= r.last) why |= 8u;
+    if (log_to && la < r.term_start) why |= 8u;
     if (r.ri_count || (flags & (F_XFER | F_XFER_REQ)) ||
         !(LEAD || role == DRB_FOLLOWER) || pcount || (riq.x | riq.y | riq.z | riq.w))
       why |= 16u;
@@ -429,7 +446,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         }
         if (confirmed_index != r.applied_index)
           st_f(L, r, F_CONFIRMED_INDEX, r.applied_index);
-        // (inMemory.appliedLogTo: marker > last, nothing to do)
+        // Peer.Commit -> entryLog.commitUpdate: nothing saved or applied;
+        // inMemory.appliedLogTo (inmemory.go:138-164) as the step kernel
+        // runs it, the term from the cache (la >= term_start, above)
+        if (log_to) {
+          st_f(L, r, F_APPLIED_TO_INDEX, la);
+          st_f(L, r, F_APPLIED_TO_TERM, r.term);
+          r.marker = la + 1;
+        }
       }
       r.ring_guard = r.guard_new;
       // at rest (see step_kernel), and the quiesce state
