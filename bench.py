@@ -187,6 +187,10 @@ def parse():
                     help="after the timed region, also time rounds whose "
                          "proposals come from host memory through "
                          "drb_stage_proposals (default: on for c2/c3, N=1)")
+    ap.add_argument("--rounds-per-call", type=int, default=-1,
+                    help="timed rounds per drb_step_rounds call (a chunk of "
+                         "every group: plain rounds from one C call); -1: 16 "
+                         "for c2, round by round otherwise")
     ap.add_argument("--chunk-ab", default="",
                     help="c3, after the timed region: A/B of drb_step_rounds "
                          "(k rounds chunk by chunk of the groups) against "
@@ -773,16 +777,43 @@ def main():
     if xch is not None:
         xch.bytes_sent = 0
     K = args.steps
+    # rounds per drb_step_rounds call (C2 by default: a Python call per
+    # round costs more host time than the GPU's round, profiles/r06_c2)
+    rpc = args.rounds_per_call if args.rounds_per_call >= 0 else \
+        (16 if c2 else 0)
+    fused_reads = reads and args.reads_mode == "fused"
+    if rpc > 1 and (c4 or c5 or args.listed or xch is not None or
+                    (reads and not fused_reads)):
+        rpc = 0  # (those step round by round)
+    if rpc > 1:
+        def rin_main(i):
+            return dict(tick=(2 * args.warmup + i) % tick_every[0] == 0,
+                        prop_slot=i % NP,
+                        ri_slot=i % NP if reads else 0xFFFFFFFF,
+                        reads_per_ctx=READS_PER_CTX if fused_reads else 0,
+                        key_space=KEY_SPACE, encode_saves=saves,
+                        ri_replica=2 if args.reads_at == "follower" else 0)
+        calls = [Engine.round_array([rin_main(i) for i in
+                                     range(i0, min(i0 + rpc, K))])
+                 for i0 in range(0, K, rpc)]
+        all_groups = (G + 255) // 256 * 256
+    n_ev = len(calls) if rpc > 1 else K
     ev = [(torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+           torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     ddist.barrier()
     torch.cuda.synchronize()
     eng.sync()
     t0 = time.perf_counter()
-    for i in range(K):
-        ev[i][0].record(stream)
-        step(2 * args.warmup + i, None if c5 else i)
-        ev[i][1].record(stream)
+    if rpc > 1:
+        for j, arr in enumerate(calls):
+            ev[j][0].record(stream)
+            eng.step_rounds(arr, all_groups)
+            ev[j][1].record(stream)
+    else:
+        for i in range(K):
+            ev[i][0].record(stream)
+            step(2 * args.warmup + i, None if c5 else i)
+            ev[i][1].record(stream)
     eng.sync()
     torch.cuda.synchronize()
     ddist.barrier()
@@ -1217,7 +1248,8 @@ def main():
             "config": {
                 "workload": wl,
                 "groups_per_gpu": g_here, "replicas": R,
-                "parallelism": par},
+                "parallelism": par,
+                "rounds_per_call": max(1, rpc)},
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

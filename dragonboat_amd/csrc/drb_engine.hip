@@ -2467,11 +2467,19 @@ extern "C" int drb_step_rounds(drb_engine *e, const drb_round_in *in,
   HIPCHK(hipEventRecord(e->ev_fork, e->stream));
   HIPCHK(hipStreamWaitEvent(e->stream2, e->ev_fork, 0));
   int rc = DRB_OK;
-  for (uint64_t c0 = 0, c = 0; c0 < gx && !rc; c0 += cb, ++c) {
-    const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, gx - c0);
-    hipStream_t st = (c & 1) ? e->stream2 : e->stream;
-    for (uint32_t t = 0; t < k && !rc; ++t)
-      rc = launch_any(e, ps[t], st, (uint32_t)c0, nb);
+  if (cb >= gx) {
+    // one chunk of every group: the k rounds as plain rounds, each with its
+    // two role launches side by side where they fit (launch_step), the
+    // host's per-round cost one C call's (C2: a Python call per round left
+    // the GPU idle a third of the time, profiles/r06_c2)
+    for (uint32_t t = 0; t < k && !rc; ++t) rc = launch_any(e, ps[t]);
+  } else {
+    for (uint64_t c0 = 0, c = 0; c0 < gx && !rc; c0 += cb, ++c) {
+      const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, gx - c0);
+      hipStream_t st = (c & 1) ? e->stream2 : e->stream;
+      for (uint32_t t = 0; t < k && !rc; ++t)
+        rc = launch_any(e, ps[t], st, (uint32_t)c0, nb);
+    }
   }
   // the second stream joins the engine stream whatever happened
   const hipError_t j1 = hipEventRecord(e->ev_join, e->stream2);

@@ -423,10 +423,11 @@ class Engine:
         _ck(lib().drb_step_round_async(self.h, C.byref(rin)),
             "drb_step_round_async")
 
-    def step_rounds(self, rounds, chunk_groups):
-        """drb_step_rounds: len(rounds) rounds chunk by chunk of the groups;
-        rounds: [dict(tick=, prop_slot=, ri_slot=, reads_per_ctx=,
-        key_space=, encode_saves=)]."""
+    @staticmethod
+    def round_array(rounds):
+        """The drb_round_in array of rounds ([dict(tick=, prop_slot=,
+        ri_slot=, reads_per_ctx=, key_space=, encode_saves=)]), for
+        step_rounds (built once, stepped many times)."""
         arr = (RoundIn * len(rounds))()
         for i, r in enumerate(rounds):
             arr[i] = RoundIn(int(bool(r.get("tick"))),
@@ -436,7 +437,15 @@ class Engine:
                              int(bool(r.get("encode_saves"))),
                              r.get("ri_replica", 0), 0,
                              r.get("prop_replica", 0))
-        _ck(lib().drb_step_rounds(self.h, arr, len(rounds), chunk_groups),
+        return arr
+
+    def step_rounds(self, rounds, chunk_groups):
+        """drb_step_rounds: the rounds chunk by chunk of the groups (a
+        chunk of every group: plain rounds, one C call); rounds: a list of
+        dicts or a round_array."""
+        arr = rounds if isinstance(rounds, C.Array) else \
+            self.round_array(rounds)
+        _ck(lib().drb_step_rounds(self.h, arr, len(arr), chunk_groups),
             "drb_step_rounds")
 
     def read_counters(self, reset=True):

@@ -751,7 +751,10 @@ int drb_step_round_async(drb_engine *e, const drb_round_in *in);
  * would give it; a chunk's mailbox, state and window rows may stay on-die
  * between its rounds.  No host synchronisation.  Co-resident replicas only,
  * without elections, listed rounds, tan records or durable_log
- * (DRB_EINVAL): those step round by round. */
+ * (DRB_EINVAL): those step round by round.  A chunk of every group
+ * (chunk_groups >= num_groups) runs the k rounds as k plain rounds from one
+ * call: a host loop that steps a small engine round by round (C2) is then
+ * bound by the GPU, not by its own per-call cost. */
 int drb_step_rounds(drb_engine *e, const drb_round_in *in, uint32_t k,
                     uint64_t chunk_groups);
 int drb_read_counters(drb_engine *e, drb_round_out *out, int reset);

@@ -54,7 +54,10 @@ def _sample(G, chunk):
 
 
 @pytest.mark.parametrize("G,chunk,k", [(1000, 256, 2), (1536, 512, 4),
-                                       (700, 256, 1), (2048, 1024, 4)])
+                                       (700, 256, 1), (2048, 1024, 4),
+                                       # one chunk of every group: plain
+                                       # rounds from one call
+                                       (1000, 1024, 4), (2048, 2048, 3)])
 def test_rounds_by_chunk_match_the_oracle(G, chunk, k):
     p = Pair(G=G, R=3, prop_slots=4, ri_slots=4, max_props=1)
     sample = _sample(G, chunk)
