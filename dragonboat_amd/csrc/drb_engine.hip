@@ -777,9 +777,10 @@ extern "C" int drb_export_replicas(drb_engine *e, uint64_t first_group,
       for (int k = 0; k < NUM_U64_EXPORTED; ++k)
         *st_u64(&o, k) = d64[a + kU64Order[k]];
       const uint32_t fl = d32[b + 1];
-      if ((fl & F_QUIESCED) && (fl & DRB_F_HOSTED) &&
+      if ((fl & F_QUIESCED) && (fl & F_AT_REST) && (fl & DRB_F_HOSTED) &&
           !(fl & (DRB_F_FALLBACK | DRB_F_ERROR))) {
-        // quiesced ticks not applied yet (drb_step.hpp, F_QS_BASE)
+        // quiesced ticks not applied yet (drb_step.hpp, F_QS_BASE: stored
+        // by a round that ends quiesced and at rest)
         const uint64_t owed = e->ticks - d64[a + F_QS_BASE];
         o.election_tick += owed;
         o.qs_current_tick += owed;

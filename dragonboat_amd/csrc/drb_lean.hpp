@@ -266,7 +266,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       r.qs_since = qsv[2];
       r.qs_exit = qsv[3];
       r.qs_dirty = 0;
-      qs_owed = p.tick_no - p.tick - qsv[4];
+      // (owed ticks and the base only for a replica that may have skipped
+      // rounds: quiesced and at rest, step_kernel)
+      if (DRB_QS_EAGER ||
+          (flags & (F_QUIESCED | F_AT_REST)) == (F_QUIESCED | F_AT_REST))
+        qs_owed = p.tick_no - p.tick - qsv[4];
       r.election_tick += qs_owed;
       r.qs_tick += qs_owed;
     }
@@ -466,7 +470,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         if (qd & 1u) over_st(L, F_QS_IDLE, r.qs_idle);
         if (qd & 2u) over_st(L, F_QS_SINCE, r.qs_since);
         if (qd & 4u) over_st(L, F_QS_EXIT, r.qs_exit);
-        over_st(L, F_QS_BASE, p.tick_no);
+        if (DRB_QS_EAGER || (r.flags & F_QUIESCED))
+          over_st(L, F_QS_BASE, p.tick_no);
       }
       // store_rep's record, re-based as it does (last did not move), and
       // only the 16 B chunks that changed
@@ -523,7 +528,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
               [slot] = tag_byte(p.round, w);
         }
       }
-      v.rtr_count[ix(v, slot, g)] = 0;
+      // (a replica that ended its last round at rest left no ReadyToRead)
+      if (DRB_QS_EAGER || !(flags0 & F_AT_REST))
+        v.rtr_count[ix(v, slot, g)] = 0;
       if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
     }
   }

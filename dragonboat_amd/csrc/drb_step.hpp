@@ -85,6 +85,11 @@ namespace drb {
 #endif
 // timing only: per-phase cycle sums of the leader / follower lanes
 // (View.phase, drb_debug_phase); 0 in shipped builds
+// the quiesce base stored and read every round, rtr_count cleared by every
+// lean round (1: the behaviour before round 6's lazy forms; timing variant)
+#ifndef DRB_QS_EAGER
+#define DRB_QS_EAGER 0
+#endif
 // the zero-copy exchange's reads (in_mbox & co.; 0: timing variant only)
 #ifndef DRB_PEERS
 #define DRB_PEERS 1
@@ -2674,8 +2679,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
       r.qs_since = over_ld(L, F_QS_SINCE);
       r.qs_exit = over_ld(L, F_QS_EXIT);
       r.qs_dirty = 0;
-      // the quiesced ticks this replica skipped (only ever while quiesced)
-      qs_owed = p.tick_no - p.tick - over_ld(L, F_QS_BASE);
+      // the quiesced ticks this replica skipped: only a replica that ended
+      // its last round quiesced and at rest skips rounds (idle_round), and
+      // only such a round stores the base (below)
+      if (DRB_QS_EAGER ||
+          (flags0 & (F_QUIESCED | F_AT_REST)) == (F_QUIESCED | F_AT_REST))
+        qs_owed = p.tick_no - p.tick - over_ld(L, F_QS_BASE);
       r.election_tick += qs_owed;
       r.qs_tick += qs_owed;
     }
@@ -3408,7 +3417,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
         if (qd & 1u) over_st(L, F_QS_IDLE, r.qs_idle);
         if (qd & 2u) over_st(L, F_QS_SINCE, r.qs_since);
         if (qd & 4u) over_st(L, F_QS_EXIT, r.qs_exit);
-        over_st(L, F_QS_BASE, p.tick_no);
+        if (DRB_QS_EAGER ||
+            (r.flags & (F_QUIESCED | F_AT_REST)) == (F_QUIESCED | F_AT_REST))
+          over_st(L, F_QS_BASE, p.tick_no);  // (it may skip rounds now)
       }
       store_rep<R, LEAD>(L, r, flags0, fb0);
       if (SLOW) {  // what only the raft launch changes
