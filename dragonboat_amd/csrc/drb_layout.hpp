@@ -253,6 +253,11 @@ constexpr uint32_t F_XFER_REQ = 1u << 19;
 // a leader with one steps in the raft launch until it is cleared
 constexpr int F_XFER_SHIFT = 20;
 constexpr uint32_t F_XFER = 0xfu << F_XFER_SHIFT;
+// save_len is 0: the replica's last encode_saves round saved nothing (set
+// and cleared by the EXT rounds, the lean kernel's clear then skipped; any
+// other writer of save_len writes 0 or leaves the bit clear, and an import
+// clears it)
+constexpr uint32_t F_SAVE_ZERO = 1u << 24;
 constexpr uint32_t F_PUBLIC = 0xffffu;
 
 // message record: 1-2 x uint4 (drb_msg.hpp)

@@ -460,8 +460,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         }
       }
       r.ring_guard = r.guard_new;
-      // at rest (see step_kernel), and the quiesce state
+      // at rest (see step_kernel), and the quiesce state; nothing saved
       r.flags |= F_AT_REST;
+      if (p.encode_saves) r.flags |= F_SAVE_ZERO;
       if (qon) {
         r.flags = qs_quiesced(r) ? (r.flags | F_QUIESCED)
                                  : (r.flags & ~F_QUIESCED);
@@ -531,7 +532,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       // (a replica that ended its last round at rest left no ReadyToRead)
       if (DRB_QS_EAGER || !(flags0 & F_AT_REST))
         v.rtr_count[ix(v, slot, g)] = 0;
-      if (p.encode_saves) v.save_len[ix(v, slot, g)] = 0;
+      if (p.encode_saves && (DRB_QS_EAGER || !(flags0 & F_SAVE_ZERO)))
+        v.save_len[ix(v, slot, g)] = 0;
     }
   }
   // the escalated lanes onto the row's list: one atomic per wave, into

@@ -3408,6 +3408,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SLOW ? DRB_
                         r.nrtr == 0 && !has_save &&
                         !(r.flags & (DRB_F_FALLBACK | DRB_F_ERROR));
       r.flags = rest ? (r.flags | F_AT_REST) : (r.flags & ~F_AT_REST);
+      if (EXT && p.encode_saves)  // (save_len: 0 below iff nothing saved)
+        r.flags = c_saved == 0 ? (r.flags | F_SAVE_ZERO)
+                               : (r.flags & ~F_SAVE_ZERO);
       if (qon) {
         r.flags = qs_quiesced(r) ? (r.flags | F_QUIESCED)
                                  : (r.flags & ~F_QUIESCED);

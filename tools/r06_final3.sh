@@ -3,9 +3,9 @@
 # C5 lines and their PMC passes, C4 local ranks
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-o=gpurun_out/r06_final3; mkdir -p $o
-tools/prof_steady.sh r06_final3/c3 || exit 1
-tools/prof_workloads.sh r06_final3/pmc c5_128 c5_1024 || exit 1
+o=gpurun_out/${1:-r06_final3}; mkdir -p $o
+tools/prof_steady.sh ${1:-r06_final3}/c3 || exit 1
+tools/prof_workloads.sh ${1:-r06_final3}/pmc c5_128 c5_1024 || exit 1
 for w in "c5_128 --workload c5 --payload 128" "c5_1024 --workload c5 --payload 1024" "c4l8 --workload c4 --local-ranks 8"; do
   set -- $w; n=$1; shift
   tools/gpu_step.sh 400 $o/bench_$n.log python bench.py "$@" --no-cpu-baseline || exit 1
